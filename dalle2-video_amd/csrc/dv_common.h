@@ -1,0 +1,84 @@
+// Shared device/host helpers for libdv_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/dv_hip.h"
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+namespace dv {
+
+// thread-local last-error message surfaced by dv_last_error()
+void set_error(const std::string& msg);
+int check_launch(const char* what);
+
+#define DV_REQUIRE(cond, msg)                      \
+  do {                                             \
+    if (!(cond)) {                                 \
+      ::dv::set_error(std::string(__func__) + ": " + (msg)); \
+      return DV_ERR_INVALID;                       \
+    }                                              \
+  } while (0)
+
+template <typename T> __device__ __forceinline__ float to_f(T v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f(float v) { return (T)v; }
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// wave64 reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sum for blockDim.x == NT (multiple of 64); `sh` holds NT/64 floats
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += sh[i];
+  return r;
+}
+
+// 16-byte vector <-> T[16/sizeof(T)] helpers
+template <typename T> struct Vec { };
+template <> struct Vec<float> {
+  static constexpr int N = 4;
+  __device__ static inline void to_f(u32x4 v, float* o) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = __builtin_bit_cast(float, v[i]);
+  }
+};
+template <> struct Vec<bf16> {
+  static constexpr int N = 8;
+  __device__ static inline void to_f(u32x4 v, float* o) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = __builtin_bit_cast(float, v[i] << 16);
+      o[2 * i + 1] = __builtin_bit_cast(float, v[i] & 0xffff0000u);
+    }
+  }
+};
+
+}  // namespace dv

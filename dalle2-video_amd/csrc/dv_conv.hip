@@ -1,0 +1,599 @@
+// Convolutions (1,k,k) / token linears for the Unet3D path as implicit GEMMs
+// on gfx950 MFMA.  Serves nn.Conv3d at dalle2_video.py:107,170,25,537,48,
+// 224-232,637 and the bias-free attention projections.
+//
+// Forward / dgrad: C^T[n][m] = sum_k Wp[n][k] * X_im2col[m][k]
+//   A operand = packed weight rows (n), B operand = im2col pixel rows (m);
+//   each lane of the 32x32 accumulator then owns one pixel and 4 consecutive
+//   channels per register quad -> vector epilogue stores.
+//   Tile BM(pixels) x BN(channels) x 64 B of K, 4 waves (2x2), LDS double
+//   buffer with a 16-B chunk XOR swizzle (conflict-free ds_read_b128).
+//   bf16: v_mfma_f32_32x32x16_bf16; f32 (parity): v_mfma_f32_32x32x2_f32.
+// Wgrad: dW[co][n'] = sum_p dY[p][co] * X_im2col[p][n'], split-K over pixels,
+//   operands staged pixel-major and read transposed (ds_read_b64_tr_b16),
+//   f32 atomics into a packed [co][tap][ci] workspace (coalesced rows).
+#include "dv_common.h"
+
+using namespace dv;
+
+namespace {
+
+__device__ __forceinline__ int sw_off(int row, int chunk) {
+  return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
+
+template <typename T> struct Mma;
+template <> struct Mma<bf16> {
+  __device__ static inline f32x16 run(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  // 4 k-steps of 2: the k-slot h of step j is element 4*chunk + j on BOTH
+  // operands, so the permuted k order is consistent.
+  // NB (hipcc 7.2): bit-casting single elements of a u32x4 (`bit_cast<float>(a[j])`)
+  // inside this unrolled loop miscompiles to element 0 for every j; cast the
+  // whole vector first.
+  __device__ static inline f32x16 run(u32x4 a, u32x4 b, f32x16 c) {
+    const f32x4 af = __builtin_bit_cast(f32x4, a), bf = __builtin_bit_cast(f32x4, b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], c, 0, 0, 0);
+    return c;
+  }
+};
+
+template <typename T>
+struct ConvFwdArgs {
+  const T* x0;
+  const T* x1;
+  int ld0, ld1, c0;
+  const T* w;
+  const float* bias;
+  const T* res;
+  int ldres;
+  T* y;
+  int ldy;
+  int H, W, cin, cout, ks, act;
+  long long M;
+  int K;
+};
+
+template <typename T>
+__device__ __forceinline__ void store4(T* dst, const float* v);
+template <>
+__device__ __forceinline__ void store4<float>(float* dst, const float* v) {
+  *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
+}
+template <>
+__device__ __forceinline__ void store4<bf16>(bf16* dst, const float* v) {
+  *(bf16x4*)dst = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+}
+template <typename T>
+__device__ __forceinline__ void load4(const T* src, float* v);
+template <>
+__device__ __forceinline__ void load4<float>(const float* src, float* v) {
+  f32x4 t = *(const f32x4*)src;
+  v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+}
+template <>
+__device__ __forceinline__ void load4<bf16>(const bf16* src, float* v) {
+  bf16x4 t = *(const bf16x4*)src;
+  v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
+}
+
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs<T> p) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int BK = 4 * VEC;  // K elements per 64-byte LDS row
+  constexpr int TI = BM / 64;  // 32-pixel MFMA tiles per wave
+  constexpr int TJ = BN / 64;  // 32-channel MFMA tiles per wave
+  constexpr int LA = BM / 64;  // pixel-row vectors loaded per thread
+  constexpr int LB = BN / 64;  // weight-row vectors loaded per thread
+  __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * 64];
+  char* sX = smem;
+  char* sW = smem + 2 * BM * 64;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int HW = p.H * p.W, pad = p.ks >> 1, K = p.K;
+  const int chunk = tid & 3;
+
+  int a_f[LA], a_y[LA], a_x[LA];
+  bool a_ok[LA];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) {
+    long long m = m0 + (tid >> 2) + 64 * i;
+    a_ok[i] = m < p.M;
+    long long mm = a_ok[i] ? m : 0;
+    int f = (int)(mm / HW);
+    int rem = (int)(mm - (long long)f * HW);
+    a_f[i] = f;
+    a_y[i] = rem / p.W;
+    a_x[i] = rem - a_y[i] * p.W;
+  }
+  // K position of this thread's vector: k = kc*BK + chunk*VEC -> (tap, ci)
+  int k_tap = 0, k_ci = chunk * VEC;
+  while (k_ci >= p.cin) { k_ci -= p.cin; ++k_tap; }
+
+  u32x4 ra[LA], rb[LB];
+  auto gload = [&](int kc) {
+    const int k = kc * BK + chunk * VEC;
+    const bool kin = k < K;
+    const int dy = k_tap / p.ks - pad, dx = k_tap % p.ks - pad;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int yy = a_y[i] + dy, xx = a_x[i] + dx;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (kin && a_ok[i] && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
+        long long pix = ((long long)a_f[i] * p.H + yy) * p.W + xx;
+        const T* src = k_ci < p.c0 ? p.x0 + pix * p.ld0 + k_ci : p.x1 + pix * p.ld1 + (k_ci - p.c0);
+        v = *(const u32x4*)src;
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int n = n0 + (tid >> 2) + 64 * i;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (kin && n < p.cout) v = *(const u32x4*)(p.w + (long long)n * K + k);
+      rb[i] = v;
+    }
+    // advance (tap, ci) by BK for the next chunk
+    k_ci += BK;
+    while (k_ci >= p.cin) { k_ci -= p.cin; ++k_tap; }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i)
+      *(u32x4*)(sX + buf * BM * 64 + sw_off((tid >> 2) + 64 * i, chunk)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < LB; ++i)
+      *(u32x4*)(sW + buf * BN * 64 + sw_off((tid >> 2) + 64 * i, chunk)) = rb[i];
+  };
+
+  f32x16 acc[TJ][TI];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+
+  const int nk = (K + BK - 1) / BK;
+  const int r = lane & 31, h = lane >> 5;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nk) gload(kc + 1);
+    const char* bx = sX + buf * BM * 64;
+    const char* bw = sW + buf * BN * 64;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 2 * s + h;
+      u32x4 wa[TJ], xb[TI];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) wa[j] = *(const u32x4*)(bw + sw_off(wn * 32 * TJ + 32 * j + r, c));
+#pragma unroll
+      for (int i = 0; i < TI; ++i) xb[i] = *(const u32x4*)(bx + sw_off(wm * 32 * TI + 32 * i + r, c));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[j][i] = Mma<T>::run(wa[j], xb[i], acc[j][i]);
+    }
+    if (kc + 1 < nk) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane owns pixel column r; channels 8g + 4h + e in each 32-tile
+  const bool vec_ok = ((p.ldy & 3) == 0) && (p.res == nullptr || (p.ldres & 3) == 0);
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const long long m = m0 + wm * 32 * TI + 32 * i + r;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * 32 * TJ + 32 * j + 8 * g + 4 * h;
+        if (n >= p.cout) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[j][i][4 * g + e];
+        if (vec_ok && n + 3 < p.cout) {
+          if (p.bias) {
+            f32x4 b = *(const f32x4*)(p.bias + n);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += b[e];
+          }
+          if (p.act == DV_ACT_SILU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
+          }
+          if (p.res) {
+            float rr[4];
+            load4<T>(p.res + m * p.ldres + n, rr);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += rr[e];
+          }
+          store4<T>(p.y + m * p.ldy + n, v);
+        } else {
+          for (int e = 0; e < 4 && n + e < p.cout; ++e) {
+            float t = v[e] + (p.bias ? p.bias[n + e] : 0.f);
+            if (p.act == DV_ACT_SILU) t = silu_f(t);
+            if (p.res) t += (float)p.res[m * p.ldres + n + e];
+            p.y[m * p.ldy + n + e] = (T)t;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wgrad
+// ---------------------------------------------------------------------------
+template <typename T>
+struct WgradArgs {
+  const T* dy;
+  int lddy;
+  const T* x0;
+  const T* x1;
+  int ld0, ld1, c0;
+  float* ws;  // packed [cout][K]
+  int H, W, cin, cout, ks, K;
+  long long M;
+  int pix_per_split;
+};
+
+// transposed 4x16 bf16 block read (gfx950 ds_read_b64_tr_b16)
+__device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(lds_addr));
+}
+
+template <typename T, int BMC, int BNK>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs<T> p) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int BP = 32;                              // pixels per K chunk
+  constexpr int SA = BMC * (int)sizeof(T) + 64;       // padded LDS row strides
+  constexpr int SB = BNK * (int)sizeof(T) + 64;
+  constexpr int TJ = BMC / 64, TI = BNK / 64;         // 2x2 waves
+  constexpr int VA = BMC / VEC, VB = BNK / VEC;       // vectors per LDS row
+  constexpr int LA = BP * VA / 256, LB = BP * VB / 256;
+  static_assert(LA >= 1 && LB >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) char smem[BP * (SA + SB)];
+  char* sA = smem;
+  char* sB = smem + BP * SA;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int co0 = blockIdx.x * BMC, nk0 = blockIdx.y * BNK;
+  const long long pbeg = (long long)blockIdx.z * p.pix_per_split;
+  long long pend = pbeg + p.pix_per_split;
+  if (pend > p.M) pend = p.M;
+  const int HW = p.H * p.W, pad = p.ks >> 1;
+
+  // fixed column per thread for A (co) and B (tap, ci)
+  const int a_col = (tid % VA) * VEC;
+  const int b_col = (tid % VB) * VEC;
+  const int b_n = nk0 + b_col;
+  const bool b_nok = b_n < p.K;
+  const int b_tap = b_nok ? b_n / p.cin : 0;
+  const int b_ci = b_n - b_tap * p.cin;
+  const int b_dy = b_tap / p.ks - pad, b_dx = b_tap % p.ks - pad;
+  const bool a_cok = co0 + a_col < p.cout;
+
+  f32x16 acc[TJ][TI];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+
+  const int r = lane & 31, h = lane >> 5;
+  u32x4 ra[LA], rb[LB];
+  auto gload = [&](long long pb) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int row = tid / VA + (256 / VA) * i;
+      const long long m = pb + row;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (m < pend && a_cok) v = *(const u32x4*)(p.dy + m * p.lddy + co0 + a_col);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int row = tid / VB + (256 / VB) * i;
+      const long long m = pb + row;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (m < pend && b_nok) {
+        const int f = (int)(m / HW);
+        const int rem = (int)(m - (long long)f * HW);
+        const int y = rem / p.W, x = rem - (rem / p.W) * p.W;
+        const int yy = y + b_dy, xx = x + b_dx;
+        if (yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
+          const long long pix = ((long long)f * p.H + yy) * p.W + xx;
+          const T* src = b_ci < p.c0 ? p.x0 + pix * p.ld0 + b_ci : p.x1 + pix * p.ld1 + (b_ci - p.c0);
+          v = *(const u32x4*)src;
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int row = tid / VA + (256 / VA) * i;
+      *(u32x4*)(sA + row * SA + a_col * (int)sizeof(T)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int row = tid / VB + (256 / VB) * i;
+      *(u32x4*)(sB + row * SB + b_col * (int)sizeof(T)) = rb[i];
+    }
+  };
+
+  if (pbeg < pend) gload(pbeg);
+  for (long long pb = pbeg; pb < pend; pb += BP) {
+    __syncthreads();  // previous chunk's LDS reads done
+    lstore();
+    __syncthreads();
+    if (pb + BP < pend) gload(pb + BP);  // next chunk in flight under the MFMAs
+    if constexpr (sizeof(T) == 2) {
+      const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int R0 = 16 * s + 8 * (g >> 1);
+        u32x4 fa[TJ], fb[TI];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int C0 = wm * 32 * TJ + 32 * j + 16 * (g & 1);
+          s16x4 lo = tr_read(sA + (R0 + q) * SA + (C0 + 4 * pp) * 2);
+          s16x4 hi = tr_read(sA + (R0 + 4 + q) * SA + (C0 + 4 * pp) * 2);
+          u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+          fa[j] = u32x4{l2[0], l2[1], h2[0], h2[1]};
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int C0 = wn * 32 * TI + 32 * i + 16 * (g & 1);
+          s16x4 lo = tr_read(sB + (R0 + q) * SB + (C0 + 4 * pp) * 2);
+          s16x4 hi = tr_read(sB + (R0 + 4 + q) * SB + (C0 + 4 * pp) * 2);
+          u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+          fb[i] = u32x4{l2[0], l2[1], h2[0], h2[1]};
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int i = 0; i < TI; ++i) acc[j][i] = Mma<bf16>::run(fa[j], fb[i], acc[j][i]);
+      }
+    } else {
+#pragma unroll 4
+      for (int s = 0; s < BP / 2; ++s) {
+        const int row = 2 * s + h;
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const float a = *(const float*)(sA + row * SA + (wm * 32 * TJ + 32 * j + r) * 4);
+#pragma unroll
+          for (int i = 0; i < TI; ++i) {
+            const float b = *(const float*)(sB + row * SB + (wn * 32 * TI + 32 * i + r) * 4);
+            acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[j][i], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  // acc[j][i]: row co = (reg&3) + 8*(reg>>2) + 4h, column n' = r
+#pragma unroll
+  for (int j = 0; j < TJ; ++j)
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int n = nk0 + wn * 32 * TI + 32 * i + r;
+      if (n >= p.K) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = co0 + wm * 32 * TJ + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (co < p.cout) atomicAdd(p.ws + (long long)co * p.K + n, acc[j][i][e]);
+      }
+    }
+}
+
+template <typename T>
+__global__ void pack_weight_kernel(const float* w, T* out, int cout, int cin, int taps,
+                                   int pad_to, int mode) {
+  // mode 0: out[co][tap][ci_p] (ci_p < pad_to); mode 1: out[ci][tap'][co_p]
+  long long total = mode == 0 ? (long long)cout * taps * pad_to : (long long)cin * taps * pad_to;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (mode == 0) {
+      int ci = (int)(idx % pad_to);
+      long long t = idx / pad_to;
+      int tap = (int)(t % taps), co = (int)(t / taps);
+      if (ci < cin) v = w[((long long)co * cin + ci) * taps + tap];
+    } else {
+      int co = (int)(idx % pad_to);
+      long long t = idx / pad_to;
+      int tapd = (int)(t % taps), ci = (int)(t / taps);
+      if (co < cout) v = w[((long long)co * cin + ci) * taps + (taps - 1 - tapd)];
+    }
+    out[idx] = (T)v;
+  }
+}
+
+__global__ void unpack_wgrad_kernel(const float* ws, float* dw, int cout, int cin, int taps,
+                                    int cout_real, int cin_real, int accumulate) {
+  long long total = (long long)cout_real * cin_real * taps;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    int tap = (int)(idx % taps);
+    long long t = idx / taps;
+    int ci = (int)(t % cin_real), co = (int)(t / cin_real);
+    float v = ws[((long long)co * taps + tap) * cin + ci];
+    dw[idx] = accumulate ? dw[idx] + v : v;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bias_grad_kernel(const T* dy, int lddy, float* db,
+                                                        long long npix, int c, long long rows_per) {
+  __shared__ float sh[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + cl;
+  long long beg = blockIdx.y * rows_per, end = beg + rows_per;
+  if (end > npix) end = npix;
+  float s = 0.f;
+  if (ch < c)
+    for (long long m = beg + rg; m < end; m += 4) s += (float)dy[m * lddy + ch];
+  sh[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && ch < c) atomicAdd(db + ch, sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]);
+}
+
+template <typename T, int BM, int BN>
+int launch_fwd(const ConvFwdArgs<T>& a, hipStream_t st) {
+  dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)((a.cout + BN - 1) / BN));
+  conv_fwd_kernel<T, BM, BN><<<grid, 256, 0, st>>>(a);
+  return check_launch("conv_fwd");
+}
+
+template <typename T>
+int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const void* w,
+               const float* bias, const void* res, int ldres, void* y, int ldy, int nf, int h,
+               int wd, int cin, int cout, int ks, int act, hipStream_t st) {
+  ConvFwdArgs<T> a;
+  a.x0 = (const T*)x0; a.x1 = (const T*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0;
+  a.c0 = x1 ? c0 : cin; a.w = (const T*)w; a.bias = bias; a.res = (const T*)res;
+  a.ldres = ldres; a.y = (T*)y; a.ldy = ldy; a.H = h; a.W = wd; a.cin = cin; a.cout = cout;
+  a.ks = ks; a.act = act; a.M = (long long)nf * h * wd; a.K = ks * ks * cin;
+  if (a.M == 0 || cout == 0) return DV_OK;
+  const long long mt128 = (a.M + 127) / 128;
+  int bn = cout <= 64 ? 64 : 128;
+  int bm = 128;
+  if (mt128 * ((cout + bn - 1) / bn) < 512) bm = 64;
+  if (bm == 64 && bn == 128 && ((a.M + 63) / 64) * ((cout + 127) / 128) < 512) bn = 64;
+  if (bm == 128 && bn == 128) return launch_fwd<T, 128, 128>(a, st);
+  if (bm == 128 && bn == 64) return launch_fwd<T, 128, 64>(a, st);
+  if (bm == 64 && bn == 128) return launch_fwd<T, 64, 128>(a, st);
+  return launch_fwd<T, 64, 64>(a, st);
+}
+
+template <typename T, int BMC, int BNK>
+int launch_wgrad(WgradArgs<T> a, hipStream_t st) {
+  const int mt = (a.cout + BMC - 1) / BMC, nt = (a.K + BNK - 1) / BNK;
+  // aim for ~4 blocks per CU over the whole grid, at least 256 pixels/split
+  long long want = 1024 / ((long long)mt * nt);
+  if (want < 1) want = 1;
+  long long per = (a.M + want - 1) / want;
+  per = ((per + 255) / 256) * 256;
+  if (per < 256) per = 256;
+  a.pix_per_split = (int)per;
+  const unsigned splits = (unsigned)((a.M + per - 1) / per);
+  dim3 grid(mt, nt, splits);
+  conv_wgrad_kernel<T, BMC, BNK><<<grid, 256, 0, st>>>(a);
+  return check_launch("conv_wgrad");
+}
+
+template <typename T>
+int conv_wgrad_t(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
+                 int ld1, float* ws, int nf, int h, int w, int cin, int cout, int ks,
+                 hipStream_t st) {
+  WgradArgs<T> a;
+  a.dy = (const T*)dy; a.lddy = lddy; a.x0 = (const T*)x0; a.x1 = (const T*)(x1 ? x1 : x0);
+  a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0; a.c0 = x1 ? c0 : cin; a.ws = ws; a.H = h; a.W = w;
+  a.cin = cin; a.cout = cout; a.ks = ks; a.K = ks * ks * cin; a.M = (long long)nf * h * w;
+  a.pix_per_split = 0;
+  if (a.M == 0) return DV_OK;
+  const bool small_co = cout <= 64;
+  const bool small_k = a.K <= 64;
+  if (small_co && small_k) return launch_wgrad<T, 64, 64>(a, st);
+  if (small_co) return launch_wgrad<T, 64, 128>(a, st);
+  if (small_k) return launch_wgrad<T, 128, 64>(a, st);
+  return launch_wgrad<T, 128, 128>(a, st);
+}
+
+}  // namespace
+
+extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
+                           const void* wpack, const float* bias, const void* res, int ldres,
+                           void* y, int ldy, int nf, int h, int w, int cin, int cout, int ksize,
+                           int act, void* stream) {
+  DV_REQUIRE(x0 && wpack && y, "null pointer");
+  DV_REQUIRE(cin > 0 && cin % 8 == 0, "cin must be a positive multiple of 8");
+  DV_REQUIRE(ld0 % 8 == 0 && (!x1 || (ld1 % 8 == 0 && c0 % 8 == 0 && c0 > 0 && c0 < cin)),
+             "input strides / split must be multiples of 8");
+  DV_REQUIRE(ksize >= 1 && (ksize & 1), "ksize must be odd");
+  DV_REQUIRE(ldy >= cout && (!res || ldres >= cout), "bad output stride");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DV_F32)
+    return conv_fwd_t<float>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, y, ldy, nf, h, w,
+                             cin, cout, ksize, act, st);
+  if (dtype == DV_BF16)
+    return conv_fwd_t<bf16>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, y, ldy, nf, h, w,
+                            cin, cout, ksize, act, st);
+  DV_REQUIRE(false, "unknown dtype");
+}
+
+extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0,
+                             int c0, const void* x1, int ld1, float* ws, int nf, int h, int w,
+                             int cin, int cout, int ksize, void* stream) {
+  DV_REQUIRE(dy && x0 && ws, "null pointer");
+  DV_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "cin/cout must be multiples of 8");
+  DV_REQUIRE(lddy % 8 == 0 && ld0 % 8 == 0 && (!x1 || (ld1 % 8 == 0 && c0 % 8 == 0)),
+             "strides must be multiples of 8");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DV_F32)
+    return conv_wgrad_t<float>(dy, lddy, x0, ld0, c0, x1, ld1, ws, nf, h, w, cin, cout, ksize, st);
+  if (dtype == DV_BF16)
+    return conv_wgrad_t<bf16>(dy, lddy, x0, ld0, c0, x1, ld1, ws, nf, h, w, cin, cout, ksize, st);
+  DV_REQUIRE(false, "unknown dtype");
+}
+
+extern "C" int dv_unpack_wgrad(const float* ws, float* dw, int cout, int cin, int ksize,
+                               int cout_real, int cin_real, int accumulate, void* stream) {
+  DV_REQUIRE(ws && dw && cout_real <= cout && cin_real <= cin, "bad arguments");
+  const int taps = ksize * ksize;
+  long long total = (long long)cout_real * cin_real * taps;
+  if (total == 0) return DV_OK;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  unpack_wgrad_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(ws, dw, cout, cin, taps, cout_real,
+                                                               cin_real, accumulate);
+  return check_launch("unpack_wgrad");
+}
+
+extern "C" int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix, int c,
+                            void* stream) {
+  DV_REQUIRE(dy && db, "null pointer");
+  if (npix == 0) return DV_OK;
+  long long rows_per = 2048;
+  dim3 grid((c + 63) / 64, (unsigned)((npix + rows_per - 1) / rows_per));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DV_F32)
+    bias_grad_kernel<float><<<grid, 256, 0, st>>>((const float*)dy, lddy, db, npix, c, rows_per);
+  else
+    bias_grad_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)dy, lddy, db, npix, c, rows_per);
+  return check_launch("bias_grad");
+}
+
+extern "C" int dv_pack_conv_weight(int dtype, const float* w, void* out, int cout, int cin,
+                                   int ksize, int pad_to, int mode, void* stream) {
+  DV_REQUIRE(w && out, "null pointer");
+  DV_REQUIRE(mode == 0 ? pad_to >= cin : pad_to >= cout, "pad_to too small");
+  const int taps = ksize * ksize;
+  long long total = mode == 0 ? (long long)cout * taps * pad_to : (long long)cin * taps * pad_to;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DV_F32)
+    pack_weight_kernel<float><<<blocks, 256, 0, st>>>(w, (float*)out, cout, cin, taps, pad_to, mode);
+  else
+    pack_weight_kernel<bf16><<<blocks, 256, 0, st>>>(w, (bf16*)out, cout, cin, taps, pad_to, mode);
+  return check_launch("pack_conv_weight");
+}

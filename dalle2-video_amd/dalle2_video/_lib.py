@@ -1,0 +1,90 @@
+"""ctypes binding of libdv_hip.so (the C-ABI declared in include/dv_hip.h).
+
+This is the reference-side stub a maintainer would add to bind the HIP path:
+plain pointers, ints and the current HIP stream.  There is NO fallback: if
+the library is missing or no GPU is present, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DV_HIP_LIB", os.path.join(_HERE, "libdv_hip.so"))
+
+DV_F32, DV_BF16 = 0, 1
+ACT_NONE, ACT_SILU = 0, 1
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_longlong
+_F = ctypes.c_float
+
+# name -> argtypes (restype is always int except dv_last_error)
+_SIGS = {
+    "dv_abi_version": [],
+    "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dv_conv_wgrad": [_I, _P, _I, _P, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_unpack_wgrad": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
+    "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
+}
+
+
+class DVError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DVError(f"libdv_hip.so not found at {LIB_PATH}; build it with "
+                          f"`make -C dalle2-video_amd/csrc` (HIP path has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.dv_last_error.restype = ctypes.c_char_p
+        L.dv_last_error.argtypes = []
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return ["dv_last_error", *_SIGS.keys()]
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().dv_last_error().decode(errors="replace")
+        raise DVError(f"{name} failed ({rc}): {msg}")
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return DV_F32
+    if t.dtype == torch.bfloat16:
+        return DV_BF16
+    raise DVError(f"unsupported dtype {t.dtype}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def require_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise DVError("the HIP path runs on the GPU only (got a CPU tensor)")

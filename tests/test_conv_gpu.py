@@ -1,0 +1,59 @@
+"""HIP implicit-GEMM conv (fwd / dgrad / wgrad / bias-grad) vs torch fp32 CPU."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # nf, h, w, c0, c1, cout, k
+    (2, 8, 8, 64, 0, 64, 3),
+    (3, 5, 7, 16, 8, 40, 3),
+    (4, 16, 16, 128, 64, 128, 3),
+    (2, 8, 8, 8, 0, 32, 7),
+    (1, 12, 12, 8, 0, 16, 15),
+    (5, 4, 4, 256, 0, 512, 1),
+    (2, 6, 6, 64, 0, 3, 1),
+    (1, 33, 9, 32, 32, 96, 3),
+]
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
+@pytest.mark.parametrize("case", CASES)
+def test_conv_fwd_bwd(case, dtype, tol):
+    from dalle2_video import ops
+
+    nf, h, w, c0, c1, cout, k = case
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    cin = c0 + c1
+    x = torch.randn(nf, h, w, cin, generator=g)
+    wt = torch.randn(cout, cin, 1, k, k, generator=g) / (cin * k * k) ** 0.5
+    b = torch.randn(cout, generator=g)
+    res = torch.randn(nf, h, w, cout, generator=g)
+    gy = torch.randn(nf, h, w, cout, generator=g)
+    # reference in fp32 on the bf16-rounded inputs
+    xr = x.to(dtype).float().clone().requires_grad_()
+    wr = wt.to(dtype).float().requires_grad_() if dtype != torch.float32 else wt.clone().requires_grad_()
+    br = b.clone().requires_grad_()
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr[:, :, 0], br, padding=k // 2).permute(0, 2, 3, 1)
+    yr = yr + res.to(dtype).float()
+    (yr * gy).sum().backward()
+
+    dev = "cuda"
+    xd = x.detach().to(dev, dtype)
+    x0 = xd[..., :c0].clone().requires_grad_() if c1 else xd.clone().requires_grad_()
+    x1 = xd[..., c0:].clone().requires_grad_() if c1 else None
+    wd = wt.to(dev).requires_grad_()
+    bd = b.to(dev).requires_grad_()
+    y = ops.conv(x0, wd, bd, x1=x1, res=res.to(dev, dtype))
+    assert rel(y.float(), yr) < tol
+    (y.float() * gy.to(dev)).sum().backward()
+    dx = torch.cat([x0.grad] + ([x1.grad] if c1 else []), dim=-1)
+    assert rel(dx.float(), xr.grad) < tol * 2
+    assert rel(wd.grad, wr.grad) < tol * 2
+    assert rel(bd.grad, br.grad) < tol

@@ -1,0 +1,59 @@
+"""Micro-benchmark of individual HIP kernels at the Cfg2 (B=4,T=16,64x64) shapes."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dalle2-video_amd"))
+import torch  # noqa: E402
+
+from dalle2_video import ops  # noqa: E402
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def conv_case(nf, h, w, cin, cout, k, dtype=torch.bfloat16):
+    x = torch.randn(nf, h, w, cin, device="cuda", dtype=dtype)
+    wt = (torch.randn(cout, cin, 1, k, k, device="cuda") / (cin * k * k) ** 0.5).requires_grad_()
+    b = torch.randn(cout, device="cuda")
+    flops = 2.0 * nf * h * w * cout * cin * k * k
+    wp = ops.pack_conv_weight(wt, dtype, cin, 0)
+    y = torch.empty(nf, h, w, cout, device="cuda", dtype=dtype)
+    from dalle2_video._lib import call, ptr, stream, dt
+    def fwd():
+        call("dv_conv_fwd", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
+             cout, nf, h, w, cin, cout, k, 0, stream())
+    ms = timeit(fwd)
+    dy = torch.randn_like(y)
+    ws = torch.zeros(cout, k * k, cin, device="cuda")
+    def wgrad():
+        call("dv_conv_wgrad", dt(x), ptr(dy), cout, ptr(x), cin, cin, None, 0, ptr(ws), nf, h, w,
+             cin, cout, k, stream())
+    msw = timeit(wgrad)
+    print(f"conv nf={nf} {h}x{w} {cin}->{cout} k={k} {str(dtype)[6:]}: fwd {ms*1e3:8.1f} us "
+          f"{flops/ms/1e9:7.1f} TF/s | wgrad {msw*1e3:8.1f} us {flops/msw/1e9:7.1f} TF/s")
+
+
+if __name__ == "__main__":
+    for dt_ in (torch.bfloat16,):
+        conv_case(64, 64, 64, 64, 64, 3, dt_)
+        conv_case(64, 64, 64, 128, 64, 3, dt_)
+        conv_case(64, 32, 32, 128, 128, 3, dt_)
+        conv_case(64, 16, 16, 256, 256, 3, dt_)
+        conv_case(64, 8, 8, 512, 512, 3, dt_)
+        conv_case(64, 8, 8, 768, 512, 3, dt_)
+        conv_case(64, 32, 32, 256, 64, 1, dt_)
+        conv_case(64, 64, 64, 8, 32, 3, dt_)
+        conv_case(64, 64, 64, 8, 16, 15, dt_)
+    conv_case(64, 64, 64, 64, 64, 3, torch.float32)
