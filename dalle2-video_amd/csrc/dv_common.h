@@ -65,18 +65,23 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 template <typename T> struct Vec { };
 template <> struct Vec<float> {
   static constexpr int N = 4;
+  // NB: cast the whole vector; bit-casting single u32x4 elements in an
+  // unrolled loop miscompiles on hipcc 7.2 (every element reads element 0).
   __device__ static inline void to_f(u32x4 v, float* o) {
+    const f32x4 f = __builtin_bit_cast(f32x4, v);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = __builtin_bit_cast(float, v[i]);
+    for (int i = 0; i < 4; ++i) o[i] = f[i];
   }
 };
 template <> struct Vec<bf16> {
   static constexpr int N = 8;
   __device__ static inline void to_f(u32x4 v, float* o) {
+    const f32x4 lo = __builtin_bit_cast(f32x4, v << 16);
+    const f32x4 hi = __builtin_bit_cast(f32x4, v & 0xffff0000u);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      o[2 * i] = __builtin_bit_cast(float, v[i] << 16);
-      o[2 * i + 1] = __builtin_bit_cast(float, v[i] & 0xffff0000u);
+      o[2 * i] = lo[i];
+      o[2 * i + 1] = hi[i];
     }
   }
 };

@@ -1,0 +1,452 @@
+// Byte-moving and small kernels of the Unet3D path (all HBM- or launch-bound):
+//   layout conversion at the NCTHW module boundary, space-to-depth
+//   (Downsample3D, dalle2_video.py:22-25), SiLU+PixelShuffle
+//   (PixelShuffleUpsample3D, :64-78), q_sample + l2 loss (p_losses :1956,
+//   :1997-2002), the p_sample posterior update (:1551-1664), the time MLPs
+//   (:348-357, :755-761, ResnetBlock3D.time_mlp :150-155), AdamW and the
+//   gradient norm (trainer.py:247-274).
+#include "dv_common.h"
+
+using namespace dv;
+
+namespace {
+
+int grid_for(long long work, int per_block = 256, int cap = 16384) {
+  long long b = (work + per_block - 1) / per_block;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+#define GRID_STRIDE(i, n) \
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (n); i += (long long)gridDim.x * blockDim.x)
+
+template <typename T>
+__global__ void ncthw_to_cl_kernel(const float* x, T* y, int B, int C, int T_, int HW, int cpad) {
+  const long long npix = (long long)B * T_ * HW;
+  GRID_STRIDE(p, npix) {
+    const int hw = (int)(p % HW);
+    const long long ft = p / HW;
+    const int t = (int)(ft % T_), b = (int)(ft / T_);
+    for (int c = 0; c < cpad; ++c) {
+      float v = c < C ? x[(((long long)b * C + c) * T_ + t) * HW + hw] : 0.f;
+      y[p * cpad + c] = (T)v;
+    }
+  }
+}
+
+template <typename T>
+__global__ void cl_to_ncthw_kernel(const T* y, int ld, float* x, int B, int C, int T_, int HW) {
+  const long long npix = (long long)B * T_ * HW;
+  GRID_STRIDE(p, npix) {
+    const int hw = (int)(p % HW);
+    const long long ft = p / HW;
+    const int t = (int)(ft % T_), b = (int)(ft / T_);
+    for (int c = 0; c < C; ++c) x[(((long long)b * C + c) * T_ + t) * HW + hw] = (float)y[p * ld + c];
+  }
+}
+
+// unit = (frame, low-res y, x, group of VEC high-res channels)
+template <typename T, int MODE>
+__global__ void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* z, int ldz, int nf,
+                               int H, int W, int C, int act) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int cg = C / VEC;
+  const long long total = (long long)nf * H * W * cg;
+  GRID_STRIDE(idx, total) {
+    const int g = (int)(idx % cg);
+    const long long lp = idx / cg;  // low-res pixel
+    const int x = (int)(lp % W);
+    const long long fy = lp / W;
+    const int y = (int)(fy % H);
+    const long long f = fy / H;
+    const int c0 = g * VEC;
+    float lo[4 * VEC];  // low-res span, element (c - c0)*4 + i*2 + j
+    if (MODE == 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Vec<T>::to_f(*(const u32x4*)(src + lp * lds + c0 * 4 + q * VEC), lo + q * VEC);
+#pragma unroll
+      for (int e = 0; e < 4 * VEC; ++e) lo[e] = act == DV_ACT_SILU ? silu_f(lo[e]) : lo[e];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const long long hp = (f * 2 * H + 2 * y + i) * 2 * W + 2 * x + j;
+          T o[VEC];
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) o[e] = (T)lo[e * 4 + i * 2 + j];
+          *(u32x4*)(dst + hp * ldd + c0) = *(const u32x4*)o;
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const long long hp = (f * 2 * H + 2 * y + i) * 2 * W + 2 * x + j;
+          float hv[VEC];
+          Vec<T>::to_f(*(const u32x4*)(src + hp * lds + c0), hv);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) lo[e * 4 + i * 2 + j] = hv[e];
+        }
+      if (z) {  // backward of SiLU+shuffle: multiply by silu'(z)
+        float zz[4 * VEC];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Vec<T>::to_f(*(const u32x4*)(z + lp * ldz + c0 * 4 + q * VEC), zz + q * VEC);
+#pragma unroll
+        for (int e = 0; e < 4 * VEC; ++e) {
+          const float sg = sigmoid_f(zz[e]);
+          lo[e] *= sg * (1.f + zz[e] * (1.f - sg));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        T o[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) o[e] = (T)lo[q * VEC + e];
+        *(u32x4*)(dst + lp * ldd + c0 * 4 + q * VEC) = *(const u32x4*)o;
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void q_sample_kernel(const float* x0, const float* noise, const long long* t,
+                                const float* sa, const float* s1m, T* y, int B, int C, int T_,
+                                int HW, int cpad, int normalize) {
+  const long long npix = (long long)B * T_ * HW;
+  GRID_STRIDE(p, npix) {
+    const int hw = (int)(p % HW);
+    const long long ft = p / HW;
+    const int tt = (int)(ft % T_), b = (int)(ft / T_);
+    const long long ti = t[b];
+    const float a = sa[ti], s = s1m[ti];
+    for (int c = 0; c < cpad; ++c) {
+      float v = 0.f;
+      if (c < C) {
+        const long long i = (((long long)b * C + c) * T_ + tt) * HW + hw;
+        const float xs = normalize ? x0[i] * 2.f - 1.f : x0[i];
+        v = a * xs + s * noise[i];
+      }
+      y[p * cpad + c] = (T)v;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void mse_kernel(const T* pred, int ld, const float* target, int B,
+                                                  int C, int T_, int HW, const float* w,
+                                                  float* loss, float scale) {
+  __shared__ float sh[4];
+  const long long npix = (long long)B * T_ * HW;
+  float acc = 0.f;
+  GRID_STRIDE(p, npix) {
+    const int hw = (int)(p % HW);
+    const long long ft = p / HW;
+    const int tt = (int)(ft % T_), b = (int)(ft / T_);
+    const float wb = w ? w[b] : 1.f;
+    for (int c = 0; c < C; ++c) {
+      const float d = (float)pred[p * ld + c] - target[(((long long)b * C + c) * T_ + tt) * HW + hw];
+      acc += wb * d * d;
+    }
+  }
+  acc = block_sum<256>(acc, sh);
+  if (threadIdx.x == 0) atomicAdd(loss, acc * scale);
+}
+
+template <typename T>
+__global__ void mse_bwd_kernel(const T* pred, int ld, const float* target, int B, int C, int T_,
+                               int HW, const float* w, const float* dloss, float scale, T* dp,
+                               int lddp) {
+  const long long npix = (long long)B * T_ * HW;
+  const float g = dloss[0] * scale;
+  GRID_STRIDE(p, npix) {
+    const int hw = (int)(p % HW);
+    const long long ft = p / HW;
+    const int tt = (int)(ft % T_), b = (int)(ft / T_);
+    const float wb = w ? w[b] : 1.f;
+    for (int c = 0; c < C; ++c) {
+      const float d = (float)pred[p * ld + c] - target[(((long long)b * C + c) * T_ + tt) * HW + hw];
+      dp[p * lddp + c] = (T)(2.f * g * wb * d);
+    }
+  }
+}
+
+// freqs[k] = exp(-k*ln(1e4)/(half-1)) is a constant table built once on the host
+// exactly as SinusoidalPosEmb builds it; t is cast to f32 (time.type_as(x)).
+__global__ void sinusoidal_kernel(const long long* t, const float* freqs, float* out, int B, int dim) {
+  const int half = dim / 2;
+  GRID_STRIDE(i, (long long)B * dim) {
+    const int b = (int)(i / dim), k = (int)(i % dim);
+    const float a = (float)t[b] * freqs[k < half ? k : k - half];
+    out[i] = k < half ? sinf(a) : cosf(a);
+  }
+}
+
+__device__ __forceinline__ float act_in_f(float x, int act) { return act == 1 ? silu_f(x) : x; }
+__device__ __forceinline__ float act_in_d(float x, int act) {
+  if (act != 1) return 1.f;
+  const float s = sigmoid_f(x);
+  return s * (1.f + x * (1.f - s));
+}
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_d(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * expf(-0.5f * x * x);
+}
+
+// y[b][n] = act_out(sum_k act_in(x[b][k]) W[n][k] + bias[n]); one wave per n
+__global__ __launch_bounds__(256) void linear_small_kernel(const float* x, int ldx, const float* W,
+                                                           const float* bias, float* y, int ldy,
+                                                           float* z, int B, int K, int N,
+                                                           int act_in, int act_out) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  for (int b = 0; b < B; ++b) {
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s += act_in_f(x[(long long)b * ldx + k], act_in) * W[(long long)n * K + k];
+    s = wave_sum(s);
+    if (lane == 0) {
+      s += bias ? bias[n] : 0.f;
+      if (z) z[(long long)b * N + n] = s;
+      y[(long long)b * ldy + n] = act_out == 2 ? gelu_f(s) : s;
+    }
+  }
+}
+
+__device__ __forceinline__ float lin_g(const float* dy, int lddy, const float* z, int b, int n, int N,
+                                       int act_out) {
+  const float d = dy[(long long)b * lddy + n];
+  return act_out == 2 ? d * gelu_d(z[(long long)b * N + n]) : d;
+}
+
+__global__ void linear_small_dw_kernel(const float* dy, int lddy, const float* x, int ldx,
+                                       const float* z, float* dW, float* db, int B, int K, int N,
+                                       int act_in, int act_out) {
+  GRID_STRIDE(i, (long long)N * K) {
+    const int n = (int)(i / K), k = (int)(i % K);
+    float s = 0.f, sb = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float g = lin_g(dy, lddy, z, b, n, N, act_out);
+      s += g * act_in_f(x[(long long)b * ldx + k], act_in);
+      sb += g;
+    }
+    dW[i] = s;
+    if (db && k == 0) db[n] = sb;
+  }
+}
+
+__global__ void linear_small_dx_kernel(const float* dy, int lddy, const float* x, int ldx,
+                                       const float* W, const float* z, float* dx, int lddx, int B,
+                                       int K, int N, int act_in, int act_out, int accumulate) {
+  GRID_STRIDE(i, (long long)B * K) {
+    const int b = (int)(i / K), k = (int)(i % K);
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += lin_g(dy, lddy, z, b, n, N, act_out) * W[(long long)n * K + k];
+    s *= act_in_d(x[(long long)b * ldx + k], act_in);
+    float* o = dx + (long long)b * lddx + k;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
+__global__ void adamw_kernel(float* p, const float* g, float* m, float* v, long long n,
+                             long long n_wd, float lr, float b1, float b2, float eps, float wd,
+                             float bc1, float bc2_sqrt, const float* clip) {
+  const float cc = clip ? clip[0] : 1.f;
+  const float step = lr / bc1;
+  GRID_STRIDE(i, n) {
+    const float gi = g[i] * cc;
+    float pi = p[i];
+    if (i < n_wd) pi *= 1.f - lr * wd;
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi - step * (mi / denom);
+  }
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* x, long long n, float* out) {
+  __shared__ float sh[4];
+  float acc = 0.f;
+  GRID_STRIDE(i, n) acc += x[i] * x[i];
+  acc = block_sum<256>(acc, sh);
+  if (threadIdx.x == 0) atomicAdd(out, acc);
+}
+
+__global__ void clip_coef_kernel(const float* sumsq, float max_norm, float* coef) {
+  const float c = max_norm / (sqrtf(sumsq[0]) + 1e-6f);
+  coef[0] = c < 1.f ? c : 1.f;
+}
+
+template <typename T>
+__global__ void p_sample_kernel(const float* x, const T* eps, int ld, const float* noise,
+                                const long long* t, const float* sra, const float* srm1,
+                                const float* c1, const float* c2, const float* logvar, float* out,
+                                float* x0_out, int B, int C, int T_, int HW, int clip) {
+  const long long n = (long long)B * C * T_ * HW;
+  GRID_STRIDE(i, n) {
+    const int hw = (int)(i % HW);
+    long long r = i / HW;
+    const int tt = (int)(r % T_);
+    r /= T_;
+    const int c = (int)(r % C), b = (int)(r / C);
+    const long long ti = t[b];
+    const long long p = ((long long)b * T_ + tt) * HW + hw;
+    float x0 = sra[ti] * x[i] - srm1[ti] * (float)eps[p * ld + c];
+    if (clip) x0 = fminf(fmaxf(x0, -1.f), 1.f);
+    const float mean = c1[ti] * x0 + c2[ti] * x[i];
+    const float nz = ti == 0 ? 0.f : 1.f;
+    out[i] = mean + nz * expf(0.5f * logvar[ti]) * noise[i];
+    if (x0_out) x0_out[i] = x0;
+  }
+}
+
+}  // namespace
+
+#define DISPATCH(dtype, KERNEL_CALL_F32, KERNEL_CALL_BF16) \
+  do {                                                      \
+    if ((dtype) == DV_F32) { KERNEL_CALL_F32; }             \
+    else if ((dtype) == DV_BF16) { KERNEL_CALL_BF16; }      \
+    else DV_REQUIRE(false, "unknown dtype");                \
+  } while (0)
+
+extern "C" int dv_ncthw_to_cl(int dtype, const float* x, void* y, int B, int C, int T, int H,
+                              int W, int cpad, void* stream) {
+  DV_REQUIRE(x && y && cpad >= C, "bad arguments");
+  const long long npix = (long long)B * T * H * W;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH(dtype,
+           (ncthw_to_cl_kernel<float><<<grid_for(npix), 256, 0, st>>>(x, (float*)y, B, C, T, H * W, cpad)),
+           (ncthw_to_cl_kernel<bf16><<<grid_for(npix), 256, 0, st>>>(x, (bf16*)y, B, C, T, H * W, cpad)));
+  return check_launch("ncthw_to_cl");
+}
+
+extern "C" int dv_cl_to_ncthw(int dtype, const void* y, int ld, float* x, int B, int C, int T, int H,
+                              int W, void* stream) {
+  DV_REQUIRE(x && y && ld >= C, "bad arguments");
+  const long long npix = (long long)B * T * H * W;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH(dtype,
+           (cl_to_ncthw_kernel<float><<<grid_for(npix), 256, 0, st>>>((const float*)y, ld, x, B, C, T, H * W)),
+           (cl_to_ncthw_kernel<bf16><<<grid_for(npix), 256, 0, st>>>((const bf16*)y, ld, x, B, C, T, H * W)));
+  return check_launch("cl_to_ncthw");
+}
+
+extern "C" int dv_shuffle(int dtype, int mode, const void* src, int lds, void* dst, int ldd,
+                          const void* z, int ldz, int nf, int H, int W, int C, int act,
+                          void* stream) {
+  DV_REQUIRE(src && dst && (mode == 0 || mode == 1), "bad arguments");
+  const int VEC = dtype == DV_BF16 ? 8 : 4;
+  DV_REQUIRE(C % VEC == 0 && lds % VEC == 0 && ldd % VEC == 0 && (!z || ldz % VEC == 0),
+             "channels / strides must be multiples of 16 bytes");
+  const long long units = (long long)nf * H * W * (C / VEC);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DV_F32) {
+    if (mode == 0) shuffle_kernel<float, 0><<<grid_for(units), 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, nf, H, W, C, act);
+    else shuffle_kernel<float, 1><<<grid_for(units), 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, nf, H, W, C, act);
+  } else {
+    if (mode == 0) shuffle_kernel<bf16, 0><<<grid_for(units), 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, nf, H, W, C, act);
+    else shuffle_kernel<bf16, 1><<<grid_for(units), 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, nf, H, W, C, act);
+  }
+  return check_launch("shuffle");
+}
+
+extern "C" int dv_q_sample(int dtype, const float* x0, const float* noise, const long long* t,
+                           const float* sqrt_ac, const float* sqrt_1m_ac, void* y, int B, int C,
+                           int T, int H, int W, int cpad, int normalize, void* stream) {
+  DV_REQUIRE(x0 && noise && t && sqrt_ac && sqrt_1m_ac && y && cpad >= C, "bad arguments");
+  const long long npix = (long long)B * T * H * W;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH(dtype,
+           (q_sample_kernel<float><<<grid_for(npix), 256, 0, st>>>(x0, noise, t, sqrt_ac, sqrt_1m_ac, (float*)y, B, C, T, H * W, cpad, normalize)),
+           (q_sample_kernel<bf16><<<grid_for(npix), 256, 0, st>>>(x0, noise, t, sqrt_ac, sqrt_1m_ac, (bf16*)y, B, C, T, H * W, cpad, normalize)));
+  return check_launch("q_sample");
+}
+
+extern "C" int dv_mse_loss(int dtype, const void* pred, int ld, const float* target, int B, int C,
+                           int T, int H, int W, const float* sample_w, float* loss, void* stream) {
+  DV_REQUIRE(pred && target && loss, "bad arguments");
+  const long long npix = (long long)B * T * H * W;
+  const float scale = 1.f / (float)((double)B * C * T * H * W);
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(loss, 0, sizeof(float), st);
+  const int g = grid_for(npix, 256, 1024);
+  DISPATCH(dtype,
+           (mse_kernel<float><<<g, 256, 0, st>>>((const float*)pred, ld, target, B, C, T, H * W, sample_w, loss, scale)),
+           (mse_kernel<bf16><<<g, 256, 0, st>>>((const bf16*)pred, ld, target, B, C, T, H * W, sample_w, loss, scale)));
+  return check_launch("mse_loss");
+}
+
+extern "C" int dv_mse_loss_bwd(int dtype, const void* pred, int ld, const float* target, int B,
+                               int C, int T, int H, int W, const float* sample_w,
+                               const float* dloss, void* dpred, int lddp, void* stream) {
+  DV_REQUIRE(pred && target && dloss && dpred, "bad arguments");
+  const long long npix = (long long)B * T * H * W;
+  const float scale = 1.f / (float)((double)B * C * T * H * W);
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH(dtype,
+           (mse_bwd_kernel<float><<<grid_for(npix), 256, 0, st>>>((const float*)pred, ld, target, B, C, T, H * W, sample_w, dloss, scale, (float*)dpred, lddp)),
+           (mse_bwd_kernel<bf16><<<grid_for(npix), 256, 0, st>>>((const bf16*)pred, ld, target, B, C, T, H * W, sample_w, dloss, scale, (bf16*)dpred, lddp)));
+  return check_launch("mse_loss_bwd");
+}
+
+extern "C" int dv_sinusoidal(const long long* t, const float* freqs, float* out, int B, int dim,
+                             void* stream) {
+  DV_REQUIRE(t && freqs && out && dim >= 4 && dim % 2 == 0, "bad arguments");
+  sinusoidal_kernel<<<grid_for((long long)B * dim), 256, 0, (hipStream_t)stream>>>(t, freqs, out, B, dim);
+  return check_launch("sinusoidal");
+}
+
+extern "C" int dv_linear_small_fwd(const float* x, int ldx, const float* W, const float* bias,
+                                   float* y, int ldy, float* z, int B, int K, int N, int act_in,
+                                   int act_out, void* stream) {
+  DV_REQUIRE(x && W && y && (act_out != 2 || z), "bad arguments");
+  linear_small_kernel<<<(N + 3) / 4, 256, 0, (hipStream_t)stream>>>(x, ldx, W, bias, y, ldy, z, B,
+                                                                     K, N, act_in, act_out);
+  return check_launch("linear_small_fwd");
+}
+
+extern "C" int dv_linear_small_bwd(const float* dy, int lddy, const float* x, int ldx,
+                                   const float* W, const float* z, float* dx, int lddx, float* dW,
+                                   float* db, int B, int K, int N, int act_in, int act_out,
+                                   int accumulate_dx, void* stream) {
+  DV_REQUIRE(dy && x && W && (act_out != 2 || z), "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  if (dW) linear_small_dw_kernel<<<grid_for((long long)N * K), 256, 0, st>>>(dy, lddy, x, ldx, z, dW, db, B, K, N, act_in, act_out);
+  if (dx) linear_small_dx_kernel<<<grid_for((long long)B * K), 256, 0, st>>>(dy, lddy, x, ldx, W, z, dx, lddx, B, K, N, act_in, act_out, accumulate_dx);
+  return check_launch("linear_small_bwd");
+}
+
+extern "C" int dv_adamw(float* p, const float* g, float* m, float* v, long long n, long long n_wd,
+                        float lr, float beta1, float beta2, float eps, float wd, float bc1,
+                        float bc2_sqrt, const float* clip_coef, void* stream) {
+  DV_REQUIRE(p && g && m && v, "null pointer");
+  adamw_kernel<<<grid_for(n, 256, 8192), 256, 0, (hipStream_t)stream>>>(p, g, m, v, n, n_wd, lr, beta1, beta2, eps, wd, bc1, bc2_sqrt, clip_coef);
+  return check_launch("adamw");
+}
+
+extern "C" int dv_grad_clip_coef(const float* g, long long n, float max_norm, float* ws,
+                                 void* stream) {
+  // ws[0] = sum of squares, ws[1] = min(max_norm / (norm + 1e-6), 1)
+  DV_REQUIRE(g && ws, "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(ws, 0, sizeof(float), st);
+  sumsq_kernel<<<grid_for(n, 256, 2048), 256, 0, st>>>(g, n, ws);
+  clip_coef_kernel<<<1, 1, 0, st>>>(ws, max_norm, ws + 1);
+  return check_launch("grad_clip_coef");
+}
+
+extern "C" int dv_p_sample(int dtype, const float* x, const void* eps, int ld, const float* noise,
+                           const long long* t, const float* sqrt_recip_ac,
+                           const float* sqrt_recipm1_ac, const float* coef1, const float* coef2,
+                           const float* logvar, float* out, float* x0_out, int B, int C, int T,
+                           int H, int W, int clip, void* stream) {
+  DV_REQUIRE(x && eps && noise && t && out, "bad arguments");
+  const long long n = (long long)B * C * T * H * W;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH(dtype,
+           (p_sample_kernel<float><<<grid_for(n), 256, 0, st>>>(x, (const float*)eps, ld, noise, t, sqrt_recip_ac, sqrt_recipm1_ac, coef1, coef2, logvar, out, x0_out, B, C, T, H * W, clip)),
+           (p_sample_kernel<bf16><<<grid_for(n), 256, 0, st>>>(x, (const bf16*)eps, ld, noise, t, sqrt_recip_ac, sqrt_recipm1_ac, coef1, coef2, logvar, out, x0_out, B, C, T, H * W, clip)));
+  return check_launch("p_sample");
+}

@@ -1,0 +1,444 @@
+// GroupNorm (Block3D.norm + scale/shift + SiLU, dalle2_video.py:109-131) and
+// row LayerNorm (dalle2-pytorch LayerNorm, used by Attention at :430 and
+// nn.LayerNorm norm_cond/norm_mid_cond at :374-375).  HBM-bound: each pass
+// reads/writes the activation once with 16-byte vectors; statistics are f32.
+#include "dv_common.h"
+
+using namespace dv;
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ void ld_vec(const T* p, float* o) {
+  Vec<T>::to_f(*(const u32x4*)p, o);
+}
+template <typename T>
+__device__ __forceinline__ void st_vec(T* p, const float* v);
+template <>
+__device__ __forceinline__ void st_vec<float>(float* p, const float* v) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+}
+template <>
+__device__ __forceinline__ void st_vec<bf16>(bf16* p, const float* v) {
+  *(bf16x8*)p = bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3],
+                       (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+}
+
+// --------------------------------------------------------------------------
+// per-(batch, channel) partial sums: ws[b][c] = {sum f(x), sum g(x)}
+//   MODE 0 (stats):    f = z, g = z^2
+//   MODE 1 (bwd):      f = dv, g = dv*zhat   (dv = dy * act'(v))
+// --------------------------------------------------------------------------
+struct GnArgs {
+  const void* z; int ldz;
+  const void* dy; int lddy;
+  void* out; int ldo;
+  const void* res; int ldres;
+  int nb; long long P; int C, G;
+  const float* mean; const float* rstd;
+  const float* gamma; const float* beta;
+  const float* ss;  // (nb, 2C): scale | shift, or null
+  int act;
+  float* ws;        // nb * C * 2
+  float* ws2;       // nb * G * 2 (bwd group coefficients)
+  long long rows_per_block;
+};
+
+template <typename T>
+__device__ __forceinline__ void gn_point(const GnArgs& a, int b, int c, float z, float& zhat,
+                                         float& u, float& v) {
+  const int g = c / (a.C / a.G);
+  const float mu = a.mean[b * a.G + g], rs = a.rstd[b * a.G + g];
+  zhat = (z - mu) * rs;
+  u = zhat * a.gamma[c] + a.beta[c];
+  v = a.ss ? u * (1.f + a.ss[(long long)b * 2 * a.C + c]) + a.ss[(long long)b * 2 * a.C + a.C + c] : u;
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
+  constexpr int VEC = 16 / sizeof(T);
+  __shared__ float sh[2][256 * VEC];
+  const int tpr = a.C / VEC;                 // threads per pixel row
+  const int rpp = 256 / tpr;                 // rows per pass
+  const int tid = threadIdx.x;
+  const int rr = tid / tpr, cv = (tid % tpr) * VEC;
+  const int b = blockIdx.y;
+  const long long beg = blockIdx.x * a.rows_per_block;
+  long long end = beg + a.rows_per_block;
+  if (end > a.P) end = a.P;
+  float s1[VEC], s2[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) s1[e] = s2[e] = 0.f;
+  if (rr < rpp) {
+    for (long long p = beg + rr; p < end; p += rpp) {
+      const long long pix = (long long)b * a.P + p;
+      float z[VEC];
+      ld_vec<T>((const T*)a.z + pix * a.ldz + cv, z);
+      if (MODE == 0) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) { s1[e] += z[e]; s2[e] += z[e] * z[e]; }
+      } else {
+        float dy[VEC];
+        ld_vec<T>((const T*)a.dy + pix * a.lddy + cv, dy);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          float zhat, u, v;
+          gn_point<T>(a, b, cv + e, z[e], zhat, u, v);
+          float dv = dy[e];
+          if (a.act == DV_ACT_SILU) {
+            const float sg = sigmoid_f(v);
+            dv *= sg * (1.f + v * (1.f - sg));
+          }
+          s1[e] += dv;
+          s2[e] += dv * zhat;
+        }
+      }
+    }
+  }
+  // block reduce over the row slots, then one atomic per channel
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    sh[0][tid * VEC + e] = (rr < rpp) ? s1[e] : 0.f;
+    sh[1][tid * VEC + e] = (rr < rpp) ? s2[e] : 0.f;
+  }
+  __syncthreads();
+  for (int c = tid; c < a.C; c += 256) {
+    const int owner = c / VEC, e = c % VEC;  // thread index within row 0 owning channel c
+    float t1 = 0.f, t2 = 0.f;
+    for (int r = 0; r < rpp; ++r) {
+      t1 += sh[0][(r * tpr + owner) * VEC + e];
+      t2 += sh[1][(r * tpr + owner) * VEC + e];
+    }
+    atomicAdd(a.ws + ((long long)b * a.C + c) * 2, t1);
+    atomicAdd(a.ws + ((long long)b * a.C + c) * 2 + 1, t2);
+  }
+}
+
+__global__ void gn_stats_finalize(const float* ws, float* mean, float* rstd, int nb, long long P,
+                                  int C, int G, float eps) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb * G) return;
+  const int b = i / G, g = i % G, cg = C / G;
+  double s1 = 0.0, s2 = 0.0;
+  for (int c = g * cg; c < (g + 1) * cg; ++c) {
+    s1 += ws[((long long)b * C + c) * 2];
+    s2 += ws[((long long)b * C + c) * 2 + 1];
+  }
+  const double n = (double)P * cg;
+  const double mu = s1 / n;
+  double var = s2 / n - mu * mu;
+  if (var < 0) var = 0;
+  mean[i] = (float)mu;
+  rstd[i] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// bwd stage 2: parameter grads and per-(b,g) correction terms
+__global__ void gn_bwd_finalize(GnArgs a, float* dgamma, float* dbeta, float* dss) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < a.C) {
+    float dg = 0.f, db = 0.f;
+    for (int b = 0; b < a.nb; ++b) {
+      const float r1 = a.ws[((long long)b * a.C + c) * 2], r2 = a.ws[((long long)b * a.C + c) * 2 + 1];
+      const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
+      dg += sc * r2;
+      db += sc * r1;
+      if (dss) {
+        dss[(long long)b * 2 * a.C + c] = a.gamma[c] * r2 + a.beta[c] * r1;  // d scale
+        dss[(long long)b * 2 * a.C + a.C + c] = r1;                          // d shift
+      }
+    }
+    if (dgamma) dgamma[c] = dg;
+    if (dbeta) dbeta[c] = db;
+  }
+  if (c < a.nb * a.G) {
+    const int b = c / a.G, g = c % a.G, cg = a.C / a.G;
+    float m1 = 0.f, m2 = 0.f;
+    for (int cc = g * cg; cc < (g + 1) * cg; ++cc) {
+      const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + cc] : 1.f;
+      const float k = a.gamma[cc] * sc;
+      m1 += k * a.ws[((long long)b * a.C + cc) * 2];
+      m2 += k * a.ws[((long long)b * a.C + cc) * 2 + 1];
+    }
+    const float n = (float)((double)a.P * cg);
+    a.ws2[c * 2] = m1 / n;
+    a.ws2[c * 2 + 1] = m2 / n;
+  }
+}
+
+// MODE 0: forward apply  out = act(v) (+ res)
+// MODE 1: backward apply out = dz
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int vpr = a.C / VEC;
+  const long long total = (long long)a.nb * a.P * vpr;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const long long pix = idx / vpr;
+    const int cv = (int)(idx - pix * vpr) * VEC;
+    const int b = (int)(pix / a.P);
+    float z[VEC], o[VEC];
+    ld_vec<T>((const T*)a.z + pix * a.ldz + cv, z);
+    if (MODE == 0) {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float zhat, u, v;
+        gn_point<T>(a, b, cv + e, z[e], zhat, u, v);
+        o[e] = a.act == DV_ACT_SILU ? silu_f(v) : v;
+      }
+      if (a.res) {
+        float r[VEC];
+        ld_vec<T>((const T*)a.res + pix * a.ldres + cv, r);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) o[e] += r[e];
+      }
+    } else {
+      float dy[VEC];
+      ld_vec<T>((const T*)a.dy + pix * a.lddy + cv, dy);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const int c = cv + e, g = c / (a.C / a.G);
+        float zhat, u, v;
+        gn_point<T>(a, b, c, z[e], zhat, u, v);
+        float dv = dy[e];
+        if (a.act == DV_ACT_SILU) {
+          const float sg = sigmoid_f(v);
+          dv *= sg * (1.f + v * (1.f - sg));
+        }
+        const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
+        const float dzhat = dv * sc * a.gamma[c];
+        const float m1 = a.ws2[(b * a.G + g) * 2], m2 = a.ws2[(b * a.G + g) * 2 + 1];
+        o[e] = a.rstd[b * a.G + g] * (dzhat - m1 - zhat * m2);
+      }
+    }
+    st_vec<T>((T*)a.out + pix * a.ldo + cv, o);
+  }
+}
+
+int grid_for(long long work, int per_block = 256) {
+  long long b = (work + per_block - 1) / per_block;
+  if (b > 16384) b = 16384;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+template <typename T>
+int gn_fwd_t(GnArgs a, float eps, hipStream_t st) {
+  const int VEC = 16 / sizeof(T);
+  a.rows_per_block = 1024;
+  dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
+  (void)hipMemsetAsync(a.ws, 0, sizeof(float) * a.nb * a.C * 2, st);
+  gn_reduce_kernel<T, 0><<<g1, 256, 0, st>>>(a);
+  gn_stats_finalize<<<(a.nb * a.G + 63) / 64, 64, 0, st>>>(a.ws, (float*)a.mean, (float*)a.rstd,
+                                                          a.nb, a.P, a.C, a.G, eps);
+  gn_apply_kernel<T, 0><<<grid_for((long long)a.nb * a.P * (a.C / VEC)), 256, 0, st>>>(a);
+  return check_launch("gn_fwd");
+}
+
+template <typename T>
+int gn_bwd_t(GnArgs a, float* dgamma, float* dbeta, float* dss, hipStream_t st) {
+  const int VEC = 16 / sizeof(T);
+  a.rows_per_block = 1024;
+  dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
+  (void)hipMemsetAsync(a.ws, 0, sizeof(float) * a.nb * a.C * 2, st);
+  gn_reduce_kernel<T, 1><<<g1, 256, 0, st>>>(a);
+  int n2 = a.C > a.nb * a.G ? a.C : a.nb * a.G;
+  gn_bwd_finalize<<<(n2 + 63) / 64, 64, 0, st>>>(a, dgamma, dbeta, dss);
+  gn_apply_kernel<T, 1><<<grid_for((long long)a.nb * a.P * (a.C / VEC)), 256, 0, st>>>(a);
+  return check_launch("gn_bwd");
+}
+
+// --------------------------------------------------------------------------
+// row LayerNorm: y = (x - mean) * rstd * g (+ b) (+ res); one wave per row
+// --------------------------------------------------------------------------
+template <typename T, int MODE>  // MODE 0 fwd, 1 bwd
+__global__ __launch_bounds__(256) void ln_kernel(const T* x, int ldx, const T* dy, int lddy, T* out,
+                                                 int ldo, const T* res, int ldres, long long rows,
+                                                 int C, const float* g, const float* bias,
+                                                 float eps, float* mean, float* rstd, float* dg,
+                                                 float* db) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int MAXV = 4;  // C <= 64 * VEC * MAXV, C % VEC == 0
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float pg[MAXV][VEC], pb[MAXV][VEC];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) pg[k][e] = pb[k][e] = 0.f;
+  for (long long row = (long long)blockIdx.x * 4 + wave; row < rows; row += (long long)gridDim.x * 4) {
+    float xv[MAXV][VEC];
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int c0 = (k * 64 + lane) * VEC;
+      if (c0 < C) ld_vec<T>(x + row * ldx + c0, xv[k]);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        if (c0 >= C) xv[k][e] = 0.f;
+        s += xv[k][e];
+      }
+    }
+    const float mu = wave_sum(s) / C;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float d = (k * 64 + lane) * VEC < C ? xv[k][e] - mu : 0.f;
+        q += d * d;
+      }
+    const float rs = rsqrtf(wave_sum(q) / C + eps);
+    if (MODE == 0) {
+      if (lane == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) {
+        const int c0 = (k * 64 + lane) * VEC;
+        if (c0 >= C) continue;
+        float o[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) o[e] = (xv[k][e] - mu) * rs * g[c0 + e] + (bias ? bias[c0 + e] : 0.f);
+        if (res) {
+          float r[VEC];
+          ld_vec<T>(res + row * ldres + c0, r);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) o[e] += r[e];
+        }
+        st_vec<T>(out + row * ldo + c0, o);
+      }
+    } else {
+      // dxhat = dy*g; dx = rs*(dxhat - mean(dxhat) - xhat*mean(dxhat*xhat))
+      float dyv[MAXV][VEC];
+      float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) {
+        const int c0 = (k * 64 + lane) * VEC;
+        if (c0 >= C) continue;
+        ld_vec<T>(dy + row * lddy + c0, dyv[k]);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float xh = (xv[k][e] - mu) * rs;
+          const float dxh = dyv[k][e] * g[c0 + e];
+          m1 += dxh;
+          m2 += dxh * xh;
+          pg[k][e] += dyv[k][e] * xh;
+          pb[k][e] += dyv[k][e];
+        }
+      }
+      m1 = wave_sum(m1) / C;
+      m2 = wave_sum(m2) / C;
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) {
+        const int c0 = (k * 64 + lane) * VEC;
+        if (c0 >= C) continue;
+        float o[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float xh = (xv[k][e] - mu) * rs;
+          o[e] = rs * (dyv[k][e] * g[c0 + e] - m1 - xh * m2);
+        }
+        st_vec<T>(out + row * ldo + c0, o);
+      }
+    }
+  }
+  if (MODE == 1) {
+    __shared__ float red[2][4][64 * VEC * MAXV];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        red[0][wave][(k * 64 + lane) * VEC + e] = pg[k][e];
+        red[1][wave][(k * 64 + lane) * VEC + e] = pb[k][e];
+      }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const float tg = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+      const float tb = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+      if (dg) atomicAdd(dg + c, tg);
+      if (db) atomicAdd(db + c, tb);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* res,
+                         int ldres, int nb, long long P, int C, int G, float eps,
+                         const float* gamma, const float* beta, const float* ss, int act,
+                         float* mean, float* rstd, float* ws, void* stream) {
+  DV_REQUIRE(z && y && gamma && beta && mean && rstd && ws, "null pointer");
+  DV_REQUIRE(C % G == 0, "C % G != 0");
+  const int VEC = dtype == DV_BF16 ? 8 : 4;
+  DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && ldy % VEC == 0 && (!res || ldres % VEC == 0),
+             "channel counts / strides must be multiples of 16 bytes");
+  DV_REQUIRE(C / VEC <= 256, "C too large");
+  GnArgs a{};
+  a.z = z; a.ldz = ldz; a.out = y; a.ldo = ldy; a.res = res; a.ldres = ldres; a.nb = nb;
+  a.P = P; a.C = C; a.G = G; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta;
+  a.ss = ss; a.act = act; a.ws = ws;
+  if (nb == 0 || P == 0) return DV_OK;
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DV_BF16 ? gn_fwd_t<bf16>(a, eps, st) : gn_fwd_t<float>(a, eps, st);
+}
+
+extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void* dz,
+                         int lddz, int nb, long long P, int C, int G, const float* gamma,
+                         const float* beta, const float* ss, int act, const float* mean,
+                         const float* rstd, float* dgamma, float* dbeta, float* dss, float* ws,
+                         void* stream) {
+  DV_REQUIRE(dy && z && dz && gamma && beta && mean && rstd && ws, "null pointer");
+  const int VEC = dtype == DV_BF16 ? 8 : 4;
+  DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && lddy % VEC == 0 && lddz % VEC == 0,
+             "channel counts / strides must be multiples of 16 bytes");
+  DV_REQUIRE(C / VEC <= 256 && C % G == 0, "bad C");
+  GnArgs a{};
+  a.z = z; a.ldz = ldz; a.dy = dy; a.lddy = lddy; a.out = dz; a.ldo = lddz; a.nb = nb; a.P = P;
+  a.C = C; a.G = G; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.ss = ss;
+  a.act = act; a.ws = ws; a.ws2 = ws + (long long)nb * C * 2;
+  if (nb == 0 || P == 0) return DV_OK;
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DV_BF16 ? gn_bwd_t<bf16>(a, dgamma, dbeta, dss, st)
+                          : gn_bwd_t<float>(a, dgamma, dbeta, dss, st);
+}
+
+extern "C" int dv_ln_fwd(int dtype, const void* x, int ldx, void* y, int ldy, const void* res,
+                         int ldres, long long rows, int C, const float* g, const float* b,
+                         float eps, float* mean, float* rstd, void* stream) {
+  DV_REQUIRE(x && y && g, "null pointer");
+  const int VEC = dtype == DV_BF16 ? 8 : 4;
+  DV_REQUIRE(C <= 64 * VEC * 4 && C % VEC == 0, "C must be a multiple of 16 bytes, <= 256 vectors");
+  DV_REQUIRE(ldx % VEC == 0 && ldy % VEC == 0 && (!res || ldres % VEC == 0),
+             "strides must be multiples of 16 bytes");
+  if (rows == 0) return DV_OK;
+  const int blocks = grid_for(rows, 4);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DV_BF16)
+    ln_kernel<bf16, 0><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, nullptr, 0, (bf16*)y, ldy,
+                                               (const bf16*)res, ldres, rows, C, g, b, eps, mean,
+                                               rstd, nullptr, nullptr);
+  else
+    ln_kernel<float, 0><<<blocks, 256, 0, st>>>((const float*)x, ldx, nullptr, 0, (float*)y, ldy,
+                                                (const float*)res, ldres, rows, C, g, b, eps, mean,
+                                                rstd, nullptr, nullptr);
+  return check_launch("ln_fwd");
+}
+
+extern "C" int dv_ln_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, void* dx,
+                         int lddx, long long rows, int C, const float* g, float eps, float* dg,
+                         float* db, void* stream) {
+  DV_REQUIRE(dy && x && dx && g, "null pointer");
+  const int VEC = dtype == DV_BF16 ? 8 : 4;
+  DV_REQUIRE(C <= 64 * VEC * 4 && C % VEC == 0, "C must be a multiple of 16 bytes, <= 256 vectors");
+  DV_REQUIRE(ldx % VEC == 0 && lddy % VEC == 0 && lddx % VEC == 0, "strides must be multiples of 16 bytes");
+  if (rows == 0) return DV_OK;
+  int blocks = grid_for(rows, 4);
+  if (blocks > 1024) blocks = 1024;  // bounds the dg/db atomics
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DV_BF16)
+    ln_kernel<bf16, 1><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (const bf16*)dy, lddy,
+                                               (bf16*)dx, lddx, nullptr, 0, rows, C, g, nullptr,
+                                               eps, nullptr, nullptr, dg, db);
+  else
+    ln_kernel<float, 1><<<blocks, 256, 0, st>>>((const float*)x, ldx, (const float*)dy, lddy,
+                                                (float*)dx, lddx, nullptr, 0, rows, C, g, nullptr,
+                                                eps, nullptr, nullptr, dg, db);
+  return check_launch("ln_bwd");
+}

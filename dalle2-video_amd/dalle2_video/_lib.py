@@ -30,6 +30,29 @@ _SIGS = {
     "dv_unpack_wgrad": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
     "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
+    "dv_gn_fwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P],
+    "dv_gn_bwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P],
+    "dv_ln_fwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _P, _F, _P, _P, _P],
+    "dv_ln_bwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _F, _P, _P, _P],
+    "dv_ncthw_to_cl": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_cl_to_ncthw": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P],
+    "dv_shuffle": [_I, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_q_sample": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dv_mse_loss": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P],
+    "dv_mse_loss_bwd": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
+    "dv_sinusoidal": [_P, _P, _P, _I, _I, _P],
+    "dv_linear_small_fwd": [_P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
+    "dv_linear_small_bwd": [_P, _I, _P, _I, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_adamw": [_P, _P, _P, _P, _L, _L, _F, _F, _F, _F, _F, _F, _F, _P, _P],
+    "dv_grad_clip_coef": [_P, _L, _F, _P, _P],
+    "dv_p_sample": [_I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_xattn_fold": [_P, _P, _P, _P, _P, _P, _I, _I, _F, _P],
+    "dv_xattn_fwd": [_I, _P, _I, _P, _I, _L, _L, _I, _P, _P, _P, _P, _F, _P, _P, _P],
+    "dv_xattn_bwd_tokens": [_I, _P, _I, _P, _I, _P, _I, _L, _L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "dv_xattn_fold_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P],
+    "dv_mqa_prep": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _P],
+    "dv_mqa_fwd": [_I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _F, _P],
+    "dv_mqa_bwd": [_I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _F, _P],
 }
 
 

@@ -111,3 +111,460 @@ def conv(x0, weight, bias=None, x1=None, res=None):
     Conv3d layout (cout, cin, 1, k, k) or Linear layout (cout, cin))."""
     k = weight.shape[-1] if weight.dim() == 5 else 1
     return ConvFn.apply(x0, x1, weight, bias, res, k)
+
+
+# ---------------------------------------------------------------------------
+# GroupNorm (+ per-sample scale/shift) + SiLU (+ residual)  — Block3D
+# ---------------------------------------------------------------------------
+class GroupNormActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, gamma, beta, ss, res, nb, groups, eps, act):
+        require_gpu(z, gamma, beta, ss, res)
+        nf, h, w, c = z.shape
+        P = (nf // nb) * h * w
+        dev = z.device
+        y = torch.empty(nf, h, w, c, dtype=z.dtype, device=dev)
+        mean = torch.empty(nb * groups, dtype=torch.float32, device=dev)
+        rstd = torch.empty_like(mean)
+        ws = torch.empty(nb * c * 2, dtype=torch.float32, device=dev)
+        g, b = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
+        s = None if ss is None else ss.detach().float().contiguous()
+        call("dv_gn_fwd", dt(z), ptr(z), cl_ld(z), ptr(y), c, ptr(res), cl_ld(res) if res is not None else 0,
+             nb, P, c, groups, ctypes_float(eps), ptr(g), ptr(b), ptr(s), act, ptr(mean), ptr(rstd),
+             ptr(ws), stream())
+        ctx.save_for_backward(z, g, b, s, mean, rstd)
+        ctx.meta = (nb, groups, act, ss is not None, res is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        z, g, b, s, mean, rstd = ctx.saved_tensors
+        nb, groups, act, has_ss, has_res = ctx.meta
+        nf, h, w, c = z.shape
+        P = (nf // nb) * h * w
+        dev = z.device
+        dy = dy.contiguous()
+        dz = torch.empty(nf, h, w, c, dtype=z.dtype, device=dev)
+        dg = torch.empty(c, dtype=torch.float32, device=dev)
+        db = torch.empty(c, dtype=torch.float32, device=dev)
+        dss = torch.empty(nb, 2 * c, dtype=torch.float32, device=dev) if has_ss else None
+        ws = torch.empty(nb * c * 2 + nb * groups * 2, dtype=torch.float32, device=dev)
+        call("dv_gn_bwd", dt(z), ptr(dy), c, ptr(z), cl_ld(z), ptr(dz), c, nb, P, c, groups, ptr(g),
+             ptr(b), ptr(s), act, ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(ws), stream())
+        return dz, dg, db, dss, (dy if has_res else None), None, None, None, None
+
+
+def ctypes_float(v):
+    import ctypes
+    return ctypes.c_float(float(v))
+
+
+def group_norm_act(z, gamma, beta, nb, groups=8, eps=1e-5, scale_shift=None, res=None,
+                   act=_lib.ACT_SILU):
+    return GroupNormActFn.apply(z, gamma, beta, scale_shift, res, nb, groups, eps, act)
+
+
+# ---------------------------------------------------------------------------
+# row LayerNorm (dalle2 gain-only LayerNorm, nn.LayerNorm) (+ residual)
+# ---------------------------------------------------------------------------
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, res, eps):
+        require_gpu(x, g, b, res)
+        c = x.shape[-1]
+        xc = x.contiguous()
+        rows = xc.numel() // c
+        y = torch.empty_like(xc)
+        rc = res.contiguous() if res is not None else None
+        gf = g.detach().float().contiguous()
+        bf = None if b is None else b.detach().float().contiguous()
+        call("dv_ln_fwd", dt(xc), ptr(xc), c, ptr(y), c, ptr(rc), c, rows, c, ptr(gf), ptr(bf),
+             ctypes_float(eps), None, None, stream())
+        ctx.save_for_backward(xc, gf)
+        ctx.meta = (eps, b is not None, res is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, gf = ctx.saved_tensors
+        eps, has_b, has_res = ctx.meta
+        c = xc.shape[-1]
+        rows = xc.numel() // c
+        dy = dy.contiguous()
+        dx = torch.empty_like(xc)
+        dg = torch.zeros(c, dtype=torch.float32, device=xc.device)
+        db = torch.zeros(c, dtype=torch.float32, device=xc.device) if has_b else None
+        call("dv_ln_bwd", dt(xc), ptr(dy), c, ptr(xc), c, ptr(dx), c, rows, c, ptr(gf),
+             ctypes_float(eps), ptr(dg), ptr(db), stream())
+        return dx, dg, db, (dy if has_res else None), None
+
+
+def layer_norm(x, g, b=None, res=None, eps=1e-5):
+    return LayerNormFn.apply(x, g, b, res, eps)
+
+
+# ---------------------------------------------------------------------------
+# small dense linears over (B, K) f32 rows (time MLPs, to_kv of the context)
+# ---------------------------------------------------------------------------
+ACT_OUT_GELU = 2
+
+
+class LinearSmallFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act_in, act_out):
+        require_gpu(x, w, b)
+        xc = x.detach().float().contiguous()
+        B, K = xc.shape
+        N = w.shape[0]
+        wc = w.detach().float().contiguous()
+        bc = None if b is None else b.detach().float().contiguous()
+        y = torch.empty(B, N, dtype=torch.float32, device=x.device)
+        z = torch.empty(B, N, dtype=torch.float32, device=x.device) if act_out == ACT_OUT_GELU else None
+        call("dv_linear_small_fwd", ptr(xc), K, ptr(wc), ptr(bc), ptr(y), N, ptr(z), B, K, N,
+             act_in, act_out, stream())
+        ctx.save_for_backward(xc, wc, z)
+        ctx.meta = (act_in, act_out, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc, z = ctx.saved_tensors
+        act_in, act_out, has_b = ctx.meta
+        B, K = xc.shape
+        N = wc.shape[0]
+        dy = dy.float().contiguous()
+        dx = torch.empty(B, K, dtype=torch.float32, device=dy.device) if ctx.needs_input_grad[0] else None
+        dw = torch.empty(N, K, dtype=torch.float32, device=dy.device) if ctx.needs_input_grad[1] else None
+        db = torch.empty(N, dtype=torch.float32, device=dy.device) if has_b and ctx.needs_input_grad[2] else None
+        if dw is None and db is not None:
+            dw_tmp = torch.empty(N, K, dtype=torch.float32, device=dy.device)
+        else:
+            dw_tmp = dw
+        call("dv_linear_small_bwd", ptr(dy), N, ptr(xc), K, ptr(wc), ptr(z), ptr(dx), K,
+             ptr(dw_tmp), ptr(db), B, K, N, act_in, act_out, 0, stream())
+        return dx, dw, db, None, None
+
+
+def linear_small(x, w, b=None, act_in=0, act_out=0):
+    return LinearSmallFn.apply(x, w, b, act_in, act_out)
+
+
+_FREQS = {}
+
+
+def sinusoid_freqs(dim: int, device) -> torch.Tensor:
+    """Constant frequency table of SinusoidalPosEmb, built once exactly as the
+    reference builds it (f32 arange times -ln(1e4)/(half-1), exp)."""
+    key = (dim, str(device))
+    if key not in _FREQS:
+        import math
+        half = dim // 2
+        f = torch.exp(torch.arange(half, dtype=torch.float32) * -(math.log(10000) / (half - 1)))
+        _FREQS[key] = f.to(device)
+    return _FREQS[key]
+
+
+def sinusoidal(times: torch.Tensor, dim: int) -> torch.Tensor:
+    require_gpu(times)
+    t = times.to(torch.int64).contiguous()
+    out = torch.empty(t.shape[0], dim, dtype=torch.float32, device=t.device)
+    call("dv_sinusoidal", ptr(t), ptr(sinusoid_freqs(dim, t.device)), ptr(out), t.shape[0], dim,
+         stream())
+    return out
+
+
+# ---------------------------------------------------------------------------
+# cross attention (folded), ResnetBlock3D.cross_attn
+# ---------------------------------------------------------------------------
+XA_HEADS, XA_DH = 8, 64
+
+
+class CrossAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps):
+        require_gpu(x, context)
+        nf, h, w, C = x.shape
+        ntok = nf * h * w
+        P = ntok // nb
+        dev = x.device
+        ctxf = context.detach().float().contiguous().reshape(-1, context.shape[-1])
+        kv = torch.empty(ctxf.shape[0], 2 * XA_HEADS * XA_DH, dtype=torch.float32, device=dev)
+        wkvf = wkv.detach().float().contiguous()
+        call("dv_linear_small_fwd", ptr(ctxf), ctxf.shape[1], ptr(wkvf), None, ptr(kv), kv.shape[1],
+             None, ctxf.shape[0], ctxf.shape[1], kv.shape[1], 0, 0, stream())
+        wqf, wof = wq.detach().float().contiguous(), wo.detach().float().contiguous()
+        nkv = null_kv.detach().float().contiguous()
+        at = torch.empty(nb, C, 24, dtype=torch.float32, device=dev)
+        vt = torch.empty_like(at)
+        scale = XA_DH ** -0.5
+        call("dv_xattn_fold", ptr(wqf), ptr(wof), ptr(kv), ptr(nkv), ptr(at), ptr(vt), nb, C,
+             ctypes_float(scale), stream())
+        out = torch.empty(nf, h, w, C, dtype=x.dtype, device=dev)
+        stats = torch.empty(ntok, 4, dtype=torch.float32, device=dev)
+        pbuf = torch.empty(ntok, 32, dtype=x.dtype, device=dev)
+        g1f, g2f = g1.detach().float().contiguous(), g2.detach().float().contiguous()
+        call("dv_xattn_fwd", dt(x), ptr(x), cl_ld(x), ptr(out), C, ntok, P, C, ptr(g1f), ptr(g2f),
+             ptr(at), ptr(vt), ctypes_float(eps), ptr(stats), ptr(pbuf), stream())
+        ctx.save_for_backward(x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, stats, pbuf)
+        ctx.meta = (nb, eps, context.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, stats, pbuf = ctx.saved_tensors
+        nb, eps, cshape = ctx.meta
+        nf, h, w, C = x.shape
+        ntok = nf * h * w
+        P = ntok // nb
+        dev = x.device
+        dy = dy.contiguous()
+        dx = torch.empty(nf, h, w, C, dtype=x.dtype, device=dev)
+        dobuf = torch.empty(ntok, C, dtype=x.dtype, device=dev)
+        dsbuf = torch.empty(ntok, 32, dtype=x.dtype, device=dev)
+        dg1 = torch.zeros(C, dtype=torch.float32, device=dev)
+        dg2 = torch.zeros(C, dtype=torch.float32, device=dev)
+        mcorr = torch.zeros(nb, 24, dtype=torch.float32, device=dev)
+        ldx = cl_ld(x)
+        call("dv_xattn_bwd_tokens", dt(x), ptr(dy), C, ptr(x), ldx, ptr(dx), C, ntok, P, C,
+             ptr(g1f), ptr(g2f), ptr(at), ptr(vt), ptr(stats), ptr(pbuf), ptr(dobuf), ptr(dsbuf),
+             ptr(dg1), ptr(dg2), ptr(mcorr), stream())
+        # per-batch token reductions on the MFMA wgrad GEMM
+        ws_a = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
+        ws_v = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
+        esz = x.element_size()
+        for bi in range(nb):
+            xb = x.data_ptr() + bi * P * ldx * esz
+            call("dv_conv_wgrad", dt(x), ctypes_vp(dsbuf.data_ptr() + bi * P * 32 * esz), 32,
+                 ctypes_vp(xb), ldx, C, None, 0, ctypes_vp(ws_a.data_ptr() + bi * 32 * C * 4),
+                 1, 1, P, C, 32, 1, stream())
+            call("dv_conv_wgrad", dt(x), ctypes_vp(pbuf.data_ptr() + bi * P * 32 * esz), 32,
+                 ctypes_vp(dobuf.data_ptr() + bi * P * C * esz), C, C, None, 0,
+                 ctypes_vp(ws_v.data_ptr() + bi * 32 * C * 4), 1, 1, P, C, 32, 1, stream())
+        dat = torch.empty(nb, C, 24, dtype=torch.float32, device=dev)
+        dvt = torch.empty_like(dat)
+        dwq = torch.empty_like(wqf)
+        dwo = torch.empty_like(wof)
+        dkv = torch.empty_like(kv)
+        dnull = torch.empty_like(nkv)
+        call("dv_xattn_fold_bwd", ptr(ws_a), ptr(ws_v), ptr(g1f), ptr(mcorr), ptr(wqf), ptr(wof),
+             ptr(kv), ptr(nkv), ptr(dat), ptr(dvt), ptr(dwq), ptr(dwo), ptr(dkv), ptr(dnull), nb, C,
+             ctypes_float(XA_DH ** -0.5), stream())
+        dctx = torch.empty_like(ctxf)
+        dwkv = torch.empty_like(wkvf)
+        call("dv_linear_small_bwd", ptr(dkv), dkv.shape[1], ptr(ctxf), ctxf.shape[1], ptr(wkvf), None,
+             ptr(dctx), ctxf.shape[1], ptr(dwkv), None, ctxf.shape[0], ctxf.shape[1], dkv.shape[1],
+             0, 0, 0, stream())
+        return dx, dctx.reshape(cshape), dg1, dnull, dwq, dwkv, dwo, dg2, None, None
+
+
+def ctypes_vp(addr):
+    import ctypes
+    return ctypes.c_void_p(addr)
+
+
+def cross_attention(x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps):
+    return CrossAttnFn.apply(x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps)
+
+
+# ---------------------------------------------------------------------------
+# multi-query flash attention core (mid_attn)
+# ---------------------------------------------------------------------------
+MQA_DH = 32
+
+
+class MQAFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, kv, null_kv, B, N, H, scale):
+        require_gpu(q, kv, null_kv)
+        dev = q.device
+        qc, kvc = q.contiguous(), kv.contiguous()
+        NKP = (N + 1 + 31) // 32 * 32
+        kp = torch.empty(B, NKP, MQA_DH, dtype=q.dtype, device=dev)
+        vp = torch.empty_like(kp)
+        nkv = null_kv.detach().float().contiguous()
+        call("dv_mqa_prep", dt(q), ptr(kvc), kvc.shape[-1], ptr(nkv), ptr(kp), ptr(vp), B, N, NKP, stream())
+        o = torch.empty(B * N, H * MQA_DH, dtype=q.dtype, device=dev)
+        lse = torch.empty(B, H, N, dtype=torch.float32, device=dev)
+        call("dv_mqa_fwd", dt(q), ptr(qc), qc.shape[-1], ptr(kp), ptr(vp), ptr(o), o.shape[-1], ptr(lse),
+             B, N, NKP, H, ctypes_float(scale), stream())
+        ctx.save_for_backward(qc, kp, vp, o, lse)
+        ctx.meta = (B, N, H, NKP, scale, kvc.shape[-1])
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qc, kp, vp, o, lse = ctx.saved_tensors
+        B, N, H, NKP, scale, ldkv = ctx.meta
+        dev = qc.device
+        do = do.contiguous()
+        dq = torch.empty_like(qc)
+        D = torch.empty(B, H, N, dtype=torch.float32, device=dev)
+        dkp = torch.empty(B, NKP, MQA_DH, dtype=torch.float32, device=dev)
+        dvp = torch.empty_like(dkp)
+        dkv = torch.empty(B * N, 2 * MQA_DH, dtype=qc.dtype, device=dev)
+        dnull = torch.empty(2, MQA_DH, dtype=torch.float32, device=dev)
+        call("dv_mqa_bwd", dt(qc), ptr(qc), qc.shape[-1], ptr(o), o.shape[-1], ptr(do), do.shape[-1],
+             ptr(lse), ptr(kp), ptr(vp), ptr(dq), dq.shape[-1], ptr(D), ptr(dkp), ptr(dvp), ptr(dkv),
+             dkv.shape[-1], ptr(dnull), B, N, NKP, H, ctypes_float(scale), stream())
+        return dq, dkv, dnull, None, None, None, None
+
+
+def mqa(q, kv, null_kv, B, N, H, scale):
+    return MQAFn.apply(q, kv, null_kv, B, N, H, scale)
+
+
+# ---------------------------------------------------------------------------
+# space-to-depth (Downsample3D) and SiLU+PixelShuffle (PixelShuffleUpsample3D)
+# ---------------------------------------------------------------------------
+class SpaceToDepthFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        require_gpu(x)
+        nf, H2, W2, C = x.shape
+        H, W = H2 // 2, W2 // 2
+        y = torch.empty(nf, H, W, 4 * C, dtype=x.dtype, device=x.device)
+        call("dv_shuffle", dt(x), 0, ptr(x), cl_ld(x), ptr(y), 4 * C, None, 0, nf, H, W, C, 0, stream())
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        nf, H, W, C4 = dy.shape
+        C = C4 // 4
+        dx = torch.empty(nf, 2 * H, 2 * W, C, dtype=dy.dtype, device=dy.device)
+        call("dv_shuffle", dt(dy), 1, ptr(dy), C4, ptr(dx), C, None, 0, nf, H, W, C, 0, stream())
+        return dx
+
+
+class SiLUPixelShuffleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z):
+        require_gpu(z)
+        nf, H, W, C4 = z.shape
+        C = C4 // 4
+        y = torch.empty(nf, 2 * H, 2 * W, C, dtype=z.dtype, device=z.device)
+        call("dv_shuffle", dt(z), 1, ptr(z), cl_ld(z), ptr(y), C, None, 0, nf, H, W, C, _lib.ACT_SILU, stream())
+        ctx.save_for_backward(z)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (z,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        nf, H, W, C4 = z.shape
+        C = C4 // 4
+        dz = torch.empty(nf, H, W, C4, dtype=z.dtype, device=z.device)
+        call("dv_shuffle", dt(z), 0, ptr(dy), C, ptr(dz), C4, ptr(z), cl_ld(z), nf, H, W, C, 0, stream())
+        return dz
+
+
+def space_to_depth(x):
+    return SpaceToDepthFn.apply(x)
+
+
+def silu_pixel_shuffle(z):
+    return SiLUPixelShuffleFn.apply(z)
+
+
+# ---------------------------------------------------------------------------
+# NCTHW (module boundary) <-> channels-last frames
+# ---------------------------------------------------------------------------
+def _pad8(c):
+    return (c + 7) // 8 * 8
+
+
+class ToCLFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dtype):
+        require_gpu(x)
+        xf = x.detach().float().contiguous()
+        B, C, T, H, W = xf.shape
+        cp = _pad8(C)
+        y = torch.empty(B * T, H, W, cp, dtype=dtype, device=x.device)
+        call("dv_ncthw_to_cl", _lib.DV_BF16 if dtype == torch.bfloat16 else _lib.DV_F32, ptr(xf), ptr(y),
+             B, C, T, H, W, cp, stream())
+        ctx.meta = (B, C, T, H, W, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, C, T, H, W, xdt = ctx.meta
+        dy = dy.contiguous()
+        dx = torch.empty(B, C, T, H, W, dtype=torch.float32, device=dy.device)
+        call("dv_cl_to_ncthw", dt(dy), ptr(dy), dy.shape[-1], ptr(dx), B, C, T, H, W, stream())
+        return dx.to(xdt), None
+
+
+class FromCLFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, B, C, T):
+        require_gpu(y)
+        nf, H, W, _ = y.shape
+        x = torch.empty(B, C, T, H, W, dtype=torch.float32, device=y.device)
+        call("dv_cl_to_ncthw", dt(y), ptr(y), cl_ld(y), ptr(x), B, C, T, H, W, stream())
+        ctx.meta = (B, C, T, H, W, y.dtype, y.shape[-1])
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        B, C, T, H, W, ydt, cy = ctx.meta
+        dxf = dx.float().contiguous()
+        dy = torch.zeros(B * T, H, W, cy, dtype=ydt, device=dx.device) if cy != _pad8(C) else None
+        if dy is None:
+            dy = torch.empty(B * T, H, W, cy, dtype=ydt, device=dx.device)
+        call("dv_ncthw_to_cl", dt(dy), ptr(dxf), ptr(dy), B, C, T, H, W, cy, stream())
+        return dy, None, None, None
+
+
+def to_cl(x, dtype):
+    return ToCLFn.apply(x, dtype)
+
+
+def from_cl(y, B, C, T):
+    return FromCLFn.apply(y, B, C, T)
+
+
+# ---------------------------------------------------------------------------
+# diffusion arithmetic (q_sample, l2 loss, posterior step)
+# ---------------------------------------------------------------------------
+def q_sample_cl(x_start, noise, times, sqrt_ac, sqrt_1m_ac, dtype, normalize=True):
+    require_gpu(x_start, noise, times)
+    x0 = x_start.float().contiguous()
+    nz = noise.float().contiguous()
+    t = times.to(torch.int64).contiguous()
+    B, C, T, H, W = x0.shape
+    cp = _pad8(C)
+    y = torch.empty(B * T, H, W, cp, dtype=dtype, device=x0.device)
+    call("dv_q_sample", _lib.DV_BF16 if dtype == torch.bfloat16 else _lib.DV_F32, ptr(x0), ptr(nz), ptr(t),
+         ptr(sqrt_ac), ptr(sqrt_1m_ac), ptr(y), B, C, T, H, W, cp, int(normalize), stream())
+    return y
+
+
+class MSELossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred_cl, target, sample_w):
+        require_gpu(pred_cl, target)
+        tgt = target.float().contiguous()
+        B, C, T, H, W = tgt.shape
+        loss = torch.empty((), dtype=torch.float32, device=tgt.device)
+        sw = None if sample_w is None else sample_w.float().contiguous()
+        call("dv_mse_loss", dt(pred_cl), ptr(pred_cl), cl_ld(pred_cl), ptr(tgt), B, C, T, H, W, ptr(sw),
+             ptr(loss), stream())
+        ctx.save_for_backward(pred_cl, tgt, sw)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dl):
+        pred_cl, tgt, sw = ctx.saved_tensors
+        B, C, T, H, W = tgt.shape
+        dlc = dl.float().contiguous().reshape(1)
+        cp = pred_cl.shape[-1]
+        alloc = torch.zeros if cp != C else torch.empty
+        dp = alloc(pred_cl.shape, dtype=pred_cl.dtype, device=pred_cl.device)
+        call("dv_mse_loss_bwd", dt(pred_cl), ptr(pred_cl), cl_ld(pred_cl), ptr(tgt), B, C, T, H, W, ptr(sw),
+             ptr(dlc), ptr(dp), cp, stream())
+        return dp, None, None
+
+
+def mse_loss_cl(pred_cl, target, sample_w=None):
+    return MSELossFn.apply(pred_cl, target, sample_w)

@@ -1,0 +1,263 @@
+"""HIP ops (GN, LN, cross-attention, MQA, shuffles, layout, loss, small
+linears) vs plain-PyTorch fp32 CPU references of the same op (forward + grads).
+fp32 mode: rel-err <= 2e-5; bf16 mode: <= 2e-2."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DTYPES = [(torch.float32, 2e-5), (torch.bfloat16, 2.5e-2)]
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def grads_match(outs_gpu, outs_ref, tol):
+    for i, (a, b) in enumerate(zip(outs_gpu, outs_ref)):
+        if b is None:
+            continue
+        e = rel(a, b)
+        assert e < tol, f"grad {i}: rel-err {e:.3e} >= {tol}"
+
+
+def _leaf(t, dev=None, dtype=None):
+    t = t.detach()
+    if dev is not None:
+        t = t.to(dev)
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.clone().requires_grad_()
+
+
+@pytest.mark.parametrize("dtype,tol", DTYPES)
+@pytest.mark.parametrize("with_ss,with_res", [(True, False), (False, True)])
+def test_group_norm_act(dtype, tol, with_ss, with_res):
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(3)
+    nb, T, H, W, C, G = 2, 3, 8, 8, 64, 8
+    z = torch.randn(nb * T, H, W, C, generator=g) * 2 + 0.5
+    gamma = 1 + 0.1 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    ss = 0.3 * torch.randn(nb, 2 * C, generator=g) if with_ss else None
+    res = torch.randn(nb * T, H, W, C, generator=g) if with_res else None
+    gy = torch.randn(nb * T, H, W, C, generator=g)
+    # reference: torch GroupNorm on (b, c, t, h, w)
+    zr = _leaf(z.to(dtype).float())
+    gr, br = _leaf(gamma), _leaf(beta)
+    ssr = _leaf(ss) if with_ss else None
+    x5 = zr.reshape(nb, T, H, W, C).permute(0, 4, 1, 2, 3)
+    y5 = F.group_norm(x5, G, gr, br, eps=1e-5)
+    if with_ss:
+        y5 = y5 * (ssr[:, :C, None, None, None] + 1) + ssr[:, C:, None, None, None]
+    y5 = F.silu(y5)
+    yr = y5.permute(0, 2, 3, 4, 1).reshape(nb * T, H, W, C)
+    if with_res:
+        yr = yr + res.to(dtype).float()
+    (yr * gy).sum().backward()
+    zd = _leaf(z, "cuda", dtype)
+    gd, bd = _leaf(gamma, "cuda"), _leaf(beta, "cuda")
+    ssd = _leaf(ss, "cuda") if with_ss else None
+    resd = res.to("cuda", dtype) if with_res else None
+    y = ops.group_norm_act(zd, gd, bd, nb, G, 1e-5, scale_shift=ssd, res=resd)
+    assert rel(y.float(), yr) < tol
+    (y.float() * gy.cuda()).sum().backward()
+    grads_match([zd.grad.float(), gd.grad, bd.grad] + ([ssd.grad] if with_ss else []),
+                [zr.grad, gr.grad, br.grad] + ([ssr.grad] if with_ss else []), tol * 2)
+
+
+@pytest.mark.parametrize("dtype,tol", DTYPES)
+@pytest.mark.parametrize("C,bias,res", [(512, False, True), (64, True, False)])
+def test_layer_norm(dtype, tol, C, bias, res):
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(5)
+    rows = 300
+    x = torch.randn(rows, C, generator=g) * 3 + 1
+    w = 1 + 0.1 * torch.randn(C, generator=g)
+    b = 0.1 * torch.randn(C, generator=g) if bias else None
+    r = torch.randn(rows, C, generator=g) if res else None
+    gy = torch.randn(rows, C, generator=g)
+    xr, wr = _leaf(x.to(dtype).float()), _leaf(w)
+    br = _leaf(b) if bias else None
+    yr = F.layer_norm(xr, (C,), wr, br, eps=1e-5)
+    if res:
+        yr = yr + r.to(dtype).float()
+    (yr * gy).sum().backward()
+    xd, wd = _leaf(x, "cuda", dtype), _leaf(w, "cuda")
+    bd = _leaf(b, "cuda") if bias else None
+    y = ops.layer_norm(xd, wd, bd, r.to("cuda", dtype) if res else None, eps=1e-5)
+    assert rel(y.float(), yr) < tol
+    (y.float() * gy.cuda()).sum().backward()
+    grads_match([xd.grad.float(), wd.grad] + ([bd.grad] if bias else []),
+                [xr.grad, wr.grad] + ([br.grad] if bias else []), tol * 2)
+
+
+def _ref_cross_attention(x_tok, ctx, g1, null_kv, wq, wkv, wo, g2, eps):
+    # dalle2-pytorch CrossAttention + residual (see oracle/dv_ref.py)
+    b = x_tok.shape[0]
+    ln = lambda t, g: (t - t.mean(-1, keepdim=True)) * (t.var(-1, unbiased=False, keepdim=True) + eps).rsqrt() * g
+    xn = ln(x_tok, g1)
+    q = xn @ wq.t()
+    kv = ctx @ wkv.t()
+    k, v = kv.chunk(2, dim=-1)
+    sp = lambda t: t.reshape(t.shape[0], t.shape[1], 8, 64).transpose(1, 2)
+    q, k, v = sp(q), sp(k), sp(v)
+    nk = null_kv[0].expand(b, 8, 1, 64)
+    nv = null_kv[1].expand(b, 8, 1, 64)
+    k, v = torch.cat((nk, k), dim=2), torch.cat((nv, v), dim=2)
+    s = (q * 64 ** -0.25) @ (k * 64 ** -0.25).transpose(-1, -2)
+    a = s.softmax(-1)
+    o = (a @ v).transpose(1, 2).reshape(b, -1, 512)
+    return ln(o @ wo.t(), g2) + x_tok
+
+
+@pytest.mark.parametrize("dtype,tol", DTYPES)
+@pytest.mark.parametrize("C", [64, 256])
+def test_cross_attention(dtype, tol, C):
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(7)
+    nb, T, H, W = 2, 2, 8, 8
+    x = torch.randn(nb * T, H, W, C, generator=g)
+    ctx = torch.randn(nb, 2, 64, generator=g)
+    g1 = 1 + 0.1 * torch.randn(C, generator=g)
+    g2 = 1 + 0.1 * torch.randn(C, generator=g)
+    null_kv = torch.randn(2, 64, generator=g)
+    wq = torch.randn(512, C, generator=g) / C ** 0.5
+    wkv = torch.randn(1024, 64, generator=g) / 8
+    wo = torch.randn(C, 512, generator=g) / 512 ** 0.5
+    gy = torch.randn(nb * T, H, W, C, generator=g)
+    ref_in = [_leaf(x.to(dtype).float()), _leaf(ctx), _leaf(g1), _leaf(null_kv), _leaf(wq),
+              _leaf(wkv), _leaf(wo), _leaf(g2)]
+    xt = ref_in[0].reshape(nb, -1, C)
+    yr = _ref_cross_attention(xt, ref_in[1], ref_in[2], ref_in[3], ref_in[4], ref_in[5], ref_in[6],
+                              ref_in[7], 1e-5).reshape(nb * T, H, W, C)
+    (yr * gy).sum().backward()
+    dev_in = [_leaf(x, "cuda", dtype)] + [_leaf(t, "cuda") for t in (ctx, g1, null_kv, wq, wkv, wo, g2)]
+    eps = 1e-5
+    y = ops.cross_attention(dev_in[0], dev_in[1], dev_in[2], dev_in[3], dev_in[4], dev_in[5],
+                            dev_in[6], dev_in[7], nb, eps)
+    assert rel(y.float(), yr) < tol
+    (y.float() * gy.cuda()).sum().backward()
+    grads_match([t.grad.float() for t in dev_in], [t.grad for t in ref_in], tol * 3)
+
+
+@pytest.mark.parametrize("dtype,tol", DTYPES)
+@pytest.mark.parametrize("N", [64, 96])
+def test_mqa(dtype, tol, N):
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(11)
+    B, H, D = 2, 16, 32
+    q = torch.randn(B * N, H * D, generator=g) * 2
+    kv = torch.randn(B * N, 2 * D, generator=g) * 2
+    null_kv = torch.randn(2, D, generator=g)
+    gy = torch.randn(B * N, H * D, generator=g)
+    qr, kvr, nr = _leaf(q.to(dtype).float()), _leaf(kv.to(dtype).float()), _leaf(null_kv)
+    qh = qr.reshape(B, N, H, D).transpose(1, 2)
+    k = torch.cat((nr[0].expand(B, 1, D), kvr[:, :D].reshape(B, N, D)), dim=1)
+    v = torch.cat((nr[1].expand(B, 1, D), kvr[:, D:].reshape(B, N, D)), dim=1)
+    s = torch.einsum("bhid,bjd->bhij", qh, k) / D
+    o = torch.einsum("bhij,bjd->bhid", s.softmax(-1), v).transpose(1, 2).reshape(B * N, H * D)
+    (o * gy).sum().backward()
+    qd, kvd, nd = _leaf(q, "cuda", dtype), _leaf(kv, "cuda", dtype), _leaf(null_kv, "cuda")
+    y = ops.mqa(qd, kvd, nd, B, N, H, 1.0 / D)
+    assert rel(y.float(), o) < tol
+    (y.float() * gy.cuda()).sum().backward()
+    grads_match([qd.grad.float(), kvd.grad.float(), nd.grad], [qr.grad, kvr.grad, nr.grad], tol * 2)
+
+
+@pytest.mark.parametrize("dtype,tol", DTYPES)
+def test_shuffles(dtype, tol):
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(13)
+    nf, H, W, C = 3, 4, 6, 16
+    x = torch.randn(nf, 2 * H, 2 * W, C, generator=g)
+    xr = _leaf(x.to(dtype).float())
+    # reference: Downsample3D's rearrange 'b c t (h s1) (w s2) -> b (c s1 s2) t h w' per frame
+    yr = F.pixel_unshuffle(xr.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    gy = torch.randn(yr.shape, generator=g)
+    (yr * gy).sum().backward()
+    xd = _leaf(x, "cuda", dtype)
+    y = ops.space_to_depth(xd)
+    assert rel(y.float(), yr) < 1e-6
+    (y.float() * gy.cuda()).sum().backward()
+    assert rel(xd.grad.float(), xr.grad) < tol
+    z = torch.randn(nf, H, W, 4 * C, generator=g)
+    zr = _leaf(z.to(dtype).float())
+    ur = F.pixel_shuffle(F.silu(zr).permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    gu = torch.randn(ur.shape, generator=g)
+    (ur * gu).sum().backward()
+    zd = _leaf(z, "cuda", dtype)
+    u = ops.silu_pixel_shuffle(zd)
+    assert rel(u.float(), ur) < tol
+    (u.float() * gu.cuda()).sum().backward()
+    assert rel(zd.grad.float(), zr.grad) < tol * 2
+
+
+@pytest.mark.parametrize("dtype,tol", DTYPES)
+def test_layout_and_loss(dtype, tol):
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(17)
+    B, C, T, H, W = 2, 3, 4, 8, 8
+    x = torch.randn(B, C, T, H, W, generator=g)
+    y = ops.to_cl(x.cuda(), dtype)
+    assert y.shape == (B * T, H, W, 8)
+    assert torch.equal(y[..., 3:].float().cpu(), torch.zeros(B * T, H, W, 5))
+    back = ops.from_cl(y, B, C, T)
+    assert rel(back, x.to(dtype).float()) < 1e-7
+    # q_sample + mse loss
+    sched_a = torch.rand(1000, generator=g)
+    sched_b = torch.rand(1000, generator=g)
+    times = torch.tensor([3, 977])
+    x0 = torch.rand(B, C, T, H, W, generator=g)
+    noise = torch.randn(B, C, T, H, W, generator=g)
+    xn = ops.q_sample_cl(x0.cuda(), noise.cuda(), times.cuda(), sched_a.cuda(), sched_b.cuda(), dtype)
+    ref = sched_a[times].reshape(B, 1, 1, 1, 1) * (2 * x0 - 1) + sched_b[times].reshape(B, 1, 1, 1, 1) * noise
+    assert rel(ops.from_cl(xn, B, C, T), ref) < tol
+    pred = torch.randn(B, C, T, H, W, generator=g)
+    pc = ops.to_cl(pred.cuda(), dtype).requires_grad_()
+    loss = ops.mse_loss_cl(pc, noise.cuda())
+    predr = _leaf(pred.to(dtype).float())
+    lr = F.mse_loss(predr, noise)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) / lr.item() < tol
+    loss.backward()
+    gd = ops.from_cl(pc.grad, B, C, T)
+    assert rel(gd, predr.grad) < tol
+
+
+def test_linear_small():
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(19)
+    B, K, N = 4, 64, 256
+    x = torch.randn(B, K, generator=g)
+    w = torch.randn(N, K, generator=g) / 8
+    b = torch.randn(N, generator=g)
+    gy = torch.randn(B, N, generator=g)
+    for act_in, act_out in [(0, 2), (1, 0)]:
+        xr, wr, br = _leaf(x), _leaf(w), _leaf(b)
+        xi = F.silu(xr) if act_in == 1 else xr
+        yr = xi @ wr.t() + br
+        if act_out == 2:
+            yr = F.gelu(yr)
+        (yr * gy).sum().backward()
+        xd, wd, bd = _leaf(x, "cuda"), _leaf(w, "cuda"), _leaf(b, "cuda")
+        y = ops.linear_small(xd, wd, bd, act_in, act_out)
+        assert rel(y, yr) < 2e-6
+        (y * gy.cuda()).sum().backward()
+        grads_match([xd.grad, wd.grad, bd.grad], [xr.grad, wr.grad, br.grad], 2e-6)
+    t = torch.tensor([0, 5, 537, 999])
+    emb = ops.sinusoidal(t.cuda(), 64).cpu()
+    half = 32
+    f = torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1)))
+    a = t.float()[:, None] * f[None]
+    assert rel(emb, torch.cat((a.sin(), a.cos()), -1)) < 2e-7
