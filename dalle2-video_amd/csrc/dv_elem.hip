@@ -293,12 +293,63 @@ __global__ void p_sample_kernel(const float* x, const T* eps, int ld, const floa
     const int c = (int)(r % C), b = (int)(r / C);
     const long long ti = t[b];
     const long long p = ((long long)b * T_ + tt) * HW + hw;
-    float x0 = sra[ti] * x[i] - srm1[ti] * (float)eps[p * ld + c];
+    const float e = ld > 0 ? (float)eps[p * ld + c] : ((const float*)eps)[i];
+    float x0 = sra[ti] * x[i] - srm1[ti] * e;
     if (clip) x0 = fminf(fmaxf(x0, -1.f), 1.f);
     const float mean = c1[ti] * x0 + c2[ti] * x[i];
     const float nz = ti == 0 ? 0.f : 1.f;
     out[i] = mean + nz * expf(0.5f * logvar[ti]) * noise[i];
     if (x0_out) x0_out[i] = x0;
+  }
+}
+
+
+// per-frame nearest resize of NCTHW f32 planes (F.interpolate(mode="nearest"),
+// resize_image_to at dalle2_video.py:2257, 1129-1146); optional clamp
+__device__ __forceinline__ int nearest_src(int o, int in, int out) {
+  if (out == in) return o;
+  if (out == 2 * in) return o >> 1;
+  const float scale = (float)in / (float)out;
+  const int s = (int)floorf((float)o * scale);
+  return s < in - 1 ? s : in - 1;
+}
+__global__ void resize_nearest_kernel(const float* x, float* y, long long planes, int hin, int win,
+                                      int hout, int wout, int do_clamp, float lo, float hi) {
+  const long long n = planes * hout * wout;
+  GRID_STRIDE(i, n) {
+    const int ox = (int)(i % wout);
+    const long long r = i / wout;
+    const int oy = (int)(r % hout);
+    const long long pl = r / hout;
+    float v = x[(pl * hin + nearest_src(oy, hin, hout)) * win + nearest_src(ox, win, wout)];
+    if (do_clamp) v = fminf(fmaxf(v, lo), hi);
+    y[i] = v;
+  }
+}
+
+// kornia gaussian_blur2d per frame: separable normalized gaussian, 'reflect' border
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  if (i < 0) i = -i;
+  if (i >= n) i = 2 * n - 2 - i;
+  return i;
+}
+__global__ void blur_kernel(const float* x, float* y, long long planes, int H, int W, int ks,
+                            const float* w1) {
+  const long long n = planes * H * W;
+  const int r = ks / 2;
+  GRID_STRIDE(i, n) {
+    const int ox = (int)(i % W);
+    const long long rr = i / W;
+    const int oy = (int)(rr % H);
+    const long long pl = rr / H;
+    float acc = 0.f;
+    for (int dy = -r; dy <= r; ++dy) {
+      const int yy = reflect_idx(oy + dy, H);
+      float row = 0.f;
+      for (int dx = -r; dx <= r; ++dx) row += w1[dx + r] * x[(pl * H + yy) * W + reflect_idx(ox + dx, W)];
+      acc += w1[dy + r] * row;
+    }
+    y[i] = acc;
   }
 }
 
@@ -449,4 +500,20 @@ extern "C" int dv_p_sample(int dtype, const float* x, const void* eps, int ld, c
            (p_sample_kernel<float><<<grid_for(n), 256, 0, st>>>(x, (const float*)eps, ld, noise, t, sqrt_recip_ac, sqrt_recipm1_ac, coef1, coef2, logvar, out, x0_out, B, C, T, H * W, clip)),
            (p_sample_kernel<bf16><<<grid_for(n), 256, 0, st>>>(x, (const bf16*)eps, ld, noise, t, sqrt_recip_ac, sqrt_recipm1_ac, coef1, coef2, logvar, out, x0_out, B, C, T, H * W, clip)));
   return check_launch("p_sample");
+}
+
+extern "C" int dv_resize_nearest(const float* x, float* y, long long planes, int hin, int win,
+                                 int hout, int wout, int do_clamp, float lo, float hi,
+                                 void* stream) {
+  DV_REQUIRE(x && y && hin > 0 && win > 0 && hout > 0 && wout > 0, "bad arguments");
+  resize_nearest_kernel<<<grid_for(planes * hout * wout), 256, 0, (hipStream_t)stream>>>(
+      x, y, planes, hin, win, hout, wout, do_clamp, lo, hi);
+  return check_launch("resize_nearest");
+}
+
+extern "C" int dv_gaussian_blur(const float* x, float* y, long long planes, int H, int W, int ks,
+                                const float* w1, void* stream) {
+  DV_REQUIRE(x && y && w1 && (ks & 1) && ks / 2 < H && ks / 2 < W, "bad arguments");
+  blur_kernel<<<grid_for(planes * H * W), 256, 0, (hipStream_t)stream>>>(x, y, planes, H, W, ks, w1);
+  return check_launch("gaussian_blur");
 }

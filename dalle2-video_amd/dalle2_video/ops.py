@@ -36,8 +36,10 @@ def _pad_channels(t: torch.Tensor, mult: int = 8) -> torch.Tensor:
 
 
 def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int) -> torch.Tensor:
+    if weight.dim() not in (2, 5) or (weight.dim() == 5 and weight.shape[-1] != weight.shape[-2]):
+        raise _lib.DVError(f"conv weight must be (cout, cin) or (cout, cin, 1, k, k), got {tuple(weight.shape)}")
     cout, cin = weight.shape[0], weight.shape[1]
-    k = weight.shape[-1]
+    k = weight.shape[-1] if weight.dim() == 5 else 1  # nn.Linear weights are 1x1 convs
     rows = cout if mode == 0 else cin
     out = (torch.empty if mode == 0 else torch.zeros)(rows, k * k, pad_to, dtype=dtype,
                                                       device=weight.device)
@@ -568,3 +570,58 @@ class MSELossFn(torch.autograd.Function):
 
 def mse_loss_cl(pred_cl, target, sample_w=None):
     return MSELossFn.apply(pred_cl, target, sample_w)
+
+
+def p_sample_step(x, eps, noise, times, sched, clip_denoised=True):
+    """x0 = sqrt(1/ac) x - sqrt(1/ac - 1) eps -> clamp -> posterior mean + sigma z
+    (p_mean_variance + p_sample, dalle2_video.py:1551-1664).  eps is an NCTHW
+    f32 tensor or a channels-last frame tensor."""
+    require_gpu(x, eps, noise, times)
+    xf = x.float().contiguous()
+    nz = noise.float().contiguous()
+    t = times.to(torch.int64).contiguous()
+    B, C, T, H, W = xf.shape
+    if eps.dim() == 5:
+        ef = eps.float().contiguous()
+        ld, edt = 0, _lib.DV_F32
+    else:
+        ef = eps
+        ld, edt = cl_ld(eps), dt(eps)
+    out = torch.empty_like(xf)
+    x0 = torch.empty_like(xf)
+    call("dv_p_sample", edt, ptr(xf), ptr(ef), ld, ptr(nz), ptr(t), ptr(sched.sqrt_recip_alphas_cumprod),
+         ptr(sched.sqrt_recipm1_alphas_cumprod), ptr(sched.posterior_mean_coef1),
+         ptr(sched.posterior_mean_coef2), ptr(sched.posterior_log_variance_clipped), ptr(out), ptr(x0),
+         B, C, T, H, W, int(clip_denoised), stream())
+    return out, x0
+
+
+def resize_nearest(video, size, clamp_range=None):
+    """Per-frame nearest resize of an NCTHW clip to size x size."""
+    require_gpu(video)
+    v = video.float().contiguous()
+    B, C, T, H, W = v.shape
+    y = torch.empty(B, C, T, size, size, dtype=torch.float32, device=v.device)
+    lo, hi = clamp_range if clamp_range is not None else (0.0, 0.0)
+    call("dv_resize_nearest", ptr(v), ptr(y), B * C * T, H, W, size, size, int(clamp_range is not None),
+         ctypes_float(lo), ctypes_float(hi), stream())
+    return y
+
+
+def gaussian_kernel1d(ks, sigma):
+    x = torch.arange(ks, dtype=torch.float32) - ks // 2
+    if ks % 2 == 0:
+        x = x + 0.5
+    g = torch.exp(-x.pow(2.0) / (2 * sigma ** 2))
+    return g / g.sum()
+
+
+def gaussian_blur(video, ks, sigma):
+    """kornia gaussian_blur2d((ks,ks), (sigma,sigma)) per frame, reflect border."""
+    require_gpu(video)
+    v = video.float().contiguous()
+    B, C, T, H, W = v.shape
+    w1 = gaussian_kernel1d(ks, sigma).to(v.device)
+    y = torch.empty_like(v)
+    call("dv_gaussian_blur", ptr(v), ptr(y), B * C * T, H, W, ks, ptr(w1), stream())
+    return y

@@ -57,3 +57,24 @@ def test_conv_fwd_bwd(case, dtype, tol):
     assert rel(dx.float(), xr.grad) < tol * 2
     assert rel(wd.grad, wr.grad) < tol * 2
     assert rel(bd.grad, br.grad) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
+def test_linear_weight_as_1x1_conv(dtype, tol):
+    """nn.Linear weights (cout, cin) run as 1x1 convs over tokens (mid attention)."""
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(4, 4, 4, 512, generator=g)
+    w = torch.randn(64, 512, generator=g) / 512 ** 0.5
+    xr, wr = x.to(dtype).float().clone().requires_grad_(), w.clone().requires_grad_()
+    yr = xr @ wr.t()
+    gy = torch.randn(yr.shape, generator=g)
+    (yr * gy).sum().backward()
+    xd = x.detach().to("cuda", dtype).requires_grad_()
+    wd = w.detach().cuda().requires_grad_()
+    y = ops.conv(xd, wd)
+    assert rel(y.float(), yr) < tol
+    (y.float() * gy.cuda()).sum().backward()
+    assert rel(xd.grad.float(), xr.grad) < tol * 2
+    assert rel(wd.grad, wr.grad) < tol * 2
