@@ -274,9 +274,13 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* x, long long n,
   if (threadIdx.x == 0) atomicAdd(out, acc);
 }
 
-__global__ void clip_coef_kernel(const float* sumsq, float max_norm, float* coef) {
-  const float c = max_norm / (sqrtf(sumsq[0]) + 1e-6f);
-  coef[0] = c < 1.f ? c : 1.f;
+// coef = prescale * min(max_norm / (||prescale * g|| + 1e-6), 1)  (prescale = 1/world
+// folds the DDP average into the update; torch.nn.utils.clip_grad_norm_ semantics)
+__global__ void clip_coef_kernel(const float* sumsq, float max_norm, float prescale, float* coef) {
+  const float norm = prescale * sqrtf(sumsq[0]);
+  float c = max_norm > 0.f ? max_norm / (norm + 1e-6f) : 1.f;
+  coef[0] = prescale * (c < 1.f ? c : 1.f);
+  coef[1] = norm;
 }
 
 template <typename T>
@@ -477,14 +481,14 @@ extern "C" int dv_adamw(float* p, const float* g, float* m, float* v, long long 
   return check_launch("adamw");
 }
 
-extern "C" int dv_grad_clip_coef(const float* g, long long n, float max_norm, float* ws,
-                                 void* stream) {
-  // ws[0] = sum of squares, ws[1] = min(max_norm / (norm + 1e-6), 1)
+extern "C" int dv_grad_clip_coef(const float* g, long long n, float max_norm, float prescale,
+                                 float* ws, void* stream) {
+  // ws[0] = sum of squares, ws[1] = update coefficient, ws[2] = gradient norm
   DV_REQUIRE(g && ws, "null pointer");
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(ws, 0, sizeof(float), st);
   sumsq_kernel<<<grid_for(n, 256, 2048), 256, 0, st>>>(g, n, ws);
-  clip_coef_kernel<<<1, 1, 0, st>>>(ws, max_norm, ws + 1);
+  clip_coef_kernel<<<1, 1, 0, st>>>(ws, max_norm, prescale, ws + 1);
   return check_launch("grad_clip_coef");
 }
 

@@ -44,7 +44,7 @@ _SIGS = {
     "dv_linear_small_fwd": [_P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
     "dv_linear_small_bwd": [_P, _I, _P, _I, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_adamw": [_P, _P, _P, _P, _L, _L, _F, _F, _F, _F, _F, _F, _F, _P, _P],
-    "dv_grad_clip_coef": [_P, _L, _F, _P, _P],
+    "dv_grad_clip_coef": [_P, _L, _F, _F, _P, _P],
     "dv_p_sample": [_I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_xattn_fold": [_P, _P, _P, _P, _P, _P, _I, _I, _F, _P],
     "dv_xattn_fwd": [_I, _P, _I, _P, _I, _L, _L, _I, _P, _P, _P, _P, _F, _P, _P, _P],
@@ -103,6 +103,14 @@ def dt(t: torch.Tensor) -> int:
     if t.dtype == torch.bfloat16:
         return DV_BF16
     raise DVError(f"unsupported dtype {t.dtype}")
+
+
+def ctypes_vp(addr):
+    return ctypes.c_void_p(addr)
+
+
+def dtype_name(t):
+    return "bf16" if t.dtype == torch.bfloat16 else "float"
 
 
 def ptr(t):

@@ -13,6 +13,55 @@ from . import _lib
 from ._lib import ACT_NONE, call, dt, ptr, require_gpu, stream
 
 
+class KernelTimer:
+    """Optional live per-kernel timing with HIP events on the launching stream
+    (bench.py uses it for the roofline of the dominant kernel)."""
+
+    def __init__(self):
+        self.records = []  # (name, flops, bytes, start_event, end_event)
+
+    def run(self, name, flops, nbytes, fn):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        self.records.append((name, flops, nbytes, s, e))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, fl, nb, s, e in self.records:
+            d = out.setdefault(name, dict(count=0, flops=0.0, bytes=0.0, ms=0.0))
+            d["count"] += 1
+            d["flops"] += fl
+            d["bytes"] += nb
+            d["ms"] += s.elapsed_time(e)
+        return out
+
+
+TIMER = None  # set to a KernelTimer to time kernel launches
+
+
+def _launch(name, flops, nbytes, fn):
+    if TIMER is None:
+        fn()
+    else:
+        TIMER.run(name, flops, nbytes, fn)
+
+
+def conv_tile(m, cout):
+    """Mirror of conv_fwd_t's tile choice (names the kernel instantiation)."""
+    mt128 = (m + 127) // 128
+    bn = 64 if cout <= 64 else 128
+    bm = 128
+    if mt128 * ((cout + bn - 1) // bn) < 512:
+        bm = 64
+    if bm == 64 and bn == 128 and ((m + 63) // 64) * ((cout + 127) // 128) < 512:
+        bn = 64
+    return bm, bn
+
+
 def cl_ld(t: torch.Tensor) -> int:
     """Pixel stride of a channels-last frame tensor (asserts the layout)."""
     if t.dim() != 4 or (t.stride(3) != 1 and t.shape[3] > 1):
@@ -69,8 +118,12 @@ class ConvFn(torch.autograd.Function):
         ld1 = cl_ld(x1) if x1 is not None else 0
         ldr = cl_ld(res) if res is not None else 0
         b = None if bias is None else bias.detach().float().contiguous()
-        call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b), ptr(res), ldr,
-             ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE, stream())
+        m = nf * h * w
+        bm, bn = conv_tile(m, cout)
+        _launch(f"conv_fwd_kernel<{_lib.dtype_name(x0)},{bm},{bn}>", 2.0 * m * cout * cin * ksize * ksize,
+                x0.element_size() * m * (cin + cout),
+                lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b), ptr(res),
+                             ldr, ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE, stream()))
         ctx.save_for_backward(x0, x1, weight)
         ctx.meta = (ksize, c0, c1, bias is not None, res is not None)
         return y
@@ -89,16 +142,23 @@ class ConvFn(torch.autograd.Function):
             wpd = pack_conv_weight(weight, dy.dtype, cout8, 1)
             alloc = torch.empty if cin_real == cin else torch.zeros
             dx = alloc(nf, h, w, cin, dtype=dy.dtype, device=dy.device)
-            call("dv_conv_fwd", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd), None, None, 0,
-                 ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE, stream())
+            m = nf * h * w
+            bm, bn = conv_tile(m, cin_real)
+            _launch(f"conv_fwd_kernel<{_lib.dtype_name(dy8)},{bm},{bn}>", 2.0 * m * cin_real * cout8 * ksize * ksize,
+                    dy8.element_size() * m * (cin + cout8),
+                    lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd), None, None, 0,
+                                 ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE, stream()))
             dx0 = dx[..., :c0]
             dx1 = dx[..., c0:] if x1 is not None else None
         if ctx.needs_input_grad[2]:
             ws = torch.zeros(cout8, ksize * ksize, cin, dtype=torch.float32, device=dy.device)
             ld0 = cl_ld(x0)
             ld1 = cl_ld(x1) if x1 is not None else 0
-            call("dv_conv_wgrad", dt(dy8), ptr(dy8), cout8, ptr(x0), ld0, c0, ptr(x1), ld1, ptr(ws),
-                 nf, h, w, cin, cout8, ksize, stream())
+            m = nf * h * w
+            _launch(f"conv_wgrad_kernel<{_lib.dtype_name(dy8)}>", 2.0 * m * cout8 * cin * ksize * ksize,
+                    dy8.element_size() * m * (cin + cout8),
+                    lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), cout8, ptr(x0), ld0, c0, ptr(x1), ld1,
+                                 ptr(ws), nf, h, w, cin, cout8, ksize, stream()))
             dw = torch.empty(weight.shape, dtype=torch.float32, device=dy.device)
             call("dv_unpack_wgrad", ptr(ws), ptr(dw), cout8, cin, ksize, cout, cin_real, 0, stream())
         if has_bias and ctx.needs_input_grad[3]:

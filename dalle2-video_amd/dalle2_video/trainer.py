@@ -1,0 +1,406 @@
+"""VideoDecoderTrainer — drop-in for dalle2_video/trainer.py (trainer.py:9-365)
+on the MI355X path.
+
+* Same constructor / `__call__(video_embed=, video=, unet_number=)` / `update()`
+  / `save` / `load` surface, `optim{i}` / `sched{i}` attributes with torch
+  param_groups, `steps` buffer, `train_loader` / `val_loader`.
+* Optimizer: dalle2-pytorch `get_optimizer` semantics (AdamW betas (0.9, 0.99),
+  weight decay only on ndim >= 2 parameters) executed as ONE fused HIP kernel
+  over a flat f32 parameter/gradient/moment buffer per unet (`FusedAdamW`,
+  state-dict compatible with torch.optim.AdamW).
+* Gradient clipping (`clip_grad_norm_(decoder.parameters(), 0.5)`,
+  trainer.py:254-257) is a HIP reduction whose coefficient is applied inside
+  the AdamW kernel: no host synchronisation.
+* Data parallel: one process per GPU (torchrun); the active unet's flat
+  gradient is summed with a single RCCL all-reduce over xGMI and the 1/world
+  average is folded into the update coefficient.  No other collective.
+"""
+from __future__ import annotations
+
+import math
+import os
+from contextlib import nullcontext
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import _lib
+from ._lib import call, ptr, stream
+from .dalle2_video import VideoDecoder, cast_tuple, default, exists
+from .ops import ctypes_float
+
+__version__ = "1.14.2-mi355x"
+
+
+def groupby_prefix_and_trim(prefix, d):
+    with_p = {k[len(prefix):]: v for k, v in d.items() if k.startswith(prefix)}
+    without = {k: v for k, v in d.items() if not k.startswith(prefix)}
+    return with_p, without
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """AdamW over one flat f32 buffer (params are re-pointed into it).
+
+    Parameters that never receive a gradient (e.g. the unused null_* embeds)
+    stay outside the flat buffer and are skipped exactly like torch skips a
+    parameter whose .grad is None."""
+
+    def __init__(self, params, lr=1e-4, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-2):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self._flat = None  # (P, G, M, V, [(group, start, end)], params)
+        self._clip_ws = None
+        self._t = 0
+
+    # -- flat storage ------------------------------------------------------
+    def _build_flat(self):
+        live = []
+        for gi, group in enumerate(self.param_groups):
+            for p in group["params"]:
+                if p.grad is not None:
+                    live.append((gi, p))
+        if not live:
+            return
+        dev = live[0][1].device
+        n = sum(p.numel() for _, p in live)
+        P = torch.empty(n, dtype=torch.float32, device=dev)
+        G = torch.empty(n, dtype=torch.float32, device=dev)
+        M = torch.zeros(n, dtype=torch.float32, device=dev)
+        V = torch.zeros(n, dtype=torch.float32, device=dev)
+        ranges = []
+        off = 0
+        for gi in range(len(self.param_groups)):
+            start = off
+            for g2, p in live:
+                if g2 != gi:
+                    continue
+                k = p.numel()
+                st = self.state.get(p, {})
+                P[off:off + k].copy_(p.detach().reshape(-1))
+                G[off:off + k].copy_(p.grad.detach().reshape(-1))
+                if "exp_avg" in st:
+                    M[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                    V[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                p.data = P[off:off + k].view_as(p)
+                p.grad = G[off:off + k].view_as(p)
+                self.state[p] = dict(step=torch.tensor(float(self._t)),
+                                     exp_avg=M[off:off + k].view_as(p),
+                                     exp_avg_sq=V[off:off + k].view_as(p))
+                off += k
+            ranges.append((gi, start, off))
+        self._flat = (P, G, M, V, ranges, [p for _, p in live])
+
+    @property
+    def flat_grad(self):
+        return None if self._flat is None else self._flat[1]
+
+    def ensure_flat(self):
+        if self._flat is None:
+            self._build_flat()
+        return self._flat is not None
+
+    @torch.no_grad()
+    def step(self, closure=None, clip_coef=None):
+        if not self.ensure_flat():
+            return None
+        P, G, M, V, ranges, _ = self._flat
+        self._t += 1
+        for gi, start, end in ranges:
+            if end <= start:
+                continue
+            group = self.param_groups[gi]
+            b1, b2 = group["betas"]
+            bc1 = 1 - b1 ** self._t
+            bc2s = math.sqrt(1 - b2 ** self._t)
+            n = end - start
+            es = 4
+            call("dv_adamw", _lib.ctypes_vp(P.data_ptr() + start * es), _lib.ctypes_vp(G.data_ptr() + start * es),
+                 _lib.ctypes_vp(M.data_ptr() + start * es), _lib.ctypes_vp(V.data_ptr() + start * es),
+                 n, n if group["weight_decay"] > 0 else 0, ctypes_float(group["lr"]), ctypes_float(b1),
+                 ctypes_float(b2), ctypes_float(group["eps"]), ctypes_float(group["weight_decay"]),
+                 ctypes_float(bc1), ctypes_float(bc2s), ptr(clip_coef), stream())
+        return None
+
+    def state_dict(self):
+        if self._flat is not None:
+            for p in self._flat[5]:
+                self.state[p]["step"] = torch.tensor(float(self._t))
+        return super().state_dict()
+
+    def zero_grad(self, set_to_none: bool = True):
+        if self._flat is not None:
+            self._flat[1].zero_()  # grads stay views of the flat buffer
+            return
+        super().zero_grad(set_to_none=set_to_none)
+
+    def clip_coefficient(self, max_norm, prescale=1.0):
+        """Device scalar: prescale * min(max_norm / (||prescale g|| + 1e-6), 1)."""
+        if not self.ensure_flat():
+            return None
+        G = self._flat[1]
+        if self._clip_ws is None:
+            self._clip_ws = torch.zeros(4, dtype=torch.float32, device=G.device)
+        call("dv_grad_clip_coef", ptr(G), G.numel(), ctypes_float(max_norm if max_norm else 0.0),
+             ctypes_float(prescale), ptr(self._clip_ws), stream())
+        return self._clip_ws[1:2]
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        steps = [float(s["step"]) for s in self.state.values() if "step" in s]
+        self._t = int(max(steps)) if steps else 0
+        if self._flat is not None:
+            self._flat = None  # rebuilt (and re-pointed) on the next step
+
+
+def get_optimizer(params, lr=1e-4, wd=1e-2, betas=(0.9, 0.99), eps=1e-8,
+                  filter_by_requires_grad=False, group_wd_params=True, **kwargs):
+    params = list(params)
+    if filter_by_requires_grad:
+        params = [p for p in params if p.requires_grad]
+    if wd == 0:
+        return FusedAdamW(params, lr=lr, betas=betas, eps=eps, weight_decay=0.0)
+    if group_wd_params:
+        wd_p = [p for p in params if p.ndim >= 2]
+        no_wd = [p for p in params if p.ndim < 2]
+        params = [{"params": wd_p}, {"params": no_wd, "weight_decay": 0.0}]
+    return FusedAdamW(params, lr=lr, weight_decay=wd, betas=betas, eps=eps)
+
+
+class _LinearWarmup:
+    """pytorch_warmup.LinearWarmup stand-in: lr factor min(1, step/period)."""
+
+    def __init__(self, optimizer, warmup_period):
+        self.optimizer = optimizer
+        self.period = warmup_period
+        self.last_step = 0
+
+    def dampening(self):
+        opt = self
+
+        class _Ctx:
+            def __enter__(self_):
+                return None
+
+            def __exit__(self_, *a):
+                opt.last_step += 1
+                f = min(1.0, opt.last_step / max(opt.period, 1))
+                for g in opt.optimizer.param_groups:
+                    g["lr"] = g["lr"] * f
+                return False
+        return _Ctx()
+
+
+class EMA(nn.Module):
+    """ema-pytorch EMA (beta 0.9999, update_after_step 100, update_every 10,
+    inv_gamma 1, power 2/3) — outside the hot path, kept for API completeness."""
+
+    def __init__(self, model, beta=0.9999, update_after_step=100, update_every=10, inv_gamma=1.0,
+                 power=2 / 3, min_value=0.0, **kwargs):
+        super().__init__()
+        import copy
+        self.beta, self.update_after_step, self.update_every = beta, update_after_step, update_every
+        self.inv_gamma, self.power, self.min_value = inv_gamma, power, min_value
+        self.online_model = [model]
+        self.ema_model = copy.deepcopy(model)
+        self.ema_model.requires_grad_(False)
+        self.register_buffer("initted", torch.tensor(False))
+        self.register_buffer("step", torch.tensor(0))
+
+    def restore_ema_model_device(self):
+        self.ema_model.to(next(self.online_model[0].parameters()).device)
+
+    def _decay(self):
+        epoch = max(self.step.item() - self.update_after_step - 1, 0)
+        if epoch <= 0:
+            return 0.0
+        value = 1 - (1 + epoch / self.inv_gamma) ** -self.power
+        return min(max(value, self.min_value), self.beta)
+
+    @torch.no_grad()
+    def update(self):
+        step = self.step.item()
+        self.step += 1
+        if step % self.update_every != 0:
+            return
+        src = self.online_model[0]
+        if step <= self.update_after_step or not self.initted.item():
+            for pe, p in zip(self.ema_model.parameters(), src.parameters()):
+                pe.copy_(p)
+            self.initted.fill_(True)
+            return
+        d = self._decay()
+        for pe, p in zip(self.ema_model.parameters(), src.parameters()):
+            pe.lerp_(p, 1 - d)
+
+
+def split_args_and_kwargs(*args, split_size=None, **kwargs):
+    all_args = (*args, *kwargs.values())
+    batch = next((a.shape[0] for a in all_args if torch.is_tensor(a)), None)
+    if split_size is None or batch is None or batch <= split_size:
+        yield 1.0, (args, kwargs)
+        return
+    n_chunks = (batch + split_size - 1) // split_size
+    for i in range(n_chunks):
+        sl = slice(i * split_size, (i + 1) * split_size)
+        cargs = tuple(a[sl] if torch.is_tensor(a) else a for a in args)
+        ckw = {k: (v[sl] if torch.is_tensor(v) else v) for k, v in kwargs.items()}
+        size = next(a.shape[0] for a in (*cargs, *ckw.values()) if torch.is_tensor(a))
+        yield size / batch, (cargs, ckw)
+
+
+class VideoDecoderTrainer(nn.Module):
+    def __init__(self, decoder, accelerator=None, dataloaders=None, use_ema=True, lr=1e-4,
+                 wd=1e-2, eps=1e-8, warmup_steps=None, cosine_decay_max_steps=None,
+                 max_grad_norm=0.5, amp=False, group_wd_params=True, **kwargs):
+        super().__init__()
+        assert isinstance(decoder, VideoDecoder)
+        ema_kwargs, kwargs = groupby_prefix_and_trim("ema_", kwargs)
+        self.accelerator = accelerator
+        self.num_unets = len(decoder.unets)
+        self.use_ema = use_ema
+        self.ema_unets = nn.ModuleList([])
+        self.amp = amp or os.environ.get("DV_AMP", "") == "bf16"
+        lr, wd, eps, warmup_steps, cosine_decay_max_steps = (
+            cast_tuple(v, self.num_unets) for v in (lr, wd, eps, warmup_steps, cosine_decay_max_steps))
+        assert all(l <= 1e-2 for l in lr), \
+            "your learning rate is too high, recommend sticking with 1e-4, at most 5e-4"
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.decoder = decoder
+        for i, (unet, ulr, uwd, ueps, uwarm, ucos) in enumerate(
+                zip(decoder.unets, lr, wd, eps, warmup_steps, cosine_decay_max_steps)):
+            opt = get_optimizer(unet.parameters(), lr=ulr, wd=uwd, eps=ueps,
+                                group_wd_params=group_wd_params, **kwargs)
+            sched = (torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=ucos) if exists(ucos)
+                     else torch.optim.lr_scheduler.LambdaLR(opt, lr_lambda=lambda step: 1.0))
+            setattr(self, f"optim{i}", opt)
+            setattr(self, f"sched{i}", sched)
+            if self.use_ema:
+                self.ema_unets.append(EMA(unet, **ema_kwargs))
+        self.warmup_schedulers = [(_LinearWarmup(getattr(self, f"optim{i}"), w) if exists(w) else None)
+                                  for i, w in enumerate(warmup_steps)]
+        self.max_grad_norm = max_grad_norm
+        self.register_buffer("steps", torch.tensor([0] * self.num_unets))
+        self.train_loader = dataloaders["train"] if exists(dataloaders) else None
+        self.val_loader = dataloaders["val"] if exists(dataloaders) else None
+        if self.world > 1:  # every rank starts from rank 0's weights (DDP init broadcast)
+            for p in decoder.parameters():
+                dist.broadcast(p.data, 0)
+
+    @property
+    def device(self):
+        return self.decoder.device
+
+    def validate_and_return_unet_number(self, unet_number=None):
+        if self.num_unets == 1:
+            unet_number = default(unet_number, 1)
+        assert exists(unet_number) and 1 <= unet_number <= self.num_unets
+        return unet_number
+
+    def num_steps_taken(self, unet_number=None):
+        return self.steps[self.validate_and_return_unet_number(unet_number) - 1].item()
+
+    @property
+    def unets(self):
+        return nn.ModuleList([ema.ema_model for ema in self.ema_unets])
+
+    def increment_step(self, unet_number):
+        self.steps[unet_number - 1] += 1
+
+    # -- one optimizer step (trainer.py:247-274) ----------------------------
+    def update(self, unet_number=None):
+        unet_number = self.validate_and_return_unet_number(unet_number)
+        index = unet_number - 1
+        opt = getattr(self, f"optim{index}")
+        sched = getattr(self, f"sched{index}")
+        opt.ensure_flat()
+        if self.world > 1 and opt.flat_grad is not None:
+            dist.all_reduce(opt.flat_grad)  # RCCL over xGMI; 1/world folded below
+        coef = opt.clip_coefficient(self.max_grad_norm, prescale=1.0 / self.world)
+        opt.step(clip_coef=coef)
+        opt.zero_grad()
+        warm = self.warmup_schedulers[index]
+        with (warm.dampening() if exists(warm) else nullcontext()):
+            sched.step()
+        if self.use_ema:
+            self.ema_unets[index].update()
+        self.increment_step(unet_number)
+
+    def _to_device(self, v):
+        if v is None:
+            return v
+        if not torch.is_tensor(v):
+            import numpy as np
+            if isinstance(v, np.ndarray):
+                v = torch.from_numpy(v)
+            else:
+                return v
+        return v.to(self.device)
+
+    def forward(self, *args, unet_number=None, max_batch_size=None, return_lowres_cond_video=False,
+                **kwargs):
+        unet_number = self.validate_and_return_unet_number(unet_number)
+        args = tuple(self._to_device(a) for a in args)
+        kwargs = {k: self._to_device(v) for k, v in kwargs.items()}
+        total_loss = 0.0
+        cond_videos = []
+        for frac, (cargs, ckw) in split_args_and_kwargs(*args, split_size=max_batch_size, **kwargs):
+            ctx = torch.autocast("cuda", dtype=torch.bfloat16) if self.amp else nullcontext()
+            with ctx:
+                out = self.decoder(*cargs, unet_number=unet_number,
+                                   return_lowres_cond_video=return_lowres_cond_video, **ckw)
+            loss, cv = (out if return_lowres_cond_video else (out, None))
+            loss = loss * frac
+            if cv is not None:
+                cond_videos.append(cv)
+            total_loss += loss.item()
+            if self.training:
+                loss.backward()
+        if return_lowres_cond_video:
+            return total_loss, torch.stack(cond_videos)
+        return total_loss
+
+    # -- checkpointing (trainer.py:158-235) ---------------------------------
+    def save(self, path, overwrite=True, **kwargs):
+        path = Path(path)
+        assert not (path.exists() and not overwrite)
+        path.parent.mkdir(parents=True, exist_ok=True)
+        obj = dict(model=self.decoder.state_dict(), version=__version__, steps=self.steps.cpu(), **kwargs)
+        for i in range(self.num_unets):
+            obj[f"optim{i}"] = getattr(self, f"optim{i}").state_dict()
+            obj[f"sched{i}"] = getattr(self, f"sched{i}").state_dict()
+        if self.use_ema:
+            obj["ema"] = self.ema_unets.state_dict()
+        if self.world == 1 or dist.get_rank() == 0:
+            torch.save(obj, str(path))
+
+    def load_state_dict(self, loaded_obj, only_model=False, strict=True):
+        self.decoder.load_state_dict(loaded_obj["model"], strict=strict)
+        self.steps.copy_(loaded_obj["steps"])
+        if only_model:
+            return loaded_obj
+        for i, last in zip(range(self.num_unets), self.steps.tolist()):
+            getattr(self, f"optim{i}").load_state_dict(loaded_obj[f"optim{i}"])
+            getattr(self, f"sched{i}").load_state_dict(loaded_obj[f"sched{i}"])
+            if exists(self.warmup_schedulers[i]):
+                self.warmup_schedulers[i].last_step = last
+        if self.use_ema:
+            self.ema_unets.load_state_dict(loaded_obj["ema"], strict=strict)
+        return loaded_obj
+
+    def load(self, path, only_model=False, strict=True):
+        path = Path(path)
+        assert path.exists()
+        obj = torch.load(str(path), map_location="cpu", weights_only=True)
+        self.load_state_dict(obj, only_model=only_model, strict=strict)
+        return obj
+
+    @torch.no_grad()
+    def sample(self, *args, **kwargs):
+        was = self.decoder.training
+        self.decoder.eval()
+        kwargs.pop("use_non_ema", None)
+        out = self.decoder.sample(*args, **kwargs)
+        self.decoder.train(was)
+        return out

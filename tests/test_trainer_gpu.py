@@ -1,0 +1,71 @@
+"""VideoDecoderTrainer (fused HIP AdamW + HIP grad-norm clip) vs the golden
+3-step training trace G4 (torch AdamW + clip_grad_norm_ on the CPU oracle)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dv_ref as R
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_three_step_trace_matches_golden():
+    from dalle2_video import dalle2_video as D
+    from dalle2_video.trainer import VideoDecoderTrainer
+
+    g = np.load(os.path.join(GOLD, "g4_plosses.npz"))
+    ou = R.deterministic_fill_(R.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+                               .cast_model_parameters(lowres_cond=False, lowres_noise_cond=False, channels=3,
+                                                      channels_out=3, cond_on_image_embeds=True,
+                                                      cond_on_text_encodings=False))
+    u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    dec = D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(4,), timesteps=1000, learned_variance=False)
+    dec.unets[0].load_state_dict(ou.state_dict(), strict=True)
+    dec = dec.cuda()
+    tr = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False)
+    x = torch.from_numpy(g["x"]).cuda()
+    times = torch.from_numpy(g["times"]).cuda()
+    noise = torch.from_numpy(g["noise"]).cuda()
+    losses = []
+    for _ in range(3):
+        loss = dec.p_losses(dec.unets[0], x, times, video_embed=None,
+                            noise_scheduler=dec.noise_schedulers[0], noise=noise)
+        losses.append(loss.item())
+        loss.backward()
+        tr.update(1)
+    ref = g["losses"]
+    print("losses", losses, "ref", ref.tolist())
+    assert np.allclose(losses, ref, rtol=1e-4)
+    psum = sum(p.double().sum().item() for p in dec.unets[0].parameters())
+    assert abs(psum - g["param_sum"][0]) / abs(g["param_sum"][0]) < 1e-5
+    w = dec.unets[0].to_out.weight.detach().cpu().flatten().numpy()
+    assert np.allclose(w, g["to_out_w"], rtol=1e-3, atol=1e-6)
+    assert tr.num_steps_taken(1) == 3
+    sd = tr.optim0.state_dict()
+    assert len(sd["state"]) > 0 and all(float(s["step"]) == 3.0 for s in sd["state"].values())
+
+
+def test_trainer_call_api_and_checkpoint(tmp_path):
+    from dalle2_video import dalle2_video as D
+    from dalle2_video.trainer import VideoDecoderTrainer
+
+    u1 = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    u2 = D.Unet3D(8, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8, 16))
+    dec = D.VideoDecoder(unet=(u1, u2), frame_sizes=(32, 64), frame_numbers=(4, 4), timesteps=1000,
+                         learned_variance=False).cuda()
+    tr = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False, amp=True)
+    video = torch.rand(2, 3, 4, 64, 64, device="cuda")
+    emb = torch.randn(2, 512, device="cuda")
+    for un in (1, 2):
+        l = tr(video_embed=emb, video=video, unet_number=un)
+        assert isinstance(l, float) and np.isfinite(l)
+        tr.update(un)
+    assert tr.optim0.param_groups[0]["lr"] == 3e-4 and tr.optim1.param_groups[0]["lr"] == 3e-4
+    path = tmp_path / "ck.pt"
+    tr.save(str(path))
+    tr2 = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False)
+    tr2.load(str(path))
+    assert tr2.steps.tolist() == [1, 1]
