@@ -334,7 +334,7 @@ __global__ void mqa_prep_kernel(const T* kv, int ldkv, const float* null_kv, T* 
 
 template <typename T>
 __global__ void mqa_finish_kernel(const float* dkp, const float* dvp, T* dkv, int lddkv,
-                                  float* dnull, int B, int N, int NKP) {
+                                  float* dnull, int B, int N, int NKP, int accumulate) {
   const long long n = (long long)B * N * DH;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -348,7 +348,7 @@ __global__ void mqa_finish_kernel(const float* dkp, const float* dvp, T* dkv, in
     const int v = threadIdx.x / DH, d = threadIdx.x % DH;
     float s = 0.f;
     for (int b = 0; b < B; ++b) s += (v ? dvp : dkp)[(long long)b * NKP * DH + d];
-    dnull[threadIdx.x] = s;
+    dnull[threadIdx.x] = accumulate ? dnull[threadIdx.x] + s : s;
   }
 }
 
@@ -390,7 +390,7 @@ extern "C" int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int 
                           const void* dout, int lddo, const float* lse, const void* kp,
                           const void* vp, void* dq, int lddq, float* D, float* dkp, float* dvp,
                           void* dkv, int lddkv, float* dnull, int B, int N, int NKP, int H,
-                          float scale, void* stream) {
+                          float scale, int accumulate, void* stream) {
   DV_REQUIRE(q && o && dout && lse && kp && vp && dq && D && dkp && dvp && dkv && dnull, "null pointer");
   DV_REQUIRE(H % 8 == 0 && NKP % 32 == 0, "bad shape");
   hipStream_t st = (hipStream_t)stream;
@@ -401,12 +401,12 @@ extern "C" int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int 
     mqa_bwd_d_kernel<bf16><<<grid_for((long long)B * N * H), 256, 0, st>>>((const bf16*)o, ldo, (const bf16*)dout, lddo, D, B, N, H);
     mqa_dq_kernel<bf16><<<dim3((N + 31) / 32, H / 4, B), 256, 0, st>>>((const bf16*)q, ldq, (const bf16*)dout, lddo, lse, D, (const bf16*)kp, (const bf16*)vp, (bf16*)dq, lddq, N, NKP, N + 1, H, scale);
     mqa_dkdv_kernel<bf16><<<dim3(NKP / 32, hg, B), 256, 0, st>>>((const bf16*)q, ldq, (const bf16*)dout, lddo, lse, D, (const bf16*)kp, (const bf16*)vp, dkp, dvp, N, NKP, N + 1, H, hpg, scale);
-    mqa_finish_kernel<bf16><<<grid_for((long long)B * N * DH), 256, 0, st>>>(dkp, dvp, (bf16*)dkv, lddkv, dnull, B, N, NKP);
+    mqa_finish_kernel<bf16><<<grid_for((long long)B * N * DH), 256, 0, st>>>(dkp, dvp, (bf16*)dkv, lddkv, dnull, B, N, NKP, accumulate);
   } else {
     mqa_bwd_d_kernel<float><<<grid_for((long long)B * N * H), 256, 0, st>>>((const float*)o, ldo, (const float*)dout, lddo, D, B, N, H);
     mqa_dq_kernel<float><<<dim3((N + 31) / 32, H / 4, B), 256, 0, st>>>((const float*)q, ldq, (const float*)dout, lddo, lse, D, (const float*)kp, (const float*)vp, (float*)dq, lddq, N, NKP, N + 1, H, scale);
     mqa_dkdv_kernel<float><<<dim3(NKP / 32, hg, B), 256, 0, st>>>((const float*)q, ldq, (const float*)dout, lddo, lse, D, (const float*)kp, (const float*)vp, dkp, dvp, N, NKP, N + 1, H, hpg, scale);
-    mqa_finish_kernel<float><<<grid_for((long long)B * N * DH), 256, 0, st>>>(dkp, dvp, (float*)dkv, lddkv, dnull, B, N, NKP);
+    mqa_finish_kernel<float><<<grid_for((long long)B * N * DH), 256, 0, st>>>(dkp, dvp, (float*)dkv, lddkv, dnull, B, N, NKP, accumulate);
   }
   return check_launch("mqa_bwd");
 }

@@ -245,6 +245,7 @@ struct WgradArgs {
   const T* x1;
   int ld0, ld1, c0;
   float* ws;  // packed [cout][K]
+  float* db;  // optional: db[co] += sum_p dY[p][co] (blocks with blockIdx.y == 0)
   int H, W, cin, cout, ks, K;
   long long M;
   int pix_per_split;
@@ -297,6 +298,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs<T> p) {
       for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
 
   const int r = lane & 31, h = lane >> 5;
+  const bool do_bias = p.db != nullptr && blockIdx.y == 0;
+  float bsum[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) bsum[e] = 0.f;
   u32x4 ra[LA], rb[LB];
   auto gload = [&](long long pb) {
 #pragma unroll
@@ -331,6 +336,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs<T> p) {
     for (int i = 0; i < LA; ++i) {
       const int row = tid / VA + (256 / VA) * i;
       *(u32x4*)(sA + row * SA + a_col * (int)sizeof(T)) = ra[i];
+      if (do_bias) {
+        float t[VEC];
+        Vec<T>::to_f(ra[i], t);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) bsum[e] += t[e];
+      }
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
@@ -389,6 +400,21 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs<T> p) {
     }
   }
 
+  if (do_bias) {  // reduce the column sums of the threads sharing a_col
+    float* red = (float*)smem;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) red[tid * VEC + e] = bsum[e];
+    __syncthreads();
+    if (tid < VA && a_cok) {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float t = 0.f;
+        for (int k = 0; k < 256 / VA; ++k) t += red[(tid + k * VA) * VEC + e];
+        if (co0 + a_col + e < p.cout) atomicAdd(p.db + co0 + a_col + e, t);
+      }
+    }
+  }
   // acc[j][i]: row co = (reg&3) + 8*(reg>>2) + 4h, column n' = r
 #pragma unroll
   for (int j = 0; j < TJ; ++j)
@@ -427,16 +453,22 @@ __global__ void pack_weight_kernel(const float* w, T* out, int cout, int cin, in
   }
 }
 
-__global__ void unpack_wgrad_kernel(const float* ws, float* dw, int cout, int cin, int taps,
+// reads the packed workspace [cout][tap][cin] and zeroes it behind itself, so a
+// cached workspace is always zero on entry to the next wgrad (no memset launch)
+__global__ void unpack_wgrad_kernel(float* ws, float* dw, int cout, int cin, int taps,
                                     int cout_real, int cin_real, int accumulate) {
-  long long total = (long long)cout_real * cin_real * taps;
+  long long total = (long long)cout * cin * taps;
   for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
-    int tap = (int)(idx % taps);
-    long long t = idx / taps;
-    int ci = (int)(t % cin_real), co = (int)(t / cin_real);
-    float v = ws[((long long)co * taps + tap) * cin + ci];
-    dw[idx] = accumulate ? dw[idx] + v : v;
+    const int ci = (int)(idx % cin);
+    const long long t = idx / cin;
+    const int tap = (int)(t % taps), co = (int)(t / taps);
+    const float v = ws[idx];
+    ws[idx] = 0.f;
+    if (co < cout_real && ci < cin_real) {
+      float* o = dw + ((long long)co * cin_real + ci) * taps + tap;
+      *o = accumulate ? *o + v : v;
+    }
   }
 }
 
@@ -502,9 +534,10 @@ int launch_wgrad(WgradArgs<T> a, hipStream_t st) {
 
 template <typename T>
 int conv_wgrad_t(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
-                 int ld1, float* ws, int nf, int h, int w, int cin, int cout, int ks,
+                 int ld1, float* ws, float* db, int nf, int h, int w, int cin, int cout, int ks,
                  hipStream_t st) {
   WgradArgs<T> a;
+  a.db = db;
   a.dy = (const T*)dy; a.lddy = lddy; a.x0 = (const T*)x0; a.x1 = (const T*)(x1 ? x1 : x0);
   a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0; a.c0 = x1 ? c0 : cin; a.ws = ws; a.H = h; a.W = w;
   a.cin = cin; a.cout = cout; a.ks = ks; a.K = ks * ks * cin; a.M = (long long)nf * h * w;
@@ -541,25 +574,25 @@ extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const voi
 }
 
 extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0,
-                             int c0, const void* x1, int ld1, float* ws, int nf, int h, int w,
-                             int cin, int cout, int ksize, void* stream) {
+                             int c0, const void* x1, int ld1, float* ws, float* db, int nf, int h,
+                             int w, int cin, int cout, int ksize, void* stream) {
   DV_REQUIRE(dy && x0 && ws, "null pointer");
   DV_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "cin/cout must be multiples of 8");
   DV_REQUIRE(lddy % 8 == 0 && ld0 % 8 == 0 && (!x1 || (ld1 % 8 == 0 && c0 % 8 == 0)),
              "strides must be multiples of 8");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DV_F32)
-    return conv_wgrad_t<float>(dy, lddy, x0, ld0, c0, x1, ld1, ws, nf, h, w, cin, cout, ksize, st);
+    return conv_wgrad_t<float>(dy, lddy, x0, ld0, c0, x1, ld1, ws, db, nf, h, w, cin, cout, ksize, st);
   if (dtype == DV_BF16)
-    return conv_wgrad_t<bf16>(dy, lddy, x0, ld0, c0, x1, ld1, ws, nf, h, w, cin, cout, ksize, st);
+    return conv_wgrad_t<bf16>(dy, lddy, x0, ld0, c0, x1, ld1, ws, db, nf, h, w, cin, cout, ksize, st);
   DV_REQUIRE(false, "unknown dtype");
 }
 
-extern "C" int dv_unpack_wgrad(const float* ws, float* dw, int cout, int cin, int ksize,
+extern "C" int dv_unpack_wgrad(float* ws, float* dw, int cout, int cin, int ksize,
                                int cout_real, int cin_real, int accumulate, void* stream) {
   DV_REQUIRE(ws && dw && cout_real <= cout && cin_real <= cin, "bad arguments");
   const int taps = ksize * ksize;
-  long long total = (long long)cout_real * cin_real * taps;
+  long long total = (long long)cout * cin * taps;
   if (total == 0) return DV_OK;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;

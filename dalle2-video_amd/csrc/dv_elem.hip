@@ -221,7 +221,7 @@ __device__ __forceinline__ float lin_g(const float* dy, int lddy, const float* z
 
 __global__ void linear_small_dw_kernel(const float* dy, int lddy, const float* x, int ldx,
                                        const float* z, float* dW, float* db, int B, int K, int N,
-                                       int act_in, int act_out) {
+                                       int act_in, int act_out, int accumulate) {
   GRID_STRIDE(i, (long long)N * K) {
     const int n = (int)(i / K), k = (int)(i % K);
     float s = 0.f, sb = 0.f;
@@ -230,21 +230,47 @@ __global__ void linear_small_dw_kernel(const float* dy, int lddy, const float* x
       s += g * act_in_f(x[(long long)b * ldx + k], act_in);
       sb += g;
     }
-    dW[i] = s;
-    if (db && k == 0) db[n] = sb;
+    dW[i] = accumulate ? dW[i] + s : s;
+    if (db && k == 0) db[n] = accumulate ? db[n] + sb : sb;
   }
 }
 
-__global__ void linear_small_dx_kernel(const float* dy, int lddy, const float* x, int ldx,
-                                       const float* W, const float* z, float* dx, int lddx, int B,
-                                       int K, int N, int act_in, int act_out, int accumulate) {
-  GRID_STRIDE(i, (long long)B * K) {
-    const int b = (int)(i / K), k = (int)(i % K);
-    float s = 0.f;
-    for (int n = 0; n < N; ++n) s += lin_g(dy, lddy, z, b, n, N, act_out) * W[(long long)n * K + k];
-    s *= act_in_d(x[(long long)b * ldx + k], act_in);
-    float* o = dx + (long long)b * lddx + k;
-    *o = accumulate ? *o + s : s;
+// dx[b][k] (+)= act_in'(x) * sum_n g[b][n] W[n][k]: block = 64 k-columns x 4
+// n-slices, grid.y splits N; partial sums meet in f32 atomics (dx pre-zeroed
+// or accumulated into).  B <= 16.
+__global__ __launch_bounds__(256) void linear_small_dx_kernel(const float* dy, int lddy,
+                                                              const float* x, int ldx,
+                                                              const float* W, const float* z,
+                                                              float* dx, int lddx, int B, int K,
+                                                              int N, int act_in, int act_out,
+                                                              int n_per_block) {
+  constexpr int MAXB = 16;
+  __shared__ float red[4][MAXB][64];
+  const int kl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + kl;
+  const int n0 = blockIdx.y * n_per_block;
+  int n1 = n0 + n_per_block;
+  if (n1 > N) n1 = N;
+  float acc[MAXB];
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b) acc[b] = 0.f;
+  if (k < K) {
+    for (int n = n0 + sl; n < n1; n += 4) {
+      const float w = W[(long long)n * K + k];
+#pragma unroll
+      for (int b = 0; b < MAXB; ++b)
+        if (b < B) acc[b] += lin_g(dy, lddy, z, b, n, N, act_out) * w;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b) red[sl][b][kl] = acc[b];
+  __syncthreads();
+  if (sl == 0 && k < K) {
+    for (int b = 0; b < B; ++b) {
+      const float s = (red[0][b][kl] + red[1][b][kl] + red[2][b][kl] + red[3][b][kl]) *
+                      act_in_d(x[(long long)b * ldx + k], act_in);
+      atomicAdd(dx + (long long)b * lddx + k, s);
+    }
   }
 }
 
@@ -465,11 +491,17 @@ extern "C" int dv_linear_small_fwd(const float* x, int ldx, const float* W, cons
 extern "C" int dv_linear_small_bwd(const float* dy, int lddy, const float* x, int ldx,
                                    const float* W, const float* z, float* dx, int lddx, float* dW,
                                    float* db, int B, int K, int N, int act_in, int act_out,
-                                   int accumulate_dx, void* stream) {
+                                   int accumulate_dx, int accumulate_w, void* stream) {
   DV_REQUIRE(dy && x && W && (act_out != 2 || z), "bad arguments");
   hipStream_t st = (hipStream_t)stream;
-  if (dW) linear_small_dw_kernel<<<grid_for((long long)N * K), 256, 0, st>>>(dy, lddy, x, ldx, z, dW, db, B, K, N, act_in, act_out);
-  if (dx) linear_small_dx_kernel<<<grid_for((long long)B * K), 256, 0, st>>>(dy, lddy, x, ldx, W, z, dx, lddx, B, K, N, act_in, act_out, accumulate_dx);
+  DV_REQUIRE(B <= 16, "linear_small supports B <= 16 rows");
+  if (dW) linear_small_dw_kernel<<<grid_for((long long)N * K), 256, 0, st>>>(dy, lddy, x, ldx, z, dW, db, B, K, N, act_in, act_out, accumulate_w);
+  if (dx) {
+    if (!accumulate_dx) (void)hipMemsetAsync(dx, 0, sizeof(float) * ((long long)(B - 1) * lddx + K), st);
+    const int npb = 64;
+    dim3 grid((K + 63) / 64, (N + npb - 1) / npb);
+    linear_small_dx_kernel<<<grid, 256, 0, st>>>(dy, lddy, x, ldx, W, z, dx, lddx, B, K, N, act_in, act_out, npb);
+  }
   return check_launch("linear_small_bwd");
 }
 

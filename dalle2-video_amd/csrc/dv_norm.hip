@@ -54,6 +54,33 @@ __device__ __forceinline__ void gn_point(const GnArgs& a, int b, int c, float z,
   v = a.ss ? u * (1.f + a.ss[(long long)b * 2 * a.C + c]) + a.ss[(long long)b * 2 * a.C + a.C + c] : u;
 }
 
+// Per-thread fixed channel vector [cv, cv+VEC) of batch b = blockIdx.y; the
+// per-channel affine coefficients are hoisted out of the pixel loop:
+//   v = z*A + B,  zhat = z*rs + zb   (A = rs*g*(1+s), B = (beta - mu*rs*g)(1+s) + sh)
+struct ChanCoef {
+  float A, B, rs, zb, K1;
+};
+template <int VEC>
+__device__ __forceinline__ void load_coef(const GnArgs& a, int b, int cv, ChanCoef* k) {
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int c = cv + e, g = c / (a.C / a.G);
+    const float mu = a.mean[b * a.G + g], rs = a.rstd[b * a.G + g];
+    const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
+    const float sh = a.ss ? a.ss[(long long)b * 2 * a.C + a.C + c] : 0.f;
+    k[e].A = rs * a.gamma[c] * sc;
+    k[e].B = (a.beta[c] - mu * rs * a.gamma[c]) * sc + sh;
+    k[e].rs = rs;
+    k[e].zb = -mu * rs;
+    k[e].K1 = rs * sc * a.gamma[c];
+  }
+}
+
+__device__ __forceinline__ float silu_grad(float v) {
+  const float sg = sigmoid_f(v);
+  return sg * (1.f + v * (1.f - sg));
+}
+
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
@@ -70,6 +97,8 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
 #pragma unroll
   for (int e = 0; e < VEC; ++e) s1[e] = s2[e] = 0.f;
   if (rr < rpp) {
+    ChanCoef k[MODE == 1 ? VEC : 1];
+    if (MODE == 1) load_coef<VEC>(a, b, cv, k);
     for (long long p = beg + rr; p < end; p += rpp) {
       const long long pix = (long long)b * a.P + p;
       float z[VEC];
@@ -82,15 +111,10 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
         ld_vec<T>((const T*)a.dy + pix * a.lddy + cv, dy);
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
-          float zhat, u, v;
-          gn_point<T>(a, b, cv + e, z[e], zhat, u, v);
-          float dv = dy[e];
-          if (a.act == DV_ACT_SILU) {
-            const float sg = sigmoid_f(v);
-            dv *= sg * (1.f + v * (1.f - sg));
-          }
+          const float v = z[e] * k[e].A + k[e].B;
+          const float dv = a.act == DV_ACT_SILU ? dy[e] * silu_grad(v) : dy[e];
           s1[e] += dv;
-          s2[e] += dv * zhat;
+          s2[e] += dv * (z[e] * k[e].rs + k[e].zb);
         }
       }
     }
@@ -103,7 +127,7 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   }
   __syncthreads();
   for (int c = tid; c < a.C; c += 256) {
-    const int owner = c / VEC, e = c % VEC;  // thread index within row 0 owning channel c
+    const int owner = c / VEC, e = c % VEC;
     float t1 = 0.f, t2 = 0.f;
     for (int r = 0; r < rpp; ++r) {
       t1 += sh[0][(r * tpr + owner) * VEC + e];
@@ -133,7 +157,7 @@ __global__ void gn_stats_finalize(const float* ws, float* mean, float* rstd, int
 }
 
 // bwd stage 2: parameter grads and per-(b,g) correction terms
-__global__ void gn_bwd_finalize(GnArgs a, float* dgamma, float* dbeta, float* dss) {
+__global__ void gn_bwd_finalize(GnArgs a, float* dgamma, float* dbeta, float* dss, int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < a.C) {
     float dg = 0.f, db = 0.f;
@@ -147,8 +171,8 @@ __global__ void gn_bwd_finalize(GnArgs a, float* dgamma, float* dbeta, float* ds
         dss[(long long)b * 2 * a.C + a.C + c] = r1;                          // d shift
       }
     }
-    if (dgamma) dgamma[c] = dg;
-    if (dbeta) dbeta[c] = db;
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + dg : dg;
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + db : db;
   }
   if (c < a.nb * a.G) {
     const int b = c / a.G, g = c % a.G, cg = a.C / a.G;
@@ -166,24 +190,36 @@ __global__ void gn_bwd_finalize(GnArgs a, float* dgamma, float* dbeta, float* ds
 }
 
 // MODE 0: forward apply  out = act(v) (+ res)
-// MODE 1: backward apply out = dz
+// MODE 1: backward apply out = dz = rs*(dv*(1+s)*g - m1 - zhat*m2)
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
-  const int vpr = a.C / VEC;
-  const long long total = (long long)a.nb * a.P * vpr;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    const long long pix = idx / vpr;
-    const int cv = (int)(idx - pix * vpr) * VEC;
-    const int b = (int)(pix / a.P);
+  const int tpr = a.C / VEC, rpp = 256 / tpr;
+  const int rr = threadIdx.x / tpr, cv = (threadIdx.x % tpr) * VEC;
+  if (rr >= rpp) return;
+  const int b = blockIdx.y;
+  const long long beg = blockIdx.x * a.rows_per_block;
+  long long end = beg + a.rows_per_block;
+  if (end > a.P) end = a.P;
+  ChanCoef k[VEC];
+  load_coef<VEC>(a, b, cv, k);
+  float m1[VEC], m2[VEC];
+  if (MODE == 1) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const int g = (cv + e) / (a.C / a.G);
+      m1[e] = -k[e].rs * a.ws2[(b * a.G + g) * 2];
+      m2[e] = -k[e].rs * a.ws2[(b * a.G + g) * 2 + 1];
+    }
+  }
+  for (long long p = beg + rr; p < end; p += rpp) {
+    const long long pix = (long long)b * a.P + p;
     float z[VEC], o[VEC];
     ld_vec<T>((const T*)a.z + pix * a.ldz + cv, z);
     if (MODE == 0) {
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        float zhat, u, v;
-        gn_point<T>(a, b, cv + e, z[e], zhat, u, v);
+        const float v = z[e] * k[e].A + k[e].B;
         o[e] = a.act == DV_ACT_SILU ? silu_f(v) : v;
       }
       if (a.res) {
@@ -197,18 +233,10 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
       ld_vec<T>((const T*)a.dy + pix * a.lddy + cv, dy);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        const int c = cv + e, g = c / (a.C / a.G);
-        float zhat, u, v;
-        gn_point<T>(a, b, c, z[e], zhat, u, v);
-        float dv = dy[e];
-        if (a.act == DV_ACT_SILU) {
-          const float sg = sigmoid_f(v);
-          dv *= sg * (1.f + v * (1.f - sg));
-        }
-        const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
-        const float dzhat = dv * sc * a.gamma[c];
-        const float m1 = a.ws2[(b * a.G + g) * 2], m2 = a.ws2[(b * a.G + g) * 2 + 1];
-        o[e] = a.rstd[b * a.G + g] * (dzhat - m1 - zhat * m2);
+        const float v = z[e] * k[e].A + k[e].B;
+        const float dv = a.act == DV_ACT_SILU ? dy[e] * silu_grad(v) : dy[e];
+        const float zhat = z[e] * k[e].rs + k[e].zb;
+        o[e] = dv * k[e].K1 + m1[e] + zhat * m2[e];
       }
     }
     st_vec<T>((T*)a.out + pix * a.ldo + cv, o);
@@ -222,29 +250,42 @@ int grid_for(long long work, int per_block = 256) {
   return (int)b;
 }
 
+// rows per reduce block: >= 8 passes of the row slots, >= ~512 blocks overall
+long long reduce_rows(const GnArgs& a, int vec) {
+  const long long rpp = 256 / (a.C / vec);
+  long long r = (a.P * a.nb + 511) / 512;
+  if (r < rpp * 8) r = rpp * 8;
+  if (r > 2048) r = 2048;
+  return (r + rpp - 1) / rpp * rpp;
+}
+
 template <typename T>
 int gn_fwd_t(GnArgs a, float eps, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
-  a.rows_per_block = 1024;
+  a.rows_per_block = reduce_rows(a, VEC);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   (void)hipMemsetAsync(a.ws, 0, sizeof(float) * a.nb * a.C * 2, st);
   gn_reduce_kernel<T, 0><<<g1, 256, 0, st>>>(a);
   gn_stats_finalize<<<(a.nb * a.G + 63) / 64, 64, 0, st>>>(a.ws, (float*)a.mean, (float*)a.rstd,
                                                           a.nb, a.P, a.C, a.G, eps);
-  gn_apply_kernel<T, 0><<<grid_for((long long)a.nb * a.P * (a.C / VEC)), 256, 0, st>>>(a);
+  a.rows_per_block = 256 / (a.C / VEC) * 16;  // 16 passes of the row slots per block
+  dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
+  gn_apply_kernel<T, 0><<<g2, 256, 0, st>>>(a);
   return check_launch("gn_fwd");
 }
 
 template <typename T>
-int gn_bwd_t(GnArgs a, float* dgamma, float* dbeta, float* dss, hipStream_t st) {
+int gn_bwd_t(GnArgs a, float* dgamma, float* dbeta, float* dss, int accumulate, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
-  a.rows_per_block = 1024;
+  a.rows_per_block = reduce_rows(a, VEC);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   (void)hipMemsetAsync(a.ws, 0, sizeof(float) * a.nb * a.C * 2, st);
   gn_reduce_kernel<T, 1><<<g1, 256, 0, st>>>(a);
   int n2 = a.C > a.nb * a.G ? a.C : a.nb * a.G;
-  gn_bwd_finalize<<<(n2 + 63) / 64, 64, 0, st>>>(a, dgamma, dbeta, dss);
-  gn_apply_kernel<T, 1><<<grid_for((long long)a.nb * a.P * (a.C / VEC)), 256, 0, st>>>(a);
+  gn_bwd_finalize<<<(n2 + 63) / 64, 64, 0, st>>>(a, dgamma, dbeta, dss, accumulate);
+  a.rows_per_block = 256 / (a.C / VEC) * 16;
+  dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
+  gn_apply_kernel<T, 1><<<g2, 256, 0, st>>>(a);
   return check_launch("gn_bwd");
 }
 
@@ -383,7 +424,7 @@ extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int
                          int lddz, int nb, long long P, int C, int G, const float* gamma,
                          const float* beta, const float* ss, int act, const float* mean,
                          const float* rstd, float* dgamma, float* dbeta, float* dss, float* ws,
-                         void* stream) {
+                         int accumulate, void* stream) {
   DV_REQUIRE(dy && z && dz && gamma && beta && mean && rstd && ws, "null pointer");
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && lddy % VEC == 0 && lddz % VEC == 0,
@@ -395,8 +436,8 @@ extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int
   a.act = act; a.ws = ws; a.ws2 = ws + (long long)nb * C * 2;
   if (nb == 0 || P == 0) return DV_OK;
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DV_BF16 ? gn_bwd_t<bf16>(a, dgamma, dbeta, dss, st)
-                          : gn_bwd_t<float>(a, dgamma, dbeta, dss, st);
+  return dtype == DV_BF16 ? gn_bwd_t<bf16>(a, dgamma, dbeta, dss, accumulate, st)
+                          : gn_bwd_t<float>(a, dgamma, dbeta, dss, accumulate, st);
 }
 
 extern "C" int dv_ln_fwd(int dtype, const void* x, int ldx, void* y, int ldy, const void* res,

@@ -272,7 +272,7 @@ __global__ void fold_grad_finish_kernel(const float* ws_a, const float* ws_v, co
 // parameter grads of the fold: dWq, dWo and dK/dV -> d(kv) and d(null_kv)
 __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const float* kv,
                                   const float* null_kv, float* dwq, float* dwo, int nb, int C,
-                                  float scale) {
+                                  float scale, int accumulate) {
   const long long n = (long long)NH * DH * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -284,7 +284,7 @@ __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const floa
       for (int b = 0; b < nb; ++b)
         for (int j = 0; j < NK; ++j)
           s += dat[((long long)b * C + c) * HK + h * NK + j] * kf(kv, null_kv, b, h, j, d, 0);
-      dwq[i] = s * scale;
+      dwq[i] = accumulate ? dwq[i] + s * scale : s * scale;
     }
     // dWo[c][hd]   (i = c*512 + hd)
     {
@@ -294,7 +294,7 @@ __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const floa
       for (int b = 0; b < nb; ++b)
         for (int j = 0; j < NK; ++j)
           s += dvt[((long long)b * C + c) * HK + h * NK + j] * kf(kv, null_kv, b, h, j, d, 1);
-      dwo[i] = s;
+      dwo[i] = accumulate ? dwo[i] + s : s;
     }
   }
 }
@@ -371,14 +371,14 @@ extern "C" int dv_xattn_fold_bwd(const float* ws_a, const float* ws_v, const flo
                                  const float* mcorr, const float* wq, const float* wo,
                                  const float* kv, const float* null_kv, float* dat, float* dvt,
                                  float* dwq, float* dwo, float* dkv, float* dnull, int nb, int C,
-                                 float scale, void* stream) {
+                                 float scale, int accumulate, void* stream) {
   DV_REQUIRE(ws_a && ws_v && g1 && mcorr && wq && wo && kv && null_kv && dat && dvt && dwq && dwo && dkv && dnull,
              "null pointer");
   hipStream_t st = (hipStream_t)stream;
   const long long n = (long long)nb * C * HK;
   fold_grad_finish_kernel<<<grid_for(n), 256, 0, st>>>(ws_a, ws_v, g1, mcorr, dat, dvt, nb, C);
-  fold_bwd_w_kernel<<<grid_for((long long)NH * DH * C), 256, 0, st>>>(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale);
-  (void)hipMemsetAsync(dnull, 0, sizeof(float) * 2 * DH, st);
+  fold_bwd_w_kernel<<<grid_for((long long)NH * DH * C), 256, 0, st>>>(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale, accumulate);
+  if (!accumulate) (void)hipMemsetAsync(dnull, 0, sizeof(float) * 2 * DH, st);
   fold_bwd_kv_kernel<<<(nb * NH * NK * DH + 255) / 256, 256, 0, st>>>(dat, dvt, wq, wo, dkv, dnull, nb, C, scale);
   return check_launch("xattn_fold_bwd");
 }

@@ -26,12 +26,12 @@ _F = ctypes.c_float
 _SIGS = {
     "dv_abi_version": [],
     "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
-    "dv_conv_wgrad": [_I, _P, _I, _P, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_conv_wgrad": [_I, _P, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_unpack_wgrad": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
     "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "dv_gn_fwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P],
-    "dv_gn_bwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P],
+    "dv_gn_bwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P],
     "dv_ln_fwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _P, _F, _P, _P, _P],
     "dv_ln_bwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _F, _P, _P, _P],
     "dv_ncthw_to_cl": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
@@ -42,19 +42,19 @@ _SIGS = {
     "dv_mse_loss_bwd": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
     "dv_sinusoidal": [_P, _P, _P, _I, _I, _P],
     "dv_linear_small_fwd": [_P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
-    "dv_linear_small_bwd": [_P, _I, _P, _I, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_linear_small_bwd": [_P, _I, _P, _I, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_adamw": [_P, _P, _P, _P, _L, _L, _F, _F, _F, _F, _F, _F, _F, _P, _P],
     "dv_grad_clip_coef": [_P, _L, _F, _F, _P, _P],
     "dv_p_sample": [_I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_xattn_fold": [_P, _P, _P, _P, _P, _P, _I, _I, _F, _P],
     "dv_xattn_fwd": [_I, _P, _I, _P, _I, _L, _L, _I, _P, _P, _P, _P, _F, _P, _P, _P],
     "dv_xattn_bwd_tokens": [_I, _P, _I, _P, _I, _P, _I, _L, _L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
-    "dv_xattn_fold_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P],
+    "dv_xattn_fold_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _P],
     "dv_resize_nearest": [_P, _P, _L, _I, _I, _I, _I, _I, _F, _F, _P],
     "dv_gaussian_blur": [_P, _P, _L, _I, _I, _I, _P, _P],
     "dv_mqa_prep": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _P],
     "dv_mqa_fwd": [_I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _F, _P],
-    "dv_mqa_bwd": [_I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _F, _P],
+    "dv_mqa_bwd": [_I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _F, _I, _P],
 }
 
 

@@ -74,6 +74,32 @@ def cl_ld(t: torch.Tensor) -> int:
     return ld
 
 
+def _grad_out(p, zero=False):
+    """In-place gradient target for a leaf parameter: (buffer, accumulate).
+
+    Backward kernels write a parameter's gradient straight into `p.grad`
+    (the trainer's flat-buffer view) and the autograd Function returns None
+    for it, so no AccumulateGrad add runs.  Returns None when `p` is not a
+    leaf that requires grad (the Function then returns the gradient)."""
+    if p is None or not (p.requires_grad and p.is_leaf) or p.dtype != torch.float32:
+        return None
+    if p.grad is None:
+        p.grad = (torch.zeros_like if zero else torch.empty_like)(p)
+        return p.grad, False
+    return p.grad, True
+
+
+_WS = {}
+
+
+def _wgrad_workspace(cout, taps, cin, device):
+    """Cached packed wgrad workspace; dv_unpack_wgrad zeroes it after use."""
+    key = (cout, taps, cin, str(device))
+    if key not in _WS:
+        _WS[key] = torch.zeros(cout, taps, cin, dtype=torch.float32, device=device)
+    return _WS[key]
+
+
 def _pad_channels(t: torch.Tensor, mult: int = 8) -> torch.Tensor:
     c = t.shape[-1]
     cp = (c + mult - 1) // mult * mult
@@ -125,6 +151,7 @@ class ConvFn(torch.autograd.Function):
                 lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b), ptr(res),
                              ldr, ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE, stream()))
         ctx.save_for_backward(x0, x1, weight)
+        ctx.params = (weight, bias)
         ctx.meta = (ksize, c0, c1, bias is not None, res is not None)
         return y
 
@@ -150,20 +177,40 @@ class ConvFn(torch.autograd.Function):
                                  ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE, stream()))
             dx0 = dx[..., :c0]
             dx1 = dx[..., c0:] if x1 is not None else None
+        wparam, bparam = ctx.params
+        want_b = has_bias and ctx.needs_input_grad[3]
+        # bias gradient target: the parameter's .grad in place when possible
+        bslot = _grad_out(bparam, zero=True) if want_b else None
+        if want_b and (bslot is None or cout8 != cout):
+            db_buf = torch.zeros(cout8, dtype=torch.float32, device=dy.device)
+        else:
+            db_buf = bslot[0] if bslot else None
         if ctx.needs_input_grad[2]:
-            ws = torch.zeros(cout8, ksize * ksize, cin, dtype=torch.float32, device=dy.device)
+            taps = ksize * ksize
+            wslot = _grad_out(wparam, zero=True)
+            direct = wslot is not None and taps == 1 and cout8 == cout and cin_real == cin
+            ws = wslot[0] if direct else _wgrad_workspace(cout8, taps, cin, dy.device)
             ld0 = cl_ld(x0)
             ld1 = cl_ld(x1) if x1 is not None else 0
             m = nf * h * w
             _launch(f"conv_wgrad_kernel<{_lib.dtype_name(dy8)}>", 2.0 * m * cout8 * cin * ksize * ksize,
                     dy8.element_size() * m * (cin + cout8),
                     lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), cout8, ptr(x0), ld0, c0, ptr(x1), ld1,
-                                 ptr(ws), nf, h, w, cin, cout8, ksize, stream()))
-            dw = torch.empty(weight.shape, dtype=torch.float32, device=dy.device)
-            call("dv_unpack_wgrad", ptr(ws), ptr(dw), cout8, cin, ksize, cout, cin_real, 0, stream())
-        if has_bias and ctx.needs_input_grad[3]:
-            db = torch.zeros(cout, dtype=torch.float32, device=dy.device)
-            call("dv_bias_grad", dt(dy8), ptr(dy8), cout8, ptr(db), nf * h * w, cout, stream())
+                                 ptr(ws), ptr(db_buf), nf, h, w, cin, cout8, ksize, stream()))
+            if not direct:
+                if wslot is not None:
+                    call("dv_unpack_wgrad", ptr(ws), ptr(wslot[0]), cout8, cin, ksize, cout, cin_real,
+                         int(wslot[1]), stream())
+                else:
+                    dw = torch.empty(weight.shape, dtype=torch.float32, device=dy.device)
+                    call("dv_unpack_wgrad", ptr(ws), ptr(dw), cout8, cin, ksize, cout, cin_real, 0, stream())
+        elif want_b:
+            call("dv_bias_grad", dt(dy8), ptr(dy8), cout8, ptr(db_buf), nf * h * w, cout, stream())
+        if want_b:
+            if bslot is None:
+                db = db_buf[:cout]
+            elif db_buf is not bslot[0]:
+                bslot[0].add_(db_buf[:cout])
         dres = dy if has_res else None
         return dx0, dx1, dw, db, dres, None
 
@@ -195,6 +242,7 @@ class GroupNormActFn(torch.autograd.Function):
              nb, P, c, groups, ctypes_float(eps), ptr(g), ptr(b), ptr(s), act, ptr(mean), ptr(rstd),
              ptr(ws), stream())
         ctx.save_for_backward(z, g, b, s, mean, rstd)
+        ctx.params = (gamma, beta)
         ctx.meta = (nb, groups, act, ss is not None, res is not None)
         return y
 
@@ -207,12 +255,21 @@ class GroupNormActFn(torch.autograd.Function):
         dev = z.device
         dy = dy.contiguous()
         dz = torch.empty(nf, h, w, c, dtype=z.dtype, device=dev)
-        dg = torch.empty(c, dtype=torch.float32, device=dev)
-        db = torch.empty(c, dtype=torch.float32, device=dev)
+        gs, bs = _grad_out(ctx.params[0]), _grad_out(ctx.params[1])
+        # one accumulate flag for both: allocate fresh buffers where they differ
+        if gs is not None and bs is not None and gs[1] == bs[1]:
+            dg, db, acc, ret = gs[0], bs[0], int(gs[1]), False
+        else:
+            dg = torch.empty(c, dtype=torch.float32, device=dev)
+            db = torch.empty(c, dtype=torch.float32, device=dev)
+            acc, ret = 0, True
         dss = torch.empty(nb, 2 * c, dtype=torch.float32, device=dev) if has_ss else None
         ws = torch.empty(nb * c * 2 + nb * groups * 2, dtype=torch.float32, device=dev)
         call("dv_gn_bwd", dt(z), ptr(dy), c, ptr(z), cl_ld(z), ptr(dz), c, nb, P, c, groups, ptr(g),
-             ptr(b), ptr(s), act, ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(ws), stream())
+             ptr(b), ptr(s), act, ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(ws), acc,
+             stream())
+        if not ret:
+            dg = db = None
         return dz, dg, db, dss, (dy if has_res else None), None, None, None, None
 
 
@@ -243,6 +300,7 @@ class LayerNormFn(torch.autograd.Function):
         call("dv_ln_fwd", dt(xc), ptr(xc), c, ptr(y), c, ptr(rc), c, rows, c, ptr(gf), ptr(bf),
              ctypes_float(eps), None, None, stream())
         ctx.save_for_backward(xc, gf)
+        ctx.params = (g, b)
         ctx.meta = (eps, b is not None, res is not None)
         return y
 
@@ -254,11 +312,14 @@ class LayerNormFn(torch.autograd.Function):
         rows = xc.numel() // c
         dy = dy.contiguous()
         dx = torch.empty_like(xc)
-        dg = torch.zeros(c, dtype=torch.float32, device=xc.device)
-        db = torch.zeros(c, dtype=torch.float32, device=xc.device) if has_b else None
+        # dg/db are accumulated with atomics: in place into .grad (zeroed if fresh)
+        gs = _grad_out(ctx.params[0], zero=True)
+        bs = _grad_out(ctx.params[1], zero=True) if has_b else None
+        dg = gs[0] if gs else torch.zeros(c, dtype=torch.float32, device=xc.device)
+        db = (bs[0] if bs else torch.zeros(c, dtype=torch.float32, device=xc.device)) if has_b else None
         call("dv_ln_bwd", dt(xc), ptr(dy), c, ptr(xc), c, ptr(dx), c, rows, c, ptr(gf),
              ctypes_float(eps), ptr(dg), ptr(db), stream())
-        return dx, dg, db, (dy if has_res else None), None
+        return dx, (None if gs else dg), (None if bs else db), (dy if has_res else None), None
 
 
 def layer_norm(x, g, b=None, res=None, eps=1e-5):
@@ -285,6 +346,7 @@ class LinearSmallFn(torch.autograd.Function):
         call("dv_linear_small_fwd", ptr(xc), K, ptr(wc), ptr(bc), ptr(y), N, ptr(z), B, K, N,
              act_in, act_out, stream())
         ctx.save_for_backward(xc, wc, z)
+        ctx.params = (w, b)
         ctx.meta = (act_in, act_out, b is not None)
         return y
 
@@ -294,16 +356,21 @@ class LinearSmallFn(torch.autograd.Function):
         act_in, act_out, has_b = ctx.meta
         B, K = xc.shape
         N = wc.shape[0]
+        dev = dy.device
         dy = dy.float().contiguous()
-        dx = torch.empty(B, K, dtype=torch.float32, device=dy.device) if ctx.needs_input_grad[0] else None
-        dw = torch.empty(N, K, dtype=torch.float32, device=dy.device) if ctx.needs_input_grad[1] else None
-        db = torch.empty(N, dtype=torch.float32, device=dy.device) if has_b and ctx.needs_input_grad[2] else None
-        if dw is None and db is not None:
-            dw_tmp = torch.empty(N, K, dtype=torch.float32, device=dy.device)
+        dx = torch.empty(B, K, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
+        ws = _grad_out(ctx.params[0]) if ctx.needs_input_grad[1] else None
+        bs = _grad_out(ctx.params[1]) if has_b and ctx.needs_input_grad[2] else None
+        if ws is not None and (not has_b or (bs is not None and bs[1] == ws[1])):
+            dw, db, acc, ret = ws[0], (bs[0] if bs else None), int(ws[1]), False
         else:
-            dw_tmp = dw
+            dw = torch.empty(N, K, dtype=torch.float32, device=dev)
+            db = torch.empty(N, dtype=torch.float32, device=dev) if has_b else None
+            acc, ret = 0, True
         call("dv_linear_small_bwd", ptr(dy), N, ptr(xc), K, ptr(wc), ptr(z), ptr(dx), K,
-             ptr(dw_tmp), ptr(db), B, K, N, act_in, act_out, 0, stream())
+             ptr(dw), ptr(db), B, K, N, act_in, act_out, 0, acc, stream())
+        if not ret:
+            dw = db = None
         return dx, dw, db, None, None
 
 
@@ -368,12 +435,14 @@ class CrossAttnFn(torch.autograd.Function):
         call("dv_xattn_fwd", dt(x), ptr(x), cl_ld(x), ptr(out), C, ntok, P, C, ptr(g1f), ptr(g2f),
              ptr(at), ptr(vt), ctypes_float(eps), ptr(stats), ptr(pbuf), stream())
         ctx.save_for_backward(x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, stats, pbuf)
+        ctx.params = (g1, null_kv, wq, wkv, wo, g2)
         ctx.meta = (nb, eps, context.shape)
         return out
 
     @staticmethod
     def backward(ctx, dy):
         x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, stats, pbuf = ctx.saved_tensors
+        g1p, nullp, wqp, wkvp, wop, g2p = ctx.params
         nb, eps, cshape = ctx.meta
         nf, h, w, C = x.shape
         ntok = nf * h * w
@@ -383,40 +452,50 @@ class CrossAttnFn(torch.autograd.Function):
         dx = torch.empty(nf, h, w, C, dtype=x.dtype, device=dev)
         dobuf = torch.empty(ntok, C, dtype=x.dtype, device=dev)
         dsbuf = torch.empty(ntok, 32, dtype=x.dtype, device=dev)
-        dg1 = torch.zeros(C, dtype=torch.float32, device=dev)
-        dg2 = torch.zeros(C, dtype=torch.float32, device=dev)
+        s1, s2 = _grad_out(g1p, zero=True), _grad_out(g2p, zero=True)
+        dg1 = s1[0] if s1 else torch.zeros(C, dtype=torch.float32, device=dev)
+        dg2 = s2[0] if s2 else torch.zeros(C, dtype=torch.float32, device=dev)
         mcorr = torch.zeros(nb, 24, dtype=torch.float32, device=dev)
         ldx = cl_ld(x)
         call("dv_xattn_bwd_tokens", dt(x), ptr(dy), C, ptr(x), ldx, ptr(dx), C, ntok, P, C,
              ptr(g1f), ptr(g2f), ptr(at), ptr(vt), ptr(stats), ptr(pbuf), ptr(dobuf), ptr(dsbuf),
              ptr(dg1), ptr(dg2), ptr(mcorr), stream())
         # per-batch token reductions on the MFMA wgrad GEMM
-        ws_a = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
-        ws_v = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
+        ws_a = _wgrad_workspace(nb * 32, 1, C, dev)
+        ws_v = _wgrad_workspace(nb * 32 + 1, 1, C, dev)  # distinct cache entry
         esz = x.element_size()
         for bi in range(nb):
             xb = x.data_ptr() + bi * P * ldx * esz
             call("dv_conv_wgrad", dt(x), ctypes_vp(dsbuf.data_ptr() + bi * P * 32 * esz), 32,
-                 ctypes_vp(xb), ldx, C, None, 0, ctypes_vp(ws_a.data_ptr() + bi * 32 * C * 4),
+                 ctypes_vp(xb), ldx, C, None, 0, ctypes_vp(ws_a.data_ptr() + bi * 32 * C * 4), None,
                  1, 1, P, C, 32, 1, stream())
             call("dv_conv_wgrad", dt(x), ctypes_vp(pbuf.data_ptr() + bi * P * 32 * esz), 32,
                  ctypes_vp(dobuf.data_ptr() + bi * P * C * esz), C, C, None, 0,
-                 ctypes_vp(ws_v.data_ptr() + bi * 32 * C * 4), 1, 1, P, C, 32, 1, stream())
+                 ctypes_vp(ws_v.data_ptr() + bi * 32 * C * 4), None, 1, 1, P, C, 32, 1, stream())
         dat = torch.empty(nb, C, 24, dtype=torch.float32, device=dev)
         dvt = torch.empty_like(dat)
-        dwq = torch.empty_like(wqf)
-        dwo = torch.empty_like(wof)
+        sq, so, sn = _grad_out(wqp), _grad_out(wop), _grad_out(nullp)
+        direct = sq is not None and so is not None and sn is not None and sq[1] == so[1] == sn[1]
+        if direct:
+            dwq, dwo, dnull, acc = sq[0], so[0], sn[0], int(sq[1])
+        else:
+            dwq, dwo, dnull, acc = torch.empty_like(wqf), torch.empty_like(wof), torch.empty_like(nkv), 0
         dkv = torch.empty_like(kv)
-        dnull = torch.empty_like(nkv)
         call("dv_xattn_fold_bwd", ptr(ws_a), ptr(ws_v), ptr(g1f), ptr(mcorr), ptr(wqf), ptr(wof),
              ptr(kv), ptr(nkv), ptr(dat), ptr(dvt), ptr(dwq), ptr(dwo), ptr(dkv), ptr(dnull), nb, C,
-             ctypes_float(XA_DH ** -0.5), stream())
+             ctypes_float(XA_DH ** -0.5), acc, stream())
+        # the workspaces are cached: re-zero them (dv_unpack_wgrad is not used here)
+        ws_a.zero_()
+        ws_v.zero_()
         dctx = torch.empty_like(ctxf)
-        dwkv = torch.empty_like(wkvf)
+        sk = _grad_out(wkvp)
+        dwkv = sk[0] if sk else torch.empty_like(wkvf)
         call("dv_linear_small_bwd", ptr(dkv), dkv.shape[1], ptr(ctxf), ctxf.shape[1], ptr(wkvf), None,
              ptr(dctx), ctxf.shape[1], ptr(dwkv), None, ctxf.shape[0], ctxf.shape[1], dkv.shape[1],
-             0, 0, 0, stream())
-        return dx, dctx.reshape(cshape), dg1, dnull, dwq, dwkv, dwo, dg2, None, None
+             0, 0, 0, int(sk[1]) if sk else 0, stream())
+        return (dx, dctx.reshape(cshape), None if s1 else dg1, None if direct else dnull,
+                None if direct else dwq, None if sk else dwkv, None if direct else dwo,
+                None if s2 else dg2, None, None)
 
 
 def ctypes_vp(addr):
@@ -450,6 +529,7 @@ class MQAFn(torch.autograd.Function):
         call("dv_mqa_fwd", dt(q), ptr(qc), qc.shape[-1], ptr(kp), ptr(vp), ptr(o), o.shape[-1], ptr(lse),
              B, N, NKP, H, ctypes_float(scale), stream())
         ctx.save_for_backward(qc, kp, vp, o, lse)
+        ctx.params = (null_kv,)
         ctx.meta = (B, N, H, NKP, scale, kvc.shape[-1])
         return o
 
@@ -464,11 +544,13 @@ class MQAFn(torch.autograd.Function):
         dkp = torch.empty(B, NKP, MQA_DH, dtype=torch.float32, device=dev)
         dvp = torch.empty_like(dkp)
         dkv = torch.empty(B * N, 2 * MQA_DH, dtype=qc.dtype, device=dev)
-        dnull = torch.empty(2, MQA_DH, dtype=torch.float32, device=dev)
+        sn = _grad_out(ctx.params[0])
+        dnull = sn[0] if sn else torch.empty(2, MQA_DH, dtype=torch.float32, device=dev)
         call("dv_mqa_bwd", dt(qc), ptr(qc), qc.shape[-1], ptr(o), o.shape[-1], ptr(do), do.shape[-1],
              ptr(lse), ptr(kp), ptr(vp), ptr(dq), dq.shape[-1], ptr(D), ptr(dkp), ptr(dvp), ptr(dkv),
-             dkv.shape[-1], ptr(dnull), B, N, NKP, H, ctypes_float(scale), stream())
-        return dq, dkv, dnull, None, None, None, None
+             dkv.shape[-1], ptr(dnull), B, N, NKP, H, ctypes_float(scale), int(sn[1]) if sn else 0,
+             stream())
+        return dq, dkv, (None if sn else dnull), None, None, None, None
 
 
 def mqa(q, kv, null_kv, B, N, H, scale):

@@ -51,14 +51,17 @@ int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const void* x1, int 
                 int act, void* stream);
 
 /* ws[co][tap][ci] += sum_pixels dY[p][co] * X[p + tap][ci]: f32 atomics into a
- * caller-zeroed packed workspace (cout*k*k*cin floats); split-K over pixels.
+ * zeroed packed workspace (cout*k*k*cin floats; for k=1 this IS the torch
+ * layout, so ws may be the parameter's gradient); split-K over pixels.
+ * db (optional): db[co] += sum_p dY[p][co] — the conv bias gradient, fused.
  * cin, cout multiples of 8 (pad and mask with dv_unpack_wgrad).            */
 int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0, int c0,
-                  const void* x1, int ld1, float* ws, int nf, int h, int w, int cin,
+                  const void* x1, int ld1, float* ws, float* db, int nf, int h, int w, int cin,
                   int cout, int ksize, void* stream);
 
-/* dw (torch layout (cout_real, cin_real, 1, k, k)) (+)= ws[co][tap][ci]      */
-int dv_unpack_wgrad(const float* ws, float* dw, int cout, int cin, int ksize, int cout_real,
+/* dw (torch layout (cout_real, cin_real, 1, k, k)) (+)= ws[co][tap][ci]; zeroes
+ * ws behind itself so a cached workspace needs no memset before reuse.       */
+int dv_unpack_wgrad(float* ws, float* dw, int cout, int cin, int ksize, int cout_real,
                     int cin_real, int accumulate, void* stream);
 
 /* db[c] += sum_p dy[p][c]  (f32 atomics) */
