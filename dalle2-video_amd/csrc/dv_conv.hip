@@ -249,6 +249,10 @@ struct WgradArgs {
   int H, W, cin, cout, ks, K;
   long long M;
   int pix_per_split;
+  // batched mode (1x1 only): pixels form nbatch groups of batch_pix; each
+  // group reduces into its own ws + g*ws_bstride (splits never straddle groups)
+  long long batch_pix, ws_bstride;
+  int splits_per_batch;
 };
 
 // transposed 4x16 bf16 block read (gfx950 ds_read_b64_tr_b16)
@@ -274,9 +278,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs<T> p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int co0 = blockIdx.x * BMC, nk0 = blockIdx.y * BNK;
-  const long long pbeg = (long long)blockIdx.z * p.pix_per_split;
-  long long pend = pbeg + p.pix_per_split;
-  if (pend > p.M) pend = p.M;
+  long long pbeg, pend;
+  float* wsb = p.ws;
+  if (p.batch_pix > 0) {
+    const int bi = blockIdx.z / p.splits_per_batch, lz = blockIdx.z % p.splits_per_batch;
+    pbeg = bi * p.batch_pix + (long long)lz * p.pix_per_split;
+    pend = pbeg + p.pix_per_split;
+    if (pend > (bi + 1) * p.batch_pix) pend = (bi + 1) * p.batch_pix;
+    wsb = p.ws + bi * p.ws_bstride;
+  } else {
+    pbeg = (long long)blockIdx.z * p.pix_per_split;
+    pend = pbeg + p.pix_per_split;
+    if (pend > p.M) pend = p.M;
+  }
   const int HW = p.H * p.W, pad = p.ks >> 1;
 
   // fixed column per thread for A (co) and B (tap, ci)
@@ -425,7 +439,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs<T> p) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int co = co0 + wm * 32 * TJ + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (co < p.cout) atomicAdd(p.ws + (long long)co * p.K + n, acc[j][i][e]);
+        if (co < p.cout) atomicAdd(wsb + (long long)co * p.K + n, acc[j][i][e]);
       }
     }
 }
@@ -525,8 +539,17 @@ int launch_wgrad(WgradArgs<T> a, hipStream_t st) {
   long long per = (a.M + want - 1) / want;
   per = ((per + 255) / 256) * 256;
   if (per < 256) per = 256;
+  unsigned splits;
+  if (a.batch_pix > 0) {
+    const long long nbatch = a.M / a.batch_pix;
+    long long spb = (a.batch_pix + per - 1) / per;
+    per = (a.batch_pix + spb - 1) / spb;
+    a.splits_per_batch = (int)spb;
+    splits = (unsigned)(nbatch * spb);
+  } else {
+    splits = (unsigned)((a.M + per - 1) / per);
+  }
   a.pix_per_split = (int)per;
-  const unsigned splits = (unsigned)((a.M + per - 1) / per);
   dim3 grid(mt, nt, splits);
   conv_wgrad_kernel<T, BMC, BNK><<<grid, 256, 0, st>>>(a);
   return check_launch("conv_wgrad");
@@ -535,13 +558,16 @@ int launch_wgrad(WgradArgs<T> a, hipStream_t st) {
 template <typename T>
 int conv_wgrad_t(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
                  int ld1, float* ws, float* db, int nf, int h, int w, int cin, int cout, int ks,
-                 hipStream_t st) {
+                 hipStream_t st, long long batch_pix = 0) {
   WgradArgs<T> a;
   a.db = db;
   a.dy = (const T*)dy; a.lddy = lddy; a.x0 = (const T*)x0; a.x1 = (const T*)(x1 ? x1 : x0);
   a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0; a.c0 = x1 ? c0 : cin; a.ws = ws; a.H = h; a.W = w;
   a.cin = cin; a.cout = cout; a.ks = ks; a.K = ks * ks * cin; a.M = (long long)nf * h * w;
   a.pix_per_split = 0;
+  a.batch_pix = batch_pix;
+  a.ws_bstride = (long long)cout * a.K;
+  a.splits_per_batch = 1;
   if (a.M == 0) return DV_OK;
   const bool small_co = cout <= 64;
   const bool small_k = a.K <= 64;
@@ -629,4 +655,20 @@ extern "C" int dv_pack_conv_weight(int dtype, const float* w, void* out, int cou
   else
     pack_weight_kernel<bf16><<<blocks, 256, 0, st>>>(w, (bf16*)out, cout, cin, taps, pad_to, mode);
   return check_launch("pack_conv_weight");
+}
+
+extern "C" int dv_gemm_tn_batched(int dtype, const void* a, int lda, const void* b, int ldb,
+                                  float* out, long long batch_rows, int nbatch, int m, int n,
+                                  void* stream) {
+  // out[g][i][j] += sum_{r in group g} A[r][i] * B[r][j]  (A: rows x m, B: rows x n)
+  DV_REQUIRE(a && b && out && m % 8 == 0 && n % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0,
+             "m, n and strides must be multiples of 8");
+  if (nbatch <= 0 || batch_rows <= 0) return DV_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int W = (int)(batch_rows * nbatch);
+  if (dtype == DV_F32)
+    return conv_wgrad_t<float>(a, lda, b, ldb, n, nullptr, 0, out, nullptr, 1, 1, W, n, m, 1, st, batch_rows);
+  if (dtype == DV_BF16)
+    return conv_wgrad_t<bf16>(a, lda, b, ldb, n, nullptr, 0, out, nullptr, 1, 1, W, n, m, 1, st, batch_rows);
+  DV_REQUIRE(false, "unknown dtype");
 }

@@ -1,12 +1,23 @@
-// CLIP-style cross attention of ResnetBlock3D (dalle2_video.py:159-162,
-// 192-201; dalle2-pytorch CrossAttention, 8 heads x 64, null k/v prepended,
-// logit factor 64^-0.5).  Each head attends over only 3 keys (null + 2 time
-// tokens), so the projections fold per batch b:
-//   A~[b][c][h*3+j] = s * sum_d Wq[h*64+d][c] K[b][h][j][d]      (scores = hn . A~)
-//   V~[b][c][h*3+j] =     sum_d Wo[c][h*64+d] V[b][h][j][d]      (o = V~ p)
-// A token then costs 2*24*C MACs instead of 2*512*C: the whole block
-//   out = LN_g2(V~ softmax(LN_g1(x) A~)) + x
-// is one HBM pass (read x, write out) in `xattn_fwd_kernel`.
+// CLIP-style cross attention of ResnetBlock3D (dalle2_video.py:159-162, 192-201;
+// dalle2-pytorch CrossAttention: 8 heads x 64, a learned null k/v prepended to
+// the 2 time tokens -> 3 keys per head, logit factor 64^-0.5, gain-only
+// LayerNorms before (g1) and after (g2) the block, residual add).
+//
+// MI355X design.  With only 3 keys per head, the q/out projections fold per
+// batch b into two C x 24 matrices (computed once per call, f32):
+//   A~[c][hj] = s * sum_d Wq[h*64+d][c] K[b,h,j,d]     scores = LN(x) . A~
+//   V~[c][hj] =     sum_d Wo[c][h*64+d] V[b,h,j,d]     o      = V~ p
+// Heads are padded to 4 rows (k' = 4h + j, j = 3 dummy) so that in a 32x32
+// MFMA accumulator every lane owns whole heads (softmax is lane-local).
+// Per wave = 32 tokens of one batch:
+//   S^T = Kt . X^T      Kt[k'][c] = g1[c] A~[c][hj]; raw x is the MFMA
+//                       operand, LN_in (mean/rstd from the same pass) is
+//                       applied algebraically: s = rs*(S^T - mu*colsum(Kt))
+//   O^T = Vt . P^T      P^T accumulator reused as the MFMA B operand
+//   out = LN_g2(o) + x  (o recomputed per 32-channel tile; 2 passes)
+// Backward: dP^T = Vt^T dO^T, dXhat^T = KtT dS^T on MFMA; the LN_in sums are
+// analytic (sum dxhat = ds.colsum, sum dxhat*xhat = ds.log p); the token
+// reductions dKt, dV~ and dg2 are batched TN GEMMs (dv_gemm_tn_batched).
 #include "dv_common.h"
 
 using namespace dv;
@@ -14,13 +25,78 @@ using namespace dv;
 namespace {
 
 constexpr int NH = 8, DH = 64, NK = 3, HK = NH * NK;  // 24 folded columns
-constexpr int PPAD = 32;                                // padded P / dS row
+constexpr int KP = 32;                                  // padded k' rows
+
+__device__ __forceinline__ int kprime(int hj) { return 4 * (hj / 3) + hj % 3; }
+__device__ __forceinline__ int hj_of(int kp) { return (kp & 3) < 3 ? (kp >> 2) * 3 + (kp & 3) : -1; }
+__device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
 
 int grid_for(long long work, int per_block = 256, int cap = 16384) {
   long long b = (work + per_block - 1) / per_block;
   if (b > cap) b = cap;
   if (b < 1) b = 1;
   return (int)b;
+}
+
+template <typename T> struct Mma;
+template <> struct Mma<bf16> {
+  __device__ static inline f32x16 run(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  __device__ static inline f32x16 run(u32x4 a, u32x4 b, f32x16 c) {
+    const f32x4 af = __builtin_bit_cast(f32x4, a), bf = __builtin_bit_cast(f32x4, b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], c, 0, 0, 0);
+    return c;
+  }
+};
+
+// acc(32x32) += A(32 x 32) . X, X an f32 accumulator tile (sum over its rows);
+// A row-major in global memory, element (i, k) at A[i*lda + k].
+template <typename T> __device__ f32x16 mm_acc_g(const T* A, int lda, const f32x16& X, f32x16 acc, int r, int h);
+template <>
+__device__ f32x16 mm_acc_g<bf16>(const bf16* A, int lda, const f32x16& X, f32x16 acc, int r, int h) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 bx;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bx[j] = (bf16)X[8 * s + j];
+    const u32x2 lo = *(const u32x2*)(A + (long long)r * lda + 16 * s + 4 * h);
+    const u32x2 hi = *(const u32x2*)(A + (long long)r * lda + 16 * s + 8 + 4 * h);
+    const u32x4 a = u32x4{lo[0], lo[1], hi[0], hi[1]};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bx, acc, 0, 0, 0);
+  }
+  return acc;
+}
+template <>
+__device__ f32x16 mm_acc_g<float>(const float* A, int lda, const f32x16& X, f32x16 acc, int r, int h) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const f32x4 a4 = *(const f32x4*)(A + (long long)r * lda + 8 * m + 4 * h);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[e], X[4 * m + e], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+template <typename T> __device__ __forceinline__ void ld4(const T* p, float* v);
+template <> __device__ __forceinline__ void ld4<float>(const float* p, float* v) {
+  const f32x4 t = *(const f32x4*)p;
+  v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+}
+template <> __device__ __forceinline__ void ld4<bf16>(const bf16* p, float* v) {
+  const bf16x4 t = *(const bf16x4*)p;
+  v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
+}
+template <typename T> __device__ __forceinline__ void st4(T* p, const float* v);
+template <> __device__ __forceinline__ void st4<float>(float* p, const float* v) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+}
+template <> __device__ __forceinline__ void st4<bf16>(bf16* p, const float* v) {
+  *(bf16x4*)p = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
 }
 
 // K/V of head h, key j (j = 0: null kv) for batch b
@@ -30,7 +106,9 @@ __device__ __forceinline__ float kf(const float* kv, const float* null_kv, int b
   return kv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + v * NH * DH + h * DH + d];
 }
 
-// A~ and V~ as [nb][C][24]
+// ---------------------------------------------------------------------------
+// fold: A~, V~ (f32 [nb][C][24]) and the MFMA operand images
+// ---------------------------------------------------------------------------
 __global__ void fold_fwd_kernel(const float* wq, const float* wo, const float* kv,
                                 const float* null_kv, float* at, float* vt, int nb, int C,
                                 float scale) {
@@ -51,233 +129,320 @@ __global__ void fold_fwd_kernel(const float* wq, const float* wo, const float* k
   }
 }
 
+// Kt[b][k'][c], KtT[b][c][k'], Vt[b][c][k'], VtT[b][k'][c] (T); dummies zero
+// images are padded to Cp = roundup(C, 32) channels with zeros
 template <typename T>
-__device__ __forceinline__ float ldc(const T* p) { return (float)*p; }
+__global__ void fold_pack_kernel(const float* at, const float* vt, const float* g1, T* Kt, T* KtT,
+                                 T* Vt, T* VtT, int nb, int C, int Cp) {
+  const long long n = (long long)nb * KP * Cp;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    const long long bk = i / Cp;
+    const int kp = (int)(bk % KP), b = (int)(bk / KP);
+    const int hj = c < C ? hj_of(kp) : -1;
+    const float a = hj >= 0 ? g1[c] * at[((long long)b * C + c) * HK + hj] : 0.f;
+    const float v = hj >= 0 ? vt[((long long)b * C + c) * HK + hj] : 0.f;
+    Kt[i] = (T)a;
+    VtT[i] = (T)v;
+    KtT[((long long)b * Cp + c) * KP + kp] = (T)a;
+    Vt[((long long)b * Cp + c) * KP + kp] = (T)v;
+  }
+}
 
-// thread per token.  Saves per-token LN stats and P (T dtype, 32-wide rows).
+// colsum[b][k'] = sum_c Kt[b][k'][c] (of the values the MFMA sees)
+template <typename T>
+__global__ void fold_colsum_kernel(const T* Kt, float* colsum, int nb, int Cp) {
+  const int row = blockIdx.x;  // b*KP + k'
+  float s = 0.f;
+  for (int c = threadIdx.x; c < Cp; c += 64) s += (float)Kt[(long long)row * Cp + c];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) colsum[row] = s;
+}
+
+// ---------------------------------------------------------------------------
+// forward: one wave = 32 tokens (of one batch element)
+// ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* out, int ldo,
                                                         long long ntok, long long P, int C,
-                                                        const float* g1, const float* g2,
-                                                        const float* at, const float* vt,
+                                                        const T* Kt, const T* Vt,
+                                                        const float* colsum, const float* g2,
                                                         float eps, float* stats, T* pbuf) {
-  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (t >= ntok) return;
-  const int b = (int)(t / P);
-  const T* xr = x + t * ldx;
-  const float* A = at + (long long)b * C * HK;
-  const float* V = vt + (long long)b * C * HK;
-  float mu = 0.f;
-  for (int c = 0; c < C; ++c) mu += ldc(xr + c);
-  mu /= C;
-  float var = 0.f;
-  for (int c = 0; c < C; ++c) { const float d = ldc(xr + c) - mu; var += d * d; }
-  const float rs = rsqrtf(var / C + eps);
-  float s[HK];
+  constexpr int VEC = 16 / sizeof(T);
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  // waves tile each batch element's P tokens; lanes past P mirror token P-1
+  // (their MFMA columns are independent) and store nothing
+  const long long wpb = (P + 31) / 32;
+  const long long wv = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wv >= (ntok / P) * wpb) return;
+  const int b = (int)(wv / wpb);
+  const long long tin = (wv % wpb) * 32 + r;
+  const bool valid = tin < P;
+  const long long tok = (long long)b * P + (valid ? tin : P - 1);
+  const T* xr = x + tok * ldx;
+  const int Cp = (C + 31) / 32 * 32;
+  const T* Ktb = Kt + (long long)b * KP * Cp;
+  const T* Vtb = Vt + (long long)b * Cp * KP;
+  // ---- scores: S^T = Kt . X^T over raw x, LN stats in the same pass ----
+  f32x16 acc;
 #pragma unroll
-  for (int k = 0; k < HK; ++k) s[k] = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float hn = (ldc(xr + c) - mu) * rs * g1[c];
-    const f32x4* a4 = (const f32x4*)(A + (long long)c * HK);
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  float sx = 0.f, sxx = 0.f;
+  for (int c0 = 0; c0 < Cp; c0 += 2 * VEC) {
+    const int c = c0 + h * VEC;
+    const u32x4 xv = c < C ? *(const u32x4*)(xr + c) : u32x4{0u, 0u, 0u, 0u};
+    const u32x4 kv = *(const u32x4*)(Ktb + (long long)r * Cp + c);
+    float f[VEC];
+    Vec<T>::to_f(xv, f);
 #pragma unroll
-    for (int q = 0; q < HK / 4; ++q) {
-      const f32x4 av = a4[q];
-      s[4 * q] += hn * av[0]; s[4 * q + 1] += hn * av[1];
-      s[4 * q + 2] += hn * av[2]; s[4 * q + 3] += hn * av[3];
-    }
+    for (int e = 0; e < VEC; ++e) { sx += f[e]; sxx += f[e] * f[e]; }
+    acc = Mma<T>::run(kv, xv, acc);
   }
+  sx += __shfl_xor(sx, 32, 64);
+  sxx += __shfl_xor(sxx, 32, 64);
+  const float mu = sx / C;
+  const float rs = rsqrtf(fmaxf(sxx / C - mu * mu, 0.f) + eps);
+  // ---- lane-local softmax over each head's 3 keys ----
+  f32x16 p;
 #pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    const float m = fmaxf(s[3 * h], fmaxf(s[3 * h + 1], s[3 * h + 2]));
-    const float e0 = __expf(s[3 * h] - m), e1 = __expf(s[3 * h + 1] - m), e2 = __expf(s[3 * h + 2] - m);
+  for (int m = 0; m < 4; ++m) {
+    float s3[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int kp = 8 * m + 4 * h + j;
+      s3[j] = rs * (acc[4 * m + j] - mu * colsum[b * KP + kp]);
+    }
+    const float mx = fmaxf(s3[0], fmaxf(s3[1], s3[2]));
+    const float e0 = __expf(s3[0] - mx), e1 = __expf(s3[1] - mx), e2 = __expf(s3[2] - mx);
     const float inv = 1.f / (e0 + e1 + e2);
-    s[3 * h] = e0 * inv; s[3 * h + 1] = e1 * inv; s[3 * h + 2] = e2 * inv;
-  }
-  // the P row as stored (T-rounded) is what the backward recomputes with
-  T* pr = pbuf + t * PPAD;
+    float pv[4] = {e0 * inv, e1 * inv, e2 * inv, 0.f};
+    // P as stored (T-rounded) is what both O and the backward use
+    T pt[4];
 #pragma unroll
-  for (int k = 0; k < PPAD; ++k) {
-    const T v = (T)(k < HK ? s[k] : 0.f);
-    pr[k] = v;
-    if (k < HK) s[k] = (float)v;
+    for (int j = 0; j < 4; ++j) { pt[j] = (T)pv[j]; p[4 * m + j] = (float)pt[j]; }
+    float pw[4] = {(float)pt[0], (float)pt[1], (float)pt[2], (float)pt[3]};
+    if (valid) st4<T>(pbuf + tok * KP + 8 * m + 4 * h, pw);
   }
-  auto o_at = [&](int c) {
-    const f32x4* v4 = (const f32x4*)(V + (long long)c * HK);
-    float o = 0.f;
+  // ---- o statistics (pass 1), then the normalised output + residual (pass 2) ----
+  float so = 0.f, soo = 0.f;
+  for (int ct = 0; ct < Cp; ct += 32) {
+    f32x16 o;
 #pragma unroll
-    for (int q = 0; q < HK / 4; ++q) {
-      const f32x4 vv = v4[q];
-      o += s[4 * q] * vv[0] + s[4 * q + 1] * vv[1] + s[4 * q + 2] * vv[2] + s[4 * q + 3] * vv[3];
+    for (int e = 0; e < 16; ++e) o[e] = 0.f;
+    o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { so += o[e]; soo += o[e] * o[e]; }
+  }
+  so += __shfl_xor(so, 32, 64);
+  soo += __shfl_xor(soo, 32, 64);
+  const float mu2 = so / C;
+  const float rs2 = rsqrtf(fmaxf(soo / C - mu2 * mu2, 0.f) + eps);
+  T* orow = out + tok * ldo;
+  for (int ct = 0; ct < Cp; ct += 32) {
+    f32x16 o;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[e] = 0.f;
+    o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = ct + 8 * g + 4 * h;
+      if (c >= C) continue;
+      float xv[4], y[4];
+      ld4<T>(xr + c, xv);
+      const f32x4 gg = *(const f32x4*)(g2 + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = (o[4 * g + e] - mu2) * rs2 * gg[e] + xv[e];
+      if (valid) st4<T>(orow + c, y);
     }
-    return o;
-  };
-  float mu2 = 0.f;
-  for (int c = 0; c < C; ++c) mu2 += o_at(c);
-  mu2 /= C;
-  float var2 = 0.f;
-  for (int c = 0; c < C; ++c) { const float d = o_at(c) - mu2; var2 += d * d; }
-  const float rs2 = rsqrtf(var2 / C + eps);
-  T* orow = out + t * ldo;
-  for (int c = 0; c < C; ++c) orow[c] = (T)((o_at(c) - mu2) * rs2 * g2[c] + ldc(xr + c));
-  float* st = stats + t * 4;
-  st[0] = mu; st[1] = rs; st[2] = mu2; st[3] = rs2;
+  }
+  if (h == 0 && valid) *(f32x4*)(stats + tok * 4) = f32x4{mu, rs, mu2, rs2};
 }
 
-// Backward per token.  Writes dx (incl. the residual), dO (for dV~), dS' = rs1*dS
-// (for dA~) and accumulates dg1, dg2 and the per-batch correction m[b][k] =
-// sum_t mu1_t * dS'_tk.
+// ---------------------------------------------------------------------------
+// backward: one wave = 32 tokens
+//   writes dx (incl. residual), dO (tokens x C), dS' = rs*dS and
+//   P' = rs2*P (k'=3 -> mu2*rs2) (tokens x 32) for the batched GEMMs, and
+//   accumulates mcorr[b][k'] = sum_t mu_t*rs_t*dS_tk'
+// ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, const T* x, int ldx,
                                                         T* dx, int lddx, long long ntok,
-                                                        long long P, int C, const float* g1,
-                                                        const float* g2, const float* at,
-                                                        const float* vt, const float* stats,
-                                                        const T* pbuf, T* dobuf, T* dsbuf,
-                                                        float* dg1, float* dg2, float* mcorr) {
-  __shared__ float sg1[1024], sg2[1024];
-  for (int c = threadIdx.x; c < C; c += blockDim.x) { sg1[c] = 0.f; sg2[c] = 0.f; }
-  __syncthreads();
-  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  const bool live = t < ntok;
-  const long long tt = live ? t : 0;
-  const int b = (int)(tt / P);
-  const int lane = threadIdx.x & 63;
-  const T* xr = x + tt * ldx;
-  const T* dyr = dy + tt * lddy;
-  const float* A = at + (long long)b * C * HK;
-  const float* V = vt + (long long)b * C * HK;
-  const float mu = stats[tt * 4], rs = stats[tt * 4 + 1], mu2 = stats[tt * 4 + 2], rs2 = stats[tt * 4 + 3];
-  float p[HK];
+                                                        long long P, int C, const T* KtT,
+                                                        const T* Vt, const T* VtT,
+                                                        const float* colsum, const float* g2,
+                                                        const float* stats, const T* pbuf,
+                                                        T* dobuf, T* dsbuf, T* p2buf,
+                                                        float* mcorr) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  // waves tile each batch element's P tokens; lanes past P mirror token P-1
+  // (their MFMA columns are independent) and store nothing
+  const long long wpb = (P + 31) / 32;
+  const long long wv = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wv >= (ntok / P) * wpb) return;
+  const int b = (int)(wv / wpb);
+  const long long tin = (wv % wpb) * 32 + r;
+  const bool valid = tin < P;
+  const long long tok = (long long)b * P + (valid ? tin : P - 1);
+  const T* xr = x + tok * ldx;
+  const T* dyr = dy + tok * lddy;
+  const int Cp = (C + 31) / 32 * 32;
+  const T* Vtb = Vt + (long long)b * Cp * KP;
+  const T* VtTb = VtT + (long long)b * KP * Cp;
+  const T* KtTb = KtT + (long long)b * Cp * KP;
+  const f32x4 st = *(const f32x4*)(stats + tok * 4);
+  const float mu = st[0], rs = st[1], mu2 = st[2], rs2 = st[3];
+  f32x16 p;
 #pragma unroll
-  for (int k = 0; k < HK; ++k) p[k] = (float)pbuf[tt * PPAD + k];
-  auto o_at = [&](int c) {
-    const f32x4* v4 = (const f32x4*)(V + (long long)c * HK);
-    float o = 0.f;
+  for (int m = 0; m < 4; ++m) {
+    float v[4];
+    ld4<T>(pbuf + tok * KP + 8 * m + 4 * h, v);
 #pragma unroll
-    for (int q = 0; q < HK / 4; ++q) {
-      const f32x4 vv = v4[q];
-      o += p[4 * q] * vv[0] + p[4 * q + 1] * vv[1] + p[4 * q + 2] * vv[2] + p[4 * q + 3] * vv[3];
-    }
-    return o;
-  };
-  // LN_out backward statistics
+    for (int j = 0; j < 4; ++j) p[4 * m + j] = v[j];
+  }
+  // ---- pass A: LN_out backward statistics ----
   float m1 = 0.f, m2 = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float oh = (o_at(c) - mu2) * rs2;
-    const float dyc = live ? ldc(dyr + c) : 0.f;
-    const float doh = dyc * g2[c];
-    m1 += doh;
-    m2 += doh * oh;
-    float part = wave_sum(dyc * oh);
-    if (lane == 0) atomicAdd(&sg2[c], part);
-  }
-  m1 /= C;
-  m2 /= C;
-  // do_c, dp
-  float dp[HK];
+  for (int ct = 0; ct < Cp; ct += 32) {
+    f32x16 o;
 #pragma unroll
-  for (int k = 0; k < HK; ++k) dp[k] = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float oh = (o_at(c) - mu2) * rs2;
-    const float dyc = live ? ldc(dyr + c) : 0.f;
-    const float dO = rs2 * (dyc * g2[c] - m1 - oh * m2);
-    if (live) dobuf[tt * C + c] = (T)dO;
-    const f32x4* v4 = (const f32x4*)(V + (long long)c * HK);
+    for (int e = 0; e < 16; ++e) o[e] = 0.f;
+    o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
 #pragma unroll
-    for (int q = 0; q < HK / 4; ++q) {
-      const f32x4 vv = v4[q];
-      dp[4 * q] += dO * vv[0]; dp[4 * q + 1] += dO * vv[1];
-      dp[4 * q + 2] += dO * vv[2]; dp[4 * q + 3] += dO * vv[3];
+    for (int g = 0; g < 4; ++g) {
+      const int c = ct + 8 * g + 4 * h;
+      if (c >= C) continue;
+      float dv[4];
+      ld4<T>(dyr + c, dv);
+      const f32x4 gg = *(const f32x4*)(g2 + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float doh = dv[e] * gg[e];
+        m1 += doh;
+        m2 += doh * (o[4 * g + e] - mu2) * rs2;
+      }
     }
   }
-  // softmax backward per head
-  float ds[HK];
+  m1 = (m1 + __shfl_xor(m1, 32, 64)) / C;
+  m2 = (m2 + __shfl_xor(m2, 32, 64)) / C;
+  // ---- pass B: dO (stored) and dP^T = Vt^T . dO^T ----
+  f32x16 dp;
 #pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    const float sdot = p[3 * h] * dp[3 * h] + p[3 * h + 1] * dp[3 * h + 1] + p[3 * h + 2] * dp[3 * h + 2];
+  for (int e = 0; e < 16; ++e) dp[e] = 0.f;
+  for (int ct = 0; ct < Cp; ct += 32) {
+    f32x16 o;
 #pragma unroll
-    for (int j = 0; j < NK; ++j) ds[3 * h + j] = p[3 * h + j] * (dp[3 * h + j] - sdot);
-  }
-  if (live) {
+    for (int e = 0; e < 16; ++e) o[e] = 0.f;
+    o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
+    f32x16 dO;
 #pragma unroll
-    for (int k = 0; k < PPAD; ++k) dsbuf[tt * PPAD + k] = (T)(k < HK ? rs * ds[k] : 0.f);
-  }
-  // per-batch correction m[b][k] = sum_t mu1_t * rs1_t * ds_tk
-  const int b0 = __builtin_amdgcn_readfirstlane(b);
-  const bool uniform = __all(b == b0);
+    for (int g = 0; g < 4; ++g) {
+      const int c = ct + 8 * g + 4 * h;
+      if (c >= C) {
 #pragma unroll
-  for (int k = 0; k < HK; ++k) {
-    const float v = live ? mu * rs * ds[k] : 0.f;
-    if (uniform) {
-      const float w = wave_sum(v);
-      if (lane == 0) atomicAdd(mcorr + (long long)b0 * HK + k, w);
-    } else if (live) {
-      atomicAdd(mcorr + (long long)b * HK + k, v);
+        for (int e = 0; e < 4; ++e) dO[4 * g + e] = 0.f;
+        continue;
+      }
+      float dv[4], w[4];
+      ld4<T>(dyr + c, dv);
+      const f32x4 gg = *(const f32x4*)(g2 + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float oh = (o[4 * g + e] - mu2) * rs2;
+        const T q = (T)(rs2 * (dv[e] * gg[e] - m1 - oh * m2));
+        w[e] = (float)q;
+        dO[4 * g + e] = w[e];
+      }
+      if (valid) st4<T>(dobuf + tok * C + c, w);
     }
+    dp = mm_acc_g<T>(VtTb + ct, Cp, dO, dp, r, h);
   }
-  // LN_in backward: dhn_c = sum_k ds_k A[c][k]
-  auto dhn_at = [&](int c) {
-    const f32x4* a4 = (const f32x4*)(A + (long long)c * HK);
-    float r = 0.f;
+  // ---- softmax backward (lane-local heads) ----
+  f32x16 ds;
+  float a1 = 0.f, a2 = 0.f;
 #pragma unroll
-    for (int q = 0; q < HK / 4; ++q) {
-      const f32x4 av = a4[q];
-      r += ds[4 * q] * av[0] + ds[4 * q + 1] * av[1] + ds[4 * q + 2] * av[2] + ds[4 * q + 3] * av[3];
+  for (int m = 0; m < 4; ++m) {
+    const float sd = p[4 * m] * dp[4 * m] + p[4 * m + 1] * dp[4 * m + 1] + p[4 * m + 2] * dp[4 * m + 2];
+    float w[4], q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kp = 8 * m + 4 * h + j;
+      const float d = j < 3 ? p[4 * m + j] * (dp[4 * m + j] - sd) : 0.f;
+      ds[4 * m + j] = d;
+      a1 += d * colsum[b * KP + kp];
+      if (j < 3 && p[4 * m + j] > 0.f) a2 += d * __logf(p[4 * m + j]);
+      w[j] = rs * d;
+      q[j] = j < 3 ? rs2 * p[4 * m + j] : (kp == 3 ? mu2 * rs2 : 0.f);
     }
-    return r;
-  };
-  float n1 = 0.f, n2 = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float xh = (ldc(xr + c) - mu) * rs;
-    const float dhn = dhn_at(c);
-    const float dxh = dhn * g1[c];
-    n1 += dxh;
-    n2 += dxh * xh;
-    float part = wave_sum(live ? dhn * xh : 0.f);
-    if (lane == 0) atomicAdd(&sg1[c], part);
+    if (valid) st4<T>(dsbuf + tok * KP + 8 * m + 4 * h, w);
+    if (valid) st4<T>(p2buf + tok * KP + 8 * m + 4 * h, q);
   }
-  n1 /= C;
-  n2 /= C;
-  if (live) {
-    T* dxr = dx + tt * lddx;
-    for (int c = 0; c < C; ++c) {
-      const float xh = (ldc(xr + c) - mu) * rs;
-      const float dxh = dhn_at(c) * g1[c];
-      dxr[c] = (T)(rs * (dxh - n1 - xh * n2) + ldc(dyr + c));
+  // mcorr[b][k'] += sum over the 32 tokens of mu*rs*ds  (reduce over lanes of each half)
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    float v = valid ? mu * rs * ds[e] : 0.f;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+    if (r == 0) atomicAdd(mcorr + b * KP + acc_row(e, h), v);
+  }
+  a1 = (a1 + __shfl_xor(a1, 32, 64)) / C;  // mean_c dxhat
+  a2 = (a2 + __shfl_xor(a2, 32, 64)) / C;  // mean_c dxhat*xhat
+  // ---- pass C: dXhat^T = KtT . dS^T, LN_in backward + residual ----
+  T* dxr = dx + tok * lddx;
+  for (int ct = 0; ct < Cp; ct += 32) {
+    f32x16 dxh;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dxh[e] = 0.f;
+    dxh = mm_acc_g<T>(KtTb + (long long)ct * KP, KP, ds, dxh, r, h);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = ct + 8 * g + 4 * h;
+      if (c >= C) continue;
+      float xv[4], dv[4], w[4];
+      ld4<T>(xr + c, xv);
+      ld4<T>(dyr + c, dv);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xh = (xv[e] - mu) * rs;
+        w[e] = rs * (dxh[4 * g + e] - a1 - xh * a2) + dv[e];
+      }
+      if (valid) st4<T>(dxr + c, w);
     }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    atomicAdd(dg1 + c, sg1[c]);
-    atomicAdd(dg2 + c, sg2[c]);
   }
 }
 
-// dA~ = g1 * (raw - m), raw = ws_a[b][k][c] (from the wgrad GEMM), in place into
-// [nb][C][24] layout; dV~ from ws_v[b][k][c] likewise (no correction).
-__global__ void fold_grad_finish_kernel(const float* ws_a, const float* ws_v, const float* g1,
-                                        const float* mcorr, float* dat, float* dvt, int nb, int C) {
-  const long long n = (long long)nb * C * HK;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int k = (int)(i % HK);
-    const long long bc = i / HK;
-    const int c = (int)(bc % C), b = (int)(bc / C);
-    const long long wi = ((long long)b * PPAD + k) * C + c;
-    dat[i] = g1[c] * (ws_a[wi] - mcorr[b * HK + k]);
-    dvt[i] = ws_v[wi];
+// dat/dvt [nb][C][24] from the GEMM results (ws_* [nb][32][C]) and the LN gain grads
+__global__ void fold_grad_finish_kernel(const float* wsR, const float* wsV, const float* wsQ,
+                                        const float* mcorr, const float* at, const float* vt,
+                                        const float* g1, float* dat, float* dvt, float* dg1,
+                                        float* dg2, int nb, int C, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int b = 0; b < nb; ++b) {
+    for (int hj = 0; hj < HK; ++hj) {
+      const int kp = kprime(hj);
+      const long long wi = ((long long)b * KP + kp) * C + c;
+      const long long fi = ((long long)b * C + c) * HK + hj;
+      const float dk = wsR[wi] - mcorr[b * KP + kp];
+      dat[fi] = g1[c] * dk;
+      s1 += at[fi] * dk;
+      dvt[fi] = wsV[wi];
+      s2 += vt[fi] * wsQ[wi];
+    }
+    s2 -= wsQ[((long long)b * KP + 3) * C + c];
   }
+  if (dg1) dg1[c] = accumulate ? dg1[c] + s1 : s1;
+  if (dg2) dg2[c] = accumulate ? dg2[c] + s2 : s2;
 }
 
-// parameter grads of the fold: dWq, dWo and dK/dV -> d(kv) and d(null_kv)
+// parameter grads of the fold: dWq, dWo
 __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const float* kv,
                                   const float* null_kv, float* dwq, float* dwo, int nb, int C,
                                   float scale, int accumulate) {
   const long long n = (long long)NH * DH * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
-    // dWq[hd][c]   (i = hd*C + c)
-    {
+    {  // dWq[hd][c]   (i = hd*C + c)
       const int c = (int)(i % C), hd = (int)(i / C);
       const int h = hd / DH, d = hd % DH;
       float s = 0.f;
@@ -286,8 +451,7 @@ __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const floa
           s += dat[((long long)b * C + c) * HK + h * NK + j] * kf(kv, null_kv, b, h, j, d, 0);
       dwq[i] = accumulate ? dwq[i] + s * scale : s * scale;
     }
-    // dWo[c][hd]   (i = c*512 + hd)
-    {
+    {  // dWo[c][hd]   (i = c*512 + hd)
       const int hd = (int)(i % (NH * DH)), c = (int)(i / (NH * DH));
       const int h = hd / DH, d = hd % DH;
       float s = 0.f;
@@ -299,86 +463,118 @@ __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const floa
   }
 }
 
-// dKf/dVf[b][h][j][d] -> dkv[b][n][...] (j>=1) and dnull_kv (j==0, summed)
-__global__ void fold_bwd_kv_kernel(const float* dat, const float* dvt, const float* wq,
-                                   const float* wo, float* dkv, float* dnull, int nb, int C,
-                                   float scale) {
-  const int n = nb * NH * NK * DH;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int d = i % DH;
-  const int j = (i / DH) % NK;
-  const int h = (i / (DH * NK)) % NH;
-  const int b = i / (DH * NK * NH);
-  float sk = 0.f, sv = 0.f;
-  for (int c = 0; c < C; ++c) {
-    sk += dat[((long long)b * C + c) * HK + h * NK + j] * wq[(long long)(h * DH + d) * C + c];
-    sv += dvt[((long long)b * C + c) * HK + h * NK + j] * wo[(long long)c * (NH * DH) + h * DH + d];
+// dK/dV of (b, h, j) -> d(kv) (j >= 1) or dnull (j == 0); one block per (b,h,j)
+__global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, const float* dvt,
+                                                          const float* wq, const float* wo,
+                                                          float* dkv, float* dnull, int nb, int C,
+                                                          float scale) {
+  __shared__ float red[4][DH];
+  __shared__ float dks[DH];
+  const int bhj = blockIdx.x;
+  const int j = bhj % NK, h = (bhj / NK) % NH, b = bhj / (NK * NH);
+  const int hj = h * NK + j;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // dK[d] = scale * sum_c dat[c][hj] Wq[h*64+d][c]: wave w owns 16 d, lanes sweep c
+  for (int dd = 0; dd < DH / 4; ++dd) {
+    const int d = w * (DH / 4) + dd;
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += dat[((long long)b * C + c) * HK + hj] * wq[(long long)(h * DH + d) * C + c];
+    s = wave_sum(s);
+    if (lane == 0) dks[d] = s * scale;
   }
-  sk *= scale;
-  if (j == 0) {
-    atomicAdd(dnull + d, sk);
-    atomicAdd(dnull + DH + d, sv);
-  } else {
-    dkv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + h * DH + d] = sk;
-    dkv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + NH * DH + h * DH + d] = sv;
+  // dV[d] = sum_c dvt[c][hj] Wo[c][h*64+d]: lane = d, 4 c-slices
+  {
+    float s = 0.f;
+    for (int c = w; c < C; c += 4) s += dvt[((long long)b * C + c) * HK + hj] * wo[(long long)c * (NH * DH) + h * DH + lane];
+    red[w][lane] = s;
   }
+  __syncthreads();
+  if (threadIdx.x < DH) {
+    const int d = threadIdx.x;
+    const float dv = red[0][d] + red[1][d] + red[2][d] + red[3][d];
+    if (j == 0) {
+      atomicAdd(dnull + d, dks[d]);
+      atomicAdd(dnull + DH + d, dv);
+    } else {
+      dkv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + h * DH + d] = dks[d];
+      dkv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + NH * DH + h * DH + d] = dv;
+    }
+  }
+}
+
+template <typename T>
+int fold_t(const float* wq, const float* wo, const float* kv, const float* null_kv,
+           const float* g1, float* at, float* vt, void* Kt, void* KtT, void* Vt, void* VtT,
+           float* colsum, int nb, int C, float scale, hipStream_t st) {
+  const long long n = (long long)nb * C * HK;
+  fold_fwd_kernel<<<grid_for(n), 256, 0, st>>>(wq, wo, kv, null_kv, at, vt, nb, C, scale);
+  const int Cp = (C + 31) / 32 * 32;
+  fold_pack_kernel<T><<<grid_for((long long)nb * KP * Cp), 256, 0, st>>>(at, vt, g1, (T*)Kt, (T*)KtT, (T*)Vt, (T*)VtT, nb, C, Cp);
+  fold_colsum_kernel<T><<<nb * KP, 64, 0, st>>>((const T*)Kt, colsum, nb, Cp);
+  return check_launch("xattn_fold");
 }
 
 }  // namespace
 
-extern "C" int dv_xattn_fold(const float* wq, const float* wo, const float* kv,
-                             const float* null_kv, float* at, float* vt, int nb, int C,
-                             float scale, void* stream) {
-  DV_REQUIRE(wq && wo && kv && null_kv && at && vt, "null pointer");
-  const long long n = (long long)nb * C * HK;
-  fold_fwd_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(wq, wo, kv, null_kv, at, vt, nb, C, scale);
-  return check_launch("xattn_fold");
+extern "C" int dv_xattn_fold(int dtype, const float* wq, const float* wo, const float* kv,
+                             const float* null_kv, const float* g1, float* at, float* vt,
+                             void* Kt, void* KtT, void* Vt, void* VtT, float* colsum, int nb,
+                             int C, float scale, void* stream) {
+  DV_REQUIRE(wq && wo && kv && null_kv && g1 && at && vt && Kt && KtT && Vt && VtT && colsum,
+             "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DV_BF16) return fold_t<bf16>(wq, wo, kv, null_kv, g1, at, vt, Kt, KtT, Vt, VtT, colsum, nb, C, scale, st);
+  return fold_t<float>(wq, wo, kv, null_kv, g1, at, vt, Kt, KtT, Vt, VtT, colsum, nb, C, scale, st);
 }
 
 extern "C" int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ldo, long long ntok,
-                            long long P, int C, const float* g1, const float* g2, const float* at,
-                            const float* vt, float eps, float* stats, void* pbuf, void* stream) {
-  DV_REQUIRE(x && out && g1 && g2 && at && vt && stats && pbuf, "null pointer");
-  DV_REQUIRE(C <= 1024, "C too large");
+                            long long P, int C, const void* Kt, const void* Vt,
+                            const float* colsum, const float* g2, float eps, float* stats,
+                            void* pbuf, void* stream) {
+  DV_REQUIRE(x && out && Kt && Vt && colsum && g2 && stats && pbuf, "null pointer");
+  DV_REQUIRE(P > 0 && ntok % P == 0, "ntok must be a multiple of P");
+  const int VEC = dtype == DV_BF16 ? 8 : 4;
+  DV_REQUIRE(C % VEC == 0 && ldx % VEC == 0 && ldo % 4 == 0, "C / strides must be multiples of 16 bytes");
   hipStream_t st = (hipStream_t)stream;
-  const int g = grid_for(ntok);
+  const int blocks = (int)(((ntok / P) * ((P + 31) / 32) + 3) / 4);
   if (dtype == DV_BF16)
-    xattn_fwd_kernel<bf16><<<g, 256, 0, st>>>((const bf16*)x, ldx, (bf16*)out, ldo, ntok, P, C, g1, g2, at, vt, eps, stats, (bf16*)pbuf);
+    xattn_fwd_kernel<bf16><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (bf16*)out, ldo, ntok, P, C, (const bf16*)Kt, (const bf16*)Vt, colsum, g2, eps, stats, (bf16*)pbuf);
   else
-    xattn_fwd_kernel<float><<<g, 256, 0, st>>>((const float*)x, ldx, (float*)out, ldo, ntok, P, C, g1, g2, at, vt, eps, stats, (float*)pbuf);
+    xattn_fwd_kernel<float><<<blocks, 256, 0, st>>>((const float*)x, ldx, (float*)out, ldo, ntok, P, C, (const float*)Kt, (const float*)Vt, colsum, g2, eps, stats, (float*)pbuf);
   return check_launch("xattn_fwd");
 }
 
 extern "C" int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const void* x, int ldx,
                                    void* dx, int lddx, long long ntok, long long P, int C,
-                                   const float* g1, const float* g2, const float* at,
-                                   const float* vt, const float* stats, const void* pbuf,
-                                   void* dobuf, void* dsbuf, float* dg1, float* dg2, float* mcorr,
-                                   void* stream) {
-  DV_REQUIRE(dy && x && dx && stats && pbuf && dobuf && dsbuf && dg1 && dg2 && mcorr, "null pointer");
-  DV_REQUIRE(C <= 1024, "C too large");
+                                   const void* KtT, const void* Vt, const void* VtT,
+                                   const float* colsum, const float* g2, const float* stats,
+                                   const void* pbuf, void* dobuf, void* dsbuf, void* p2buf,
+                                   float* mcorr, void* stream) {
+  DV_REQUIRE(dy && x && dx && KtT && Vt && VtT && colsum && g2 && stats && pbuf && dobuf && dsbuf &&
+             p2buf && mcorr, "null pointer");
+  DV_REQUIRE(P > 0 && ntok % P == 0 && C % 8 == 0, "bad shape");
   hipStream_t st = (hipStream_t)stream;
-  const int g = (int)((ntok + 255) / 256);
+  const int blocks = (int)(((ntok / P) * ((P + 31) / 32) + 3) / 4);
   if (dtype == DV_BF16)
-    xattn_bwd_kernel<bf16><<<g, 256, 0, st>>>((const bf16*)dy, lddy, (const bf16*)x, ldx, (bf16*)dx, lddx, ntok, P, C, g1, g2, at, vt, stats, (const bf16*)pbuf, (bf16*)dobuf, (bf16*)dsbuf, dg1, dg2, mcorr);
+    xattn_bwd_kernel<bf16><<<blocks, 256, 0, st>>>((const bf16*)dy, lddy, (const bf16*)x, ldx, (bf16*)dx, lddx, ntok, P, C, (const bf16*)KtT, (const bf16*)Vt, (const bf16*)VtT, colsum, g2, stats, (const bf16*)pbuf, (bf16*)dobuf, (bf16*)dsbuf, (bf16*)p2buf, mcorr);
   else
-    xattn_bwd_kernel<float><<<g, 256, 0, st>>>((const float*)dy, lddy, (const float*)x, ldx, (float*)dx, lddx, ntok, P, C, g1, g2, at, vt, stats, (const float*)pbuf, (float*)dobuf, (float*)dsbuf, dg1, dg2, mcorr);
+    xattn_bwd_kernel<float><<<blocks, 256, 0, st>>>((const float*)dy, lddy, (const float*)x, ldx, (float*)dx, lddx, ntok, P, C, (const float*)KtT, (const float*)Vt, (const float*)VtT, colsum, g2, stats, (const float*)pbuf, (float*)dobuf, (float*)dsbuf, (float*)p2buf, mcorr);
   return check_launch("xattn_bwd_tokens");
 }
 
-extern "C" int dv_xattn_fold_bwd(const float* ws_a, const float* ws_v, const float* g1,
-                                 const float* mcorr, const float* wq, const float* wo,
+extern "C" int dv_xattn_fold_bwd(const float* wsR, const float* wsV, const float* wsQ,
+                                 const float* mcorr, const float* at, const float* vt,
+                                 const float* g1, const float* wq, const float* wo,
                                  const float* kv, const float* null_kv, float* dat, float* dvt,
-                                 float* dwq, float* dwo, float* dkv, float* dnull, int nb, int C,
-                                 float scale, int accumulate, void* stream) {
-  DV_REQUIRE(ws_a && ws_v && g1 && mcorr && wq && wo && kv && null_kv && dat && dvt && dwq && dwo && dkv && dnull,
-             "null pointer");
+                                 float* dg1, float* dg2, float* dwq, float* dwo, float* dkv,
+                                 float* dnull, int nb, int C, float scale, int acc_g, int acc_w,
+                                 void* stream) {
+  DV_REQUIRE(wsR && wsV && wsQ && mcorr && at && vt && g1 && wq && wo && kv && null_kv && dat &&
+             dvt && dwq && dwo && dkv && dnull, "null pointer");
   hipStream_t st = (hipStream_t)stream;
-  const long long n = (long long)nb * C * HK;
-  fold_grad_finish_kernel<<<grid_for(n), 256, 0, st>>>(ws_a, ws_v, g1, mcorr, dat, dvt, nb, C);
-  fold_bwd_w_kernel<<<grid_for((long long)NH * DH * C), 256, 0, st>>>(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale, accumulate);
-  if (!accumulate) (void)hipMemsetAsync(dnull, 0, sizeof(float) * 2 * DH, st);
-  fold_bwd_kv_kernel<<<(nb * NH * NK * DH + 255) / 256, 256, 0, st>>>(dat, dvt, wq, wo, dkv, dnull, nb, C, scale);
+  fold_grad_finish_kernel<<<(C + 255) / 256, 256, 0, st>>>(wsR, wsV, wsQ, mcorr, at, vt, g1, dat, dvt, dg1, dg2, nb, C, acc_g);
+  fold_bwd_w_kernel<<<grid_for((long long)NH * DH * C), 256, 0, st>>>(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale, acc_w);
+  if (!acc_w) (void)hipMemsetAsync(dnull, 0, sizeof(float) * 2 * DH, st);
+  fold_bwd_kv_kernel<<<nb * NH * NK, 256, 0, st>>>(dat, dvt, wq, wo, dkv, dnull, nb, C, scale);
   return check_launch("xattn_fold_bwd");
 }

@@ -409,13 +409,15 @@ XA_HEADS, XA_DH = 8, 64
 
 
 class CrossAttnFn(torch.autograd.Function):
+    """out = CrossAttention(x, context) + x, folded per batch element (dv_xattn.hip)."""
+
     @staticmethod
     def forward(ctx, x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps):
         require_gpu(x, context)
         nf, h, w, C = x.shape
         ntok = nf * h * w
         P = ntok // nb
-        dev = x.device
+        dev, dtype = x.device, x.dtype
         ctxf = context.detach().float().contiguous().reshape(-1, context.shape[-1])
         kv = torch.empty(ctxf.shape[0], 2 * XA_HEADS * XA_DH, dtype=torch.float32, device=dev)
         wkvf = wkv.detach().float().contiguous()
@@ -423,79 +425,85 @@ class CrossAttnFn(torch.autograd.Function):
              None, ctxf.shape[0], ctxf.shape[1], kv.shape[1], 0, 0, stream())
         wqf, wof = wq.detach().float().contiguous(), wo.detach().float().contiguous()
         nkv = null_kv.detach().float().contiguous()
+        g1f, g2f = g1.detach().float().contiguous(), g2.detach().float().contiguous()
         at = torch.empty(nb, C, 24, dtype=torch.float32, device=dev)
         vt = torch.empty_like(at)
-        scale = XA_DH ** -0.5
-        call("dv_xattn_fold", ptr(wqf), ptr(wof), ptr(kv), ptr(nkv), ptr(at), ptr(vt), nb, C,
-             ctypes_float(scale), stream())
-        out = torch.empty(nf, h, w, C, dtype=x.dtype, device=dev)
+        Cp = (C + 31) // 32 * 32  # operand images padded to whole 32-channel MFMA tiles
+        Kt = torch.empty(nb, 32, Cp, dtype=dtype, device=dev)
+        KtT = torch.empty(nb, Cp, 32, dtype=dtype, device=dev)
+        Vt = torch.empty(nb, Cp, 32, dtype=dtype, device=dev)
+        VtT = torch.empty(nb, 32, Cp, dtype=dtype, device=dev)
+        colsum = torch.empty(nb, 32, dtype=torch.float32, device=dev)
+        call("dv_xattn_fold", dt(x), ptr(wqf), ptr(wof), ptr(kv), ptr(nkv), ptr(g1f), ptr(at), ptr(vt),
+             ptr(Kt), ptr(KtT), ptr(Vt), ptr(VtT), ptr(colsum), nb, C, ctypes_float(XA_DH ** -0.5),
+             stream())
+        out = torch.empty(nf, h, w, C, dtype=dtype, device=dev)
         stats = torch.empty(ntok, 4, dtype=torch.float32, device=dev)
-        pbuf = torch.empty(ntok, 32, dtype=x.dtype, device=dev)
-        g1f, g2f = g1.detach().float().contiguous(), g2.detach().float().contiguous()
-        call("dv_xattn_fwd", dt(x), ptr(x), cl_ld(x), ptr(out), C, ntok, P, C, ptr(g1f), ptr(g2f),
-             ptr(at), ptr(vt), ctypes_float(eps), ptr(stats), ptr(pbuf), stream())
-        ctx.save_for_backward(x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, stats, pbuf)
+        pbuf = torch.empty(ntok, 32, dtype=dtype, device=dev)
+        call("dv_xattn_fwd", dt(x), ptr(x), cl_ld(x), ptr(out), C, ntok, P, C, ptr(Kt), ptr(Vt),
+             ptr(colsum), ptr(g2f), ctypes_float(eps), ptr(stats), ptr(pbuf), stream())
+        ctx.save_for_backward(x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, KtT, Vt, VtT,
+                              colsum, stats, pbuf)
         ctx.params = (g1, null_kv, wq, wkv, wo, g2)
         ctx.meta = (nb, eps, context.shape)
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, stats, pbuf = ctx.saved_tensors
+        (x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, KtT, Vt, VtT, colsum, stats,
+         pbuf) = ctx.saved_tensors
         g1p, nullp, wqp, wkvp, wop, g2p = ctx.params
         nb, eps, cshape = ctx.meta
         nf, h, w, C = x.shape
         ntok = nf * h * w
         P = ntok // nb
-        dev = x.device
+        dev, dtype = x.device, x.dtype
         dy = dy.contiguous()
-        dx = torch.empty(nf, h, w, C, dtype=x.dtype, device=dev)
-        dobuf = torch.empty(ntok, C, dtype=x.dtype, device=dev)
-        dsbuf = torch.empty(ntok, 32, dtype=x.dtype, device=dev)
-        s1, s2 = _grad_out(g1p, zero=True), _grad_out(g2p, zero=True)
-        dg1 = s1[0] if s1 else torch.zeros(C, dtype=torch.float32, device=dev)
-        dg2 = s2[0] if s2 else torch.zeros(C, dtype=torch.float32, device=dev)
-        mcorr = torch.zeros(nb, 24, dtype=torch.float32, device=dev)
+        dx = torch.empty(nf, h, w, C, dtype=dtype, device=dev)
+        dobuf = torch.empty(ntok, C, dtype=dtype, device=dev)
+        dsbuf = torch.empty(ntok, 32, dtype=dtype, device=dev)
+        p2buf = torch.empty(ntok, 32, dtype=dtype, device=dev)
+        mcorr = torch.zeros(nb, 32, dtype=torch.float32, device=dev)
         ldx = cl_ld(x)
         call("dv_xattn_bwd_tokens", dt(x), ptr(dy), C, ptr(x), ldx, ptr(dx), C, ntok, P, C,
-             ptr(g1f), ptr(g2f), ptr(at), ptr(vt), ptr(stats), ptr(pbuf), ptr(dobuf), ptr(dsbuf),
-             ptr(dg1), ptr(dg2), ptr(mcorr), stream())
-        # per-batch token reductions on the MFMA wgrad GEMM
-        ws_a = _wgrad_workspace(nb * 32, 1, C, dev)
-        ws_v = _wgrad_workspace(nb * 32 + 1, 1, C, dev)  # distinct cache entry
-        esz = x.element_size()
-        for bi in range(nb):
-            xb = x.data_ptr() + bi * P * ldx * esz
-            call("dv_conv_wgrad", dt(x), ctypes_vp(dsbuf.data_ptr() + bi * P * 32 * esz), 32,
-                 ctypes_vp(xb), ldx, C, None, 0, ctypes_vp(ws_a.data_ptr() + bi * 32 * C * 4), None,
-                 1, 1, P, C, 32, 1, stream())
-            call("dv_conv_wgrad", dt(x), ctypes_vp(pbuf.data_ptr() + bi * P * 32 * esz), 32,
-                 ctypes_vp(dobuf.data_ptr() + bi * P * C * esz), C, C, None, 0,
-                 ctypes_vp(ws_v.data_ptr() + bi * 32 * C * 4), None, 1, 1, P, C, 32, 1, stream())
+             ptr(KtT), ptr(Vt), ptr(VtT), ptr(colsum), ptr(g2f), ptr(stats), ptr(pbuf), ptr(dobuf),
+             ptr(dsbuf), ptr(p2buf), ptr(mcorr), stream())
+        # per-batch token reductions: R = dS'^T X, V' = P^T dO, Q = P'^T dY (one batched GEMM each)
+        wsR = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
+        wsV = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
+        wsQ = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
+        for a_, b_, ldb, o_ in ((dsbuf, x, ldx, wsR), (pbuf, dobuf, C, wsV), (p2buf, dy, C, wsQ)):
+            _launch(f"conv_wgrad_kernel<{_lib.dtype_name(x)}>", 2.0 * ntok * 32 * C, 0,
+                    lambda a_=a_, b_=b_, ldb=ldb, o_=o_: call(
+                        "dv_gemm_tn_batched", dt(x), ptr(a_), 32, ptr(b_), ldb, ptr(o_), P, nb, 32, C,
+                        stream()))
         dat = torch.empty(nb, C, 24, dtype=torch.float32, device=dev)
         dvt = torch.empty_like(dat)
+        s1, s2 = _grad_out(g1p), _grad_out(g2p)
+        if s1 is not None and s2 is not None and s1[1] == s2[1]:
+            dg1, dg2, acc_g, ret_g = s1[0], s2[0], int(s1[1]), False
+        else:
+            dg1, dg2 = torch.empty(C, dtype=torch.float32, device=dev), torch.empty(C, dtype=torch.float32, device=dev)
+            acc_g, ret_g = 0, True
         sq, so, sn = _grad_out(wqp), _grad_out(wop), _grad_out(nullp)
         direct = sq is not None and so is not None and sn is not None and sq[1] == so[1] == sn[1]
         if direct:
-            dwq, dwo, dnull, acc = sq[0], so[0], sn[0], int(sq[1])
+            dwq, dwo, dnull, acc_w = sq[0], so[0], sn[0], int(sq[1])
         else:
-            dwq, dwo, dnull, acc = torch.empty_like(wqf), torch.empty_like(wof), torch.empty_like(nkv), 0
+            dwq, dwo, dnull, acc_w = torch.empty_like(wqf), torch.empty_like(wof), torch.empty_like(nkv), 0
         dkv = torch.empty_like(kv)
-        call("dv_xattn_fold_bwd", ptr(ws_a), ptr(ws_v), ptr(g1f), ptr(mcorr), ptr(wqf), ptr(wof),
-             ptr(kv), ptr(nkv), ptr(dat), ptr(dvt), ptr(dwq), ptr(dwo), ptr(dkv), ptr(dnull), nb, C,
-             ctypes_float(XA_DH ** -0.5), acc, stream())
-        # the workspaces are cached: re-zero them (dv_unpack_wgrad is not used here)
-        ws_a.zero_()
-        ws_v.zero_()
+        call("dv_xattn_fold_bwd", ptr(wsR), ptr(wsV), ptr(wsQ), ptr(mcorr), ptr(at), ptr(vt), ptr(g1f),
+             ptr(wqf), ptr(wof), ptr(kv), ptr(nkv), ptr(dat), ptr(dvt), ptr(dg1), ptr(dg2), ptr(dwq),
+             ptr(dwo), ptr(dkv), ptr(dnull), nb, C, ctypes_float(XA_DH ** -0.5), acc_g, acc_w, stream())
         dctx = torch.empty_like(ctxf)
         sk = _grad_out(wkvp)
         dwkv = sk[0] if sk else torch.empty_like(wkvf)
         call("dv_linear_small_bwd", ptr(dkv), dkv.shape[1], ptr(ctxf), ctxf.shape[1], ptr(wkvf), None,
              ptr(dctx), ctxf.shape[1], ptr(dwkv), None, ctxf.shape[0], ctxf.shape[1], dkv.shape[1],
              0, 0, 0, int(sk[1]) if sk else 0, stream())
-        return (dx, dctx.reshape(cshape), None if s1 else dg1, None if direct else dnull,
+        return (dx, dctx.reshape(cshape), dg1 if ret_g else None, None if direct else dnull,
                 None if direct else dwq, None if sk else dwkv, None if direct else dwo,
-                None if s2 else dg2, None, None)
+                dg2 if ret_g else None, None, None)
 
 
 def ctypes_vp(addr):

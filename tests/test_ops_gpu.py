@@ -117,12 +117,14 @@ def _ref_cross_attention(x_tok, ctx, g1, null_kv, wq, wkv, wo, g2, eps):
 
 
 @pytest.mark.parametrize("dtype,tol", DTYPES)
-@pytest.mark.parametrize("C", [64, 256])
-def test_cross_attention(dtype, tol, C):
+@pytest.mark.parametrize("C,T,H", [(64, 2, 8), (256, 2, 8), (16, 2, 4), (8, 2, 2), (48, 3, 3)])
+def test_cross_attention(dtype, tol, C, T, H):
+    # (16,2,4), (8,2,2), (48,3,3): channel counts below / not a multiple of one
+    # 32-channel MFMA tile and tokens per clip (T*H*W) not a multiple of 32
     from dalle2_video import ops
 
     g = torch.Generator().manual_seed(7)
-    nb, T, H, W = 2, 2, 8, 8
+    nb, W = 2, H
     x = torch.randn(nb * T, H, W, C, generator=g)
     ctx = torch.randn(nb, 2, 64, generator=g)
     g1 = 1 + 0.1 * torch.randn(C, generator=g)
