@@ -250,6 +250,22 @@ def split_args_and_kwargs(*args, split_size=None, **kwargs):
         yield size / batch, (cargs, ckw)
 
 
+def broadcast_parameters(module, src=0):
+    """DDP's init broadcast: every rank starts from rank `src`'s weights."""
+    for p in module.parameters():
+        dist.broadcast(p.data, src)
+
+
+def allreduce_flat_grad(flat_grad, world):
+    """The only collective on the data path: ONE all-reduce (SUM) of the active
+    unet's flat f32 gradient (RCCL over xGMI on the GPU box).  The 1/world
+    average is not applied here: it is folded into the clip coefficient
+    (dv_grad_clip_coef's prescale), which the AdamW kernel multiplies in."""
+    if world > 1 and flat_grad is not None:
+        dist.all_reduce(flat_grad)
+    return flat_grad
+
+
 class VideoDecoderTrainer(nn.Module):
     def __init__(self, decoder, accelerator=None, dataloaders=None, use_ema=True, lr=1e-4,
                  wd=1e-2, eps=1e-8, warmup_steps=None, cosine_decay_max_steps=None,
@@ -284,9 +300,8 @@ class VideoDecoderTrainer(nn.Module):
         self.register_buffer("steps", torch.tensor([0] * self.num_unets))
         self.train_loader = dataloaders["train"] if exists(dataloaders) else None
         self.val_loader = dataloaders["val"] if exists(dataloaders) else None
-        if self.world > 1:  # every rank starts from rank 0's weights (DDP init broadcast)
-            for p in decoder.parameters():
-                dist.broadcast(p.data, 0)
+        if self.world > 1:
+            broadcast_parameters(decoder, 0)
 
     @property
     def device(self):
@@ -315,8 +330,7 @@ class VideoDecoderTrainer(nn.Module):
         opt = getattr(self, f"optim{index}")
         sched = getattr(self, f"sched{index}")
         opt.ensure_flat()
-        if self.world > 1 and opt.flat_grad is not None:
-            dist.all_reduce(opt.flat_grad)  # RCCL over xGMI; 1/world folded below
+        allreduce_flat_grad(opt.flat_grad, self.world)
         coef = opt.clip_coefficient(self.max_grad_norm, prescale=1.0 / self.world)
         opt.step(clip_coef=coef)
         opt.zero_grad()

@@ -30,7 +30,7 @@ extern "C" {
 
 enum { DV_F32 = 0, DV_BF16 = 1 };
 enum { DV_OK = 0, DV_ERR_INVALID = -1, DV_ERR_LAUNCH = -2, DV_ERR_UNSUPPORTED = -3 };
-enum { DV_ACT_NONE = 0, DV_ACT_SILU = 1 };
+enum { DV_ACT_NONE = 0, DV_ACT_SILU = 1, DV_ACT_GELU = 2 };
 
 const char* dv_last_error(void);
 int dv_abi_version(void);
@@ -73,6 +73,168 @@ int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix,
  *   mode 1 (dgrad):    out[ci][tap'][co_pad] = w[co][ci][k*k-1-tap']      */
 int dv_pack_conv_weight(int dtype, const float* w, void* out, int cout, int cin, int ksize,
                         int pad_to, int mode, void* stream);
+
+/* Batched TN GEMM on the wgrad engine: out[g][i][j] += sum_{r in group g}
+ * A[r][i]*B[r][j]; A rows x m (lda), B rows x n (ldb), nbatch groups of
+ * batch_rows consecutive rows; out f32 [nbatch][m][n] (atomics, pre-zeroed).
+ * Used for the token reductions of the cross-attention backward.           */
+int dv_gemm_tn_batched(int dtype, const void* a, int lda, const void* b, int ldb, float* out,
+                       long long batch_rows, int nbatch, int m, int n, void* stream);
+
+/* ---- GroupNorm (+ FiLM scale/shift, SiLU, residual) -----------------------
+ * Block3D.norm/act with ResnetBlock3D's scale_shift (dalle2_video.py:109-133,
+ * 183-189): y = act(GN(z)*gamma + beta) (optionally *(ss_scale+1)+ss_shift,
+ * ss = [nb][2C] f32 with scale first), + res.  nb batch elements of P pixels
+ * (all frames of one clip form one GroupNorm sample), C channels, G groups.
+ * mean/rstd [nb][G] f32 are saved for the backward; ws is a scratch of
+ * nb*C*2 floats.  C % 8 == 0, C <= 256 vectors of 16 B.  act: DV_ACT_*.    */
+int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* res, int ldres,
+              int nb, long long P, int C, int G, float eps, const float* gamma,
+              const float* beta, const float* ss, int act, float* mean, float* rstd, float* ws,
+              void* stream);
+/* dz from dy (z is the pre-norm input); dgamma/dbeta [C] and dss [nb][2C]
+ * (+)= their gradients (accumulate != 0 adds).                               */
+int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void* dz, int lddz,
+              int nb, long long P, int C, int G, const float* gamma, const float* beta,
+              const float* ss, int act, const float* mean, const float* rstd, float* dgamma,
+              float* dbeta, float* dss, float* ws, int accumulate, void* stream);
+
+/* ---- row LayerNorm over channels (dalle2-pytorch LayerNorm, gain only, eps
+ * 1e-5 fp32; the mid-attention pre/post norms, dalle2_video.py:431, 551,
+ * 921-922).  y = (x-mu)*rstd*g (+b) (+res).  One wave per row; C a
+ * multiple of 16 bytes, at most 256 such vectors.                           */
+int dv_ln_fwd(int dtype, const void* x, int ldx, void* y, int ldy, const void* res, int ldres,
+              long long rows, int C, const float* g, const float* b, float eps, float* mean,
+              float* rstd, void* stream);
+int dv_ln_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, void* dx, int lddx,
+              long long rows, int C, const float* g, float eps, float* dg, float* db, void* stream);
+
+/* ---- layout, space-to-depth / pixel shuffle --------------------------------
+ * NCTHW f32 <-> channels-last frames (cpad: padded channel stride, zeros).  */
+int dv_ncthw_to_cl(int dtype, const float* x, void* y, int B, int C, int T, int H, int W, int cpad,
+                   void* stream);
+int dv_cl_to_ncthw(int dtype, const void* y, int ld, float* x, int B, int C, int T, int H, int W,
+                   void* stream);
+/* mode 0: space-to-depth 2x2 (Downsample3D's "(h 2) (w 2) -> (c 4)",
+ * dalle2_video.py:18-30), src [nf][H][W][C] -> dst [nf][H/2][W/2][4C];
+ * mode 1: PixelShuffle(2) after SiLU (PixelShuffleUpsample3D,
+ * dalle2_video.py:64-79), src [nf][H][W][4C] -> dst [nf][2H][2W][C];
+ * backward passes use the inverse mode, with z (the pre-SiLU conv output)
+ * for SiLU' when act = DV_ACT_SILU.                                         */
+int dv_shuffle(int dtype, int mode, const void* src, int lds, void* dst, int ldd, const void* z,
+               int ldz, int nf, int H, int W, int C, int act, void* stream);
+
+/* ---- diffusion step pieces (VideoDecoder.p_losses, dalle2_video.py:1908-2010)
+ * x_noisy = sqrt_ac[t]*x0 + sqrt_1m_ac[t]*noise, written channels-last into
+ * y (cpad stride); normalize != 0 maps x0 from [0,1] to [-1,1] first
+ * (normalize_neg_one_to_one, :1277, 1947-1956).                             */
+int dv_q_sample(int dtype, const float* x0, const float* noise, const long long* t,
+                const float* sqrt_ac, const float* sqrt_1m_ac, void* y, int B, int C, int T,
+                int H, int W, int cpad, int normalize, void* stream);
+/* loss = mean_b( w[b] * mean_(c,t,h,w) (pred - target)^2 )   (:1997-2000;
+ * sample_w = p2 loss weights, NULL = 1).  loss: one f32, overwritten.        */
+int dv_mse_loss(int dtype, const void* pred, int ld, const float* target, int B, int C, int T,
+                int H, int W, const float* sample_w, float* loss, void* stream);
+int dv_mse_loss_bwd(int dtype, const void* pred, int ld, const float* target, int B, int C, int T,
+                    int H, int W, const float* sample_w, const float* dloss, void* dpred, int lddp,
+                    void* stream);
+/* one ancestral DDPM step (VideoDecoder.p_sample, :1621-1665, with
+ * NoiseScheduler.q_posterior and predict_start_from_noise): eps is the unet
+ * output (channels-last, stride ld; ld == 0: NCTHW f32).  clip != 0 clamps
+ * x0 to [-1,1].  out and (optional) x0_out are NCTHW f32.                    */
+int dv_p_sample(int dtype, const float* x, const void* eps, int ld, const float* noise,
+                const long long* t, const float* sqrt_recip_ac, const float* sqrt_recipm1_ac,
+                const float* coef1, const float* coef2, const float* logvar, float* out,
+                float* x0_out, int B, int C, int T, int H, int W, int clip, void* stream);
+
+/* ---- time conditioning MLPs (Unet3D.to_time_hiddens / to_time_tokens /
+ * to_time_cond, dalle2_video.py:348-357; ResnetBlock3D.time_mlp, :152-155)
+ * SinusoidalPosEmb (:349): out[b] = [sin(t*f), cos(t*f)], freqs = dim/2
+ * host-built f32 frequencies (bit-identical to the torch expression).       */
+int dv_sinusoidal(const long long* t, const float* freqs, float* out, int B, int dim, void* stream);
+/* y = act_out(act_in(x) W^T + bias), B rows (the batch; <= 16 for the
+ * backward), f32;
+ * act_in: DV_ACT_SILU or none; act_out: none / SiLU / 2 = GELU (erf).
+ * z (optional) keeps the pre-activation for the backward.                   */
+int dv_linear_small_fwd(const float* x, int ldx, const float* W, const float* bias, float* y,
+                        int ldy, float* z, int B, int K, int N, int act_in, int act_out,
+                        void* stream);
+int dv_linear_small_bwd(const float* dy, int lddy, const float* x, int ldx, const float* W,
+                        const float* z, float* dx, int lddx, float* dW, float* db, int B, int K,
+                        int N, int act_in, int act_out, int accumulate_dx, int accumulate_w,
+                        void* stream);
+
+/* ---- optimizer (trainer.py:65 get_optimizer -> torch AdamW; :254-257
+ * clip_grad_norm_).  Flat f32 buffers; elements [0, n_wd) get weight decay
+ * (ndim >= 2 parameters).  clip_coef: device scalar multiplying g (NULL: 1). */
+int dv_adamw(float* p, const float* g, float* m, float* v, long long n, long long n_wd, float lr,
+             float beta1, float beta2, float eps, float wd, float bc1, float bc2_sqrt,
+             const float* clip_coef, void* stream);
+/* ws[1] = prescale * min(max_norm / (||prescale*g|| + 1e-6), 1), ws[2] = the
+ * norm (torch clip_grad_norm_ semantics; prescale = 1/world after the RCCL
+ * sum).  ws: 4 floats, ws[0] scratch.  max_norm <= 0: no clipping.          */
+int dv_grad_clip_coef(const float* g, long long n, float max_norm, float prescale, float* ws,
+                      void* stream);
+
+/* ---- low-resolution conditioning (LowresVideoConditioner,
+ * dalle2_video.py:1044-1112): resize_video_to (nearest, PyTorch index rule,
+ * optional clamp) and the per-frame gaussian_blur2d (reflect padding, odd
+ * ks, w1 = normalised 1-D kernel).  planes = B*C*T images, f32.             */
+int dv_resize_nearest(const float* x, float* y, long long planes, int hin, int win, int hout,
+                      int wout, int do_clamp, float lo, float hi, void* stream);
+int dv_gaussian_blur(const float* x, float* y, long long planes, int H, int W, int ks,
+                     const float* w1, void* stream);
+
+/* ---- ResnetBlock3D cross attention (dalle2_video.py:159-162, 192-201;
+ * dalle2-pytorch CrossAttention, 8 heads x 64, null kv + 2 time tokens, LN
+ * before/after, residual).  Projections fold per clip b into C x 24
+ * matrices: dv_xattn_fold computes at/vt [nb][C][24]
+ * f32 and the MFMA operand images Kt,VtT [nb][32][Cp], KtT,Vt [nb][Cp][32]
+ * (Cp = roundup(C,32)) and colsum [nb][32]; kv [nb][2][1024] f32 is the
+ * to_kv projection of the context tokens.                                    */
+int dv_xattn_fold(int dtype, const float* wq, const float* wo, const float* kv,
+                  const float* null_kv, const float* g1, float* at, float* vt, void* Kt, void* KtT,
+                  void* Vt, void* VtT, float* colsum, int nb, int C, float scale, void* stream);
+/* out = LN_g2(attn(LN_g1(x))) + x over ntok = nb*P tokens (P per clip, any
+ * P; C % 8 == 0).  stats [ntok][4] f32 and pbuf [ntok][32] are saved.       */
+int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ldo, long long ntok,
+                 long long P, int C, const void* Kt, const void* Vt, const float* colsum,
+                 const float* g2, float eps, float* stats, void* pbuf, void* stream);
+/* token part of the backward: dx (incl. residual); dobuf [ntok][C], dsbuf
+ * and p2buf [ntok][32] feed three dv_gemm_tn_batched reductions; mcorr
+ * [nb][32] f32 (pre-zeroed) accumulates the LN mean correction.             */
+int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const void* x, int ldx, void* dx,
+                        int lddx, long long ntok, long long P, int C, const void* KtT,
+                        const void* Vt, const void* VtT, const float* colsum, const float* g2,
+                        const float* stats, const void* pbuf, void* dobuf, void* dsbuf,
+                        void* p2buf, float* mcorr, void* stream);
+/* parameter part: from the GEMM results wsR/wsV/wsQ [nb][32][C] to
+ * dg1, dg2 (acc_g), dwq [512][C], dwo [C][512], dnull [2][64] (acc_w) and
+ * dkv [nb][2][1024] (overwritten).                                          */
+int dv_xattn_fold_bwd(const float* wsR, const float* wsV, const float* wsQ, const float* mcorr,
+                      const float* at, const float* vt, const float* g1, const float* wq,
+                      const float* wo, const float* kv, const float* null_kv, float* dat,
+                      float* dvt, float* dg1, float* dg2, float* dwq, float* dwo, float* dkv,
+                      float* dnull, int nb, int C, float scale, int acc_g, int acc_w,
+                      void* stream);
+
+/* ---- mid self-attention (Unet3D.mid_attn = Residual(Attention(mid_dim)),
+ * dalle2_video.py:431, 551, 921-922; dalle2-pytorch Attention: 16 heads x 32,
+ * ONE shared k/v head (multi-query), learned null k/v at key 0, q scaled
+ * twice by 32^-0.5 with cosine-sim off -> logit factor 1/32).
+ * prep: kv [B][N][*] (k at 0, v at 32, stride ldkv) -> kp/vp [B][NKP][32]
+ * (row 0 null, rows > N zero; NKP = roundup(N+1, 32)).                      */
+int dv_mqa_prep(int dtype, const void* kv, int ldkv, const float* null_kv, void* kp, void* vp,
+                int B, int N, int NKP, void* stream);
+/* o[b][n][h*32+d] = softmax_j(scale * q.k_j) v_j; lse [B][H][N] f32 saved.   */
+int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, const void* vp, void* o, int ldo,
+               float* lse, int B, int N, int NKP, int H, float scale, void* stream);
+/* dq, dkv (k at 0, v at 32, stride lddkv) and dnull (+)= (accumulate);
+ * D [B][H][N], dkp/dvp [B][NKP][32] f32 are scratch (dkp/dvp pre-zeroed).   */
+int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int ldo, const void* dout,
+               int lddo, const float* lse, const void* kp, const void* vp, void* dq, int lddq,
+               float* D, float* dkp, float* dvp, void* dkv, int lddkv, float* dnull, int B, int N,
+               int NKP, int H, float scale, int accumulate, void* stream);
 
 #ifdef __cplusplus
 }

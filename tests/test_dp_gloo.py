@@ -1,0 +1,125 @@
+"""Data-parallel path on CPU (gloo, world_size 2), no GPU needed.
+
+Checks the two collectives the trainer uses (trainer.broadcast_parameters at
+init, trainer.allreduce_flat_grad per update) and the DP identity they
+implement: the 1/world-scaled SUM of per-rank gradients over disjoint halves
+of a batch equals the single-process gradient of the whole batch (p_losses is
+a batch mean).  Gradients come from the CPU oracle unet (the product forward
+is GPU-only); the exchange code is the product's.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _small_oracle_unet():
+    from oracle import dv_ref as R
+
+    u = R.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    u = u.cast_model_parameters(lowres_cond=False, lowres_noise_cond=False, channels=3,
+                                channels_out=3, cond_on_image_embeds=True,
+                                cond_on_text_encodings=False)
+    return R.deterministic_fill_(u)
+
+
+def _grads(u, x, times, noise):
+    from oracle import dv_ref as R
+
+    sched = R.NoiseScheduler(beta_schedule="cosine", timesteps=1000, loss_type="l2")
+    u.zero_grad(set_to_none=True)
+    R.p_losses(u, sched, x, times, noise, video_cond_drop_prob=0.0, text_cond_drop_prob=0.0).backward()
+    return torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
+                      for p in u.parameters()])
+
+
+def _worker(rank, world, port, q):
+    import sys
+
+    for p in (ROOT, os.path.join(ROOT, "dalle2-video_amd")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dalle2_video import dalle2_video as D
+        from dalle2_video.trainer import VideoDecoderTrainer, allreduce_flat_grad
+
+        # 1) init broadcast through the real trainer: ranks start from different weights
+        torch.manual_seed(100 + rank)
+        u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+        dec = D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(4,), timesteps=1000,
+                             learned_variance=False)
+        with torch.no_grad():
+            for p in dec.parameters():
+                p.normal_()
+        tr = VideoDecoderTrainer(dec, lr=3e-4, use_ema=False)
+        assert tr.world == world
+        flat = torch.cat([p.detach().reshape(-1) for p in dec.parameters()])
+        gathered = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(gathered, flat)
+        ok_bcast = all(torch.equal(gathered[0], t) for t in gathered)
+
+        # 2) DP identity with the product's all-reduce
+        g = torch.Generator().manual_seed(1234)
+        x = torch.rand(4, 3, 4, 32, 32, generator=g)
+        times = torch.tensor([537, 3, 999, 41])
+        noise = torch.randn(x.shape, generator=g)
+        ou = _small_oracle_unet()
+        full = _grads(ou, x, times, noise)
+        sl = slice(2 * rank, 2 * rank + 2)
+        mine = _grads(ou, x[sl], times[sl], noise[sl])
+        allreduce_flat_grad(mine, world)
+        avg = mine / world
+        err = ((avg - full).norm() / full.norm()).item()
+        q.put((rank, ok_bcast, err))
+    except BaseException as e:  # report instead of leaving the parent waiting
+        import traceback
+
+        q.put((rank, False, f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_gloo_world2_broadcast_and_grad_allreduce():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=300) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, ok_bcast, err in res:
+        assert not isinstance(err, str), f"rank {rank} failed:\n{err}"
+        assert ok_bcast, f"rank {rank}: parameters differ after the init broadcast"
+        assert err < 1e-5, f"rank {rank}: averaged DP gradient differs from full batch ({err:.2e})"
+
+
+def test_allreduce_is_identity_single_process():
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "dalle2-video_amd"))
+    from dalle2_video.trainer import allreduce_flat_grad
+
+    t = torch.arange(5.0)
+    assert allreduce_flat_grad(t, 1) is t and torch.equal(t, torch.arange(5.0))
+    assert allreduce_flat_grad(None, 2) is None

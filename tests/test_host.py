@@ -1,0 +1,139 @@
+"""Host-side logic of the drop-in package that runs without a GPU: module
+wiring and state-dict layout identical to the oracle's (which is pinned to the
+reference's, G2), the deterministic weight fill shared with the oracle, loud
+failure of the compute path on CPU tensors (no fallback), and the trainer's
+pure-Python helpers (optimizer grouping, warmup, EMA schedule, batch split).
+"""
+import math
+
+import pytest
+import torch
+
+from oracle import dv_ref as R
+
+
+def _both(dim, mults, lowres):
+    from dalle2_video import dalle2_video as D
+
+    out = []
+    for mod in (R, D):
+        u = mod.Unet3D(dim, video_embed_dim=512, channels=3, dim_mults=mults,
+                       cond_on_text_encodings=False)
+        out.append(u.cast_model_parameters(lowres_cond=lowres, lowres_noise_cond=False, channels=3,
+                                           channels_out=3, cond_on_image_embeds=not lowres,
+                                           cond_on_text_encodings=False))
+    return out
+
+
+@pytest.mark.parametrize("dim,mults,lowres,nkeys,nparams", [
+    (64, (1, 2, 4, 8), False, 439, 49_967_171),
+    (8, (1, 2, 4, 8, 16), True, 539, 4_203_412),
+])
+def test_state_dict_layout_matches_oracle(dim, mults, lowres, nkeys, nparams):
+    o, p = _both(dim, mults, lowres)
+    so, sp = o.state_dict(), p.state_dict()
+    assert list(so.keys()) == list(sp.keys())
+    assert len(sp) == nkeys
+    assert all(so[k].shape == sp[k].shape for k in so)
+    assert sum(t.numel() for t in p.parameters()) == nparams
+    assert p.cond_on_video_embeds is False  # cast quirk: embed conditioning off
+    p.load_state_dict(so, strict=True)
+
+
+def test_deterministic_fill_identical_to_oracle():
+    from dalle2_video.utils import deterministic_fill_
+
+    o, p = _both(16, (1, 2, 4, 8), False)
+    R.deterministic_fill_(o)
+    deterministic_fill_(p)
+    for (n, a), (_, b) in zip(o.named_parameters(), p.named_parameters()):
+        assert torch.equal(a, b), n
+
+
+def test_compute_path_fails_loudly_on_cpu():
+    from dalle2_video import dalle2_video as D
+    from dalle2_video._lib import DVError
+
+    u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    x, t = torch.randn(1, 3, 4, 32, 32), torch.tensor([5])
+    with pytest.raises(DVError, match="GPU only"):
+        u(x, t)
+    dec = D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(4,), timesteps=1000,
+                         learned_variance=False)
+    with pytest.raises(DVError):
+        dec(x, unet_number=1)
+
+
+def test_out_of_path_features_raise():
+    from dalle2_video import dalle2_video as D
+
+    u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    with pytest.raises(NotImplementedError):
+        D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(4,), learned_variance=True)
+
+
+def test_get_optimizer_groups_match_reference_rule():
+    from dalle2_video.trainer import FusedAdamW, get_optimizer
+
+    _, p = _both(16, (1, 2, 4, 8), False)
+    opt = get_optimizer(p.parameters(), lr=3e-4, wd=1e-2)
+    assert isinstance(opt, FusedAdamW)
+    g0, g1 = opt.param_groups
+    assert all(t.ndim >= 2 for t in g0["params"]) and g0["weight_decay"] == 1e-2
+    assert all(t.ndim < 2 for t in g1["params"]) and g1["weight_decay"] == 0.0
+    assert g0["betas"] == (0.9, 0.99) and g0["eps"] == 1e-8
+    assert len(g0["params"]) + len(g1["params"]) == len(list(p.parameters()))
+    opt0 = get_optimizer(p.parameters(), lr=1e-4, wd=0)
+    assert len(opt0.param_groups) == 1 and opt0.param_groups[0]["weight_decay"] == 0.0
+
+
+def test_linear_warmup_dampening():
+    from dalle2_video.trainer import _LinearWarmup
+
+    opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=1.0)
+    w = _LinearWarmup(opt, 4)
+    lrs = []
+    for _ in range(3):
+        opt.param_groups[0]["lr"] = 1.0  # what the base scheduler restores
+        with w.dampening():
+            pass
+        lrs.append(opt.param_groups[0]["lr"])
+    assert lrs == [0.25, 0.5, 0.75]
+
+
+def test_ema_schedule():
+    from dalle2_video.trainer import EMA
+
+    m = torch.nn.Linear(2, 2)
+    ema = EMA(m, beta=0.9999, update_after_step=100, update_every=10)
+    ema.step.fill_(111)
+    epoch = 111 - 100 - 1
+    assert math.isclose(ema._decay(), 1 - (1 + epoch) ** (-2 / 3), rel_tol=1e-12)
+    ema.step.fill_(50)
+    assert ema._decay() == 0.0
+    with torch.no_grad():
+        m.weight.fill_(3.0)
+    ema.step.fill_(0)
+    ema.update()  # first update copies the online weights
+    assert torch.equal(ema.ema_model.weight, m.weight)
+
+
+def test_split_args_and_kwargs():
+    from dalle2_video.trainer import split_args_and_kwargs
+
+    x = torch.arange(10).reshape(5, 2)
+    chunks = list(split_args_and_kwargs(x, split_size=2, video_embed=torch.zeros(5, 3), flag=True))
+    assert [round(f, 6) for f, _ in chunks] == [0.4, 0.4, 0.2]
+    assert sum(f for f, _ in chunks) == pytest.approx(1.0)
+    (a,), kw = chunks[-1][1]
+    assert a.shape == (1, 2) and kw["video_embed"].shape == (1, 3) and kw["flag"] is True
+    assert list(split_args_and_kwargs(x, split_size=None))[0][0] == 1.0
+
+
+def test_sinusoid_freqs_match_torch_expression():
+    from dalle2_video import ops
+
+    for dim in (16, 64, 128):
+        half = dim // 2
+        ref = torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1)))
+        assert torch.equal(ops.sinusoid_freqs(dim, "cpu"), ref.float())
