@@ -82,6 +82,55 @@ __device__ __forceinline__ void load4<bf16>(const bf16* src, float* v) {
   v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
 }
 
+// epilogue: lane owns pixel column r of each 32-pixel tile; channels
+// 8g + 4h + e of each 32-channel tile.  y = act(acc + bias) + res.
+template <typename T, int TI, int TJ>
+__device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32x16 (&acc)[TJ][TI],
+                                              long long mb, int nb, int r, int h) {
+  const bool vec_ok = ((p.ldy & 3) == 0) && (p.res == nullptr || (p.ldres & 3) == 0);
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const long long m = mb + 32 * i + r;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = nb + 32 * j + 8 * g + 4 * h;
+        if (n >= p.cout) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[j][i][4 * g + e];
+        if (vec_ok && n + 3 < p.cout) {
+          if (p.bias) {
+            f32x4 b = *(const f32x4*)(p.bias + n);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += b[e];
+          }
+          if (p.act == DV_ACT_SILU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
+          }
+          if (p.res) {
+            float rr[4];
+            load4<T>(p.res + m * p.ldres + n, rr);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += rr[e];
+          }
+          store4<T>(p.y + m * p.ldy + n, v);
+        } else {
+          for (int e = 0; e < 4 && n + e < p.cout; ++e) {
+            float t = v[e] + (p.bias ? p.bias[n + e] : 0.f);
+            if (p.act == DV_ACT_SILU) t = silu_f(t);
+            if (p.res) t += (float)p.res[m * p.ldres + n + e];
+            p.y[m * p.ldy + n + e] = (T)t;
+          }
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int BM, int BN>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs<T> p) {
   constexpr int VEC = 16 / sizeof(T);
@@ -189,49 +238,146 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs<T> p) {
     __syncthreads();
   }
 
-  // epilogue: lane owns pixel column r; channels 8g + 4h + e in each 32-tile
-  const bool vec_ok = ((p.ldy & 3) == 0) && (p.res == nullptr || (p.ldres & 3) == 0);
+  conv_epilogue<T, TI, TJ>(p, acc, m0 + wm * 32 * TI, n0 + wn * 32 * TJ, r, h);
+}
+
+
+// ---------------------------------------------------------------------------
+// bf16 forward, cin % 64 == 0: LDS-DMA (global_load_lds_dwordx4) staging,
+// BK = 64 (one 128-B row per pixel / per output channel and K-tile; a K-tile
+// is 64 input channels of ONE tap), two LDS buffers, one K-tile in flight
+// across the raw barrier (counted vmcnt).  LDS images are lane-linear (the
+// DMA writes base + lane*16); the 16-B chunk XOR swizzle is applied to the
+// SOURCE address and undone on the ds_read_b128 (both sides, same involution).
+// Out-of-image taps and tail pixels / channels read a zeroed 16-B line.
+// Block ids are remapped so each XCD owns a contiguous pixel range (its
+// im2col halos and all cout tiles of a pixel tile share that XCD's L2).
+// ---------------------------------------------------------------------------
+__device__ __attribute__((aligned(64))) unsigned int g_zero_line[16];
+
+__device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p, int tiles_n) {
+  constexpr int TI = BM / 64, TJ = BN / 64;
+  constexpr int GB = BM / 32, GA = BN / 32;  // DMA instructions per thread per K-tile
+  constexpr int BUF = (BM + BN) * 128;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+
+  // XCD-aware bijective remap of the 1-D block id
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg >> 3, rr8 = nwg & 7, xcd = orig & 7;
+  const int wg = (xcd < rr8 ? xcd * (q + 1) : rr8 * (q + 1) + (xcd - rr8) * q) + (orig >> 3);
+  const int tn = wg % tiles_n;
+  const long long m0 = (long long)(wg / tiles_n) * BM;
+  const int n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int HW = p.H * p.W, pad = p.ks >> 1;
+  const int cblocks = p.cin >> 6;
+  const int chunk = lane & 7;
+
+  // pixel rows this thread DMAs: row = 32*i + (tid >> 3).  Offsets are 32-bit
+  // (the dispatcher guarantees M*ld < 2^31); invalid rows get y = -2^20 so
+  // every tap of them selects the zero line.
+  int b_y[GB], b_x[GB], b_pix[GB];
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
-    const long long m = m0 + wm * 32 * TI + 32 * i + r;
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n = n0 + wn * 32 * TJ + 32 * j + 8 * g + 4 * h;
-        if (n >= p.cout) continue;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[j][i][4 * g + e];
-        if (vec_ok && n + 3 < p.cout) {
-          if (p.bias) {
-            f32x4 b = *(const f32x4*)(p.bias + n);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += b[e];
-          }
-          if (p.act == DV_ACT_SILU) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
-          }
-          if (p.res) {
-            float rr[4];
-            load4<T>(p.res + m * p.ldres + n, rr);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += rr[e];
-          }
-          store4<T>(p.y + m * p.ldy + n, v);
-        } else {
-          for (int e = 0; e < 4 && n + e < p.cout; ++e) {
-            float t = v[e] + (p.bias ? p.bias[n + e] : 0.f);
-            if (p.act == DV_ACT_SILU) t = silu_f(t);
-            if (p.res) t += (float)p.res[m * p.ldres + n + e];
-            p.y[m * p.ldy + n + e] = (T)t;
-          }
-        }
-      }
-    }
+  for (int i = 0; i < GB; ++i) {
+    const int row = 32 * i + (tid >> 3);
+    const long long m = m0 + row;
+    const bool ok = m < p.M;
+    const int mi = ok ? (int)m : 0;
+    const int f = mi / HW;
+    const int rem = mi - f * HW;
+    const int y = rem / p.W;
+    b_y[i] = ok ? y : -(1 << 20);
+    b_x[i] = rem - y * p.W;
+    b_pix[i] = mi;
   }
+  const bf16* zero = (const bf16*)g_zero_line;
+  const int a_rowoff = (tid >> 3);
+
+  auto issue = [&](int kt, int buf) {
+    const int tap = kt / cblocks;
+    const int ci = ((kt - tap * cblocks) << 6);
+    const int dy = tap / p.ks - pad, dx = tap % p.ks - pad;
+    const int doff = dy * p.W + dx;
+    const bool first = ci < p.c0;  // wave-uniform: the 64-channel block never straddles c0
+    const bf16* xb = first ? p.x0 + ci : p.x1 + (ci - p.c0);
+    const int ld = first ? p.ld0 : p.ld1;
+    char* sB = smem + buf * BUF;
+    char* sA = sB + BM * 128;
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int row = 32 * i + (tid >> 3);
+      const int cs = chunk ^ swz8(row);
+      const int yy = b_y[i] + dy, xx = b_x[i] + dx;
+      const bool in = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      const bf16* src = in ? xb + ((b_pix[i] + doff) * ld + cs * 8) : zero;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(sB + (32 * i + 8 * wave) * 128),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int row = 32 * i + a_rowoff;
+      const int cs = chunk ^ swz8(row);
+      const int n = n0 + row;
+      const bf16* src = n < p.cout ? p.w + ((long long)n * p.K + (kt << 6) + cs * 8) : zero;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(sA + (32 * i + 8 * wave) * 128),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x16 acc[TJ][TI];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+
+  const int r = lane & 31, h = lane >> 5;
+  const int nk = (p.K >> 6);
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) {
+      issue(kt + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GA + GB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* sB = smem + buf * BUF;
+    const char* sA = sB + BM * 128;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = 2 * s + h;
+      u32x4 wa[TJ], xb[TI];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int row = wn * 32 * TJ + 32 * j + r;
+        wa[j] = *(const u32x4*)(sA + row * 128 + ((c ^ swz8(row)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int row = wm * 32 * TI + 32 * i + r;
+        xb[i] = *(const u32x4*)(sB + row * 128 + ((c ^ swz8(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[j][i] = Mma<bf16>::run(wa[j], xb[i], acc[j][i]);
+    }
+    // every wave's reads of `buf` are done before the next iteration re-fills it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  conv_epilogue<bf16, TI, TJ>(p, acc, m0 + wm * 32 * TI, n0 + wn * 32 * TJ, r, h);
 }
 
 // ---------------------------------------------------------------------------
@@ -509,6 +655,21 @@ int launch_fwd(const ConvFwdArgs<T>& a, hipStream_t st) {
   return check_launch("conv_fwd");
 }
 
+template <int BM, int BN>
+int launch_fwd_glds(const ConvFwdArgs<bf16>& a, hipStream_t st) {
+  const int tn = (a.cout + BN - 1) / BN;
+  const long long nb = ((a.M + BM - 1) / BM) * tn;
+  conv_fwd_glds_kernel<BM, BN><<<(unsigned)nb, 256, 0, st>>>(a, tn);
+  return check_launch("conv_fwd_glds");
+}
+
+// tile choice for the glds path (mirrored by ops.conv_tile for kernel naming)
+inline void glds_tile(long long M, int cout, int& bm, int& bn) {
+  bn = cout <= 64 ? 64 : 128;
+  bm = bn == 64 ? 256 : 128;
+  if (((M + bm - 1) / bm) * ((cout + bn - 1) / bn) < 512) bm = 128;
+}
+
 template <typename T>
 int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const void* w,
                const float* bias, const void* res, int ldres, void* y, int ldy, int nf, int h,
@@ -519,6 +680,16 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
   a.ldres = ldres; a.y = (T*)y; a.ldy = ldy; a.H = h; a.W = wd; a.cin = cin; a.cout = cout;
   a.ks = ks; a.act = act; a.M = (long long)nf * h * wd; a.K = ks * ks * cin;
   if (a.M == 0 || cout == 0) return DV_OK;
+  if constexpr (sizeof(T) == 2) {
+    const long long maxld = ld0 > (x1 ? ld1 : 0) ? ld0 : ld1;
+    if (cin % 64 == 0 && a.c0 % 64 == 0 && a.M * maxld < (1ll << 31)) {
+      int bm, bn;
+      glds_tile(a.M, cout, bm, bn);
+      if (bm == 256) return launch_fwd_glds<256, 64>(a, st);
+      if (bn == 64) return launch_fwd_glds<128, 64>(a, st);
+      return launch_fwd_glds<128, 128>(a, st);
+    }
+  }
   const long long mt128 = (a.M + 127) / 128;
   int bn = cout <= 64 ? 64 : 128;
   int bm = 128;

@@ -410,29 +410,43 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
   }
 }
 
-// dat/dvt [nb][C][24] from the GEMM results (ws_* [nb][32][C]) and the LN gain grads
-__global__ void fold_grad_finish_kernel(const float* wsR, const float* wsV, const float* wsQ,
-                                        const float* mcorr, const float* at, const float* vt,
-                                        const float* g1, float* dat, float* dvt, float* dg1,
-                                        float* dg2, int nb, int C, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// dat/dvt [nb][C][24] from the GEMM results (ws_* [nb][32][C]) and the LN gain
+// grads.  grid (ceil(C/64), nb), 256 threads = 64 channels x 4 groups of 6
+// folded columns; dg1/dg2 (pre-zeroed unless accumulating) take one atomic
+// per (b, c).
+__global__ __launch_bounds__(256) void fold_grad_finish_kernel(
+    const float* wsR, const float* wsV, const float* wsQ, const float* mcorr, const float* at,
+    const float* vt, const float* g1, float* dat, float* dvt, float* dg1, float* dg2, int nb,
+    int C) {
+  __shared__ float red[2][4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
   float s1 = 0.f, s2 = 0.f;
-  for (int b = 0; b < nb; ++b) {
-    for (int hj = 0; hj < HK; ++hj) {
+  if (c < C) {
+    const float g = g1[c];
+#pragma unroll
+    for (int q = 0; q < HK / 4; ++q) {
+      const int hj = grp * (HK / 4) + q;
       const int kp = kprime(hj);
       const long long wi = ((long long)b * KP + kp) * C + c;
       const long long fi = ((long long)b * C + c) * HK + hj;
       const float dk = wsR[wi] - mcorr[b * KP + kp];
-      dat[fi] = g1[c] * dk;
+      dat[fi] = g * dk;
       s1 += at[fi] * dk;
       dvt[fi] = wsV[wi];
       s2 += vt[fi] * wsQ[wi];
     }
-    s2 -= wsQ[((long long)b * KP + 3) * C + c];
+    if (grp == 0) s2 -= wsQ[((long long)b * KP + 3) * C + c];
   }
-  if (dg1) dg1[c] = accumulate ? dg1[c] + s1 : s1;
-  if (dg2) dg2[c] = accumulate ? dg2[c] + s2 : s2;
+  red[0][grp][cl] = s1;
+  red[1][grp][cl] = s2;
+  __syncthreads();
+  if (grp == 0 && c < C) {
+    const float t1 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    const float t2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+    if (dg1) atomicAdd(dg1 + c, t1);
+    if (dg2) atomicAdd(dg2 + c, t2);
+  }
 }
 
 // parameter grads of the fold: dWq, dWo
@@ -463,42 +477,59 @@ __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const floa
   }
 }
 
-// dK/dV of (b, h, j) -> d(kv) (j >= 1) or dnull (j == 0); one block per (b,h,j)
+// dK/dV of (b, h, all 3 keys) -> d(kv) (j >= 1) or dnull (j == 0).
+// grid (NH, nb, 2): z = 0 computes dK = scale * dat[:, hj]^T Wq_h^T (wave w owns
+// 16 head dims, lanes sweep c, wave reductions); z = 1 computes
+// dV = dvt[:, hj]^T Wo_h (lane = head dim, coalesced Wo rows, waves split c).
 __global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, const float* dvt,
                                                           const float* wq, const float* wo,
-                                                          float* dkv, float* dnull, int nb, int C,
+                                                          float* dkv, float* dnull, int C,
                                                           float scale) {
-  __shared__ float red[4][DH];
-  __shared__ float dks[DH];
-  const int bhj = blockIdx.x;
-  const int j = bhj % NK, h = (bhj / NK) % NH, b = bhj / (NK * NH);
-  const int hj = h * NK + j;
+  __shared__ float red[4][NK][DH];
+  const int h = blockIdx.x, b = blockIdx.y, part = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // dK[d] = scale * sum_c dat[c][hj] Wq[h*64+d][c]: wave w owns 16 d, lanes sweep c
-  for (int dd = 0; dd < DH / 4; ++dd) {
-    const int d = w * (DH / 4) + dd;
-    float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += dat[((long long)b * C + c) * HK + hj] * wq[(long long)(h * DH + d) * C + c];
-    s = wave_sum(s);
-    if (lane == 0) dks[d] = s * scale;
-  }
-  // dV[d] = sum_c dvt[c][hj] Wo[c][h*64+d]: lane = d, 4 c-slices
-  {
-    float s = 0.f;
-    for (int c = w; c < C; c += 4) s += dvt[((long long)b * C + c) * HK + hj] * wo[(long long)c * (NH * DH) + h * DH + lane];
-    red[w][lane] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x < DH) {
-    const int d = threadIdx.x;
-    const float dv = red[0][d] + red[1][d] + red[2][d] + red[3][d];
-    if (j == 0) {
-      atomicAdd(dnull + d, dks[d]);
-      atomicAdd(dnull + DH + d, dv);
-    } else {
-      dkv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + h * DH + d] = dks[d];
-      dkv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + NH * DH + h * DH + d] = dv;
+  const float* datb = dat + (long long)b * C * HK + h * NK;
+  const float* dvtb = dvt + (long long)b * C * HK + h * NK;
+  auto emit = [&](int j, int d, float v) {
+    if (j == 0) atomicAdd(dnull + part * DH + d, v);
+    else dkv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + part * NH * DH + h * DH + d] = v;
+  };
+  if (part == 0) {
+    for (int dd = 0; dd < DH / 4; ++dd) {
+      const int d = w * (DH / 4) + dd;
+      const float* wrow = wq + (long long)(h * DH + d) * C;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+      for (int c = lane; c < C; c += 64) {
+        const float wv = wrow[c];
+        const float* dr = datb + (long long)c * HK;
+        s0 += dr[0] * wv;
+        s1 += dr[1] * wv;
+        s2 += dr[2] * wv;
+      }
+      s0 = wave_sum(s0);
+      s1 = wave_sum(s1);
+      s2 = wave_sum(s2);
+      if (lane == 0) {
+        emit(0, d, s0 * scale);
+        emit(1, d, s1 * scale);
+        emit(2, d, s2 * scale);
+      }
     }
+  } else {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll 4
+    for (int c = w; c < C; c += 4) {
+      const float wv = wo[(long long)c * (NH * DH) + h * DH + lane];
+      const float* dr = dvtb + (long long)c * HK;
+      s0 += dr[0] * wv;
+      s1 += dr[1] * wv;
+      s2 += dr[2] * wv;
+    }
+    red[w][0][lane] = s0;
+    red[w][1][lane] = s1;
+    red[w][2][lane] = s2;
+    __syncthreads();
+    if (w < NK) emit(w, lane, red[0][w][lane] + red[1][w][lane] + red[2][w][lane] + red[3][w][lane]);
   }
 }
 
@@ -572,9 +603,13 @@ extern "C" int dv_xattn_fold_bwd(const float* wsR, const float* wsV, const float
   DV_REQUIRE(wsR && wsV && wsQ && mcorr && at && vt && g1 && wq && wo && kv && null_kv && dat &&
              dvt && dwq && dwo && dkv && dnull, "null pointer");
   hipStream_t st = (hipStream_t)stream;
-  fold_grad_finish_kernel<<<(C + 255) / 256, 256, 0, st>>>(wsR, wsV, wsQ, mcorr, at, vt, g1, dat, dvt, dg1, dg2, nb, C, acc_g);
+  if (!acc_g) {
+    if (dg1) (void)hipMemsetAsync(dg1, 0, sizeof(float) * C, st);
+    if (dg2) (void)hipMemsetAsync(dg2, 0, sizeof(float) * C, st);
+  }
+  fold_grad_finish_kernel<<<dim3((C + 63) / 64, nb), 256, 0, st>>>(wsR, wsV, wsQ, mcorr, at, vt, g1, dat, dvt, dg1, dg2, nb, C);
   fold_bwd_w_kernel<<<grid_for((long long)NH * DH * C), 256, 0, st>>>(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale, acc_w);
   if (!acc_w) (void)hipMemsetAsync(dnull, 0, sizeof(float) * 2 * DH, st);
-  fold_bwd_kv_kernel<<<nb * NH * NK, 256, 0, st>>>(dat, dvt, wq, wo, dkv, dnull, nb, C, scale);
+  fold_bwd_kv_kernel<<<dim3(NH, nb, 2), 256, 0, st>>>(dat, dvt, wq, wo, dkv, dnull, C, scale);
   return check_launch("xattn_fold_bwd");
 }

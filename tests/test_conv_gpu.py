@@ -15,6 +15,8 @@ CASES = [
     (5, 4, 4, 256, 0, 512, 1),
     (2, 6, 6, 64, 0, 3, 1),
     (1, 33, 9, 32, 32, 96, 3),
+    (3, 9, 11, 128, 64, 192, 3),    # glds path: dual source, ragged pixel and channel tiles
+    (32, 64, 64, 64, 0, 64, 3),     # glds path: 256x64 tile (M >= 512 tiles)
 ]
 
 
@@ -36,13 +38,14 @@ def test_conv_fwd_bwd(case, dtype, tol):
     b = torch.randn(cout, generator=g)
     res = torch.randn(nf, h, w, cout, generator=g)
     gy = torch.randn(nf, h, w, cout, generator=g)
-    # reference in fp32 on the bf16-rounded inputs
-    xr = x.to(dtype).float().clone().requires_grad_()
-    wr = wt.to(dtype).float().requires_grad_() if dtype != torch.float32 else wt.clone().requires_grad_()
-    br = b.clone().requires_grad_()
+    # reference in fp64 on the (bf16-rounded) inputs: long pixel reductions
+    # (wgrad / bias grad over 131k pixels) would otherwise measure the CPU's error
+    xr = x.to(dtype).double().clone().requires_grad_()
+    wr = wt.to(dtype).double().requires_grad_()
+    br = b.double().requires_grad_()
     yr = F.conv2d(xr.permute(0, 3, 1, 2), wr[:, :, 0], br, padding=k // 2).permute(0, 2, 3, 1)
-    yr = yr + res.to(dtype).float()
-    (yr * gy).sum().backward()
+    yr = yr + res.to(dtype).double()
+    (yr * gy.double()).sum().backward()
 
     dev = "cuda"
     xd = x.detach().to(dev, dtype)

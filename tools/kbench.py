@@ -38,7 +38,7 @@ def conv_case(nf, h, w, cin, cout, k, dtype=torch.bfloat16):
     dy = torch.randn_like(y)
     ws = torch.zeros(cout, k * k, cin, device="cuda")
     def wgrad():
-        call("dv_conv_wgrad", dt(x), ptr(dy), cout, ptr(x), cin, cin, None, 0, ptr(ws), nf, h, w,
+        call("dv_conv_wgrad", dt(x), ptr(dy), cout, ptr(x), cin, cin, None, 0, ptr(ws), None, nf, h, w,
              cin, cout, k, stream())
     msw = timeit(wgrad)
     print(f"conv nf={nf} {h}x{w} {cin}->{cout} k={k} {str(dtype)[6:]}: fwd {ms*1e3:8.1f} us "
