@@ -128,6 +128,7 @@ def main():
 
     roof = None
     kernels = None
+    attention = None
     if not args.no_roofline:
         # live per-launch HIP-event timing of every conv kernel over K more steps
         from dalle2_video import ops
@@ -148,6 +149,16 @@ def main():
         kernels = {k: {"ms_per_step": round(v["ms"] / max(2, min(args.steps, 5)), 3),
                        "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
                    for k, v in sorted(summ.items(), key=lambda kv: -kv[1]["ms"])}
+        # north-star sub-metric: mid-attention QK^T/PV (fwd + bwd) vs the bf16 MFMA peak
+        att = [v for k, v in summ.items() if k.startswith("attn:")]
+        if att:
+            fl = sum(v["flops"] for v in att)
+            ms = sum(v["ms"] for v in att)
+            nrep = max(2, min(args.steps, 5))
+            attention = {"kernels": "mqa_fwd + mqa_bwd (mid self-attention, 16 heads x 32, 1,025 keys)",
+                         "flop_per_step": round(fl / nrep), "ms_per_step": round(ms / nrep, 4),
+                         "achieved": round(fl / (ms * 1e-3) / 1e12, 1), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4)}
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -165,7 +176,7 @@ def main():
                        "clip": [args.frames, args.size, args.size], "batch_per_gpu": args.batch,
                        "global_batch": args.batch * world, "parallelism": f"dp{world}"},
             "step_tflops_algorithmic": round(STEP_TFLOP * sps, 1),
-            "roofline": roof, "cpu_baseline": base, "kernels": kernels,
+            "roofline": roof, "attention": attention, "cpu_baseline": base, "kernels": kernels,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -14,6 +14,9 @@
 //   f32 atomics into a packed [co][tap][ci] workspace (coalesced rows).
 #include "dv_common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 using namespace dv;
 
 namespace {
@@ -590,6 +593,271 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs<T> p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// bf16 wgrad on LDS-DMA staging.  Stage = 64 pixels; the A image (dY rows,
+// BMC channels) and the B image (im2col rows, BNK columns of (tap, ci)) are
+// pixel-major and read transposed (ds_read_b64_tr_b16) as MFMA operands.
+// Each lane DMAs a FIXED 16-B chunk column of every row it stages (the chunk
+// XOR of a row depends only on row & 3 or (row >> 1) & 1), so its (tap, ci)
+// and source pointer are loop-invariant; per-row im2col coordinates come from
+// magic-number division.  The bias gradient rides on the MFMA: waves of the
+// blockIdx.y == 0 column multiply the dY fragments by a ones fragment.
+// ---------------------------------------------------------------------------
+struct FastDiv {
+  unsigned m;
+  int s1, s2;
+  unsigned d;
+};
+inline FastDiv make_fastdiv(unsigned d) {
+  FastDiv f;
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  f.m = (unsigned)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+  f.s1 = l < 1 ? l : 1;
+  f.s2 = l > 1 ? l - 1 : 0;
+  f.d = d;
+  return f;
+}
+__device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) {
+  const unsigned t = __umulhi(n, f.m);
+  return (t + ((n - t) >> f.s1)) >> f.s2;
+}
+
+struct WgradGArgs {
+  const bf16* dy;
+  int lddy;
+  const bf16* x0;
+  const bf16* x1;
+  int ld0, ld1, c0;
+  float* ws;
+  float* db;
+  int H, W, cin, cout, ks, K;
+  int M;  // pixels (< 2^31, checked)
+  int pix_per_split;
+  int batch_pix, splits_per_batch;
+  long long ws_bstride;
+  FastDiv fd_hw, fd_w, fd_cin, fd_ks;
+};
+
+// byte offset of 16-B chunk `ch` of `row` in an image with RB-byte rows
+template <int RB>
+__device__ __forceinline__ int img_off(int row, int ch) {
+  const int x = RB == 128 ? (((row >> 1) & 1) << 2) : ((row & 3) << 2);
+  return row * RB + ((ch ^ x) << 4);
+}
+
+template <int BMC, int BNK>
+__global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
+  constexpr int BP = 64;
+  constexpr int RA = BMC * 2, RB = BNK * 2;  // row bytes
+  constexpr int RPI_A = 1024 / RA, RPI_B = 1024 / RB;  // rows per wave-instruction
+  constexpr int GA = BP / (4 * RPI_A), GB = BP / (4 * RPI_B);  // DMAs per thread per stage
+  constexpr int BUF = BP * (RA + RB);
+  constexpr int WM = BMC / 64, WN = 4 / WM;  // wave grid
+  constexpr int TJ = 2, TI = BNK / (32 * WN);  // 32x32 tiles per wave
+  static_assert(TI >= 1, "tile");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int co0 = blockIdx.x * BMC, nk0 = blockIdx.y * BNK;
+  int pbeg, pend;
+  float* wsb = p.ws;
+  if (p.batch_pix > 0) {
+    const int bi = blockIdx.z / p.splits_per_batch, lz = blockIdx.z % p.splits_per_batch;
+    pbeg = bi * p.batch_pix + lz * p.pix_per_split;
+    pend = min(pbeg + p.pix_per_split, (bi + 1) * p.batch_pix);
+    wsb = p.ws + bi * p.ws_bstride;
+  } else {
+    pbeg = blockIdx.z * p.pix_per_split;
+    pend = min(pbeg + p.pix_per_split, p.M);
+  }
+  const int pad = p.ks >> 1;
+  const bf16* zero = (const bf16*)g_zero_line;
+
+  // A: this lane's fixed chunk column (channels co0 + 8*cha .. +7)
+  const int a_lrow = lane / (RA / 16), a_slot = lane % (RA / 16);
+  // rows this lane stages are a_row0 + 4*RPI_A*i: same XOR for all of them
+  const int a_row0 = wave * RPI_A + a_lrow;
+  const int a_x = RA == 128 ? (((a_row0 >> 1) & 1) << 2) : ((a_row0 & 3) << 2);
+  const int cha = a_slot ^ a_x;
+  const bool a_ok = co0 + 8 * cha < p.cout;
+  const bf16* a_src = p.dy + co0 + 8 * cha;
+  // B: fixed chunk column -> (tap, ci)
+  const int b_lrow = lane / (RB / 16), b_slot = lane % (RB / 16);
+  const int b_row0 = wave * RPI_B + b_lrow;
+  const int b_x = RB == 128 ? (((b_row0 >> 1) & 1) << 2) : ((b_row0 & 3) << 2);
+  const int chb = b_slot ^ b_x;
+  const int n = nk0 + 8 * chb;
+  const bool b_ok = n < p.K;
+  const int tap = b_ok ? (int)fdiv((unsigned)n, p.fd_cin) : 0;
+  const int ci = n - tap * p.cin;
+  const int ty = b_ok ? (int)fdiv((unsigned)tap, p.fd_ks) : 0;
+  const int dy = ty - pad, dx = tap - ty * p.ks - pad;
+  const bool first = ci < p.c0;
+  const bf16* b_src = first ? p.x0 + ci : p.x1 + (ci - p.c0);
+  const int b_ld = first ? p.ld0 : p.ld1;
+  const int doff = dy * p.W + dx;
+
+  auto issue = [&](int pb, int buf) {
+    char* sA = smem + buf * BUF;
+    char* sB = sA + BP * RA;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int row = (4 * i + wave) * RPI_A + a_lrow;
+      const int m = pb + row;
+      const bf16* src = (a_ok && m < pend) ? a_src + m * p.lddy : zero;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(sA + (4 * i + wave) * 1024),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int row = (4 * i + wave) * RPI_B + b_lrow;
+      const int m = pb + row;
+      const int f = (int)fdiv((unsigned)m, p.fd_hw);
+      const int rem = m - f * p.H * p.W;
+      const int y = (int)fdiv((unsigned)rem, p.fd_w);
+      const int xx = rem - y * p.W + dx, yy = y + dy;
+      const bool in = b_ok && m < pend && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      const bf16* src = in ? b_src + (m + doff) * b_ld : zero;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(sB + (4 * i + wave) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x16 acc[TJ][TI], accb[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) accb[j][e] = 0.f;
+  }
+  const bool do_bias = p.db != nullptr && blockIdx.y == 0 && wn == 0;  // wave-uniform
+  const u32x4 ones = {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};  // bf16 1.0 x8
+
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int nst = (pend - pbeg + BP - 1) / BP;
+  if (nst > 0) issue(pbeg, 0);
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) {
+      issue(pbeg + (st + 1) * BP, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GA + GB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* sA = smem + buf * BUF;
+    const char* sB = sA + BP * RA;
+#pragma unroll
+    for (int s = 0; s < BP / 16; ++s) {
+      const int R0 = 16 * s + 8 * (g >> 1);
+      u32x4 fa[TJ], fb[TI];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int C0 = wm * 64 + 32 * j + 16 * (g & 1) + 4 * pp;  // element column
+        const int ch = C0 >> 3, o8 = (C0 & 7) * 2;
+        const s16x4 lo = tr_read(sA + img_off<RA>(R0 + q, ch) + o8);
+        const s16x4 hi = tr_read(sA + img_off<RA>(R0 + 4 + q, ch) + o8);
+        const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+        fa[j] = u32x4{l2[0], l2[1], h2[0], h2[1]};
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int C0 = wn * 32 * TI + 32 * i + 16 * (g & 1) + 4 * pp;
+        const int ch = C0 >> 3, o8 = (C0 & 7) * 2;
+        const s16x4 lo = tr_read(sB + img_off<RB>(R0 + q, ch) + o8);
+        const s16x4 hi = tr_read(sB + img_off<RB>(R0 + 4 + q, ch) + o8);
+        const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+        fb[i] = u32x4{l2[0], l2[1], h2[0], h2[1]};
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[j][i] = Mma<bf16>::run(fa[j], fb[i], acc[j][i]);
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) accb[j] = Mma<bf16>::run(fa[j], ones, accb[j]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  const int r = lane & 31, h = lane >> 5;
+  if (do_bias && r == 0) {  // every column of accb holds the row sums
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = co0 + wm * 64 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (co < p.cout) atomicAdd(p.db + co, accb[j][e]);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < TJ; ++j)
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int nn = nk0 + wn * 32 * TI + 32 * i + r;
+      if (nn >= p.K) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = co0 + wm * 64 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (co < p.cout) atomicAdd(wsb + (long long)co * p.K + nn, acc[j][i][e]);
+      }
+    }
+}
+
+template <int BMC, int BNK>
+int launch_wgrad_glds(WgradGArgs a, hipStream_t st) {
+  const int mt = (a.cout + BMC - 1) / BMC, nt = (a.K + BNK - 1) / BNK;
+  static const long long target = getenv("DV_WGRAD_TARGET") ? atoll(getenv("DV_WGRAD_TARGET")) : 512;
+  long long want = target / ((long long)mt * nt);
+  if (want < 1) want = 1;
+  long long per = ((long long)a.M + want - 1) / want;
+  per = ((per + 255) / 256) * 256;
+  if (per < 256) per = 256;
+  unsigned splits;
+  if (a.batch_pix > 0) {
+    const long long nbatch = a.M / a.batch_pix;
+    long long spb = (a.batch_pix + per - 1) / per;
+    per = (a.batch_pix + spb - 1) / spb;
+    a.splits_per_batch = (int)spb;
+    splits = (unsigned)(nbatch * spb);
+  } else {
+    splits = (unsigned)((a.M + per - 1) / per);
+  }
+  a.pix_per_split = (int)per;
+  conv_wgrad_glds_kernel<BMC, BNK><<<dim3(mt, nt, splits), 256, 0, st>>>(a);
+  return check_launch("conv_wgrad_glds");
+}
+
+int conv_wgrad_glds(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
+                    int ld1, float* ws, float* db, int nf, int h, int w, int cin, int cout, int ks,
+                    hipStream_t st, long long batch_pix) {
+  WgradGArgs a;
+  a.dy = (const bf16*)dy; a.lddy = lddy; a.x0 = (const bf16*)x0;
+  a.x1 = (const bf16*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0; a.c0 = x1 ? c0 : cin;
+  a.ws = ws; a.db = db; a.H = h; a.W = w; a.cin = cin; a.cout = cout; a.ks = ks;
+  a.K = ks * ks * cin; a.M = nf * h * w;
+  a.batch_pix = (int)batch_pix; a.splits_per_batch = 1; a.pix_per_split = 0;
+  a.ws_bstride = (long long)cout * a.K;
+  a.fd_hw = make_fastdiv((unsigned)(h * w)); a.fd_w = make_fastdiv((unsigned)w);
+  a.fd_cin = make_fastdiv((unsigned)cin); a.fd_ks = make_fastdiv((unsigned)ks);
+  if (a.M == 0) return DV_OK;
+  if (cout <= 64) {
+    if (a.K >= 2048 || a.K % 256 == 0) return launch_wgrad_glds<64, 256>(a, st);
+    return launch_wgrad_glds<64, 128>(a, st);
+  }
+  return launch_wgrad_glds<128, 128>(a, st);
+}
+
 template <typename T>
 __global__ void pack_weight_kernel(const float* w, T* out, int cout, int cin, int taps,
                                    int pad_to, int mode) {
@@ -740,6 +1008,12 @@ int conv_wgrad_t(const void* dy, int lddy, const void* x0, int ld0, int c0, cons
   a.ws_bstride = (long long)cout * a.K;
   a.splits_per_batch = 1;
   if (a.M == 0) return DV_OK;
+  if constexpr (sizeof(T) == 2) {
+    const long long maxld = std::max<long long>(std::max(lddy, ld0), x1 ? ld1 : 0);
+    if (a.M * maxld < (1ll << 31) && (long long)cout * a.K < (1ll << 31))
+      return conv_wgrad_glds(dy, lddy, x0, ld0, c0, x1, ld1, ws, db, nf, h, w, cin, cout, ks, st,
+                             batch_pix);
+  }
   const bool small_co = cout <= 64;
   const bool small_k = a.K <= 64;
   if (small_co && small_k) return launch_wgrad<T, 64, 64>(a, st);

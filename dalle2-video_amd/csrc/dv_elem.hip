@@ -235,43 +235,38 @@ __global__ void linear_small_dw_kernel(const float* dy, int lddy, const float* x
   }
 }
 
-// dx[b][k] (+)= act_in'(x) * sum_n g[b][n] W[n][k]: block = 64 k-columns x 4
-// n-slices, grid.y splits N; partial sums meet in f32 atomics (dx pre-zeroed
-// or accumulated into).  B <= 16.
+// dx[b][k] (+)= act_in'(x) * sum_n g[b][n] W[n][k].  Block = 256 k-columns x
+// one 32-row slice of n (grid.y); g for the slice is staged in LDS once, W
+// rows are streamed coalesced with 8 loads in flight; slices meet in f32
+// atomics (dx pre-zeroed or accumulated into).  B <= 16.
 __global__ __launch_bounds__(256) void linear_small_dx_kernel(const float* dy, int lddy,
                                                               const float* x, int ldx,
                                                               const float* W, const float* z,
                                                               float* dx, int lddx, int B, int K,
-                                                              int N, int act_in, int act_out,
-                                                              int n_per_block) {
-  constexpr int MAXB = 16;
-  __shared__ float red[4][MAXB][64];
-  const int kl = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int k = blockIdx.x * 64 + kl;
-  const int n0 = blockIdx.y * n_per_block;
-  int n1 = n0 + n_per_block;
-  if (n1 > N) n1 = N;
+                                                              int N, int act_in, int act_out) {
+  constexpr int MAXB = 16, NS = 32;
+  __shared__ float gs[MAXB][NS];
+  const int n0 = blockIdx.y * NS;
+  const int nend = min(NS, N - n0);
+  for (int i = threadIdx.x; i < MAXB * NS; i += 256) {
+    const int b = i / NS, nn = i % NS;
+    gs[b][nn] = (b < B && nn < nend) ? lin_g(dy, lddy, z, b, n0 + nn, N, act_out) : 0.f;
+  }
+  __syncthreads();
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
   float acc[MAXB];
 #pragma unroll
   for (int b = 0; b < MAXB; ++b) acc[b] = 0.f;
-  if (k < K) {
-    for (int n = n0 + sl; n < n1; n += 4) {
-      const float w = W[(long long)n * K + k];
+  const float* wp = W + (long long)n0 * K + k;
+#pragma unroll 8
+  for (int nn = 0; nn < nend; ++nn) {
+    const float w = wp[(long long)nn * K];
 #pragma unroll
-      for (int b = 0; b < MAXB; ++b)
-        if (b < B) acc[b] += lin_g(dy, lddy, z, b, n, N, act_out) * w;
-    }
+    for (int b = 0; b < MAXB; ++b) acc[b] += gs[b][nn] * w;  // rows b >= B are zero
   }
-#pragma unroll
-  for (int b = 0; b < MAXB; ++b) red[sl][b][kl] = acc[b];
-  __syncthreads();
-  if (sl == 0 && k < K) {
-    for (int b = 0; b < B; ++b) {
-      const float s = (red[0][b][kl] + red[1][b][kl] + red[2][b][kl] + red[3][b][kl]) *
-                      act_in_d(x[(long long)b * ldx + k], act_in);
-      atomicAdd(dx + (long long)b * lddx + k, s);
-    }
-  }
+  for (int b = 0; b < B; ++b)
+    atomicAdd(dx + (long long)b * lddx + k, acc[b] * act_in_d(x[(long long)b * ldx + k], act_in));
 }
 
 __global__ void adamw_kernel(float* p, const float* g, float* m, float* v, long long n,
@@ -498,9 +493,8 @@ extern "C" int dv_linear_small_bwd(const float* dy, int lddy, const float* x, in
   if (dW) linear_small_dw_kernel<<<grid_for((long long)N * K), 256, 0, st>>>(dy, lddy, x, ldx, z, dW, db, B, K, N, act_in, act_out, accumulate_w);
   if (dx) {
     if (!accumulate_dx) (void)hipMemsetAsync(dx, 0, sizeof(float) * ((long long)(B - 1) * lddx + K), st);
-    const int npb = 64;
-    dim3 grid((K + 63) / 64, (N + npb - 1) / npb);
-    linear_small_dx_kernel<<<grid, 256, 0, st>>>(dy, lddy, x, ldx, W, z, dx, lddx, B, K, N, act_in, act_out, npb);
+    dim3 grid((K + 255) / 256, (N + 31) / 32);
+    linear_small_dx_kernel<<<grid, 256, 0, st>>>(dy, lddy, x, ldx, W, z, dx, lddx, B, K, N, act_in, act_out);
   }
   return check_launch("linear_small_bwd");
 }

@@ -138,15 +138,18 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   }
 }
 
-__global__ void gn_stats_finalize(const float* ws, float* mean, float* rstd, int nb, long long P,
+__global__ void gn_stats_finalize(float* ws, float* mean, float* rstd, int nb, long long P,
                                   int C, int G, float eps) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nb * G) return;
   const int b = i / G, g = i % G, cg = C / G;
   double s1 = 0.0, s2 = 0.0;
   for (int c = g * cg; c < (g + 1) * cg; ++c) {
-    s1 += ws[((long long)b * C + c) * 2];
-    s2 += ws[((long long)b * C + c) * 2 + 1];
+    float* w = ws + ((long long)b * C + c) * 2;
+    s1 += w[0];
+    s2 += w[1];
+    w[0] = 0.f;  // leave the workspace zeroed for the next reduction
+    w[1] = 0.f;
   }
   const double n = (double)P * cg;
   const double mu = s1 / n;
@@ -196,8 +199,11 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   const int tpr = a.C / VEC, rpp = 256 / tpr;
   const int rr = threadIdx.x / tpr, cv = (threadIdx.x % tpr) * VEC;
-  if (rr >= rpp) return;
   const int b = blockIdx.y;
+  if (MODE == 1 && blockIdx.x == 0) {  // the reduction sums are consumed: re-zero them
+    for (int i = threadIdx.x; i < 2 * a.C; i += 256) a.ws[(long long)b * a.C * 2 + i] = 0.f;
+  }
+  if (rr >= rpp) return;
   const long long beg = blockIdx.x * a.rows_per_block;
   long long end = beg + a.rows_per_block;
   if (end > a.P) end = a.P;
@@ -264,7 +270,6 @@ int gn_fwd_t(GnArgs a, float eps, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
   a.rows_per_block = reduce_rows(a, VEC);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
-  (void)hipMemsetAsync(a.ws, 0, sizeof(float) * a.nb * a.C * 2, st);
   gn_reduce_kernel<T, 0><<<g1, 256, 0, st>>>(a);
   gn_stats_finalize<<<(a.nb * a.G + 63) / 64, 64, 0, st>>>(a.ws, (float*)a.mean, (float*)a.rstd,
                                                           a.nb, a.P, a.C, a.G, eps);
@@ -279,7 +284,6 @@ int gn_bwd_t(GnArgs a, float* dgamma, float* dbeta, float* dss, int accumulate, 
   const int VEC = 16 / sizeof(T);
   a.rows_per_block = reduce_rows(a, VEC);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
-  (void)hipMemsetAsync(a.ws, 0, sizeof(float) * a.nb * a.C * 2, st);
   gn_reduce_kernel<T, 1><<<g1, 256, 0, st>>>(a);
   int n2 = a.C > a.nb * a.G ? a.C : a.nb * a.G;
   gn_bwd_finalize<<<(n2 + 63) / 64, 64, 0, st>>>(a, dgamma, dbeta, dss, accumulate);
@@ -424,8 +428,8 @@ extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int
                          int lddz, int nb, long long P, int C, int G, const float* gamma,
                          const float* beta, const float* ss, int act, const float* mean,
                          const float* rstd, float* dgamma, float* dbeta, float* dss, float* ws,
-                         int accumulate, void* stream) {
-  DV_REQUIRE(dy && z && dz && gamma && beta && mean && rstd && ws, "null pointer");
+                         float* ws2, int accumulate, void* stream) {
+  DV_REQUIRE(dy && z && dz && gamma && beta && mean && rstd && ws && ws2, "null pointer");
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && lddy % VEC == 0 && lddz % VEC == 0,
              "channel counts / strides must be multiples of 16 bytes");
@@ -433,7 +437,7 @@ extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int
   GnArgs a{};
   a.z = z; a.ldz = ldz; a.dy = dy; a.lddy = lddy; a.out = dz; a.ldo = lddz; a.nb = nb; a.P = P;
   a.C = C; a.G = G; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.ss = ss;
-  a.act = act; a.ws = ws; a.ws2 = ws + (long long)nb * C * 2;
+  a.act = act; a.ws = ws; a.ws2 = ws2;
   if (nb == 0 || P == 0) return DV_OK;
   hipStream_t st = (hipStream_t)stream;
   return dtype == DV_BF16 ? gn_bwd_t<bf16>(a, dgamma, dbeta, dss, accumulate, st)

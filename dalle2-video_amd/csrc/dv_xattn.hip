@@ -415,7 +415,7 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
 // folded columns; dg1/dg2 (pre-zeroed unless accumulating) take one atomic
 // per (b, c).
 __global__ __launch_bounds__(256) void fold_grad_finish_kernel(
-    const float* wsR, const float* wsV, const float* wsQ, const float* mcorr, const float* at,
+    float* wsR, float* wsV, float* wsQ, const float* mcorr, const float* at,
     const float* vt, const float* g1, float* dat, float* dvt, float* dg1, float* dg2, int nb,
     int C) {
   __shared__ float red[2][4][64];
@@ -441,6 +441,16 @@ __global__ __launch_bounds__(256) void fold_grad_finish_kernel(
   red[0][grp][cl] = s1;
   red[1][grp][cl] = s2;
   __syncthreads();
+  if (c < C) {  // consumed: leave the GEMM accumulators zeroed for the next call
+    float *wr = wsR, *wv = wsV, *wq2 = wsQ;
+#pragma unroll
+    for (int q = 0; q < KP / 4; ++q) {
+      const long long wi = ((long long)b * KP + grp * (KP / 4) + q) * C + c;
+      wr[wi] = 0.f;
+      wv[wi] = 0.f;
+      wq2[wi] = 0.f;
+    }
+  }
   if (grp == 0 && c < C) {
     const float t1 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
     const float t2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
@@ -483,11 +493,12 @@ __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const floa
 // dV = dvt[:, hj]^T Wo_h (lane = head dim, coalesced Wo rows, waves split c).
 __global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, const float* dvt,
                                                           const float* wq, const float* wo,
-                                                          float* dkv, float* dnull, int C,
-                                                          float scale) {
+                                                          float* dkv, float* dnull, float* mcorr,
+                                                          int C, float scale) {
   __shared__ float red[4][NK][DH];
   const int h = blockIdx.x, b = blockIdx.y, part = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (h == 0 && part == 0 && threadIdx.x < KP) mcorr[b * KP + threadIdx.x] = 0.f;  // consumed
   const float* datb = dat + (long long)b * C * HK + h * NK;
   const float* dvtb = dvt + (long long)b * C * HK + h * NK;
   auto emit = [&](int j, int d, float v) {
@@ -593,8 +604,8 @@ extern "C" int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const vo
   return check_launch("xattn_bwd_tokens");
 }
 
-extern "C" int dv_xattn_fold_bwd(const float* wsR, const float* wsV, const float* wsQ,
-                                 const float* mcorr, const float* at, const float* vt,
+extern "C" int dv_xattn_fold_bwd(float* wsR, float* wsV, float* wsQ,
+                                 float* mcorr, const float* at, const float* vt,
                                  const float* g1, const float* wq, const float* wo,
                                  const float* kv, const float* null_kv, float* dat, float* dvt,
                                  float* dg1, float* dg2, float* dwq, float* dwo, float* dkv,
@@ -610,6 +621,7 @@ extern "C" int dv_xattn_fold_bwd(const float* wsR, const float* wsV, const float
   fold_grad_finish_kernel<<<dim3((C + 63) / 64, nb), 256, 0, st>>>(wsR, wsV, wsQ, mcorr, at, vt, g1, dat, dvt, dg1, dg2, nb, C);
   fold_bwd_w_kernel<<<grid_for((long long)NH * DH * C), 256, 0, st>>>(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale, acc_w);
   if (!acc_w) (void)hipMemsetAsync(dnull, 0, sizeof(float) * 2 * DH, st);
-  fold_bwd_kv_kernel<<<dim3(NH, nb, 2), 256, 0, st>>>(dat, dvt, wq, wo, dkv, dnull, C, scale);
+  fold_bwd_kv_kernel<<<dim3(NH, nb, 2), 256, 0, st>>>(dat, dvt, wq, wo, dkv, dnull,
+                                                     mcorr, C, scale);
   return check_launch("xattn_fold_bwd");
 }

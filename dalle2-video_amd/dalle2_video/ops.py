@@ -50,8 +50,30 @@ def _launch(name, flops, nbytes, fn):
         TIMER.run(name, flops, nbytes, fn)
 
 
+def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld):
+    """Kernel instantiation dv_conv_fwd dispatches to (mirror of conv_fwd_t /
+    glds_tile in dv_conv.hip) — names the launch for the live roofline."""
+    if dtype_name == "bf16" and cin % 64 == 0 and c0 % 64 == 0 and m * maxld < (1 << 31):
+        bn = 64 if cout <= 64 else 128
+        bm = 256 if bn == 64 else 128
+        if ((m + bm - 1) // bm) * ((cout + bn - 1) // bn) < 512:
+            bm = 128
+        return f"conv_fwd_glds_kernel<{bm},{bn}>"
+    bm, bn = conv_tile(m, cout)
+    return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"
+
+
+def conv_wgrad_name(dtype_name, m, cout, K, maxld):
+    """Mirror of conv_wgrad_t / conv_wgrad_glds's tile choice."""
+    if dtype_name == "bf16" and m * maxld < (1 << 31) and cout * K < (1 << 31):
+        if cout <= 64:
+            return "conv_wgrad_glds_kernel<64,256>" if (K >= 2048 or K % 256 == 0) else "conv_wgrad_glds_kernel<64,128>"
+        return "conv_wgrad_glds_kernel<128,128>"
+    return f"conv_wgrad_kernel<{dtype_name}>"
+
+
 def conv_tile(m, cout):
-    """Mirror of conv_fwd_t's tile choice (names the kernel instantiation)."""
+    """Mirror of conv_fwd_t's tile choice for the register-staged kernel."""
     mt128 = (m + 127) // 128
     bn = 64 if cout <= 64 else 128
     bm = 128
@@ -100,6 +122,32 @@ def _wgrad_workspace(cout, taps, cin, device):
     return _WS[key]
 
 
+_GN_WS = {}
+_XA_WS = {}
+
+
+def _xattn_workspace(nb, C, device):
+    """Cross-attention backward accumulators (wsR, wsV, wsQ [nb][32][C], mcorr
+    [nb][32]): zero on entry, re-zeroed by dv_xattn_fold_bwd after use."""
+    key = (nb, C, str(device))
+    if key not in _XA_WS:
+        _XA_WS[key] = tuple(torch.zeros(nb, 32, C, dtype=torch.float32, device=device) for _ in range(3)) + (
+            torch.zeros(nb, 32, dtype=torch.float32, device=device),)
+    return _XA_WS[key]
+
+
+def _gn_workspace(n, device):
+    """GroupNorm partial-sum workspace: zero on entry, left zeroed by the GN
+    kernels themselves (dv_gn_fwd / dv_gn_bwd contract), so it is allocated
+    once per device and never memset."""
+    key = str(device)
+    buf = _GN_WS.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.zeros(max(n, 1 << 16), dtype=torch.float32, device=device)
+        _GN_WS[key] = buf
+    return buf
+
+
 def _pad_channels(t: torch.Tensor, mult: int = 8) -> torch.Tensor:
     c = t.shape[-1]
     cp = (c + mult - 1) // mult * mult
@@ -116,7 +164,7 @@ def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int) -> tor
     cout, cin = weight.shape[0], weight.shape[1]
     k = weight.shape[-1] if weight.dim() == 5 else 1  # nn.Linear weights are 1x1 convs
     rows = cout if mode == 0 else cin
-    out = (torch.empty if mode == 0 else torch.zeros)(rows, k * k, pad_to, dtype=dtype,
+    out = torch.empty(rows, k * k, pad_to, dtype=dtype,
                                                       device=weight.device)
     w = weight.detach()
     if w.dtype != torch.float32 or not w.is_contiguous():
@@ -145,8 +193,8 @@ class ConvFn(torch.autograd.Function):
         ldr = cl_ld(res) if res is not None else 0
         b = None if bias is None else bias.detach().float().contiguous()
         m = nf * h * w
-        bm, bn = conv_tile(m, cout)
-        _launch(f"conv_fwd_kernel<{_lib.dtype_name(x0)},{bm},{bn}>", 2.0 * m * cout * cin * ksize * ksize,
+        _launch(conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
+                              max(ld0, ld1)), 2.0 * m * cout * cin * ksize * ksize,
                 x0.element_size() * m * (cin + cout),
                 lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b), ptr(res),
                              ldr, ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE, stream()))
@@ -170,8 +218,8 @@ class ConvFn(torch.autograd.Function):
             alloc = torch.empty if cin_real == cin else torch.zeros
             dx = alloc(nf, h, w, cin, dtype=dy.dtype, device=dy.device)
             m = nf * h * w
-            bm, bn = conv_tile(m, cin_real)
-            _launch(f"conv_fwd_kernel<{_lib.dtype_name(dy8)},{bm},{bn}>", 2.0 * m * cin_real * cout8 * ksize * ksize,
+            _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, cout8),
+                    2.0 * m * cin_real * cout8 * ksize * ksize,
                     dy8.element_size() * m * (cin + cout8),
                     lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd), None, None, 0,
                                  ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE, stream()))
@@ -193,7 +241,8 @@ class ConvFn(torch.autograd.Function):
             ld0 = cl_ld(x0)
             ld1 = cl_ld(x1) if x1 is not None else 0
             m = nf * h * w
-            _launch(f"conv_wgrad_kernel<{_lib.dtype_name(dy8)}>", 2.0 * m * cout8 * cin * ksize * ksize,
+            _launch(conv_wgrad_name(_lib.dtype_name(dy8), m, cout8, cin * ksize * ksize, max(cout8, ld0, ld1)),
+                    2.0 * m * cout8 * cin * ksize * ksize,
                     dy8.element_size() * m * (cin + cout8),
                     lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), cout8, ptr(x0), ld0, c0, ptr(x1), ld1,
                                  ptr(ws), ptr(db_buf), nf, h, w, cin, cout8, ksize, stream()))
@@ -235,7 +284,7 @@ class GroupNormActFn(torch.autograd.Function):
         y = torch.empty(nf, h, w, c, dtype=z.dtype, device=dev)
         mean = torch.empty(nb * groups, dtype=torch.float32, device=dev)
         rstd = torch.empty_like(mean)
-        ws = torch.empty(nb * c * 2, dtype=torch.float32, device=dev)
+        ws = _gn_workspace(nb * c * 2, dev)
         g, b = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
         s = None if ss is None else ss.detach().float().contiguous()
         call("dv_gn_fwd", dt(z), ptr(z), cl_ld(z), ptr(y), c, ptr(res), cl_ld(res) if res is not None else 0,
@@ -264,10 +313,11 @@ class GroupNormActFn(torch.autograd.Function):
             db = torch.empty(c, dtype=torch.float32, device=dev)
             acc, ret = 0, True
         dss = torch.empty(nb, 2 * c, dtype=torch.float32, device=dev) if has_ss else None
-        ws = torch.empty(nb * c * 2 + nb * groups * 2, dtype=torch.float32, device=dev)
+        ws = _gn_workspace(nb * c * 2, dev)
+        ws2 = torch.empty(nb * groups * 2, dtype=torch.float32, device=dev)
         call("dv_gn_bwd", dt(z), ptr(dy), c, ptr(z), cl_ld(z), ptr(dz), c, nb, P, c, groups, ptr(g),
-             ptr(b), ptr(s), act, ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(ws), acc,
-             stream())
+             ptr(b), ptr(s), act, ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(ws), ptr(ws2),
+             acc, stream())
         if not ret:
             dg = db = None
         return dz, dg, db, dss, (dy if has_res else None), None, None, None, None
@@ -463,17 +513,15 @@ class CrossAttnFn(torch.autograd.Function):
         dobuf = torch.empty(ntok, C, dtype=dtype, device=dev)
         dsbuf = torch.empty(ntok, 32, dtype=dtype, device=dev)
         p2buf = torch.empty(ntok, 32, dtype=dtype, device=dev)
-        mcorr = torch.zeros(nb, 32, dtype=torch.float32, device=dev)
+        wsR, wsV, wsQ, mcorr = _xattn_workspace(nb, C, dev)
         ldx = cl_ld(x)
         call("dv_xattn_bwd_tokens", dt(x), ptr(dy), C, ptr(x), ldx, ptr(dx), C, ntok, P, C,
              ptr(KtT), ptr(Vt), ptr(VtT), ptr(colsum), ptr(g2f), ptr(stats), ptr(pbuf), ptr(dobuf),
              ptr(dsbuf), ptr(p2buf), ptr(mcorr), stream())
         # per-batch token reductions: R = dS'^T X, V' = P^T dO, Q = P'^T dY (one batched GEMM each)
-        wsR = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
-        wsV = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
-        wsQ = torch.zeros(nb, 32, C, dtype=torch.float32, device=dev)
         for a_, b_, ldb, o_ in ((dsbuf, x, ldx, wsR), (pbuf, dobuf, C, wsV), (p2buf, dy, C, wsQ)):
-            _launch(f"conv_wgrad_kernel<{_lib.dtype_name(x)}>", 2.0 * ntok * 32 * C, 0,
+            _launch("gemm_tn_batched:" + conv_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldb)),
+                    2.0 * ntok * 32 * C, 0,
                     lambda a_=a_, b_=b_, ldb=ldb, o_=o_: call(
                         "dv_gemm_tn_batched", dt(x), ptr(a_), 32, ptr(b_), ldb, ptr(o_), P, nb, 32, C,
                         stream()))
@@ -534,8 +582,9 @@ class MQAFn(torch.autograd.Function):
         call("dv_mqa_prep", dt(q), ptr(kvc), kvc.shape[-1], ptr(nkv), ptr(kp), ptr(vp), B, N, NKP, stream())
         o = torch.empty(B * N, H * MQA_DH, dtype=q.dtype, device=dev)
         lse = torch.empty(B, H, N, dtype=torch.float32, device=dev)
-        call("dv_mqa_fwd", dt(q), ptr(qc), qc.shape[-1], ptr(kp), ptr(vp), ptr(o), o.shape[-1], ptr(lse),
-             B, N, NKP, H, ctypes_float(scale), stream())
+        _launch("attn:mqa_fwd", 4.0 * B * H * N * (N + 1) * MQA_DH, 0,
+                lambda: call("dv_mqa_fwd", dt(q), ptr(qc), qc.shape[-1], ptr(kp), ptr(vp), ptr(o),
+                             o.shape[-1], ptr(lse), B, N, NKP, H, ctypes_float(scale), stream()))
         ctx.save_for_backward(qc, kp, vp, o, lse)
         ctx.params = (null_kv,)
         ctx.meta = (B, N, H, NKP, scale, kvc.shape[-1])
@@ -554,10 +603,12 @@ class MQAFn(torch.autograd.Function):
         dkv = torch.empty(B * N, 2 * MQA_DH, dtype=qc.dtype, device=dev)
         sn = _grad_out(ctx.params[0])
         dnull = sn[0] if sn else torch.empty(2, MQA_DH, dtype=torch.float32, device=dev)
-        call("dv_mqa_bwd", dt(qc), ptr(qc), qc.shape[-1], ptr(o), o.shape[-1], ptr(do), do.shape[-1],
-             ptr(lse), ptr(kp), ptr(vp), ptr(dq), dq.shape[-1], ptr(D), ptr(dkp), ptr(dvp), ptr(dkv),
-             dkv.shape[-1], ptr(dnull), B, N, NKP, H, ctypes_float(scale), int(sn[1]) if sn else 0,
-             stream())
+        # algorithmic backward = 2x the forward contractions (dS/dQ/dK/dV, no recompute)
+        _launch("attn:mqa_bwd", 8.0 * B * H * N * (N + 1) * MQA_DH, 0,
+                lambda: call("dv_mqa_bwd", dt(qc), ptr(qc), qc.shape[-1], ptr(o), o.shape[-1], ptr(do),
+                             do.shape[-1], ptr(lse), ptr(kp), ptr(vp), ptr(dq), dq.shape[-1], ptr(D),
+                             ptr(dkp), ptr(dvp), ptr(dkv), dkv.shape[-1], ptr(dnull), B, N, NKP, H,
+                             ctypes_float(scale), int(sn[1]) if sn else 0, stream()))
         return dq, dkv, (None if sn else dnull), None, None, None, None
 
 

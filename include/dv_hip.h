@@ -86,8 +86,10 @@ int dv_gemm_tn_batched(int dtype, const void* a, int lda, const void* b, int ldb
  * 183-189): y = act(GN(z)*gamma + beta) (optionally *(ss_scale+1)+ss_shift,
  * ss = [nb][2C] f32 with scale first), + res.  nb batch elements of P pixels
  * (all frames of one clip form one GroupNorm sample), C channels, G groups.
- * mean/rstd [nb][G] f32 are saved for the backward; ws is a scratch of
- * nb*C*2 floats.  C % 8 == 0, C <= 256 vectors of 16 B.  act: DV_ACT_*.    */
+ * mean/rstd [nb][G] f32 are saved for the backward.  ws: nb*C*2 floats
+ * that must be ZERO on entry; both calls leave them zeroed again, so a
+ * cached workspace needs no memset.  ws2 (backward): nb*G*2 floats scratch.
+ * C % 8 == 0, C <= 256 vectors of 16 B.  act: DV_ACT_*.                     */
 int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* res, int ldres,
               int nb, long long P, int C, int G, float eps, const float* gamma,
               const float* beta, const float* ss, int act, float* mean, float* rstd, float* ws,
@@ -97,7 +99,7 @@ int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* r
 int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void* dz, int lddz,
               int nb, long long P, int C, int G, const float* gamma, const float* beta,
               const float* ss, int act, const float* mean, const float* rstd, float* dgamma,
-              float* dbeta, float* dss, float* ws, int accumulate, void* stream);
+              float* dbeta, float* dss, float* ws, float* ws2, int accumulate, void* stream);
 
 /* ---- row LayerNorm over channels (dalle2-pytorch LayerNorm, gain only, eps
  * 1e-5 fp32; the mid-attention pre/post norms, dalle2_video.py:431, 551,
@@ -202,7 +204,7 @@ int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ldo, long lon
                  const float* g2, float eps, float* stats, void* pbuf, void* stream);
 /* token part of the backward: dx (incl. residual); dobuf [ntok][C], dsbuf
  * and p2buf [ntok][32] feed three dv_gemm_tn_batched reductions; mcorr
- * [nb][32] f32 (pre-zeroed) accumulates the LN mean correction.             */
+ * [nb][32] f32 (zero on entry) accumulates the LN mean correction.          */
 int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const void* x, int ldx, void* dx,
                         int lddx, long long ntok, long long P, int C, const void* KtT,
                         const void* Vt, const void* VtT, const float* colsum, const float* g2,
@@ -210,8 +212,9 @@ int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const void* x, int 
                         void* p2buf, float* mcorr, void* stream);
 /* parameter part: from the GEMM results wsR/wsV/wsQ [nb][32][C] to
  * dg1, dg2 (acc_g), dwq [512][C], dwo [C][512], dnull [2][64] (acc_w) and
- * dkv [nb][2][1024] (overwritten).                                          */
-int dv_xattn_fold_bwd(const float* wsR, const float* wsV, const float* wsQ, const float* mcorr,
+ * dkv [nb][2][1024] (overwritten).  wsR/wsV/wsQ and mcorr are consumed and
+ * left ZEROED, so cached accumulators need no memset before the next call. */
+int dv_xattn_fold_bwd(float* wsR, float* wsV, float* wsQ, float* mcorr,
                       const float* at, const float* vt, const float* g1, const float* wq,
                       const float* wo, const float* kv, const float* null_kv, float* dat,
                       float* dvt, float* dg1, float* dg2, float* dwq, float* dwo, float* dkv,

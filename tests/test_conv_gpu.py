@@ -17,6 +17,8 @@ CASES = [
     (1, 33, 9, 32, 32, 96, 3),
     (3, 9, 11, 128, 64, 192, 3),    # glds path: dual source, ragged pixel and channel tiles
     (32, 64, 64, 64, 0, 64, 3),     # glds path: 256x64 tile (M >= 512 tiles)
+    (2, 7, 5, 256, 0, 64, 3),       # wgrad 64x256 tile (K = 2304)
+    (3, 4, 6, 24, 16, 32, 3),       # cout 32 < one 64-channel A tile, dual source
 ]
 
 
