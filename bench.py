@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-graphs", action="store_true",
+                    help="launch every kernel eagerly instead of replaying the captured HIP graph")
     return ap.parse_args()
 
 
@@ -58,7 +60,8 @@ def build(args, device):
                        timesteps=1000, learned_variance=False)
     deterministic_fill_(dec.unets[0])
     dec = dec.to(device)
-    trainer = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False, amp=args.dtype == "bf16")
+    trainer = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False, amp=args.dtype == "bf16",
+                                  use_graphs=not getattr(args, "no_graphs", False))
     return dec, trainer
 
 

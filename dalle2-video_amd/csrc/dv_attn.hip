@@ -394,8 +394,8 @@ extern "C" int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int 
   DV_REQUIRE(q && o && dout && lse && kp && vp && dq && D && dkp && dvp && dkv && dnull, "null pointer");
   DV_REQUIRE(H % 8 == 0 && NKP % 32 == 0, "bad shape");
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(dkp, 0, sizeof(float) * B * NKP * DH, st);
-  (void)hipMemsetAsync(dvp, 0, sizeof(float) * B * NKP * DH, st);
+  zero_f32(dkp, (long long)B * NKP * DH, st);
+  zero_f32(dvp, (long long)B * NKP * DH, st);
   const int hg = 2, hpg = H / hg;
   if (dtype == DV_BF16) {
     mqa_bwd_d_kernel<bf16><<<grid_for((long long)B * N * H), 256, 0, st>>>((const bf16*)o, ldo, (const bf16*)dout, lddo, D, B, N, H);

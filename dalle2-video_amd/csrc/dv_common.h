@@ -20,6 +20,9 @@ namespace dv {
 // thread-local last-error message surfaced by dv_last_error()
 void set_error(const std::string& msg);
 int check_launch(const char* what);
+// zero n floats on `st` with a kernel (used instead of hipMemsetAsync so that
+// zeroing is an ordinary kernel node when the stream is captured into a graph)
+void zero_f32(float* p, long long n, hipStream_t st);
 
 #define DV_REQUIRE(cond, msg)                      \
   do {                                             \

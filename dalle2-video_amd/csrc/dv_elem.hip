@@ -446,7 +446,7 @@ extern "C" int dv_mse_loss(int dtype, const void* pred, int ld, const float* tar
   const long long npix = (long long)B * T * H * W;
   const float scale = 1.f / (float)((double)B * C * T * H * W);
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(loss, 0, sizeof(float), st);
+  zero_f32(loss, 1, st);
   const int g = grid_for(npix, 256, 1024);
   DISPATCH(dtype,
            (mse_kernel<float><<<g, 256, 0, st>>>((const float*)pred, ld, target, B, C, T, H * W, sample_w, loss, scale)),
@@ -492,7 +492,7 @@ extern "C" int dv_linear_small_bwd(const float* dy, int lddy, const float* x, in
   DV_REQUIRE(B <= 16, "linear_small supports B <= 16 rows");
   if (dW) linear_small_dw_kernel<<<grid_for((long long)N * K), 256, 0, st>>>(dy, lddy, x, ldx, z, dW, db, B, K, N, act_in, act_out, accumulate_w);
   if (dx) {
-    if (!accumulate_dx) (void)hipMemsetAsync(dx, 0, sizeof(float) * ((long long)(B - 1) * lddx + K), st);
+    if (!accumulate_dx) zero_f32(dx, (long long)(B - 1) * lddx + K, st);
     dim3 grid((K + 255) / 256, (N + 31) / 32);
     linear_small_dx_kernel<<<grid, 256, 0, st>>>(dy, lddy, x, ldx, W, z, dx, lddx, B, K, N, act_in, act_out);
   }
@@ -512,7 +512,7 @@ extern "C" int dv_grad_clip_coef(const float* g, long long n, float max_norm, fl
   // ws[0] = sum of squares, ws[1] = update coefficient, ws[2] = gradient norm
   DV_REQUIRE(g && ws, "null pointer");
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(ws, 0, sizeof(float), st);
+  zero_f32(ws, 1, st);
   sumsq_kernel<<<grid_for(n, 256, 2048), 256, 0, st>>>(g, n, ws);
   clip_coef_kernel<<<1, 1, 0, st>>>(ws, max_norm, prescale, ws + 1);
   return check_launch("grad_clip_coef");

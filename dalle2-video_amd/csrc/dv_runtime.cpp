@@ -10,6 +10,19 @@ static thread_local std::string g_last_error;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 
+__global__ void zero_f32_kernel(float* p, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    p[i] = 0.f;
+}
+
+void zero_f32(float* p, long long n, hipStream_t st) {
+  if (n <= 0) return;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  zero_f32_kernel<<<(unsigned)blocks, 256, 0, st>>>(p, n);
+}
+
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

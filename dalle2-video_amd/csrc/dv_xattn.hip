@@ -615,12 +615,12 @@ extern "C" int dv_xattn_fold_bwd(float* wsR, float* wsV, float* wsQ,
              dvt && dwq && dwo && dkv && dnull, "null pointer");
   hipStream_t st = (hipStream_t)stream;
   if (!acc_g) {
-    if (dg1) (void)hipMemsetAsync(dg1, 0, sizeof(float) * C, st);
-    if (dg2) (void)hipMemsetAsync(dg2, 0, sizeof(float) * C, st);
+    if (dg1) zero_f32(dg1, C, st);
+    if (dg2) zero_f32(dg2, C, st);
   }
   fold_grad_finish_kernel<<<dim3((C + 63) / 64, nb), 256, 0, st>>>(wsR, wsV, wsQ, mcorr, at, vt, g1, dat, dvt, dg1, dg2, nb, C);
   fold_bwd_w_kernel<<<grid_for((long long)NH * DH * C), 256, 0, st>>>(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale, acc_w);
-  if (!acc_w) (void)hipMemsetAsync(dnull, 0, sizeof(float) * 2 * DH, st);
+  if (!acc_w) zero_f32(dnull, 2 * DH, st);
   fold_bwd_kv_kernel<<<dim3(NH, nb, 2), 256, 0, st>>>(dat, dvt, wq, wo, dkv, dnull,
                                                      mcorr, C, scale);
   return check_launch("xattn_fold_bwd");

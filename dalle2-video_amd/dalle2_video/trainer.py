@@ -269,8 +269,14 @@ def allreduce_flat_grad(flat_grad, world):
 class VideoDecoderTrainer(nn.Module):
     def __init__(self, decoder, accelerator=None, dataloaders=None, use_ema=True, lr=1e-4,
                  wd=1e-2, eps=1e-8, warmup_steps=None, cosine_decay_max_steps=None,
-                 max_grad_norm=0.5, amp=False, group_wd_params=True, **kwargs):
+                 max_grad_norm=0.5, amp=False, group_wd_params=True, use_graphs=None, **kwargs):
         super().__init__()
+        # HIP-graph replay of the forward+backward (opt-in; DV_GRAPHS=1): after two
+        # eager calls per (unet, input shapes), the whole p_losses forward and the
+        # autograd backward are captured once and replayed, removing the ~600
+        # host-side kernel launches per step.
+        self.use_graphs = (os.environ.get("DV_GRAPHS", "") == "1") if use_graphs is None else use_graphs
+        self._graphs = {}
         assert isinstance(decoder, VideoDecoder)
         ema_kwargs, kwargs = groupby_prefix_and_trim("ema_", kwargs)
         self.accelerator = accelerator
@@ -352,11 +358,56 @@ class VideoDecoderTrainer(nn.Module):
                 return v
         return v.to(self.device)
 
+    def _graphable(self, unet_number, max_batch_size, return_lowres_cond_video):
+        from . import ops
+        # host-side randomness (lowres blur choice) or per-launch timing cannot be replayed
+        return (self.use_graphs and self.training and max_batch_size is None
+                and not return_lowres_cond_video and ops.TIMER is None
+                and self.decoder.lowres_conds[unet_number - 1] is None
+                and getattr(self, f"optim{unet_number - 1}").flat_grad is not None)
+
+    def _graphed_call(self, unet_number, args, kwargs):
+        """Replay (capturing on first use) forward + backward of one training call."""
+        sig = (unet_number, self.amp,
+               tuple((tuple(a.shape), a.dtype) if torch.is_tensor(a) else repr(a) for a in args),
+               tuple((k, (tuple(v.shape), v.dtype) if torch.is_tensor(v) else repr(v))
+                     for k, v in sorted(kwargs.items())))
+        ent = self._graphs.get(sig)
+        if ent is None:
+            ent = self._graphs[sig] = {"eager": 0}
+        if ent["eager"] < 2:  # warm every lazy allocation / workspace first
+            ent["eager"] += 1
+            return None
+        if "graph" not in ent:
+            sargs = tuple(a.clone() if torch.is_tensor(a) else a for a in args)
+            skw = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in kwargs.items()}
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                ctx = (torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False)
+                       if self.amp else nullcontext())
+                with ctx:
+                    loss = self.decoder(*sargs, unet_number=unet_number, **skw)
+                loss.backward()
+            ent.update(graph=g, args=sargs, kwargs=skw, loss=loss.detach())
+        for dst, src in zip(ent["args"], args):
+            if torch.is_tensor(dst):
+                dst.copy_(src)
+        for k, v in kwargs.items():
+            if torch.is_tensor(v):
+                ent["kwargs"][k].copy_(v)
+        ent["graph"].replay()
+        return ent["loss"].item()
+
     def forward(self, *args, unet_number=None, max_batch_size=None, return_lowres_cond_video=False,
                 **kwargs):
         unet_number = self.validate_and_return_unet_number(unet_number)
         args = tuple(self._to_device(a) for a in args)
         kwargs = {k: self._to_device(v) for k, v in kwargs.items()}
+        if self._graphable(unet_number, max_batch_size, return_lowres_cond_video):
+            out = self._graphed_call(unet_number, args, kwargs)
+            if out is not None:
+                return out
         total_loss = 0.0
         cond_videos = []
         for frac, (cargs, ckw) in split_args_and_kwargs(*args, split_size=max_batch_size, **kwargs):

@@ -69,3 +69,44 @@ def test_trainer_call_api_and_checkpoint(tmp_path):
     tr2 = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False)
     tr2.load(str(path))
     assert tr2.steps.tolist() == [1, 1]
+
+
+def test_graph_replay_matches_eager():
+    """HIP-graph capture/replay of forward+backward (use_graphs=True) reproduces
+    the eager call: same seed -> same sampled times/noise -> same loss and
+    gradients (atomics reorder f32 sums: tolerance 1e-5)."""
+    from dalle2_video import dalle2_video as D
+    from dalle2_video.trainer import VideoDecoderTrainer
+    from dalle2_video.utils import deterministic_fill_
+
+    u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    dec = D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(4,), timesteps=1000, learned_variance=False)
+    deterministic_fill_(dec.unets[0])
+    dec = dec.cuda()
+    tr = VideoDecoderTrainer(dec, lr=3e-4, use_ema=False, use_graphs=True)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    video = torch.rand(2, 3, 4, 32, 32, device="cuda", generator=g)
+    torch.cuda.manual_seed(1)
+    tr(video=video, unet_number=1)
+    tr.update(1)  # builds the flat gradient buffer
+    opt = tr.optim0
+    res = {}
+    for tag, seed in (("A", 7), ("B", 8), ("C", 7), ("D", 8)):  # A, B eager warm-up; C captures
+        opt.zero_grad()
+        torch.cuda.manual_seed(seed)
+        loss = tr(video=video, unet_number=1)
+        torch.cuda.synchronize()
+        res[tag] = (loss, opt.flat_grad.clone())
+    assert len(tr._graphs) == 1 and "graph" in next(iter(tr._graphs.values()))
+    G = opt.flat_grad
+    views = [(n, (p.grad.data_ptr() - G.data_ptr()) // 4, p.numel()) for n, p in dec.named_parameters()
+             if p.grad is not None]
+    for e, gph in (("A", "C"), ("B", "D")):
+        le, ge = res[e]
+        lg, gg = res[gph]
+        assert abs(le - lg) <= 1e-5 * abs(le), (e, le, lg)
+        err = ((ge - gg).norm() / ge.norm()).item()
+        if err >= 1e-5:
+            worst = sorted(((((ge[o:o + k] - gg[o:o + k]).norm() / ge[o:o + k].norm().clamp_min(1e-30)).item(), n)
+                            for n, o, k in views), reverse=True)[:8]
+            raise AssertionError(f"{e} vs {gph}: rel {err:.3e}; worst params {worst}")
