@@ -823,6 +823,10 @@ int launch_wgrad_glds(WgradGArgs a, hipStream_t st) {
   long long per = ((long long)a.M + want - 1) / want;
   per = ((per + 255) / 256) * 256;
   if (per < 256) per = 256;
+  // batched GEMMs have tiny outputs: at most 16 blocks add into one element
+  // (same-address atomic contention dominated them otherwise)
+  if (a.batch_pix > 0 && (a.batch_pix + per - 1) / per > 16)
+    per = ((a.batch_pix + 15) / 16 + 63) / 64 * 64;
   unsigned splits;
   if (a.batch_pix > 0) {
     const long long nbatch = a.M / a.batch_pix;
@@ -936,6 +940,8 @@ inline void glds_tile(long long M, int cout, int& bm, int& bn) {
   bn = cout <= 64 ? 64 : 128;
   bm = bn == 64 ? 256 : 128;
   if (((M + bm - 1) / bm) * ((cout + bn - 1) / bn) < 512) bm = 128;
+  // fewer 128-pixel tiles than CUs (8x8 stage, mid block): halve the pixel tile
+  if (bn == 128 && ((M + 127) / 128) * ((cout + 127) / 128) < 256) bm = 64;
 }
 
 template <typename T>
@@ -955,6 +961,7 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
       glds_tile(a.M, cout, bm, bn);
       if (bm == 256) return launch_fwd_glds<256, 64>(a, st);
       if (bn == 64) return launch_fwd_glds<128, 64>(a, st);
+      if (bm == 64) return launch_fwd_glds<64, 128>(a, st);
       return launch_fwd_glds<128, 128>(a, st);
     }
   }

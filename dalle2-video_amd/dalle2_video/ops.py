@@ -58,6 +58,8 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld):
         bm = 256 if bn == 64 else 128
         if ((m + bm - 1) // bm) * ((cout + bn - 1) // bn) < 512:
             bm = 128
+        if bn == 128 and ((m + 127) // 128) * ((cout + 127) // 128) < 256:
+            bm = 64
         return f"conv_fwd_glds_kernel<{bm},{bn}>"
     bm, bn = conv_tile(m, cout)
     return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"

@@ -45,7 +45,19 @@ def conv_case(nf, h, w, cin, cout, k, dtype=torch.bfloat16):
           f"{flops/ms/1e9:7.1f} TF/s | wgrad {msw*1e3:8.1f} us {flops/msw/1e9:7.1f} TF/s")
 
 
+def gemm_case(nb, rows, m, n):
+    from dalle2_video._lib import call, ptr, stream
+    a = torch.randn(nb * rows, m, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(nb * rows, n, device="cuda", dtype=torch.bfloat16)
+    o = torch.zeros(nb, m, n, device="cuda")
+    ms = timeit(lambda: call("dv_gemm_tn_batched", 1, ptr(a), m, ptr(b), n, ptr(o), rows, nb, m, n, stream()))
+    print(f"gemm_tn_batched nb={nb} rows={rows} {m}x{n}: {ms*1e3:8.1f} us")
+
+
 if __name__ == "__main__":
+    gemm_case(4, 16384, 32, 64)
+    gemm_case(4, 4096, 32, 128)
+    gemm_case(4, 1024, 32, 256)
     for dt_ in (torch.bfloat16,):
         conv_case(64, 64, 64, 64, 64, 3, dt_)
         conv_case(64, 64, 64, 128, 64, 3, dt_)
