@@ -885,6 +885,30 @@ __global__ void pack_weight_kernel(const float* w, T* out, int cout, int cin, in
   }
 }
 
+// many weights in one launch: blockIdx.y selects the table entry
+__global__ void pack_weight_batched_kernel(const DvPackEntry* table) {
+  const DvPackEntry e = table[blockIdx.y];
+  const long long rows = e.mode == 0 ? e.cout : e.cin;
+  const long long total = rows * e.taps * e.pad_to;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (e.mode == 0) {
+      const int ci = (int)(idx % e.pad_to);
+      const long long t = idx / e.pad_to;
+      const int tap = (int)(t % e.taps), co = (int)(t / e.taps);
+      if (ci < e.cin) v = e.w[((long long)co * e.cin + ci) * e.taps + tap];
+    } else {
+      const int co = (int)(idx % e.pad_to);
+      const long long t = idx / e.pad_to;
+      const int tapd = (int)(t % e.taps), ci = (int)(t / e.taps);
+      if (co < e.cout) v = e.w[((long long)co * e.cin + ci) * e.taps + (e.taps - 1 - tapd)];
+    }
+    if (e.dtype == DV_BF16) ((bf16*)e.out)[idx] = (bf16)v;
+    else ((float*)e.out)[idx] = v;
+  }
+}
+
 // reads the packed workspace [cout][tap][cin] and zeroes it behind itself, so a
 // cached workspace is always zero on entry to the next wgrad (no memset launch)
 __global__ void unpack_wgrad_kernel(float* ws, float* dw, int cout, int cin, int taps,
@@ -1064,6 +1088,16 @@ extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0
   if (dtype == DV_BF16)
     return conv_wgrad_t<bf16>(dy, lddy, x0, ld0, c0, x1, ld1, ws, db, nf, h, w, cin, cout, ksize, st);
   DV_REQUIRE(false, "unknown dtype");
+}
+
+extern "C" int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, long long max_elems,
+                                            void* stream) {
+  DV_REQUIRE(table && n >= 0 && n <= 65535, "bad table");
+  if (n == 0 || max_elems <= 0) return DV_OK;
+  long long bx = (max_elems + 255) / 256;
+  if (bx > 256) bx = 256;
+  pack_weight_batched_kernel<<<dim3((unsigned)bx, (unsigned)n), 256, 0, (hipStream_t)stream>>>(table);
+  return check_launch("pack_conv_weights_batched");
 }
 
 extern "C" int dv_unpack_wgrad(float* ws, float* dw, int cout, int cin, int ksize,

@@ -506,24 +506,39 @@ __global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, cons
     else dkv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + part * NH * DH + h * DH + d] = v;
   };
   if (part == 0) {
-    for (int dd = 0; dd < DH / 4; ++dd) {
-      const int d = w * (DH / 4) + dd;
-      const float* wrow = wq + (long long)(h * DH + d) * C;
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    // stage dat[b][:, h*3 .. h*3+2] once (C x 3 floats); then wave w owns 16
+    // head dims, lanes sweep c over coalesced Wq rows, 4 rows in flight
+    extern __shared__ float dsh[];  // 3*C floats
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const float* dr = datb + (long long)c * HK;
+      dsh[3 * c] = dr[0];
+      dsh[3 * c + 1] = dr[1];
+      dsh[3 * c + 2] = dr[2];
+    }
+    __syncthreads();
+    for (int dd = 0; dd < DH / 4; dd += 4) {
+      float s[4][3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u][0] = s[u][1] = s[u][2] = 0.f;
       for (int c = lane; c < C; c += 64) {
-        const float wv = wrow[c];
-        const float* dr = datb + (long long)c * HK;
-        s0 += dr[0] * wv;
-        s1 += dr[1] * wv;
-        s2 += dr[2] * wv;
+        const float a0 = dsh[3 * c], a1 = dsh[3 * c + 1], a2 = dsh[3 * c + 2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float wv = wq[(long long)(h * DH + w * (DH / 4) + dd + u) * C + c];
+          s[u][0] += a0 * wv;
+          s[u][1] += a1 * wv;
+          s[u][2] += a2 * wv;
+        }
       }
-      s0 = wave_sum(s0);
-      s1 = wave_sum(s1);
-      s2 = wave_sum(s2);
-      if (lane == 0) {
-        emit(0, d, s0 * scale);
-        emit(1, d, s1 * scale);
-        emit(2, d, s2 * scale);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float t0 = wave_sum(s[u][0]), t1 = wave_sum(s[u][1]), t2 = wave_sum(s[u][2]);
+        if (lane == 0) {
+          const int d = w * (DH / 4) + dd + u;
+          emit(0, d, t0 * scale);
+          emit(1, d, t1 * scale);
+          emit(2, d, t2 * scale);
+        }
       }
     }
   } else {
@@ -621,7 +636,7 @@ extern "C" int dv_xattn_fold_bwd(float* wsR, float* wsV, float* wsQ,
   fold_grad_finish_kernel<<<dim3((C + 63) / 64, nb), 256, 0, st>>>(wsR, wsV, wsQ, mcorr, at, vt, g1, dat, dvt, dg1, dg2, nb, C);
   fold_bwd_w_kernel<<<grid_for((long long)NH * DH * C), 256, 0, st>>>(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale, acc_w);
   if (!acc_w) zero_f32(dnull, 2 * DH, st);
-  fold_bwd_kv_kernel<<<dim3(NH, nb, 2), 256, 0, st>>>(dat, dvt, wq, wo, dkv, dnull,
+  fold_bwd_kv_kernel<<<dim3(NH, nb, 2), 256, sizeof(float) * 3 * C, st>>>(dat, dvt, wq, wo, dkv, dnull,
                                                      mcorr, C, scale);
   return check_launch("xattn_fold_bwd");
 }

@@ -30,6 +30,7 @@ _SIGS = {
     "dv_unpack_wgrad": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
     "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
+    "dv_pack_conv_weights_batched": [_P, _I, _L, _P],
     "dv_gn_fwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P],
     "dv_gn_bwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "dv_ln_fwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _P, _F, _P, _P, _P],

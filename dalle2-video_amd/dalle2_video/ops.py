@@ -160,17 +160,83 @@ def _pad_channels(t: torch.Tensor, mult: int = 8) -> torch.Tensor:
     return out
 
 
+class PackCache:
+    """Packed MFMA images of conv / token-linear weights, kept in fixed buffers.
+
+    Disabled by default (every conv packs its weight on the fly).  The trainer
+    enables it: weights then only change inside `update()`, which calls
+    `refresh()` — ONE batched launch repacks every cached weight in place — so
+    the forward/backward (and a captured HIP graph of them) launch no pack
+    kernels.  An entry is reused only if the trainer's epoch and the weight's
+    torch version counter (bumped by load_state_dict, EMA lerp_, ...) match."""
+
+    def __init__(self):
+        self.enabled = False
+        self.epoch = 0
+        self.entries = {}  # key -> dict(out, w, meta, epoch, version)
+        self._table = None
+        self._table_key = None
+
+    def lookup(self, weight, w, dtype, cout, cin, k, pad_to, mode):
+        key = (weight.data_ptr(), tuple(weight.shape), dtype, pad_to, mode)
+        e = self.entries.get(key)
+        if e is not None and e["epoch"] == self.epoch and e["version"] == weight._version:
+            return e["out"], False
+        if e is None:
+            rows = cout if mode == 0 else cin
+            e = dict(out=torch.empty(rows, k * k, pad_to, dtype=dtype, device=weight.device),
+                     w=w, meta=(cout, cin, k * k, pad_to, mode))
+            self.entries[key] = e
+            self._table_key = None
+        e["epoch"], e["version"] = self.epoch, weight._version
+        return e["out"], True
+
+    def refresh(self):
+        """New epoch (weights were updated): repack all entries in one launch."""
+        import ctypes
+        self.epoch += 1
+        if not self.entries:
+            return
+        ents = list(self.entries.values())
+        dev = ents[0]["out"].device
+        if self._table_key != len(ents) or self._table is None:
+            rows = []
+            for e in ents:
+                cout, cin, taps, pad_to, mode = e["meta"]
+                dtc = _lib.DV_BF16 if e["out"].dtype == torch.bfloat16 else _lib.DV_F32
+                rows.append((e["w"].data_ptr(), e["out"].data_ptr(), dtc, cout, cin, taps, pad_to, mode))
+            raw = torch.tensor([[a, b, (c | (d << 32)), (f | (g << 32)), (h | (m << 32))]
+                                for a, b, c, d, f, g, h, m in rows], dtype=torch.int64)
+            self._table = raw.to(dev)
+            self._table_key = len(ents)
+            self._max = max(e["out"].numel() for e in ents)
+        call("dv_pack_conv_weights_batched", ptr(self._table), len(ents), self._max, stream())
+        for e in ents:
+            e["epoch"] = self.epoch
+
+    def clear(self):
+        self.entries.clear()
+        self._table = self._table_key = None
+
+
+PACK = PackCache()
+
+
 def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int) -> torch.Tensor:
     if weight.dim() not in (2, 5) or (weight.dim() == 5 and weight.shape[-1] != weight.shape[-2]):
         raise _lib.DVError(f"conv weight must be (cout, cin) or (cout, cin, 1, k, k), got {tuple(weight.shape)}")
     cout, cin = weight.shape[0], weight.shape[1]
     k = weight.shape[-1] if weight.dim() == 5 else 1  # nn.Linear weights are 1x1 convs
-    rows = cout if mode == 0 else cin
-    out = torch.empty(rows, k * k, pad_to, dtype=dtype,
-                                                      device=weight.device)
     w = weight.detach()
     if w.dtype != torch.float32 or not w.is_contiguous():
         w = w.float().contiguous()
+    if PACK.enabled and w.data_ptr() == weight.data_ptr():
+        out, stale = PACK.lookup(weight, w, dtype, cout, cin, k, pad_to, mode)
+        if not stale:
+            return out
+    else:
+        rows = cout if mode == 0 else cin
+        out = torch.empty(rows, k * k, pad_to, dtype=dtype, device=weight.device)
     call("dv_pack_conv_weight", _lib.DV_BF16 if dtype == torch.bfloat16 else _lib.DV_F32,
          ptr(w), ptr(out), cout, cin, k, pad_to, mode, stream())
     return out

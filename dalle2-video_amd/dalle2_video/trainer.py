@@ -277,6 +277,10 @@ class VideoDecoderTrainer(nn.Module):
         # host-side kernel launches per step.
         self.use_graphs = (os.environ.get("DV_GRAPHS", "") == "1") if use_graphs is None else use_graphs
         self._graphs = {}
+        # weights change only in update(): keep their packed MFMA images cached
+        from . import ops
+        if os.environ.get("DV_PACK_CACHE", "1") != "0":
+            ops.PACK.enabled = True
         assert isinstance(decoder, VideoDecoder)
         ema_kwargs, kwargs = groupby_prefix_and_trim("ema_", kwargs)
         self.accelerator = accelerator
@@ -335,11 +339,17 @@ class VideoDecoderTrainer(nn.Module):
         index = unet_number - 1
         opt = getattr(self, f"optim{index}")
         sched = getattr(self, f"sched{index}")
+        fresh = opt.flat_grad is None
         opt.ensure_flat()
         allreduce_flat_grad(opt.flat_grad, self.world)
         coef = opt.clip_coefficient(self.max_grad_norm, prescale=1.0 / self.world)
         opt.step(clip_coef=coef)
         opt.zero_grad()
+        from . import ops
+        if ops.PACK.enabled:
+            # the first step re-points parameters into the flat buffer: drop the
+            # images keyed on the old storage; afterwards repack in one launch
+            ops.PACK.clear() if fresh else ops.PACK.refresh()
         warm = self.warmup_schedulers[index]
         with (warm.dampening() if exists(warm) else nullcontext()):
             sched.step()
@@ -459,6 +469,8 @@ class VideoDecoderTrainer(nn.Module):
         assert path.exists()
         obj = torch.load(str(path), map_location="cpu", weights_only=True)
         self.load_state_dict(obj, only_model=only_model, strict=strict)
+        from . import ops
+        ops.PACK.refresh()  # weights replaced: repack every cached image
         return obj
 
     @torch.no_grad()

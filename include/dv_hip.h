@@ -74,6 +74,17 @@ int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix,
 int dv_pack_conv_weight(int dtype, const float* w, void* out, int cout, int cin, int ksize,
                         int pad_to, int mode, void* stream);
 
+/* Repack many weights in one launch (the trainer calls it once per optimizer
+ * step for every cached conv / token-linear weight).  `table` is a DEVICE
+ * array of n entries; max_elems = the largest entry's element count.       */
+typedef struct {
+  const float* w;  /* f32 torch weight (cout, cin, 1, k, k) */
+  void* out;       /* packed image, layout as dv_pack_conv_weight(mode) */
+  int dtype, cout, cin, taps, pad_to, mode;
+} DvPackEntry;
+int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, long long max_elems,
+                                 void* stream);
+
 /* Batched TN GEMM on the wgrad engine: out[g][i][j] += sum_{r in group g}
  * A[r][i]*B[r][j]; A rows x m (lda), B rows x n (ldb), nbatch groups of
  * batch_rows consecutive rows; out f32 [nbatch][m][n] (atomics, pre-zeroed).
