@@ -263,7 +263,8 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
 // backward: one wave = 32 tokens
 //   writes dx (incl. residual), dO (tokens x C), dS' = rs*dS and
 //   P' = rs2*P (k'=3 -> mu2*rs2) (tokens x 32) for the batched GEMMs, and
-//   accumulates mcorr[b][k'] = sum_t mu_t*rs_t*dS_tk'
+//   (the LN mean correction sum_t mu_t*rs_t*dS_tk' is NOT accumulated here:
+//    it equals (1/C) sum_c R[b][k'][c], the row sums of the R = dS'^T X GEMM)
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, const T* x, int ldx,
@@ -272,8 +273,7 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
                                                         const T* Vt, const T* VtT,
                                                         const float* colsum, const float* g2,
                                                         const float* stats, const T* pbuf,
-                                                        T* dobuf, T* dsbuf, T* p2buf,
-                                                        float* mcorr) {
+                                                        T* dobuf, T* dsbuf, T* p2buf) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   // waves tile each batch element's P tokens; lanes past P mirror token P-1
   // (their MFMA columns are independent) and store nothing
@@ -376,14 +376,6 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
     if (valid) st4<T>(dsbuf + tok * KP + 8 * m + 4 * h, w);
     if (valid) st4<T>(p2buf + tok * KP + 8 * m + 4 * h, q);
   }
-  // mcorr[b][k'] += sum over the 32 tokens of mu*rs*ds  (reduce over lanes of each half)
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    float v = valid ? mu * rs * ds[e] : 0.f;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
-    if (r == 0) atomicAdd(mcorr + b * KP + acc_row(e, h), v);
-  }
   a1 = (a1 + __shfl_xor(a1, 32, 64)) / C;  // mean_c dxhat
   a2 = (a2 + __shfl_xor(a2, 32, 64)) / C;  // mean_c dxhat*xhat
   // ---- pass C: dXhat^T = KtT . dS^T, LN_in backward + residual ----
@@ -408,6 +400,19 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
       if (valid) st4<T>(dxr + c, w);
     }
   }
+}
+
+// mcorr[b][k'] = (1/C) sum_c R[b][k'][c]  (= sum_t mu_t * dS'_tk', mu_t the
+// channel mean of token t); one block per (b, k'), R rows read coalesced
+__global__ __launch_bounds__(256) void fold_mcorr_kernel(const float* wsR, float* mcorr, int C) {
+  __shared__ float red[4];
+  const int row = blockIdx.x;  // b*KP + k'
+  float s = 0.f;
+  for (int c = threadIdx.x; c < C; c += 256) s += wsR[(long long)row * C + c];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) mcorr[row] = (red[0] + red[1] + red[2] + red[3]) / C;
 }
 
 // dat/dvt [nb][C][24] from the GEMM results (ws_* [nb][32][C]) and the LN gain
@@ -493,12 +498,11 @@ __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const floa
 // dV = dvt[:, hj]^T Wo_h (lane = head dim, coalesced Wo rows, waves split c).
 __global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, const float* dvt,
                                                           const float* wq, const float* wo,
-                                                          float* dkv, float* dnull, float* mcorr,
-                                                          int C, float scale) {
+                                                          float* dkv, float* dnull, int C,
+                                                          float scale) {
   __shared__ float red[4][NK][DH];
   const int h = blockIdx.x, b = blockIdx.y, part = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (h == 0 && part == 0 && threadIdx.x < KP) mcorr[b * KP + threadIdx.x] = 0.f;  // consumed
   const float* datb = dat + (long long)b * C * HK + h * NK;
   const float* dvtb = dvt + (long long)b * C * HK + h * NK;
   auto emit = [&](int j, int d, float v) {
@@ -606,16 +610,16 @@ extern "C" int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const vo
                                    const void* KtT, const void* Vt, const void* VtT,
                                    const float* colsum, const float* g2, const float* stats,
                                    const void* pbuf, void* dobuf, void* dsbuf, void* p2buf,
-                                   float* mcorr, void* stream) {
+                                   void* stream) {
   DV_REQUIRE(dy && x && dx && KtT && Vt && VtT && colsum && g2 && stats && pbuf && dobuf && dsbuf &&
-             p2buf && mcorr, "null pointer");
+             p2buf, "null pointer");
   DV_REQUIRE(P > 0 && ntok % P == 0 && C % 8 == 0, "bad shape");
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (int)(((ntok / P) * ((P + 31) / 32) + 3) / 4);
   if (dtype == DV_BF16)
-    xattn_bwd_kernel<bf16><<<blocks, 256, 0, st>>>((const bf16*)dy, lddy, (const bf16*)x, ldx, (bf16*)dx, lddx, ntok, P, C, (const bf16*)KtT, (const bf16*)Vt, (const bf16*)VtT, colsum, g2, stats, (const bf16*)pbuf, (bf16*)dobuf, (bf16*)dsbuf, (bf16*)p2buf, mcorr);
+    xattn_bwd_kernel<bf16><<<blocks, 256, 0, st>>>((const bf16*)dy, lddy, (const bf16*)x, ldx, (bf16*)dx, lddx, ntok, P, C, (const bf16*)KtT, (const bf16*)Vt, (const bf16*)VtT, colsum, g2, stats, (const bf16*)pbuf, (bf16*)dobuf, (bf16*)dsbuf, (bf16*)p2buf);
   else
-    xattn_bwd_kernel<float><<<blocks, 256, 0, st>>>((const float*)dy, lddy, (const float*)x, ldx, (float*)dx, lddx, ntok, P, C, (const float*)KtT, (const float*)Vt, (const float*)VtT, colsum, g2, stats, (const float*)pbuf, (float*)dobuf, (float*)dsbuf, (float*)p2buf, mcorr);
+    xattn_bwd_kernel<float><<<blocks, 256, 0, st>>>((const float*)dy, lddy, (const float*)x, ldx, (float*)dx, lddx, ntok, P, C, (const float*)KtT, (const float*)Vt, (const float*)VtT, colsum, g2, stats, (const float*)pbuf, (float*)dobuf, (float*)dsbuf, (float*)p2buf);
   return check_launch("xattn_bwd_tokens");
 }
 
@@ -633,10 +637,11 @@ extern "C" int dv_xattn_fold_bwd(float* wsR, float* wsV, float* wsQ,
     if (dg1) zero_f32(dg1, C, st);
     if (dg2) zero_f32(dg2, C, st);
   }
+  fold_mcorr_kernel<<<nb * KP, 256, 0, st>>>(wsR, mcorr, C);
   fold_grad_finish_kernel<<<dim3((C + 63) / 64, nb), 256, 0, st>>>(wsR, wsV, wsQ, mcorr, at, vt, g1, dat, dvt, dg1, dg2, nb, C);
   fold_bwd_w_kernel<<<grid_for((long long)NH * DH * C), 256, 0, st>>>(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale, acc_w);
   if (!acc_w) zero_f32(dnull, 2 * DH, st);
   fold_bwd_kv_kernel<<<dim3(NH, nb, 2), 256, sizeof(float) * 3 * C, st>>>(dat, dvt, wq, wo, dkv, dnull,
-                                                     mcorr, C, scale);
+                                                     C, scale);
   return check_launch("xattn_fold_bwd");
 }

@@ -49,7 +49,7 @@ _SIGS = {
     "dv_p_sample": [_I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_xattn_fold": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P],
     "dv_xattn_fwd": [_I, _P, _I, _P, _I, _L, _L, _I, _P, _P, _P, _P, _F, _P, _P, _P],
-    "dv_xattn_bwd_tokens": [_I, _P, _I, _P, _I, _P, _I, _L, _L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "dv_xattn_bwd_tokens": [_I, _P, _I, _P, _I, _P, _I, _L, _L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "dv_xattn_fold_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _I, _P],
     "dv_gemm_tn_batched": [_I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _P],
     "dv_resize_nearest": [_P, _P, _L, _I, _I, _I, _I, _I, _F, _F, _P],

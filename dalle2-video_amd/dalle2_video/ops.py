@@ -129,8 +129,8 @@ _XA_WS = {}
 
 
 def _xattn_workspace(nb, C, device):
-    """Cross-attention backward accumulators (wsR, wsV, wsQ [nb][32][C], mcorr
-    [nb][32]): zero on entry, re-zeroed by dv_xattn_fold_bwd after use."""
+    """Cross-attention backward accumulators (wsR, wsV, wsQ [nb][32][C]): zero
+    on entry, re-zeroed by dv_xattn_fold_bwd after use; mcorr [nb][32] scratch."""
     key = (nb, C, str(device))
     if key not in _XA_WS:
         _XA_WS[key] = tuple(torch.zeros(nb, 32, C, dtype=torch.float32, device=device) for _ in range(3)) + (
@@ -585,7 +585,7 @@ class CrossAttnFn(torch.autograd.Function):
         ldx = cl_ld(x)
         call("dv_xattn_bwd_tokens", dt(x), ptr(dy), C, ptr(x), ldx, ptr(dx), C, ntok, P, C,
              ptr(KtT), ptr(Vt), ptr(VtT), ptr(colsum), ptr(g2f), ptr(stats), ptr(pbuf), ptr(dobuf),
-             ptr(dsbuf), ptr(p2buf), ptr(mcorr), stream())
+             ptr(dsbuf), ptr(p2buf), stream())
         # per-batch token reductions: R = dS'^T X, V' = P^T dO, Q = P'^T dY (one batched GEMM each)
         for a_, b_, ldb, o_ in ((dsbuf, x, ldx, wsR), (pbuf, dobuf, C, wsV), (p2buf, dy, C, wsQ)):
             _launch("gemm_tn_batched:" + conv_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldb)),

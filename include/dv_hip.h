@@ -214,17 +214,17 @@ int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ldo, long lon
                  long long P, int C, const void* Kt, const void* Vt, const float* colsum,
                  const float* g2, float eps, float* stats, void* pbuf, void* stream);
 /* token part of the backward: dx (incl. residual); dobuf [ntok][C], dsbuf
- * and p2buf [ntok][32] feed three dv_gemm_tn_batched reductions; mcorr
- * [nb][32] f32 (zero on entry) accumulates the LN mean correction.          */
+ * and p2buf [ntok][32] feed three dv_gemm_tn_batched reductions.           */
 int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const void* x, int ldx, void* dx,
                         int lddx, long long ntok, long long P, int C, const void* KtT,
                         const void* Vt, const void* VtT, const float* colsum, const float* g2,
                         const float* stats, const void* pbuf, void* dobuf, void* dsbuf,
-                        void* p2buf, float* mcorr, void* stream);
+                        void* p2buf, void* stream);
 /* parameter part: from the GEMM results wsR/wsV/wsQ [nb][32][C] to
  * dg1, dg2 (acc_g), dwq [512][C], dwo [C][512], dnull [2][64] (acc_w) and
- * dkv [nb][2][1024] (overwritten).  wsR/wsV/wsQ and mcorr are consumed and
- * left ZEROED, so cached accumulators need no memset before the next call. */
+ * dkv [nb][2][1024] (overwritten).  wsR/wsV/wsQ are consumed and left
+ * ZEROED, so cached accumulators need no memset before the next call; mcorr
+ * [nb][32] is scratch (the LN mean correction, from the row sums of wsR).  */
 int dv_xattn_fold_bwd(float* wsR, float* wsV, float* wsQ, float* mcorr,
                       const float* at, const float* vt, const float* g1, const float* wq,
                       const float* wo, const float* kv, const float* null_kv, float* dat,
