@@ -909,25 +909,6 @@ __global__ void pack_weight_batched_kernel(const DvPackEntry* table) {
   }
 }
 
-// reads the packed workspace [cout][tap][cin] and zeroes it behind itself, so a
-// cached workspace is always zero on entry to the next wgrad (no memset launch)
-__global__ void unpack_wgrad_kernel(float* ws, float* dw, int cout, int cin, int taps,
-                                    int cout_real, int cin_real, int accumulate) {
-  long long total = (long long)cout * cin * taps;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    const int ci = (int)(idx % cin);
-    const long long t = idx / cin;
-    const int tap = (int)(t % taps), co = (int)(t / taps);
-    const float v = ws[idx];
-    ws[idx] = 0.f;
-    if (co < cout_real && ci < cin_real) {
-      float* o = dw + ((long long)co * cin_real + ci) * taps + tap;
-      *o = accumulate ? *o + v : v;
-    }
-  }
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void bias_grad_kernel(const T* dy, int lddy, float* db,
                                                         long long npix, int c, long long rows_per) {
@@ -1053,6 +1034,327 @@ int conv_wgrad_t(const void* dy, int lddy, const void* x0, int ld0, int c0, cons
   return launch_wgrad<T, 128, 128>(a, st);
 }
 
+// ---------------------------------------------------------------------------
+// bf16 3x3 wgrad, stripe form (cin, cout % 64 == 0; W in {8, 16, 32, 64}):
+// dW[co][tap][ci] = sum_p dY[p][co] X[p + tap][ci] for ALL nine taps of a
+// 64(co) x 64(ci) tile in one workgroup, over a contiguous range of 128-pixel
+// stages (grid z = pixel split).  A stage stages its 128 dY rows and the
+// WINDOW of X pixels they see — NSEG segments of (seg + 2) image rows of
+// W + 2 pixels (halo from a zeroed line), 128 B per pixel — so X is staged
+// once per stage (not once per tap: the nine taps read the same window at
+// row offsets dy*(W+2) + dx), and each CU does all nine taps' MFMAs per byte
+// staged.  8 waves: waves 4-7 take the second 64-pixel half of every stage;
+// each wave owns a 32(co) x 32(ci) tile of every tap (9 accumulators).  The
+// two halves are summed through LDS and written with plain stores to
+// part[z][co][tap][ci] (no atomics); wgrad_reduce_kernel sums the splits.
+// ---------------------------------------------------------------------------
+struct WgradSArgs {
+  const bf16* dy;
+  int lddy;
+  const bf16* x0;
+  const bf16* x1;
+  int ld0, ld1, c0;
+  float* part;    // [S][cout][K]
+  float* dbpart;  // [S][cout] or null
+  int H, cin, cout, K;
+  int nstages, stages_per_split;
+  int seg, nseg;  // image rows per window segment, segments per stage
+};
+
+template <int W> struct StripeGeom {
+  static constexpr int WP = W + 2;
+  static constexpr int WR = W == 8 ? 200 : (128 / W + 2) * WP;  // window rows (max over H)
+  static constexpr int NRH = (WR + 127) / 128;                  // 128-row DMA rounds per half
+  static constexpr int AIMG = 2 * 128 * 64;                     // dY image: 2 co halves x 128 rows x 64 B
+  static constexpr int BHALF = NRH * 128 * 64;                  // window image of one ci half
+  static constexpr int STG = AIMG + 2 * BHALF;
+  static constexpr int NBUF = STG * 3 <= 160 * 1024 ? 3 : 2;
+};
+
+// LDS images are split by 32-channel half into 64-B rows: four consecutive
+// rows then start 16 banks apart, so the transposed operand reads are
+// conflict-free WITHOUT a swizzle, and an operand address is linear in the
+// row — every tap's window offset folds into the ds_read immediate.
+template <int W>
+__global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
+  using G = StripeGeom<W>;
+  constexpr int WP = G::WP, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF;
+  constexpr int AIMG = G::AIMG, BHALF = G::BHALF;
+  constexpr int DPS = 2 + 2 * NRH;  // DMAs per thread per stage
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * STG];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wave >> 2, wq = wave & 3, wm = wq >> 1, wn = wq & 1;
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64;
+  const int sbeg = blockIdx.z * a.stages_per_split;
+  const int send = min(sbeg + a.stages_per_split, a.nstages);
+  const int nst = send - sbeg;
+  const bf16* zero = (const bf16*)g_zero_line;
+  const int HW = a.H * W, seg = a.seg, segrows = (seg + 2) * WP;
+
+  // ---- static per-lane DMA slots: row 16*wave + (lane >> 2) of each 128-row
+  // round, 16-B chunk (lane & 3) of a 64-B half row ----
+  const int l4 = lane >> 2, c4 = lane & 3;
+  const bf16* a_src = a.dy + co0 + 8 * c4;
+  const bool first = ci0 < a.c0;
+  const bf16* b_src = (first ? a.x0 + ci0 : a.x1 + (ci0 - a.c0)) + 8 * c4;
+  const int xld = first ? a.ld0 : a.ld1;
+  int b_off[NRH], b_ry[NRH];  // b_ry: image-row offset, or a large negative for halo / junk rows
+#pragma unroll
+  for (int i = 0; i < NRH; ++i) {
+    const int wr = 128 * i + 16 * wave + l4;
+    const int sg = wr / segrows, rem = wr - sg * segrows;
+    const int ry = rem / WP, rx = rem - ry * WP;
+    const bool ok = sg < a.nseg && rx >= 1 && rx <= W;
+    b_ry[i] = ok ? ry - 1 : -(1 << 20);
+    b_off[i] = sg * seg * W + (ry - 1) * W + (rx - 1);
+  }
+
+  auto issue = [&](int st, int buf) {
+    const int m0 = (sbeg + st) * 128;
+    char* sA = smem + buf * STG;
+    char* sB = sA + AIMG;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const bf16* src = a_src + 32 * hh + (long long)(m0 + 16 * wave + l4) * a.lddy;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(sA + hh * (AIMG / 2) + 16 * wave * 64),
+                                       16, 0, 0);
+    }
+    const int y0 = a.nseg > 1 ? 0 : (m0 % HW) / W;
+#pragma unroll
+    for (int i = 0; i < NRH; ++i) {
+      const bool in = (unsigned)(y0 + b_ry[i]) < (unsigned)a.H;
+      const bf16* src = in ? b_src + (long long)(m0 + b_off[i]) * xld : zero;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(in ? src + 32 * hh : zero),
+                                         (__attribute__((address_space(3))) void*)(sB + hh * BHALF + (128 * i + 16 * wave) * 64),
+                                         16, 0, 0);
+    }
+  };
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int d = 0; d < 9; ++d)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[d][e] = 0.f;
+  // bias gradient on the VALU: a lane's A fragment holds 8 pixels of ONE
+  // output channel (row lane % 32 of the 32x32x16 A operand)
+  float accb = 0.f;
+  const bool do_bias = a.dbpart != nullptr && blockIdx.y == 0 && wn == 0;  // wave-uniform
+
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int colb = 32 * (g & 1) + 8 * pp;  // byte column of this lane in a 64-B half row
+  // window rows (tap (0,0)) of this lane's two pixels in each of the 4 k-steps
+  int wlo[4], whi[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int plo = half * 64 + 16 * s + 8 * (g >> 1) + q, phi = plo + 4;
+    const int sl = plo / (seg * W), sh = phi / (seg * W);
+    const int rl = plo - sl * seg * W, rh = phi - sh * seg * W;
+    wlo[s] = (sl * segrows + (rl / W) * WP + rl % W) * 64 + colb;
+    whi[s] = (sh * segrows + (rh / W) * WP + rh % W) * 64 + colb;
+  }
+
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < nst) issue(i, i);
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st % NBUF;
+    if (st + NBUF - 1 < nst) {
+      issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS * (NBUF - 1)) : "memory");
+    } else if (NBUF >= 3 && st + 2 < nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS * 2) : "memory");
+    } else if (st + 1 < nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* sA = smem + buf * STG + wm * (AIMG / 2);
+    const char* sB = smem + buf * STG + AIMG + wn * BHALF;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int R0 = half * 64 + 16 * s + 8 * (g >> 1);
+      u32x4 fa;
+      {
+        const s16x4 lo = tr_read(sA + (R0 + q) * 64 + colb);
+        const s16x4 hi = tr_read(sA + (R0 + 4 + q) * 64 + colb);
+        const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+        fa = u32x4{l2[0], l2[1], h2[0], h2[1]};
+      }
+#pragma unroll
+      for (int d = 0; d < 9; ++d) {
+        const int toff = ((d / 3) * WP + (d % 3)) * 64;
+        const s16x4 lo = tr_read(sB + wlo[s] + toff);
+        const s16x4 hi = tr_read(sB + whi[s] + toff);
+        const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+        acc[d] = Mma<bf16>::run(fa, u32x4{l2[0], l2[1], h2[0], h2[1]}, acc[d]);
+      }
+      if (do_bias) {
+        float t[8];
+        Vec<bf16>::to_f(fa, t);
+        accb += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  accb += __shfl_xor(accb, 32, 64);  // both k-halves of the channel
+
+  // ---- sum the two pixel halves through LDS (two passes), plain stores ----
+  float* red = (float*)smem;
+  const int r = lane & 31, h = lane >> 5;
+  float* pz = a.part + (long long)blockIdx.z * a.cout * a.K;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    constexpr int PER = (5 * 16 + 1) * 64;  // <= 5 taps + the bias sums per wave
+    const int d0 = pass == 0 ? 0 : 5, d1 = pass == 0 ? 5 : 9;
+    if (half == 1) {
+#pragma unroll
+      for (int d = d0; d < d1; ++d)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) red[wq * PER + ((d - d0) * 16 + e) * 64 + lane] = acc[d][e];
+      if (pass == 0) red[wq * PER + 5 * 16 * 64 + lane] = accb;
+    }
+    __syncthreads();
+    if (half == 0) {
+#pragma unroll
+      for (int d = d0; d < d1; ++d) {
+        const int col = d * a.cin + ci0 + wn * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int co = co0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          pz[(long long)co * a.K + col] = acc[d][e] + red[wq * PER + ((d - d0) * 16 + e) * 64 + lane];
+        }
+      }
+      if (pass == 0 && do_bias && lane < 32)
+        a.dbpart[(long long)blockIdx.z * a.cout + co0 + wm * 32 + lane] =
+            accb + red[wq * PER + 5 * 16 * 64 + lane];
+    }
+    __syncthreads();
+  }
+}
+
+// dw[co][ci][tap] (torch layout, real sizes) (+)= sum_s part[s][co][tap][ci]
+// and db[co] (+)= sum_s dbpart[s][co].  A workgroup sums 64 consecutive
+// packed elements; its 4 waves take every 4th split (coalesced 256-B rows,
+// 4 loads in flight per lane) and meet in LDS.  The last ceil(cout/64)
+// workgroups reduce the bias partials the same way.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, int S, int cout,
+                                                           int cin, int taps, float* dw,
+                                                           int cout_real, int cin_real, int acc_w,
+                                                           const float* dbpart, float* db,
+                                                           int acc_b) {
+  __shared__ float sh[4][64];
+  const long long total = (long long)cout * cin * taps;
+  const long long wblocks = (total + 63) / 64;
+  const int ol = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const bool bias = blockIdx.x >= wblocks;
+  const long long o = (bias ? blockIdx.x - wblocks : blockIdx.x) * 64 + ol;
+  const long long n = bias ? cout : total;
+  const float* src = bias ? dbpart : part;
+  float v = 0.f;
+  if (o < n) {
+    int s = grp;
+    for (; s + 12 < S; s += 16) {
+      const float p0 = src[(long long)s * n + o], p1 = src[(long long)(s + 4) * n + o];
+      const float p2 = src[(long long)(s + 8) * n + o], p3 = src[(long long)(s + 12) * n + o];
+      v += (p0 + p1) + (p2 + p3);
+    }
+    for (; s < S; s += 4) v += src[(long long)s * n + o];
+  }
+  sh[grp][ol] = v;
+  __syncthreads();
+  if (grp != 0 || o >= n) return;
+  v = sh[0][ol] + sh[1][ol] + sh[2][ol] + sh[3][ol];
+  if (bias) {
+    if (o < cout_real) db[o] = acc_b ? db[o] + v : v;
+    return;
+  }
+  const int ci = (int)(o % cin);
+  const long long t = o / cin;
+  const int tap = (int)(t % taps), co = (int)(t / taps);
+  if (co >= cout_real || ci >= cin_real) return;
+  float* out = dw + ((long long)co * cin_real + ci) * taps + tap;
+  *out = acc_w ? *out + v : v;
+}
+
+void launch_wgrad_reduce(const float* part, int S, int cout, int cin, int taps, float* dw,
+                         int cout_real, int cin_real, int acc_w, const float* dbpart, float* db,
+                         int acc_b, hipStream_t st) {
+  const long long total = (long long)cout * cin * taps;
+  const long long blocks = (total + 63) / 64 + (db ? (cout + 63) / 64 : 0);
+  wgrad_reduce_kernel<<<(unsigned)blocks, 256, 0, st>>>(part, S, cout, cin, taps, dw, cout_real,
+                                                          cin_real, acc_w, dbpart, db, acc_b);
+}
+
+// stage geometry for the stripe wgrad (0 = shape not supported)
+bool stripe_geom(int h, int w, int& seg, int& nseg) {
+  if (!(w == 8 || w == 16 || w == 32 || w == 64)) return false;
+  const int hw = h * w;
+  if (hw >= 128) {
+    seg = 128 / w;
+    nseg = 1;
+    return h % seg == 0 && (w != 8 || seg + 2 <= 20);
+  }
+  if (128 % hw) return false;
+  seg = h;
+  nseg = 128 / hw;
+  return nseg * (h + 2) * (w + 2) <= (w == 8 ? 200 : (128 / w + 2) * (w + 2));
+}
+
+bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout, int ks) {
+  int seg, nseg;
+  if (ks != 3 || cin % 64 || cout % 64 || (split && c0 % 64)) return false;
+  const long long M = (long long)nf * h * w;
+  if (M % 128 || M >= (1ll << 31)) return false;
+  return stripe_geom(h, w, seg, nseg);
+}
+
+// split count: ~256 workgroups (one per CU: the stage ring takes up to 112 KB of LDS)
+inline void stripe_split(int nstages, int grid_xy, int& sps, int& S) {
+  long long want = 256 / grid_xy;
+  if (want < 1) want = 1;
+  if (want > nstages) want = nstages;
+  sps = (int)((nstages + want - 1) / want);
+  S = (nstages + sps - 1) / sps;
+}
+
+long long wgrad_stripe_ws(int nf, int h, int w, int cin, int cout) {
+  const int nstages = (int)((long long)nf * h * w / 128);
+  int sps, S;
+  stripe_split(nstages, (cout / 64) * (cin / 64), sps, S);
+  return (long long)S * cout * (9LL * cin + 1);
+}
+
+int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
+                      int ld1, float* ws, float* dw, int acc_w, float* db, int acc_b, int nf, int h,
+                      int w, int cin, int cout, int cout_real, int cin_real, hipStream_t st) {
+  WgradSArgs a;
+  a.dy = (const bf16*)dy; a.lddy = lddy; a.x0 = (const bf16*)x0;
+  a.x1 = (const bf16*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0; a.c0 = x1 ? c0 : cin;
+  a.H = h; a.cin = cin; a.cout = cout; a.K = 9 * cin;
+  stripe_geom(h, w, a.seg, a.nseg);
+  a.nstages = (int)((long long)nf * h * w / 128);
+  int S;
+  stripe_split(a.nstages, (cout / 64) * (cin / 64), a.stages_per_split, S);
+  a.part = ws;
+  a.dbpart = db ? ws + (long long)S * cout * a.K : nullptr;
+  dim3 grid(cout / 64, cin / 64, S);
+  switch (w) {
+    case 64: conv_wgrad_stripe_kernel<64><<<grid, 512, 0, st>>>(a); break;
+    case 32: conv_wgrad_stripe_kernel<32><<<grid, 512, 0, st>>>(a); break;
+    case 16: conv_wgrad_stripe_kernel<16><<<grid, 512, 0, st>>>(a); break;
+    default: conv_wgrad_stripe_kernel<8><<<grid, 512, 0, st>>>(a); break;
+  }
+  launch_wgrad_reduce(a.part, S, cout, cin, 9, dw, cout_real, cin_real, acc_w, a.dbpart, db, acc_b, st);
+  return check_launch("conv_wgrad_stripe");
+}
+
 }  // namespace
 
 extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
@@ -1075,19 +1377,49 @@ extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const voi
   DV_REQUIRE(false, "unknown dtype");
 }
 
+extern "C" int dv_conv_wgrad_ws(int dtype, int nf, int h, int w, int cin, int c0, int split,
+                                int cout, int ksize, long long* floats) {
+  DV_REQUIRE(floats, "null pointer");
+  DV_REQUIRE(cin > 0 && cout > 0 && ksize >= 1, "bad sizes");
+  const long long K = (long long)ksize * ksize * cin;
+  if (dtype == DV_BF16 && wgrad_stripe_ok(nf, h, w, cin, c0, split != 0, cout, ksize))
+    *floats = wgrad_stripe_ws(nf, h, w, cin, cout);
+  else
+    *floats = (long long)cout * (K + 1);
+  return DV_OK;
+}
+
 extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0,
-                             int c0, const void* x1, int ld1, float* ws, float* db, int nf, int h,
-                             int w, int cin, int cout, int ksize, void* stream) {
-  DV_REQUIRE(dy && x0 && ws, "null pointer");
+                             int c0, const void* x1, int ld1, float* dw, int accumulate_w,
+                             float* db, int accumulate_b, float* ws, long long ws_floats, int nf,
+                             int h, int w, int cin, int cout, int cout_real, int cin_real,
+                             int ksize, void* stream) {
+  DV_REQUIRE(dy && x0 && dw && ws, "null pointer");
   DV_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "cin/cout must be multiples of 8");
+  DV_REQUIRE(cout_real <= cout && cin_real <= cin && cout_real > 0 && cin_real > 0,
+             "real sizes exceed the padded ones");
   DV_REQUIRE(lddy % 8 == 0 && ld0 % 8 == 0 && (!x1 || (ld1 % 8 == 0 && c0 % 8 == 0)),
              "strides must be multiples of 8");
+  DV_REQUIRE(dtype == DV_F32 || dtype == DV_BF16, "unknown dtype");
+  long long need = 0;
+  dv_conv_wgrad_ws(dtype, nf, h, w, cin, c0, x1 != nullptr, cout, ksize, &need);
+  DV_REQUIRE(ws_floats >= need, "workspace too small (see dv_conv_wgrad_ws)");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == DV_F32)
-    return conv_wgrad_t<float>(dy, lddy, x0, ld0, c0, x1, ld1, ws, db, nf, h, w, cin, cout, ksize, st);
-  if (dtype == DV_BF16)
-    return conv_wgrad_t<bf16>(dy, lddy, x0, ld0, c0, x1, ld1, ws, db, nf, h, w, cin, cout, ksize, st);
-  DV_REQUIRE(false, "unknown dtype");
+  if ((long long)nf * h * w == 0) return DV_OK;
+  if (dtype == DV_BF16 && wgrad_stripe_ok(nf, h, w, cin, c0, x1 != nullptr, cout, ksize))
+    return conv_wgrad_stripe(dy, lddy, x0, ld0, c0, x1, ld1, ws, dw, accumulate_w, db, accumulate_b,
+                             nf, h, w, cin, cout, cout_real, cin_real, st);
+  // general path: f32 atomics into the zeroed packed workspace, then one reduce
+  const long long K = (long long)ksize * ksize * cin;
+  float* dbp = db ? ws + cout * K : nullptr;
+  zero_f32(ws, cout * (K + 1), st);
+  int rc = dtype == DV_F32
+               ? conv_wgrad_t<float>(dy, lddy, x0, ld0, c0, x1, ld1, ws, dbp, nf, h, w, cin, cout, ksize, st)
+               : conv_wgrad_t<bf16>(dy, lddy, x0, ld0, c0, x1, ld1, ws, dbp, nf, h, w, cin, cout, ksize, st);
+  if (rc != DV_OK) return rc;
+  launch_wgrad_reduce(ws, 1, cout, cin, ksize * ksize, dw, cout_real, cin_real, accumulate_w, dbp,
+                      db, accumulate_b, st);
+  return check_launch("conv_wgrad");
 }
 
 extern "C" int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, long long max_elems,
@@ -1098,19 +1430,6 @@ extern "C" int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, lon
   if (bx > 256) bx = 256;
   pack_weight_batched_kernel<<<dim3((unsigned)bx, (unsigned)n), 256, 0, (hipStream_t)stream>>>(table);
   return check_launch("pack_conv_weights_batched");
-}
-
-extern "C" int dv_unpack_wgrad(float* ws, float* dw, int cout, int cin, int ksize,
-                               int cout_real, int cin_real, int accumulate, void* stream) {
-  DV_REQUIRE(ws && dw && cout_real <= cout && cin_real <= cin, "bad arguments");
-  const int taps = ksize * ksize;
-  long long total = (long long)cout * cin * taps;
-  if (total == 0) return DV_OK;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  unpack_wgrad_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(ws, dw, cout, cin, taps, cout_real,
-                                                               cin_real, accumulate);
-  return check_launch("unpack_wgrad");
 }
 
 extern "C" int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix, int c,

@@ -269,6 +269,142 @@ __global__ __launch_bounds__(256) void linear_small_dx_kernel(const float* dy, i
     atomicAdd(dx + (long long)b * lddx + k, acc[b] * act_in_d(x[(long long)b * ldx + k], act_in));
 }
 
+
+// ---------------------------------------------------------------------------
+// grouped small linears (dv_linear_group_*): every entry's rows are cut into
+// 64-row workgroup tiles; the entry table rides in the kernel arguments (no
+// device table, graph-capture safe).  Forward: 4 lanes per output row stream
+// its W row in 16-B pieces against act_in(x) staged in LDS, then a 2-step
+// lane reduction.  Backward: the same row mapping writes dW / db; for dx each
+// thread owns a k column and streams the tile's W rows coalesced, and the
+// tiles meet in f32 atomics in `ws`; the workgroup arriving last applies
+// act_in'(x), writes dx and re-zeroes ws.
+// ---------------------------------------------------------------------------
+constexpr int LG_MAX = 48, LG_ROWS = 64, LG_MAXB = 8, LG_MAXK = 512;
+struct LinGroupArgs {
+  const float* x;
+  float* dx;
+  float* ws;
+  int B, K, act_in, n, acc_dx, finalize;
+  int blk0[LG_MAX + 1];
+  DvLinEntry e[LG_MAX];
+};
+
+__device__ __forceinline__ int lg_entry(const LinGroupArgs& a, int blk) {
+  int e = 0;
+  while (e + 1 < a.n && blk >= a.blk0[e + 1]) ++e;
+  return e;
+}
+
+__global__ __launch_bounds__(256) void linear_group_fwd_kernel(LinGroupArgs a) {
+  __shared__ __attribute__((aligned(16))) float xs[LG_MAXB * LG_MAXK];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < a.B * a.K; i += 256) xs[i] = act_in_f(a.x[i], a.act_in);
+  __syncthreads();
+  const int e = lg_entry(a, blockIdx.x);
+  const DvLinEntry E = a.e[e];
+  const int lane = tid & 63, q = lane & 3;
+  const int n = (blockIdx.x - a.blk0[e]) * LG_ROWS + (tid >> 6) * 16 + (lane >> 2);
+  float acc[LG_MAXB];
+#pragma unroll
+  for (int b = 0; b < LG_MAXB; ++b) acc[b] = 0.f;
+  if (n < E.n) {
+    const float* wr = E.w + (long long)n * a.K;
+    for (int k = q * 4; k < a.K; k += 16) {
+      const f32x4 w = *(const f32x4*)(wr + k);
+#pragma unroll
+      for (int b = 0; b < LG_MAXB; ++b) {
+        if (b < a.B) {
+          const f32x4 xv = *(const f32x4*)(xs + b * a.K + k);
+          acc[b] += w[0] * xv[0] + w[1] * xv[1] + w[2] * xv[2] + w[3] * xv[3];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < LG_MAXB; ++b) {
+    acc[b] += __shfl_xor(acc[b], 1, 64);
+    acc[b] += __shfl_xor(acc[b], 2, 64);
+  }
+  if (n < E.n && q == 0) {
+    const float bias = E.bias ? E.bias[n] : 0.f;
+#pragma unroll
+    for (int b = 0; b < LG_MAXB; ++b)
+      if (b < a.B) E.y[(long long)b * E.n + n] = acc[b] + bias;
+  }
+}
+
+__global__ __launch_bounds__(256) void linear_group_bwd_kernel(LinGroupArgs a) {
+  __shared__ __attribute__((aligned(16))) float xs[LG_MAXB * LG_MAXK];
+  __shared__ float gs[LG_MAXB][LG_ROWS];
+  __shared__ int last;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < a.B * a.K; i += 256) xs[i] = act_in_f(a.x[i], a.act_in);
+  const int e = lg_entry(a, blockIdx.x);
+  const DvLinEntry E = a.e[e];
+  const int row0 = (blockIdx.x - a.blk0[e]) * LG_ROWS;
+  const int rows = min(LG_ROWS, E.n - row0);
+  for (int i = tid; i < LG_MAXB * LG_ROWS; i += 256) {
+    const int b = i / LG_ROWS, r = i % LG_ROWS;
+    gs[b][r] = (b < a.B && r < rows) ? E.y[(long long)b * E.n + row0 + r] : 0.f;
+  }
+  __syncthreads();
+  // dW / db rows: 4 lanes per row
+  if (E.dw) {
+    const int lane = tid & 63, q = lane & 3, r = (tid >> 6) * 16 + (lane >> 2);
+    if (r < rows) {
+      const int n = row0 + r;
+      float* dwr = E.dw + (long long)n * a.K;
+      for (int k = q * 4; k < a.K; k += 16) {
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < LG_MAXB; ++b) {
+          if (b < a.B) {
+            const f32x4 xv = *(const f32x4*)(xs + b * a.K + k);
+            s += gs[b][r] * xv;
+          }
+        }
+        if (E.accumulate_w) s += *(const f32x4*)(dwr + k);
+        *(f32x4*)(dwr + k) = s;
+      }
+      if (E.db && q == 0) {
+        float sb = 0.f;
+        for (int b = 0; b < a.B; ++b) sb += gs[b][r];
+        E.db[n] = E.accumulate_w ? E.db[n] + sb : sb;
+      }
+    }
+  }
+  // dx partial over this tile's rows: one thread per k column
+  if (a.dx) {
+    for (int k = tid; k < a.K; k += 256) {
+      float acc[LG_MAXB];
+#pragma unroll
+      for (int b = 0; b < LG_MAXB; ++b) acc[b] = 0.f;
+      const float* wp = E.w + (long long)row0 * a.K + k;
+#pragma unroll 8
+      for (int r = 0; r < rows; ++r) {
+        const float w = wp[(long long)r * a.K];
+#pragma unroll
+        for (int b = 0; b < LG_MAXB; ++b) acc[b] += gs[b][r] * w;  // rows b >= B are zero
+      }
+      for (int b = 0; b < a.B; ++b) atomicAdd(a.ws + b * a.K + k, acc[b]);
+    }
+    if (!a.finalize) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics are performed
+    __syncthreads();
+    if (tid == 0) last = atomicAdd((unsigned*)(a.ws + a.B * a.K), 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    for (int i = tid; i < a.B * a.K; i += 256) {
+      const float v = __hip_atomic_load(a.ws + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.ws[i] = 0.f;
+      const float d = v * act_in_d(a.x[i], a.act_in);
+      a.dx[i] = a.acc_dx ? a.dx[i] + d : d;
+    }
+    if (tid == 0) *(unsigned*)(a.ws + a.B * a.K) = 0u;
+  }
+}
+
 __global__ void adamw_kernel(float* p, const float* g, float* m, float* v, long long n,
                              long long n_wd, float lr, float b1, float b2, float eps, float wd,
                              float bc1, float bc2_sqrt, const float* clip) {
@@ -546,4 +682,58 @@ extern "C" int dv_gaussian_blur(const float* x, float* y, long long planes, int 
   DV_REQUIRE(x && y && w1 && (ks & 1) && ks / 2 < H && ks / 2 < W, "bad arguments");
   blur_kernel<<<grid_for(planes * H * W), 256, 0, (hipStream_t)stream>>>(x, y, planes, H, W, ks, w1);
   return check_launch("gaussian_blur");
+}
+
+static int linear_group(bool bwd, const float* x, int B, int K, int act_in, const DvLinEntry* entries,
+                        int n_entries, float* dx, int accumulate_dx, float* ws, hipStream_t st) {
+  bool any = false;
+  for (int s0 = 0; s0 < n_entries; s0 += LG_MAX) {
+    LinGroupArgs a;
+    a.x = x; a.dx = dx; a.ws = ws; a.B = B; a.K = K; a.act_in = act_in; a.acc_dx = accumulate_dx;
+    a.n = n_entries - s0 < LG_MAX ? n_entries - s0 : LG_MAX;
+    a.finalize = s0 + LG_MAX >= n_entries;
+    int blk = 0;
+    for (int i = 0; i < a.n; ++i) {
+      a.e[i] = entries[s0 + i];
+      a.blk0[i] = blk;
+      blk += (entries[s0 + i].n + LG_ROWS - 1) / LG_ROWS;
+    }
+    a.blk0[a.n] = blk;
+    if (blk == 0) continue;
+    any = true;
+    if (bwd) linear_group_bwd_kernel<<<blk, 256, 0, st>>>(a);
+    else linear_group_fwd_kernel<<<blk, 256, 0, st>>>(a);
+  }
+  if (bwd && dx && !any) {  // no rows at all: dx gets nothing (still honour accumulate)
+    if (!accumulate_dx) zero_f32(dx, (long long)B * K, st);
+  }
+  return check_launch(bwd ? "linear_group_bwd" : "linear_group_fwd");
+}
+
+static const char* lg_validate(const float* x, int B, int K, const DvLinEntry* entries,
+                               int n_entries) {
+  if (!x || !entries || n_entries < 0) return "null pointer";
+  if (B < 1 || B > LG_MAXB || K < 4 || K > LG_MAXK || K % 4 != 0)
+    return "need 1 <= B <= 8, K % 4 == 0, K <= 512";
+  for (int i = 0; i < n_entries; ++i)
+    if (!entries[i].w || !entries[i].y || entries[i].n < 0) return "bad entry";
+  return nullptr;
+}
+
+extern "C" int dv_linear_group_fwd(const float* x, int B, int K, int act_in, const DvLinEntry* entries,
+                                   int n_entries, void* stream) {
+  const char* bad = lg_validate(x, B, K, entries, n_entries);
+  DV_REQUIRE(!bad, bad ? bad : "");
+  return linear_group(false, x, B, K, act_in, entries, n_entries, nullptr, 0, nullptr,
+                      (hipStream_t)stream);
+}
+
+extern "C" int dv_linear_group_bwd(const float* x, int B, int K, int act_in, const DvLinEntry* entries,
+                                   int n_entries, float* dx, int accumulate_dx, float* ws,
+                                   void* stream) {
+  const char* bad = lg_validate(x, B, K, entries, n_entries);
+  DV_REQUIRE(!bad, bad ? bad : "");
+  DV_REQUIRE(!dx || ws, "backward dx needs ws");
+  return linear_group(true, x, B, K, act_in, entries, n_entries, dx, accumulate_dx, ws,
+                      (hipStream_t)stream);
 }

@@ -25,9 +25,17 @@ __device__ __forceinline__ void st_vec<bf16>(bf16* p, const float* v) {
 }
 
 // --------------------------------------------------------------------------
-// per-(batch, channel) partial sums: ws[b][c] = {sum f(x), sum g(x)}
-//   MODE 0 (stats):    f = z, g = z^2
-//   MODE 1 (bwd):      f = dv, g = dv*zhat   (dv = dy * act'(v))
+// GroupNorm in two launches per direction, no finalize launch:
+//   reduce: per-(batch, channel) partial sums into `sums` [nb][C][2] (f32
+//           atomics; zero on entry):
+//             MODE 0 (stats): f = z, g = z^2
+//             MODE 1 (bwd):   f = dv, g = dv*zhat   (dv = dy * act'(v))
+//   apply:  every workgroup derives its sample's per-group terms from the
+//           2C sums in its prologue (mean/rstd, or m1/m2), then streams.
+// The sums are not re-zeroed by the call that used them (its apply
+// workgroups are still reading them); instead every apply zeroes `next`, the
+// buffer the NEXT GroupNorm call accumulates into (the caller alternates two
+// buffers), so no counter, fence or serial tail is needed.
 // --------------------------------------------------------------------------
 struct GnArgs {
   const void* z; int ldz;
@@ -35,24 +43,18 @@ struct GnArgs {
   void* out; int ldo;
   const void* res; int ldres;
   int nb; long long P; int C, G;
-  const float* mean; const float* rstd;
+  float* mean; float* rstd;   // fwd: written by the apply; bwd: read
   const float* gamma; const float* beta;
   const float* ss;  // (nb, 2C): scale | shift, or null
   int act;
-  float* ws;        // nb * C * 2
-  float* ws2;       // nb * G * 2 (bwd group coefficients)
+  float* sums;      // nb * C * 2, zero on entry
+  float* next;      // zeroed by the apply (next call's sums), or null
+  long long next_n;
+  float eps;
+  float *dgamma, *dbeta, *dss;
+  int accumulate;
   long long rows_per_block;
 };
-
-template <typename T>
-__device__ __forceinline__ void gn_point(const GnArgs& a, int b, int c, float z, float& zhat,
-                                         float& u, float& v) {
-  const int g = c / (a.C / a.G);
-  const float mu = a.mean[b * a.G + g], rs = a.rstd[b * a.G + g];
-  zhat = (z - mu) * rs;
-  u = zhat * a.gamma[c] + a.beta[c];
-  v = a.ss ? u * (1.f + a.ss[(long long)b * 2 * a.C + c]) + a.ss[(long long)b * 2 * a.C + a.C + c] : u;
-}
 
 // Per-thread fixed channel vector [cv, cv+VEC) of batch b = blockIdx.y; the
 // per-channel affine coefficients are hoisted out of the pixel loop:
@@ -61,11 +63,12 @@ struct ChanCoef {
   float A, B, rs, zb, K1;
 };
 template <int VEC>
-__device__ __forceinline__ void load_coef(const GnArgs& a, int b, int cv, ChanCoef* k) {
+__device__ __forceinline__ void load_coef(const GnArgs& a, int b, int cv, const float* mean,
+                                          const float* rstd, ChanCoef* k) {
 #pragma unroll
   for (int e = 0; e < VEC; ++e) {
     const int c = cv + e, g = c / (a.C / a.G);
-    const float mu = a.mean[b * a.G + g], rs = a.rstd[b * a.G + g];
+    const float mu = mean[g], rs = rstd[g];
     const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
     const float sh = a.ss ? a.ss[(long long)b * 2 * a.C + a.C + c] : 0.f;
     k[e].A = rs * a.gamma[c] * sc;
@@ -81,15 +84,27 @@ __device__ __forceinline__ float silu_grad(float v) {
   return sg * (1.f + v * (1.f - sg));
 }
 
+// U pixel rows per thread are loaded before any is used (U x 16 B, or 2U x 16 B
+// in the backward, in flight per lane) so the streaming passes are not
+// latency-bound; the reduce keeps ~768 workgroups so its per-(b, c) atomics
+// stay lightly contended.
+constexpr int GN_U = 4;
+
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
+  constexpr int U = MODE == 0 ? 2 * GN_U : GN_U;
   __shared__ float sh[2][256 * VEC];
+  __shared__ float smu[64], srs[64];
   const int tpr = a.C / VEC;                 // threads per pixel row
   const int rpp = 256 / tpr;                 // rows per pass
   const int tid = threadIdx.x;
   const int rr = tid / tpr, cv = (tid % tpr) * VEC;
   const int b = blockIdx.y;
+  if (MODE == 1) {
+    for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
+    __syncthreads();
+  }
   const long long beg = blockIdx.x * a.rows_per_block;
   long long end = beg + a.rows_per_block;
   if (end > a.P) end = a.P;
@@ -98,23 +113,37 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   for (int e = 0; e < VEC; ++e) s1[e] = s2[e] = 0.f;
   if (rr < rpp) {
     ChanCoef k[MODE == 1 ? VEC : 1];
-    if (MODE == 1) load_coef<VEC>(a, b, cv, k);
-    for (long long p = beg + rr; p < end; p += rpp) {
-      const long long pix = (long long)b * a.P + p;
-      float z[VEC];
-      ld_vec<T>((const T*)a.z + pix * a.ldz + cv, z);
-      if (MODE == 0) {
+    if (MODE == 1) load_coef<VEC>(a, b, cv, smu, srs, k);
+    const T* zb = (const T*)a.z + (long long)b * a.P * a.ldz + cv;
+    const T* dyb = (const T*)a.dy + (long long)b * a.P * a.lddy + cv;
+    for (long long p0 = beg + rr; p0 < end; p0 += (long long)rpp * U) {
+      u32x4 zr[U], dr[MODE == 1 ? U : 1];
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) { s1[e] += z[e]; s2[e] += z[e] * z[e]; }
-      } else {
-        float dy[VEC];
-        ld_vec<T>((const T*)a.dy + pix * a.lddy + cv, dy);
+      for (int u = 0; u < U; ++u) {
+        const long long p = p0 + (long long)u * rpp;
+        if (p < end) {
+          zr[u] = *(const u32x4*)(zb + p * a.ldz);
+          if (MODE == 1) dr[u] = *(const u32x4*)(dyb + p * a.lddy);
+        }
+      }
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          const float v = z[e] * k[e].A + k[e].B;
-          const float dv = a.act == DV_ACT_SILU ? dy[e] * silu_grad(v) : dy[e];
-          s1[e] += dv;
-          s2[e] += dv * (z[e] * k[e].rs + k[e].zb);
+      for (int u = 0; u < U; ++u) {
+        if (p0 + (long long)u * rpp >= end) break;
+        float z[VEC];
+        Vec<T>::to_f(zr[u], z);
+        if (MODE == 0) {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) { s1[e] += z[e]; s2[e] += z[e] * z[e]; }
+        } else {
+          float dy[VEC];
+          Vec<T>::to_f(dr[u], dy);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            const float v = z[e] * k[e].A + k[e].B;
+            const float dv = a.act == DV_ACT_SILU ? dy[e] * silu_grad(v) : dy[e];
+            s1[e] += dv;
+            s2[e] += dv * (z[e] * k[e].rs + k[e].zb);
+          }
         }
       }
     }
@@ -133,62 +162,51 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
       t1 += sh[0][(r * tpr + owner) * VEC + e];
       t2 += sh[1][(r * tpr + owner) * VEC + e];
     }
-    atomicAdd(a.ws + ((long long)b * a.C + c) * 2, t1);
-    atomicAdd(a.ws + ((long long)b * a.C + c) * 2 + 1, t2);
+    atomicAdd(a.sums + ((long long)b * a.C + c) * 2, t1);
+    atomicAdd(a.sums + ((long long)b * a.C + c) * 2 + 1, t2);
   }
 }
 
-__global__ void gn_stats_finalize(float* ws, float* mean, float* rstd, int nb, long long P,
-                                  int C, int G, float eps) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nb * G) return;
-  const int b = i / G, g = i % G, cg = C / G;
-  double s1 = 0.0, s2 = 0.0;
-  for (int c = g * cg; c < (g + 1) * cg; ++c) {
-    float* w = ws + ((long long)b * C + c) * 2;
-    s1 += w[0];
-    s2 += w[1];
-    w[0] = 0.f;  // leave the workspace zeroed for the next reduction
-    w[1] = 0.f;
-  }
-  const double n = (double)P * cg;
-  const double mu = s1 / n;
-  double var = s2 / n - mu * mu;
-  if (var < 0) var = 0;
-  mean[i] = (float)mu;
-  rstd[i] = (float)(1.0 / sqrt(var + (double)eps));
-}
-
-// bwd stage 2: parameter grads and per-(b,g) correction terms
-__global__ void gn_bwd_finalize(GnArgs a, float* dgamma, float* dbeta, float* dss, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < a.C) {
-    float dg = 0.f, db = 0.f;
-    for (int b = 0; b < a.nb; ++b) {
-      const float r1 = a.ws[((long long)b * a.C + c) * 2], r2 = a.ws[((long long)b * a.C + c) * 2 + 1];
-      const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
-      dg += sc * r2;
-      db += sc * r1;
-      if (dss) {
-        dss[(long long)b * 2 * a.C + c] = a.gamma[c] * r2 + a.beta[c] * r1;  // d scale
-        dss[(long long)b * 2 * a.C + a.C + c] = r1;                          // d shift
+// apply prologue: this sample's per-group terms from its [C][2] sums, one
+// wave per group (channel sums combined in double for the variance).
+//   MODE 0: t1 = mean, t2 = rstd      MODE 1: t1 = m1, t2 = m2
+template <int MODE>
+__device__ void gn_group_terms(const GnArgs& a, int b, float* t1, float* t2) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cg = a.C / a.G;
+  const float* sb = a.sums + (long long)b * a.C * 2;
+  for (int g = wave; g < a.G; g += 4) {
+    if (MODE == 0) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int c = g * cg + lane; c < (g + 1) * cg; c += 64) {
+        s1 += sb[2 * c];
+        s2 += sb[2 * c + 1];
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      if (lane == 0) {
+        const double n = (double)a.P * cg;
+        const double mu = s1 / n;
+        double var = s2 / n - mu * mu;
+        if (var < 0) var = 0;
+        t1[g] = (float)mu;
+        t2[g] = (float)(1.0 / sqrt(var + (double)a.eps));
+      }
+    } else {
+      float m1 = 0.f, m2 = 0.f;
+      for (int c = g * cg + lane; c < (g + 1) * cg; c += 64) {
+        const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
+        const float k = a.gamma[c] * sc;
+        m1 += k * sb[2 * c];
+        m2 += k * sb[2 * c + 1];
+      }
+      m1 = wave_sum(m1);
+      m2 = wave_sum(m2);
+      if (lane == 0) {
+        const float n = (float)((double)a.P * cg);
+        t1[g] = m1 / n;
+        t2[g] = m2 / n;
       }
     }
-    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + dg : dg;
-    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + db : db;
-  }
-  if (c < a.nb * a.G) {
-    const int b = c / a.G, g = c % a.G, cg = a.C / a.G;
-    float m1 = 0.f, m2 = 0.f;
-    for (int cc = g * cg; cc < (g + 1) * cg; ++cc) {
-      const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + cc] : 1.f;
-      const float k = a.gamma[cc] * sc;
-      m1 += k * a.ws[((long long)b * a.C + cc) * 2];
-      m2 += k * a.ws[((long long)b * a.C + cc) * 2 + 1];
-    }
-    const float n = (float)((double)a.P * cg);
-    a.ws2[c * 2] = m1 / n;
-    a.ws2[c * 2 + 1] = m2 / n;
   }
 }
 
@@ -197,55 +215,104 @@ __global__ void gn_bwd_finalize(GnArgs a, float* dgamma, float* dbeta, float* ds
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
+  constexpr int U = GN_U;
+  __shared__ float t1[64], t2[64], smu[64], srs[64];
+  const int tid = threadIdx.x;
   const int tpr = a.C / VEC, rpp = 256 / tpr;
-  const int rr = threadIdx.x / tpr, cv = (threadIdx.x % tpr) * VEC;
-  const int b = blockIdx.y;
-  if (MODE == 1 && blockIdx.x == 0) {  // the reduction sums are consumed: re-zero them
-    for (int i = threadIdx.x; i < 2 * a.C; i += 256) a.ws[(long long)b * a.C * 2 + i] = 0.f;
+  const int rr = tid / tpr, cv = (tid % tpr) * VEC;
+  const int b = blockIdx.y, cg = a.C / a.G;
+  gn_group_terms<MODE>(a, b, t1, t2);
+  if (MODE == 1)
+    for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    if (MODE == 0) {  // saved for the backward
+      for (int g = tid; g < a.G; g += 256) { a.mean[b * a.G + g] = t1[g]; a.rstd[b * a.G + g] = t2[g]; }
+    } else if (b == 0) {  // parameter gradients over all samples
+      for (int c = tid; c < a.C; c += 256) {
+        float dg = 0.f, db = 0.f;
+        for (int bb = 0; bb < a.nb; ++bb) {
+          const float r1 = a.sums[((long long)bb * a.C + c) * 2];
+          const float r2 = a.sums[((long long)bb * a.C + c) * 2 + 1];
+          const float sc = a.ss ? 1.f + a.ss[(long long)bb * 2 * a.C + c] : 1.f;
+          dg += sc * r2;
+          db += sc * r1;
+          if (a.dss) {
+            a.dss[(long long)bb * 2 * a.C + c] = a.gamma[c] * r2 + a.beta[c] * r1;  // d scale
+            a.dss[(long long)bb * 2 * a.C + a.C + c] = r1;                          // d shift
+          }
+        }
+        if (a.dgamma) a.dgamma[c] = a.accumulate ? a.dgamma[c] + dg : dg;
+        if (a.dbeta) a.dbeta[c] = a.accumulate ? a.dbeta[c] + db : db;
+      }
+    }
+    if (b == 0 && a.next) {  // the next GroupNorm call's sums start at zero
+      for (long long i = tid * 4; i < a.next_n; i += 1024) {
+        if (i + 4 <= a.next_n) *(f32x4*)(a.next + i) = f32x4{0.f, 0.f, 0.f, 0.f};
+        else for (long long j = i; j < a.next_n; ++j) a.next[j] = 0.f;
+      }
+    }
   }
   if (rr >= rpp) return;
+  ChanCoef k[VEC];
+  float m1[VEC], m2[VEC];
+  if (MODE == 0) {
+    load_coef<VEC>(a, b, cv, t1, t2, k);
+  } else {
+    load_coef<VEC>(a, b, cv, smu, srs, k);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const int g = (cv + e) / cg;
+      m1[e] = -k[e].rs * t1[g];
+      m2[e] = -k[e].rs * t2[g];
+    }
+  }
   const long long beg = blockIdx.x * a.rows_per_block;
   long long end = beg + a.rows_per_block;
   if (end > a.P) end = a.P;
-  ChanCoef k[VEC];
-  load_coef<VEC>(a, b, cv, k);
-  float m1[VEC], m2[VEC];
-  if (MODE == 1) {
+  const long long pb = (long long)b * a.P;
+  for (long long p0 = beg + rr; p0 < end; p0 += (long long)rpp * U) {
+    u32x4 zr[U], xr[U];  // xr: res (fwd) or dy (bwd)
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      const int g = (cv + e) / (a.C / a.G);
-      m1[e] = -k[e].rs * a.ws2[(b * a.G + g) * 2];
-      m2[e] = -k[e].rs * a.ws2[(b * a.G + g) * 2 + 1];
-    }
-  }
-  for (long long p = beg + rr; p < end; p += rpp) {
-    const long long pix = (long long)b * a.P + p;
-    float z[VEC], o[VEC];
-    ld_vec<T>((const T*)a.z + pix * a.ldz + cv, z);
-    if (MODE == 0) {
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        const float v = z[e] * k[e].A + k[e].B;
-        o[e] = a.act == DV_ACT_SILU ? silu_f(v) : v;
-      }
-      if (a.res) {
-        float r[VEC];
-        ld_vec<T>((const T*)a.res + pix * a.ldres + cv, r);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) o[e] += r[e];
-      }
-    } else {
-      float dy[VEC];
-      ld_vec<T>((const T*)a.dy + pix * a.lddy + cv, dy);
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        const float v = z[e] * k[e].A + k[e].B;
-        const float dv = a.act == DV_ACT_SILU ? dy[e] * silu_grad(v) : dy[e];
-        const float zhat = z[e] * k[e].rs + k[e].zb;
-        o[e] = dv * k[e].K1 + m1[e] + zhat * m2[e];
+    for (int u = 0; u < U; ++u) {
+      const long long p = p0 + (long long)u * rpp;
+      if (p < end) {
+        zr[u] = *(const u32x4*)((const T*)a.z + (pb + p) * a.ldz + cv);
+        if (MODE == 1) xr[u] = *(const u32x4*)((const T*)a.dy + (pb + p) * a.lddy + cv);
+        else if (a.res) xr[u] = *(const u32x4*)((const T*)a.res + (pb + p) * a.ldres + cv);
       }
     }
-    st_vec<T>((T*)a.out + pix * a.ldo + cv, o);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long p = p0 + (long long)u * rpp;
+      if (p >= end) break;
+      float z[VEC], o[VEC];
+      Vec<T>::to_f(zr[u], z);
+      if (MODE == 0) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float v = z[e] * k[e].A + k[e].B;
+          o[e] = a.act == DV_ACT_SILU ? silu_f(v) : v;
+        }
+        if (a.res) {
+          float r[VEC];
+          Vec<T>::to_f(xr[u], r);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) o[e] += r[e];
+        }
+      } else {
+        float dy[VEC];
+        Vec<T>::to_f(xr[u], dy);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float v = z[e] * k[e].A + k[e].B;
+          const float dv = a.act == DV_ACT_SILU ? dy[e] * silu_grad(v) : dy[e];
+          const float zhat = z[e] * k[e].rs + k[e].zb;
+          o[e] = dv * k[e].K1 + m1[e] + zhat * m2[e];
+        }
+      }
+      st_vec<T>((T*)a.out + (pb + p) * a.ldo + cv, o);
+    }
   }
 }
 
@@ -256,38 +323,34 @@ int grid_for(long long work, int per_block = 256) {
   return (int)b;
 }
 
-// rows per reduce block: >= 8 passes of the row slots, >= ~512 blocks overall
-long long reduce_rows(const GnArgs& a, int vec) {
-  const long long rpp = 256 / (a.C / vec);
-  long long r = (a.P * a.nb + 511) / 512;
-  if (r < rpp * 8) r = rpp * 8;
-  if (r > 2048) r = 2048;
-  return (r + rpp - 1) / rpp * rpp;
+// rows per workgroup: a multiple of one unrolled pass (rpp * U), sized for
+// about `target` workgroups over the whole call
+long long gn_rows(const GnArgs& a, int vec, int u, long long target) {
+  const long long pass = (long long)(256 / (a.C / vec)) * u;
+  long long r = (a.P * a.nb + target - 1) / target;
+  r = (r + pass - 1) / pass * pass;
+  return r < pass ? pass : r;
 }
 
 template <typename T>
-int gn_fwd_t(GnArgs a, float eps, hipStream_t st) {
+int gn_fwd_t(GnArgs a, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
-  a.rows_per_block = reduce_rows(a, VEC);
+  a.rows_per_block = gn_rows(a, VEC, 2 * GN_U, 768);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_reduce_kernel<T, 0><<<g1, 256, 0, st>>>(a);
-  gn_stats_finalize<<<(a.nb * a.G + 63) / 64, 64, 0, st>>>(a.ws, (float*)a.mean, (float*)a.rstd,
-                                                          a.nb, a.P, a.C, a.G, eps);
-  a.rows_per_block = 256 / (a.C / VEC) * 16;  // 16 passes of the row slots per block
+  a.rows_per_block = gn_rows(a, VEC, GN_U, 2048);
   dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_apply_kernel<T, 0><<<g2, 256, 0, st>>>(a);
   return check_launch("gn_fwd");
 }
 
 template <typename T>
-int gn_bwd_t(GnArgs a, float* dgamma, float* dbeta, float* dss, int accumulate, hipStream_t st) {
+int gn_bwd_t(GnArgs a, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
-  a.rows_per_block = reduce_rows(a, VEC);
+  a.rows_per_block = gn_rows(a, VEC, GN_U, 768);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_reduce_kernel<T, 1><<<g1, 256, 0, st>>>(a);
-  int n2 = a.C > a.nb * a.G ? a.C : a.nb * a.G;
-  gn_bwd_finalize<<<(n2 + 63) / 64, 64, 0, st>>>(a, dgamma, dbeta, dss, accumulate);
-  a.rows_per_block = 256 / (a.C / VEC) * 16;
+  a.rows_per_block = gn_rows(a, VEC, GN_U, 2048);
   dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_apply_kernel<T, 1><<<g2, 256, 0, st>>>(a);
   return check_launch("gn_bwd");
@@ -408,40 +471,43 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* x, int ldx, const T* d
 extern "C" int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* res,
                          int ldres, int nb, long long P, int C, int G, float eps,
                          const float* gamma, const float* beta, const float* ss, int act,
-                         float* mean, float* rstd, float* ws, void* stream) {
-  DV_REQUIRE(z && y && gamma && beta && mean && rstd && ws, "null pointer");
+                         float* mean, float* rstd, float* sums, float* next, long long next_n,
+                         void* stream) {
+  DV_REQUIRE(z && y && gamma && beta && mean && rstd && sums, "null pointer");
   DV_REQUIRE(C % G == 0, "C % G != 0");
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && ldy % VEC == 0 && (!res || ldres % VEC == 0),
              "channel counts / strides must be multiples of 16 bytes");
-  DV_REQUIRE(C / VEC <= 256, "C too large");
+  DV_REQUIRE(C / VEC <= 256 && G <= 64, "C > 256 vectors or G > 64");
+  DV_REQUIRE(next != sums || !next, "next must not alias sums");
   GnArgs a{};
   a.z = z; a.ldz = ldz; a.out = y; a.ldo = ldy; a.res = res; a.ldres = ldres; a.nb = nb;
   a.P = P; a.C = C; a.G = G; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta;
-  a.ss = ss; a.act = act; a.ws = ws;
+  a.ss = ss; a.act = act; a.sums = sums; a.next = next; a.next_n = next ? next_n : 0; a.eps = eps;
   if (nb == 0 || P == 0) return DV_OK;
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DV_BF16 ? gn_fwd_t<bf16>(a, eps, st) : gn_fwd_t<float>(a, eps, st);
+  return dtype == DV_BF16 ? gn_fwd_t<bf16>(a, st) : gn_fwd_t<float>(a, st);
 }
 
 extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void* dz,
                          int lddz, int nb, long long P, int C, int G, const float* gamma,
                          const float* beta, const float* ss, int act, const float* mean,
-                         const float* rstd, float* dgamma, float* dbeta, float* dss, float* ws,
-                         float* ws2, int accumulate, void* stream) {
-  DV_REQUIRE(dy && z && dz && gamma && beta && mean && rstd && ws && ws2, "null pointer");
+                         const float* rstd, float* dgamma, float* dbeta, float* dss, float* sums,
+                         float* next, long long next_n, int accumulate, void* stream) {
+  DV_REQUIRE(dy && z && dz && gamma && beta && mean && rstd && sums, "null pointer");
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && lddy % VEC == 0 && lddz % VEC == 0,
              "channel counts / strides must be multiples of 16 bytes");
-  DV_REQUIRE(C / VEC <= 256 && C % G == 0, "bad C");
+  DV_REQUIRE(C / VEC <= 256 && G <= 64 && C % G == 0, "bad C / G");
+  DV_REQUIRE(next != sums || !next, "next must not alias sums");
   GnArgs a{};
   a.z = z; a.ldz = ldz; a.dy = dy; a.lddy = lddy; a.out = dz; a.ldo = lddz; a.nb = nb; a.P = P;
-  a.C = C; a.G = G; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.ss = ss;
-  a.act = act; a.ws = ws; a.ws2 = ws2;
+  a.C = C; a.G = G; a.mean = (float*)mean; a.rstd = (float*)rstd; a.gamma = gamma; a.beta = beta;
+  a.ss = ss; a.act = act; a.sums = sums; a.next = next; a.next_n = next ? next_n : 0;
+  a.dgamma = dgamma; a.dbeta = dbeta; a.dss = dss; a.accumulate = accumulate;
   if (nb == 0 || P == 0) return DV_OK;
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DV_BF16 ? gn_bwd_t<bf16>(a, dgamma, dbeta, dss, accumulate, st)
-                          : gn_bwd_t<float>(a, dgamma, dbeta, dss, accumulate, st);
+  return dtype == DV_BF16 ? gn_bwd_t<bf16>(a, st) : gn_bwd_t<float>(a, st);
 }
 
 extern "C" int dv_ln_fwd(int dtype, const void* x, int ldx, void* y, int ldy, const void* res,

@@ -34,4 +34,13 @@ int check_launch(const char* what) {
 }  // namespace dv
 
 extern "C" const char* dv_last_error(void) { return dv::g_last_error.c_str(); }
-extern "C" int dv_abi_version(void) { return 1; }
+extern "C" int dv_abi_version(void) { return 2; }
+
+extern "C" int dv_zero_f32(float* p, long long n, void* stream) {
+  if (!p) {
+    dv::set_error("dv_zero_f32: null pointer");
+    return DV_ERR_INVALID;
+  }
+  dv::zero_f32(p, n, (hipStream_t)stream);
+  return dv::check_launch("zero_f32");
+}

@@ -25,14 +25,15 @@ _F = ctypes.c_float
 # name -> argtypes (restype is always int except dv_last_error)
 _SIGS = {
     "dv_abi_version": [],
+    "dv_zero_f32": [_P, _L, _P],
     "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
-    "dv_conv_wgrad": [_I, _P, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
-    "dv_unpack_wgrad": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_conv_wgrad_ws": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dv_conv_wgrad": [_I, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
     "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "dv_pack_conv_weights_batched": [_P, _I, _L, _P],
-    "dv_gn_fwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P],
-    "dv_gn_bwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "dv_gn_fwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P, _L, _P],
+    "dv_gn_bwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "dv_ln_fwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _P, _F, _P, _P, _P],
     "dv_ln_bwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _F, _P, _P, _P],
     "dv_ncthw_to_cl": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
@@ -42,6 +43,8 @@ _SIGS = {
     "dv_mse_loss": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P],
     "dv_mse_loss_bwd": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
     "dv_sinusoidal": [_P, _P, _P, _I, _I, _P],
+    "dv_linear_group_fwd": [_P, _I, _I, _I, _P, _I, _P],
+    "dv_linear_group_bwd": [_P, _I, _I, _I, _P, _I, _P, _I, _P, _P],
     "dv_linear_small_fwd": [_P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
     "dv_linear_small_bwd": [_P, _I, _P, _I, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_adamw": [_P, _P, _P, _P, _L, _L, _F, _F, _F, _F, _F, _F, _F, _P, _P],

@@ -233,11 +233,12 @@ class CrossAttention(nn.Module):
         self.to_kv = nn.Linear(context_dim, inner * 2, bias=False)
         self.to_out = nn.Sequential(nn.Linear(inner, dim, bias=False), LayerNorm(dim))
 
-    def forward_cl(self, x, context, nb):
-        """Returns cross_attn(x, context) + x (the residual of ResnetBlock3D:197)."""
+    def forward_cl(self, x, context, nb, kv=None):
+        """Returns cross_attn(x, context) + x (the residual of ResnetBlock3D:197);
+        kv: this block's to_kv(context) when the Unet batched the projections."""
         return ops.cross_attention(x, context, self.norm.g, self.null_kv, self.to_q.weight,
                                    self.to_kv.weight, self.to_out[0].weight, self.to_out[1].g, nb,
-                                   _ln_eps(x.dtype))
+                                   _ln_eps(x.dtype), kv=kv)
 
 
 class UpsampleCombiner(nn.Module):
@@ -427,15 +428,16 @@ class ResnetBlock3D(nn.Module):
         self.block2 = Block3D(dim_out, dim_out, groups=groups, weight_standardization=weight_standardization)
         self.res_conv = nn.Conv3d(dim, dim_out, 1) if dim != dim_out else nn.Identity()
 
-    def forward_cl(self, x0, time_emb, cond, nb, x1=None):
-        ss = None
-        if exists(self.time_mlp) and exists(time_emb):
-            ss = ops.linear_small(time_emb, self.time_mlp[1].weight, self.time_mlp[1].bias,
-                                  act_in=ACT_SILU)
+    def forward_cl(self, x0, time_emb, cond, nb, x1=None, ss=None, kv=None):
+        """ss / kv: this block's time_mlp(time_emb) / to_kv(cond) when the Unet
+        computed them for all blocks in one grouped launch (ops.linear_group)."""
+        if ss is None and exists(self.time_mlp) and exists(time_emb):
+            ss = ops.linear_group(time_emb, [self.time_mlp[1].weight], [self.time_mlp[1].bias],
+                                  act_in=ACT_SILU)[0]
         h = self.block1.forward_cl(x0, nb, x1=x1, scale_shift=ss)
         if exists(self.cross_attn):
             assert exists(cond)
-            h = self.cross_attn.forward_cl(h, cond, nb)
+            h = self.cross_attn.forward_cl(h, cond, nb, kv=kv)
         if isinstance(self.res_conv, nn.Identity):
             if x1 is not None:
                 raise DVError("identity residual with a split input")
@@ -647,6 +649,37 @@ class Unet3D(nn.Module):
                                                                    self.cond_dim)
         return t, c, mid_c
 
+    def _resnet_blocks(self):
+        """(block, uses mid_c) for every ResnetBlock3D in forward order."""
+        out = []
+        for _, init_block, blocks, _, _ in self.downs:
+            out += [(init_block, False)] + [(b, False) for b in blocks]
+        out += [(self.mid_block1, True), (self.mid_block2, True)]
+        for init_block, blocks, _, _ in self.ups:
+            out += [(init_block, False)] + [(b, False) for b in blocks]
+        out.append((self.final_resnet_block, False))
+        return out
+
+    def _grouped_projections(self, t, c, mid_c):
+        """Every ResnetBlock3D's time_mlp(t) in ONE launch, and every cross-attention
+        to_kv(c) / to_kv(mid_c) in one launch per context (ops.linear_group):
+        {id(block): (scale_shift, kv)}.  Same arithmetic as the per-block
+        Linear layers (dalle2_video.py:182-185, 195-201)."""
+        blks = self._resnet_blocks()
+        timed = [b for b, _ in blks if exists(b.time_mlp)]
+        ss = ops.linear_group(t, [b.time_mlp[1].weight for b in timed],
+                              [b.time_mlp[1].bias for b in timed], act_in=ACT_SILU)
+        pre = {id(b): [s, None] for b, s in zip(timed, ss)}
+        for use_mid, ctx in ((False, c), (True, mid_c)):
+            xa = [b for b, m in blks if m == use_mid and exists(b.cross_attn)]
+            if not xa:
+                continue
+            kvs = ops.linear_group(ctx.reshape(-1, ctx.shape[-1]),
+                                   [b.cross_attn.to_kv.weight for b in xa], [None] * len(xa))
+            for b, kv in zip(xa, kvs):
+                pre.setdefault(id(b), [None, None])[1] = kv
+        return {k: tuple(v) for k, v in pre.items()}
+
     def forward_cl(self, x, time, *, batch, lowres_cl=None, video_cond_drop_prob=0.0,
                    text_cond_drop_prob=0.0):
         """Core denoiser on channels-last frames x (batch*T, H, W, C8); returns
@@ -655,25 +688,31 @@ class Unet3D(nn.Module):
         r = x
         t, c, mid_c = self._conditioning(time, batch, x.device, video_cond_drop_prob,
                                          text_cond_drop_prob)
+        pre = self._grouped_projections(t, c, mid_c)
+
+        def run(blk, x, cond, x1=None):
+            ss, kv = pre.get(id(blk), (None, None))
+            return blk.forward_cl(x, t, cond, batch, x1=x1, ss=ss, kv=kv)
+
         hiddens = []
         for _, init_block, blocks, attn, post in self.downs:
-            x = init_block.forward_cl(x, t, c, batch)
+            x = run(init_block, x, c)
             for blk in blocks:
-                x = blk.forward_cl(x, t, c, batch)
+                x = run(blk, x, c)
                 hiddens.append(x)
             hiddens.append(x)  # after the Identity attention
             x = post.forward_cl(x)
-        x = self.mid_block1.forward_cl(x, t, mid_c, batch)
+        x = run(self.mid_block1, x, mid_c)
         if exists(self.mid_attn):
             x = self.mid_attn.forward_cl(x, batch)
-        x = self.mid_block2.forward_cl(x, t, mid_c, batch)
+        x = run(self.mid_block2, x, mid_c)
         for init_block, blocks, attn, up in self.ups:
-            x = init_block.forward_cl(x, t, c, batch, x1=hiddens.pop())
+            x = run(init_block, x, c, x1=hiddens.pop())
             for blk in blocks:
-                x = blk.forward_cl(x, t, c, batch, x1=hiddens.pop())
+                x = run(blk, x, c, x1=hiddens.pop())
             if not isinstance(up, nn.Identity):
                 x = up.forward_cl(x)
-        x = self.final_resnet_block.forward_cl(x, t, None, batch, x1=r)
+        x = run(self.final_resnet_block, x, None, x1=r)
         return ops.conv(x, self.to_out.weight, self.to_out.bias, x1=lowres_cl)
 
     def forward(self, x, time, *, video_embed=None, lowres_cond_video=None,

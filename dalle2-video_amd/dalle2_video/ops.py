@@ -7,6 +7,8 @@ is no torch-compute fallback.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -20,9 +22,15 @@ class KernelTimer:
     def __init__(self):
         self.records = []  # (name, flops, bytes, start_event, end_event)
 
+    # a short device-side spin before each timed launch keeps the GPU behind the
+    # host, so the start event, the kernel and the end event run back to back and
+    # the elapsed time is the kernel's own (not host launch gaps)
+    SPIN_CYCLES = 400_000
+
     def run(self, name, flops, nbytes, fn):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(self.SPIN_CYCLES)
         s.record()
         fn()
         e.record()
@@ -65,7 +73,19 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld):
     return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"
 
 
-def conv_wgrad_name(dtype_name, m, cout, K, maxld):
+def conv_wgrad_name(dtype_name, m, cout, cin, c0, split, ks, h, w, maxld):
+    """Mirror of dv_conv_wgrad's kernel choice (wgrad_stripe_ok / conv_wgrad_glds)."""
+    if (dtype_name == "bf16" and ks == 3 and cin % 64 == 0 and cout % 64 == 0
+            and (not split or c0 % 64 == 0) and m % 128 == 0 and w in (8, 16, 32, 64)
+            and ((h * w >= 128 and h % (128 // w) == 0)
+                 or (h * w < 128 and 128 % (h * w) == 0
+                     and (128 // (h * w)) * (h + 2) * (w + 2) <= (200 if w == 8 else (128 // w + 2) * (w + 2))))):
+        return f"conv_wgrad_stripe_kernel<{w}>"
+    K = ks * ks * cin
+    return gemm_wgrad_name(dtype_name, m, cout, K, maxld)
+
+
+def gemm_wgrad_name(dtype_name, m, cout, K, maxld):
     """Mirror of conv_wgrad_t / conv_wgrad_glds's tile choice."""
     if dtype_name == "bf16" and m * maxld < (1 << 31) and cout * K < (1 << 31):
         if cout <= 64:
@@ -116,15 +136,20 @@ def _grad_out(p, zero=False):
 _WS = {}
 
 
-def _wgrad_workspace(cout, taps, cin, device):
-    """Cached packed wgrad workspace; dv_unpack_wgrad zeroes it after use."""
-    key = (cout, taps, cin, str(device))
-    if key not in _WS:
-        _WS[key] = torch.zeros(cout, taps, cin, dtype=torch.float32, device=device)
-    return _WS[key]
+def _wgrad_workspace(dname, nf, h, w, cin, c0, split, cout, ks, device):
+    """One cached f32 scratch per device for dv_conv_wgrad (grown on demand;
+    kernels on the stream use it one after another)."""
+    need = ctypes.c_longlong(0)
+    call("dv_conv_wgrad_ws", _lib.DV_BF16 if dname == "bf16" else _lib.DV_F32, nf, h, w, cin, c0,
+         int(split), cout, ks, ctypes.byref(need))
+    key = str(device)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < need.value:
+        buf = torch.empty(max(need.value, 1 << 20), dtype=torch.float32, device=device)
+        _WS[key] = buf
+    return buf
 
 
-_GN_WS = {}
 _XA_WS = {}
 
 
@@ -138,16 +163,44 @@ def _xattn_workspace(nb, C, device):
     return _XA_WS[key]
 
 
-def _gn_workspace(n, device):
-    """GroupNorm partial-sum workspace: zero on entry, left zeroed by the GN
-    kernels themselves (dv_gn_fwd / dv_gn_bwd contract), so it is allocated
-    once per device and never memset."""
+class _GnSums:
+    """The two alternating GroupNorm sums buffers of a device (dv_gn_fwd /
+    dv_gn_bwd contract): call i accumulates into buffer i % 2, which is zero on
+    entry, and zeroes buffer (i + 1) % 2 for call i + 1."""
+
+    CAP = 1 << 15  # floats per buffer (nb * C * 2 <= 32768)
+
+    def __init__(self, device):
+        self.bufs = torch.zeros(2, self.CAP, dtype=torch.float32, device=device)
+        self.i = 0
+
+    def take(self, n):
+        if n > self.CAP:
+            raise _lib.DVError(f"GroupNorm: nb*C*2 = {n} exceeds the sums buffer ({self.CAP})")
+        cur, nxt = self.bufs[self.i % 2], self.bufs[(self.i + 1) % 2]
+        self.i += 1
+        return cur, nxt
+
+    def reset(self):
+        """Zero both buffers (one launch): ends a captured graph region so a
+        replay starts from zero sums whatever the call-count parity."""
+        _lib.call("dv_zero_f32", ptr(self.bufs), self.bufs.numel(), stream())
+
+
+_GN_WS = {}
+
+
+def _gn_sums(device):
     key = str(device)
-    buf = _GN_WS.get(key)
-    if buf is None or buf.numel() < n:
-        buf = torch.zeros(max(n, 1 << 16), dtype=torch.float32, device=device)
-        _GN_WS[key] = buf
-    return buf
+    if key not in _GN_WS:
+        _GN_WS[key] = _GnSums(device)
+    return _GN_WS[key]
+
+
+def gn_graph_boundary(device):
+    """Call at the end of a captured region that runs GroupNorms."""
+    if str(device) in _GN_WS:
+        _GN_WS[str(device)].reset()
 
 
 def _pad_channels(t: torch.Tensor, mult: int = 8) -> torch.Tensor:
@@ -294,36 +347,46 @@ class ConvFn(torch.autograd.Function):
             dx0 = dx[..., :c0]
             dx1 = dx[..., c0:] if x1 is not None else None
         wparam, bparam = ctx.params
+        want_w = ctx.needs_input_grad[2]
         want_b = has_bias and ctx.needs_input_grad[3]
-        # bias gradient target: the parameter's .grad in place when possible
-        bslot = _grad_out(bparam, zero=True) if want_b else None
-        if want_b and (bslot is None or cout8 != cout):
-            db_buf = torch.zeros(cout8, dtype=torch.float32, device=dy.device)
-        else:
-            db_buf = bslot[0] if bslot else None
-        if ctx.needs_input_grad[2]:
-            taps = ksize * ksize
-            wslot = _grad_out(wparam, zero=True)
-            direct = wslot is not None and taps == 1 and cout8 == cout and cin_real == cin
-            ws = wslot[0] if direct else _wgrad_workspace(cout8, taps, cin, dy.device)
+        if want_w:
+            # weight (+ fused bias) gradient straight into the parameters' .grad
+            # (the trainer's flat buffer) when they are leaves; else returned
+            wslot = _grad_out(wparam)
+            bslot = _grad_out(bparam) if want_b else None
+            if wslot is not None:
+                dw_t, acc_w = wslot
+            else:
+                dw = dw_t = torch.empty(weight.shape, dtype=torch.float32, device=dy.device)
+                acc_w = False
+            if want_b:
+                if bslot is not None:
+                    db_t, acc_b = bslot
+                else:
+                    db = db_t = torch.empty(cout, dtype=torch.float32, device=dy.device)
+                    acc_b = False
+            else:
+                db_t, acc_b = None, False
             ld0 = cl_ld(x0)
             ld1 = cl_ld(x1) if x1 is not None else 0
             m = nf * h * w
-            _launch(conv_wgrad_name(_lib.dtype_name(dy8), m, cout8, cin * ksize * ksize, max(cout8, ld0, ld1)),
+            dname = _lib.dtype_name(dy8)
+            ws = _wgrad_workspace(_lib.dtype_name(dy8), nf, h, w, cin, c0, x1 is not None, cout8,
+                                  ksize, dy.device)
+            _launch(conv_wgrad_name(dname, m, cout8, cin, c0, x1 is not None, ksize, h, w,
+                                    max(cout8, ld0, ld1)),
                     2.0 * m * cout8 * cin * ksize * ksize,
                     dy8.element_size() * m * (cin + cout8),
                     lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), cout8, ptr(x0), ld0, c0, ptr(x1), ld1,
-                                 ptr(ws), ptr(db_buf), nf, h, w, cin, cout8, ksize, stream()))
-            if not direct:
-                if wslot is not None:
-                    call("dv_unpack_wgrad", ptr(ws), ptr(wslot[0]), cout8, cin, ksize, cout, cin_real,
-                         int(wslot[1]), stream())
-                else:
-                    dw = torch.empty(weight.shape, dtype=torch.float32, device=dy.device)
-                    call("dv_unpack_wgrad", ptr(ws), ptr(dw), cout8, cin, ksize, cout, cin_real, 0, stream())
+                                 ptr(dw_t), int(acc_w), ptr(db_t), int(acc_b), ptr(ws), ws.numel(),
+                                 nf, h, w, cin, cout8, cout, cin_real, ksize, stream()))
         elif want_b:
+            bslot = _grad_out(bparam, zero=True)
+            if bslot is None or cout8 != cout:
+                db_buf = torch.zeros(cout8, dtype=torch.float32, device=dy.device)
+            else:
+                db_buf = bslot[0]
             call("dv_bias_grad", dt(dy8), ptr(dy8), cout8, ptr(db_buf), nf * h * w, cout, stream())
-        if want_b:
             if bslot is None:
                 db = db_buf[:cout]
             elif db_buf is not bslot[0]:
@@ -352,12 +415,12 @@ class GroupNormActFn(torch.autograd.Function):
         y = torch.empty(nf, h, w, c, dtype=z.dtype, device=dev)
         mean = torch.empty(nb * groups, dtype=torch.float32, device=dev)
         rstd = torch.empty_like(mean)
-        ws = _gn_workspace(nb * c * 2, dev)
+        cur, nxt = _gn_sums(dev).take(nb * c * 2)
         g, b = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
         s = None if ss is None else ss.detach().float().contiguous()
         call("dv_gn_fwd", dt(z), ptr(z), cl_ld(z), ptr(y), c, ptr(res), cl_ld(res) if res is not None else 0,
              nb, P, c, groups, ctypes_float(eps), ptr(g), ptr(b), ptr(s), act, ptr(mean), ptr(rstd),
-             ptr(ws), stream())
+             ptr(cur), ptr(nxt), nxt.numel(), stream())
         ctx.save_for_backward(z, g, b, s, mean, rstd)
         ctx.params = (gamma, beta)
         ctx.meta = (nb, groups, act, ss is not None, res is not None)
@@ -381,10 +444,9 @@ class GroupNormActFn(torch.autograd.Function):
             db = torch.empty(c, dtype=torch.float32, device=dev)
             acc, ret = 0, True
         dss = torch.empty(nb, 2 * c, dtype=torch.float32, device=dev) if has_ss else None
-        ws = _gn_workspace(nb * c * 2, dev)
-        ws2 = torch.empty(nb * groups * 2, dtype=torch.float32, device=dev)
+        cur, nxt = _gn_sums(dev).take(nb * c * 2)
         call("dv_gn_bwd", dt(z), ptr(dy), c, ptr(z), cl_ld(z), ptr(dz), c, nb, P, c, groups, ptr(g),
-             ptr(b), ptr(s), act, ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(ws), ptr(ws2),
+             ptr(b), ptr(s), act, ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(cur), ptr(nxt), nxt.numel(),
              acc, stream())
         if not ret:
             dg = db = None
@@ -496,6 +558,92 @@ def linear_small(x, w, b=None, act_in=0, act_out=0):
     return LinearSmallFn.apply(x, w, b, act_in, act_out)
 
 
+class _LinEntry(ctypes.Structure):
+    """ctypes mirror of DvLinEntry (include/dv_hip.h)."""
+    _fields_ = [("w", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("y", ctypes.c_void_p),
+                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p), ("n", ctypes.c_int),
+                ("accumulate_w", ctypes.c_int)]
+
+
+_LG_WS = {}
+
+
+class LinearGroupFn(torch.autograd.Function):
+    """Many small nn.Linear layers over the same rows x (B, K), one launch each
+    way: y_e = act_in(x) W_e^T + b_e.  The time MLPs of every ResnetBlock3D
+    (dalle2_video.py:143-146, 182-185) share t; the CrossAttention to_kv
+    projections share the context c (or mid_c)."""
+
+    @staticmethod
+    def forward(ctx, x, act_in, n_lin, *params):
+        require_gpu(x, *[q for q in params if q is not None])
+        xc = x.detach().float().contiguous()
+        B, K = xc.shape
+        ws, bs = params[:n_lin], params[n_lin:]
+        ns = [w.shape[0] for w in ws]
+        y = torch.empty(B * sum(ns), dtype=torch.float32, device=x.device)
+        outs, off = [], 0
+        for n in ns:
+            outs.append(y[off:off + B * n].view(B, n))
+            off += B * n
+        wcs = [w.detach().float().contiguous() for w in ws]
+        bcs = [None if b is None else b.detach().float().contiguous() for b in bs]
+        ents = (_LinEntry * n_lin)(*[_LinEntry(w.data_ptr(), 0 if b is None else b.data_ptr(),
+                                               o.data_ptr(), 0, 0, w.shape[0], 0)
+                                     for w, b, o in zip(wcs, bcs, outs)])
+        call("dv_linear_group_fwd", ptr(xc), B, K, act_in, ctypes.cast(ents, ctypes.c_void_p), n_lin,
+             stream())
+        ctx.save_for_backward(xc, *wcs)
+        ctx.params = params
+        ctx.meta = (act_in, n_lin)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        xc, *wcs = ctx.saved_tensors
+        act_in, n_lin = ctx.meta
+        ws, bs = ctx.params[:n_lin], ctx.params[n_lin:]
+        B, K = xc.shape
+        dev = xc.device
+        key = (B * K, str(dev))
+        if key not in _LG_WS:
+            _LG_WS[key] = torch.zeros(B * K + 1, dtype=torch.float32, device=dev)
+        wsbuf = _LG_WS[key]
+        dx = torch.empty(B, K, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
+        ents, ret_w, ret_b, keep = [], [], [], []
+        for i, (w, b, wc, dy) in enumerate(zip(ws, bs, wcs, dys)):
+            dy = (torch.zeros(B, wc.shape[0], dtype=torch.float32, device=dev) if dy is None
+                  else dy.float().contiguous())
+            keep.append(dy)
+            want_w = ctx.needs_input_grad[3 + i]
+            want_b = b is not None and ctx.needs_input_grad[3 + n_lin + i]
+            sw = _grad_out(w) if want_w else None
+            sb = _grad_out(b) if want_b else None
+            acc = 0
+            if sw is not None and (not want_b or (sb is not None and sb[1] == sw[1])):
+                dw, db, acc = sw[0], (sb[0] if sb else None), int(sw[1])
+                ret_w.append(None)
+                ret_b.append(None)
+            else:
+                dw = torch.empty_like(wc) if want_w else None
+                db = torch.empty(wc.shape[0], dtype=torch.float32, device=dev) if want_b else None
+                ret_w.append(dw)
+                ret_b.append(db)
+            ents.append(_LinEntry(wc.data_ptr(), 0, dy.data_ptr(), 0 if dw is None else dw.data_ptr(),
+                                  0 if db is None else db.data_ptr(), wc.shape[0], acc))
+        arr = (_LinEntry * n_lin)(*ents)
+        call("dv_linear_group_bwd", ptr(xc), B, K, act_in, ctypes.cast(arr, ctypes.c_void_p), n_lin,
+             ptr(dx), 0, ptr(wsbuf), stream())
+        return (dx, None, None, *ret_w, *ret_b)
+
+
+def linear_group(x, weights, biases, act_in=0):
+    """[act_in(x) @ W_e^T + b_e for each e] in one launch (x: (B, K) f32)."""
+    if len(weights) == 0:
+        return []
+    return list(LinearGroupFn.apply(x, act_in, len(weights), *weights, *biases))
+
+
 _FREQS = {}
 
 
@@ -530,17 +678,13 @@ class CrossAttnFn(torch.autograd.Function):
     """out = CrossAttention(x, context) + x, folded per batch element (dv_xattn.hip)."""
 
     @staticmethod
-    def forward(ctx, x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps):
-        require_gpu(x, context)
+    def forward(ctx, x, kv_in, g1, null_kv, wq, wo, g2, nb, eps):
+        require_gpu(x, kv_in)
         nf, h, w, C = x.shape
         ntok = nf * h * w
         P = ntok // nb
         dev, dtype = x.device, x.dtype
-        ctxf = context.detach().float().contiguous().reshape(-1, context.shape[-1])
-        kv = torch.empty(ctxf.shape[0], 2 * XA_HEADS * XA_DH, dtype=torch.float32, device=dev)
-        wkvf = wkv.detach().float().contiguous()
-        call("dv_linear_small_fwd", ptr(ctxf), ctxf.shape[1], ptr(wkvf), None, ptr(kv), kv.shape[1],
-             None, ctxf.shape[0], ctxf.shape[1], kv.shape[1], 0, 0, stream())
+        kv = kv_in.detach().float().contiguous()  # (nb * tokens, 2 * 512): to_kv(context)
         wqf, wof = wq.detach().float().contiguous(), wo.detach().float().contiguous()
         nkv = null_kv.detach().float().contiguous()
         g1f, g2f = g1.detach().float().contiguous(), g2.detach().float().contiguous()
@@ -560,18 +704,18 @@ class CrossAttnFn(torch.autograd.Function):
         pbuf = torch.empty(ntok, 32, dtype=dtype, device=dev)
         call("dv_xattn_fwd", dt(x), ptr(x), cl_ld(x), ptr(out), C, ntok, P, C, ptr(Kt), ptr(Vt),
              ptr(colsum), ptr(g2f), ctypes_float(eps), ptr(stats), ptr(pbuf), stream())
-        ctx.save_for_backward(x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, KtT, Vt, VtT,
+        ctx.save_for_backward(x, g1f, g2f, nkv, wqf, wof, kv, at, vt, KtT, Vt, VtT,
                               colsum, stats, pbuf)
-        ctx.params = (g1, null_kv, wq, wkv, wo, g2)
-        ctx.meta = (nb, eps, context.shape)
+        ctx.params = (g1, null_kv, wq, wo, g2)
+        ctx.meta = (nb, eps)
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        (x, ctxf, g1f, g2f, nkv, wqf, wkvf, wof, kv, at, vt, KtT, Vt, VtT, colsum, stats,
+        (x, g1f, g2f, nkv, wqf, wof, kv, at, vt, KtT, Vt, VtT, colsum, stats,
          pbuf) = ctx.saved_tensors
-        g1p, nullp, wqp, wkvp, wop, g2p = ctx.params
-        nb, eps, cshape = ctx.meta
+        g1p, nullp, wqp, wop, g2p = ctx.params
+        nb, eps = ctx.meta
         nf, h, w, C = x.shape
         ntok = nf * h * w
         P = ntok // nb
@@ -588,7 +732,7 @@ class CrossAttnFn(torch.autograd.Function):
              ptr(dsbuf), ptr(p2buf), stream())
         # per-batch token reductions: R = dS'^T X, V' = P^T dO, Q = P'^T dY (one batched GEMM each)
         for a_, b_, ldb, o_ in ((dsbuf, x, ldx, wsR), (pbuf, dobuf, C, wsV), (p2buf, dy, C, wsQ)):
-            _launch("gemm_tn_batched:" + conv_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldb)),
+            _launch(gemm_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldb)),
                     2.0 * ntok * 32 * C, 0,
                     lambda a_=a_, b_=b_, ldb=ldb, o_=o_: call(
                         "dv_gemm_tn_batched", dt(x), ptr(a_), 32, ptr(b_), ldb, ptr(o_), P, nb, 32, C,
@@ -611,14 +755,8 @@ class CrossAttnFn(torch.autograd.Function):
         call("dv_xattn_fold_bwd", ptr(wsR), ptr(wsV), ptr(wsQ), ptr(mcorr), ptr(at), ptr(vt), ptr(g1f),
              ptr(wqf), ptr(wof), ptr(kv), ptr(nkv), ptr(dat), ptr(dvt), ptr(dg1), ptr(dg2), ptr(dwq),
              ptr(dwo), ptr(dkv), ptr(dnull), nb, C, ctypes_float(XA_DH ** -0.5), acc_g, acc_w, stream())
-        dctx = torch.empty_like(ctxf)
-        sk = _grad_out(wkvp)
-        dwkv = sk[0] if sk else torch.empty_like(wkvf)
-        call("dv_linear_small_bwd", ptr(dkv), dkv.shape[1], ptr(ctxf), ctxf.shape[1], ptr(wkvf), None,
-             ptr(dctx), ctxf.shape[1], ptr(dwkv), None, ctxf.shape[0], ctxf.shape[1], dkv.shape[1],
-             0, 0, 0, int(sk[1]) if sk else 0, stream())
-        return (dx, dctx.reshape(cshape), dg1 if ret_g else None, None if direct else dnull,
-                None if direct else dwq, None if sk else dwkv, None if direct else dwo,
+        return (dx, dkv, dg1 if ret_g else None, None if direct else dnull,
+                None if direct else dwq, None if direct else dwo,
                 dg2 if ret_g else None, None, None)
 
 
@@ -627,8 +765,12 @@ def ctypes_vp(addr):
     return ctypes.c_void_p(addr)
 
 
-def cross_attention(x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps):
-    return CrossAttnFn.apply(x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps)
+def cross_attention(x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps, kv=None):
+    """kv: to_kv(context) rows when the caller batched the projection
+    (linear_group over every block sharing the context); else computed here."""
+    if kv is None:
+        kv = linear_group(context.float().reshape(-1, context.shape[-1]), [wkv], [None])[0]
+    return CrossAttnFn.apply(x, kv, g1, null_kv, wq, wo, g2, nb, eps)
 
 
 # ---------------------------------------------------------------------------

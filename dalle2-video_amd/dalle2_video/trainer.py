@@ -26,7 +26,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from . import _lib
+from . import _lib, ops
 from ._lib import call, ptr, stream
 from .dalle2_video import VideoDecoder, cast_tuple, default, exists
 from .ops import ctypes_float
@@ -399,6 +399,9 @@ class VideoDecoderTrainer(nn.Module):
                 with ctx:
                     loss = self.decoder(*sargs, unet_number=unet_number, **skw)
                 loss.backward()
+                # replays start from zeroed GroupNorm sums whatever the parity
+                # of the GroupNorm calls inside the graph (ops._GnSums)
+                ops.gn_graph_boundary(loss.device)
             ent.update(graph=g, args=sargs, kwargs=skw, loss=loss.detach())
         for dst, src in zip(ent["args"], args):
             if torch.is_tensor(dst):

@@ -34,6 +34,9 @@ enum { DV_ACT_NONE = 0, DV_ACT_SILU = 1, DV_ACT_GELU = 2 };
 
 const char* dv_last_error(void);
 int dv_abi_version(void);
+/* Zero n floats on the stream with a kernel (graph-capture safe: a kernel
+ * node, not a memset node).  Used to reset cached workspaces.               */
+int dv_zero_f32(float* p, long long n, void* stream);
 
 /* ---- convolutions (1,k,k), stride 1, padding k//2 -------------------------
  * Replaces nn.Conv3d in Block3D.project (dalle2_video.py:107), res_conv
@@ -50,19 +53,20 @@ int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const void* x1, int 
                 void* y, int ldy, int nf, int h, int w, int cin, int cout, int ksize,
                 int act, void* stream);
 
-/* ws[co][tap][ci] += sum_pixels dY[p][co] * X[p + tap][ci]: f32 atomics into a
- * zeroed packed workspace (cout*k*k*cin floats; for k=1 this IS the torch
- * layout, so ws may be the parameter's gradient); split-K over pixels.
- * db (optional): db[co] += sum_p dY[p][co] — the conv bias gradient, fused.
- * cin, cout multiples of 8 (pad and mask with dv_unpack_wgrad).            */
+/* Weight (and fused bias) gradient of dv_conv_fwd, written in torch layout:
+ * dw (cout_real, cin_real, 1, k, k) (+)= sum_p dY[p][co] X[p + tap][ci]
+ * (accumulate_w), db[cout_real] (+)= sum_p dY[p][co] (accumulate_b; db may
+ * be NULL).  cout / cin are the padded sizes of dy's channels / x's channels.
+ * ws: caller-owned f32 scratch of at least dv_conv_wgrad_ws() floats (no
+ * zeroing required).  bf16 3x3 / 1x1 convolutions with cin, cout % 64 == 0
+ * run the row-window kernel (split over pixels, plain-store partials summed
+ * by a second launch); other shapes run f32-atomic split-K over pixels.     */
+int dv_conv_wgrad_ws(int dtype, int nf, int h, int w, int cin, int c0, int split, int cout,
+                     int ksize, long long* floats);
 int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0, int c0,
-                  const void* x1, int ld1, float* ws, float* db, int nf, int h, int w, int cin,
-                  int cout, int ksize, void* stream);
-
-/* dw (torch layout (cout_real, cin_real, 1, k, k)) (+)= ws[co][tap][ci]; zeroes
- * ws behind itself so a cached workspace needs no memset before reuse.       */
-int dv_unpack_wgrad(float* ws, float* dw, int cout, int cin, int ksize, int cout_real,
-                    int cin_real, int accumulate, void* stream);
+                  const void* x1, int ld1, float* dw, int accumulate_w, float* db,
+                  int accumulate_b, float* ws, long long ws_floats, int nf, int h, int w,
+                  int cin, int cout, int cout_real, int cin_real, int ksize, void* stream);
 
 /* db[c] += sum_p dy[p][c]  (f32 atomics) */
 int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix, int c,
@@ -85,6 +89,31 @@ typedef struct {
 int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, long long max_elems,
                                  void* stream);
 
+/* ---- grouped small linears ------------------------------------------------
+ * Many nn.Linear layers over the SAME f32 input rows x [B][K] in ONE launch:
+ * y_e [B][n_e] = act_in(x) W_e^T (+ bias_e) for every entry e.  Serves the
+ * time_mlp of every ResnetBlock3D (SiLU -> Linear(time_cond_dim, 2*dim_out),
+ * dalle2_video.py:143-146, applied at :182-185 — all 27 blocks of unet1 take
+ * the same time embedding t) and the to_kv projections of CrossAttention over
+ * the shared context c / mid_c (dalle2-pytorch CrossAttention, called at
+ * :195-201).  B <= 8, K <= 512, K % 4 == 0, act_in: DV_ACT_*; W_e f32
+ * [n_e][K] row-major; more than 48 entries are split into several launches. */
+typedef struct DvLinEntry {
+  const float* w;     /* [n][K] */
+  const float* bias;  /* [n] or NULL */
+  float* y;           /* forward: output [B][n]; backward: dy [B][n] */
+  float* dw;          /* backward: [n][K] (+)= gradient, or NULL */
+  float* db;          /* backward: [n] (+)= gradient, or NULL */
+  int n;
+  int accumulate_w;   /* backward: 1 adds into dw/db, 0 overwrites */
+} DvLinEntry;
+int dv_linear_group_fwd(const float* x, int B, int K, int act_in, const DvLinEntry* entries,
+                        int n_entries, void* stream);
+/* dx [B][K] (+)= act_in'(x) * sum_e dy_e W_e (accumulate_dx), dw/db per entry.
+ * ws: B*K + 1 floats, ZERO on entry and left zeroed.                          */
+int dv_linear_group_bwd(const float* x, int B, int K, int act_in, const DvLinEntry* entries,
+                        int n_entries, float* dx, int accumulate_dx, float* ws, void* stream);
+
 /* Batched TN GEMM on the wgrad engine: out[g][i][j] += sum_{r in group g}
  * A[r][i]*B[r][j]; A rows x m (lda), B rows x n (ldb), nbatch groups of
  * batch_rows consecutive rows; out f32 [nbatch][m][n] (atomics, pre-zeroed).
@@ -97,20 +126,24 @@ int dv_gemm_tn_batched(int dtype, const void* a, int lda, const void* b, int ldb
  * 183-189): y = act(GN(z)*gamma + beta) (optionally *(ss_scale+1)+ss_shift,
  * ss = [nb][2C] f32 with scale first), + res.  nb batch elements of P pixels
  * (all frames of one clip form one GroupNorm sample), C channels, G groups.
- * mean/rstd [nb][G] f32 are saved for the backward.  ws: nb*C*2 floats
- * that must be ZERO on entry; both calls leave them zeroed again, so a
- * cached workspace needs no memset.  ws2 (backward): nb*G*2 floats scratch.
- * C % 8 == 0, C <= 256 vectors of 16 B.  act: DV_ACT_*.                     */
+ * mean/rstd [nb][G] f32 are written for the backward.  Two launches per
+ * call (reduce, apply).  sums: nb*C*2 floats that must be ZERO on entry; the
+ * call does NOT re-zero them (its apply still reads them) but zeroes `next`
+ * (next_n floats, may be NULL): the buffer the caller's NEXT GroupNorm call
+ * (forward or backward) will pass as `sums`.  Alternating two buffers keeps
+ * both zero on entry without any memset launch.
+ * C % (16 B) == 0, C <= 256 vectors, G <= 64.  act: DV_ACT_*.               */
 int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* res, int ldres,
               int nb, long long P, int C, int G, float eps, const float* gamma,
-              const float* beta, const float* ss, int act, float* mean, float* rstd, float* ws,
-              void* stream);
+              const float* beta, const float* ss, int act, float* mean, float* rstd, float* sums,
+              float* next, long long next_n, void* stream);
 /* dz from dy (z is the pre-norm input); dgamma/dbeta [C] and dss [nb][2C]
- * (+)= their gradients (accumulate != 0 adds).                               */
+ * (+)= their gradients (accumulate != 0 adds).  sums/next as dv_gn_fwd.      */
 int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void* dz, int lddz,
               int nb, long long P, int C, int G, const float* gamma, const float* beta,
               const float* ss, int act, const float* mean, const float* rstd, float* dgamma,
-              float* dbeta, float* dss, float* ws, float* ws2, int accumulate, void* stream);
+              float* dbeta, float* dss, float* sums, float* next, long long next_n,
+              int accumulate, void* stream);
 
 /* ---- row LayerNorm over channels (dalle2-pytorch LayerNorm, gain only, eps
  * 1e-5 fp32; the mid-attention pre/post norms, dalle2_video.py:431, 551,

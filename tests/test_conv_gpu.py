@@ -19,6 +19,11 @@ CASES = [
     (32, 64, 64, 64, 0, 64, 3),     # glds path: 256x64 tile (M >= 512 tiles)
     (2, 7, 5, 256, 0, 64, 3),       # wgrad 64x256 tile (K = 2304)
     (3, 4, 6, 24, 16, 32, 3),       # cout 32 < one 64-channel A tile, dual source
+    # row-window wgrad (bf16, cin/cout % 64 == 0, W | 64): every window width
+    (4, 32, 32, 64, 64, 64, 3),     # W=32, dual source (up-path skip concat)
+    (2, 8, 8, 512, 256, 512, 3),    # W=8, 12 channel chunks x 3 tap rows, one split
+    (8, 16, 16, 256, 0, 64, 1),     # 1x1 (Downsample3D-like), many splits
+    (16, 8, 8, 64, 0, 128, 3),      # W=8, 2 cout tiles
 ]
 
 

@@ -34,12 +34,15 @@ def _leaf(t, dev=None, dtype=None):
 
 
 @pytest.mark.parametrize("dtype,tol", DTYPES)
-@pytest.mark.parametrize("with_ss,with_res", [(True, False), (False, True)])
-def test_group_norm_act(dtype, tol, with_ss, with_res):
+@pytest.mark.parametrize("with_ss,with_res,nb,C", [(True, False, 2, 64), (False, True, 2, 64),
+                                                   (True, False, 4, 512), (True, True, 3, 1024)])
+def test_group_norm_act(dtype, tol, with_ss, with_res, nb, C):
+    """GroupNorm (+FiLM, SiLU, residual): the reduce's last workgroup finishes the
+    statistics / parameter gradients in sample chunks (C=512, 1024 take several)."""
     from dalle2_video import ops
 
     g = torch.Generator().manual_seed(3)
-    nb, T, H, W, C, G = 2, 3, 8, 8, 64, 8
+    T, H, W, G = 3, 8, 8, 8
     z = torch.randn(nb * T, H, W, C, generator=g) * 2 + 0.5
     gamma = 1 + 0.1 * torch.randn(C, generator=g)
     beta = 0.1 * torch.randn(C, generator=g)
@@ -263,3 +266,33 @@ def test_linear_small():
     f = torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1)))
     a = t.float()[:, None] * f[None]
     assert rel(emb, torch.cat((a.sin(), a.cos()), -1)) < 2e-7
+
+
+@pytest.mark.parametrize("act_in,ns,K", [(1, (128, 1024, 70, 512), 256), (0, (1024,) * 3, 64),
+                                         (1, tuple(64 + 8 * i for i in range(50)), 32)])
+def test_linear_group(act_in, ns, K):
+    """Grouped small linears (time MLPs / to_kv): every entry's output and the
+    dx / dW / db gradients vs per-layer fp32 torch; 50 entries span 2 launches."""
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(23)
+    B = 4 if K != 64 else 8
+    x = torch.randn(B, K, generator=g)
+    ws = [torch.randn(n, K, generator=g) / 8 for n in ns]
+    bs = [torch.randn(n, generator=g) if (act_in or i % 2) else None for i, n in enumerate(ns)]
+    gys = [torch.randn(B, n, generator=g) for n in ns]
+    xr = _leaf(x)
+    wr = [_leaf(w) for w in ws]
+    br = [None if b is None else _leaf(b) for b in bs]
+    xi = F.silu(xr) if act_in == 1 else xr
+    yr = [xi @ w.t() + (0 if b is None else b) for w, b in zip(wr, br)]
+    sum((y * gy).sum() for y, gy in zip(yr, gys)).backward()
+    xd = _leaf(x, "cuda")
+    wd = [_leaf(w, "cuda") for w in ws]
+    bd = [None if b is None else _leaf(b, "cuda") for b in bs]
+    yd = ops.linear_group(xd, wd, bd, act_in=act_in)
+    for a, b in zip(yd, yr):
+        assert rel(a, b) < 2e-6
+    sum((y * gy.cuda()).sum() for y, gy in zip(yd, gys)).backward()
+    grads_match([xd.grad] + [w.grad for w in wd] + [b.grad for b in bd if b is not None],
+                [xr.grad] + [w.grad for w in wr] + [b.grad for b in br if b is not None], 2e-6)

@@ -36,10 +36,12 @@ def conv_case(nf, h, w, cin, cout, k, dtype=torch.bfloat16):
              cout, nf, h, w, cin, cout, k, 0, stream())
     ms = timeit(fwd)
     dy = torch.randn_like(y)
-    ws = torch.zeros(cout, k * k, cin, device="cuda")
+    ws = ops._wgrad_workspace(ops._lib.dtype_name(x), nf, h, w, cin, cin, False, cout, k, x.device)
+    dw = torch.empty(cout, cin, 1, k, k, device="cuda")
+    db = torch.empty(cout, device="cuda")
     def wgrad():
-        call("dv_conv_wgrad", dt(x), ptr(dy), cout, ptr(x), cin, cin, None, 0, ptr(ws), None, nf, h, w,
-             cin, cout, k, stream())
+        call("dv_conv_wgrad", dt(x), ptr(dy), cout, ptr(x), cin, cin, None, 0, ptr(dw), 0, ptr(db), 0,
+             ptr(ws), ws.numel(), nf, h, w, cin, cout, cout, cin, k, stream())
     msw = timeit(wgrad)
     print(f"conv nf={nf} {h}x{w} {cin}->{cout} k={k} {str(dtype)[6:]}: fwd {ms*1e3:8.1f} us "
           f"{flops/ms/1e9:7.1f} TF/s | wgrad {msw*1e3:8.1f} us {flops/msw/1e9:7.1f} TF/s")
