@@ -940,6 +940,134 @@ int launch_fwd_glds(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   return check_launch("conv_fwd_glds");
 }
 
+
+// ---------------------------------------------------------------------------
+// bf16 3x3 forward / dgrad, stripe form (cin == 64 single source, cout % 64
+// == 0, W in {32, 64}): one workgroup = 64 output channels over a contiguous
+// range of 128-pixel stages.  The packed weights of its 64 channels
+// (64 x 576 bf16) stay RESIDENT in LDS for the whole range; per stage only
+// the X window (128 / W + 2 image rows of W + 2 pixels, halo zero-filled) is
+// staged — once for all nine taps, which read it at row offsets
+// dy*(W+2) + dx.  So a stage costs ~38 KB of L2 traffic for 288 MFMAs,
+// against 9 x (pixel tile + weight tile) re-reads in the implicit-GEMM form.
+// LDS rows are padded to 144 B (window) / 1168 B (weights): 16 consecutive
+// rows then start 9 x 16 B apart (mod 256 B), so ds_read_b128 is
+// conflict-free with NO swizzle and every tap / k-step offset is an
+// immediate.  Register-staged window (loads for stage s+1 in flight during
+// the MFMAs of stage s), double-buffered.  8 waves: 4 pixel tiles x 2
+// channel halves, 32 x 32 accumulator each; epilogue = conv_epilogue.
+// ---------------------------------------------------------------------------
+constexpr int FS_WP = 1168;  // weight row pitch (576 bf16 + 16 B)
+constexpr int FS_XP = 144;   // window pixel pitch (64 bf16 + 16 B)
+
+template <int W>
+__global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> p, int nstages,
+                                                              int stages_per_block) {
+  constexpr int WP = W + 2, SEG = 128 / W, NWIN = (SEG + 2) * WP;
+  constexpr int NR = (NWIN * 8 + 511) / 512;  // 16-B window chunks per thread per stage
+  constexpr int WBUF = NWIN * FS_XP;
+  __shared__ __attribute__((aligned(16))) char smem[64 * FS_WP + 2 * WBUF];
+  char* sW = smem;
+  char* sX = smem + 64 * FS_WP;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pt = wave & 3, ch = wave >> 2;
+  const int co0 = blockIdx.y * 64;
+  const int sbeg = blockIdx.x * stages_per_block;
+  const int send = min(sbeg + stages_per_block, nstages);
+  const int HW = p.H * W;
+
+  // resident weights: 64 rows x 72 chunks of 16 B
+  for (int idx = tid; idx < 64 * 72; idx += 512) {
+    const int row = idx / 72, c = idx - row * 72;
+    *(u32x4*)(sW + row * FS_WP + c * 16) = *(const u32x4*)(p.w + (long long)(co0 + row) * 576 + c * 8);
+  }
+
+  // this thread's window chunks: pixel (idx >> 3) of the window, chunk idx & 7
+  int w_off[NR], w_ry[NR];  // source pixel offset from the stage base; image-row offset (or invalid)
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int idx = tid + 512 * i, px = idx >> 3;
+    const int wy = px / WP, wx = px - wy * WP;
+    const bool ok = px < NWIN && wx >= 1 && wx <= W;
+    w_ry[i] = ok ? wy - 1 : -(1 << 20);
+    w_off[i] = (wy - 1) * W + (wx - 1);
+  }
+  const int cidx = tid & 7;
+  u32x4 stg[NR];
+  auto load = [&](int st) {
+    const int m0 = (sbeg + st) * 128;
+    const int y0 = (m0 % HW) / W;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const bool in = (unsigned)(y0 + w_ry[i]) < (unsigned)p.H;
+      stg[i] = in ? *(const u32x4*)(p.x0 + (long long)(m0 + w_off[i]) * p.ld0 + cidx * 8)
+                  : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int idx = tid + 512 * i;
+      if ((idx >> 3) < NWIN) *(u32x4*)(sX + buf * WBUF + (idx >> 3) * FS_XP + cidx * 16) = stg[i];
+    }
+  };
+
+  const int r = lane & 31, h = lane >> 5;
+  // lane's pixel in its tile and its window row (tap (0,0) = top-left)
+  const int px = pt * 32 + r;
+  const int wrow = (px / W) * WP + (px % W);
+  const char* aW = sW + (ch * 32 + r) * FS_WP + h * 16;
+  const int bofs = wrow * FS_XP + h * 16;
+
+  const int nst = send - sbeg;
+  if (nst > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) load(st + 1);
+    const char* bX = sX + (st & 1) * WBUF + bofs;
+    f32x16 acc[1][1];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[0][0][e] = 0.f;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      const int toff = ((d / 3) * WP + (d % 3)) * FS_XP;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const u32x4 a = *(const u32x4*)(aW + (d * 64 + ks * 16) * 2);
+        const u32x4 b = *(const u32x4*)(bX + toff + ks * 32);
+        acc[0][0] = Mma<bf16>::run(a, b, acc[0][0]);
+      }
+    }
+    conv_epilogue<bf16, 1, 1>(p, acc, (long long)(sbeg + st) * 128 + pt * 32, co0 + ch * 32, r, h);
+    if (st + 1 < nst) store((st + 1) & 1);
+    __syncthreads();
+  }
+}
+
+bool fwd_stripe_ok(long long M, int h, int w, int cin, bool split, int cout, int ks, int ld0) {
+  return ks == 3 && cin == 64 && !split && cout % 64 == 0 && (w == 32 || w == 64) &&
+         h % (128 / w) == 0 && M % 128 == 0 && ld0 % 8 == 0 && M * ld0 < (1ll << 31);
+}
+
+int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
+  const int nstages = (int)(a.M / 128);
+  const int ct = a.cout / 64;
+  int bx = 256 / ct;
+  if (bx < 1) bx = 1;
+  if (bx > nstages) bx = nstages;
+  const int sps = (nstages + bx - 1) / bx;
+  bx = (nstages + sps - 1) / sps;
+  dim3 grid(bx, ct);
+  if (a.W == 64) conv_fwd_stripe_kernel<64><<<grid, 512, 0, st>>>(a, nstages, sps);
+  else conv_fwd_stripe_kernel<32><<<grid, 512, 0, st>>>(a, nstages, sps);
+  return check_launch("conv_fwd_stripe");
+}
+
 // tile choice for the glds path (mirrored by ops.conv_tile for kernel naming)
 inline void glds_tile(long long M, int cout, int& bm, int& bn) {
   bn = cout <= 64 ? 64 : 128;
@@ -960,6 +1088,7 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
   a.ks = ks; a.act = act; a.M = (long long)nf * h * wd; a.K = ks * ks * cin;
   if (a.M == 0 || cout == 0) return DV_OK;
   if constexpr (sizeof(T) == 2) {
+    if (fwd_stripe_ok(a.M, h, wd, cin, x1 != nullptr, cout, ks, ld0)) return launch_fwd_stripe(a, st);
     const long long maxld = ld0 > (x1 ? ld1 : 0) ? ld0 : ld1;
     if (cin % 64 == 0 && a.c0 % 64 == 0 && a.M * maxld < (1ll << 31)) {
       int bm, bn;
@@ -1054,8 +1183,11 @@ struct WgradSArgs {
   const bf16* x0;
   const bf16* x1;
   int ld0, ld1, c0;
-  float* part;    // [S][cout][K]
+  float* part;    // [S][cout][cin][9] partials (S > 1)
   float* dbpart;  // [S][cout] or null
+  float* dw;      // (cout, cin, 1, 3, 3) gradient (S == 1)
+  float* db;      // [cout] or null
+  int acc_w, acc_b;
   int H, cin, cout, K;
   int nstages, stages_per_split;
   int seg, nseg;  // image rows per window segment, segments per stage
@@ -1143,7 +1275,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   // bias gradient on the VALU: a lane's A fragment holds 8 pixels of ONE
   // output channel (row lane % 32 of the 32x32x16 A operand)
   float accb = 0.f;
-  const bool do_bias = a.dbpart != nullptr && blockIdx.y == 0 && wn == 0;  // wave-uniform
+  const bool do_bias = a.db != nullptr && blockIdx.y == 0 && wn == 0;  // wave-uniform
 
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   const int colb = 32 * (g & 1) + 8 * pp;  // byte column of this lane in a 64-B half row
@@ -1205,10 +1337,8 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   }
   accb += __shfl_xor(accb, 32, 64);  // both k-halves of the channel
 
-  // ---- sum the two pixel halves through LDS (two passes), plain stores ----
+  // ---- sum the two pixel halves through LDS (two passes over the taps) ----
   float* red = (float*)smem;
-  const int r = lane & 31, h = lane >> 5;
-  float* pz = a.part + (long long)blockIdx.z * a.cout * a.K;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     constexpr int PER = (5 * 16 + 1) * 64;  // <= 5 taps + the bias sums per wave
@@ -1223,20 +1353,94 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
     __syncthreads();
     if (half == 0) {
 #pragma unroll
-      for (int d = d0; d < d1; ++d) {
-        const int col = d * a.cin + ci0 + wn * 32 + r;
+      for (int d = d0; d < d1; ++d)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int co = co0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          pz[(long long)co * a.K + col] = acc[d][e] + red[wq * PER + ((d - d0) * 16 + e) * 64 + lane];
-        }
-      }
-      if (pass == 0 && do_bias && lane < 32)
-        a.dbpart[(long long)blockIdx.z * a.cout + co0 + wm * 32 + lane] =
-            accb + red[wq * PER + 5 * 16 * 64 + lane];
+        for (int e = 0; e < 16; ++e) acc[d][e] += red[wq * PER + ((d - d0) * 16 + e) * 64 + lane];
+      if (pass == 0) accb += red[wq * PER + 5 * 16 * 64 + lane];
     }
     __syncthreads();
   }
+  // ---- torch-layout output [co][ci][tap]: each wave's 32 x 32 x 9 tile is
+  // transposed through LDS (two waves at a time, 36 KB each) so every output
+  // channel's 32 ci x 9 taps go out as 1152 contiguous bytes (float4 stores).
+  // One split writes the gradient itself (accumulate honoured); several
+  // splits write partials that wgrad_reduce4_kernel sums. ----
+  const bool direct = gridDim.z == 1;
+  float* dst = direct ? a.dw : a.part + (long long)blockIdx.z * a.cout * a.K;
+  const int acc_o = direct && a.acc_w;
+  const int r = lane & 31, h = lane >> 5;
+  constexpr int TP = 32 * 9;  // floats per output channel in a tile
+#pragma unroll
+  for (int rnd = 0; rnd < 2; ++rnd) {
+    float* tile = red + wn * (32 * TP);
+    if (half == 0 && wm == rnd) {
+#pragma unroll
+      for (int d = 0; d < 9; ++d)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int col = (e & 3) + 8 * (e >> 2) + 4 * h;  // local co
+          tile[col * TP + r * 9 + d] = acc[d][e];
+        }
+    }
+    __syncthreads();
+    if (half == 0 && wm == rnd) {
+      const long long rowbase = (long long)(co0 + wm * 32) * a.K + (ci0 + wn * 32) * 9;
+      for (int idx = lane; idx < 32 * (TP / 4); idx += 64) {
+        const int col = idx / (TP / 4), j = idx - col * (TP / 4);
+        f32x4 v = *(const f32x4*)(tile + col * TP + 4 * j);
+        f32x4* o = (f32x4*)(dst + rowbase + (long long)col * a.K + 4 * j);
+        if (acc_o) v += *o;
+        *o = v;
+      }
+    }
+    __syncthreads();
+  }
+  if (do_bias && half == 0 && lane < 32) {
+    const int co = co0 + wm * 32 + lane;
+    if (direct) a.db[co] = a.acc_b ? a.db[co] + accb : accb;
+    else a.dbpart[(long long)blockIdx.z * a.cout + co] = accb;
+  }
+}
+
+// dw (+)= sum_s part[s] over float4s (partials already in torch layout).
+// A workgroup = (256 / G) float4 columns x G split groups (G <= 8, a power
+// of two <= S): every lane keeps 8 loads in flight and the groups meet in
+// LDS, so even a 256-split sum of a small gradient spreads over hundreds of
+// workgroups.  The bias partials ([S][cout], cout % 4 == 0) are reduced the
+// same way by the workgroups after the weight ones.
+__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* part, int S, int G,
+                                                            long long n4, float* dw, int acc_w,
+                                                            const float* dbpart, float* db,
+                                                            int cout, int acc_b) {
+  __shared__ f32x4 sh[256];
+  const int cols = 256 / G;
+  const long long wblocks = (n4 + cols - 1) / cols;
+  const bool bias = blockIdx.x >= wblocks;
+  const long long n = bias ? cout / 4 : n4;
+  const f32x4* src = (const f32x4*)(bias ? dbpart : part);
+  float* dst = bias ? db : dw;
+  const int acc = bias ? acc_b : acc_w;
+  const int c = threadIdx.x % cols, grp = threadIdx.x / cols;
+  const long long i = (bias ? blockIdx.x - wblocks : blockIdx.x) * (long long)cols + c;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (i < n) {
+    const f32x4* p = src + i;
+    int s = grp;
+    for (; s + 7 * G < S; s += 8 * G) {
+      f32x4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = p[(long long)(s + u * G) * n];
+      v += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+    }
+    for (; s < S; s += G) v += p[(long long)s * n];
+  }
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  if (grp != 0 || i >= n) return;
+  for (int gg = 1; gg < G; ++gg) v += sh[gg * cols + c];
+  f32x4* o = (f32x4*)dst + i;
+  if (acc) v += *o;
+  *o = v;
 }
 
 // dw[co][ci][tap] (torch layout, real sizes) (+)= sum_s part[s][co][tap][ci]
@@ -1333,7 +1537,7 @@ long long wgrad_stripe_ws(int nf, int h, int w, int cin, int cout) {
 
 int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
                       int ld1, float* ws, float* dw, int acc_w, float* db, int acc_b, int nf, int h,
-                      int w, int cin, int cout, int cout_real, int cin_real, hipStream_t st) {
+                      int w, int cin, int cout, hipStream_t st) {
   WgradSArgs a;
   a.dy = (const bf16*)dy; a.lddy = lddy; a.x0 = (const bf16*)x0;
   a.x1 = (const bf16*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0; a.c0 = x1 ? c0 : cin;
@@ -1344,6 +1548,7 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   stripe_split(a.nstages, (cout / 64) * (cin / 64), a.stages_per_split, S);
   a.part = ws;
   a.dbpart = db ? ws + (long long)S * cout * a.K : nullptr;
+  a.dw = dw; a.db = db; a.acc_w = acc_w; a.acc_b = acc_b;
   dim3 grid(cout / 64, cin / 64, S);
   switch (w) {
     case 64: conv_wgrad_stripe_kernel<64><<<grid, 512, 0, st>>>(a); break;
@@ -1351,7 +1556,15 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
     case 16: conv_wgrad_stripe_kernel<16><<<grid, 512, 0, st>>>(a); break;
     default: conv_wgrad_stripe_kernel<8><<<grid, 512, 0, st>>>(a); break;
   }
-  launch_wgrad_reduce(a.part, S, cout, cin, 9, dw, cout_real, cin_real, acc_w, a.dbpart, db, acc_b, st);
+  if (S > 1) {
+    const long long n4 = (long long)cout * a.K / 4;
+    static const int gmax = getenv("DV_RED_G") ? atoi(getenv("DV_RED_G")) : 8;
+    int G = 1;
+    while (G * 2 <= gmax && G * 2 <= S) G *= 2;
+    const long long blocks = (n4 + 256 / G - 1) / (256 / G) + (db ? (cout / 4 + 256 / G - 1) / (256 / G) : 0);
+    wgrad_reduce4_kernel<<<(unsigned)blocks, 256, 0, st>>>(ws, S, G, n4, dw, acc_w, a.dbpart, db,
+                                                            cout, acc_b);
+  }
   return check_launch("conv_wgrad_stripe");
 }
 
@@ -1406,9 +1619,10 @@ extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0
   DV_REQUIRE(ws_floats >= need, "workspace too small (see dv_conv_wgrad_ws)");
   hipStream_t st = (hipStream_t)stream;
   if ((long long)nf * h * w == 0) return DV_OK;
-  if (dtype == DV_BF16 && wgrad_stripe_ok(nf, h, w, cin, c0, x1 != nullptr, cout, ksize))
+  if (dtype == DV_BF16 && cout_real == cout && cin_real == cin &&
+      wgrad_stripe_ok(nf, h, w, cin, c0, x1 != nullptr, cout, ksize))
     return conv_wgrad_stripe(dy, lddy, x0, ld0, c0, x1, ld1, ws, dw, accumulate_w, db, accumulate_b,
-                             nf, h, w, cin, cout, cout_real, cin_real, st);
+                             nf, h, w, cin, cout, st);
   // general path: f32 atomics into the zeroed packed workspace, then one reduce
   const long long K = (long long)ksize * ksize * cin;
   float* dbp = db ? ws + cout * K : nullptr;

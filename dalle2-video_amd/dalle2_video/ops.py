@@ -58,9 +58,12 @@ def _launch(name, flops, nbytes, fn):
         TIMER.run(name, flops, nbytes, fn)
 
 
-def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld):
+def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0):
     """Kernel instantiation dv_conv_fwd dispatches to (mirror of conv_fwd_t /
     glds_tile in dv_conv.hip) — names the launch for the live roofline."""
+    if (dtype_name == "bf16" and ks == 3 and cin == 64 and c0 == cin and cout % 64 == 0
+            and w in (32, 64) and h % (128 // w) == 0 and m % 128 == 0 and m * maxld < (1 << 31)):
+        return f"conv_fwd_stripe_kernel<{w}>"
     if dtype_name == "bf16" and cin % 64 == 0 and c0 % 64 == 0 and m * maxld < (1 << 31):
         bn = 64 if cout <= 64 else 128
         bm = 256 if bn == 64 else 128
@@ -315,7 +318,7 @@ class ConvFn(torch.autograd.Function):
         b = None if bias is None else bias.detach().float().contiguous()
         m = nf * h * w
         _launch(conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
-                              max(ld0, ld1)), 2.0 * m * cout * cin * ksize * ksize,
+                              max(ld0, ld1), ksize, h, w), 2.0 * m * cout * cin * ksize * ksize,
                 x0.element_size() * m * (cin + cout),
                 lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b), ptr(res),
                              ldr, ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE, stream()))
@@ -339,7 +342,7 @@ class ConvFn(torch.autograd.Function):
             alloc = torch.empty if cin_real == cin else torch.zeros
             dx = alloc(nf, h, w, cin, dtype=dy.dtype, device=dy.device)
             m = nf * h * w
-            _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, cout8),
+            _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, cout8, ksize, h, w),
                     2.0 * m * cin_real * cout8 * ksize * ksize,
                     dy8.element_size() * m * (cin + cout8),
                     lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd), None, None, 0,
@@ -373,8 +376,10 @@ class ConvFn(torch.autograd.Function):
             dname = _lib.dtype_name(dy8)
             ws = _wgrad_workspace(_lib.dtype_name(dy8), nf, h, w, cin, c0, x1 is not None, cout8,
                                   ksize, dy.device)
-            _launch(conv_wgrad_name(dname, m, cout8, cin, c0, x1 is not None, ksize, h, w,
-                                    max(cout8, ld0, ld1)),
+            kname = (conv_wgrad_name(dname, m, cout8, cin, c0, x1 is not None, ksize, h, w,
+                                     max(cout8, ld0, ld1)) if (cout8 == cout and cin_real == cin)
+                     else gemm_wgrad_name(dname, m, cout8, cin * ksize * ksize, max(cout8, ld0, ld1)))
+            _launch(kname,
                     2.0 * m * cout8 * cin * ksize * ksize,
                     dy8.element_size() * m * (cin + cout8),
                     lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), cout8, ptr(x0), ld0, c0, ptr(x1), ld1,

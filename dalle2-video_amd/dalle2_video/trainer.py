@@ -64,9 +64,13 @@ class FusedAdamW(torch.optim.Optimizer):
         if not live:
             return
         dev = live[0][1].device
-        n = sum(p.numel() for _, p in live)
-        P = torch.empty(n, dtype=torch.float32, device=dev)
-        G = torch.empty(n, dtype=torch.float32, device=dev)
+        # every parameter starts on a 64-B boundary (16 floats): the HIP kernels
+        # write gradients with 16-B vector stores; the zero gaps are inert for
+        # AdamW (zero grad and moments) and for the gradient norm
+        al = lambda k: (k + 15) // 16 * 16
+        n = sum(al(p.numel()) for _, p in live)
+        P = torch.zeros(n, dtype=torch.float32, device=dev)
+        G = torch.zeros(n, dtype=torch.float32, device=dev)
         M = torch.zeros(n, dtype=torch.float32, device=dev)
         V = torch.zeros(n, dtype=torch.float32, device=dev)
         ranges = []
@@ -88,7 +92,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 self.state[p] = dict(step=torch.tensor(float(self._t)),
                                      exp_avg=M[off:off + k].view_as(p),
                                      exp_avg_sq=V[off:off + k].view_as(p))
-                off += k
+                off += al(k)
             ranges.append((gi, start, off))
         self._flat = (P, G, M, V, ranges, [p for _, p in live])
 

@@ -57,6 +57,9 @@ def gemm_case(nb, rows, m, n):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "one":
+        conv_case(64, 64, 64, 64, 64, 3)
+        sys.exit(0)
     gemm_case(4, 16384, 32, 64)
     gemm_case(4, 4096, 32, 128)
     gemm_case(4, 1024, 32, 256)
