@@ -260,12 +260,13 @@ __device__ __attribute__((aligned(64))) unsigned int g_zero_line[16];
 
 __device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN>
+template <int BM, int BN, int NBUF>
 __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p, int tiles_n) {
   constexpr int TI = BM / 64, TJ = BN / 64;
   constexpr int GB = BM / 32, GA = BN / 32;  // DMA instructions per thread per K-tile
   constexpr int BUF = (BM + BN) * 128;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+  constexpr int DPK = GA + GB;               // DMAs per thread per K-tile
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
 
   // XCD-aware bijective remap of the 1-D block id
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -345,12 +346,26 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p,
 
   const int r = lane & 31, h = lane >> 5;
   const int nk = (p.K >> 6);
-  issue(0, 0);
+  // NBUF-deep ring, NBUF - 1 K-tiles in flight (deep rings when few
+  // workgroups share a CU: the load latency is then hidden by prefetch
+  // distance instead of by other workgroups)
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < nk) issue(i, i);
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) {
-      issue(kt + 1, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GA + GB) : "memory");
+    const int buf = kt % NBUF;
+    const int ahead = nk - 1 - kt;  // K-tiles issued after this one (before the new issue)
+    if (ahead >= NBUF - 1) {
+      issue(kt + NBUF - 1, (kt + NBUF - 1) % NBUF);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPK * (NBUF - 1)) : "memory");
+    } else if (NBUF >= 5 && ahead >= 4) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPK * 4) : "memory");
+    } else if (NBUF >= 4 && ahead >= 3) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPK * 3) : "memory");
+    } else if (NBUF >= 3 && ahead >= 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPK * 2) : "memory");
+    } else if (ahead >= 1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPK) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -936,7 +951,13 @@ template <int BM, int BN>
 int launch_fwd_glds(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   const int tn = (a.cout + BN - 1) / BN;
   const long long nb = ((a.M + BM - 1) / BM) * tn;
-  conv_fwd_glds_kernel<BM, BN><<<(unsigned)nb, 256, 0, st>>>(a, tn);
+  // ring depth by residency: one workgroup per CU -> as deep as LDS allows
+  constexpr int BUF = (BM + BN) * 128;
+  constexpr int DEEP = (160 * 1024) / BUF > 6 ? 6 : (160 * 1024) / BUF;
+  constexpr int MID = (80 * 1024) / BUF > 3 ? 3 : (80 * 1024) / BUF;
+  if (nb <= 256) conv_fwd_glds_kernel<BM, BN, DEEP><<<(unsigned)nb, 256, 0, st>>>(a, tn);
+  else if (nb <= 512 && MID >= 3) conv_fwd_glds_kernel<BM, BN, MID><<<(unsigned)nb, 256, 0, st>>>(a, tn);
+  else conv_fwd_glds_kernel<BM, BN, 2><<<(unsigned)nb, 256, 0, st>>>(a, tn);
   return check_launch("conv_fwd_glds");
 }
 
@@ -1193,24 +1214,26 @@ struct WgradSArgs {
   int seg, nseg;  // image rows per window segment, segments per stage
 };
 
-template <int W> struct StripeGeom {
+template <int W, int KS> struct StripeGeom {
   static constexpr int WP = W + 2;
-  static constexpr int WR = W == 8 ? 200 : (128 / W + 2) * WP;  // window rows (max over H)
+  // window rows (max over H): KS == 1 stages the 128 pixels themselves
+  static constexpr int WR = KS == 1 ? 128 : (W == 8 ? 200 : (128 / W + 2) * WP);
   static constexpr int NRH = (WR + 127) / 128;                  // 128-row DMA rounds per half
   static constexpr int AIMG = 2 * 128 * 64;                     // dY image: 2 co halves x 128 rows x 64 B
   static constexpr int BHALF = NRH * 128 * 64;                  // window image of one ci half
   static constexpr int STG = AIMG + 2 * BHALF;
   static constexpr int NBUF = STG * 3 <= 160 * 1024 ? 3 : 2;
+  static constexpr int NT = KS * KS;                            // taps
 };
 
 // LDS images are split by 32-channel half into 64-B rows: four consecutive
 // rows then start 16 banks apart, so the transposed operand reads are
 // conflict-free WITHOUT a swizzle, and an operand address is linear in the
 // row — every tap's window offset folds into the ds_read immediate.
-template <int W>
+template <int W, int KS>
 __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
-  using G = StripeGeom<W>;
-  constexpr int WP = G::WP, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF;
+  using G = StripeGeom<W, KS>;
+  constexpr int WP = G::WP, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF, NT = G::NT;
   constexpr int AIMG = G::AIMG, BHALF = G::BHALF;
   constexpr int DPS = 2 + 2 * NRH;  // DMAs per thread per stage
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * STG];
@@ -1236,6 +1259,11 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
 #pragma unroll
   for (int i = 0; i < NRH; ++i) {
     const int wr = 128 * i + 16 * wave + l4;
+    if (KS == 1) {  // the stage's own pixels
+      b_ry[i] = 0;
+      b_off[i] = wr;
+      continue;
+    }
     const int sg = wr / segrows, rem = wr - sg * segrows;
     const int ry = rem / WP, rx = rem - ry * WP;
     const bool ok = sg < a.nseg && rx >= 1 && rx <= W;
@@ -1254,10 +1282,10 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
                                        (__attribute__((address_space(3))) void*)(sA + hh * (AIMG / 2) + 16 * wave * 64),
                                        16, 0, 0);
     }
-    const int y0 = a.nseg > 1 ? 0 : (m0 % HW) / W;
+    const int y0 = (KS == 1 || a.nseg > 1) ? 0 : (m0 % HW) / W;
 #pragma unroll
     for (int i = 0; i < NRH; ++i) {
-      const bool in = (unsigned)(y0 + b_ry[i]) < (unsigned)a.H;
+      const bool in = KS == 1 || (unsigned)(y0 + b_ry[i]) < (unsigned)a.H;
       const bf16* src = in ? b_src + (long long)(m0 + b_off[i]) * xld : zero;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
@@ -1267,9 +1295,9 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
     }
   };
 
-  f32x16 acc[9];
+  f32x16 acc[NT];
 #pragma unroll
-  for (int d = 0; d < 9; ++d)
+  for (int d = 0; d < NT; ++d)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[d][e] = 0.f;
   // bias gradient on the VALU: a lane's A fragment holds 8 pixels of ONE
@@ -1284,6 +1312,11 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int plo = half * 64 + 16 * s + 8 * (g >> 1) + q, phi = plo + 4;
+    if (KS == 1) {
+      wlo[s] = plo * 64 + colb;
+      whi[s] = phi * 64 + colb;
+      continue;
+    }
     const int sl = plo / (seg * W), sh = phi / (seg * W);
     const int rl = plo - sl * seg * W, rh = phi - sh * seg * W;
     wlo[s] = (sl * segrows + (rl / W) * WP + rl % W) * 64 + colb;
@@ -1319,8 +1352,8 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
         fa = u32x4{l2[0], l2[1], h2[0], h2[1]};
       }
 #pragma unroll
-      for (int d = 0; d < 9; ++d) {
-        const int toff = ((d / 3) * WP + (d % 3)) * 64;
+      for (int d = 0; d < NT; ++d) {
+        const int toff = KS == 1 ? 0 : ((d / 3) * WP + (d % 3)) * 64;
         const s16x4 lo = tr_read(sB + wlo[s] + toff);
         const s16x4 hi = tr_read(sB + whi[s] + toff);
         const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
@@ -1342,7 +1375,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     constexpr int PER = (5 * 16 + 1) * 64;  // <= 5 taps + the bias sums per wave
-    const int d0 = pass == 0 ? 0 : 5, d1 = pass == 0 ? 5 : 9;
+    const int d0 = pass == 0 ? 0 : (NT < 5 ? NT : 5), d1 = pass == 0 ? (NT < 5 ? NT : 5) : NT;
     if (half == 1) {
 #pragma unroll
       for (int d = d0; d < d1; ++d)
@@ -1369,22 +1402,22 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   float* dst = direct ? a.dw : a.part + (long long)blockIdx.z * a.cout * a.K;
   const int acc_o = direct && a.acc_w;
   const int r = lane & 31, h = lane >> 5;
-  constexpr int TP = 32 * 9;  // floats per output channel in a tile
+  constexpr int TP = 32 * NT;  // floats per output channel in a tile
 #pragma unroll
   for (int rnd = 0; rnd < 2; ++rnd) {
     float* tile = red + wn * (32 * TP);
     if (half == 0 && wm == rnd) {
 #pragma unroll
-      for (int d = 0; d < 9; ++d)
+      for (int d = 0; d < NT; ++d)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int col = (e & 3) + 8 * (e >> 2) + 4 * h;  // local co
-          tile[col * TP + r * 9 + d] = acc[d][e];
+          tile[col * TP + r * NT + d] = acc[d][e];
         }
     }
     __syncthreads();
     if (half == 0 && wm == rnd) {
-      const long long rowbase = (long long)(co0 + wm * 32) * a.K + (ci0 + wn * 32) * 9;
+      const long long rowbase = (long long)(co0 + wm * 32) * a.K + (ci0 + wn * 32) * NT;
       for (int idx = lane; idx < 32 * (TP / 4); idx += 64) {
         const int col = idx / (TP / 4), j = idx - col * (TP / 4);
         f32x4 v = *(const f32x4*)(tile + col * TP + 4 * j);
@@ -1513,10 +1546,10 @@ bool stripe_geom(int h, int w, int& seg, int& nseg) {
 
 bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout, int ks) {
   int seg, nseg;
-  if (ks != 3 || cin % 64 || cout % 64 || (split && c0 % 64)) return false;
+  if ((ks != 3 && ks != 1) || cin % 64 || cout % 64 || (split && c0 % 64)) return false;
   const long long M = (long long)nf * h * w;
   if (M % 128 || M >= (1ll << 31)) return false;
-  return stripe_geom(h, w, seg, nseg);
+  return ks == 1 || stripe_geom(h, w, seg, nseg);
 }
 
 // split count: ~256 workgroups (one per CU: the stage ring takes up to 112 KB of LDS)
@@ -1528,21 +1561,22 @@ inline void stripe_split(int nstages, int grid_xy, int& sps, int& S) {
   S = (nstages + sps - 1) / sps;
 }
 
-long long wgrad_stripe_ws(int nf, int h, int w, int cin, int cout) {
+long long wgrad_stripe_ws(int nf, int h, int w, int cin, int cout, int ks) {
   const int nstages = (int)((long long)nf * h * w / 128);
   int sps, S;
   stripe_split(nstages, (cout / 64) * (cin / 64), sps, S);
-  return (long long)S * cout * (9LL * cin + 1);
+  return (long long)S * cout * ((long long)ks * ks * cin + 1);
 }
 
 int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
                       int ld1, float* ws, float* dw, int acc_w, float* db, int acc_b, int nf, int h,
-                      int w, int cin, int cout, hipStream_t st) {
+                      int w, int cin, int cout, int ks, hipStream_t st) {
   WgradSArgs a;
   a.dy = (const bf16*)dy; a.lddy = lddy; a.x0 = (const bf16*)x0;
   a.x1 = (const bf16*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0; a.c0 = x1 ? c0 : cin;
-  a.H = h; a.cin = cin; a.cout = cout; a.K = 9 * cin;
-  stripe_geom(h, w, a.seg, a.nseg);
+  a.H = h; a.cin = cin; a.cout = cout; a.K = ks * ks * cin;
+  a.seg = 1; a.nseg = 1;
+  if (ks == 3) stripe_geom(h, w, a.seg, a.nseg);
   a.nstages = (int)((long long)nf * h * w / 128);
   int S;
   stripe_split(a.nstages, (cout / 64) * (cin / 64), a.stages_per_split, S);
@@ -1550,11 +1584,15 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   a.dbpart = db ? ws + (long long)S * cout * a.K : nullptr;
   a.dw = dw; a.db = db; a.acc_w = acc_w; a.acc_b = acc_b;
   dim3 grid(cout / 64, cin / 64, S);
-  switch (w) {
-    case 64: conv_wgrad_stripe_kernel<64><<<grid, 512, 0, st>>>(a); break;
-    case 32: conv_wgrad_stripe_kernel<32><<<grid, 512, 0, st>>>(a); break;
-    case 16: conv_wgrad_stripe_kernel<16><<<grid, 512, 0, st>>>(a); break;
-    default: conv_wgrad_stripe_kernel<8><<<grid, 512, 0, st>>>(a); break;
+  if (ks == 1) {
+    conv_wgrad_stripe_kernel<64, 1><<<grid, 512, 0, st>>>(a);
+  } else {
+    switch (w) {
+      case 64: conv_wgrad_stripe_kernel<64, 3><<<grid, 512, 0, st>>>(a); break;
+      case 32: conv_wgrad_stripe_kernel<32, 3><<<grid, 512, 0, st>>>(a); break;
+      case 16: conv_wgrad_stripe_kernel<16, 3><<<grid, 512, 0, st>>>(a); break;
+      default: conv_wgrad_stripe_kernel<8, 3><<<grid, 512, 0, st>>>(a); break;
+    }
   }
   if (S > 1) {
     const long long n4 = (long long)cout * a.K / 4;
@@ -1596,7 +1634,7 @@ extern "C" int dv_conv_wgrad_ws(int dtype, int nf, int h, int w, int cin, int c0
   DV_REQUIRE(cin > 0 && cout > 0 && ksize >= 1, "bad sizes");
   const long long K = (long long)ksize * ksize * cin;
   if (dtype == DV_BF16 && wgrad_stripe_ok(nf, h, w, cin, c0, split != 0, cout, ksize))
-    *floats = wgrad_stripe_ws(nf, h, w, cin, cout);
+    *floats = wgrad_stripe_ws(nf, h, w, cin, cout, ksize);
   else
     *floats = (long long)cout * (K + 1);
   return DV_OK;
@@ -1622,7 +1660,7 @@ extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0
   if (dtype == DV_BF16 && cout_real == cout && cin_real == cin &&
       wgrad_stripe_ok(nf, h, w, cin, c0, x1 != nullptr, cout, ksize))
     return conv_wgrad_stripe(dy, lddy, x0, ld0, c0, x1, ld1, ws, dw, accumulate_w, db, accumulate_b,
-                             nf, h, w, cin, cout, st);
+                             nf, h, w, cin, cout, ksize, st);
   // general path: f32 atomics into the zeroed packed workspace, then one reduce
   const long long K = (long long)ksize * ksize * cin;
   float* dbp = db ? ws + cout * K : nullptr;

@@ -4,6 +4,8 @@
 // reads/writes the activation once with 16-byte vectors; statistics are f32.
 #include "dv_common.h"
 
+#include <algorithm>
+
 using namespace dv;
 
 namespace {
@@ -50,6 +52,8 @@ struct GnArgs {
   float* sums;      // nb * C * 2, zero on entry
   float* next;      // zeroed by the apply (next call's sums), or null
   long long next_n;
+  int R;            // replicas of the sums the reduce spreads its atomics over
+  long long rstride;
   float eps;
   float *dgamma, *dbeta, *dss;
   int accumulate;
@@ -94,6 +98,7 @@ template <typename T, int MODE>
 __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int U = MODE == 0 ? 2 * GN_U : GN_U;
+  constexpr int NL = MODE == 1 ? 2 : 1;  // tensors streamed (z, dy)
   __shared__ float sh[2][256 * VEC];
   __shared__ float smu[64], srs[64];
   const int tpr = a.C / VEC;                 // threads per pixel row
@@ -101,42 +106,56 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   const int tid = threadIdx.x;
   const int rr = tid / tpr, cv = (tid % tpr) * VEC;
   const int b = blockIdx.y;
+  const long long beg = blockIdx.x * a.rows_per_block;
+  long long end = beg + a.rows_per_block;
+  if (end > a.P) end = a.P;
+  const long long step = (long long)rpp * U;
+  const T* zb = (const T*)a.z + (long long)b * a.P * a.ldz + cv;
+  const T* dyb = (const T*)a.dy + (long long)b * a.P * a.lddy + cv;
+  const bool act_rows = rr < rpp;
+  // batch loads (rows p0 + u*rpp), issued one batch ahead of their use
+  u32x4 cur[NL][U], nxt[NL][U];
+  auto load = [&](long long p0, u32x4 (&buf)[NL][U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long p = p0 + (long long)u * rpp;
+      if (act_rows && p < end) {
+        buf[0][u] = *(const u32x4*)(zb + p * a.ldz);
+        if (MODE == 1) buf[NL - 1][u] = *(const u32x4*)(dyb + p * a.lddy);
+      }
+    }
+  };
+  long long p0 = beg + rr;
+  load(p0, cur);  // in flight across the prologue
+  if (MODE == 1 && !a.accumulate && blockIdx.x == 0 && b == 0) {  // the apply atomically adds
+    for (int c = tid; c < a.C; c += 256) {
+      if (a.dgamma) a.dgamma[c] = 0.f;
+      if (a.dbeta) a.dbeta[c] = 0.f;
+    }
+  }
   if (MODE == 1) {
     for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
     __syncthreads();
   }
-  const long long beg = blockIdx.x * a.rows_per_block;
-  long long end = beg + a.rows_per_block;
-  if (end > a.P) end = a.P;
   float s1[VEC], s2[VEC];
 #pragma unroll
   for (int e = 0; e < VEC; ++e) s1[e] = s2[e] = 0.f;
-  if (rr < rpp) {
+  if (act_rows) {
     ChanCoef k[MODE == 1 ? VEC : 1];
     if (MODE == 1) load_coef<VEC>(a, b, cv, smu, srs, k);
-    const T* zb = (const T*)a.z + (long long)b * a.P * a.ldz + cv;
-    const T* dyb = (const T*)a.dy + (long long)b * a.P * a.lddy + cv;
-    for (long long p0 = beg + rr; p0 < end; p0 += (long long)rpp * U) {
-      u32x4 zr[U], dr[MODE == 1 ? U : 1];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const long long p = p0 + (long long)u * rpp;
-        if (p < end) {
-          zr[u] = *(const u32x4*)(zb + p * a.ldz);
-          if (MODE == 1) dr[u] = *(const u32x4*)(dyb + p * a.lddy);
-        }
-      }
+    for (; p0 < end; p0 += step) {
+      if (p0 + step < end) load(p0 + step, nxt);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (p0 + (long long)u * rpp >= end) break;
         float z[VEC];
-        Vec<T>::to_f(zr[u], z);
+        Vec<T>::to_f(cur[0][u], z);
         if (MODE == 0) {
 #pragma unroll
           for (int e = 0; e < VEC; ++e) { s1[e] += z[e]; s2[e] += z[e] * z[e]; }
         } else {
           float dy[VEC];
-          Vec<T>::to_f(dr[u], dy);
+          Vec<T>::to_f(cur[NL - 1][u], dy);
 #pragma unroll
           for (int e = 0; e < VEC; ++e) {
             const float v = z[e] * k[e].A + k[e].B;
@@ -146,6 +165,10 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
           }
         }
       }
+#pragma unroll
+      for (int l = 0; l < NL; ++l)
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[l][u] = nxt[l][u];
     }
   }
   // block reduce over the row slots, then one atomic per channel
@@ -162,24 +185,37 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
       t1 += sh[0][(r * tpr + owner) * VEC + e];
       t2 += sh[1][(r * tpr + owner) * VEC + e];
     }
-    atomicAdd(a.sums + ((long long)b * a.C + c) * 2, t1);
-    atomicAdd(a.sums + ((long long)b * a.C + c) * 2 + 1, t2);
+    float* rs = a.sums + (blockIdx.x % a.R) * a.rstride;  // 1/R of the same-address contention
+    atomicAdd(rs + ((long long)b * a.C + c) * 2, t1);
+    atomicAdd(rs + ((long long)b * a.C + c) * 2 + 1, t2);
   }
 }
 
-// apply prologue: this sample's per-group terms from its [C][2] sums, one
-// wave per group (channel sums combined in double for the variance).
+
+// apply prologue: this sample's per-channel totals (summed over the R
+// replicas; one parallel round of loads) staged in LDS as cs[0..C) / cs[C..2C),
+// then one wave per group (channel sums combined in double for the variance).
 //   MODE 0: t1 = mean, t2 = rstd      MODE 1: t1 = m1, t2 = m2
 template <int MODE>
-__device__ void gn_group_terms(const GnArgs& a, int b, float* t1, float* t2) {
+__device__ void gn_group_terms(const GnArgs& a, int b, float* cs, float* t1, float* t2) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cg = a.C / a.G;
-  const float* sb = a.sums + (long long)b * a.C * 2;
+  const long long sb = (long long)b * a.C * 2;
+  for (int c = threadIdx.x; c < a.C; c += 256) {
+    float v1 = 0.f, v2 = 0.f;
+    for (int r = 0; r < a.R; ++r) {
+      v1 += a.sums[r * a.rstride + sb + 2 * c];
+      v2 += a.sums[r * a.rstride + sb + 2 * c + 1];
+    }
+    cs[c] = v1;
+    cs[a.C + c] = v2;
+  }
+  __syncthreads();
   for (int g = wave; g < a.G; g += 4) {
     if (MODE == 0) {
       double s1 = 0.0, s2 = 0.0;
       for (int c = g * cg + lane; c < (g + 1) * cg; c += 64) {
-        s1 += sb[2 * c];
-        s2 += sb[2 * c + 1];
+        s1 += cs[c];
+        s2 += cs[a.C + c];
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
@@ -196,8 +232,8 @@ __device__ void gn_group_terms(const GnArgs& a, int b, float* t1, float* t2) {
       for (int c = g * cg + lane; c < (g + 1) * cg; c += 64) {
         const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
         const float k = a.gamma[c] * sc;
-        m1 += k * sb[2 * c];
-        m2 += k * sb[2 * c + 1];
+        m1 += k * cs[c];
+        m2 += k * cs[a.C + c];
       }
       m1 = wave_sum(m1);
       m2 = wave_sum(m2);
@@ -217,43 +253,64 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int U = GN_U;
   __shared__ float t1[64], t2[64], smu[64], srs[64];
+  __shared__ float cs[2 * 1024];  // this sample's per-channel totals
   const int tid = threadIdx.x;
   const int tpr = a.C / VEC, rpp = 256 / tpr;
   const int rr = tid / tpr, cv = (tid % tpr) * VEC;
   const int b = blockIdx.y, cg = a.C / a.G;
-  gn_group_terms<MODE>(a, b, t1, t2);
+  const long long beg = blockIdx.x * a.rows_per_block;
+  long long end = beg + a.rows_per_block;
+  if (end > a.P) end = a.P;
+  const long long pb = (long long)b * a.P;
+  const long long step = (long long)rpp * U;
+  const bool act_rows = rr < rpp;
+  const bool has_x = MODE == 1 || a.res != nullptr;  // second stream: dy (bwd) or res (fwd)
+  const T* xsrc = MODE == 1 ? (const T*)a.dy : (const T*)a.res;
+  const int ldx = MODE == 1 ? a.lddy : a.ldres;
+  u32x4 zc[U], xc[U], zn[U], xn[U];
+  auto load = [&](long long p0, u32x4 (&zb)[U], u32x4 (&xb)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long p = p0 + (long long)u * rpp;
+      if (act_rows && p < end) {
+        zb[u] = *(const u32x4*)((const T*)a.z + (pb + p) * a.ldz + cv);
+        if (has_x) xb[u] = *(const u32x4*)(xsrc + (pb + p) * ldx + cv);
+      }
+    }
+  };
+  long long p0 = beg + rr;
+  load(p0, zc, xc);  // the first batch is in flight across the prologue
+  gn_group_terms<MODE>(a, b, cs, t1, t2);
   if (MODE == 1)
     for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
   __syncthreads();
   if (blockIdx.x == 0) {
     if (MODE == 0) {  // saved for the backward
       for (int g = tid; g < a.G; g += 256) { a.mean[b * a.G + g] = t1[g]; a.rstd[b * a.G + g] = t2[g]; }
-    } else if (b == 0) {  // parameter gradients over all samples
+    } else {  // this sample's FiLM gradients; its share of dgamma / dbeta (zeroed by the reduce)
       for (int c = tid; c < a.C; c += 256) {
-        float dg = 0.f, db = 0.f;
-        for (int bb = 0; bb < a.nb; ++bb) {
-          const float r1 = a.sums[((long long)bb * a.C + c) * 2];
-          const float r2 = a.sums[((long long)bb * a.C + c) * 2 + 1];
-          const float sc = a.ss ? 1.f + a.ss[(long long)bb * 2 * a.C + c] : 1.f;
-          dg += sc * r2;
-          db += sc * r1;
-          if (a.dss) {
-            a.dss[(long long)bb * 2 * a.C + c] = a.gamma[c] * r2 + a.beta[c] * r1;  // d scale
-            a.dss[(long long)bb * 2 * a.C + a.C + c] = r1;                          // d shift
-          }
+        const float r1 = cs[c], r2 = cs[a.C + c];
+        const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
+        const float gm = a.gamma[c], bt = a.beta[c];
+        if (a.dss) {
+          a.dss[(long long)b * 2 * a.C + c] = gm * r2 + bt * r1;  // d scale
+          a.dss[(long long)b * 2 * a.C + a.C + c] = r1;           // d shift
         }
-        if (a.dgamma) a.dgamma[c] = a.accumulate ? a.dgamma[c] + dg : dg;
-        if (a.dbeta) a.dbeta[c] = a.accumulate ? a.dbeta[c] + db : db;
-      }
-    }
-    if (b == 0 && a.next) {  // the next GroupNorm call's sums start at zero
-      for (long long i = tid * 4; i < a.next_n; i += 1024) {
-        if (i + 4 <= a.next_n) *(f32x4*)(a.next + i) = f32x4{0.f, 0.f, 0.f, 0.f};
-        else for (long long j = i; j < a.next_n; ++j) a.next[j] = 0.f;
+        if (a.dgamma) atomicAdd(a.dgamma + c, sc * r2);
+        if (a.dbeta) atomicAdd(a.dbeta + c, sc * r1);
       }
     }
   }
-  if (rr >= rpp) return;
+  if (a.next) {  // the next GroupNorm call's sums start at zero (spread over the grid)
+    const long long nblk = (long long)gridDim.x * gridDim.y;
+    const long long per = ((a.next_n + nblk - 1) / nblk + 3) / 4 * 4;
+    const long long i0 = ((long long)b * gridDim.x + blockIdx.x) * per;
+    for (long long i = i0 + tid * 4; i < i0 + per && i < a.next_n; i += 1024) {
+      if (i + 4 <= a.next_n) *(f32x4*)(a.next + i) = f32x4{0.f, 0.f, 0.f, 0.f};
+      else for (long long j = i; j < a.next_n; ++j) a.next[j] = 0.f;
+    }
+  }
+  if (!act_rows) return;
   ChanCoef k[VEC];
   float m1[VEC], m2[VEC];
   if (MODE == 0) {
@@ -267,42 +324,29 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
       m2[e] = -k[e].rs * t2[g];
     }
   }
-  const long long beg = blockIdx.x * a.rows_per_block;
-  long long end = beg + a.rows_per_block;
-  if (end > a.P) end = a.P;
-  const long long pb = (long long)b * a.P;
-  for (long long p0 = beg + rr; p0 < end; p0 += (long long)rpp * U) {
-    u32x4 zr[U], xr[U];  // xr: res (fwd) or dy (bwd)
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long p = p0 + (long long)u * rpp;
-      if (p < end) {
-        zr[u] = *(const u32x4*)((const T*)a.z + (pb + p) * a.ldz + cv);
-        if (MODE == 1) xr[u] = *(const u32x4*)((const T*)a.dy + (pb + p) * a.lddy + cv);
-        else if (a.res) xr[u] = *(const u32x4*)((const T*)a.res + (pb + p) * a.ldres + cv);
-      }
-    }
+  for (; p0 < end; p0 += step) {
+    if (p0 + step < end) load(p0 + step, zn, xn);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long p = p0 + (long long)u * rpp;
       if (p >= end) break;
       float z[VEC], o[VEC];
-      Vec<T>::to_f(zr[u], z);
+      Vec<T>::to_f(zc[u], z);
       if (MODE == 0) {
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
           const float v = z[e] * k[e].A + k[e].B;
           o[e] = a.act == DV_ACT_SILU ? silu_f(v) : v;
         }
-        if (a.res) {
+        if (has_x) {
           float r[VEC];
-          Vec<T>::to_f(xr[u], r);
+          Vec<T>::to_f(xc[u], r);
 #pragma unroll
           for (int e = 0; e < VEC; ++e) o[e] += r[e];
         }
       } else {
         float dy[VEC];
-        Vec<T>::to_f(xr[u], dy);
+        Vec<T>::to_f(xc[u], dy);
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
           const float v = z[e] * k[e].A + k[e].B;
@@ -313,6 +357,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
       }
       st_vec<T>((T*)a.out + (pb + p) * a.ldo + cv, o);
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) { zc[u] = zn[u]; xc[u] = xn[u]; }
   }
 }
 
@@ -338,7 +384,7 @@ int gn_fwd_t(GnArgs a, hipStream_t st) {
   a.rows_per_block = gn_rows(a, VEC, 2 * GN_U, 768);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_reduce_kernel<T, 0><<<g1, 256, 0, st>>>(a);
-  a.rows_per_block = gn_rows(a, VEC, GN_U, 2048);
+  a.rows_per_block = gn_rows(a, VEC, GN_U, 1024);
   dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_apply_kernel<T, 0><<<g2, 256, 0, st>>>(a);
   return check_launch("gn_fwd");
@@ -350,7 +396,7 @@ int gn_bwd_t(GnArgs a, hipStream_t st) {
   a.rows_per_block = gn_rows(a, VEC, GN_U, 768);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_reduce_kernel<T, 1><<<g1, 256, 0, st>>>(a);
-  a.rows_per_block = gn_rows(a, VEC, GN_U, 2048);
+  a.rows_per_block = gn_rows(a, VEC, GN_U, 1024);
   dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_apply_kernel<T, 1><<<g2, 256, 0, st>>>(a);
   return check_launch("gn_bwd");
@@ -484,6 +530,8 @@ extern "C" int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, co
   a.z = z; a.ldz = ldz; a.out = y; a.ldo = ldy; a.res = res; a.ldres = ldres; a.nb = nb;
   a.P = P; a.C = C; a.G = G; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta;
   a.ss = ss; a.act = act; a.sums = sums; a.next = next; a.next_n = next ? next_n : 0; a.eps = eps;
+  a.rstride = (long long)nb * C * 2;
+  a.R = next && a.rstride > 0 ? (int)std::min<long long>(8, std::max<long long>(1, next_n / a.rstride)) : 1;
   if (nb == 0 || P == 0) return DV_OK;
   hipStream_t st = (hipStream_t)stream;
   return dtype == DV_BF16 ? gn_fwd_t<bf16>(a, st) : gn_fwd_t<float>(a, st);
@@ -504,6 +552,8 @@ extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int
   a.z = z; a.ldz = ldz; a.dy = dy; a.lddy = lddy; a.out = dz; a.ldo = lddz; a.nb = nb; a.P = P;
   a.C = C; a.G = G; a.mean = (float*)mean; a.rstd = (float*)rstd; a.gamma = gamma; a.beta = beta;
   a.ss = ss; a.act = act; a.sums = sums; a.next = next; a.next_n = next ? next_n : 0;
+  a.rstride = (long long)nb * C * 2;
+  a.R = next && a.rstride > 0 ? (int)std::min<long long>(8, std::max<long long>(1, next_n / a.rstride)) : 1;
   a.dgamma = dgamma; a.dbeta = dbeta; a.dss = dss; a.accumulate = accumulate;
   if (nb == 0 || P == 0) return DV_OK;
   hipStream_t st = (hipStream_t)stream;

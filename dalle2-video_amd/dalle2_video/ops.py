@@ -71,19 +71,26 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0):
             bm = 128
         if bn == 128 and ((m + 127) // 128) * ((cout + 127) // 128) < 256:
             bm = 64
-        return f"conv_fwd_glds_kernel<{bm},{bn}>"
+        nb = ((m + bm - 1) // bm) * ((cout + bn - 1) // bn)
+        buf = (bm + bn) * 128
+        deep, mid = min(6, 160 * 1024 // buf), min(3, 80 * 1024 // buf)
+        nbuf = deep if nb <= 256 else (mid if nb <= 512 and mid >= 3 else 2)
+        return f"conv_fwd_glds_kernel<{bm},{bn},{nbuf}>"
     bm, bn = conv_tile(m, cout)
     return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"
 
 
 def conv_wgrad_name(dtype_name, m, cout, cin, c0, split, ks, h, w, maxld):
     """Mirror of dv_conv_wgrad's kernel choice (wgrad_stripe_ok / conv_wgrad_glds)."""
+    if (dtype_name == "bf16" and ks == 1 and cin % 64 == 0 and cout % 64 == 0
+            and (not split or c0 % 64 == 0) and m % 128 == 0):
+        return "conv_wgrad_stripe_kernel<64,1>"
     if (dtype_name == "bf16" and ks == 3 and cin % 64 == 0 and cout % 64 == 0
             and (not split or c0 % 64 == 0) and m % 128 == 0 and w in (8, 16, 32, 64)
             and ((h * w >= 128 and h % (128 // w) == 0)
                  or (h * w < 128 and 128 % (h * w) == 0
                      and (128 // (h * w)) * (h + 2) * (w + 2) <= (200 if w == 8 else (128 // w + 2) * (w + 2))))):
-        return f"conv_wgrad_stripe_kernel<{w}>"
+        return f"conv_wgrad_stripe_kernel<{w},3>"
     K = ks * ks * cin
     return gemm_wgrad_name(dtype_name, m, cout, K, maxld)
 

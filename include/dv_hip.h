@@ -127,11 +127,13 @@ int dv_gemm_tn_batched(int dtype, const void* a, int lda, const void* b, int ldb
  * ss = [nb][2C] f32 with scale first), + res.  nb batch elements of P pixels
  * (all frames of one clip form one GroupNorm sample), C channels, G groups.
  * mean/rstd [nb][G] f32 are written for the backward.  Two launches per
- * call (reduce, apply).  sums: nb*C*2 floats that must be ZERO on entry; the
- * call does NOT re-zero them (its apply still reads them) but zeroes `next`
- * (next_n floats, may be NULL): the buffer the caller's NEXT GroupNorm call
- * (forward or backward) will pass as `sums`.  Alternating two buffers keeps
- * both zero on entry without any memset launch.
+ * call (reduce, apply).  sums: next_n floats (>= nb*C*2) that must be ZERO on
+ * entry — the reduce spreads its atomics over up to 8 replicas of the
+ * nb*C*2 sums that fit; the call does NOT re-zero them (its apply still
+ * reads them) but zeroes `next` (next_n floats; NULL means one replica and
+ * no zeroing): the buffer the caller's NEXT GroupNorm call (forward or
+ * backward) will pass as `sums`.  Alternating two buffers keeps both zero on
+ * entry without any memset launch.
  * C % (16 B) == 0, C <= 256 vectors, G <= 64.  act: DV_ACT_*.               */
 int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* res, int ldres,
               int nb, long long P, int C, int G, float eps, const float* gamma,

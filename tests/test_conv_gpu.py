@@ -24,6 +24,11 @@ CASES = [
     (2, 8, 8, 512, 256, 512, 3),    # W=8, 12 channel chunks x 3 tap rows, one split
     (8, 16, 16, 256, 0, 64, 1),     # 1x1 (Downsample3D-like), many splits
     (16, 8, 8, 64, 0, 128, 3),      # W=8, 2 cout tiles
+    (16, 32, 32, 128, 0, 64, 1),    # 1x1 stripe wgrad (res_conv-like), 2 channel chunks
+    (8, 16, 16, 64, 64, 128, 1),    # 1x1 stripe wgrad, dual source
+    # stripe forward / dgrad (64 input channels, W in {32, 64})
+    (8, 32, 32, 64, 0, 128, 3),     # W=32, 2 cout tiles (dgrad: 128 -> 64 implicit GEMM)
+    (4, 64, 64, 64, 0, 64, 3),      # W=64, forward and dgrad both stripe
 ]
 
 
