@@ -81,13 +81,54 @@ def cpu_baseline(args):
     t = torch.randint(0, 1000, (args.batch,), generator=g)
     noise = torch.randn(x.shape, generator=g)
     R.train_step(u, sched, opt, x, t, noise)  # warm-up
+    n = 2
     t0 = time.perf_counter()
-    R.train_step(u, sched, opt, x, t, noise)
-    dt = time.perf_counter() - t0
+    for _ in range(n):
+        R.train_step(u, sched, opt, x, t, noise)
+    dt = (time.perf_counter() - t0) / n
     return {"value": round(1.0 / dt, 5), "unit": "denoise-steps/s", "cores": threads, "kind": "port",
-            "sample": f"1 timed train step (p_losses fwd+bwd+AdamW, f32) of the CPU oracle at "
+            "sample": f"{n} timed train steps (p_losses fwd+bwd+AdamW, f32) of the CPU oracle at "
                       f"{args.frames}x{args.size}x{args.size} bs={args.batch} after 1 warm-up step "
-                      f"({dt:.2f} s)"}
+                      f"({dt:.2f} s each)"}
+
+
+def kernel_key(name):
+    """(identifier, integer template args) of a mangled / demangled kernel name
+    or of a bench label such as 'conv_fwd_glds_kernel<64,128,6>'."""
+    import re
+    if name.startswith("_Z"):
+        m = re.search(r"_GLOBAL__N_1", name)
+        rest = name[m.end():] if m else re.sub(r"^_ZN?", "", name)
+        n = re.match(r"(\d+)", rest)
+        if n:
+            ln = int(n.group(1))
+            base = rest[len(n.group(1)):len(n.group(1)) + ln]
+            targs = rest[len(n.group(1)) + ln:]
+            ints = tuple(int(v) for v in re.findall(r"Li(\d+)E", targs.split("EEv")[0] + "E")) \
+                if targs.startswith("I") else ()
+            return base, ints
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "").strip()
+    m = re.match(r"([A-Za-z_]\w*)(<([^>]*)>)?", name)
+    if not m:
+        return name, ()
+    ints = tuple(int(t.strip()) for t in (m.group(3) or "").split(",") if re.fullmatch(r"\s*-?\d+\s*", t))
+    return m.group(1), ints
+
+
+def pmc_traffic(name):
+    """HBM bytes per launch of kernel `name` from the newest committed PMC
+    summary (profiles/pmc_traffic_*.json, made by tools/pmc_traffic.py from
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")))
+    if not files:
+        return None
+    table = json.load(open(files[-1]))
+    want = kernel_key(name)
+    for k, v in table.items():
+        if kernel_key(k) == want:
+            return v.get("traffic_bytes")
+    return None
 
 
 def main():
@@ -139,14 +180,20 @@ def main():
         for _ in range(max(2, min(args.steps, 5))):
             step()
         summ = ops.TIMER.summary()
+        event_ovh_us = ops.TIMER.event_overhead_ms * 1e3
         ops.TIMER = None
         name, d = max(summ.items(), key=lambda kv: kv[1]["ms"])
         peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
         avg_ms = d["ms"] / d["count"]
         achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+        traffic = pmc_traffic(name)
         roof = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 1), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "traffic": None if traffic is None else round(traffic),
+                "traffic_unit": "bytes/launch (2*FETCH_SIZE + WRITE_SIZE, PMC)",
+                "algorithmic_bytes_per_launch": round(d["bytes"] / d["count"]),
                 "launches_per_step": d["count"] // max(2, min(args.steps, 5)),
+                "event_overhead_us_subtracted": round(event_ovh_us, 2),
                 "avg_launch_us": round(avg_ms * 1e3, 2),
                 "algorithmic_flop_per_launch": round(d["flops"] / d["count"])}
         kernels = {k: {"ms_per_step": round(v["ms"] / max(2, min(args.steps, 5)), 3),

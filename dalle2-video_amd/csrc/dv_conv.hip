@@ -877,51 +877,77 @@ int conv_wgrad_glds(const void* dy, int lddy, const void* x0, int ld0, int c0, c
   return launch_wgrad_glds<128, 128>(a, st);
 }
 
-template <typename T>
-__global__ void pack_weight_kernel(const float* w, T* out, int cout, int cin, int taps,
-                                   int pad_to, int mode) {
-  // mode 0: out[co][tap][ci_p] (ci_p < pad_to); mode 1: out[ci][tap'][co_p]
-  long long total = mode == 0 ? (long long)cout * taps * pad_to : (long long)cin * taps * pad_to;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    if (mode == 0) {
-      int ci = (int)(idx % pad_to);
-      long long t = idx / pad_to;
-      int tap = (int)(t % taps), co = (int)(t / taps);
-      if (ci < cin) v = w[((long long)co * cin + ci) * taps + tap];
-    } else {
-      int co = (int)(idx % pad_to);
-      long long t = idx / pad_to;
-      int tapd = (int)(t % taps), ci = (int)(t / taps);
-      if (co < cout) v = w[((long long)co * cin + ci) * taps + (taps - 1 - tapd)];
+// Weight packing, LDS-staged so both the torch-layout reads and the packed
+// writes are coalesced:
+//   mode 0 (forward):  out[co][tap][ci_p]  <- w[co][ci][tap]   (tile = 1 co row)
+//   mode 1 (dgrad):    out[ci][tap'][co_p] <- w[co][ci][taps-1-tap']
+//                      (tile = CT input channels: every co's contiguous
+//                      w[co][ci0:ci0+CT][:] segment is read, then transposed)
+constexpr int PACK_LDS = 8192;   // floats: the largest row / column group accepted
+constexpr int PACK_TILE = 8192;  // floats staged per tile (several rows when they are small)
+
+__device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
+  const int taps = e.taps, cin = e.cin, cout = e.cout, pad = e.pad_to;
+  if ((long long)(e.mode == 0 ? cin : cout) * taps > PACK_LDS) return;  // rejected on the host
+  const bool bf = e.dtype == DV_BF16;
+  if (e.mode == 0) {
+    const int row = cin * taps;
+    int rt = PACK_TILE / row;
+    if (rt < 1) rt = 1;
+    const int co0 = tile * rt, rn = min(rt, cout - co0);
+    const float* src = e.w + (long long)co0 * row;  // rn consecutive rows: contiguous
+    for (int i = threadIdx.x; i < rn * row; i += 256) sm[i] = src[i];
+    __syncthreads();
+    const int orow = taps * pad;
+    const long long ob = (long long)co0 * orow;
+    for (int i = threadIdx.x; i < rn * orow; i += 256) {
+      const int rl = i / orow, j = i - rl * orow;
+      const int tap = j / pad, ci = j - tap * pad;
+      const float v = ci < cin ? sm[rl * row + ci * taps + tap] : 0.f;
+      if (bf) ((bf16*)e.out)[ob + i] = (bf16)v;
+      else ((float*)e.out)[ob + i] = v;
     }
-    out[idx] = (T)v;
+  } else {
+    int ct = PACK_TILE / (cout * taps);
+    if (ct < 1) ct = 1;
+    const int ci0 = tile * ct, cn = min(ct, cin - ci0);
+    const int seg = cn * taps;  // contiguous floats per co
+    for (int i = threadIdx.x; i < cout * seg; i += 256) {
+      const int co = i / seg, j = i - co * seg;
+      sm[i] = e.w[((long long)co * cin + ci0) * taps + j];
+    }
+    __syncthreads();
+    const int orow = taps * pad;
+    const long long ob = (long long)ci0 * orow;
+    for (int i = threadIdx.x; i < cn * orow; i += 256) {
+      const int cl = i / orow, j = i - cl * orow;
+      const int tapd = j / pad, co = j - tapd * pad;
+      const float v = co < cout ? sm[co * seg + cl * taps + (taps - 1 - tapd)] : 0.f;
+      if (bf) ((bf16*)e.out)[ob + i] = (bf16)v;
+      else ((float*)e.out)[ob + i] = v;
+    }
   }
+  __syncthreads();  // sm is reused by the next tile
+}
+
+__device__ __forceinline__ int pack_tiles(const DvPackEntry& e) {
+  const int unit = (e.mode == 0 ? e.cin : e.cout) * e.taps;
+  int per = PACK_TILE / unit;
+  if (per < 1) per = 1;
+  const int rows = e.mode == 0 ? e.cout : e.cin;
+  return (rows + per - 1) / per;
+}
+
+__global__ __launch_bounds__(256) void pack_weight_kernel(DvPackEntry e) {
+  __shared__ float sm[PACK_LDS];  // one row may need up to PACK_LDS floats
+  for (int t = blockIdx.x; t < pack_tiles(e); t += gridDim.x) pack_tile(e, t, sm);
 }
 
 // many weights in one launch: blockIdx.y selects the table entry
-__global__ void pack_weight_batched_kernel(const DvPackEntry* table) {
+__global__ __launch_bounds__(256) void pack_weight_batched_kernel(const DvPackEntry* table) {
+  __shared__ float sm[PACK_LDS];
   const DvPackEntry e = table[blockIdx.y];
-  const long long rows = e.mode == 0 ? e.cout : e.cin;
-  const long long total = rows * e.taps * e.pad_to;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    if (e.mode == 0) {
-      const int ci = (int)(idx % e.pad_to);
-      const long long t = idx / e.pad_to;
-      const int tap = (int)(t % e.taps), co = (int)(t / e.taps);
-      if (ci < e.cin) v = e.w[((long long)co * e.cin + ci) * e.taps + tap];
-    } else {
-      const int co = (int)(idx % e.pad_to);
-      const long long t = idx / e.pad_to;
-      const int tapd = (int)(t % e.taps), ci = (int)(t / e.taps);
-      if (co < e.cout) v = e.w[((long long)co * e.cin + ci) * e.taps + (e.taps - 1 - tapd)];
-    }
-    if (e.dtype == DV_BF16) ((bf16*)e.out)[idx] = (bf16)v;
-    else ((float*)e.out)[idx] = v;
-  }
+  for (int t = blockIdx.x; t < pack_tiles(e); t += gridDim.x) pack_tile(e, t, sm);
 }
 
 template <typename T>
@@ -1678,8 +1704,8 @@ extern "C" int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, lon
                                             void* stream) {
   DV_REQUIRE(table && n >= 0 && n <= 65535, "bad table");
   if (n == 0 || max_elems <= 0) return DV_OK;
-  long long bx = (max_elems + 255) / 256;
-  if (bx > 256) bx = 256;
+  long long bx = (max_elems + 4095) / 4096;
+  if (bx > 128) bx = 128;
   pack_weight_batched_kernel<<<dim3((unsigned)bx, (unsigned)n), 256, 0, (hipStream_t)stream>>>(table);
   return check_launch("pack_conv_weights_batched");
 }
@@ -1702,15 +1728,15 @@ extern "C" int dv_pack_conv_weight(int dtype, const float* w, void* out, int cou
                                    int ksize, int pad_to, int mode, void* stream) {
   DV_REQUIRE(w && out, "null pointer");
   DV_REQUIRE(mode == 0 ? pad_to >= cin : pad_to >= cout, "pad_to too small");
-  const int taps = ksize * ksize;
-  long long total = mode == 0 ? (long long)cout * taps * pad_to : (long long)cin * taps * pad_to;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 8192) blocks = 8192;
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == DV_F32)
-    pack_weight_kernel<float><<<blocks, 256, 0, st>>>(w, (float*)out, cout, cin, taps, pad_to, mode);
-  else
-    pack_weight_kernel<bf16><<<blocks, 256, 0, st>>>(w, (bf16*)out, cout, cin, taps, pad_to, mode);
+  DV_REQUIRE(mode != 0 || (long long)cin * ksize * ksize <= PACK_LDS, "cin * k * k too large");
+  DV_REQUIRE(mode == 0 || (long long)cout * ksize * ksize <= PACK_LDS, "cout * k * k too large");
+  DvPackEntry e;
+  e.w = w; e.out = out; e.dtype = dtype; e.cout = cout; e.cin = cin; e.taps = ksize * ksize;
+  e.pad_to = pad_to; e.mode = mode;
+  const int rows = mode == 0 ? cout : cin;
+  int blocks = rows < 256 ? rows : 256;
+  if (blocks < 1) return DV_OK;
+  pack_weight_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(e);
   return check_launch("pack_conv_weight");
 }
 

@@ -36,15 +36,33 @@ class KernelTimer:
         e.record()
         self.records.append((name, flops, nbytes, s, e))
 
+    def overhead_ms(self, n=32):
+        """Median elapsed time of an EMPTY start/end event pair recorded the
+        same way (after the spin): the fixed cost the event brackets add to
+        every timed launch, subtracted in summary()."""
+        pairs = []
+        for _ in range(n):
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(self.SPIN_CYCLES)
+            s.record()
+            e.record()
+            pairs.append((s, e))
+        torch.cuda.synchronize()
+        v = sorted(s.elapsed_time(e) for s, e in pairs)
+        return v[len(v) // 2]
+
     def summary(self):
         torch.cuda.synchronize()
+        ovh = self.overhead_ms()
         out = {}
         for name, fl, nb, s, e in self.records:
             d = out.setdefault(name, dict(count=0, flops=0.0, bytes=0.0, ms=0.0))
             d["count"] += 1
             d["flops"] += fl
             d["bytes"] += nb
-            d["ms"] += s.elapsed_time(e)
+            d["ms"] += max(s.elapsed_time(e) - ovh, 1e-4)
+        self.event_overhead_ms = ovh
         return out
 
 
@@ -241,6 +259,8 @@ class PackCache:
         self._table_key = None
 
     def lookup(self, weight, w, dtype, cout, cin, k, pad_to, mode):
+        if (cin if mode == 0 else cout) * k * k > 8192:  # PACK_LDS of dv_conv.hip
+            raise _lib.DVError(f"weight ({cout}, {cin}, {k}, {k}) too large for the packer")
         key = (weight.data_ptr(), tuple(weight.shape), dtype, pad_to, mode)
         e = self.entries.get(key)
         if e is not None and e["epoch"] == self.epoch and e["version"] == weight._version:

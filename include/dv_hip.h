@@ -74,7 +74,9 @@ int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix,
 
 /* f32 torch weight (cout, cin, 1, k, k) -> packed `dtype`
  *   mode 0 (forward):  out[co][tap][ci_pad]          (ci >= cin zero)
- *   mode 1 (dgrad):    out[ci][tap'][co_pad] = w[co][ci][k*k-1-tap']      */
+ *   mode 1 (dgrad):    out[ci][tap'][co_pad] = w[co][ci][k*k-1-tap']
+ * LDS-staged (coalesced both ways); needs cin*k*k (mode 0) or cout*k*k
+ * (mode 1) <= 8192.                                                        */
 int dv_pack_conv_weight(int dtype, const float* w, void* out, int cout, int cin, int ksize,
                         int pad_to, int mode, void* stream);
 
