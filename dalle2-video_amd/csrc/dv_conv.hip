@@ -1115,6 +1115,146 @@ int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   return check_launch("conv_fwd_stripe");
 }
 
+
+// ---------------------------------------------------------------------------
+// bf16 3x3 forward / dgrad, streamed-weight stripe form (cin % 32 == 0,
+// cout % 64 == 0, W in {8, 16, 32, 64}; the 8x8 / 16x16 / 32x32 stage convs
+// with cin >= 128 and their dgrads): one workgroup = 64 output channels x ONE
+// 128-pixel stage.  The K loop runs over 32-channel half-chunks; per
+// half-chunk the workgroup stages (a) its 64 channels' weights for all nine
+// taps (64 x 288 bf16) and (b) the X window of the stage for those 32
+// channels (one window serves all nine taps, as in the resident form).  Per
+// CU that is ~52 KB of L2 traffic per 1152 MFMA cycles, against ~94 B/clk for
+// the 64x128 implicit-GEMM tile it replaces.  Rows padded to 592 B (weights)
+// / 80 B (window): ds_read_b128 conflict-free, immediate tap offsets.
+// Register-staged, double-buffered.  8 waves: 4 pixel tiles x 2 channel
+// halves, one 32x32 accumulator each.
+// ---------------------------------------------------------------------------
+bool stripe_geom(int h, int w, int& seg, int& nseg);
+
+constexpr int F2_WP = 592;  // weight row pitch: 9 taps x 32 ci bf16 + 16 B
+constexpr int F2_XP = 80;   // window pixel pitch: 32 ci bf16 + 16 B
+
+template <int W>
+__global__ __launch_bounds__(512) void conv_fwd_stripe2_kernel(ConvFwdArgs<bf16> p, int seg, int nseg) {
+  constexpr int WP = W + 2;
+  constexpr int NWIN = W == 8 ? 200 : (128 / W + 2) * WP;   // window pixels (max over H)
+  constexpr int WB = 64 * F2_WP, XB = NWIN * F2_XP;
+  constexpr int BUF = WB + XB;
+  constexpr int NLW = (64 * 36 + 511) / 512;                // weight 16-B chunks per thread
+  constexpr int NLX = (NWIN * 4 + 511) / 512;               // window 16-B chunks per thread
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pt = wave & 3, ch = wave >> 2;
+  const int co0 = blockIdx.y * 64;
+  const long long m0 = (long long)blockIdx.x * 128;
+  const int HW = p.H * W, segrows = (seg + 2) * WP;
+  const int y0 = nseg > 1 ? 0 : (int)((m0 % HW) / W);
+
+  // static load slots: weights (row, 16-B chunk of 36), window (pixel, chunk of 4)
+  int w_src[NLW], w_dst[NLW];
+#pragma unroll
+  for (int i = 0; i < NLW; ++i) {
+    const int idx = tid + 512 * i;
+    const int row = idx / 36, c = idx - row * 36;  // c: tap = c / 4, 8-ci group = c % 4
+    const bool ok = row < 64;
+    w_src[i] = ok ? (co0 + row) * p.K + (c >> 2) * p.cin + (c & 3) * 8 : -1;
+    w_dst[i] = row * F2_WP + c * 16;
+  }
+  int x_off[NLX], x_ry[NLX], x_dst[NLX], x_c[NLX];
+#pragma unroll
+  for (int i = 0; i < NLX; ++i) {
+    const int idx = tid + 512 * i;
+    const int px = idx >> 2, c = idx & 3;
+    const int sg = px / segrows, rem = px - sg * segrows;
+    const int ry = rem / WP, rx = rem - ry * WP;
+    const bool ok = px < NWIN && sg < nseg && rx >= 1 && rx <= W;
+    x_ry[i] = ok ? ry - 1 : -(1 << 20);
+    x_off[i] = sg * seg * W + (ry - 1) * W + (rx - 1);
+    x_dst[i] = px < NWIN ? px * F2_XP + c * 16 : -1;
+    x_c[i] = c * 8;
+  }
+  u32x4 rw[NLW], rx_[NLX];
+  auto load = [&](int hc) {
+    const int ci = hc * 32;
+    const bool first = ci < p.c0;
+    const bf16* xb = first ? p.x0 + ci : p.x1 + (ci - p.c0);
+    const int ld = first ? p.ld0 : p.ld1;
+#pragma unroll
+    for (int i = 0; i < NLW; ++i)
+      if (w_src[i] >= 0) rw[i] = *(const u32x4*)(p.w + w_src[i] + ci);
+#pragma unroll
+    for (int i = 0; i < NLX; ++i) {
+      const bool in = (unsigned)(y0 + x_ry[i]) < (unsigned)p.H;
+      rx_[i] = in ? *(const u32x4*)(xb + (m0 + x_off[i]) * ld + x_c[i]) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+    char* b = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < NLW; ++i)
+      if (w_src[i] >= 0) *(u32x4*)(b + w_dst[i]) = rw[i];
+#pragma unroll
+    for (int i = 0; i < NLX; ++i)
+      if (x_dst[i] >= 0) *(u32x4*)(b + WB + x_dst[i]) = rx_[i];
+  };
+
+  const int r = lane & 31, h = lane >> 5;
+  const int px = pt * 32 + r;
+  const int sl = px / (seg * W), rl = px - sl * seg * W;
+  const int wrow = sl * segrows + (rl / W) * WP + rl % W;
+  const int aofs = (ch * 32 + r) * F2_WP + h * 16;
+  const int bofs = WB + wrow * F2_XP + h * 16;
+
+  f32x16 acc[1][1];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[0][0][e] = 0.f;
+  const int nhc = p.cin / 32;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int hc = 0; hc < nhc; ++hc) {
+    if (hc + 1 < nhc) load(hc + 1);
+    const char* b = smem + (hc & 1) * BUF;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      const int toff = ((d / 3) * WP + (d % 3)) * F2_XP;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const u32x4 av = *(const u32x4*)(b + aofs + (d * 32 + ks * 16) * 2);
+        const u32x4 bv = *(const u32x4*)(b + bofs + toff + ks * 32);
+        acc[0][0] = Mma<bf16>::run(av, bv, acc[0][0]);
+      }
+    }
+    if (hc + 1 < nhc) store((hc + 1) & 1);
+    __syncthreads();
+  }
+  conv_epilogue<bf16, 1, 1>(p, acc, m0 + pt * 32, co0 + ch * 32, r, h);
+}
+
+bool fwd_stripe2_ok(long long M, int h, int w, int cin, int c0, bool split, int cout, int ks, int& seg,
+                    int& nseg) {
+  if (ks != 3 || cin % 32 || (split && c0 % 32) || cout % 64 || M % 128 || !stripe_geom(h, w, seg, nseg))
+    return false;
+  // measured against the glds implicit GEMM (tools/ab_fwd.sh): the streamed
+  // stripe wins on the whole-frame windows of the 8x8 stage and on the
+  // smaller 16x16 convs; at W >= 32 the deep-ring glds tiles win
+  return w == 8 || (w == 16 && (long long)cin * cout <= 256 * 256);
+}
+
+int launch_fwd_stripe2(const ConvFwdArgs<bf16>& a, int seg, int nseg, hipStream_t st) {
+  dim3 grid((unsigned)(a.M / 128), a.cout / 64);
+  switch (a.W) {
+    case 64: conv_fwd_stripe2_kernel<64><<<grid, 512, 0, st>>>(a, seg, nseg); break;
+    case 32: conv_fwd_stripe2_kernel<32><<<grid, 512, 0, st>>>(a, seg, nseg); break;
+    case 16: conv_fwd_stripe2_kernel<16><<<grid, 512, 0, st>>>(a, seg, nseg); break;
+    default: conv_fwd_stripe2_kernel<8><<<grid, 512, 0, st>>>(a, seg, nseg); break;
+  }
+  return check_launch("conv_fwd_stripe2");
+}
+
 // tile choice for the glds path (mirrored by ops.conv_tile for kernel naming)
 inline void glds_tile(long long M, int cout, int& bm, int& bn) {
   bn = cout <= 64 ? 64 : 128;
@@ -1136,6 +1276,12 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
   if (a.M == 0 || cout == 0) return DV_OK;
   if constexpr (sizeof(T) == 2) {
     if (fwd_stripe_ok(a.M, h, wd, cin, x1 != nullptr, cout, ks, ld0)) return launch_fwd_stripe(a, st);
+    int seg, nseg;
+    static const bool no_s2 = getenv("DV_NO_STRIPE2") != nullptr;  // A/B switch for profiling
+    if (!no_s2 &&
+        fwd_stripe2_ok(a.M, h, wd, cin, a.c0, x1 != nullptr, cout, ks, seg, nseg) &&
+        a.M * std::max(ld0, x1 ? ld1 : 0) < (1ll << 31))
+      return launch_fwd_stripe2(a, seg, nseg, st);
     const long long maxld = ld0 > (x1 ? ld1 : 0) ? ld0 : ld1;
     if (cin % 64 == 0 && a.c0 % 64 == 0 && a.M * maxld < (1ll << 31)) {
       int bm, bn;
@@ -1579,10 +1725,14 @@ bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout
 }
 
 // split count: ~256 workgroups (one per CU: the stage ring takes up to 112 KB of LDS)
-inline void stripe_split(int nstages, int grid_xy, int& sps, int& S) {
+// split count: ~256 workgroups (one per CU: the stage ring takes up to 147 KB
+// of LDS).  Capping the splits by stages or by partial bytes was measured
+// slower on every Cfg2 shape (tools/ab_fwd.sh): occupancy wins.
+inline void stripe_split(int nstages, int grid_xy, long long grad_floats, int& sps, int& S) {
+  (void)grad_floats;
   long long want = 256 / grid_xy;
-  if (want < 1) want = 1;
   if (want > nstages) want = nstages;
+  if (want < 1) want = 1;
   sps = (int)((nstages + want - 1) / want);
   S = (nstages + sps - 1) / sps;
 }
@@ -1590,7 +1740,7 @@ inline void stripe_split(int nstages, int grid_xy, int& sps, int& S) {
 long long wgrad_stripe_ws(int nf, int h, int w, int cin, int cout, int ks) {
   const int nstages = (int)((long long)nf * h * w / 128);
   int sps, S;
-  stripe_split(nstages, (cout / 64) * (cin / 64), sps, S);
+  stripe_split(nstages, (cout / 64) * (cin / 64), (long long)cout * ks * ks * cin, sps, S);
   return (long long)S * cout * ((long long)ks * ks * cin + 1);
 }
 
@@ -1605,7 +1755,7 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   if (ks == 3) stripe_geom(h, w, a.seg, a.nseg);
   a.nstages = (int)((long long)nf * h * w / 128);
   int S;
-  stripe_split(a.nstages, (cout / 64) * (cin / 64), a.stages_per_split, S);
+  stripe_split(a.nstages, (cout / 64) * (cin / 64), (long long)cout * a.K, a.stages_per_split, S);
   a.part = ws;
   a.dbpart = db ? ws + (long long)S * cout * a.K : nullptr;
   a.dw = dw; a.db = db; a.acc_w = acc_w; a.acc_b = acc_b;

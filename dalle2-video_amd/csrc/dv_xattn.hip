@@ -163,7 +163,28 @@ __global__ void fold_colsum_kernel(const T* Kt, float* colsum, int nb, int Cp) {
 // ---------------------------------------------------------------------------
 // forward: one wave = 32 tokens (of one batch element)
 // ---------------------------------------------------------------------------
-template <typename T>
+
+// Channel-split mode (CS = 4): the 4 waves of a workgroup share ONE 32-token
+// tile and take every 4th 32-channel tile each, meeting in LDS for the
+// per-token reductions (scores / dP accumulators, LayerNorm sums).  Used when
+// the token count is too small to give every CU a tile of its own (the 8x8
+// and 16x16 stages): 4x the workgroups, 1/4 of each wave's serial chain.
+constexpr int XRS = 18;  // reduction slots per lane
+template <int CS>
+__device__ __forceinline__ void xwave_sum(float* v, int n, float* sh, int cw, int lane) {
+  if (CS == 1) return;
+  __syncthreads();  // the previous use of sh is complete
+  for (int i = 0; i < n; ++i) sh[(cw * XRS + i) * 64 + lane] = v[i];
+  __syncthreads();
+  for (int i = 0; i < n; ++i) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < CS; ++w) t += sh[(w * XRS + i) * 64 + lane];
+    v[i] = t;
+  }
+}
+
+template <typename T, int CS>
 __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* out, int ldo,
                                                         long long ntok, long long P, int C,
                                                         const T* Kt, const T* Vt,
@@ -173,12 +194,15 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   // waves tile each batch element's P tokens; lanes past P mirror token P-1
   // (their MFMA columns are independent) and store nothing
+  __shared__ float xred[CS == 1 ? 1 : CS * XRS * 64];
+  const int cw = CS == 1 ? 0 : (threadIdx.x >> 6);  // channel group of this wave
   const long long wpb = (P + 31) / 32;
-  const long long wv = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (wv >= (ntok / P) * wpb) return;
+  const long long wv = CS == 1 ? (long long)blockIdx.x * 4 + (threadIdx.x >> 6) : (long long)blockIdx.x;
+  if (wv >= (ntok / P) * wpb) return;  // uniform per workgroup when CS > 1
   const int b = (int)(wv / wpb);
   const long long tin = (wv % wpb) * 32 + r;
   const bool valid = tin < P;
+  const bool lead = cw == 0;  // stores the per-token outputs shared by the channel groups
   const long long tok = (long long)b * P + (valid ? tin : P - 1);
   const T* xr = x + tok * ldx;
   const int Cp = (C + 31) / 32 * 32;
@@ -189,7 +213,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
   float sx = 0.f, sxx = 0.f;
-  for (int c0 = 0; c0 < Cp; c0 += 2 * VEC) {
+  for (int c0 = 2 * VEC * cw; c0 < Cp; c0 += 2 * VEC * CS) {
     const int c = c0 + h * VEC;
     const u32x4 xv = c < C ? *(const u32x4*)(xr + c) : u32x4{0u, 0u, 0u, 0u};
     const u32x4 kv = *(const u32x4*)(Ktb + (long long)r * Cp + c);
@@ -198,6 +222,18 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
 #pragma unroll
     for (int e = 0; e < VEC; ++e) { sx += f[e]; sxx += f[e] * f[e]; }
     acc = Mma<T>::run(kv, xv, acc);
+  }
+  if (CS > 1) {
+    float v[XRS];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = acc[e];
+    v[16] = sx;
+    v[17] = sxx;
+    xwave_sum<CS>(v, XRS, xred, cw, lane);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = v[e];
+    sx = v[16];
+    sxx = v[17];
   }
   sx += __shfl_xor(sx, 32, 64);
   sxx += __shfl_xor(sxx, 32, 64);
@@ -222,11 +258,11 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
 #pragma unroll
     for (int j = 0; j < 4; ++j) { pt[j] = (T)pv[j]; p[4 * m + j] = (float)pt[j]; }
     float pw[4] = {(float)pt[0], (float)pt[1], (float)pt[2], (float)pt[3]};
-    if (valid) st4<T>(pbuf + tok * KP + 8 * m + 4 * h, pw);
+    if (valid && lead) st4<T>(pbuf + tok * KP + 8 * m + 4 * h, pw);
   }
   // ---- o statistics (pass 1), then the normalised output + residual (pass 2) ----
   float so = 0.f, soo = 0.f;
-  for (int ct = 0; ct < Cp; ct += 32) {
+  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
@@ -234,12 +270,18 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
 #pragma unroll
     for (int e = 0; e < 16; ++e) { so += o[e]; soo += o[e] * o[e]; }
   }
+  if (CS > 1) {
+    float v[2] = {so, soo};
+    xwave_sum<CS>(v, 2, xred, cw, lane);
+    so = v[0];
+    soo = v[1];
+  }
   so += __shfl_xor(so, 32, 64);
   soo += __shfl_xor(soo, 32, 64);
   const float mu2 = so / C;
   const float rs2 = rsqrtf(fmaxf(soo / C - mu2 * mu2, 0.f) + eps);
   T* orow = out + tok * ldo;
-  for (int ct = 0; ct < Cp; ct += 32) {
+  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
@@ -256,7 +298,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
       if (valid) st4<T>(orow + c, y);
     }
   }
-  if (h == 0 && valid) *(f32x4*)(stats + tok * 4) = f32x4{mu, rs, mu2, rs2};
+  if (h == 0 && valid && lead) *(f32x4*)(stats + tok * 4) = f32x4{mu, rs, mu2, rs2};
 }
 
 // ---------------------------------------------------------------------------
@@ -266,7 +308,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
 //   (the LN mean correction sum_t mu_t*rs_t*dS_tk' is NOT accumulated here:
 //    it equals (1/C) sum_c R[b][k'][c], the row sums of the R = dS'^T X GEMM)
 // ---------------------------------------------------------------------------
-template <typename T>
+template <typename T, int CS>
 __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, const T* x, int ldx,
                                                         T* dx, int lddx, long long ntok,
                                                         long long P, int C, const T* KtT,
@@ -277,12 +319,15 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   // waves tile each batch element's P tokens; lanes past P mirror token P-1
   // (their MFMA columns are independent) and store nothing
+  __shared__ float xred[CS == 1 ? 1 : CS * XRS * 64];
+  const int cw = CS == 1 ? 0 : (threadIdx.x >> 6);  // channel group of this wave
   const long long wpb = (P + 31) / 32;
-  const long long wv = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (wv >= (ntok / P) * wpb) return;
+  const long long wv = CS == 1 ? (long long)blockIdx.x * 4 + (threadIdx.x >> 6) : (long long)blockIdx.x;
+  if (wv >= (ntok / P) * wpb) return;  // uniform per workgroup when CS > 1
   const int b = (int)(wv / wpb);
   const long long tin = (wv % wpb) * 32 + r;
   const bool valid = tin < P;
+  const bool lead = cw == 0;
   const long long tok = (long long)b * P + (valid ? tin : P - 1);
   const T* xr = x + tok * ldx;
   const T* dyr = dy + tok * lddy;
@@ -302,7 +347,7 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
   }
   // ---- pass A: LN_out backward statistics ----
   float m1 = 0.f, m2 = 0.f;
-  for (int ct = 0; ct < Cp; ct += 32) {
+  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
@@ -322,13 +367,19 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
       }
     }
   }
+  if (CS > 1) {
+    float v[2] = {m1, m2};
+    xwave_sum<CS>(v, 2, xred, cw, lane);
+    m1 = v[0];
+    m2 = v[1];
+  }
   m1 = (m1 + __shfl_xor(m1, 32, 64)) / C;
   m2 = (m2 + __shfl_xor(m2, 32, 64)) / C;
   // ---- pass B: dO (stored) and dP^T = Vt^T . dO^T ----
   f32x16 dp;
 #pragma unroll
   for (int e = 0; e < 16; ++e) dp[e] = 0.f;
-  for (int ct = 0; ct < Cp; ct += 32) {
+  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
@@ -356,6 +407,14 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
     }
     dp = mm_acc_g<T>(VtTb + ct, Cp, dO, dp, r, h);
   }
+  if (CS > 1) {
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = dp[e];
+    xwave_sum<CS>(v, 16, xred, cw, lane);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dp[e] = v[e];
+  }
   // ---- softmax backward (lane-local heads) ----
   f32x16 ds;
   float a1 = 0.f, a2 = 0.f;
@@ -373,14 +432,14 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
       w[j] = rs * d;
       q[j] = j < 3 ? rs2 * p[4 * m + j] : (kp == 3 ? mu2 * rs2 : 0.f);
     }
-    if (valid) st4<T>(dsbuf + tok * KP + 8 * m + 4 * h, w);
-    if (valid) st4<T>(p2buf + tok * KP + 8 * m + 4 * h, q);
+    if (valid && lead) st4<T>(dsbuf + tok * KP + 8 * m + 4 * h, w);
+    if (valid && lead) st4<T>(p2buf + tok * KP + 8 * m + 4 * h, q);
   }
   a1 = (a1 + __shfl_xor(a1, 32, 64)) / C;  // mean_c dxhat
   a2 = (a2 + __shfl_xor(a2, 32, 64)) / C;  // mean_c dxhat*xhat
   // ---- pass C: dXhat^T = KtT . dS^T, LN_in backward + residual ----
   T* dxr = dx + tok * lddx;
-  for (int ct = 0; ct < Cp; ct += 32) {
+  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
     f32x16 dxh;
 #pragma unroll
     for (int e = 0; e < 16; ++e) dxh[e] = 0.f;
@@ -597,11 +656,16 @@ extern "C" int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ld
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C % VEC == 0 && ldx % VEC == 0 && ldo % 4 == 0, "C / strides must be multiples of 16 bytes");
   hipStream_t st = (hipStream_t)stream;
-  const int blocks = (int)(((ntok / P) * ((P + 31) / 32) + 3) / 4);
-  if (dtype == DV_BF16)
-    xattn_fwd_kernel<bf16><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (bf16*)out, ldo, ntok, P, C, (const bf16*)Kt, (const bf16*)Vt, colsum, g2, eps, stats, (bf16*)pbuf);
-  else
-    xattn_fwd_kernel<float><<<blocks, 256, 0, st>>>((const float*)x, ldx, (float*)out, ldo, ntok, P, C, (const float*)Kt, (const float*)Vt, colsum, g2, eps, stats, (float*)pbuf);
+  const long long tiles = (ntok / P) * ((P + 31) / 32);
+  const bool split = tiles < 4096 && C >= 128;  // fewer than 1024 four-wave workgroups
+  const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
+  if (dtype == DV_BF16) {
+    if (split) xattn_fwd_kernel<bf16, 4><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (bf16*)out, ldo, ntok, P, C, (const bf16*)Kt, (const bf16*)Vt, colsum, g2, eps, stats, (bf16*)pbuf);
+    else xattn_fwd_kernel<bf16, 1><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (bf16*)out, ldo, ntok, P, C, (const bf16*)Kt, (const bf16*)Vt, colsum, g2, eps, stats, (bf16*)pbuf);
+  } else {
+    if (split) xattn_fwd_kernel<float, 4><<<blocks, 256, 0, st>>>((const float*)x, ldx, (float*)out, ldo, ntok, P, C, (const float*)Kt, (const float*)Vt, colsum, g2, eps, stats, (float*)pbuf);
+    else xattn_fwd_kernel<float, 1><<<blocks, 256, 0, st>>>((const float*)x, ldx, (float*)out, ldo, ntok, P, C, (const float*)Kt, (const float*)Vt, colsum, g2, eps, stats, (float*)pbuf);
+  }
   return check_launch("xattn_fwd");
 }
 
@@ -615,11 +679,19 @@ extern "C" int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const vo
              p2buf, "null pointer");
   DV_REQUIRE(P > 0 && ntok % P == 0 && C % 8 == 0, "bad shape");
   hipStream_t st = (hipStream_t)stream;
-  const int blocks = (int)(((ntok / P) * ((P + 31) / 32) + 3) / 4);
-  if (dtype == DV_BF16)
-    xattn_bwd_kernel<bf16><<<blocks, 256, 0, st>>>((const bf16*)dy, lddy, (const bf16*)x, ldx, (bf16*)dx, lddx, ntok, P, C, (const bf16*)KtT, (const bf16*)Vt, (const bf16*)VtT, colsum, g2, stats, (const bf16*)pbuf, (bf16*)dobuf, (bf16*)dsbuf, (bf16*)p2buf);
-  else
-    xattn_bwd_kernel<float><<<blocks, 256, 0, st>>>((const float*)dy, lddy, (const float*)x, ldx, (float*)dx, lddx, ntok, P, C, (const float*)KtT, (const float*)Vt, (const float*)VtT, colsum, g2, stats, (const float*)pbuf, (float*)dobuf, (float*)dsbuf, (float*)p2buf);
+  const long long tiles = (ntok / P) * ((P + 31) / 32);
+  const bool split = tiles < 4096 && C >= 128;
+  const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
+#define XB_ARGS(T) (const T*)dy, lddy, (const T*)x, ldx, (T*)dx, lddx, ntok, P, C, (const T*)KtT, \
+    (const T*)Vt, (const T*)VtT, colsum, g2, stats, (const T*)pbuf, (T*)dobuf, (T*)dsbuf, (T*)p2buf
+  if (dtype == DV_BF16) {
+    if (split) xattn_bwd_kernel<bf16, 4><<<blocks, 256, 0, st>>>(XB_ARGS(bf16));
+    else xattn_bwd_kernel<bf16, 1><<<blocks, 256, 0, st>>>(XB_ARGS(bf16));
+  } else {
+    if (split) xattn_bwd_kernel<float, 4><<<blocks, 256, 0, st>>>(XB_ARGS(float));
+    else xattn_bwd_kernel<float, 1><<<blocks, 256, 0, st>>>(XB_ARGS(float));
+  }
+#undef XB_ARGS
   return check_launch("xattn_bwd_tokens");
 }
 

@@ -82,6 +82,10 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0):
     if (dtype_name == "bf16" and ks == 3 and cin == 64 and c0 == cin and cout % 64 == 0
             and w in (32, 64) and h % (128 // w) == 0 and m % 128 == 0 and m * maxld < (1 << 31)):
         return f"conv_fwd_stripe_kernel<{w}>"
+    if (dtype_name == "bf16" and ks == 3 and cin % 32 == 0 and c0 % 32 == 0 and cout % 64 == 0
+            and m % 128 == 0 and m * maxld < (1 << 31) and _stripe_geom_ok(h, w)
+            and (w == 8 or (w == 16 and cin * cout <= 256 * 256))):
+        return f"conv_fwd_stripe2_kernel<{w}>"
     if dtype_name == "bf16" and cin % 64 == 0 and c0 % 64 == 0 and m * maxld < (1 << 31):
         bn = 64 if cout <= 64 else 128
         bm = 256 if bn == 64 else 128
@@ -96,6 +100,17 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0):
         return f"conv_fwd_glds_kernel<{bm},{bn},{nbuf}>"
     bm, bn = conv_tile(m, cout)
     return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"
+
+
+def _stripe_geom_ok(h, w):
+    """Mirror of stripe_geom() in dv_conv.hip (128-pixel stage windows)."""
+    if w not in (8, 16, 32, 64):
+        return False
+    if h * w >= 128:
+        return h % (128 // w) == 0
+    if 128 % (h * w):
+        return False
+    return (128 // (h * w)) * (h + 2) * (w + 2) <= (200 if w == 8 else (128 // w + 2) * (w + 2))
 
 
 def conv_wgrad_name(dtype_name, m, cout, cin, c0, split, ks, h, w, maxld):

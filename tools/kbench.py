@@ -60,6 +60,12 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "one":
         conv_case(64, 64, 64, 64, 64, 3)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "fwd":
+        for c in ((64, 16, 16, 128, 128), (64, 32, 32, 192, 128), (64, 64, 64, 128, 64), (64, 16, 16, 384, 256),
+                  (64, 16, 16, 256, 256), (64, 8, 8, 256, 256), (64, 8, 8, 512, 512), (64, 8, 8, 768, 512),
+                  (64, 32, 32, 128, 128), (64, 8, 8, 512, 256), (64, 16, 16, 256, 128)):
+            conv_case(*c, 3)
+        sys.exit(0)
     gemm_case(4, 16384, 32, 64)
     gemm_case(4, 4096, 32, 128)
     gemm_case(4, 1024, 32, 256)
