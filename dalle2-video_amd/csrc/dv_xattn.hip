@@ -109,23 +109,38 @@ __device__ __forceinline__ float kf(const float* kv, const float* null_kv, int b
 // ---------------------------------------------------------------------------
 // fold: A~, V~ (f32 [nb][C][24]) and the MFMA operand images
 // ---------------------------------------------------------------------------
-__global__ void fold_fwd_kernel(const float* wq, const float* wo, const float* kv,
-                                const float* null_kv, float* at, float* vt, int nb, int C,
-                                float scale) {
-  const long long n = (long long)nb * C * HK;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int k = (int)(i % HK);
-    const long long bc = i / HK;
-    const int c = (int)(bc % C), b = (int)(bc / C);
-    const int h = k / NK, j = k % NK;
-    float sa = 0.f, sv = 0.f;
-    for (int d = 0; d < DH; ++d) {
-      sa += wq[(long long)(h * DH + d) * C + c] * kf(kv, null_kv, b, h, j, d, 0);
-      sv += wo[(long long)c * (NH * DH) + h * DH + d] * kf(kv, null_kv, b, h, j, d, 1);
+// one workgroup per (head, clip): the head's 3 keys / values (null + 2 time
+// tokens) are staged in LDS, every thread owns channels c (Wq columns read
+// coalesced across threads, its Wo row read as 16-B vectors) and produces all
+// three folded columns of both maps
+__global__ __launch_bounds__(256) void fold_fwd_kernel(const float* wq, const float* wo,
+                                                       const float* kv, const float* null_kv,
+                                                       float* at, float* vt, int nb, int C,
+                                                       float scale) {
+  __shared__ float sk[NK][DH], sv[NK][DH];
+  const int h = blockIdx.x, b = blockIdx.y;
+  for (int i = threadIdx.x; i < NK * DH; i += 256) {
+    const int j = i / DH, d = i % DH;
+    sk[j][d] = kf(kv, null_kv, b, h, j, d, 0);
+    sv[j][d] = kf(kv, null_kv, b, h, j, d, 1);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    const float* wor = wo + (long long)c * (NH * DH) + h * DH;
+#pragma unroll 4
+    for (int d = 0; d < DH; d += 4) {
+      const f32x4 w4 = *(const f32x4*)(wor + d);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float q = wq[(long long)(h * DH + d + e) * C + c];
+        a0 += q * sk[0][d + e]; a1 += q * sk[1][d + e]; a2 += q * sk[2][d + e];
+        v0 += w4[e] * sv[0][d + e]; v1 += w4[e] * sv[1][d + e]; v2 += w4[e] * sv[2][d + e];
+      }
     }
-    at[i] = sa * scale;
-    vt[i] = sv;
+    const long long o = ((long long)b * C + c) * HK + h * NK;
+    at[o] = a0 * scale; at[o + 1] = a1 * scale; at[o + 2] = a2 * scale;
+    vt[o] = v0; vt[o + 1] = v1; vt[o + 2] = v2;
   }
 }
 
@@ -569,8 +584,8 @@ __global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, cons
     else dkv[((long long)b * 2 + (j - 1)) * (2 * NH * DH) + part * NH * DH + h * DH + d] = v;
   };
   if (part == 0) {
-    // stage dat[b][:, h*3 .. h*3+2] once (C x 3 floats); then wave w owns 16
-    // head dims, lanes sweep c over coalesced Wq rows, 4 rows in flight
+    // stage dat[b][:, h*3 .. h*3+2] once (C x 3 floats); thread (j, d) owns one
+    // output and sweeps its Wq row as 16-B vectors (no cross-lane reductions)
     extern __shared__ float dsh[];  // 3*C floats
     for (int c = threadIdx.x; c < C; c += 256) {
       const float* dr = datb + (long long)c * HK;
@@ -579,30 +594,20 @@ __global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, cons
       dsh[3 * c + 2] = dr[2];
     }
     __syncthreads();
-    for (int dd = 0; dd < DH / 4; dd += 4) {
-      float s[4][3];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) s[u][0] = s[u][1] = s[u][2] = 0.f;
-      for (int c = lane; c < C; c += 64) {
-        const float a0 = dsh[3 * c], a1 = dsh[3 * c + 1], a2 = dsh[3 * c + 2];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float wv = wq[(long long)(h * DH + w * (DH / 4) + dd + u) * C + c];
-          s[u][0] += a0 * wv;
-          s[u][1] += a1 * wv;
-          s[u][2] += a2 * wv;
-        }
+    const int d = lane, j = w;
+    if (j < NK) {
+      const float* wr = wq + (long long)(h * DH + d) * C;
+      float s0 = 0.f, s1 = 0.f;
+      int c = 0;
+      for (; c + 8 <= C; c += 8) {
+        const f32x4 u = *(const f32x4*)(wr + c), v = *(const f32x4*)(wr + c + 4);
+        s0 += u[0] * dsh[3 * c + j] + u[1] * dsh[3 * (c + 1) + j] + u[2] * dsh[3 * (c + 2) + j] +
+              u[3] * dsh[3 * (c + 3) + j];
+        s1 += v[0] * dsh[3 * (c + 4) + j] + v[1] * dsh[3 * (c + 5) + j] + v[2] * dsh[3 * (c + 6) + j] +
+              v[3] * dsh[3 * (c + 7) + j];
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float t0 = wave_sum(s[u][0]), t1 = wave_sum(s[u][1]), t2 = wave_sum(s[u][2]);
-        if (lane == 0) {
-          const int d = w * (DH / 4) + dd + u;
-          emit(0, d, t0 * scale);
-          emit(1, d, t1 * scale);
-          emit(2, d, t2 * scale);
-        }
-      }
+      for (; c < C; ++c) s0 += wr[c] * dsh[3 * c + j];
+      emit(j, d, (s0 + s1) * scale);
     }
   } else {
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
@@ -627,7 +632,7 @@ int fold_t(const float* wq, const float* wo, const float* kv, const float* null_
            const float* g1, float* at, float* vt, void* Kt, void* KtT, void* Vt, void* VtT,
            float* colsum, int nb, int C, float scale, hipStream_t st) {
   const long long n = (long long)nb * C * HK;
-  fold_fwd_kernel<<<grid_for(n), 256, 0, st>>>(wq, wo, kv, null_kv, at, vt, nb, C, scale);
+  fold_fwd_kernel<<<dim3(NH, nb), 256, 0, st>>>(wq, wo, kv, null_kv, at, vt, nb, C, scale);
   const int Cp = (C + 31) / 32 * 32;
   fold_pack_kernel<T><<<grid_for((long long)nb * KP * Cp), 256, 0, st>>>(at, vt, g1, (T*)Kt, (T*)KtT, (T*)Vt, (T*)VtT, nb, C, Cp);
   fold_colsum_kernel<T><<<nb * KP, 64, 0, st>>>((const T*)Kt, colsum, nb, Cp);
@@ -657,7 +662,7 @@ extern "C" int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ld
   DV_REQUIRE(C % VEC == 0 && ldx % VEC == 0 && ldo % 4 == 0, "C / strides must be multiples of 16 bytes");
   hipStream_t st = (hipStream_t)stream;
   const long long tiles = (ntok / P) * ((P + 31) / 32);
-  const bool split = tiles < 4096 && C >= 128;  // fewer than 1024 four-wave workgroups
+  const bool split = tiles < 1024 && C >= 128;  // fewer than 256 four-wave workgroups otherwise
   const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
   if (dtype == DV_BF16) {
     if (split) xattn_fwd_kernel<bf16, 4><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (bf16*)out, ldo, ntok, P, C, (const bf16*)Kt, (const bf16*)Vt, colsum, g2, eps, stats, (bf16*)pbuf);
@@ -680,7 +685,7 @@ extern "C" int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const vo
   DV_REQUIRE(P > 0 && ntok % P == 0 && C % 8 == 0, "bad shape");
   hipStream_t st = (hipStream_t)stream;
   const long long tiles = (ntok / P) * ((P + 31) / 32);
-  const bool split = tiles < 4096 && C >= 128;
+  const bool split = tiles < 1024 && C >= 128;
   const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
 #define XB_ARGS(T) (const T*)dy, lddy, (const T*)x, ldx, (T*)dx, lddx, ntok, P, C, (const T*)KtT, \
     (const T*)Vt, (const T*)VtT, colsum, g2, stats, (const T*)pbuf, (T*)dobuf, (T*)dsbuf, (T*)p2buf
