@@ -396,7 +396,8 @@ int gn_bwd_t(GnArgs a, hipStream_t st) {
   a.rows_per_block = gn_rows(a, VEC, GN_U, 768);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_reduce_kernel<T, 1><<<g1, 256, 0, st>>>(a);
-  a.rows_per_block = gn_rows(a, VEC, GN_U, 1024);
+  // 165 VGPRs -> 3 waves / SIMD: 768 workgroups are exactly one resident round
+  a.rows_per_block = gn_rows(a, VEC, GN_U, 768);
   dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   gn_apply_kernel<T, 1><<<g2, 256, 0, st>>>(a);
   return check_launch("gn_bwd");

@@ -109,15 +109,16 @@ __device__ __forceinline__ float kf(const float* kv, const float* null_kv, int b
 // ---------------------------------------------------------------------------
 // fold: A~, V~ (f32 [nb][C][24]) and the MFMA operand images
 // ---------------------------------------------------------------------------
-// one workgroup per (head, clip): the head's 3 keys / values (null + 2 time
-// tokens) are staged in LDS, every thread owns channels c (Wq columns read
-// coalesced across threads, its Wo row read as 16-B vectors) and produces all
-// three folded columns of both maps
+// one workgroup per (head, clip, 64-channel block): the head's 3 keys / values
+// (null + 2 time tokens) are staged in LDS; thread (c, dq) sums a quarter of
+// the 64 head dims for channel c (Wq columns read coalesced across threads,
+// its Wo row segment as 16-B vectors) and the quarters meet in LDS
 __global__ __launch_bounds__(256) void fold_fwd_kernel(const float* wq, const float* wo,
                                                        const float* kv, const float* null_kv,
                                                        float* at, float* vt, int nb, int C,
                                                        float scale) {
   __shared__ float sk[NK][DH], sv[NK][DH];
+  __shared__ float part[4][6][64];
   const int h = blockIdx.x, b = blockIdx.y;
   for (int i = threadIdx.x; i < NK * DH; i += 256) {
     const int j = i / DH, d = i % DH;
@@ -125,11 +126,13 @@ __global__ __launch_bounds__(256) void fold_fwd_kernel(const float* wq, const fl
     sv[j][d] = kf(kv, null_kv, b, h, j, d, 1);
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, v0 = 0.f, v1 = 0.f, v2 = 0.f;
+  const int cl = threadIdx.x & 63, dq = threadIdx.x >> 6;
+  const int c = blockIdx.z * 64 + cl;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, v0 = 0.f, v1 = 0.f, v2 = 0.f;
+  if (c < C) {
     const float* wor = wo + (long long)c * (NH * DH) + h * DH;
-#pragma unroll 4
-    for (int d = 0; d < DH; d += 4) {
+#pragma unroll
+    for (int d = 16 * dq; d < 16 * dq + 16; d += 4) {
       const f32x4 w4 = *(const f32x4*)(wor + d);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -138,9 +141,17 @@ __global__ __launch_bounds__(256) void fold_fwd_kernel(const float* wq, const fl
         v0 += w4[e] * sv[0][d + e]; v1 += w4[e] * sv[1][d + e]; v2 += w4[e] * sv[2][d + e];
       }
     }
+  }
+  part[dq][0][cl] = a0; part[dq][1][cl] = a1; part[dq][2][cl] = a2;
+  part[dq][3][cl] = v0; part[dq][4][cl] = v1; part[dq][5][cl] = v2;
+  __syncthreads();
+  if (dq == 0 && c < C) {
+    float t[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) t[k] = part[0][k][cl] + part[1][k][cl] + part[2][k][cl] + part[3][k][cl];
     const long long o = ((long long)b * C + c) * HK + h * NK;
-    at[o] = a0 * scale; at[o + 1] = a1 * scale; at[o + 2] = a2 * scale;
-    vt[o] = v0; vt[o + 1] = v1; vt[o + 2] = v2;
+    at[o] = t[0] * scale; at[o + 1] = t[1] * scale; at[o + 2] = t[2] * scale;
+    vt[o] = t[3]; vt[o + 1] = t[4]; vt[o + 2] = t[5];
   }
 }
 
@@ -632,7 +643,7 @@ int fold_t(const float* wq, const float* wo, const float* kv, const float* null_
            const float* g1, float* at, float* vt, void* Kt, void* KtT, void* Vt, void* VtT,
            float* colsum, int nb, int C, float scale, hipStream_t st) {
   const long long n = (long long)nb * C * HK;
-  fold_fwd_kernel<<<dim3(NH, nb), 256, 0, st>>>(wq, wo, kv, null_kv, at, vt, nb, C, scale);
+  fold_fwd_kernel<<<dim3(NH, nb, (C + 63) / 64), 256, 0, st>>>(wq, wo, kv, null_kv, at, vt, nb, C, scale);
   const int Cp = (C + 31) / 32 * 32;
   fold_pack_kernel<T><<<grid_for((long long)nb * KP * Cp), 256, 0, st>>>(at, vt, g1, (T*)Kt, (T*)KtT, (T*)Vt, (T*)VtT, nb, C, Cp);
   fold_colsum_kernel<T><<<nb * KP, 64, 0, st>>>((const T*)Kt, colsum, nb, Cp);
