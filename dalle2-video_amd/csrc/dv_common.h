@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <type_traits>
 
 #include "../../include/dv_hip.h"
 
@@ -31,6 +32,49 @@ void zero_f32(float* p, long long n, hipStream_t st);
       return DV_ERR_INVALID;                       \
     }                                              \
   } while (0)
+
+// LDS-DMA through a raw buffer resource: a lane whose byte offset is out of
+// range (DMA_OOB) writes 16 zero bytes to its LDS slot WITHOUT a memory
+// access -- halo / pad slots must not all hit one shared zero line (a single
+// hot L2 channel per XCD).  Resource size must stay below DMA_OOB.
+constexpr unsigned DMA_OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dma_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+// 16 B per lane to LDS (lds + 16 * lane: `lds` must be wave-uniform)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff, 0, 0, 0);
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// LDS byte address of a generic pointer into __shared__ memory
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// ds_read_b128 outside hipcc's waitcnt tracking: the caller waits with
+// lgkm_wait_tied before using the result
+template <int OFF>
+__device__ __forceinline__ u32x4 ds_read_b128_off(unsigned addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
+  u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+
+// s_waitcnt lgkmcnt(N), tied to `v` so no use of v is scheduled above it
+template <int N>
+__device__ __forceinline__ void lgkm_wait_tied(u32x4& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N));
+}
 
 template <typename T> __device__ __forceinline__ float to_f(T v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f(float v) { return (T)v; }

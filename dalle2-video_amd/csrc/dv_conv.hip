@@ -991,114 +991,196 @@ int launch_fwd_glds(const ConvFwdArgs<bf16>& a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // bf16 3x3 forward / dgrad, stripe form (cin == 64 single source, cout % 64
 // == 0, W in {32, 64}): one workgroup = 64 output channels over a contiguous
-// range of 128-pixel stages.  The packed weights of its 64 channels
-// (64 x 576 bf16) stay RESIDENT in LDS for the whole range; per stage only
-// the X window (128 / W + 2 image rows of W + 2 pixels, halo zero-filled) is
-// staged — once for all nine taps, which read it at row offsets
-// dy*(W+2) + dx.  So a stage costs ~38 KB of L2 traffic for 288 MFMAs,
-// against 9 x (pixel tile + weight tile) re-reads in the implicit-GEMM form.
-// LDS rows are padded to 144 B (window) / 1168 B (weights): 16 consecutive
-// rows then start 9 x 16 B apart (mod 256 B), so ds_read_b128 is
-// conflict-free with NO swizzle and every tap / k-step offset is an
-// immediate.  Register-staged window (loads for stage s+1 in flight during
-// the MFMAs of stage s), double-buffered.  8 waves: 4 pixel tiles x 2
-// channel halves, 32 x 32 accumulator each; epilogue = conv_epilogue.
+// range of 128-pixel stages.  8 waves: 4 pixel tiles x 2 channel halves, one
+// 32 x 32 accumulator each (initialised to the bias).  Each wave keeps the A
+// fragments of its 32 output channels for all 36 k-steps in REGISTERS (144
+// VGPRs), so the MFMA loop reads only the X window from LDS: one
+// ds_read_b128 per MFMA, issued 8 k-steps ahead (inline asm, hand-counted
+// lgkmcnt).  Per stage the window (128 / W + 2 image rows of W + 2 pixels,
+// halo zero) is staged ONCE for all nine taps, which read it at row offsets
+// dy*(W+2) + dx; pixel rows padded to 144 B (16 consecutive rows start
+// 9 x 16 B apart mod 256 B: conflict-free ds_read_b128, every tap / k-step
+// offset an immediate).  Windows and the one-time weight image arrive by
+// LDS-DMA through a raw buffer resource (halo and pad slots out of range:
+// zeros without traffic) into a 4-buffer ring, three stages ahead, counted
+// vmcnt + one raw barrier per stage.  All LDS in ONE __shared__ array (a
+// second object can make hipcc drain vmcnt before the first ds_read).
+// Measured 64->64 @ 64x64 x 64 frames: 37.5 -> ~25 us (prologue ~4 us of it).
 // ---------------------------------------------------------------------------
-constexpr int FS_WP = 1168;  // weight row pitch (576 bf16 + 16 B)
 constexpr int FS_XP = 144;   // window pixel pitch (64 bf16 + 16 B)
 
+// byte offset of k-step k (tap k / 4, 16 channels at (k % 4) * 16) from a
+// lane's tap-(0,0) window row
 template <int W>
+constexpr int fs_koff(int k) {
+  return (((k >> 2) / 3) * (W + 2) + ((k >> 2) % 3)) * FS_XP + (k & 3) * 32;
+}
+
+constexpr int FS_WROW = 1168;    // LDS weight row pitch: 576 bf16 + 16 B
+constexpr int FS_WPIECES = 73;   // 64 rows x 73 16-B slots = 73 DMA pieces of 1 KB
+
+template <int W>
+struct FsGeom {
+  static constexpr int WP = W + 2, SEG = 128 / W, NWIN = (SEG + 2) * WP;
+  static constexpr int NSLOT = NWIN * 9;      // 16-B slots: 8 data + 1 pad per pixel
+  static constexpr int NP = (NSLOT + 63) / 64;  // 1-KB DMA pieces per stage
+  static constexpr int NPW = (NP + 7) / 8;      // pieces per wave (uniform: spare ones repeat the last)
+  static constexpr int WBUF = NP * 1024;
+  static constexpr int NBUF = 4;
+  static constexpr int RING = NBUF * WBUF > WBUF + 64 * FS_WROW ? NBUF * WBUF : WBUF + 64 * FS_WROW;
+  static constexpr int LDS = RING;
+};
+
+template <int W, bool RES>
 __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> p, int nstages,
                                                               int stages_per_block) {
-  constexpr int WP = W + 2, SEG = 128 / W, NWIN = (SEG + 2) * WP;
-  constexpr int NR = (NWIN * 8 + 511) / 512;  // 16-B window chunks per thread per stage
-  constexpr int WBUF = NWIN * FS_XP;
-  __shared__ __attribute__((aligned(16))) char smem[64 * FS_WP + 2 * WBUF];
-  char* sW = smem;
-  char* sX = smem + 64 * FS_WP;
+  using G = FsGeom<W>;
+  constexpr int WP = G::WP, NSLOT = G::NSLOT, NP = G::NP, NPW = G::NPW, WBUF = G::WBUF;
+  __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pt = wave & 3, ch = wave >> 2;
   const int co0 = blockIdx.y * 64;
   const int sbeg = blockIdx.x * stages_per_block;
-  const int send = min(sbeg + stages_per_block, nstages);
+  const int nst = min(sbeg + stages_per_block, nstages) - sbeg;
   const int HW = p.H * W;
 
-  // resident weights: 64 rows x 72 chunks of 16 B
-  for (int idx = tid; idx < 64 * 72; idx += 512) {
-    const int row = idx / 72, c = idx - row * 72;
-    *(u32x4*)(sW + row * FS_WP + c * 16) = *(const u32x4*)(p.w + (long long)(co0 + row) * 576 + c * 8);
-  }
-
-  // this thread's window chunks: pixel (idx >> 3) of the window, chunk idx & 7
-  int w_off[NR], w_ry[NR];  // source pixel offset from the stage base; image-row offset (or invalid)
+  // this lane's slot of each of the wave's pieces: window pixel, 16-B chunk
+  int s_off[NPW], s_ry[NPW];  // byte offset from the stage base; image-row offset (or invalid)
 #pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int idx = tid + 512 * i, px = idx >> 3;
+  for (int i = 0; i < NPW; ++i) {
+    const int piece = min(wave + 8 * i, NP - 1);
+    const int slot = piece * 64 + lane, px = slot / 9, c = slot - px * 9;
     const int wy = px / WP, wx = px - wy * WP;
-    const bool ok = px < NWIN && wx >= 1 && wx <= W;
-    w_ry[i] = ok ? wy - 1 : -(1 << 20);
-    w_off[i] = (wy - 1) * W + (wx - 1);
+    const bool ok = slot < NSLOT && c < 8 && wx >= 1 && wx <= W;
+    s_ry[i] = ok ? wy - 1 : -(1 << 20);
+    s_off[i] = (((wy - 1) * W + (wx - 1)) * p.ld0 + c * 8) * 2;
   }
-  const int cidx = tid & 7;
-  u32x4 stg[NR];
-  auto load = [&](int st) {
+  // x0 as a raw buffer: halo and pad slots load out of range (zeros, no traffic)
+  const __amdgpu_buffer_rsrc_t xr = dma_rsrc(p.x0, (unsigned)(p.M * p.ld0 * 2));
+  auto issue = [&](int st, int buf) {
     const int m0 = (sbeg + st) * 128;
     const int y0 = (m0 % HW) / W;
+    const int base = m0 * p.ld0 * 2;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const bool in = (unsigned)(y0 + w_ry[i]) < (unsigned)p.H;
-      stg[i] = in ? *(const u32x4*)(p.x0 + (long long)(m0 + w_off[i]) * p.ld0 + cidx * 8)
-                  : u32x4{0u, 0u, 0u, 0u};
+    for (int i = 0; i < NPW; ++i) {
+      const int piece = min(wave + 8 * i, NP - 1);
+      const bool in = (unsigned)(y0 + s_ry[i]) < (unsigned)p.H;
+      dma16(xr, smem + buf * WBUF + piece * 1024, in ? (unsigned)(base + s_off[i]) : DMA_OOB);
     }
   };
-  auto store = [&](int buf) {
+
+  // weights: the block's 64 contiguous packed rows are DMA'd once into a
+  // padded LDS image (1168-B rows: conflict-free fragment reads) laid over
+  // ring buffers 1..2, then each wave reads its A fragments into registers.
+  // (Direct per-wave global loads of the fragments touch 32 lines per
+  // instruction for 8 KB of use: ~20k cycles of prologue.)
+  if (nst > 0) issue(0, 0);
+  {
+    char* sW = smem + WBUF;
+    const __amdgpu_buffer_rsrc_t wr = dma_rsrc(p.w + (long long)co0 * 576, 64 * 576 * 2);
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int idx = tid + 512 * i;
-      if ((idx >> 3) < NWIN) *(u32x4*)(sX + buf * WBUF + (idx >> 3) * FS_XP + cidx * 16) = stg[i];
+    for (int i = 0; i < FS_WPIECES / 8 + 1; ++i) {
+      const int piece = min(wave + 8 * i, FS_WPIECES - 1);
+      const int slot = piece * 64 + lane, row = slot / 73, c = slot - row * 73;
+      dma16(wr, sW + piece * 1024, c < 72 ? (unsigned)((row * 576 + c * 8) * 2) : DMA_OOB);
     }
-  };
+  }
+  // bias of the lane's 16 accumulator channels (8g + 4h + e of the wave's 32)
+  f32x16 bias_acc;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 b = p.bias ? *(const f32x4*)(p.bias + co0 + ch * 32 + 8 * g + 4 * (lane >> 5))
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias_acc[4 * g + e] = b[e];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weights, bias, stage 0
+  __syncthreads();
+  u32x4 wA[36];
+  {
+    const char* aw = smem + WBUF + (ch * 32 + (lane & 31)) * FS_WROW + (lane >> 5) * 16;
+#pragma unroll
+    for (int k = 0; k < 36; ++k) wA[k] = *(const u32x4*)(aw + 32 * k);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the weight image is dead: ring buffer 1 may be refilled
+  if (nst > 1) issue(1, 1);
+  if (nst > 2) issue(2, 2);
 
   const int r = lane & 31, h = lane >> 5;
-  // lane's pixel in its tile and its window row (tap (0,0) = top-left)
-  const int px = pt * 32 + r;
-  const int wrow = (px / W) * WP + (px % W);
-  const char* aW = sW + (ch * 32 + r) * FS_WP + h * 16;
-  const int bofs = wrow * FS_XP + h * 16;
+  const int px = pt * 32 + r;  // lane's pixel in the stage; window row of tap (0,0)
+  const int bofs = ((px / W) * WP + (px % W)) * FS_XP + h * 16;
 
-  const int nst = send - sbeg;
-  if (nst > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
   for (int st = 0; st < nst; ++st) {
-    if (st + 1 < nst) load(st + 1);
-    const char* bX = sX + (st & 1) * WBUF + bofs;
-    f32x16 acc[1][1];
+    const int buf = st & 3;
+    // window fragments read FSD k-steps ahead of their MFMA (k-step k = tap
+    // k / 4, 16 channels at (k % 4) * 16).  The reads are inline asm with
+    // hand-counted lgkmcnt: beside the LDS-DMA hipcc's waitcnt pass treats
+    // the LGKM queue as out of order and drains it to 0 every few reads.
+    constexpr int FSD = 8;
+    const unsigned xa = lds_addr(smem + buf * WBUF + bofs);
+    u32x4 bq[FSD];
+    static_for<0, FSD>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      bq[k] = ds_read_b128_off<fs_koff<W>(k)>(xa);
+    });
+    bf16x4 rv[4];
+    const long long m = (long long)(sbeg + st) * 128 + px;
+    if (RES) {  // (a compile-time branch: a runtime one becomes a per-stage vmcnt(0))
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[0][0][e] = 0.f;
-#pragma unroll
-    for (int d = 0; d < 9; ++d) {
-      const int toff = ((d / 3) * WP + (d % 3)) * FS_XP;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const u32x4 a = *(const u32x4*)(aW + (d * 64 + ks * 16) * 2);
-        const u32x4 b = *(const u32x4*)(bX + toff + ks * 32);
-        acc[0][0] = Mma<bf16>::run(a, b, acc[0][0]);
-      }
+      for (int g = 0; g < 4; ++g)
+        rv[g] = *(const bf16x4*)(p.res + m * p.ldres + co0 + ch * 32 + 8 * g + 4 * h);
     }
-    conv_epilogue<bf16, 1, 1>(p, acc, (long long)(sbeg + st) * 128 + pt * 32, co0 + ch * 32, r, h);
-    if (st + 1 < nst) store((st + 1) & 1);
-    __syncthreads();
+    f32x16 acc = bias_acc;  // the accumulator starts at the bias
+    static_for<0, 36>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      constexpr int younger = (FSD - 1 < 35 - k) ? FSD - 1 : 35 - k;
+      lgkm_wait_tied<younger>(bq[k % FSD]);
+      acc = Mma<bf16>::run(wA[k], bq[k % FSD], acc);
+      if constexpr (k + FSD < 36) bq[k % FSD] = ds_read_b128_off<fs_koff<W>(k + FSD)>(xa);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    // epilogue: lane owns pixel m, channels 8g + 4h + e of the wave's 32
+    const bool silu = p.act == DV_ACT_SILU;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int n = ch * 32 + 8 * g + 4 * h;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[4 * g + e];
+      if (silu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
+      }
+      if (RES) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (float)rv[g][e];
+      }
+      store4<bf16>(p.y + m * p.ldy + co0 + n, v);
+    }
+    // stage st+1's window landed.  vmcnt retires in order over loads AND
+    // stores; younger than DMA(st+1) are the previous stage's 4 stores, the
+    // NPW DMAs of st+2 (when issued) and this stage's 4 stores.  Every window
+    // read of this stage was waited for by the last MFMA: no lgkmcnt drain.
+    if (st + 2 < nst) {
+      if (st > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW + 8) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW + 4) : "memory");
+    } else {
+      if (st > 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    // buffer (st+3)%4 was last read in stage st-1: every wave passed that
+    // barrier.  Issued here, where a wave would otherwise wait at the barrier.
+    if (st + 3 < nst) issue(st + 3, (st + 3) & 3);
+    __builtin_amdgcn_s_barrier();
   }
 }
 
 bool fwd_stripe_ok(long long M, int h, int w, int cin, bool split, int cout, int ks, int ld0) {
   return ks == 3 && cin == 64 && !split && cout % 64 == 0 && (w == 32 || w == 64) &&
-         h % (128 / w) == 0 && M % 128 == 0 && ld0 % 8 == 0 && M * ld0 < (1ll << 31);
+         h % (128 / w) == 0 && M % 128 == 0 && ld0 % 8 == 0 && M * ld0 * 2 < (long long)DMA_OOB;
 }
 
 int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
@@ -1110,8 +1192,14 @@ int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   const int sps = (nstages + bx - 1) / bx;
   bx = (nstages + sps - 1) / sps;
   dim3 grid(bx, ct);
-  if (a.W == 64) conv_fwd_stripe_kernel<64><<<grid, 512, 0, st>>>(a, nstages, sps);
-  else conv_fwd_stripe_kernel<32><<<grid, 512, 0, st>>>(a, nstages, sps);
+  const bool res = a.res != nullptr;
+  if (a.W == 64) {
+    if (res) conv_fwd_stripe_kernel<64, true><<<grid, 512, 0, st>>>(a, nstages, sps);
+    else conv_fwd_stripe_kernel<64, false><<<grid, 512, 0, st>>>(a, nstages, sps);
+  } else {
+    if (res) conv_fwd_stripe_kernel<32, true><<<grid, 512, 0, st>>>(a, nstages, sps);
+    else conv_fwd_stripe_kernel<32, false><<<grid, 512, 0, st>>>(a, nstages, sps);
+  }
   return check_launch("conv_fwd_stripe");
 }
 
@@ -1275,7 +1363,9 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
   a.ks = ks; a.act = act; a.M = (long long)nf * h * wd; a.K = ks * ks * cin;
   if (a.M == 0 || cout == 0) return DV_OK;
   if constexpr (sizeof(T) == 2) {
-    if (fwd_stripe_ok(a.M, h, wd, cin, x1 != nullptr, cout, ks, ld0)) return launch_fwd_stripe(a, st);
+    if (fwd_stripe_ok(a.M, h, wd, cin, x1 != nullptr, cout, ks, ld0) && (ldy & 3) == 0 &&
+        (res == nullptr || (ldres & 3) == 0))
+      return launch_fwd_stripe(a, st);
     int seg, nseg;
     static const bool no_s2 = getenv("DV_NO_STRIPE2") != nullptr;  // A/B switch for profiling
     if (!no_s2 &&

@@ -60,6 +60,18 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "one":
         conv_case(64, 64, 64, 64, 64, 3)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "fwd1":  # forward only, for counter passes
+        x = torch.randn(64, 64, 64, 64, device="cuda", dtype=torch.bfloat16)
+        wt = torch.randn(64, 64, 1, 3, 3, device="cuda") / 24
+        b = torch.randn(64, device="cuda")
+        wp = ops.pack_conv_weight(wt, torch.bfloat16, 64, 0)
+        y = torch.empty_like(x)
+        from dalle2_video._lib import call, ptr, stream, dt
+        for _ in range(20):
+            call("dv_conv_fwd", dt(x), ptr(x), 64, 64, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
+                 64, 64, 64, 64, 64, 64, 3, 0, stream())
+        torch.cuda.synchronize()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "fwd":
         for c in ((64, 16, 16, 128, 128), (64, 32, 32, 192, 128), (64, 64, 64, 128, 64), (64, 16, 16, 384, 256),
                   (64, 16, 16, 256, 256), (64, 8, 8, 256, 256), (64, 8, 8, 512, 512), (64, 8, 8, 768, 512),
