@@ -352,6 +352,402 @@ __global__ void mqa_finish_kernel(const float* dkp, const float* dvp, T* dkv, in
   }
 }
 
+// ==========================================================================
+// bf16 fast path (gfx950).  Multi-query attention is single-head attention
+// of R = N*H query rows per clip (row j = n*H + head, 64 B each when
+// ldq == H*32) against NKP keys, so:
+//   * forward and dq are query-major: a 512-thread workgroup holds the whole
+//     clip's K and V (NKP x 64 B each, <= 160 KiB) in LDS, staged once, and
+//     each wave streams all key tiles for its 32 query rows with no further
+//     barrier;
+//   * dk/dv is key-major: each wave keeps K/V rows of 32 keys in registers
+//     and streams 32-row Q / dO tiles (double-buffered, one barrier per two
+//     tiles) over a slice of the rows; slices write f32 partials that the
+//     finish kernel sums (no atomics).
+// LDS images use 64-B rows with the 16-B chunk swizzle c ^ ((r >> 2) & 3),
+// which makes both the ds_read_b128 row reads and the ds_read_b64_tr_b16
+// transposed reads conflict-free.  Softmax runs in log2 units (c = scale *
+// log2 e), lse/D are [B][R]; the running max is only raised when a tile's
+// max exceeds it by more than 8 (p <= 256), which skips almost every O
+// rescale.
+namespace fa {
+constexpr int ROW = 64;
+constexpr int NW = 8;  // waves per workgroup
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+__device__ __forceinline__ int img(int r, int c) { return r * ROW + 16 * (c ^ ((r >> 2) & 3)); }
+
+__device__ __forceinline__ s16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+__device__ __forceinline__ bf16x8 cat8(s16x4 a, s16x4 b) {
+  const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+// A operand (rows = MFMA m = the image's columns d, k = image rows R0 + 16s +
+// the accumulator-operand permutation) read transposed from a row image
+__device__ __forceinline__ bf16x8 tr_frag(const char* base, int R0, int s, int lane) {
+  const int h = lane >> 5, q = (lane >> 2) & 3;
+  const int c = 2 * ((lane >> 4) & 1) + ((lane & 3) >> 1), bo = 8 * (lane & 1);
+  const int r0 = R0 + 16 * s + 4 * h + q;
+  return cat8(tr_read(base + img(r0, c) + bo), tr_read(base + img(r0 + 8, c) + bo));
+}
+// A operand from natural rows: lane (r, h) gets row R0 + r, k-step s
+__device__ __forceinline__ bf16x8 row_frag(const char* base, int R0, int s, int r, int h) {
+  return *(const bf16x8*)(base + img(R0 + r, 2 * s + h));
+}
+__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (bf16)x[8 * s + j];
+  return v;
+}
+__device__ __forceinline__ f32x16 mma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float dot8(bf16x8 a, bf16x8 b) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += (float)a[j] * (float)b[j];
+  return s;
+}
+
+// whole-clip K and V images (NKP rows each) into LDS
+__device__ __forceinline__ void stage_kv(const bf16* kb, const bf16* vb, char* sK, char* sV,
+                                         int NKP, int tid) {
+  constexpr int NT = NW * 64, U = 4;
+  const int n = NKP * 4;  // 16-B chunks per image
+  for (int i0 = 0; i0 < n; i0 += NT * U) {
+    u32x4 vk[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * NT + tid;
+      if (i < n) {
+        vk[u] = ((const u32x4*)kb)[i];
+        vv[u] = ((const u32x4*)vb)[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * NT + tid;
+      if (i < n) {
+        const int off = img(i >> 2, i & 3);
+        *(u32x4*)(sK + off) = vk[u];
+        *(u32x4*)(sV + off) = vv[u];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bf16x8 load_row8(const bf16* p, bool ok) {
+  if (!ok) return bf16x8{};
+  return *(const bf16x8*)p;
+}
+
+// grid (ceil(R / 256), B), 512 threads, dynamic LDS 2 * NKP * 64 B
+__global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restrict__ q,
+                                                             const bf16* __restrict__ kp,
+                                                             const bf16* __restrict__ vp,
+                                                             bf16* __restrict__ o, float* lse,
+                                                             int R, int NKP, int nkeys, float c) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sK = smem;
+  char* sV = smem + NKP * ROW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.y;
+  const int row = blockIdx.x * NW * 32 + wave * 32 + r;
+  const bool rok = row < R;
+  const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
+  const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
+  stage_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, tid);
+  __syncthreads();
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int nkt = NKP / 32;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 32;
+    f32x16 s;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s[e] = 0.f;
+    s = mma(row_frag(sK, k0, 0, r, h), qf0, s);
+    s = mma(row_frag(sK, k0, 1, r, h), qf1, s);
+    float mx = -INFINITY;
+    if (k0 + 32 > nkeys) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        s[e] = k0 + acc_row(e, h) < nkeys ? s[e] * c : -INFINITY;
+        mx = fmaxf(mx, s[e]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        s[e] *= c;
+        mx = fmaxf(mx, s[e]);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const bool upd = mx > m + 8.f;
+    if (__ballot(upd)) {
+      const float mn = upd ? mx : m;
+      const float alpha = ex2(m - mn);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] *= alpha;
+      l *= alpha;
+      m = mn;
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      s[e] = ex2(s[e] - m);
+      l += s[e];
+    }
+    acc = mma(tr_frag(sV, k0, 0, lane), pack8(s, 0), acc);
+    acc = mma(tr_frag(sV, k0, 1, lane), pack8(s, 1), acc);
+  }
+  l += __shfl_xor(l, 32, 64);
+  if (rok) {
+    const float inv = 1.f / l;
+    bf16* orow = o + ((long long)b * R + row) * 32;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)(acc[4 * g + e] * inv);
+      *(bf16x4*)(orow + 8 * g + 4 * h) = v;
+    }
+    if (h == 0) lse[(long long)b * R + row] = m + __log2f(l);
+  }
+}
+
+// dq (query-major, as the forward) and D = rowsum(dO * O) for the dk/dv pass
+__global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
+    bf16* __restrict__ dq, float* __restrict__ D, int R, int NKP, int nkeys, float c, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sK = smem;
+  char* sV = smem + NKP * ROW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.y;
+  const int row = blockIdx.x * NW * 32 + wave * 32 + r;
+  const bool rok = row < R;
+  const long long ro = ((long long)b * R + (rok ? row : 0)) * 32;
+  const bf16x8 qf0 = load_row8(q + ro + 8 * h, rok), qf1 = load_row8(q + ro + 16 + 8 * h, rok);
+  const bf16x8 df0 = load_row8(dout + ro + 8 * h, rok), df1 = load_row8(dout + ro + 16 + 8 * h, rok);
+  float dd = dot8(df0, load_row8(o + ro + 8 * h, rok)) + dot8(df1, load_row8(o + ro + 16 + 8 * h, rok));
+  dd += __shfl_xor(dd, 32, 64);
+  const float L2 = rok ? lse[(long long)b * R + row] : 0.f;
+  if (rok && h == 0) D[(long long)b * R + row] = dd;
+  stage_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, tid);
+  __syncthreads();
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  const int nkt = NKP / 32;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 32;
+    f32x16 s, dp;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      s[e] = 0.f;
+      dp[e] = -dd;
+    }
+    s = mma(row_frag(sK, k0, 0, r, h), qf0, s);
+    s = mma(row_frag(sK, k0, 1, r, h), qf1, s);
+    dp = mma(row_frag(sV, k0, 0, r, h), df0, dp);
+    dp = mma(row_frag(sV, k0, 1, r, h), df1, dp);
+    if (k0 + 32 > nkeys) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        s[e] = k0 + acc_row(e, h) < nkeys ? ex2(fmaf(s[e], c, -L2)) * dp[e] : 0.f;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s[e] = ex2(fmaf(s[e], c, -L2)) * dp[e];
+    }
+    acc = mma(tr_frag(sK, k0, 0, lane), pack8(s, 0), acc);
+    acc = mma(tr_frag(sK, k0, 1, lane), pack8(s, 1), acc);
+  }
+  if (rok) {
+    bf16* qrow = dq + ((long long)b * R + row) * 32;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)(acc[4 * g + e] * scale);
+      *(bf16x4*)(qrow + 8 * g + 4 * h) = v;
+    }
+  }
+}
+
+// dk/dv, key-major.  grid (ceil(nkt / 4), S, B); wave w: key tile
+// blockIdx.x * 4 + (w & 3), query-tile parity w >> 2 (two tiles per step).
+// Partials ws[split][b][NKP][64] = (scale * dK | dV) over the split's rows.
+constexpr int TB = 2 * 32 * ROW + 2 * 32 * 4;  // one tile: Q, dO images, L, D
+__global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ D, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
+    float* __restrict__ ws, int R, int NKP, int nkeys, int rows_per_split, float c, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB > 4 * 2 * 16 * 64 * 4 ? 4 * TB : 4 * 2 * 16 * 64 * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.z, split = blockIdx.y;
+  const int kt = blockIdx.x * 4 + (wave & 3), qp = wave >> 2;
+  const bool kvalid = kt < NKP / 32;
+  const long long krow = (long long)b * NKP + (kvalid ? kt * 32 + r : 0);
+  const bf16x8 kf0 = *(const bf16x8*)(kp + krow * 32 + 8 * h), kf1 = *(const bf16x8*)(kp + krow * 32 + 16 + 8 * h);
+  const bf16x8 vf0 = *(const bf16x8*)(vp + krow * 32 + 8 * h), vf1 = *(const bf16x8*)(vp + krow * 32 + 16 + 8 * h);
+  const int r0 = split * rows_per_split;
+  const int r1 = min(R, r0 + rows_per_split);
+  const int nsteps = r1 > r0 ? (r1 - r0 + 63) / 64 : 0;
+  // staging role: thread t -> tile parity t >> 8; u < 128 Q chunk, else dO chunk; u < 32 also L, D
+  const int sp = tid >> 8, u = tid & 255, cu = u & 127, crow = cu >> 2, cch = cu & 3;
+  const bf16* src = (u < 128 ? q : dout) + (long long)b * R * 32;
+  u32x4 cv;
+  float lv = 0.f, dv = 0.f;
+  auto load = [&](int st) {
+    const int rr = r0 + (2 * st + sp) * 32 + crow;
+    const bool ok = rr < r1;
+    cv = ok ? *(const u32x4*)(src + (long long)rr * 32 + cch * 8) : u32x4{0u, 0u, 0u, 0u};
+    if (u < 32) {
+      const int rl = r0 + (2 * st + sp) * 32 + u;
+      lv = rl < r1 ? lse[(long long)b * R + rl] : INFINITY;
+      dv = rl < r1 ? D[(long long)b * R + rl] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+    char* t = smem + (2 * buf + sp) * TB;
+    *(u32x4*)(t + (u < 128 ? 0 : 32 * ROW) + img(crow, cch)) = cv;
+    if (u < 32) {
+      ((float*)(t + 2 * 32 * ROW))[u] = lv;
+      ((float*)(t + 2 * 32 * ROW))[32 + u] = dv;
+    }
+  };
+  f32x16 dk, dvv;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) dk[e] = dvv[e] = 0.f;
+  if (nsteps > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    if (st + 1 < nsteps) load(st + 1);
+    const char* t = smem + (2 * (st & 1) + qp) * TB;
+    const bool tvalid = r0 + (2 * st + qp) * 32 < r1;
+    if (kvalid && tvalid) {
+      const char* sQ = t;
+      const char* sdO = t + 32 * ROW;
+      const float* sL = (const float*)(t + 2 * 32 * ROW);
+      const float* sD = sL + 32;
+      f32x16 s, dp;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 d4 = *(const f32x4*)(sD + 8 * g + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[4 * g + e] = 0.f;
+          dp[4 * g + e] = -d4[e];
+        }
+      }
+      s = mma(row_frag(sQ, 0, 0, r, h), kf0, s);
+      s = mma(row_frag(sQ, 0, 1, r, h), kf1, s);
+      dp = mma(row_frag(sdO, 0, 0, r, h), vf0, dp);
+      dp = mma(row_frag(sdO, 0, 1, r, h), vf1, dp);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 l4 = *(const f32x4*)(sL + 8 * g + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = ex2(fmaf(s[4 * g + e], c, -l4[e]));
+          s[4 * g + e] = p;
+          dp[4 * g + e] *= p;
+        }
+      }
+      dvv = mma(tr_frag(sdO, 0, 0, lane), pack8(s, 0), dvv);
+      dvv = mma(tr_frag(sdO, 0, 1, lane), pack8(s, 1), dvv);
+      dk = mma(tr_frag(sQ, 0, 0, lane), pack8(dp, 0), dk);
+      dk = mma(tr_frag(sQ, 0, 1, lane), pack8(dp, 1), dk);
+    }
+    if (st + 1 < nsteps) store((st + 1) & 1);
+    __syncthreads();
+  }
+  // combine the two parities through LDS, then one partial per split
+  float* red = (float*)smem;
+  if (qp == 1) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      red[((wave & 3) * 32 + e) * 64 + lane] = dk[e];
+      red[((wave & 3) * 32 + 16 + e) * 64 + lane] = dvv[e];
+    }
+  }
+  __syncthreads();
+  if (qp == 0 && kvalid) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      dk[e] += red[((wave & 3) * 32 + e) * 64 + lane];
+      dvv[e] += red[((wave & 3) * 32 + 16 + e) * 64 + lane];
+    }
+    float* w = ws + (((long long)split * gridDim.z + b) * NKP + kt * 32 + r) * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 a, v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = dk[4 * g + e] * scale;
+        v[e] = dvv[4 * g + e];
+      }
+      *(f32x4*)(w + 8 * g + 4 * h) = a;
+      *(f32x4*)(w + 32 + 8 * g + 4 * h) = v;
+    }
+  }
+}
+
+// dkv[b*N + n] = sum over splits of ws[.][b][n + 1]; dnull (+)= sum over b, splits of key 0
+__global__ void mqa_finish_fa_kernel(const float* __restrict__ ws, int S, int B, int N, int NKP,
+                                     bf16* __restrict__ dkv, int lddkv, float* dnull, int accumulate) {
+  const long long n = (long long)B * N * 16;  // float4 groups
+  const long long sstride = (long long)B * NKP * 64;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(i & 15);
+    const long long tok = i >> 4;
+    const int b = (int)(tok / N), key = (int)(tok % N) + 1;
+    const float* p = ws + ((long long)b * NKP + key) * 64 + 4 * g;
+    f32x4 a = *(const f32x4*)p;
+    for (int s = 1; s < S; ++s) a += *(const f32x4*)(p + s * sstride);
+    bf16x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (bf16)a[e];
+    *(bf16x4*)(dkv + tok * lddkv + 4 * g) = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b)
+      for (int sp = 0; sp < S; ++sp) s += ws[sp * sstride + (long long)b * NKP * 64 + threadIdx.x];
+    dnull[threadIdx.x] = accumulate ? dnull[threadIdx.x] + s : s;
+  }
+}
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+// the forward and the backward must take the same path (lse layout/units)
+bool eligible(int dtype, int ldq, int ldo, int H, int NKP) {
+  return dtype == DV_BF16 && ldq == H * DH && ldo == H * DH &&
+         (long long)NKP * 2 * ROW <= 160 * 1024;
+}
+
+int splits(int NKP, int B) {
+  const int nkg = (NKP / 32 + 3) / 4;
+  int s = 256 / (nkg * B);
+  return s < 1 ? 1 : (s > 16 ? 16 : s);
+}
+
+void set_lds(const void* fn, int bytes) {
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+}  // namespace fa
+
 int grid_for(long long work) {
   long long b = (work + 255) / 256;
   if (b > 16384) b = 16384;
@@ -379,21 +775,57 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
   DV_REQUIRE(ldq % 8 == 0 && ldo >= H * DH, "bad strides");
   dim3 grid((N + 31) / 32, H / 4, B);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == DV_BF16)
+  if (fa::eligible(dtype, ldq, ldo, H, NKP)) {
+    const int R = N * H, lds = NKP * 2 * fa::ROW;
+    fa::set_lds((const void*)fa::mqa_fwd_fa_kernel, lds);
+    fa::mqa_fwd_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
+        (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, scale * fa::LOG2E);
+  } else if (dtype == DV_BF16)
     mqa_fwd_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)q, ldq, (const bf16*)kp, (const bf16*)vp, (bf16*)o, ldo, lse, N, NKP, N + 1, H, scale);
   else
     mqa_fwd_kernel<float><<<grid, 256, 0, st>>>((const float*)q, ldq, (const float*)kp, (const float*)vp, (float*)o, ldo, lse, N, NKP, N + 1, H, scale);
   return check_launch("mqa_fwd");
 }
 
+extern "C" int dv_mqa_bwd_ws(int dtype, int ldq, int ldo, int B, int N, int NKP, int H,
+                             long long* floats) {
+  DV_REQUIRE(floats && B > 0 && N > 0 && NKP % 32 == 0, "bad arguments");
+  if (fa::eligible(dtype, ldq, ldo, H, NKP))
+    *floats = (long long)fa::splits(NKP, B) * B * NKP * 64;
+  else
+    *floats = (long long)B * NKP * DH * 2;
+  return DV_OK;
+}
+
 extern "C" int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int ldo,
                           const void* dout, int lddo, const float* lse, const void* kp,
-                          const void* vp, void* dq, int lddq, float* D, float* dkp, float* dvp,
-                          void* dkv, int lddkv, float* dnull, int B, int N, int NKP, int H,
-                          float scale, int accumulate, void* stream) {
-  DV_REQUIRE(q && o && dout && lse && kp && vp && dq && D && dkp && dvp && dkv && dnull, "null pointer");
+                          const void* vp, void* dq, int lddq, float* D, float* ws,
+                          long long ws_floats, void* dkv, int lddkv, float* dnull, int B, int N,
+                          int NKP, int H, float scale, int accumulate, void* stream) {
+  DV_REQUIRE(q && o && dout && lse && kp && vp && dq && D && ws && dkv && dnull, "null pointer");
   DV_REQUIRE(H % 8 == 0 && NKP % 32 == 0, "bad shape");
+  long long need = 0;
+  dv_mqa_bwd_ws(dtype, ldq, ldo, B, N, NKP, H, &need);
+  DV_REQUIRE(ws_floats >= need, "workspace too small (see dv_mqa_bwd_ws)");
   hipStream_t st = (hipStream_t)stream;
+  if (fa::eligible(dtype, ldq, ldo, H, NKP)) {
+    DV_REQUIRE(lddo == H * DH && lddq == H * DH, "bf16 path needs dense dout/dq rows");
+    const int R = N * H, lds = NKP * 2 * fa::ROW, S = fa::splits(NKP, B);
+    const int rps = ((R + S - 1) / S + 63) / 64 * 64;
+    const float c = scale * fa::LOG2E;
+    fa::set_lds((const void*)fa::mqa_dq_fa_kernel, lds);
+    fa::mqa_dq_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
+        (const bf16*)q, (const bf16*)o, (const bf16*)dout, lse, (const bf16*)kp, (const bf16*)vp,
+        (bf16*)dq, D, R, NKP, N + 1, c, scale);
+    fa::mqa_dkdv_fa_kernel<<<dim3((NKP / 32 + 3) / 4, S, B), fa::NW * 64, 0, st>>>(
+        (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP,
+        N + 1, rps, c, scale);
+    fa::mqa_finish_fa_kernel<<<grid_for((long long)B * N * 16), 256, 0, st>>>(
+        ws, S, B, N, NKP, (bf16*)dkv, lddkv, dnull, accumulate);
+    return check_launch("mqa_bwd");
+  }
+  float* dkp = ws;
+  float* dvp = ws + (long long)B * NKP * DH;
   zero_f32(dkp, (long long)B * NKP * DH, st);
   zero_f32(dvp, (long long)B * NKP * DH, st);
   const int hg = 2, hpg = H / hg;

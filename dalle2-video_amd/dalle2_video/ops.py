@@ -855,8 +855,9 @@ class MQAFn(torch.autograd.Function):
         do = do.contiguous()
         dq = torch.empty_like(qc)
         D = torch.empty(B, H, N, dtype=torch.float32, device=dev)
-        dkp = torch.empty(B, NKP, MQA_DH, dtype=torch.float32, device=dev)
-        dvp = torch.empty_like(dkp)
+        need = ctypes.c_longlong(0)
+        call("dv_mqa_bwd_ws", dt(qc), qc.shape[-1], o.shape[-1], B, N, NKP, H, ctypes.byref(need))
+        ws = torch.empty(need.value, dtype=torch.float32, device=dev)
         dkv = torch.empty(B * N, 2 * MQA_DH, dtype=qc.dtype, device=dev)
         sn = _grad_out(ctx.params[0])
         dnull = sn[0] if sn else torch.empty(2, MQA_DH, dtype=torch.float32, device=dev)
@@ -864,7 +865,7 @@ class MQAFn(torch.autograd.Function):
         _launch("attn:mqa_bwd", 8.0 * B * H * N * (N + 1) * MQA_DH, 0,
                 lambda: call("dv_mqa_bwd", dt(qc), ptr(qc), qc.shape[-1], ptr(o), o.shape[-1], ptr(do),
                              do.shape[-1], ptr(lse), ptr(kp), ptr(vp), ptr(dq), dq.shape[-1], ptr(D),
-                             ptr(dkp), ptr(dvp), ptr(dkv), dkv.shape[-1], ptr(dnull), B, N, NKP, H,
+                             ptr(ws), need.value, ptr(dkv), dkv.shape[-1], ptr(dnull), B, N, NKP, H,
                              ctypes_float(scale), int(sn[1]) if sn else 0, stream()))
         return dq, dkv, (None if sn else dnull), None, None, None, None
 

@@ -277,15 +277,22 @@ int dv_xattn_fold_bwd(float* wsR, float* wsV, float* wsQ, float* mcorr,
  * (row 0 null, rows > N zero; NKP = roundup(N+1, 32)).                      */
 int dv_mqa_prep(int dtype, const void* kv, int ldkv, const float* null_kv, void* kp, void* vp,
                 int B, int N, int NKP, void* stream);
-/* o[b][n][h*32+d] = softmax_j(scale * q.k_j) v_j; lse [B][H][N] f32 saved.   */
+/* o[b][n][h*32+d] = softmax_j(scale * q.k_j) v_j; lse f32 saved (opaque to the
+ * caller, B*H*N floats: [B][N*H] log2 units on the bf16 path, [B][H][N]
+ * natural-log otherwise).  bf16 with dense rows (ldq == ldo == H*32) and
+ * NKP <= 1280 runs the whole-clip-K/V-in-LDS kernels.                       */
 int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, const void* vp, void* o, int ldo,
                float* lse, int B, int N, int NKP, int H, float scale, void* stream);
+/* f32 scratch dv_mqa_bwd needs (floats); same path choice as dv_mqa_fwd.     */
+int dv_mqa_bwd_ws(int dtype, int ldq, int ldo, int B, int N, int NKP, int H, long long* floats);
 /* dq, dkv (k at 0, v at 32, stride lddkv) and dnull (+)= (accumulate);
- * D [B][H][N], dkp/dvp [B][NKP][32] f32 are scratch (dkp/dvp pre-zeroed).   */
+ * D (B*H*N floats) and ws (>= dv_mqa_bwd_ws floats, no zeroing needed) are
+ * scratch.  bf16 path: dq (query-major) writes D, dk/dv (key-major) writes
+ * per-slice partials to ws, a finish launch sums them.                      */
 int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int ldo, const void* dout,
                int lddo, const float* lse, const void* kp, const void* vp, void* dq, int lddq,
-               float* D, float* dkp, float* dvp, void* dkv, int lddkv, float* dnull, int B, int N,
-               int NKP, int H, float scale, int accumulate, void* stream);
+               float* D, float* ws, long long ws_floats, void* dkv, int lddkv, float* dnull, int B,
+               int N, int NKP, int H, float scale, int accumulate, void* stream);
 
 #ifdef __cplusplus
 }

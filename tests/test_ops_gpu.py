@@ -154,7 +154,7 @@ def test_cross_attention(dtype, tol, C, T, H):
 
 
 @pytest.mark.parametrize("dtype,tol", DTYPES)
-@pytest.mark.parametrize("N", [64, 96])
+@pytest.mark.parametrize("N", [64, 96, 97, 1024])
 def test_mqa(dtype, tol, N):
     from dalle2_video import ops
 
