@@ -372,7 +372,8 @@ __global__ void mqa_finish_kernel(const float* dkp, const float* dvp, T* dkv, in
 // rescale.
 namespace fa {
 constexpr int ROW = 64;
-constexpr int NW = 8;  // waves per workgroup
+constexpr int NW = 16;  // waves per workgroup (4 per SIMD)
+constexpr int RG = 8;   // 32-row groups per forward / dq workgroup (256 rows)
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 
 __device__ __forceinline__ int img(int r, int c) { return r * ROW + 16 * (c ^ ((r >> 2) & 3)); }
@@ -384,23 +385,51 @@ __device__ __forceinline__ bf16x8 cat8(s16x4 a, s16x4 b) {
   const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
 }
-// A operand (rows = MFMA m = the image's columns d, k = image rows R0 + 16s +
-// the accumulator-operand permutation) read transposed from a row image
-__device__ __forceinline__ bf16x8 tr_frag(const char* base, int R0, int s, int lane) {
+// per-lane byte offsets of the row / transposed fragments inside a 32-row
+// tile; a tile at row k0 (k0 % 16 == 0) adds k0 * ROW (the swizzle only
+// depends on the row within 16)
+struct FragOff {
+  int row[2];
+  int tr[2][2];
+};
+__device__ __forceinline__ FragOff frag_off(int lane) {
+  const int r = lane & 31, h = lane >> 5, q = (lane >> 2) & 3;
+  const int c = 2 * ((lane >> 4) & 1) + ((lane & 3) >> 1), bo = 8 * (lane & 1);
+  FragOff f;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    f.row[s] = img(r, 2 * s + h);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) f.tr[s][t] = img(16 * s + 8 * t + 4 * h + q, c) + bo;
+  }
+  return f;
+}
+// fragments of a 32-row tile at `base` with addresses computed in place
+__device__ __forceinline__ bf16x8 tr_frag(const char* base, int s, int lane) {
   const int h = lane >> 5, q = (lane >> 2) & 3;
   const int c = 2 * ((lane >> 4) & 1) + ((lane & 3) >> 1), bo = 8 * (lane & 1);
-  const int r0 = R0 + 16 * s + 4 * h + q;
+  const int r0 = 16 * s + 4 * h + q;
   return cat8(tr_read(base + img(r0, c) + bo), tr_read(base + img(r0 + 8, c) + bo));
 }
-// A operand from natural rows: lane (r, h) gets row R0 + r, k-step s
-__device__ __forceinline__ bf16x8 row_frag(const char* base, int R0, int s, int r, int h) {
-  return *(const bf16x8*)(base + img(R0 + r, 2 * s + h));
+__device__ __forceinline__ bf16x8 row_frag(const char* base, int s, int r, int h) {
+  return *(const bf16x8*)(base + img(r, 2 * s + h));
+}
+__device__ __forceinline__ bf16x8 row_at(const char* tile, const FragOff& f, int s) {
+  return *(const bf16x8*)(tile + f.row[s]);
+}
+__device__ __forceinline__ bf16x8 tr_at(const char* tile, const FragOff& f, int s) {
+  return cat8(tr_read(tile + f.tr[s][0]), tr_read(tile + f.tr[s][1]));
+}
+
+__device__ __forceinline__ unsigned cvt_pk(float lo, float hi) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
 }
 __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
-  bf16x8 v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (bf16)x[8 * s + j];
-  return v;
+  const u32x4 v = {cvt_pk(x[8 * s], x[8 * s + 1]), cvt_pk(x[8 * s + 2], x[8 * s + 3]),
+                   cvt_pk(x[8 * s + 4], x[8 * s + 5]), cvt_pk(x[8 * s + 6], x[8 * s + 7])};
+  return __builtin_bit_cast(bf16x8, v);
 }
 __device__ __forceinline__ f32x16 mma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -412,31 +441,38 @@ __device__ __forceinline__ float dot8(bf16x8 a, bf16x8 b) {
   for (int j = 0; j < 8; ++j) s += (float)a[j] * (float)b[j];
   return s;
 }
+// v_max3_f32 without the NaN-canonicalising moves fmaxf costs (scores are finite or -inf)
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) z[e] = 0.f;
+  return z;
+}
 
-// whole-clip K and V images (NKP rows each) into LDS
-__device__ __forceinline__ void stage_kv(const bf16* kb, const bf16* vb, char* sK, char* sV,
-                                         int NKP, int tid) {
-  constexpr int NT = NW * 64, U = 4;
-  const int n = NKP * 4;  // 16-B chunks per image
-  for (int i0 = 0; i0 < n; i0 += NT * U) {
-    u32x4 vk[U], vv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * NT + tid;
-      if (i < n) {
-        vk[u] = ((const u32x4*)kb)[i];
-        vv[u] = ((const u32x4*)vb)[i];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * NT + tid;
-      if (i < n) {
-        const int off = img(i >> 2, i & 3);
-        *(u32x4*)(sK + off) = vk[u];
-        *(u32x4*)(sV + off) = vv[u];
-      }
-    }
+// whole-clip K and V images (NKP rows each) into LDS by LDS-DMA: one 1-KiB
+// piece (16 rows) per wave-instruction, source chunks permuted so the
+// lane-linear write lands in the swizzled image.  Caller waits vmcnt(0) and
+// barriers before reading.
+__device__ __forceinline__ void dma_kv(const bf16* kb, const bf16* vb, char* sK, char* sV, int NKP,
+                                       int wave, int lane) {
+  const __amdgpu_buffer_rsrc_t rk = dma_rsrc(kb, (unsigned)NKP * ROW);
+  const __amdgpu_buffer_rsrc_t rv = dma_rsrc(vb, (unsigned)NKP * ROW);
+  const int np = NKP / 16;
+  const int rr = lane >> 2, slot = lane & 3;
+  for (int i = wave; i < 2 * np; i += NW) {
+    const bool isv = i >= np;
+    const int pc = isv ? i - np : i;
+    const int row = pc * 16 + rr;
+    const unsigned voff = row * ROW + 16 * (slot ^ ((row >> 2) & 3));
+    if (isv)
+      dma16(rv, sV + pc * 1024, voff);
+    else
+      dma16(rk, sK + pc * 1024, voff);
   }
 }
 
@@ -445,7 +481,12 @@ __device__ __forceinline__ bf16x8 load_row8(const bf16* p, bool ok) {
   return *(const bf16x8*)p;
 }
 
-// grid (ceil(R / 256), B), 512 threads, dynamic LDS 2 * NKP * 64 B
+// grid (ceil(R / 256), B), 1024 threads, dynamic LDS 2 * NKP * 64 B.
+// Wave w: 32 query rows (group w & 7) against key half w >> 3; the halves
+// merge (m, l, O) through LDS at the end.  Per key tile: S^T = K Q^T (rows
+// keys, column = this lane's query row), the running max on raw scores
+// (c > 0), p = exp2(c s - m) by one fma, then O^T += V^T P^T with P^T as
+// the B operand straight from the accumulator.
 __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restrict__ q,
                                                              const bf16* __restrict__ kp,
                                                              const bf16* __restrict__ vp,
@@ -455,40 +496,35 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   char* sK = smem;
   char* sV = smem + NKP * ROW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int rg = wave & (RG - 1), kh = wave / RG;
   const int b = blockIdx.y;
-  const int row = blockIdx.x * NW * 32 + wave * 32 + r;
+  dma_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, wave, lane);
+  const int row = blockIdx.x * RG * 32 + rg * 32 + r;
   const bool rok = row < R;
   const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
   const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
-  stage_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, tid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  f32x16 acc;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-  float m = -INFINITY, l = 0.f;
-  const int nkt = NKP / 32;
-  for (int kt = 0; kt < nkt; ++kt) {
+  const FragOff fo = frag_off(lane);
+  f32x16 acc = zero16();
+  float m = -INFINITY, l = 0.f;  // m: running max of c * s (log2 units)
+  const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
+  const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid;
+  for (int kt = kbeg; kt < kend; ++kt) {
     const int k0 = kt * 32;
-    f32x16 s;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) s[e] = 0.f;
-    s = mma(row_frag(sK, k0, 0, r, h), qf0, s);
-    s = mma(row_frag(sK, k0, 1, r, h), qf1, s);
-    float mx = -INFINITY;
+    f32x16 s = zero16();
+    const char* tK = sK + k0 * ROW;
+    s = mma(row_at(tK, fo, 0), qf0, s);
+    s = mma(row_at(tK, fo, 1), qf1, s);
     if (k0 + 32 > nkeys) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        s[e] = k0 + acc_row(e, h) < nkeys ? s[e] * c : -INFINITY;
-        mx = fmaxf(mx, s[e]);
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        s[e] *= c;
-        mx = fmaxf(mx, s[e]);
-      }
+      for (int e = 0; e < 16; ++e)
+        if (k0 + acc_row(e, h) >= nkeys) s[e] = -INFINITY;
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float mx = max3(s[0], s[1], s[2]);
+#pragma unroll
+    for (int e = 3; e < 15; e += 2) mx = max3(mx, s[e], s[e + 1]);
+    mx = max3(mx, s[15], __shfl_xor(max3(mx, s[15], s[15]), 32, 64)) * c;
     const bool upd = mx > m + 8.f;
     if (__ballot(upd)) {
       const float mn = upd ? mx : m;
@@ -500,11 +536,30 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      s[e] = ex2(s[e] - m);
+      s[e] = ex2(fmaf(s[e], c, -m));
       l += s[e];
     }
-    acc = mma(tr_frag(sV, k0, 0, lane), pack8(s, 0), acc);
-    acc = mma(tr_frag(sV, k0, 1, lane), pack8(s, 1), acc);
+    acc = mma(tr_at(sV + k0 * ROW, fo, 0), pack8(s, 0), acc);
+    acc = mma(tr_at(sV + k0 * ROW, fo, 1), pack8(s, 1), acc);
+  }
+  // merge the key halves: half 1 parks (acc, l, m) in LDS (K/V no longer read)
+  __syncthreads();
+  float* red = (float*)smem + rg * 18 * 64;
+  if (kh) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[e * 64 + lane] = acc[e];
+    red[16 * 64 + lane] = l;
+    red[17 * 64 + lane] = m;
+  }
+  __syncthreads();
+  if (kh) return;
+  {
+    const float m1 = red[17 * 64 + lane], mn = fmaxf(m, m1);
+    const float a0 = ex2(m - mn), a1 = ex2(m1 - mn);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = acc[e] * a0 + red[e * 64 + lane] * a1;
+    l = l * a0 + red[16 * 64 + lane] * a1;
+    m = mn;
   }
   l += __shfl_xor(l, 32, 64);
   if (rok) {
@@ -512,16 +567,16 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
     bf16* orow = o + ((long long)b * R + row) * 32;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      bf16x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (bf16)(acc[4 * g + e] * inv);
-      *(bf16x4*)(orow + 8 * g + 4 * h) = v;
+      const u32x2 v = {cvt_pk(acc[4 * g] * inv, acc[4 * g + 1] * inv),
+                       cvt_pk(acc[4 * g + 2] * inv, acc[4 * g + 3] * inv)};
+      *(u32x2*)(orow + 8 * g + 4 * h) = v;
     }
     if (h == 0) lse[(long long)b * R + row] = m + __log2f(l);
   }
 }
 
-// dq (query-major, as the forward) and D = rowsum(dO * O) for the dk/dv pass
+// dq (query-major, as the forward: key halves summed through LDS) and
+// D = rowsum(dO * O) for the dk/dv pass
 __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
@@ -530,8 +585,10 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   char* sK = smem;
   char* sV = smem + NKP * ROW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int rg = wave & (RG - 1), kh = wave / RG;
   const int b = blockIdx.y;
-  const int row = blockIdx.x * NW * 32 + wave * 32 + r;
+  dma_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, wave, lane);
+  const int row = blockIdx.x * RG * 32 + rg * 32 + r;
   const bool rok = row < R;
   const long long ro = ((long long)b * R + (rok ? row : 0)) * 32;
   const bf16x8 qf0 = load_row8(q + ro + 8 * h, rok), qf1 = load_row8(q + ro + 16 + 8 * h, rok);
@@ -539,121 +596,128 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   float dd = dot8(df0, load_row8(o + ro + 8 * h, rok)) + dot8(df1, load_row8(o + ro + 16 + 8 * h, rok));
   dd += __shfl_xor(dd, 32, 64);
   const float L2 = rok ? lse[(long long)b * R + row] : 0.f;
-  if (rok && h == 0) D[(long long)b * R + row] = dd;
-  stage_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, tid);
+  if (rok && h == 0 && kh == 0) D[(long long)b * R + row] = dd;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  f32x16 acc;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-  const int nkt = NKP / 32;
-  for (int kt = 0; kt < nkt; ++kt) {
+  const FragOff fo = frag_off(lane);
+  f32x16 acc = zero16();
+  const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
+  const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid;
+  for (int kt = kbeg; kt < kend; ++kt) {
     const int k0 = kt * 32;
-    f32x16 s, dp;
+    f32x16 s = zero16(), dp = zero16();
+    const char* tK = sK + k0 * ROW;
+    const char* tV = sV + k0 * ROW;
+    s = mma(row_at(tK, fo, 0), qf0, s);
+    dp = mma(row_at(tV, fo, 0), df0, dp);
+    s = mma(row_at(tK, fo, 1), qf1, s);
+    dp = mma(row_at(tV, fo, 1), df1, dp);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      s[e] = 0.f;
-      dp[e] = -dd;
-    }
-    s = mma(row_frag(sK, k0, 0, r, h), qf0, s);
-    s = mma(row_frag(sK, k0, 1, r, h), qf1, s);
-    dp = mma(row_frag(sV, k0, 0, r, h), df0, dp);
-    dp = mma(row_frag(sV, k0, 1, r, h), df1, dp);
+    for (int e = 0; e < 16; ++e) s[e] = ex2(fmaf(s[e], c, -L2)) * (dp[e] - dd);
     if (k0 + 32 > nkeys) {
 #pragma unroll
       for (int e = 0; e < 16; ++e)
-        s[e] = k0 + acc_row(e, h) < nkeys ? ex2(fmaf(s[e], c, -L2)) * dp[e] : 0.f;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) s[e] = ex2(fmaf(s[e], c, -L2)) * dp[e];
+        if (k0 + acc_row(e, h) >= nkeys) s[e] = 0.f;
     }
-    acc = mma(tr_frag(sK, k0, 0, lane), pack8(s, 0), acc);
-    acc = mma(tr_frag(sK, k0, 1, lane), pack8(s, 1), acc);
+    acc = mma(tr_at(tK, fo, 0), pack8(s, 0), acc);
+    acc = mma(tr_at(tK, fo, 1), pack8(s, 1), acc);
   }
+  __syncthreads();
+  float* red = (float*)smem + rg * 16 * 64;
+  if (kh) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[e * 64 + lane] = acc[e];
+  }
+  __syncthreads();
+  if (kh) return;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] += red[e * 64 + lane];
   if (rok) {
     bf16* qrow = dq + ((long long)b * R + row) * 32;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      bf16x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (bf16)(acc[4 * g + e] * scale);
-      *(bf16x4*)(qrow + 8 * g + 4 * h) = v;
+      const u32x2 v = {cvt_pk(acc[4 * g] * scale, acc[4 * g + 1] * scale),
+                       cvt_pk(acc[4 * g + 2] * scale, acc[4 * g + 3] * scale)};
+      *(u32x2*)(qrow + 8 * g + 4 * h) = v;
     }
   }
 }
 
 // dk/dv, key-major.  grid (ceil(nkt / 4), S, B); wave w: key tile
-// blockIdx.x * 4 + (w & 3), query-tile parity w >> 2 (two tiles per step).
+// blockIdx.x * 4 + (w & 3), query-tile parity w >> 2 (four tiles per step).
 // Partials ws[split][b][NKP][64] = (scale * dK | dV) over the split's rows.
-constexpr int TB = 2 * 32 * ROW + 2 * 32 * 4;  // one tile: Q, dO images, L, D
+// Rows past the slice load a clamped row with L = +inf (p = 0), so every
+// step issues the same loads (exact vmcnt accounting, no exec branches).
+constexpr int TB = 2 * 32 * ROW + 2 * 32 * 4;  // one tile: Q, dO images, L, -D
+constexpr int QP = NW / 4;                      // query-tile parities
+constexpr int RED = 2 * 4 * 2 * 16 * 64 * 4;    // parity combine (two parities at a time)
 __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ D, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
     float* __restrict__ ws, int R, int NKP, int nkeys, int rows_per_split, float c, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB > 4 * 2 * 16 * 64 * 4 ? 4 * TB : 4 * 2 * 16 * 64 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * QP * TB > RED ? 2 * QP * TB : RED];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int b = blockIdx.z, split = blockIdx.y;
   const int kt = blockIdx.x * 4 + (wave & 3), qp = wave >> 2;
   const bool kvalid = kt < NKP / 32;
   const long long krow = (long long)b * NKP + (kvalid ? kt * 32 + r : 0);
-  const bf16x8 kf0 = *(const bf16x8*)(kp + krow * 32 + 8 * h), kf1 = *(const bf16x8*)(kp + krow * 32 + 16 + 8 * h);
-  const bf16x8 vf0 = *(const bf16x8*)(vp + krow * 32 + 8 * h), vf1 = *(const bf16x8*)(vp + krow * 32 + 16 + 8 * h);
+  bf16x8 kf0 = *(const bf16x8*)(kp + krow * 32 + 8 * h), kf1 = *(const bf16x8*)(kp + krow * 32 + 16 + 8 * h);
+  bf16x8 vf0 = *(const bf16x8*)(vp + krow * 32 + 8 * h), vf1 = *(const bf16x8*)(vp + krow * 32 + 16 + 8 * h);
   const int r0 = split * rows_per_split;
   const int r1 = min(R, r0 + rows_per_split);
-  const int nsteps = r1 > r0 ? (r1 - r0 + 63) / 64 : 0;
-  // staging role: thread t -> tile parity t >> 8; u < 128 Q chunk, else dO chunk; u < 32 also L, D
+  const int nsteps = r1 > r0 ? (r1 - r0 + 32 * QP - 1) / (32 * QP) : 0;
+  // staging role: thread t -> tile parity t >> 8; u < 128 Q chunk, else dO chunk; u < 32 also L, -D
   const int sp = tid >> 8, u = tid & 255, cu = u & 127, crow = cu >> 2, cch = cu & 3;
   const bf16* src = (u < 128 ? q : dout) + (long long)b * R * 32;
+  const float* lsrc = lse + (long long)b * R;
+  const float* dsrc = D + (long long)b * R;
   u32x4 cv;
-  float lv = 0.f, dv = 0.f;
+  float lv, dv;
+  int lrow;
   auto load = [&](int st) {
-    const int rr = r0 + (2 * st + sp) * 32 + crow;
-    const bool ok = rr < r1;
-    cv = ok ? *(const u32x4*)(src + (long long)rr * 32 + cch * 8) : u32x4{0u, 0u, 0u, 0u};
-    if (u < 32) {
-      const int rl = r0 + (2 * st + sp) * 32 + u;
-      lv = rl < r1 ? lse[(long long)b * R + rl] : INFINITY;
-      dv = rl < r1 ? D[(long long)b * R + rl] : 0.f;
-    }
+    const int rr = r0 + (QP * st + sp) * 32 + crow;
+    cv = *(const u32x4*)(src + (long long)min(rr, r1 - 1) * 32 + cch * 8);
+    lrow = r0 + (QP * st + sp) * 32 + (u & 31);
+    lv = lsrc[min(lrow, r1 - 1)];
+    dv = dsrc[min(lrow, r1 - 1)];
   };
   auto store = [&](int buf) {
-    char* t = smem + (2 * buf + sp) * TB;
+    char* t = smem + (QP * buf + sp) * TB;
     *(u32x4*)(t + (u < 128 ? 0 : 32 * ROW) + img(crow, cch)) = cv;
     if (u < 32) {
-      ((float*)(t + 2 * 32 * ROW))[u] = lv;
-      ((float*)(t + 2 * 32 * ROW))[32 + u] = dv;
+      ((float*)(t + 2 * 32 * ROW))[u] = lrow < r1 ? lv : INFINITY;
+      ((float*)(t + 2 * 32 * ROW))[32 + u] = -dv;
     }
   };
-  f32x16 dk, dvv;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) dk[e] = dvv[e] = 0.f;
+  // retire the K/V fragment loads here so the loop carries no vmcnt for them
+  asm volatile("" : "+v"(kf0), "+v"(kf1), "+v"(vf0), "+v"(vf1));
+  f32x16 dk = zero16(), dvv = zero16();
   if (nsteps > 0) {
     load(0);
     store(0);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int st = 0; st < nsteps; ++st) {
-    if (st + 1 < nsteps) load(st + 1);
-    const char* t = smem + (2 * (st & 1) + qp) * TB;
-    const bool tvalid = r0 + (2 * st + qp) * 32 < r1;
-    if (kvalid && tvalid) {
+    const bool more = st + 1 < nsteps;
+    if (more) load(st + 1);
+    const char* t = smem + (QP * (st & 1) + qp) * TB;
+    if (kvalid) {
       const char* sQ = t;
       const char* sdO = t + 32 * ROW;
       const float* sL = (const float*)(t + 2 * 32 * ROW);
       const float* sD = sL + 32;
-      f32x16 s, dp;
+      f32x16 s = zero16(), dp;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 d4 = *(const f32x4*)(sD + 8 * g + 4 * h);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s[4 * g + e] = 0.f;
-          dp[4 * g + e] = -d4[e];
-        }
+        for (int e = 0; e < 4; ++e) dp[4 * g + e] = d4[e];
       }
-      s = mma(row_frag(sQ, 0, 0, r, h), kf0, s);
-      s = mma(row_frag(sQ, 0, 1, r, h), kf1, s);
-      dp = mma(row_frag(sdO, 0, 0, r, h), vf0, dp);
-      dp = mma(row_frag(sdO, 0, 1, r, h), vf1, dp);
+      s = mma(row_frag(sQ, 0, r, h), kf0, s);
+      dp = mma(row_frag(sdO, 0, r, h), vf0, dp);
+      s = mma(row_frag(sQ, 1, r, h), kf1, s);
+      dp = mma(row_frag(sdO, 1, r, h), vf1, dp);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 l4 = *(const f32x4*)(sL + 8 * g + 4 * h);
@@ -664,30 +728,41 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
           dp[4 * g + e] *= p;
         }
       }
-      dvv = mma(tr_frag(sdO, 0, 0, lane), pack8(s, 0), dvv);
-      dvv = mma(tr_frag(sdO, 0, 1, lane), pack8(s, 1), dvv);
-      dk = mma(tr_frag(sQ, 0, 0, lane), pack8(dp, 0), dk);
-      dk = mma(tr_frag(sQ, 0, 1, lane), pack8(dp, 1), dk);
+      dvv = mma(tr_frag(sdO, 0, lane), pack8(s, 0), dvv);
+      dk = mma(tr_frag(sQ, 0, lane), pack8(dp, 0), dk);
+      dvv = mma(tr_frag(sdO, 1, lane), pack8(s, 1), dvv);
+      dk = mma(tr_frag(sQ, 1, lane), pack8(dp, 1), dk);
     }
-    if (st + 1 < nsteps) store((st + 1) & 1);
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store((st + 1) & 1);
+    }
     __syncthreads();
   }
-  // combine the two parities through LDS, then one partial per split
+  // combine the parities through LDS (3,2 -> 1,0, then 1 -> 0), one partial per split
   float* red = (float*)smem;
-  if (qp == 1) {
+  auto park = [&](int slot) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      red[((wave & 3) * 32 + e) * 64 + lane] = dk[e];
-      red[((wave & 3) * 32 + 16 + e) * 64 + lane] = dvv[e];
+      red[((slot * 4 + (wave & 3)) * 32 + e) * 64 + lane] = dk[e];
+      red[((slot * 4 + (wave & 3)) * 32 + 16 + e) * 64 + lane] = dvv[e];
     }
-  }
+  };
+  auto take = [&](int slot) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      dk[e] += red[((slot * 4 + (wave & 3)) * 32 + e) * 64 + lane];
+      dvv[e] += red[((slot * 4 + (wave & 3)) * 32 + 16 + e) * 64 + lane];
+    }
+  };
+  if (qp >= 2) park(qp - 2);
+  __syncthreads();
+  if (qp < 2) take(qp);
+  __syncthreads();
+  if (qp == 1) park(0);
   __syncthreads();
   if (qp == 0 && kvalid) {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      dk[e] += red[((wave & 3) * 32 + e) * 64 + lane];
-      dvv[e] += red[((wave & 3) * 32 + 16 + e) * 64 + lane];
-    }
+    take(0);
     float* w = ws + (((long long)split * gridDim.z + b) * NKP + kt * 32 + r) * 64;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -704,7 +779,8 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
 }
 
 // dkv[b*N + n] = sum over splits of ws[.][b][n + 1]; dnull (+)= sum over b, splits of key 0
-__global__ void mqa_finish_fa_kernel(const float* __restrict__ ws, int S, int B, int N, int NKP,
+template <int S>
+__global__ void mqa_finish_fa_kernel(const float* __restrict__ ws, int B, int N, int NKP,
                                      bf16* __restrict__ dkv, int lddkv, float* dnull, int accumulate) {
   const long long n = (long long)B * N * 16;  // float4 groups
   const long long sstride = (long long)B * NKP * 64;
@@ -714,12 +790,13 @@ __global__ void mqa_finish_fa_kernel(const float* __restrict__ ws, int S, int B,
     const long long tok = i >> 4;
     const int b = (int)(tok / N), key = (int)(tok % N) + 1;
     const float* p = ws + ((long long)b * NKP + key) * 64 + 4 * g;
-    f32x4 a = *(const f32x4*)p;
-    for (int s = 1; s < S; ++s) a += *(const f32x4*)(p + s * sstride);
-    bf16x4 v;
+    f32x4 v[S];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (bf16)a[e];
-    *(bf16x4*)(dkv + tok * lddkv + 4 * g) = v;
+    for (int s = 0; s < S; ++s) v[s] = *(const f32x4*)(p + s * sstride);
+#pragma unroll
+    for (int s = 1; s < S; ++s) v[0] += v[s];
+    const u32x2 o = {cvt_pk(v[0][0], v[0][1]), cvt_pk(v[0][2], v[0][3])};
+    *(u32x2*)(dkv + tok * lddkv + 4 * g) = o;
   }
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     float s = 0.f;
@@ -741,6 +818,17 @@ int splits(int NKP, int B) {
   const int nkg = (NKP / 32 + 3) / 4;
   int s = 256 / (nkg * B);
   return s < 1 ? 1 : (s > 16 ? 16 : s);
+}
+
+template <int S>
+void launch_finish(int s, int grid, hipStream_t st, const float* ws, int B, int N, int NKP, bf16* dkv,
+                   int lddkv, float* dnull, int accumulate) {
+  if constexpr (S >= 1) {
+    if (s == S)
+      mqa_finish_fa_kernel<S><<<grid, 256, 0, st>>>(ws, B, N, NKP, dkv, lddkv, dnull, accumulate);
+    else
+      launch_finish<S - 1>(s, grid, st, ws, B, N, NKP, dkv, lddkv, dnull, accumulate);
+  }
 }
 
 void set_lds(const void* fn, int bytes) {
@@ -776,7 +864,7 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
   dim3 grid((N + 31) / 32, H / 4, B);
   hipStream_t st = (hipStream_t)stream;
   if (fa::eligible(dtype, ldq, ldo, H, NKP)) {
-    const int R = N * H, lds = NKP * 2 * fa::ROW;
+    const int R = N * H, lds = max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4);
     fa::set_lds((const void*)fa::mqa_fwd_fa_kernel, lds);
     fa::mqa_fwd_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
         (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, scale * fa::LOG2E);
@@ -810,7 +898,7 @@ extern "C" int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int 
   hipStream_t st = (hipStream_t)stream;
   if (fa::eligible(dtype, ldq, ldo, H, NKP)) {
     DV_REQUIRE(lddo == H * DH && lddq == H * DH, "bf16 path needs dense dout/dq rows");
-    const int R = N * H, lds = NKP * 2 * fa::ROW, S = fa::splits(NKP, B);
+    const int R = N * H, lds = max(NKP * 2 * fa::ROW, fa::RG * 16 * 64 * 4), S = fa::splits(NKP, B);
     const int rps = ((R + S - 1) / S + 63) / 64 * 64;
     const float c = scale * fa::LOG2E;
     fa::set_lds((const void*)fa::mqa_dq_fa_kernel, lds);
@@ -820,8 +908,10 @@ extern "C" int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int 
     fa::mqa_dkdv_fa_kernel<<<dim3((NKP / 32 + 3) / 4, S, B), fa::NW * 64, 0, st>>>(
         (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP,
         N + 1, rps, c, scale);
-    fa::mqa_finish_fa_kernel<<<grid_for((long long)B * N * 16), 256, 0, st>>>(
-        ws, S, B, N, NKP, (bf16*)dkv, lddkv, dnull, accumulate);
+    DV_REQUIRE(S >= 1 && S <= 16, "split count out of range");
+    fa::launch_finish<16>(S, grid_for((long long)B * N * 16), st, ws, B, N, NKP, (bf16*)dkv, lddkv,
+                          dnull, accumulate);
+
     return check_launch("mqa_bwd");
   }
   float* dkp = ws;
