@@ -46,6 +46,12 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, unsig
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff, 0, 0, 0);
 }
 
+// as dma16 with a wave-uniform byte offset added to every lane's address
+// (the instruction's SGPR soffset: a per-chunk offset costs no VALU)
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff, (int)soff, 0, 0);
+}
+
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {

@@ -883,14 +883,28 @@ int conv_wgrad_glds(const void* dy, int lddy, const void* x0, int ld0, int c0, c
 //   mode 1 (dgrad):    out[ci][tap'][co_p] <- w[co][ci][taps-1-tap']
 //                      (tile = CT input channels: every co's contiguous
 //                      w[co][ci0:ci0+CT][:] segment is read, then transposed)
+//   modes 2 / 3: modes 0 / 1 with each row 16-channel-chunk-major,
+//                      out[row][c_p / 16][tap][16] (pad % 16 == 0): the 8x8
+//                      frame conv reads one chunk of a row as one contiguous run
+__device__ __forceinline__ void pack_col(int j, int taps, int pad, bool chunked, int& tap, int& c) {
+  if (chunked) {
+    const int ch = j / (taps * 16), rem = j - ch * taps * 16;
+    tap = rem >> 4;
+    c = ch * 16 + (rem & 15);
+  } else {
+    tap = j / pad;
+    c = j - tap * pad;
+  }
+}
 constexpr int PACK_LDS = 8192;   // floats: the largest row / column group accepted
 constexpr int PACK_TILE = 8192;  // floats staged per tile (several rows when they are small)
 
 __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
   const int taps = e.taps, cin = e.cin, cout = e.cout, pad = e.pad_to;
-  if ((long long)(e.mode == 0 ? cin : cout) * taps > PACK_LDS) return;  // rejected on the host
+  const bool fwd = (e.mode & 1) == 0, chunked = (e.mode & 2) != 0;
+  if ((long long)(fwd ? cin : cout) * taps > PACK_LDS) return;  // rejected on the host
   const bool bf = e.dtype == DV_BF16;
-  if (e.mode == 0) {
+  if (fwd) {
     const int row = cin * taps;
     int rt = PACK_TILE / row;
     if (rt < 1) rt = 1;
@@ -902,7 +916,8 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
     const long long ob = (long long)co0 * orow;
     for (int i = threadIdx.x; i < rn * orow; i += 256) {
       const int rl = i / orow, j = i - rl * orow;
-      const int tap = j / pad, ci = j - tap * pad;
+      int tap, ci;
+      pack_col(j, taps, pad, chunked, tap, ci);
       const float v = ci < cin ? sm[rl * row + ci * taps + tap] : 0.f;
       if (bf) ((bf16*)e.out)[ob + i] = (bf16)v;
       else ((float*)e.out)[ob + i] = v;
@@ -921,7 +936,8 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
     const long long ob = (long long)ci0 * orow;
     for (int i = threadIdx.x; i < cn * orow; i += 256) {
       const int cl = i / orow, j = i - cl * orow;
-      const int tapd = j / pad, co = j - tapd * pad;
+      int tapd, co;
+      pack_col(j, taps, pad, chunked, tapd, co);
       const float v = co < cout ? sm[co * seg + cl * taps + (taps - 1 - tapd)] : 0.f;
       if (bf) ((bf16*)e.out)[ob + i] = (bf16)v;
       else ((float*)e.out)[ob + i] = v;
@@ -931,10 +947,10 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
 }
 
 __device__ __forceinline__ int pack_tiles(const DvPackEntry& e) {
-  const int unit = (e.mode == 0 ? e.cin : e.cout) * e.taps;
+  const int unit = ((e.mode & 1) == 0 ? e.cin : e.cout) * e.taps;
   int per = PACK_TILE / unit;
   if (per < 1) per = 1;
-  const int rows = e.mode == 0 ? e.cout : e.cin;
+  const int rows = (e.mode & 1) == 0 ? e.cout : e.cin;
   return (rows + per - 1) / per;
 }
 
@@ -1341,6 +1357,199 @@ int launch_fwd_stripe2(const ConvFwdArgs<bf16>& a, int seg, int nseg, hipStream_
     default: conv_fwd_stripe2_kernel<8><<<grid, 512, 0, st>>>(a, seg, nseg); break;
   }
   return check_launch("conv_fwd_stripe2");
+}
+
+// ---------------------------------------------------------------------------
+// bf16 3x3 forward / dgrad for 8x8 frames (the Unet3D 8x8 stage: mid blocks,
+// stage-3 / up-0 convs and their dgrads; H = W = 8, cin % 16 == 0, cout %
+// 64 == 0, M % 128 == 0; weights packed 16-channel-chunk-major, modes 2 / 3,
+// so a chunk of a weight row is one contiguous 288-B run: with the plain
+// [tap][ci] rows every 16-channel piece was a separate 32-B request and L2
+// moved twice the bytes).  One workgroup = 128 pixels (two frames) x 64
+// output channels, 4 waves; each wave owns 32 pixels x 64 channels (two
+// 32x32 accumulators sharing one window fragment: 1.5 LDS reads per MFMA,
+// against 2 for one accumulator per wave).  K runs over 16-channel chunks:
+// per chunk the block's 64 packed weight rows (9 taps x 16 ci) and the
+// two-frame window (zero halo) arrive by LDS-DMA into a 5-deep ring, four
+// chunks ahead; counted vmcnt + one raw barrier per chunk; no VGPR staging.
+// Window image: 12 pixel slots per window row (10 used), 3 16-B slots per
+// pixel (2 data + pad).  The row pitch 12 makes every residue of the window
+// pixel index mod 16 occur exactly twice among a wave's 32 pixels, and lanes
+// map to pixels (f8_pix) so that each ds_read_b128 16-lane group takes one
+// pixel of each residue: with the odd slot pitch every window read is
+// conflict-free for all nine taps.  Weight rows: 19 slots (odd): conflict-
+// free.  Blocks are ordered so that one XCD works on one output-channel
+// block at a time (its 64 weight rows stay in that XCD's L2).
+// ---------------------------------------------------------------------------
+constexpr int F8_WQ = 12;                                  // window pixel slots per window row
+constexpr int F8_WPIX = 2 * 10 * F8_WQ;                    // two frames
+constexpr int F8_WROW = 19;                                // 16-B slots per weight row
+constexpr int F8_WPIECES = F8_WROW;                        // 64 rows x 19 slots = 19 KiB
+constexpr int F8_XPIECES = (F8_WPIX * 3 + 63) / 64;        // 12
+constexpr int F8_PIECES = F8_WPIECES + F8_XPIECES;         // 31 1-KiB DMA pieces per chunk
+constexpr int F8_NPW = (F8_PIECES + 3) / 4;                // 8 per wave (one repeat)
+constexpr int F8_BUF = F8_PIECES * 1024;
+constexpr int F8_NBUF = 5;                                 // ring depth (155 KiB)
+
+// lane r -> pixel (row * 8 + col) of the wave's 4 x 8 pixel tile: ds_read_b128
+// group {0-3, 12-15, 20-27} takes image rows 0 and 2, the other rows 1 and 3
+__device__ __forceinline__ int f8_pix(int r) {
+  const bool ga = r < 4 || (r >= 12 && r < 16) || (r >= 20 && r < 28);
+  const int a = ga ? (r < 4 ? r : (r < 16 ? r - 8 : r - 12))
+                   : (r < 12 ? r - 4 : (r < 20 ? r - 8 : r - 16));
+  return (2 * (a >> 3) + (ga ? 0 : 1)) * 8 + (a & 7);
+}
+
+__global__ __launch_bounds__(256) void conv_fwd_frame8_kernel(ConvFwdArgs<bf16> p) {
+  __shared__ __attribute__((aligned(1024))) char smem[F8_NBUF * F8_BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int npx = (int)(p.M / 128), nblk = npx * (p.cout / 64);
+  int L = blockIdx.x;
+  if (nblk % 8 == 0) L = (L % 8) * (nblk / 8) + L / 8;  // consecutive blocks share an XCD
+  const int co0 = (L / npx) * 64;
+  const long long m0 = (long long)(L % npx) * 128;
+  const int nch = p.cin / 16;
+
+  // this lane's slot of each of the wave's DMA pieces: a fixed byte offset
+  // (or DMA_OOB); the chunk's offset rides in the instruction's soffset
+  unsigned voff0[F8_NPW], voff1[F8_NPW];
+#pragma unroll
+  for (int i = 0; i < F8_NPW; ++i) {
+    const int k = min(wave + 4 * i, F8_PIECES - 1);
+    voff0[i] = voff1[i] = DMA_OOB;
+    if (k < F8_WPIECES) {
+      // chunk-major packed row (mode 2/3): [cin / 16][9 taps][16]; slot c = 2 tap + half
+      const int slot = k * 64 + lane, row = slot / F8_WROW, c = slot - row * F8_WROW;
+      if (c < 18) voff0[i] = (unsigned)((((long long)co0 + row) * p.K + c * 8) * 2);
+    } else {
+      const int slot = (k - F8_WPIECES) * 64 + lane, px = slot / 3, s = slot - px * 3;
+      const int f = px / 120, rem = px - f * 120, wy = rem / F8_WQ, wx = rem - wy * F8_WQ;
+      if (px < F8_WPIX && s < 2 && wy >= 1 && wy <= 8 && wx >= 1 && wx <= 8) {
+        const long long pix = m0 + f * 64 + (wy - 1) * 8 + (wx - 1);
+        voff0[i] = (unsigned)(pix * p.ld0 * 2 + s * 16);
+        voff1[i] = (unsigned)(pix * p.ld1 * 2 + s * 16);
+      }
+    }
+  }
+  const __amdgpu_buffer_rsrc_t wr = dma_rsrc(p.w, (unsigned)((long long)p.cout * p.K * 2));
+  const __amdgpu_buffer_rsrc_t xr0 = dma_rsrc(p.x0, (unsigned)(p.M * p.ld0 * 2));
+  const __amdgpu_buffer_rsrc_t xr1 = dma_rsrc(p.x1, (unsigned)(p.M * p.ld1 * 2));
+  // piece i of chunk c (i < F8_NPW)
+  auto issue1 = [&](int c, int i) {
+    const int ci0 = c * 16;
+    const bool first = ci0 < p.c0;
+    char* b = smem + (c % F8_NBUF) * F8_BUF;
+    const int k = min(wave + 4 * i, F8_PIECES - 1);
+    if (k < F8_WPIECES) dma16s(wr, b + k * 1024, voff0[i], (unsigned)ci0 * 18);
+    else if (first) dma16s(xr0, b + k * 1024, voff0[i], (unsigned)ci0 * 2);
+    else dma16s(xr1, b + k * 1024, voff1[i], (unsigned)(ci0 - p.c0) * 2);
+  };
+  auto issue = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < F8_NPW; ++i) issue1(c, i);
+  };
+
+  // prologue: chunks 0 .. F8_NBUF-2 in flight, wait for chunk 0
+  issue(0);
+  if (nch > 1) issue(1);
+  if (nch > 2) issue(2);
+  if (nch > 3) issue(3);
+  if (nch > 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * F8_NPW) : "memory");
+  else if (nch > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * F8_NPW) : "memory");
+  else if (nch > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(F8_NPW) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  const int r = lane & 31, h = lane >> 5;
+  const int pix = f8_pix(r);
+  const int wb = (wave >> 1) * 120 + (4 * (wave & 1) + (pix >> 3)) * F8_WQ + (pix & 7);
+  const int bofs = F8_WPIECES * 1024 + (wb * 3 + h) * 16;
+  const int aofs = r * (F8_WROW * 16) + h * 16;
+  // two accumulator chains per channel half (even / odd taps): four
+  // independent MFMA chains, summed in the epilogue
+  f32x16 acc0, acc1, acc2, acc3;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc0[e] = acc1[e] = acc2[e] = acc3[e] = 0.f;
+  for (int c = 0; c < nch; ++c) {
+    const char* b = smem + (c % F8_NBUF) * F8_BUF;
+    // fragments of tap d + 2 are read while tap d multiplies (one wave per
+    // SIMD: the LDS latency is hidden by this wave's own MFMAs)
+    u32x4 bq[3], aq0[3], aq1[3];
+    auto rd = [&](int d, int s) {
+      const int T = ((d / 3) * F8_WQ + (d % 3)) * 48;
+      bq[s] = *(const u32x4*)(b + bofs + T);
+      aq0[s] = *(const u32x4*)(b + aofs + d * 32);
+      aq1[s] = *(const u32x4*)(b + aofs + 32 * F8_WROW * 16 + d * 32);
+    };
+    rd(0, 0);
+    rd(1, 1);
+    // chunk c+4's pieces go out one per tap, in the MFMA shadow: its buffer
+    // was last read in chunk c-1, before the last barrier
+    const bool pre = c + 4 < nch;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      if (d + 2 < 9) rd(d + 2, (d + 2) % 3);
+      if (d & 1) {
+        acc2 = Mma<bf16>::run(aq0[d % 3], bq[d % 3], acc2);
+        acc3 = Mma<bf16>::run(aq1[d % 3], bq[d % 3], acc3);
+      } else {
+        acc0 = Mma<bf16>::run(aq0[d % 3], bq[d % 3], acc0);
+        acc1 = Mma<bf16>::run(aq1[d % 3], bq[d % 3], acc1);
+      }
+      if (d < F8_NPW && pre) issue1(c + 4, d);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // chunk c+1 landed: younger are the pieces of chunks c+2 .. c+4
+    if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * F8_NPW) : "memory");
+    else if (c + 3 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * F8_NPW) : "memory");
+    else if (c + 2 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(F8_NPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e
+  const long long m = m0 + wave * 32 + pix;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int n = co0 + 32 * j + 8 * g + 4 * h;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = j ? acc1[4 * g + e] + acc3[4 * g + e] : acc0[4 * g + e] + acc2[4 * g + e];
+      if (p.bias) {
+        const f32x4 bb = *(const f32x4*)(p.bias + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bb[e];
+      }
+      if (p.act == DV_ACT_SILU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
+      }
+      if (p.res) {
+        float rr[4];
+        load4<bf16>(p.res + m * p.ldres + n, rr);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += rr[e];
+      }
+      store4<bf16>(p.y + m * p.ldy + n, v);
+    }
+  }
+}
+
+bool fwd_frame8_ok(const ConvFwdArgs<bf16>& a, int h, int w) {
+  const long long maxb = (long long)DMA_OOB;
+  return a.ks == 3 && h == 8 && w == 8 && a.cin % 16 == 0 && a.c0 % 16 == 0 && a.cout % 64 == 0 &&
+         a.M % 128 == 0 && a.ld0 % 8 == 0 && a.ld1 % 8 == 0 && (a.ldy & 3) == 0 &&
+         (a.res == nullptr || (a.ldres & 3) == 0) && a.M * a.ld0 * 2 < maxb &&
+         a.M * a.ld1 * 2 < maxb && (long long)a.cout * a.K * 2 < maxb &&
+         ((uintptr_t)a.x0 & 15) == 0 && ((uintptr_t)a.x1 & 15) == 0 && ((uintptr_t)a.w & 15) == 0;
+}
+
+int launch_fwd_frame8(const ConvFwdArgs<bf16>& a, hipStream_t st) {
+  const int nblk = (int)(a.M / 128) * (a.cout / 64);
+  conv_fwd_frame8_kernel<<<nblk, 256, 0, st>>>(a);
+  return check_launch("conv_fwd_frame8");
 }
 
 // tile choice for the glds path (mirrored by ops.conv_tile for kernel naming)
@@ -1894,6 +2103,23 @@ extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const voi
   DV_REQUIRE(false, "unknown dtype");
 }
 
+extern "C" int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
+                            const void* wpack, const float* bias, const void* res, int ldres,
+                            void* y, int ldy, int nf, int cin, int cout, int act, void* stream) {
+  DV_REQUIRE(dtype == DV_BF16, "the 8x8-frame conv is bf16 only");
+  DV_REQUIRE(x0 && wpack && y, "null pointer");
+  DV_REQUIRE(cin > 0 && (!x1 || (c0 > 0 && c0 < cin)), "bad channel split");
+  DV_REQUIRE(ldy >= cout && (!res || ldres >= cout), "bad output stride");
+  ConvFwdArgs<bf16> a;
+  a.x0 = (const bf16*)x0; a.x1 = (const bf16*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0;
+  a.c0 = x1 ? c0 : cin; a.w = (const bf16*)wpack; a.bias = bias; a.res = (const bf16*)res;
+  a.ldres = ldres; a.y = (bf16*)y; a.ldy = ldy; a.H = 8; a.W = 8; a.cin = cin; a.cout = cout;
+  a.ks = 3; a.act = act; a.M = (long long)nf * 64; a.K = 9 * cin;
+  DV_REQUIRE(fwd_frame8_ok(a, 8, 8), "shape/stride outside the 8x8-frame kernel (see dv_hip.h)");
+  if (a.M == 0) return DV_OK;
+  return launch_fwd_frame8(a, (hipStream_t)stream);
+}
+
 extern "C" int dv_conv_wgrad_ws(int dtype, int nf, int h, int w, int cin, int c0, int split,
                                 int cout, int ksize, long long* floats) {
   DV_REQUIRE(floats, "null pointer");
@@ -1967,13 +2193,15 @@ extern "C" int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long
 extern "C" int dv_pack_conv_weight(int dtype, const float* w, void* out, int cout, int cin,
                                    int ksize, int pad_to, int mode, void* stream) {
   DV_REQUIRE(w && out, "null pointer");
-  DV_REQUIRE(mode == 0 ? pad_to >= cin : pad_to >= cout, "pad_to too small");
-  DV_REQUIRE(mode != 0 || (long long)cin * ksize * ksize <= PACK_LDS, "cin * k * k too large");
-  DV_REQUIRE(mode == 0 || (long long)cout * ksize * ksize <= PACK_LDS, "cout * k * k too large");
+  DV_REQUIRE(mode >= 0 && mode <= 3 && (mode < 2 || pad_to % 16 == 0), "bad mode / pad_to");
+  const bool fwd = (mode & 1) == 0;
+  DV_REQUIRE(fwd ? pad_to >= cin : pad_to >= cout, "pad_to too small");
+  DV_REQUIRE(!fwd || (long long)cin * ksize * ksize <= PACK_LDS, "cin * k * k too large");
+  DV_REQUIRE(fwd || (long long)cout * ksize * ksize <= PACK_LDS, "cout * k * k too large");
   DvPackEntry e;
   e.w = w; e.out = out; e.dtype = dtype; e.cout = cout; e.cin = cin; e.taps = ksize * ksize;
   e.pad_to = pad_to; e.mode = mode;
-  const int rows = mode == 0 ? cout : cin;
+  const int rows = fwd ? cout : cin;
   int blocks = rows < 256 ? rows : 256;
   if (blocks < 1) return DV_OK;
   pack_weight_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(e);

@@ -8,6 +8,7 @@ is no torch-compute fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -100,6 +101,18 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0):
         return f"conv_fwd_glds_kernel<{bm},{bn},{nbuf}>"
     bm, bn = conv_tile(m, cout)
     return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"
+
+
+_NO_FRAME8 = bool(os.environ.get("DV_NO_FRAME8"))  # A/B switch: 8x8 convs on dv_conv_fwd
+
+
+def frame8_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf):
+    """Mirror of fwd_frame8_ok (dv_conv.hip): the 8x8-frame conv (dv_conv_fwd8)."""
+    return (not _NO_FRAME8 and x0.dtype == torch.bfloat16 and ksize == 3 and h == 8 and w == 8
+            and cin % 16 == 0 and c0 % 16 == 0 and cout % 64 == 0 and nf % 2 == 0
+            and ld0 % 8 == 0 and ld1 % 8 == 0 and ldy % 4 == 0 and ldres % 4 == 0
+            and nf * 64 * max(ld0, ld1) * 2 < (1 << 31)
+            and x0.data_ptr() % 16 == 0 and (x1 is None or x1.data_ptr() % 16 == 0))
 
 
 def _stripe_geom_ok(h, w):
@@ -274,14 +287,14 @@ class PackCache:
         self._table_key = None
 
     def lookup(self, weight, w, dtype, cout, cin, k, pad_to, mode):
-        if (cin if mode == 0 else cout) * k * k > 8192:  # PACK_LDS of dv_conv.hip
+        if (cin if mode % 2 == 0 else cout) * k * k > 8192:  # PACK_LDS of dv_conv.hip
             raise _lib.DVError(f"weight ({cout}, {cin}, {k}, {k}) too large for the packer")
         key = (weight.data_ptr(), tuple(weight.shape), dtype, pad_to, mode)
         e = self.entries.get(key)
         if e is not None and e["epoch"] == self.epoch and e["version"] == weight._version:
             return e["out"], False
         if e is None:
-            rows = cout if mode == 0 else cin
+            rows = cout if mode % 2 == 0 else cin
             e = dict(out=torch.empty(rows, k * k, pad_to, dtype=dtype, device=weight.device),
                      w=w, meta=(cout, cin, k * k, pad_to, mode))
             self.entries[key] = e
@@ -333,7 +346,7 @@ def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int) -> tor
         if not stale:
             return out
     else:
-        rows = cout if mode == 0 else cin
+        rows = cout if mode % 2 == 0 else cin
         out = torch.empty(rows, k * k, pad_to, dtype=dtype, device=weight.device)
     call("dv_pack_conv_weight", _lib.DV_BF16 if dtype == torch.bfloat16 else _lib.DV_F32,
          ptr(w), ptr(out), cout, cin, k, pad_to, mode, stream())
@@ -352,18 +365,27 @@ class ConvFn(torch.autograd.Function):
         cout, cin_real = weight.shape[0], weight.shape[1]
         if cin_real > cin:
             raise _lib.DVError(f"conv: weight expects {cin_real} input channels, got {cin}")
-        wp = pack_conv_weight(weight, x0.dtype, cin, 0)
         y = torch.empty(nf, h, w, cout, dtype=x0.dtype, device=x0.device)
         ld0 = cl_ld(x0)
         ld1 = cl_ld(x1) if x1 is not None else 0
         ldr = cl_ld(res) if res is not None else 0
         b = None if bias is None else bias.detach().float().contiguous()
         m = nf * h * w
-        _launch(conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
-                              max(ld0, ld1), ksize, h, w), 2.0 * m * cout * cin * ksize * ksize,
-                x0.element_size() * m * (cin + cout),
-                lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b), ptr(res),
-                             ldr, ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE, stream()))
+        flops, nbytes = 2.0 * m * cout * cin * ksize * ksize, x0.element_size() * m * (cin + cout)
+        if frame8_ok(x0, x1, cin, c0 if x1 is not None else cin, cout, ld0, ld1 or ld0, cout,
+                     ldr, ksize, h, w, nf):
+            wp = pack_conv_weight(weight, x0.dtype, cin, 2)
+            _launch("conv_fwd_frame8_kernel", flops, nbytes,
+                    lambda: call("dv_conv_fwd8", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp),
+                                 ptr(b), ptr(res), ldr, ptr(y), cout, nf, cin, cout, ACT_NONE,
+                                 stream()))
+        else:
+            wp = pack_conv_weight(weight, x0.dtype, cin, 0)
+            _launch(conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
+                                  max(ld0, ld1), ksize, h, w), flops, nbytes,
+                    lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b),
+                                 ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE,
+                                 stream()))
         ctx.save_for_backward(x0, x1, weight)
         ctx.params = (weight, bias)
         ctx.meta = (ksize, c0, c1, bias is not None, res is not None)
@@ -380,15 +402,24 @@ class ConvFn(torch.autograd.Function):
         cout8 = dy8.shape[3]
         dx0 = dx1 = dw = db = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            wpd = pack_conv_weight(weight, dy.dtype, cout8, 1)
             alloc = torch.empty if cin_real == cin else torch.zeros
             dx = alloc(nf, h, w, cin, dtype=dy.dtype, device=dy.device)
             m = nf * h * w
-            _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, cout8, ksize, h, w),
-                    2.0 * m * cin_real * cout8 * ksize * ksize,
-                    dy8.element_size() * m * (cin + cout8),
-                    lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd), None, None, 0,
-                                 ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE, stream()))
+            flops = 2.0 * m * cin_real * cout8 * ksize * ksize
+            nbytes = dy8.element_size() * m * (cin + cout8)
+            if frame8_ok(dy8, None, cout8, cout8, cin_real, cout8, cout8, cin, 0, ksize, h, w, nf):
+                wpd = pack_conv_weight(weight, dy.dtype, cout8, 3)
+                _launch("conv_fwd_frame8_kernel", flops, nbytes,
+                        lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd),
+                                     None, None, 0, ptr(dx), cin, nf, cout8, cin_real, ACT_NONE,
+                                     stream()))
+            else:
+                wpd = pack_conv_weight(weight, dy.dtype, cout8, 1)
+                _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, cout8, ksize, h, w),
+                        flops, nbytes,
+                        lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd), None,
+                                     None, 0, ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE,
+                                     stream()))
             dx0 = dx[..., :c0]
             dx1 = dx[..., c0:] if x1 is not None else None
         wparam, bparam = ctx.params

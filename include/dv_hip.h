@@ -68,6 +68,17 @@ int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0, 
                   int accumulate_b, float* ws, long long ws_floats, int nf, int h, int w,
                   int cin, int cout, int cout_real, int cin_real, int ksize, void* stream);
 
+/* 3x3 forward / dgrad of 8x8 frames (the Unet3D 8x8 stage,
+ * dalle2_video.py:107 at 8x8 and the dgrads of those convs): same contract
+ * as dv_conv_fwd with h = w = 8, ksize = 3, but `wpack` is the 16-channel-
+ * chunk-major image of dv_pack_conv_weight mode 2 (forward) or 3 (dgrad).
+ * bf16 only; needs cin % 16 == 0, c0 % 16 == 0 (split), cout % 64 == 0,
+ * nf even, ld0 / ld1 % 8 == 0, ldy / ldres % 4 == 0, 16-B aligned x0 / x1 /
+ * wpack, nf * 64 * ld * 2 < 2^31; returns DV_ERR_INVALID otherwise.       */
+int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
+                 const void* wpack, const float* bias, const void* res, int ldres, void* y,
+                 int ldy, int nf, int cin, int cout, int act, void* stream);
+
 /* db[c] += sum_p dy[p][c]  (f32 atomics) */
 int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix, int c,
                  void* stream);
@@ -75,6 +86,8 @@ int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix,
 /* f32 torch weight (cout, cin, 1, k, k) -> packed `dtype`
  *   mode 0 (forward):  out[co][tap][ci_pad]          (ci >= cin zero)
  *   mode 1 (dgrad):    out[ci][tap'][co_pad] = w[co][ci][k*k-1-tap']
+ *   modes 2 / 3:       modes 0 / 1 with each row chunk-major,
+ *                      [pad / 16][k*k][16] (pad_to % 16 == 0; dv_conv_fwd8) 
  * LDS-staged (coalesced both ways); needs cin*k*k (mode 0) or cout*k*k
  * (mode 1) <= 8192.                                                        */
 int dv_pack_conv_weight(int dtype, const float* w, void* out, int cout, int cin, int ksize,

@@ -29,6 +29,9 @@ CASES = [
     # stripe forward / dgrad (64 input channels, W in {32, 64})
     (8, 32, 32, 64, 0, 128, 3),     # W=32, 2 cout tiles (dgrad: 128 -> 64 implicit GEMM)
     (4, 64, 64, 64, 0, 64, 3),      # W=64, forward and dgrad both stripe
+    # 8x8-frame forward / dgrad (H = W = 8, 16-channel chunks, two frames per block)
+    (4, 8, 8, 48, 16, 64, 3),       # dual source at a 16-channel boundary, dgrad 64 -> 48 + 16
+    (6, 8, 8, 128, 0, 192, 3),      # three channel blocks (no XCD regrouping), 8 chunks
 ]
 
 

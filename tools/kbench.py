@@ -28,12 +28,18 @@ def conv_case(nf, h, w, cin, cout, k, dtype=torch.bfloat16):
     wt = (torch.randn(cout, cin, 1, k, k, device="cuda") / (cin * k * k) ** 0.5).requires_grad_()
     b = torch.randn(cout, device="cuda")
     flops = 2.0 * nf * h * w * cout * cin * k * k
-    wp = ops.pack_conv_weight(wt, dtype, cin, 0)
     y = torch.empty(nf, h, w, cout, device="cuda", dtype=dtype)
     from dalle2_video._lib import call, ptr, stream, dt
-    def fwd():
-        call("dv_conv_fwd", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
-             cout, nf, h, w, cin, cout, k, 0, stream())
+    if ops.frame8_ok(x, None, cin, cin, cout, cin, cin, cout, 0, k, h, w, nf):
+        wp = ops.pack_conv_weight(wt, dtype, cin, 2)
+        def fwd():
+            call("dv_conv_fwd8", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
+                 cout, nf, cin, cout, 0, stream())
+    else:
+        wp = ops.pack_conv_weight(wt, dtype, cin, 0)
+        def fwd():
+            call("dv_conv_fwd", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
+                 cout, nf, h, w, cin, cout, k, 0, stream())
     ms = timeit(fwd)
     dy = torch.randn_like(y)
     ws = ops._wgrad_workspace(ops._lib.dtype_name(x), nf, h, w, cin, cin, False, cout, k, x.device)
@@ -70,6 +76,18 @@ if __name__ == "__main__":
         for _ in range(20):
             call("dv_conv_fwd", dt(x), ptr(x), 64, 64, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
                  64, 64, 64, 64, 64, 64, 3, 0, stream())
+        torch.cuda.synchronize()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "fwd8":  # the 8x8-stage 512->512 forward, for counter passes
+        x = torch.randn(64, 8, 8, 512, device="cuda", dtype=torch.bfloat16)
+        wt = torch.randn(512, 512, 1, 3, 3, device="cuda") / 68
+        b = torch.randn(512, device="cuda")
+        wp = ops.pack_conv_weight(wt, torch.bfloat16, 512, 2)
+        y = torch.empty_like(x)
+        from dalle2_video._lib import call, ptr, stream, dt
+        for _ in range(20):
+            call("dv_conv_fwd8", dt(x), ptr(x), 512, 512, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
+                 512, 64, 512, 512, 0, stream())
         torch.cuda.synchronize()
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "fwd":
