@@ -1360,48 +1360,71 @@ int launch_fwd_stripe2(const ConvFwdArgs<bf16>& a, int seg, int nseg, hipStream_
 }
 
 // ---------------------------------------------------------------------------
-// bf16 3x3 forward / dgrad for 8x8 frames (the Unet3D 8x8 stage: mid blocks,
-// stage-3 / up-0 convs and their dgrads; H = W = 8, cin % 16 == 0, cout %
-// 64 == 0, M % 128 == 0; weights packed 16-channel-chunk-major, modes 2 / 3,
-// so a chunk of a weight row is one contiguous 288-B run: with the plain
-// [tap][ci] rows every 16-channel piece was a separate 32-B request and L2
-// moved twice the bytes).  One workgroup = 128 pixels (two frames) x 64
-// output channels, 4 waves; each wave owns 32 pixels x 64 channels (two
-// 32x32 accumulators sharing one window fragment: 1.5 LDS reads per MFMA,
-// against 2 for one accumulator per wave).  K runs over 16-channel chunks:
-// per chunk the block's 64 packed weight rows (9 taps x 16 ci) and the
-// two-frame window (zero halo) arrive by LDS-DMA into a 5-deep ring, four
-// chunks ahead; counted vmcnt + one raw barrier per chunk; no VGPR staging.
-// Window image: 12 pixel slots per window row (10 used), 3 16-B slots per
-// pixel (2 data + pad).  The row pitch 12 makes every residue of the window
-// pixel index mod 16 occur exactly twice among a wave's 32 pixels, and lanes
-// map to pixels (f8_pix) so that each ds_read_b128 16-lane group takes one
-// pixel of each residue: with the odd slot pitch every window read is
+// bf16 3x3 forward / dgrad, "window" form, for frame widths W = 8 (H = 8),
+// 16, 32, 64 (H*W % 128 == 0): the Unet3D 8x8 / 16x16 / 32x32 / 64x64
+// stage convs with cin % 16 == 0 and cout % 64 == 0, and their dgrads.
+// Weights are packed 16-channel-chunk-major (dv_pack_conv_weight modes 2 /
+// 3), so a chunk of a weight row is one contiguous 288-B run (with [tap][ci]
+// rows every 16-channel piece was a separate 32-B request and L2 moved twice
+// the bytes).  One workgroup = 128 pixels (two 8x8 frames, or 128 / W rows
+// of one frame) x 64 output channels, 4 waves; each wave owns 32 pixels x
+// 64 channels (two 32x32 accumulators sharing one window fragment: 1.5 LDS
+// reads per MFMA, against 2 for one accumulator per wave).  K runs over
+// 16-channel chunks: per chunk the block's 64 weight rows (9 taps x 16 ci)
+// and the pixel window (zero halo) arrive by LDS-DMA into a 4-5 deep ring;
+// counted vmcnt + one raw barrier per chunk; the chunk offset rides in the
+// DMA's SGPR soffset; no VGPR staging.
+// Window image: rows of WQ pixel slots, 3 16-B slots per pixel (2 data +
+// pad).  Lanes map to pixels (fw_pix) so that each ds_read_b128 16-lane
+// group takes one pixel of every residue of the window index mod 16 (for
+// W = 8 the row pitch 12 makes every residue occur exactly twice among a
+// wave's 32 pixels): with the odd slot pitch every window read is
 // conflict-free for all nine taps.  Weight rows: 19 slots (odd): conflict-
 // free.  Blocks are ordered so that one XCD works on one output-channel
 // block at a time (its 64 weight rows stay in that XCD's L2).
+// Measured (512->512 at 8x8, 64 frames): 44 us (stripe2) -> 28 us.
 // ---------------------------------------------------------------------------
-constexpr int F8_WQ = 12;                                  // window pixel slots per window row
-constexpr int F8_WPIX = 2 * 10 * F8_WQ;                    // two frames
+// Window geometry per frame width (a 128-pixel tile: two 8x8 frames, or
+// 128 / W rows of one frame when H*W % 128 == 0): window rows NWR of WQ pixel
+// slots (W + 2 used; W = 8 pads to 12 so the residues work out, see above),
+// three 16-B slots per pixel.
+template <int W>
+struct FwGeom {
+  static constexpr int NF = W == 8 ? 2 : 1;                  // frames per tile
+  static constexpr int NWR = W == 8 ? 10 : 128 / W + 2;      // window rows per frame
+  static constexpr int WQ = W == 8 ? 12 : W + 2;             // pixel slots per window row
+  static constexpr int FPIX = NWR * WQ;                      // window pixels per frame
+  static constexpr int WPIX = NF * FPIX;
+  static constexpr int XPIECES = (WPIX * 3 + 63) / 64;
+  static constexpr int PIECES = 19 + XPIECES;                // + 64 weight rows x 19 slots
+  static constexpr int NPW = (PIECES + 3) / 4;
+  static constexpr int BUF = PIECES * 1024;
+  static constexpr int NBUF = 5 * BUF <= 160 * 1024 - 1024 ? 5 : 4;
+};
 constexpr int F8_WROW = 19;                                // 16-B slots per weight row
 constexpr int F8_WPIECES = F8_WROW;                        // 64 rows x 19 slots = 19 KiB
-constexpr int F8_XPIECES = (F8_WPIX * 3 + 63) / 64;        // 12
-constexpr int F8_PIECES = F8_WPIECES + F8_XPIECES;         // 31 1-KiB DMA pieces per chunk
-constexpr int F8_NPW = (F8_PIECES + 3) / 4;                // 8 per wave (one repeat)
-constexpr int F8_BUF = F8_PIECES * 1024;
-constexpr int F8_NBUF = 5;                                 // ring depth (155 KiB)
 
-// lane r -> pixel (row * 8 + col) of the wave's 4 x 8 pixel tile: ds_read_b128
-// group {0-3, 12-15, 20-27} takes image rows 0 and 2, the other rows 1 and 3
-__device__ __forceinline__ int f8_pix(int r) {
+// lane r -> pixel (row * W + col) of the wave's 32-pixel tile so that the
+// ds_read_b128 16-lane group {0-3, 12-15, 20-27} and its complement each take
+// one pixel of every residue of the window index mod 16:
+//   W = 8 (4 rows x 8): group A rows 0 and 2, the rest rows 1 and 3
+//   W = 16 (2 rows x 16): group A row 0, the rest row 1
+//   W >= 32 (32 columns of one row): group A columns 0-15, the rest 16-31
+template <int W>
+__device__ __forceinline__ int fw_pix(int r) {
   const bool ga = r < 4 || (r >= 12 && r < 16) || (r >= 20 && r < 28);
   const int a = ga ? (r < 4 ? r : (r < 16 ? r - 8 : r - 12))
                    : (r < 12 ? r - 4 : (r < 20 ? r - 8 : r - 16));
-  return (2 * (a >> 3) + (ga ? 0 : 1)) * 8 + (a & 7);
+  if constexpr (W == 8) return (2 * (a >> 3) + (ga ? 0 : 1)) * 8 + (a & 7);
+  else if constexpr (W == 16) return (ga ? 0 : 16) + a;
+  else return (ga ? 0 : 16) + a;
 }
 
-__global__ __launch_bounds__(256) void conv_fwd_frame8_kernel(ConvFwdArgs<bf16> p) {
-  __shared__ __attribute__((aligned(1024))) char smem[F8_NBUF * F8_BUF];
+template <int W>
+__global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
+  using G = FwGeom<W>;
+  constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int npx = (int)(p.M / 128), nblk = npx * (p.cout / 64);
@@ -1410,13 +1433,16 @@ __global__ __launch_bounds__(256) void conv_fwd_frame8_kernel(ConvFwdArgs<bf16> 
   const int co0 = (L / npx) * 64;
   const long long m0 = (long long)(L % npx) * 128;
   const int nch = p.cin / 16;
+  const int HW = p.H * W;
+  const int y0 = W == 8 ? 0 : (int)((m0 % HW) / W);        // tile's first image row
+  const long long fb = W == 8 ? m0 : m0 - (m0 % HW) + (long long)y0 * W;  // pixel of (y0, 0)
 
   // this lane's slot of each of the wave's DMA pieces: a fixed byte offset
   // (or DMA_OOB); the chunk's offset rides in the instruction's soffset
-  unsigned voff0[F8_NPW], voff1[F8_NPW];
+  unsigned voff0[NPW], voff1[NPW];
 #pragma unroll
-  for (int i = 0; i < F8_NPW; ++i) {
-    const int k = min(wave + 4 * i, F8_PIECES - 1);
+  for (int i = 0; i < NPW; ++i) {
+    const int k = min(wave + 4 * i, PIECES - 1);
     voff0[i] = voff1[i] = DMA_OOB;
     if (k < F8_WPIECES) {
       // chunk-major packed row (mode 2/3): [cin / 16][9 taps][16]; slot c = 2 tap + half
@@ -1424,9 +1450,11 @@ __global__ __launch_bounds__(256) void conv_fwd_frame8_kernel(ConvFwdArgs<bf16> 
       if (c < 18) voff0[i] = (unsigned)((((long long)co0 + row) * p.K + c * 8) * 2);
     } else {
       const int slot = (k - F8_WPIECES) * 64 + lane, px = slot / 3, s = slot - px * 3;
-      const int f = px / 120, rem = px - f * 120, wy = rem / F8_WQ, wx = rem - wy * F8_WQ;
-      if (px < F8_WPIX && s < 2 && wy >= 1 && wy <= 8 && wx >= 1 && wx <= 8) {
-        const long long pix = m0 + f * 64 + (wy - 1) * 8 + (wx - 1);
+      const int f = px / G::FPIX, rem = px - f * G::FPIX, wy = rem / WQ, wx = rem - wy * WQ;
+      const int y = y0 + wy - 1;  // image row (W = 8: within frame f of the tile)
+      if (px < G::WPIX && s < 2 && wx >= 1 && wx <= W && y >= 0 && y < p.H &&
+          (W == 8 || wy <= 128 / W + 1)) {
+        const long long pix = fb + (long long)f * 64 + (long long)(wy - 1) * W + (wx - 1);
         voff0[i] = (unsigned)(pix * p.ld0 * 2 + s * 16);
         voff1[i] = (unsigned)(pix * p.ld1 * 2 + s * 16);
       }
@@ -1435,35 +1463,38 @@ __global__ __launch_bounds__(256) void conv_fwd_frame8_kernel(ConvFwdArgs<bf16> 
   const __amdgpu_buffer_rsrc_t wr = dma_rsrc(p.w, (unsigned)((long long)p.cout * p.K * 2));
   const __amdgpu_buffer_rsrc_t xr0 = dma_rsrc(p.x0, (unsigned)(p.M * p.ld0 * 2));
   const __amdgpu_buffer_rsrc_t xr1 = dma_rsrc(p.x1, (unsigned)(p.M * p.ld1 * 2));
-  // piece i of chunk c (i < F8_NPW)
+  // piece i of chunk c (i < NPW)
   auto issue1 = [&](int c, int i) {
     const int ci0 = c * 16;
     const bool first = ci0 < p.c0;
-    char* b = smem + (c % F8_NBUF) * F8_BUF;
-    const int k = min(wave + 4 * i, F8_PIECES - 1);
+    char* b = smem + (c % NBUF) * BUF;
+    const int k = min(wave + 4 * i, PIECES - 1);
     if (k < F8_WPIECES) dma16s(wr, b + k * 1024, voff0[i], (unsigned)ci0 * 18);
     else if (first) dma16s(xr0, b + k * 1024, voff0[i], (unsigned)ci0 * 2);
     else dma16s(xr1, b + k * 1024, voff1[i], (unsigned)(ci0 - p.c0) * 2);
   };
   auto issue = [&](int c) {
 #pragma unroll
-    for (int i = 0; i < F8_NPW; ++i) issue1(c, i);
+    for (int i = 0; i < NPW; ++i) issue1(c, i);
   };
+  constexpr int AHEAD = NBUF - 1;  // chunks in flight beyond the one being read
 
-  // prologue: chunks 0 .. F8_NBUF-2 in flight, wait for chunk 0
-  issue(0);
-  if (nch > 1) issue(1);
-  if (nch > 2) issue(2);
-  if (nch > 3) issue(3);
-  if (nch > 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * F8_NPW) : "memory");
-  else if (nch > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * F8_NPW) : "memory");
-  else if (nch > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(F8_NPW) : "memory");
+  // prologue: chunks 0 .. AHEAD-1 in flight, wait for chunk 0
+#pragma unroll
+  for (int c = 0; c < AHEAD; ++c)
+    if (c < nch) issue(c);
+  const int pro = min(AHEAD, nch) - 1;  // younger chunks than chunk 0
+  if (pro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
+  else if (pro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
+  else if (pro == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
   const int r = lane & 31, h = lane >> 5;
-  const int pix = f8_pix(r);
-  const int wb = (wave >> 1) * 120 + (4 * (wave & 1) + (pix >> 3)) * F8_WQ + (pix & 7);
+  const int pix = fw_pix<W>(r);                    // within the wave's 32 pixels
+  const int tpx = wave * 32 + pix;                 // within the 128-pixel tile
+  const int wb = W == 8 ? (tpx >> 6) * G::FPIX + ((tpx & 63) >> 3) * WQ + (tpx & 7)
+                        : (tpx / W) * WQ + tpx % W;  // window pixel of tap (0, 0)
   const int bofs = F8_WPIECES * 1024 + (wb * 3 + h) * 16;
   const int aofs = r * (F8_WROW * 16) + h * 16;
   // two accumulator chains per channel half (even / odd taps): four
@@ -1472,21 +1503,21 @@ __global__ __launch_bounds__(256) void conv_fwd_frame8_kernel(ConvFwdArgs<bf16> 
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc0[e] = acc1[e] = acc2[e] = acc3[e] = 0.f;
   for (int c = 0; c < nch; ++c) {
-    const char* b = smem + (c % F8_NBUF) * F8_BUF;
+    const char* b = smem + (c % NBUF) * BUF;
     // fragments of tap d + 2 are read while tap d multiplies (one wave per
     // SIMD: the LDS latency is hidden by this wave's own MFMAs)
     u32x4 bq[3], aq0[3], aq1[3];
     auto rd = [&](int d, int s) {
-      const int T = ((d / 3) * F8_WQ + (d % 3)) * 48;
+      const int T = ((d / 3) * WQ + (d % 3)) * 48;
       bq[s] = *(const u32x4*)(b + bofs + T);
       aq0[s] = *(const u32x4*)(b + aofs + d * 32);
       aq1[s] = *(const u32x4*)(b + aofs + 32 * F8_WROW * 16 + d * 32);
     };
     rd(0, 0);
     rd(1, 1);
-    // chunk c+4's pieces go out one per tap, in the MFMA shadow: its buffer
-    // was last read in chunk c-1, before the last barrier
-    const bool pre = c + 4 < nch;
+    // chunk c+AHEAD's pieces go out one per tap, in the MFMA shadow: its
+    // buffer was last read in chunk c-1, before the last barrier
+    const bool pre = c + AHEAD < nch;
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
       if (d + 2 < 9) rd(d + 2, (d + 2) % 3);
@@ -1497,18 +1528,19 @@ __global__ __launch_bounds__(256) void conv_fwd_frame8_kernel(ConvFwdArgs<bf16> 
         acc0 = Mma<bf16>::run(aq0[d % 3], bq[d % 3], acc0);
         acc1 = Mma<bf16>::run(aq1[d % 3], bq[d % 3], acc1);
       }
-      if (d < F8_NPW && pre) issue1(c + 4, d);
+      if (d < NPW && pre) issue1(c + AHEAD, d);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // chunk c+1 landed: younger are the pieces of chunks c+2 .. c+4
-    if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * F8_NPW) : "memory");
-    else if (c + 3 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * F8_NPW) : "memory");
-    else if (c + 2 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(F8_NPW) : "memory");
+    // chunk c+1 landed: younger are the pieces of chunks c+2 .. c+AHEAD
+    const int young = min(c + AHEAD, nch - 1) - (c + 1);
+    if (young >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
+    else if (young == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
+    else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e
-  const long long m = m0 + wave * 32 + pix;
+  const long long m = m0 + tpx;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
 #pragma unroll
@@ -1537,19 +1569,25 @@ __global__ __launch_bounds__(256) void conv_fwd_frame8_kernel(ConvFwdArgs<bf16> 
   }
 }
 
-bool fwd_frame8_ok(const ConvFwdArgs<bf16>& a, int h, int w) {
+bool fwd_frame_ok(const ConvFwdArgs<bf16>& a, int h, int w) {
   const long long maxb = (long long)DMA_OOB;
-  return a.ks == 3 && h == 8 && w == 8 && a.cin % 16 == 0 && a.c0 % 16 == 0 && a.cout % 64 == 0 &&
+  const bool geom = (h == 8 && w == 8) || ((w == 16 || w == 32 || w == 64) && (h * w) % 128 == 0);
+  return a.ks == 3 && geom && a.cin % 16 == 0 && a.c0 % 16 == 0 && a.cout % 64 == 0 &&
          a.M % 128 == 0 && a.ld0 % 8 == 0 && a.ld1 % 8 == 0 && (a.ldy & 3) == 0 &&
          (a.res == nullptr || (a.ldres & 3) == 0) && a.M * a.ld0 * 2 < maxb &&
          a.M * a.ld1 * 2 < maxb && (long long)a.cout * a.K * 2 < maxb &&
          ((uintptr_t)a.x0 & 15) == 0 && ((uintptr_t)a.x1 & 15) == 0 && ((uintptr_t)a.w & 15) == 0;
 }
 
-int launch_fwd_frame8(const ConvFwdArgs<bf16>& a, hipStream_t st) {
+int launch_fwd_frame(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   const int nblk = (int)(a.M / 128) * (a.cout / 64);
-  conv_fwd_frame8_kernel<<<nblk, 256, 0, st>>>(a);
-  return check_launch("conv_fwd_frame8");
+  switch (a.W) {
+    case 8: conv_fwd_frame_kernel<8><<<nblk, 256, 0, st>>>(a); break;
+    case 16: conv_fwd_frame_kernel<16><<<nblk, 256, 0, st>>>(a); break;
+    case 32: conv_fwd_frame_kernel<32><<<nblk, 256, 0, st>>>(a); break;
+    default: conv_fwd_frame_kernel<64><<<nblk, 256, 0, st>>>(a); break;
+  }
+  return check_launch("conv_fwd_frame");
 }
 
 // tile choice for the glds path (mirrored by ops.conv_tile for kernel naming)
@@ -2105,19 +2143,20 @@ extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const voi
 
 extern "C" int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
                             const void* wpack, const float* bias, const void* res, int ldres,
-                            void* y, int ldy, int nf, int cin, int cout, int act, void* stream) {
-  DV_REQUIRE(dtype == DV_BF16, "the 8x8-frame conv is bf16 only");
+                            void* y, int ldy, int nf, int h, int w, int cin, int cout, int act,
+                            void* stream) {
+  DV_REQUIRE(dtype == DV_BF16, "the window conv is bf16 only");
   DV_REQUIRE(x0 && wpack && y, "null pointer");
   DV_REQUIRE(cin > 0 && (!x1 || (c0 > 0 && c0 < cin)), "bad channel split");
   DV_REQUIRE(ldy >= cout && (!res || ldres >= cout), "bad output stride");
   ConvFwdArgs<bf16> a;
   a.x0 = (const bf16*)x0; a.x1 = (const bf16*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0;
   a.c0 = x1 ? c0 : cin; a.w = (const bf16*)wpack; a.bias = bias; a.res = (const bf16*)res;
-  a.ldres = ldres; a.y = (bf16*)y; a.ldy = ldy; a.H = 8; a.W = 8; a.cin = cin; a.cout = cout;
-  a.ks = 3; a.act = act; a.M = (long long)nf * 64; a.K = 9 * cin;
-  DV_REQUIRE(fwd_frame8_ok(a, 8, 8), "shape/stride outside the 8x8-frame kernel (see dv_hip.h)");
+  a.ldres = ldres; a.y = (bf16*)y; a.ldy = ldy; a.H = h; a.W = w; a.cin = cin; a.cout = cout;
+  a.ks = 3; a.act = act; a.M = (long long)nf * h * w; a.K = 9 * cin;
+  DV_REQUIRE(fwd_frame_ok(a, h, w), "shape/stride outside the window conv (see dv_hip.h)");
   if (a.M == 0) return DV_OK;
-  return launch_fwd_frame8(a, (hipStream_t)stream);
+  return launch_fwd_frame(a, (hipStream_t)stream);
 }
 
 extern "C" int dv_conv_wgrad_ws(int dtype, int nf, int h, int w, int cin, int c0, int split,

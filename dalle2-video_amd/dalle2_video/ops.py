@@ -103,15 +103,20 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0):
     return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"
 
 
-_NO_FRAME8 = bool(os.environ.get("DV_NO_FRAME8"))  # A/B switch: 8x8 convs on dv_conv_fwd
+_NO_WINDOW = bool(os.environ.get("DV_NO_WINDOW"))  # A/B switch: 3x3 convs on dv_conv_fwd only
+# measured (tools/kbench.py fwd): the window form wins at 8x8 and 16x16, the glds /
+# stripe kernels at 32x32 and 64x64
+_WINDOW_W = tuple(int(v) for v in os.environ.get("DV_WINDOW_W", "8,16").split(",") if v)
 
 
-def frame8_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf):
-    """Mirror of fwd_frame8_ok (dv_conv.hip): the 8x8-frame conv (dv_conv_fwd8)."""
-    return (not _NO_FRAME8 and x0.dtype == torch.bfloat16 and ksize == 3 and h == 8 and w == 8
-            and cin % 16 == 0 and c0 % 16 == 0 and cout % 64 == 0 and nf % 2 == 0
+def window_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf):
+    """Mirror of fwd_frame_ok (dv_conv.hip): the window-form 3x3 conv (dv_conv_fwd8)."""
+    geom = (h == 8 and w == 8 and nf % 2 == 0) or (w in (16, 32, 64) and (h * w) % 128 == 0)
+    return (not _NO_WINDOW and w in _WINDOW_W and x0.dtype == torch.bfloat16 and ksize == 3
+            and geom and cin % 16 == 0 and c0 % 16 == 0 and cout % 64 == 0
+            and not (cin == 64 and c0 == cin and w in (32, 64))  # the resident-weight stripe kernel
             and ld0 % 8 == 0 and ld1 % 8 == 0 and ldy % 4 == 0 and ldres % 4 == 0
-            and nf * 64 * max(ld0, ld1) * 2 < (1 << 31)
+            and nf * h * w * max(ld0, ld1) * 2 < (1 << 31)
             and x0.data_ptr() % 16 == 0 and (x1 is None or x1.data_ptr() % 16 == 0))
 
 
@@ -372,12 +377,12 @@ class ConvFn(torch.autograd.Function):
         b = None if bias is None else bias.detach().float().contiguous()
         m = nf * h * w
         flops, nbytes = 2.0 * m * cout * cin * ksize * ksize, x0.element_size() * m * (cin + cout)
-        if frame8_ok(x0, x1, cin, c0 if x1 is not None else cin, cout, ld0, ld1 or ld0, cout,
+        if window_ok(x0, x1, cin, c0 if x1 is not None else cin, cout, ld0, ld1 or ld0, cout,
                      ldr, ksize, h, w, nf):
             wp = pack_conv_weight(weight, x0.dtype, cin, 2)
-            _launch("conv_fwd_frame8_kernel", flops, nbytes,
+            _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                     lambda: call("dv_conv_fwd8", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp),
-                                 ptr(b), ptr(res), ldr, ptr(y), cout, nf, cin, cout, ACT_NONE,
+                                 ptr(b), ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ACT_NONE,
                                  stream()))
         else:
             wp = pack_conv_weight(weight, x0.dtype, cin, 0)
@@ -407,11 +412,11 @@ class ConvFn(torch.autograd.Function):
             m = nf * h * w
             flops = 2.0 * m * cin_real * cout8 * ksize * ksize
             nbytes = dy8.element_size() * m * (cin + cout8)
-            if frame8_ok(dy8, None, cout8, cout8, cin_real, cout8, cout8, cin, 0, ksize, h, w, nf):
+            if window_ok(dy8, None, cout8, cout8, cin_real, cout8, cout8, cin, 0, ksize, h, w, nf):
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 3)
-                _launch("conv_fwd_frame8_kernel", flops, nbytes,
+                _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                         lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd),
-                                     None, None, 0, ptr(dx), cin, nf, cout8, cin_real, ACT_NONE,
+                                     None, None, 0, ptr(dx), cin, nf, h, w, cout8, cin_real, ACT_NONE,
                                      stream()))
             else:
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 1)

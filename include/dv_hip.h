@@ -68,16 +68,17 @@ int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0, 
                   int accumulate_b, float* ws, long long ws_floats, int nf, int h, int w,
                   int cin, int cout, int cout_real, int cin_real, int ksize, void* stream);
 
-/* 3x3 forward / dgrad of 8x8 frames (the Unet3D 8x8 stage,
- * dalle2_video.py:107 at 8x8 and the dgrads of those convs): same contract
- * as dv_conv_fwd with h = w = 8, ksize = 3, but `wpack` is the 16-channel-
- * chunk-major image of dv_pack_conv_weight mode 2 (forward) or 3 (dgrad).
- * bf16 only; needs cin % 16 == 0, c0 % 16 == 0 (split), cout % 64 == 0,
- * nf even, ld0 / ld1 % 8 == 0, ldy / ldres % 4 == 0, 16-B aligned x0 / x1 /
- * wpack, nf * 64 * ld * 2 < 2^31; returns DV_ERR_INVALID otherwise.       */
+/* 3x3 forward / dgrad, window form (dalle2_video.py:107 Block3D.project at
+ * the 8x8 .. 64x64 stages, and the dgrads of those convs): same contract as
+ * dv_conv_fwd with ksize = 3, but `wpack` is the 16-channel-chunk-major
+ * image of dv_pack_conv_weight mode 2 (forward) or 3 (dgrad).  bf16 only;
+ * needs (h, w) = (8, 8) with nf even, or w in {16, 32, 64} with
+ * h * w % 128 == 0; cin % 16 == 0, c0 % 16 == 0 (split), cout % 64 == 0,
+ * ld0 / ld1 % 8 == 0, ldy / ldres % 4 == 0, 16-B aligned x0 / x1 / wpack,
+ * nf * h * w * ld * 2 < 2^31; returns DV_ERR_INVALID otherwise.          */
 int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
                  const void* wpack, const float* bias, const void* res, int ldres, void* y,
-                 int ldy, int nf, int cin, int cout, int act, void* stream);
+                 int ldy, int nf, int h, int w, int cin, int cout, int act, void* stream);
 
 /* db[c] += sum_p dy[p][c]  (f32 atomics) */
 int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix, int c,

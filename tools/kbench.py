@@ -30,11 +30,11 @@ def conv_case(nf, h, w, cin, cout, k, dtype=torch.bfloat16):
     flops = 2.0 * nf * h * w * cout * cin * k * k
     y = torch.empty(nf, h, w, cout, device="cuda", dtype=dtype)
     from dalle2_video._lib import call, ptr, stream, dt
-    if ops.frame8_ok(x, None, cin, cin, cout, cin, cin, cout, 0, k, h, w, nf):
+    if ops.window_ok(x, None, cin, cin, cout, cin, cin, cout, 0, k, h, w, nf):
         wp = ops.pack_conv_weight(wt, dtype, cin, 2)
         def fwd():
             call("dv_conv_fwd8", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
-                 cout, nf, cin, cout, 0, stream())
+                 cout, nf, h, w, cin, cout, 0, stream())
     else:
         wp = ops.pack_conv_weight(wt, dtype, cin, 0)
         def fwd():
@@ -87,7 +87,7 @@ if __name__ == "__main__":
         from dalle2_video._lib import call, ptr, stream, dt
         for _ in range(20):
             call("dv_conv_fwd8", dt(x), ptr(x), 512, 512, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
-                 512, 64, 512, 512, 0, stream())
+                 512, 64, 8, 8, 512, 512, 0, stream())
         torch.cuda.synchronize()
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "fwd":
