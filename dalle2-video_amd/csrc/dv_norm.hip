@@ -5,6 +5,7 @@
 #include "dv_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 using namespace dv;
 
@@ -378,11 +379,23 @@ long long gn_rows(const GnArgs& a, int vec, int u, long long target) {
   return r < pass ? pass : r;
 }
 
+// replicas of the sums: enough that ~16 reduce workgroups share one address
+// (a clip's reduce blocks all add into its C sums), no more -- every apply
+// workgroup reads all R replicas in its prologue
+int gn_replicas(const GnArgs& a, int blocks_per_clip) {
+  static const int fixed = getenv("DV_GN_R") ? atoi(getenv("DV_GN_R")) : 0;  // A/B switch
+  int r = fixed > 0 ? fixed : (blocks_per_clip + 15) / 16;
+  r = std::min(r, 8);
+  if (a.R < r) r = a.R;  // the caller's buffer holds a.R replicas
+  return std::max(r, 1);
+}
+
 template <typename T>
 int gn_fwd_t(GnArgs a, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
   a.rows_per_block = gn_rows(a, VEC, 2 * GN_U, 768);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
+  a.R = gn_replicas(a, (int)g1.x);
   gn_reduce_kernel<T, 0><<<g1, 256, 0, st>>>(a);
   a.rows_per_block = gn_rows(a, VEC, GN_U, 1024);
   dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
@@ -395,6 +408,7 @@ int gn_bwd_t(GnArgs a, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
   a.rows_per_block = gn_rows(a, VEC, GN_U, 768);
   dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
+  a.R = gn_replicas(a, (int)g1.x);
   gn_reduce_kernel<T, 1><<<g1, 256, 0, st>>>(a);
   // 165 VGPRs -> 3 waves / SIMD: 768 workgroups are exactly one resident round
   a.rows_per_block = gn_rows(a, VEC, GN_U, 768);
