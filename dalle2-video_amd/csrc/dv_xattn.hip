@@ -20,6 +20,8 @@
 // reductions dKt, dV~ and dg2 are batched TN GEMMs (dv_gemm_tn_batched).
 #include "dv_common.h"
 
+#include <algorithm>
+
 using namespace dv;
 
 namespace {
@@ -113,13 +115,11 @@ __device__ __forceinline__ float kf(const float* kv, const float* null_kv, int b
 // (null + 2 time tokens) are staged in LDS; thread (c, dq) sums a quarter of
 // the 64 head dims for channel c (Wq columns read coalesced across threads,
 // its Wo row segment as 16-B vectors) and the quarters meet in LDS
-__global__ __launch_bounds__(256) void fold_fwd_kernel(const float* wq, const float* wo,
-                                                       const float* kv, const float* null_kv,
-                                                       float* at, float* vt, int nb, int C,
-                                                       float scale) {
+__device__ __forceinline__ void fold_fwd_body(const float* wq, const float* wo, const float* kv,
+                                              const float* null_kv, float* at, float* vt, int C,
+                                              float scale, int h, int b, int cz) {
   __shared__ float sk[NK][DH], sv[NK][DH];
   __shared__ float part[4][6][64];
-  const int h = blockIdx.x, b = blockIdx.y;
   for (int i = threadIdx.x; i < NK * DH; i += 256) {
     const int j = i / DH, d = i % DH;
     sk[j][d] = kf(kv, null_kv, b, h, j, d, 0);
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void fold_fwd_kernel(const float* wq, const fl
   }
   __syncthreads();
   const int cl = threadIdx.x & 63, dq = threadIdx.x >> 6;
-  const int c = blockIdx.z * 64 + cl;
+  const int c = cz * 64 + cl;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, v0 = 0.f, v1 = 0.f, v2 = 0.f;
   if (c < C) {
     const float* wor = wo + (long long)c * (NH * DH) + h * DH;
@@ -155,11 +155,19 @@ __global__ __launch_bounds__(256) void fold_fwd_kernel(const float* wq, const fl
   }
 }
 
+__global__ __launch_bounds__(256) void fold_fwd_kernel(const float* wq, const float* wo,
+                                                       const float* kv, const float* null_kv,
+                                                       float* at, float* vt, int nb, int C,
+                                                       float scale) {
+  fold_fwd_body(wq, wo, kv, null_kv, at, vt, C, scale, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
 // Kt[b][k'][c], KtT[b][c][k'], Vt[b][c][k'], VtT[b][k'][c] (T); dummies zero
 // images are padded to Cp = roundup(C, 32) channels with zeros
 template <typename T>
-__global__ void fold_pack_kernel(const float* at, const float* vt, const float* g1, T* Kt, T* KtT,
-                                 T* Vt, T* VtT, int nb, int C, int Cp) {
+__device__ __forceinline__ void fold_pack_body(const float* at, const float* vt, const float* g1,
+                                               T* Kt, T* KtT, T* Vt, T* VtT, int nb, int C,
+                                               int Cp) {
   const long long n = (long long)nb * KP * Cp;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -176,6 +184,12 @@ __global__ void fold_pack_kernel(const float* at, const float* vt, const float* 
   }
 }
 
+template <typename T>
+__global__ void fold_pack_kernel(const float* at, const float* vt, const float* g1, T* Kt, T* KtT,
+                                 T* Vt, T* VtT, int nb, int C, int Cp) {
+  fold_pack_body<T>(at, vt, g1, Kt, KtT, Vt, VtT, nb, C, Cp);
+}
+
 // colsum[b][k'] = sum_c Kt[b][k'][c] (of the values the MFMA sees)
 template <typename T>
 __global__ void fold_colsum_kernel(const T* Kt, float* colsum, int nb, int Cp) {
@@ -184,6 +198,41 @@ __global__ void fold_colsum_kernel(const T* Kt, float* colsum, int nb, int Cp) {
   for (int c = threadIdx.x; c < Cp; c += 64) s += (float)Kt[(long long)row * Cp + c];
   s = wave_sum(s);
   if (threadIdx.x == 0) colsum[row] = s;
+}
+
+// Every cross-attention block's fold in three launches (the folds depend on
+// weights and the context only, so Unet3D runs them all up front): the job
+// table rides in the kernel arguments (graph-safe, no host-to-device copy).
+struct FoldBatch {
+  DvFoldJob j[DV_FOLD_MAX];
+  int n;
+  float scale;
+};
+
+__global__ __launch_bounds__(256) void fold_fwd_batched_kernel(FoldBatch t) {
+  const DvFoldJob& J = t.j[blockIdx.z / 8];
+  const int cz = blockIdx.z % 8;
+  if ((int)blockIdx.y >= J.nb || cz * 64 >= J.C) return;
+  fold_fwd_body(J.wq, J.wo, J.kv, J.null_kv, J.at, J.vt, J.C, t.scale, blockIdx.x, blockIdx.y, cz);
+}
+
+template <typename T>
+__global__ void fold_pack_batched_kernel(FoldBatch t) {
+  const DvFoldJob& J = t.j[blockIdx.y];
+  fold_pack_body<T>(J.at, J.vt, J.g1, (T*)J.Kt, (T*)J.KtT, (T*)J.Vt, (T*)J.VtT, J.nb, J.C,
+                    (J.C + 31) / 32 * 32);
+}
+
+template <typename T>
+__global__ void fold_colsum_batched_kernel(FoldBatch t) {
+  const DvFoldJob& J = t.j[blockIdx.y];
+  const int row = blockIdx.x, Cp = (J.C + 31) / 32 * 32;
+  if (row >= J.nb * KP) return;
+  const T* Kt = (const T*)J.Kt;
+  float s = 0.f;
+  for (int c = threadIdx.x; c < Cp; c += 64) s += (float)Kt[(long long)row * Cp + c];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) J.colsum[row] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -651,6 +700,38 @@ int fold_t(const float* wq, const float* wo, const float* kv, const float* null_
 }
 
 }  // namespace
+
+extern "C" int dv_xattn_fold_batched(int dtype, const DvFoldJob* jobs, int n, float scale,
+                                     void* stream) {
+  DV_REQUIRE(jobs && n >= 0 && n <= DV_FOLD_MAX, "bad job table");
+  if (n == 0) return DV_OK;
+  FoldBatch t;
+  t.n = n;
+  t.scale = scale;
+  int nbmax = 0, rowsmax = 0;
+  long long packmax = 0;
+  for (int i = 0; i < n; ++i) {
+    const DvFoldJob& J = jobs[i];
+    DV_REQUIRE(J.wq && J.wo && J.kv && J.null_kv && J.g1 && J.at && J.vt && J.Kt && J.KtT && J.Vt &&
+                   J.VtT && J.colsum, "null pointer");
+    DV_REQUIRE(J.nb > 0 && J.C > 0 && J.C <= 512, "bad job shape");
+    t.j[i] = J;
+    nbmax = std::max(nbmax, J.nb);
+    rowsmax = std::max(rowsmax, J.nb * KP);
+    packmax = std::max(packmax, (long long)J.nb * KP * ((J.C + 31) / 32 * 32));
+  }
+  hipStream_t st = (hipStream_t)stream;
+  fold_fwd_batched_kernel<<<dim3(NH, nbmax, n * 8), 256, 0, st>>>(t);
+  const dim3 pg((unsigned)std::min<long long>((packmax + 255) / 256, 1024), n);
+  if (dtype == DV_BF16) {
+    fold_pack_batched_kernel<bf16><<<pg, 256, 0, st>>>(t);
+    fold_colsum_batched_kernel<bf16><<<dim3(rowsmax, n), 64, 0, st>>>(t);
+  } else {
+    fold_pack_batched_kernel<float><<<pg, 256, 0, st>>>(t);
+    fold_colsum_batched_kernel<float><<<dim3(rowsmax, n), 64, 0, st>>>(t);
+  }
+  return check_launch("xattn_fold_batched");
+}
 
 extern "C" int dv_xattn_fold(int dtype, const float* wq, const float* wo, const float* kv,
                              const float* null_kv, const float* g1, float* at, float* vt,

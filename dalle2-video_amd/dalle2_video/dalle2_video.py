@@ -233,12 +233,18 @@ class CrossAttention(nn.Module):
         self.to_kv = nn.Linear(context_dim, inner * 2, bias=False)
         self.to_out = nn.Sequential(nn.Linear(inner, dim, bias=False), LayerNorm(dim))
 
-    def forward_cl(self, x, context, nb, kv=None):
+    def forward_cl(self, x, context, nb, kv=None, fold=None):
         """Returns cross_attn(x, context) + x (the residual of ResnetBlock3D:197);
-        kv: this block's to_kv(context) when the Unet batched the projections."""
+        kv / fold: this block's to_kv(context) and folded operands when the Unet
+        batched them (one launch for every block)."""
         return ops.cross_attention(x, context, self.norm.g, self.null_kv, self.to_q.weight,
                                    self.to_kv.weight, self.to_out[0].weight, self.to_out[1].g, nb,
-                                   _ln_eps(x.dtype), kv=kv)
+                                   _ln_eps(x.dtype), kv=kv, fold=fold)
+
+    def make_fold(self, kv, nb, dtype):
+        """Unrun XattnFold of this block for ops.xattn_fold_batched."""
+        return ops.XattnFold(dtype, kv, self.norm.g, self.null_kv, self.to_q.weight,
+                             self.to_out[0].weight, nb, self.to_out[0].weight.shape[0])
 
 
 class UpsampleCombiner(nn.Module):
@@ -428,7 +434,7 @@ class ResnetBlock3D(nn.Module):
         self.block2 = Block3D(dim_out, dim_out, groups=groups, weight_standardization=weight_standardization)
         self.res_conv = nn.Conv3d(dim, dim_out, 1) if dim != dim_out else nn.Identity()
 
-    def forward_cl(self, x0, time_emb, cond, nb, x1=None, ss=None, kv=None):
+    def forward_cl(self, x0, time_emb, cond, nb, x1=None, ss=None, kv=None, fold=None):
         """ss / kv: this block's time_mlp(time_emb) / to_kv(cond) when the Unet
         computed them for all blocks in one grouped launch (ops.linear_group)."""
         if ss is None and exists(self.time_mlp) and exists(time_emb):
@@ -437,7 +443,7 @@ class ResnetBlock3D(nn.Module):
         h = self.block1.forward_cl(x0, nb, x1=x1, scale_shift=ss)
         if exists(self.cross_attn):
             assert exists(cond)
-            h = self.cross_attn.forward_cl(h, cond, nb, kv=kv)
+            h = self.cross_attn.forward_cl(h, cond, nb, kv=kv, fold=fold)
         if isinstance(self.res_conv, nn.Identity):
             if x1 is not None:
                 raise DVError("identity residual with a split input")
@@ -660,7 +666,7 @@ class Unet3D(nn.Module):
         out.append((self.final_resnet_block, False))
         return out
 
-    def _grouped_projections(self, t, c, mid_c):
+    def _grouped_projections(self, t, c, mid_c, nb, dtype):
         """Every ResnetBlock3D's time_mlp(t) in ONE launch, and every cross-attention
         to_kv(c) / to_kv(mid_c) in one launch per context (ops.linear_group):
         {id(block): (scale_shift, kv)}.  Same arithmetic as the per-block
@@ -678,7 +684,13 @@ class Unet3D(nn.Module):
                                    [b.cross_attn.to_kv.weight for b in xa], [None] * len(xa))
             for b, kv in zip(xa, kvs):
                 pre.setdefault(id(b), [None, None])[1] = kv
-        return {k: tuple(v) for k, v in pre.items()}
+        # every block's cross-attention fold (weights x context only) in one go
+        folds = {}
+        for b, _ in blks:
+            if exists(b.cross_attn) and id(b) in pre and pre[id(b)][1] is not None:
+                folds[id(b)] = b.cross_attn.make_fold(pre[id(b)][1], nb, dtype)
+        ops.xattn_fold_batched(folds.values())
+        return {k: (v[0], v[1], folds.get(k)) for k, v in pre.items()}
 
     def forward_cl(self, x, time, *, batch, lowres_cl=None, video_cond_drop_prob=0.0,
                    text_cond_drop_prob=0.0):
@@ -688,11 +700,11 @@ class Unet3D(nn.Module):
         r = x
         t, c, mid_c = self._conditioning(time, batch, x.device, video_cond_drop_prob,
                                          text_cond_drop_prob)
-        pre = self._grouped_projections(t, c, mid_c)
+        pre = self._grouped_projections(t, c, mid_c, batch, x.dtype)
 
         def run(blk, x, cond, x1=None):
-            ss, kv = pre.get(id(blk), (None, None))
-            return blk.forward_cl(x, t, cond, batch, x1=x1, ss=ss, kv=kv)
+            ss, kv, fold = pre.get(id(blk), (None, None, None))
+            return blk.forward_cl(x, t, cond, batch, x1=x1, ss=ss, kv=kv, fold=fold)
 
         hiddens = []
         for _, init_block, blocks, attn, post in self.downs:

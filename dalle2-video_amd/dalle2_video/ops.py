@@ -757,31 +757,75 @@ def sinusoidal(times: torch.Tensor, dim: int) -> torch.Tensor:
 XA_HEADS, XA_DH = 8, 64
 
 
+class DvFoldJob(ctypes.Structure):
+    """struct DvFoldJob of dv_hip.h (dv_xattn_fold_batched)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wq", "wo", "kv", "null_kv", "g1", "at", "vt", "Kt",
+                                               "KtT", "Vt", "VtT", "colsum")] + \
+               [("nb", ctypes.c_int), ("C", ctypes.c_int)]
+
+
+class XattnFold:
+    """Folded cross-attention operands of one block (dv_xattn_fold outputs) and
+    the f32 copies of the inputs they were made from (saved for the backward)."""
+
+    def __init__(self, dtype, kv_in, g1, null_kv, wq, wo, nb, C):
+        dev = kv_in.device
+        self.kv = kv_in.detach().float().contiguous()  # (nb * tokens, 2 * 512): to_kv(context)
+        self.wqf, self.wof = wq.detach().float().contiguous(), wo.detach().float().contiguous()
+        self.nkv = null_kv.detach().float().contiguous()
+        self.g1f = g1.detach().float().contiguous()
+        self.at = torch.empty(nb, C, 24, dtype=torch.float32, device=dev)
+        self.vt = torch.empty_like(self.at)
+        Cp = (C + 31) // 32 * 32  # operand images padded to whole 32-channel MFMA tiles
+        self.Kt = torch.empty(nb, 32, Cp, dtype=dtype, device=dev)
+        self.KtT = torch.empty(nb, Cp, 32, dtype=dtype, device=dev)
+        self.Vt = torch.empty(nb, Cp, 32, dtype=dtype, device=dev)
+        self.VtT = torch.empty(nb, 32, Cp, dtype=dtype, device=dev)
+        self.colsum = torch.empty(nb, 32, dtype=torch.float32, device=dev)
+        self.nb, self.C, self.dtype = nb, C, dtype
+
+    def job(self):
+        return DvFoldJob(*(ptr(t).value for t in (self.wqf, self.wof, self.kv, self.nkv, self.g1f,
+                                                   self.at, self.vt, self.Kt, self.KtT, self.Vt,
+                                                   self.VtT, self.colsum)), self.nb, self.C)
+
+    def run(self):
+        call("dv_xattn_fold", _lib.DV_BF16 if self.dtype == torch.bfloat16 else _lib.DV_F32,
+             ptr(self.wqf), ptr(self.wof), ptr(self.kv), ptr(self.nkv), ptr(self.g1f), ptr(self.at),
+             ptr(self.vt), ptr(self.Kt), ptr(self.KtT), ptr(self.Vt), ptr(self.VtT), ptr(self.colsum),
+             self.nb, self.C, ctypes_float(XA_DH ** -0.5), stream())
+
+
+def xattn_fold_batched(folds):
+    """Run every block's fold in three launches (dv_xattn_fold_batched)."""
+    folds = list(folds)
+    for i in range(0, len(folds), 24):  # DV_FOLD_MAX
+        part = folds[i:i + 24]
+        jobs = (DvFoldJob * len(part))(*[f.job() for f in part])
+        call("dv_xattn_fold_batched",
+             _lib.DV_BF16 if part[0].dtype == torch.bfloat16 else _lib.DV_F32,
+             ctypes.cast(jobs, ctypes.c_void_p), len(part), ctypes_float(XA_DH ** -0.5), stream())
+
+
 class CrossAttnFn(torch.autograd.Function):
-    """out = CrossAttention(x, context) + x, folded per batch element (dv_xattn.hip)."""
+    """out = CrossAttention(x, context) + x, folded per batch element (dv_xattn.hip).
+    `fold`: an XattnFold already run for this block (Unet3D batches all blocks'
+    folds in one launch), or None to fold here."""
 
     @staticmethod
-    def forward(ctx, x, kv_in, g1, null_kv, wq, wo, g2, nb, eps):
+    def forward(ctx, x, kv_in, g1, null_kv, wq, wo, g2, nb, eps, fold=None):
         require_gpu(x, kv_in)
         nf, h, w, C = x.shape
         ntok = nf * h * w
         P = ntok // nb
         dev, dtype = x.device, x.dtype
-        kv = kv_in.detach().float().contiguous()  # (nb * tokens, 2 * 512): to_kv(context)
-        wqf, wof = wq.detach().float().contiguous(), wo.detach().float().contiguous()
-        nkv = null_kv.detach().float().contiguous()
-        g1f, g2f = g1.detach().float().contiguous(), g2.detach().float().contiguous()
-        at = torch.empty(nb, C, 24, dtype=torch.float32, device=dev)
-        vt = torch.empty_like(at)
-        Cp = (C + 31) // 32 * 32  # operand images padded to whole 32-channel MFMA tiles
-        Kt = torch.empty(nb, 32, Cp, dtype=dtype, device=dev)
-        KtT = torch.empty(nb, Cp, 32, dtype=dtype, device=dev)
-        Vt = torch.empty(nb, Cp, 32, dtype=dtype, device=dev)
-        VtT = torch.empty(nb, 32, Cp, dtype=dtype, device=dev)
-        colsum = torch.empty(nb, 32, dtype=torch.float32, device=dev)
-        call("dv_xattn_fold", dt(x), ptr(wqf), ptr(wof), ptr(kv), ptr(nkv), ptr(g1f), ptr(at), ptr(vt),
-             ptr(Kt), ptr(KtT), ptr(Vt), ptr(VtT), ptr(colsum), nb, C, ctypes_float(XA_DH ** -0.5),
-             stream())
+        if fold is None:
+            fold = XattnFold(dtype, kv_in, g1, null_kv, wq, wo, nb, C)
+            fold.run()
+        kv, wqf, wof, nkv, g1f = fold.kv, fold.wqf, fold.wof, fold.nkv, fold.g1f
+        at, vt, Kt, KtT, Vt, VtT, colsum = (fold.at, fold.vt, fold.Kt, fold.KtT, fold.Vt, fold.VtT,
+                                            fold.colsum)
+        g2f = g2.detach().float().contiguous()
         out = torch.empty(nf, h, w, C, dtype=dtype, device=dev)
         stats = torch.empty(ntok, 4, dtype=torch.float32, device=dev)
         pbuf = torch.empty(ntok, 32, dtype=dtype, device=dev)
@@ -840,7 +884,7 @@ class CrossAttnFn(torch.autograd.Function):
              ptr(dwo), ptr(dkv), ptr(dnull), nb, C, ctypes_float(XA_DH ** -0.5), acc_g, acc_w, stream())
         return (dx, dkv, dg1 if ret_g else None, None if direct else dnull,
                 None if direct else dwq, None if direct else dwo,
-                dg2 if ret_g else None, None, None)
+                dg2 if ret_g else None, None, None, None)
 
 
 def ctypes_vp(addr):
@@ -848,12 +892,13 @@ def ctypes_vp(addr):
     return ctypes.c_void_p(addr)
 
 
-def cross_attention(x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps, kv=None):
+def cross_attention(x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps, kv=None, fold=None):
     """kv: to_kv(context) rows when the caller batched the projection
-    (linear_group over every block sharing the context); else computed here."""
+    (linear_group over every block sharing the context); else computed here.
+    fold: this block's XattnFold when the caller batched the folds."""
     if kv is None:
         kv = linear_group(context.float().reshape(-1, context.shape[-1]), [wkv], [None])[0]
-    return CrossAttnFn.apply(x, kv, g1, null_kv, wq, wo, g2, nb, eps)
+    return CrossAttnFn.apply(x, kv, g1, null_kv, wq, wo, g2, nb, eps, fold)
 
 
 # ---------------------------------------------------------------------------

@@ -249,6 +249,27 @@ int dv_resize_nearest(const float* x, float* y, long long planes, int hin, int w
 int dv_gaussian_blur(const float* x, float* y, long long planes, int H, int W, int ks,
                      const float* w1, void* stream);
 
+/* All cross-attention folds of a Unet3D forward in three launches: one job
+ * per block, the same arguments as dv_xattn_fold (host-memory table of at
+ * most DV_FOLD_MAX jobs, copied into the kernel arguments; graph-safe). */
+#define DV_FOLD_MAX 24
+typedef struct DvFoldJob {
+  const float* wq;
+  const float* wo;
+  const float* kv;
+  const float* null_kv;
+  const float* g1;
+  float* at;
+  float* vt;
+  void* Kt;
+  void* KtT;
+  void* Vt;
+  void* VtT;
+  float* colsum;
+  int nb, C;
+} DvFoldJob;
+int dv_xattn_fold_batched(int dtype, const DvFoldJob* jobs, int n, float scale, void* stream);
+
 /* ---- ResnetBlock3D cross attention (dalle2_video.py:159-162, 192-201;
  * dalle2-pytorch CrossAttention, 8 heads x 64, null kv + 2 time tokens, LN
  * before/after, residual).  Projections fold per clip b into C x 24
