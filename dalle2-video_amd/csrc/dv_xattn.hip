@@ -553,13 +553,13 @@ __global__ __launch_bounds__(256) void fold_mcorr_kernel(const float* wsR, float
 // grads.  grid (ceil(C/64), nb), 256 threads = 64 channels x 4 groups of 6
 // folded columns; dg1/dg2 (pre-zeroed unless accumulating) take one atomic
 // per (b, c).
-__global__ __launch_bounds__(256) void fold_grad_finish_kernel(
+__device__ __forceinline__ void fold_grad_finish_body(
     float* wsR, float* wsV, float* wsQ, const float* mcorr, const float* at,
-    const float* vt, const float* g1, float* dat, float* dvt, float* dg1, float* dg2, int nb,
-    int C) {
+    const float* vt, const float* g1, float* dat, float* dvt, float* dg1, float* dg2, int C,
+    int bx, int b) {
   __shared__ float red[2][4][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
+  const int c = bx * 64 + cl;
   float s1 = 0.f, s2 = 0.f;
   if (c < C) {
     const float g = g1[c];
@@ -598,10 +598,18 @@ __global__ __launch_bounds__(256) void fold_grad_finish_kernel(
   }
 }
 
+__global__ __launch_bounds__(256) void fold_grad_finish_kernel(
+    float* wsR, float* wsV, float* wsQ, const float* mcorr, const float* at,
+    const float* vt, const float* g1, float* dat, float* dvt, float* dg1, float* dg2, int nb,
+    int C) {
+  fold_grad_finish_body(wsR, wsV, wsQ, mcorr, at, vt, g1, dat, dvt, dg1, dg2, C, blockIdx.x,
+                        blockIdx.y);
+}
+
 // parameter grads of the fold: dWq, dWo
-__global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const float* kv,
-                                  const float* null_kv, float* dwq, float* dwo, int nb, int C,
-                                  float scale, int accumulate) {
+__device__ __forceinline__ void fold_bwd_w_body(const float* dat, const float* dvt, const float* kv,
+                                               const float* null_kv, float* dwq, float* dwo, int nb,
+                                               int C, float scale, int accumulate) {
   const long long n = (long long)NH * DH * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -626,16 +634,21 @@ __global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const floa
   }
 }
 
+__global__ void fold_bwd_w_kernel(const float* dat, const float* dvt, const float* kv,
+                                  const float* null_kv, float* dwq, float* dwo, int nb, int C,
+                                  float scale, int accumulate) {
+  fold_bwd_w_body(dat, dvt, kv, null_kv, dwq, dwo, nb, C, scale, accumulate);
+}
+
 // dK/dV of (b, h, all 3 keys) -> d(kv) (j >= 1) or dnull (j == 0).
 // grid (NH, nb, 2): z = 0 computes dK = scale * dat[:, hj]^T Wq_h^T (wave w owns
 // 16 head dims, lanes sweep c, wave reductions); z = 1 computes
 // dV = dvt[:, hj]^T Wo_h (lane = head dim, coalesced Wo rows, waves split c).
-__global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, const float* dvt,
-                                                          const float* wq, const float* wo,
-                                                          float* dkv, float* dnull, int C,
-                                                          float scale) {
+__device__ __forceinline__ void fold_bwd_kv_body(const float* dat, const float* dvt,
+                                                 const float* wq, const float* wo, float* dkv,
+                                                 float* dnull, int C, float scale, int h, int b,
+                                                 int part) {
   __shared__ float red[4][NK][DH];
-  const int h = blockIdx.x, b = blockIdx.y, part = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* datb = dat + (long long)b * C * HK + h * NK;
   const float* dvtb = dvt + (long long)b * C * HK + h * NK;
@@ -687,6 +700,13 @@ __global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, cons
   }
 }
 
+__global__ __launch_bounds__(256) void fold_bwd_kv_kernel(const float* dat, const float* dvt,
+                                                          const float* wq, const float* wo,
+                                                          float* dkv, float* dnull, int C,
+                                                          float scale) {
+  fold_bwd_kv_body(dat, dvt, wq, wo, dkv, dnull, C, scale, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
 template <typename T>
 int fold_t(const float* wq, const float* wo, const float* kv, const float* null_kv,
            const float* g1, float* at, float* vt, void* Kt, void* KtT, void* Vt, void* VtT,
@@ -700,6 +720,81 @@ int fold_t(const float* wq, const float* wo, const float* kv, const float* null_
 }
 
 }  // namespace
+
+// ---- batched fold backward: every block's fold gradients in four launches,
+// run once all blocks' token reductions are done (the kv gradients feed the
+// grouped to_kv backward, the rest are parameter gradients) ----
+struct FoldBwdBatch {
+  DvFoldBwdJob j[DV_FOLD_BWD_MAX];
+  int n;
+  float scale;
+};
+
+__global__ __launch_bounds__(256) void fold_mcorr_batched_kernel(FoldBwdBatch t) {
+  const DvFoldBwdJob& J = t.j[blockIdx.y];
+  const int row = blockIdx.x;
+  if (row >= J.nb * KP) return;
+  if (row == 0) {  // zero what the later launches accumulate into
+    if (!J.acc_g) {
+      for (int c = threadIdx.x; c < J.C; c += 256) {
+        if (J.dg1) J.dg1[c] = 0.f;
+        if (J.dg2) J.dg2[c] = 0.f;
+      }
+    }
+    if (!J.acc_w && threadIdx.x < 2 * DH) J.dnull[threadIdx.x] = 0.f;
+  }
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int c = threadIdx.x; c < J.C; c += 256) s += J.wsR[(long long)row * J.C + c];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) J.mcorr[row] = (red[0] + red[1] + red[2] + red[3]) / J.C;
+}
+
+__global__ __launch_bounds__(256) void fold_grad_finish_batched_kernel(FoldBwdBatch t) {
+  const DvFoldBwdJob& J = t.j[blockIdx.z];
+  if ((int)blockIdx.x * 64 >= J.C || (int)blockIdx.y >= J.nb) return;
+  fold_grad_finish_body(J.wsR, J.wsV, J.wsQ, J.mcorr, J.at, J.vt, J.g1, J.dat, J.dvt, J.dg1, J.dg2,
+                        J.C, blockIdx.x, blockIdx.y);
+}
+
+__global__ void fold_bwd_w_batched_kernel(FoldBwdBatch t) {
+  const DvFoldBwdJob& J = t.j[blockIdx.y];
+  fold_bwd_w_body(J.dat, J.dvt, J.kv, J.null_kv, J.dwq, J.dwo, J.nb, J.C, t.scale, J.acc_w);
+}
+
+__global__ __launch_bounds__(256) void fold_bwd_kv_batched_kernel(FoldBwdBatch t) {
+  const DvFoldBwdJob& J = t.j[blockIdx.z >> 1];
+  if ((int)blockIdx.y >= J.nb) return;
+  fold_bwd_kv_body(J.dat, J.dvt, J.wq, J.wo, J.dkv, J.dnull, J.C, t.scale, blockIdx.x, blockIdx.y,
+                   blockIdx.z & 1);
+}
+
+extern "C" int dv_xattn_fold_bwd_batched(const DvFoldBwdJob* jobs, int n, float scale,
+                                         void* stream) {
+  DV_REQUIRE(jobs && n >= 0 && n <= DV_FOLD_BWD_MAX, "bad job table");
+  if (n == 0) return DV_OK;
+  FoldBwdBatch t;
+  t.n = n;
+  t.scale = scale;
+  int nbmax = 0, cmax = 0;
+  for (int i = 0; i < n; ++i) {
+    const DvFoldBwdJob& J = jobs[i];
+    DV_REQUIRE(J.wsR && J.wsV && J.wsQ && J.mcorr && J.at && J.vt && J.g1 && J.wq && J.wo && J.kv &&
+                   J.null_kv && J.dat && J.dvt && J.dwq && J.dwo && J.dkv && J.dnull, "null pointer");
+    DV_REQUIRE(J.nb > 0 && J.C > 0 && J.C <= 512, "bad job shape");
+    t.j[i] = J;
+    nbmax = std::max(nbmax, J.nb);
+    cmax = std::max(cmax, J.C);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  fold_mcorr_batched_kernel<<<dim3(nbmax * KP, n), 256, 0, st>>>(t);
+  fold_grad_finish_batched_kernel<<<dim3((cmax + 63) / 64, nbmax, n), 256, 0, st>>>(t);
+  fold_bwd_w_batched_kernel<<<dim3(grid_for((long long)NH * DH * cmax), n), 256, 0, st>>>(t);
+  fold_bwd_kv_batched_kernel<<<dim3(NH, nbmax, 2 * n), 256, sizeof(float) * 3 * cmax, st>>>(t);
+  return check_launch("xattn_fold_bwd_batched");
+}
 
 extern "C" int dv_xattn_fold_batched(int dtype, const DvFoldJob* jobs, int n, float scale,
                                      void* stream) {

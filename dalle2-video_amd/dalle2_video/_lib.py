@@ -29,6 +29,7 @@ _SIGS = {
     "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_conv_fwd8": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_xattn_fold_batched": [_I, _P, _I, _F, _P],
+    "dv_xattn_fold_bwd_batched": [_P, _I, _F, _P],
     "dv_conv_wgrad_ws": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_conv_wgrad": [_I, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],

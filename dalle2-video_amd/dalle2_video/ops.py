@@ -214,10 +214,12 @@ def _wgrad_workspace(dname, nf, h, w, cin, c0, split, cout, ks, device):
 _XA_WS = {}
 
 
-def _xattn_workspace(nb, C, device):
+def _xattn_workspace(nb, C, device, owner=None):
     """Cross-attention backward accumulators (wsR, wsV, wsQ [nb][32][C]): zero
-    on entry, re-zeroed by dv_xattn_fold_bwd after use; mcorr [nb][32] scratch."""
-    key = (nb, C, str(device))
+    on entry, re-zeroed by dv_xattn_fold_bwd after use; mcorr [nb][32] scratch.
+    `owner` (a block's parameter) gives the block its own set, for fold
+    backwards deferred into one batched launch."""
+    key = (nb, C, str(device), None if owner is None else id(owner))
     if key not in _XA_WS:
         _XA_WS[key] = tuple(torch.zeros(nb, 32, C, dtype=torch.float32, device=device) for _ in range(3)) + (
             torch.zeros(nb, 32, dtype=torch.float32, device=device),)
@@ -683,6 +685,7 @@ class LinearGroupFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *dys):
+        flush_fold_bwd()  # deferred cross-attention fold grads fill these dys
         xc, *wcs = ctx.saved_tensors
         act_in, n_lin = ctx.meta
         ws, bs = ctx.params[:n_lin], ctx.params[n_lin:]
@@ -757,6 +760,32 @@ def sinusoidal(times: torch.Tensor, dim: int) -> torch.Tensor:
 XA_HEADS, XA_DH = 8, 64
 
 
+class DvFoldBwdJob(ctypes.Structure):
+    """struct DvFoldBwdJob of dv_hip.h (dv_xattn_fold_bwd_batched)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wsR", "wsV", "wsQ", "mcorr", "at", "vt", "g1", "wq",
+                                               "wo", "kv", "null_kv", "dat", "dvt", "dg1", "dg2",
+                                               "dwq", "dwo", "dkv", "dnull")] + \
+               [("nb", ctypes.c_int), ("C", ctypes.c_int), ("acc_g", ctypes.c_int),
+                ("acc_w", ctypes.c_int)]
+
+
+# fold backwards deferred by CrossAttnFn.backward (blocks whose fold the Unet
+# batched, so kv comes from a grouped to_kv): (job, tensors kept alive)
+_FOLD_BWD_PENDING = []
+
+
+def flush_fold_bwd():
+    """Run every deferred fold backward in four launches (called by the grouped
+    to_kv backward, which consumes their kv gradients, before anything else)."""
+    global _FOLD_BWD_PENDING
+    pend, _FOLD_BWD_PENDING = _FOLD_BWD_PENDING, []
+    for i in range(0, len(pend), 20):  # DV_FOLD_BWD_MAX
+        part = pend[i:i + 20]
+        jobs = (DvFoldBwdJob * len(part))(*[j for j, _ in part])
+        call("dv_xattn_fold_bwd_batched", ctypes.cast(jobs, ctypes.c_void_p), len(part),
+             ctypes_float(XA_DH ** -0.5), stream())
+
+
 class DvFoldJob(ctypes.Structure):
     """struct DvFoldJob of dv_hip.h (dv_xattn_fold_batched)."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("wq", "wo", "kv", "null_kv", "g1", "at", "vt", "Kt",
@@ -783,6 +812,7 @@ class XattnFold:
         self.VtT = torch.empty(nb, 32, Cp, dtype=dtype, device=dev)
         self.colsum = torch.empty(nb, 32, dtype=torch.float32, device=dev)
         self.nb, self.C, self.dtype = nb, C, dtype
+        self.batched = False  # set by xattn_fold_batched: backward may be deferred
 
     def job(self):
         return DvFoldJob(*(ptr(t).value for t in (self.wqf, self.wof, self.kv, self.nkv, self.g1f,
@@ -799,6 +829,8 @@ class XattnFold:
 def xattn_fold_batched(folds):
     """Run every block's fold in three launches (dv_xattn_fold_batched)."""
     folds = list(folds)
+    for f in folds:
+        f.batched = True
     for i in range(0, len(folds), 24):  # DV_FOLD_MAX
         part = folds[i:i + 24]
         jobs = (DvFoldJob * len(part))(*[f.job() for f in part])
@@ -834,7 +866,7 @@ class CrossAttnFn(torch.autograd.Function):
         ctx.save_for_backward(x, g1f, g2f, nkv, wqf, wof, kv, at, vt, KtT, Vt, VtT,
                               colsum, stats, pbuf)
         ctx.params = (g1, null_kv, wq, wo, g2)
-        ctx.meta = (nb, eps)
+        ctx.meta = (nb, eps, fold.batched)
         return out
 
     @staticmethod
@@ -842,7 +874,7 @@ class CrossAttnFn(torch.autograd.Function):
         (x, g1f, g2f, nkv, wqf, wof, kv, at, vt, KtT, Vt, VtT, colsum, stats,
          pbuf) = ctx.saved_tensors
         g1p, nullp, wqp, wop, g2p = ctx.params
-        nb, eps = ctx.meta
+        nb, eps, defer = ctx.meta
         nf, h, w, C = x.shape
         ntok = nf * h * w
         P = ntok // nb
@@ -852,7 +884,7 @@ class CrossAttnFn(torch.autograd.Function):
         dobuf = torch.empty(ntok, C, dtype=dtype, device=dev)
         dsbuf = torch.empty(ntok, 32, dtype=dtype, device=dev)
         p2buf = torch.empty(ntok, 32, dtype=dtype, device=dev)
-        wsR, wsV, wsQ, mcorr = _xattn_workspace(nb, C, dev)
+        wsR, wsV, wsQ, mcorr = _xattn_workspace(nb, C, dev, owner=wqp if defer else None)
         ldx = cl_ld(x)
         call("dv_xattn_bwd_tokens", dt(x), ptr(dy), C, ptr(x), ldx, ptr(dx), C, ntok, P, C,
              ptr(KtT), ptr(Vt), ptr(VtT), ptr(colsum), ptr(g2f), ptr(stats), ptr(pbuf), ptr(dobuf),
@@ -879,9 +911,18 @@ class CrossAttnFn(torch.autograd.Function):
         else:
             dwq, dwo, dnull, acc_w = torch.empty_like(wqf), torch.empty_like(wof), torch.empty_like(nkv), 0
         dkv = torch.empty_like(kv)
-        call("dv_xattn_fold_bwd", ptr(wsR), ptr(wsV), ptr(wsQ), ptr(mcorr), ptr(at), ptr(vt), ptr(g1f),
-             ptr(wqf), ptr(wof), ptr(kv), ptr(nkv), ptr(dat), ptr(dvt), ptr(dg1), ptr(dg2), ptr(dwq),
-             ptr(dwo), ptr(dkv), ptr(dnull), nb, C, ctypes_float(XA_DH ** -0.5), acc_g, acc_w, stream())
+        if defer:  # filled by flush_fold_bwd() before the grouped to_kv backward reads dkv
+            job = DvFoldBwdJob(*(ptr(t).value if t is not None else None
+                                 for t in (wsR, wsV, wsQ, mcorr, at, vt, g1f, wqf, wof, kv, nkv, dat,
+                                           dvt, dg1, dg2, dwq, dwo, dkv, dnull)),
+                               nb, C, acc_g, acc_w)
+            _FOLD_BWD_PENDING.append((job, (wsR, wsV, wsQ, mcorr, at, vt, g1f, wqf, wof, kv, nkv, dat,
+                                            dvt, dg1, dg2, dwq, dwo, dkv, dnull)))
+        else:
+            call("dv_xattn_fold_bwd", ptr(wsR), ptr(wsV), ptr(wsQ), ptr(mcorr), ptr(at), ptr(vt),
+                 ptr(g1f), ptr(wqf), ptr(wof), ptr(kv), ptr(nkv), ptr(dat), ptr(dvt), ptr(dg1),
+                 ptr(dg2), ptr(dwq), ptr(dwo), ptr(dkv), ptr(dnull), nb, C, ctypes_float(XA_DH ** -0.5),
+                 acc_g, acc_w, stream())
         return (dx, dkv, dg1 if ret_g else None, None if direct else dnull,
                 None if direct else dwq, None if direct else dwo,
                 dg2 if ret_g else None, None, None, None)

@@ -270,6 +270,34 @@ typedef struct DvFoldJob {
 } DvFoldJob;
 int dv_xattn_fold_batched(int dtype, const DvFoldJob* jobs, int n, float scale, void* stream);
 
+/* Fold gradients of many blocks in four launches: the same pointers and
+ * flags as dv_xattn_fold_bwd per job (host table, <= DV_FOLD_BWD_MAX).
+ * Run after every job's token reductions (ws_*) are complete.            */
+#define DV_FOLD_BWD_MAX 20
+typedef struct DvFoldBwdJob {
+  float* wsR;
+  float* wsV;
+  float* wsQ;
+  float* mcorr;
+  const float* at;
+  const float* vt;
+  const float* g1;
+  const float* wq;
+  const float* wo;
+  const float* kv;
+  const float* null_kv;
+  float* dat;
+  float* dvt;
+  float* dg1;
+  float* dg2;
+  float* dwq;
+  float* dwo;
+  float* dkv;
+  float* dnull;
+  int nb, C, acc_g, acc_w;
+} DvFoldBwdJob;
+int dv_xattn_fold_bwd_batched(const DvFoldBwdJob* jobs, int n, float scale, void* stream);
+
 /* ---- ResnetBlock3D cross attention (dalle2_video.py:159-162, 192-201;
  * dalle2-pytorch CrossAttention, 8 heads x 64, null kv + 2 time tokens, LN
  * before/after, residual).  Projections fold per clip b into C x 24
