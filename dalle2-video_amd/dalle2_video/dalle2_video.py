@@ -405,8 +405,8 @@ class Block3D(nn.Module):
         self.norm = nn.GroupNorm(groups, dim_out)
         self.act = nn.SiLU()
 
-    def forward_cl(self, x0, nb, x1=None, scale_shift=None, res=None):
-        z = ops.conv(x0, self.project.weight, self.project.bias, x1=x1)
+    def forward_cl(self, x0, nb, x1=None, scale_shift=None, res=None, sink=None):
+        z = ops.conv(x0, self.project.weight, self.project.bias, x1=x1, sink=sink)
         return ops.group_norm_act(z, self.norm.weight, self.norm.bias, nb, self.norm.num_groups,
                                   self.norm.eps, scale_shift=scale_shift, res=res, act=ACT_SILU)
 
@@ -440,16 +440,22 @@ class ResnetBlock3D(nn.Module):
         if ss is None and exists(self.time_mlp) and exists(time_emb):
             ss = ops.linear_group(time_emb, [self.time_mlp[1].weight], [self.time_mlp[1].bias],
                                   act_in=ACT_SILU)[0]
-        h = self.block1.forward_cl(x0, nb, x1=x1, scale_shift=ss)
-        if exists(self.cross_attn):
-            assert exists(cond)
-            h = self.cross_attn.forward_cl(h, cond, nb, kv=kv, fold=fold)
+        # block1's conv and res_conv read the same input: one shared dX buffer
+        # (ops.GradSink) instead of an autograd add of two input gradients
+        # res_conv runs first so that its (cheap, 1x1) input-gradient is the
+        # one that accumulates into block1's 3x3 dgrad output, not the reverse:
+        # autograd runs the later-recorded node's backward first
         if isinstance(self.res_conv, nn.Identity):
             if x1 is not None:
                 raise DVError("identity residual with a split input")
-            res = x0
+            sink, res = None, x0
         else:
-            res = ops.conv(x0, self.res_conv.weight, self.res_conv.bias, x1=x1)
+            sink = ops.GradSink()
+            res = ops.conv(x0, self.res_conv.weight, self.res_conv.bias, x1=x1, sink=sink)
+        h = self.block1.forward_cl(x0, nb, x1=x1, scale_shift=ss, sink=sink)
+        if exists(self.cross_attn):
+            assert exists(cond)
+            h = self.cross_attn.forward_cl(h, cond, nb, kv=kv, fold=fold)
         return self.block2.forward_cl(h, nb, res=res)
 
     def forward(self, x, time_emb=None, cond=None):

@@ -266,6 +266,22 @@ def gn_graph_boundary(device):
         _GN_WS[str(device)].reset()
 
 
+def _grad_view(t: torch.Tensor):
+    """(tensor, ld) of an incoming channels-last gradient: a channel slice of a
+    wider buffer (GradSink's dX split for x0 / x1) is used in place through its
+    pixel stride instead of being copied; anything else is made contiguous."""
+    if t.is_contiguous():
+        return t, t.shape[-1]
+    try:
+        ld = cl_ld(t)
+        if ld % 8 == 0 and t.data_ptr() % 16 == 0:
+            return t, ld
+    except _lib.DVError:
+        pass
+    t = t.contiguous()
+    return t, t.shape[-1]
+
+
 def _pad_channels(t: torch.Tensor, mult: int = 8) -> torch.Tensor:
     c = t.shape[-1]
     cp = (c + mult - 1) // mult * mult
@@ -360,11 +376,22 @@ def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int) -> tor
     return out
 
 
+class GradSink:
+    """Shared input-gradient buffer of two convolutions reading the same input
+    (ResnetBlock3D's block1 conv and res_conv, dalle2_video.py:170, 188-205):
+    the first backward to run keeps its dX here and returns None for the
+    input; the second adds its dgrad into that buffer in its epilogue (res =
+    y = dX) and returns the total -- no autograd accumulation kernel."""
+
+    def __init__(self):
+        self.dx = None
+
+
 class ConvFn(torch.autograd.Function):
     """y = conv_(1,k,k)(cat(x0, x1)) + bias (+ res).  dalle2_video.py:107 etc."""
 
     @staticmethod
-    def forward(ctx, x0, x1, weight, bias, res, ksize):
+    def forward(ctx, x0, x1, weight, bias, res, ksize, sink=None):
         require_gpu(x0, x1, weight, bias, res)
         nf, h, w, c0 = x0.shape
         c1 = 0 if x1 is None else x1.shape[3]
@@ -396,6 +423,7 @@ class ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x0, x1, weight)
         ctx.params = (weight, bias)
         ctx.meta = (ksize, c0, c1, bias is not None, res is not None)
+        ctx.sink = sink
         return y
 
     @staticmethod
@@ -405,30 +433,45 @@ class ConvFn(torch.autograd.Function):
         nf, h, w, _ = x0.shape
         cin = c0 + c1
         cout, cin_real = weight.shape[0], weight.shape[1]
-        dy8 = _pad_channels(dy.contiguous())
+        dyv, lddy = _grad_view(dy)
+        if dy.shape[3] % 8 == 0 and lddy % 8 == 0:
+            dy8 = dyv  # strided channel slices are read in place (ld = lddy)
+        else:
+            dy8 = _pad_channels(dyv.contiguous())
+            lddy = dy8.shape[3]
         cout8 = dy8.shape[3]
         dx0 = dx1 = dw = db = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            alloc = torch.empty if cin_real == cin else torch.zeros
-            dx = alloc(nf, h, w, cin, dtype=dy.dtype, device=dy.device)
+            sink = ctx.sink
+            acc = sink.dx if sink is not None else None  # second reader: add into the first's dX
+            if acc is not None:
+                dx = acc
+                sink.dx = None
+            else:
+                alloc = torch.empty if cin_real == cin else torch.zeros
+                dx = alloc(nf, h, w, cin, dtype=dy.dtype, device=dy.device)
+            rp, rld = (ptr(dx), cin) if acc is not None else (None, 0)
             m = nf * h * w
             flops = 2.0 * m * cin_real * cout8 * ksize * ksize
             nbytes = dy8.element_size() * m * (cin + cout8)
-            if window_ok(dy8, None, cout8, cout8, cin_real, cout8, cout8, cin, 0, ksize, h, w, nf):
+            if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, cin, 0, ksize, h, w, nf):
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 3)
                 _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
-                        lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd),
-                                     None, None, 0, ptr(dx), cin, nf, h, w, cout8, cin_real, ACT_NONE,
+                        lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd),
+                                     None, rp, rld, ptr(dx), cin, nf, h, w, cout8, cin_real, ACT_NONE,
                                      stream()))
             else:
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 1)
-                _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, cout8, ksize, h, w),
+                _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, lddy, ksize, h, w),
                         flops, nbytes,
-                        lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), cout8, cout8, None, 0, ptr(wpd), None,
-                                     None, 0, ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE,
+                        lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd), None,
+                                     rp, rld, ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE,
                                      stream()))
-            dx0 = dx[..., :c0]
-            dx1 = dx[..., c0:] if x1 is not None else None
+            if sink is not None and acc is None:
+                sink.dx = dx  # first reader: the other conv's backward adds into it
+            else:
+                dx0 = dx[..., :c0]
+                dx1 = dx[..., c0:] if x1 is not None else None
         wparam, bparam = ctx.params
         want_w = ctx.needs_input_grad[2]
         want_b = has_bias and ctx.needs_input_grad[3]
@@ -457,12 +500,12 @@ class ConvFn(torch.autograd.Function):
             ws = _wgrad_workspace(_lib.dtype_name(dy8), nf, h, w, cin, c0, x1 is not None, cout8,
                                   ksize, dy.device)
             kname = (conv_wgrad_name(dname, m, cout8, cin, c0, x1 is not None, ksize, h, w,
-                                     max(cout8, ld0, ld1)) if (cout8 == cout and cin_real == cin)
-                     else gemm_wgrad_name(dname, m, cout8, cin * ksize * ksize, max(cout8, ld0, ld1)))
+                                     max(lddy, ld0, ld1)) if (cout8 == cout and cin_real == cin)
+                     else gemm_wgrad_name(dname, m, cout8, cin * ksize * ksize, max(lddy, ld0, ld1)))
             _launch(kname,
                     2.0 * m * cout8 * cin * ksize * ksize,
                     dy8.element_size() * m * (cin + cout8),
-                    lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), cout8, ptr(x0), ld0, c0, ptr(x1), ld1,
+                    lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), lddy, ptr(x0), ld0, c0, ptr(x1), ld1,
                                  ptr(dw_t), int(acc_w), ptr(db_t), int(acc_b), ptr(ws), ws.numel(),
                                  nf, h, w, cin, cout8, cout, cin_real, ksize, stream()))
         elif want_b:
@@ -471,20 +514,21 @@ class ConvFn(torch.autograd.Function):
                 db_buf = torch.zeros(cout8, dtype=torch.float32, device=dy.device)
             else:
                 db_buf = bslot[0]
-            call("dv_bias_grad", dt(dy8), ptr(dy8), cout8, ptr(db_buf), nf * h * w, cout, stream())
+            call("dv_bias_grad", dt(dy8), ptr(dy8), lddy, ptr(db_buf), nf * h * w, cout, stream())
             if bslot is None:
                 db = db_buf[:cout]
             elif db_buf is not bslot[0]:
                 bslot[0].add_(db_buf[:cout])
         dres = dy if has_res else None
-        return dx0, dx1, dw, db, dres, None
+        return dx0, dx1, dw, db, dres, None, None
 
 
-def conv(x0, weight, bias=None, x1=None, res=None):
+def conv(x0, weight, bias=None, x1=None, res=None, sink=None):
     """(1,k,k) 'same' convolution over channels-last frames (weight in torch
-    Conv3d layout (cout, cin, 1, k, k) or Linear layout (cout, cin))."""
+    Conv3d layout (cout, cin, 1, k, k) or Linear layout (cout, cin)).
+    sink: a GradSink shared with the other conv reading (x0, x1)."""
     k = weight.shape[-1] if weight.dim() == 5 else 1
-    return ConvFn.apply(x0, x1, weight, bias, res, k)
+    return ConvFn.apply(x0, x1, weight, bias, res, k, sink)
 
 
 # ---------------------------------------------------------------------------
@@ -518,7 +562,7 @@ class GroupNormActFn(torch.autograd.Function):
         nf, h, w, c = z.shape
         P = (nf // nb) * h * w
         dev = z.device
-        dy = dy.contiguous()
+        dy, lddy = _grad_view(dy)
         dz = torch.empty(nf, h, w, c, dtype=z.dtype, device=dev)
         gs, bs = _grad_out(ctx.params[0]), _grad_out(ctx.params[1])
         # one accumulate flag for both: allocate fresh buffers where they differ
@@ -530,7 +574,7 @@ class GroupNormActFn(torch.autograd.Function):
             acc, ret = 0, True
         dss = torch.empty(nb, 2 * c, dtype=torch.float32, device=dev) if has_ss else None
         cur, nxt = _gn_sums(dev).take(nb * c * 2)
-        call("dv_gn_bwd", dt(z), ptr(dy), c, ptr(z), cl_ld(z), ptr(dz), c, nb, P, c, groups, ptr(g),
+        call("dv_gn_bwd", dt(z), ptr(dy), lddy, ptr(z), cl_ld(z), ptr(dz), c, nb, P, c, groups, ptr(g),
              ptr(b), ptr(s), act, ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(cur), ptr(nxt), nxt.numel(),
              acc, stream())
         if not ret:
@@ -879,18 +923,18 @@ class CrossAttnFn(torch.autograd.Function):
         ntok = nf * h * w
         P = ntok // nb
         dev, dtype = x.device, x.dtype
-        dy = dy.contiguous()
+        dy, lddy = _grad_view(dy)
         dx = torch.empty(nf, h, w, C, dtype=dtype, device=dev)
         dobuf = torch.empty(ntok, C, dtype=dtype, device=dev)
         dsbuf = torch.empty(ntok, 32, dtype=dtype, device=dev)
         p2buf = torch.empty(ntok, 32, dtype=dtype, device=dev)
         wsR, wsV, wsQ, mcorr = _xattn_workspace(nb, C, dev, owner=wqp if defer else None)
         ldx = cl_ld(x)
-        call("dv_xattn_bwd_tokens", dt(x), ptr(dy), C, ptr(x), ldx, ptr(dx), C, ntok, P, C,
+        call("dv_xattn_bwd_tokens", dt(x), ptr(dy), lddy, ptr(x), ldx, ptr(dx), C, ntok, P, C,
              ptr(KtT), ptr(Vt), ptr(VtT), ptr(colsum), ptr(g2f), ptr(stats), ptr(pbuf), ptr(dobuf),
              ptr(dsbuf), ptr(p2buf), stream())
         # per-batch token reductions: R = dS'^T X, V' = P^T dO, Q = P'^T dY (one batched GEMM each)
-        for a_, b_, ldb, o_ in ((dsbuf, x, ldx, wsR), (pbuf, dobuf, C, wsV), (p2buf, dy, C, wsQ)):
+        for a_, b_, ldb, o_ in ((dsbuf, x, ldx, wsR), (pbuf, dobuf, C, wsV), (p2buf, dy, lddy, wsQ)):
             _launch(gemm_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldb)),
                     2.0 * ntok * 32 * C, 0,
                     lambda a_=a_, b_=b_, ldb=ldb, o_=o_: call(
@@ -1011,11 +1055,11 @@ class SpaceToDepthFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        dy = dy.contiguous()
+        dy, ldd = _grad_view(dy)
         nf, H, W, C4 = dy.shape
         C = C4 // 4
         dx = torch.empty(nf, 2 * H, 2 * W, C, dtype=dy.dtype, device=dy.device)
-        call("dv_shuffle", dt(dy), 1, ptr(dy), C4, ptr(dx), C, None, 0, nf, H, W, C, 0, stream())
+        call("dv_shuffle", dt(dy), 1, ptr(dy), ldd, ptr(dx), C, None, 0, nf, H, W, C, 0, stream())
         return dx
 
 
@@ -1033,11 +1077,11 @@ class SiLUPixelShuffleFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (z,) = ctx.saved_tensors
-        dy = dy.contiguous()
+        dy, ldd = _grad_view(dy)
         nf, H, W, C4 = z.shape
         C = C4 // 4
         dz = torch.empty(nf, H, W, C4, dtype=z.dtype, device=z.device)
-        call("dv_shuffle", dt(z), 0, ptr(dy), C, ptr(dz), C4, ptr(z), cl_ld(z), nf, H, W, C, 0, stream())
+        call("dv_shuffle", dt(z), 0, ptr(dy), ldd, ptr(dz), C4, ptr(z), cl_ld(z), nf, H, W, C, 0, stream())
         return dz
 
 
