@@ -67,20 +67,36 @@ struct GnArgs {
 struct ChanCoef {
   float A, B, rs, zb, K1;
 };
+// The per-channel parameters of sample b -- gamma, beta, 1 + FiLM scale,
+// FiLM shift -- staged in LDS as prm[0..C), [C..2C), [2C..3C), [3C..4C) by one
+// coalesced round of loads (not 4 x VEC dependent per-lane global loads in
+// every workgroup's prologue).
+constexpr int GN_CMAX = 1024;
+__device__ __forceinline__ void stage_params(const GnArgs& a, int b, float* prm) {
+  const float* ssb = a.ss ? a.ss + (long long)b * 2 * a.C : nullptr;
+  for (int c = threadIdx.x; c < a.C; c += 256) {
+    const float g = a.gamma[c], bt = a.beta[c];
+    const float sc = ssb ? 1.f + ssb[c] : 1.f, sh = ssb ? ssb[a.C + c] : 0.f;
+    prm[c] = g;
+    prm[a.C + c] = bt;
+    prm[2 * a.C + c] = sc;
+    prm[3 * a.C + c] = sh;
+  }
+}
+
 template <int VEC>
-__device__ __forceinline__ void load_coef(const GnArgs& a, int b, int cv, const float* mean,
-                                          const float* rstd, ChanCoef* k) {
+__device__ __forceinline__ void load_coef(const GnArgs& a, int cv, const float* mean,
+                                          const float* rstd, const float* prm, ChanCoef* k) {
 #pragma unroll
   for (int e = 0; e < VEC; ++e) {
     const int c = cv + e, g = c / (a.C / a.G);
     const float mu = mean[g], rs = rstd[g];
-    const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
-    const float sh = a.ss ? a.ss[(long long)b * 2 * a.C + a.C + c] : 0.f;
-    k[e].A = rs * a.gamma[c] * sc;
-    k[e].B = (a.beta[c] - mu * rs * a.gamma[c]) * sc + sh;
+    const float gm = prm[c], bt = prm[a.C + c], sc = prm[2 * a.C + c], sh = prm[3 * a.C + c];
+    k[e].A = rs * gm * sc;
+    k[e].B = (bt - mu * rs * gm) * sc + sh;
     k[e].rs = rs;
     k[e].zb = -mu * rs;
-    k[e].K1 = rs * sc * a.gamma[c];
+    k[e].K1 = rs * sc * gm;
   }
 }
 
@@ -95,13 +111,13 @@ __device__ __forceinline__ float silu_grad(float v) {
 // stay lightly contended.
 constexpr int GN_U = 4;
 
-template <typename T, int MODE>
+template <typename T, int MODE, int U>
 __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
-  constexpr int U = MODE == 0 ? 2 * GN_U : GN_U;
   constexpr int NL = MODE == 1 ? 2 : 1;  // tensors streamed (z, dy)
   __shared__ float sh[2][256 * VEC];
   __shared__ float smu[64], srs[64];
+  __shared__ float prm[MODE == 1 ? 4 * GN_CMAX : 1];
   const int tpr = a.C / VEC;                 // threads per pixel row
   const int rpp = 256 / tpr;                 // rows per pass
   const int tid = threadIdx.x;
@@ -135,6 +151,7 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
     }
   }
   if (MODE == 1) {
+    stage_params(a, b, prm);
     for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
     __syncthreads();
   }
@@ -143,7 +160,7 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   for (int e = 0; e < VEC; ++e) s1[e] = s2[e] = 0.f;
   if (act_rows) {
     ChanCoef k[MODE == 1 ? VEC : 1];
-    if (MODE == 1) load_coef<VEC>(a, b, cv, smu, srs, k);
+    if (MODE == 1) load_coef<VEC>(a, cv, smu, srs, prm, k);
     for (; p0 < end; p0 += step) {
       if (p0 + step < end) load(p0 + step, nxt);
 #pragma unroll
@@ -172,7 +189,7 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
         for (int u = 0; u < U; ++u) cur[l][u] = nxt[l][u];
     }
   }
-  // block reduce over the row slots, then one atomic per channel
+  // block reduce over the row slots ([rpp][C] in LDS), then one atomic per channel
 #pragma unroll
   for (int e = 0; e < VEC; ++e) {
     sh[0][tid * VEC + e] = (rr < rpp) ? s1[e] : 0.f;
@@ -180,11 +197,10 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   }
   __syncthreads();
   for (int c = tid; c < a.C; c += 256) {
-    const int owner = c / VEC, e = c % VEC;
     float t1 = 0.f, t2 = 0.f;
     for (int r = 0; r < rpp; ++r) {
-      t1 += sh[0][(r * tpr + owner) * VEC + e];
-      t2 += sh[1][(r * tpr + owner) * VEC + e];
+      t1 += sh[0][r * a.C + c];
+      t2 += sh[1][r * a.C + c];
     }
     float* rs = a.sums + (blockIdx.x % a.R) * a.rstride;  // 1/R of the same-address contention
     atomicAdd(rs + ((long long)b * a.C + c) * 2, t1);
@@ -198,18 +214,22 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
 // then one wave per group (channel sums combined in double for the variance).
 //   MODE 0: t1 = mean, t2 = rstd      MODE 1: t1 = m1, t2 = m2
 template <int MODE>
-__device__ void gn_group_terms(const GnArgs& a, int b, float* cs, float* t1, float* t2) {
+__device__ void gn_group_terms(const GnArgs& a, int b, float* cs, float* prm, float* t1, float* t2) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cg = a.C / a.G;
   const long long sb = (long long)b * a.C * 2;
   for (int c = threadIdx.x; c < a.C; c += 256) {
+    float __attribute__((ext_vector_type(2))) v[8];  // all R (<= 8) replicas in flight at once
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      if (r < a.R) v[r] = *(const float __attribute__((ext_vector_type(2)))*)(a.sums + r * a.rstride + sb + 2 * c);
     float v1 = 0.f, v2 = 0.f;
-    for (int r = 0; r < a.R; ++r) {
-      v1 += a.sums[r * a.rstride + sb + 2 * c];
-      v2 += a.sums[r * a.rstride + sb + 2 * c + 1];
-    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      if (r < a.R) { v1 += v[r][0]; v2 += v[r][1]; }
     cs[c] = v1;
     cs[a.C + c] = v2;
   }
+  stage_params(a, b, prm);
   __syncthreads();
   for (int g = wave; g < a.G; g += 4) {
     if (MODE == 0) {
@@ -231,8 +251,7 @@ __device__ void gn_group_terms(const GnArgs& a, int b, float* cs, float* t1, flo
     } else {
       float m1 = 0.f, m2 = 0.f;
       for (int c = g * cg + lane; c < (g + 1) * cg; c += 64) {
-        const float sc = a.ss ? 1.f + a.ss[(long long)b * 2 * a.C + c] : 1.f;
-        const float k = a.gamma[c] * sc;
+        const float k = prm[c] * prm[2 * a.C + c];
         m1 += k * cs[c];
         m2 += k * cs[a.C + c];
       }
@@ -249,12 +268,12 @@ __device__ void gn_group_terms(const GnArgs& a, int b, float* cs, float* t1, flo
 
 // MODE 0: forward apply  out = act(v) (+ res)
 // MODE 1: backward apply out = dz = rs*(dv*(1+s)*g - m1 - zhat*m2)
-template <typename T, int MODE>
+template <typename T, int MODE, int U>
 __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
-  constexpr int U = GN_U;
   __shared__ float t1[64], t2[64], smu[64], srs[64];
-  __shared__ float cs[2 * 1024];  // this sample's per-channel totals
+  __shared__ float cs[2 * GN_CMAX];  // this sample's per-channel totals
+  __shared__ float prm[4 * GN_CMAX];
   const int tid = threadIdx.x;
   const int tpr = a.C / VEC, rpp = 256 / tpr;
   const int rr = tid / tpr, cv = (tid % tpr) * VEC;
@@ -281,7 +300,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   };
   long long p0 = beg + rr;
   load(p0, zc, xc);  // the first batch is in flight across the prologue
-  gn_group_terms<MODE>(a, b, cs, t1, t2);
+  gn_group_terms<MODE>(a, b, cs, prm, t1, t2);
   if (MODE == 1)
     for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
   __syncthreads();
@@ -315,9 +334,9 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   ChanCoef k[VEC];
   float m1[VEC], m2[VEC];
   if (MODE == 0) {
-    load_coef<VEC>(a, b, cv, t1, t2, k);
+    load_coef<VEC>(a, cv, t1, t2, prm, k);
   } else {
-    load_coef<VEC>(a, b, cv, smu, srs, k);
+    load_coef<VEC>(a, cv, smu, srs, prm, k);
 #pragma unroll
     for (int e = 0; e < VEC; ++e) {
       const int g = (cv + e) / cg;
@@ -390,30 +409,66 @@ int gn_replicas(const GnArgs& a, int blocks_per_clip) {
   return std::max(r, 1);
 }
 
+// Launch shape knobs (A/B switches, read once): unroll depth U (pixel rows
+// in flight per lane) and the workgroup-count target of each pass.
+struct GnTune {
+  int ur0, ua0, ur1, ua1;   // U: fwd reduce / fwd apply / bwd reduce / bwd apply
+  long long tr0, ta0, tr1, ta1;
+};
+const GnTune& gn_tune() {
+  static const GnTune t = [] {
+    auto env = [](const char* n, long long d) {
+      const char* v = getenv(n);
+      return v && atoll(v) > 0 ? atoll(v) : d;
+    };
+    GnTune g;
+    g.ur0 = (int)env("DV_GN_UR0", 2 * GN_U); g.ua0 = (int)env("DV_GN_UA0", GN_U);
+    g.ur1 = (int)env("DV_GN_UR1", GN_U);     g.ua1 = (int)env("DV_GN_UA1", 2);
+    g.tr0 = env("DV_GN_TR0", 768);  g.ta0 = env("DV_GN_TA0", 1024);
+    g.tr1 = env("DV_GN_TR1", 768);  g.ta1 = env("DV_GN_TA1", 768);
+    return g;
+  }();
+  return t;
+}
+
+template <typename T, int MODE>
+void gn_reduce_launch(GnArgs& a, int u, long long target, hipStream_t st) {
+  const int VEC = 16 / sizeof(T);
+  a.rows_per_block = gn_rows(a, VEC, u, target);
+  dim3 g((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
+  a.R = gn_replicas(a, (int)g.x);
+  switch (u) {
+    case 2: gn_reduce_kernel<T, MODE, 2><<<g, 256, 0, st>>>(a); break;
+    case 4: gn_reduce_kernel<T, MODE, 4><<<g, 256, 0, st>>>(a); break;
+    default: gn_reduce_kernel<T, MODE, 8><<<g, 256, 0, st>>>(a); break;
+  }
+}
+
+template <typename T, int MODE>
+void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
+  const int VEC = 16 / sizeof(T);
+  a.rows_per_block = gn_rows(a, VEC, u, target);
+  dim3 g((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
+  switch (u) {
+    case 2: gn_apply_kernel<T, MODE, 2><<<g, 256, 0, st>>>(a); break;
+    case 8: gn_apply_kernel<T, MODE, 8><<<g, 256, 0, st>>>(a); break;
+    default: gn_apply_kernel<T, MODE, 4><<<g, 256, 0, st>>>(a); break;
+  }
+}
+
 template <typename T>
 int gn_fwd_t(GnArgs a, hipStream_t st) {
-  const int VEC = 16 / sizeof(T);
-  a.rows_per_block = gn_rows(a, VEC, 2 * GN_U, 768);
-  dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
-  a.R = gn_replicas(a, (int)g1.x);
-  gn_reduce_kernel<T, 0><<<g1, 256, 0, st>>>(a);
-  a.rows_per_block = gn_rows(a, VEC, GN_U, 1024);
-  dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
-  gn_apply_kernel<T, 0><<<g2, 256, 0, st>>>(a);
+  const GnTune& t = gn_tune();
+  gn_reduce_launch<T, 0>(a, t.ur0, t.tr0, st);
+  gn_apply_launch<T, 0>(a, t.ua0, t.ta0, st);
   return check_launch("gn_fwd");
 }
 
 template <typename T>
 int gn_bwd_t(GnArgs a, hipStream_t st) {
-  const int VEC = 16 / sizeof(T);
-  a.rows_per_block = gn_rows(a, VEC, GN_U, 768);
-  dim3 g1((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
-  a.R = gn_replicas(a, (int)g1.x);
-  gn_reduce_kernel<T, 1><<<g1, 256, 0, st>>>(a);
-  // 165 VGPRs -> 3 waves / SIMD: 768 workgroups are exactly one resident round
-  a.rows_per_block = gn_rows(a, VEC, GN_U, 768);
-  dim3 g2((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
-  gn_apply_kernel<T, 1><<<g2, 256, 0, st>>>(a);
+  const GnTune& t = gn_tune();
+  gn_reduce_launch<T, 1>(a, t.ur1, t.tr1, st);
+  gn_apply_launch<T, 1>(a, t.ua1, t.ta1, st);  // U=2 (123 VGPRs, 4 waves/SIMD) measured ahead of U=4
   return check_launch("gn_bwd");
 }
 
@@ -539,7 +594,7 @@ extern "C" int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, co
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && ldy % VEC == 0 && (!res || ldres % VEC == 0),
              "channel counts / strides must be multiples of 16 bytes");
-  DV_REQUIRE(C / VEC <= 256 && G <= 64, "C > 256 vectors or G > 64");
+  DV_REQUIRE(C <= GN_CMAX && G <= 64, "C > 1024 or G > 64");
   DV_REQUIRE(next != sums || !next, "next must not alias sums");
   GnArgs a{};
   a.z = z; a.ldz = ldz; a.out = y; a.ldo = ldy; a.res = res; a.ldres = ldres; a.nb = nb;
@@ -561,7 +616,7 @@ extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && lddy % VEC == 0 && lddz % VEC == 0,
              "channel counts / strides must be multiples of 16 bytes");
-  DV_REQUIRE(C / VEC <= 256 && G <= 64 && C % G == 0, "bad C / G");
+  DV_REQUIRE(C <= GN_CMAX && G <= 64 && C % G == 0, "bad C / G");
   DV_REQUIRE(next != sums || !next, "next must not alias sums");
   GnArgs a{};
   a.z = z; a.ldz = ldz; a.dy = dy; a.lddy = lddy; a.out = dz; a.ldo = lddz; a.nb = nb; a.P = P;
