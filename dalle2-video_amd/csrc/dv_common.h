@@ -85,8 +85,12 @@ __device__ __forceinline__ void lgkm_wait_tied(u32x4& v) {
 template <typename T> __device__ __forceinline__ float to_f(T v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f(float v) { return (T)v; }
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
-__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_exp_f32 + v_rcp_f32 (1 ulp), not the ~10-instruction IEEE divide: these
+// sit in the per-element loops of the GroupNorm passes and conv epilogues,
+// which are VALU-bound at their occupancy.  Large |x| saturates correctly
+// (rcp(inf) = 0).
+__device__ __forceinline__ float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
 
 // wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {
