@@ -100,6 +100,35 @@ __device__ __forceinline__ void load_coef(const GnArgs& a, int cv, const float* 
   }
 }
 
+// Pairs of channels on packed-f32 VALU (v_pk_fma/mul/add_f32); exp / rcp
+// stay per lane.  The element loops below are VALU-bound at their occupancy.
+typedef float __attribute__((ext_vector_type(2))) f2;
+__device__ __forceinline__ f2 sigmoid2(f2 v) {
+  const f2 m = v * -1.4426950408889634f;
+  const f2 d = 1.f + f2{__builtin_amdgcn_exp2f(m.x), __builtin_amdgcn_exp2f(m.y)};
+  return f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+// d silu(v) / dv = s * (1 + v * (1 - s))
+__device__ __forceinline__ f2 silu_grad2(f2 v) {
+  const f2 sg = sigmoid2(v);
+  return sg * (v * (1.f - sg) + 1.f);
+}
+// per-channel coefficients regrouped as channel pairs
+template <int VEC>
+struct Coef2 {
+  f2 A[VEC / 2], B[VEC / 2], rs[VEC / 2], zb[VEC / 2], K1[VEC / 2];
+  __device__ __forceinline__ void set(const ChanCoef* k) {
+#pragma unroll
+    for (int j = 0; j < VEC / 2; ++j) {
+      A[j] = f2{k[2 * j].A, k[2 * j + 1].A};
+      B[j] = f2{k[2 * j].B, k[2 * j + 1].B};
+      rs[j] = f2{k[2 * j].rs, k[2 * j + 1].rs};
+      zb[j] = f2{k[2 * j].zb, k[2 * j + 1].zb};
+      K1[j] = f2{k[2 * j].K1, k[2 * j + 1].K1};
+    }
+  }
+};
+
 __device__ __forceinline__ float silu_grad(float v) {
   const float sg = sigmoid_f(v);
   return sg * (1.f + v * (1.f - sg));
@@ -111,7 +140,7 @@ __device__ __forceinline__ float silu_grad(float v) {
 // stay lightly contended.
 constexpr int GN_U = 4;
 
-template <typename T, int MODE, int U>
+template <typename T, int MODE, int U, bool SILU>
 __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int NL = MODE == 1 ? 2 : 1;  // tensors streamed (z, dy)
@@ -155,12 +184,16 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
     for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
     __syncthreads();
   }
-  float s1[VEC], s2[VEC];
+  f2 s1[VEC / 2], s2[VEC / 2];
 #pragma unroll
-  for (int e = 0; e < VEC; ++e) s1[e] = s2[e] = 0.f;
+  for (int j = 0; j < VEC / 2; ++j) s1[j] = s2[j] = f2{0.f, 0.f};
   if (act_rows) {
-    ChanCoef k[MODE == 1 ? VEC : 1];
-    if (MODE == 1) load_coef<VEC>(a, cv, smu, srs, prm, k);
+    Coef2<VEC> k2;
+    if (MODE == 1) {
+      ChanCoef k[VEC];
+      load_coef<VEC>(a, cv, smu, srs, prm, k);
+      k2.set(k);
+    }
     for (; p0 < end; p0 += step) {
       if (p0 + step < end) load(p0 + step, nxt);
 #pragma unroll
@@ -170,16 +203,21 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
         Vec<T>::to_f(cur[0][u], z);
         if (MODE == 0) {
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) { s1[e] += z[e]; s2[e] += z[e] * z[e]; }
+          for (int j = 0; j < VEC / 2; ++j) {
+            const f2 zz{z[2 * j], z[2 * j + 1]};
+            s1[j] += zz;
+            s2[j] += zz * zz;
+          }
         } else {
           float dy[VEC];
           Vec<T>::to_f(cur[NL - 1][u], dy);
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) {
-            const float v = z[e] * k[e].A + k[e].B;
-            const float dv = a.act == DV_ACT_SILU ? dy[e] * silu_grad(v) : dy[e];
-            s1[e] += dv;
-            s2[e] += dv * (z[e] * k[e].rs + k[e].zb);
+          for (int j = 0; j < VEC / 2; ++j) {
+            const f2 zz{z[2 * j], z[2 * j + 1]}, dd{dy[2 * j], dy[2 * j + 1]};
+            f2 dv = dd;
+            if (SILU) dv *= silu_grad2(zz * k2.A[j] + k2.B[j]);
+            s1[j] += dv;
+            s2[j] += dv * (zz * k2.rs[j] + k2.zb[j]);
           }
         }
       }
@@ -192,8 +230,8 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   // block reduce over the row slots ([rpp][C] in LDS), then one atomic per channel
 #pragma unroll
   for (int e = 0; e < VEC; ++e) {
-    sh[0][tid * VEC + e] = (rr < rpp) ? s1[e] : 0.f;
-    sh[1][tid * VEC + e] = (rr < rpp) ? s2[e] : 0.f;
+    sh[0][tid * VEC + e] = (rr < rpp) ? s1[e / 2][e % 2] : 0.f;
+    sh[1][tid * VEC + e] = (rr < rpp) ? s2[e / 2][e % 2] : 0.f;
   }
   __syncthreads();
   for (int c = tid; c < a.C; c += 256) {
@@ -268,7 +306,7 @@ __device__ void gn_group_terms(const GnArgs& a, int b, float* cs, float* prm, fl
 
 // MODE 0: forward apply  out = act(v) (+ res)
 // MODE 1: backward apply out = dz = rs*(dv*(1+s)*g - m1 - zhat*m2)
-template <typename T, int MODE, int U>
+template <typename T, int MODE, int U, bool SILU>
 __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float t1[64], t2[64], smu[64], srs[64];
@@ -331,18 +369,28 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
     }
   }
   if (!act_rows) return;
-  ChanCoef k[VEC];
-  float m1[VEC], m2[VEC];
-  if (MODE == 0) {
-    load_coef<VEC>(a, cv, t1, t2, prm, k);
-  } else {
-    load_coef<VEC>(a, cv, smu, srs, prm, k);
+  Coef2<VEC> k2;
+  f2 m1[VEC / 2], m2[VEC / 2];
+  {
+    ChanCoef k[VEC];
+    float n1[VEC], n2[VEC];
+    if (MODE == 0) {
+      load_coef<VEC>(a, cv, t1, t2, prm, k);
+    } else {
+      load_coef<VEC>(a, cv, smu, srs, prm, k);
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      const int g = (cv + e) / cg;
-      m1[e] = -k[e].rs * t1[g];
-      m2[e] = -k[e].rs * t2[g];
+      for (int e = 0; e < VEC; ++e) {
+        const int g = (cv + e) / cg;
+        n1[e] = -k[e].rs * t1[g];
+        n2[e] = -k[e].rs * t2[g];
+      }
+#pragma unroll
+      for (int j = 0; j < VEC / 2; ++j) {
+        m1[j] = f2{n1[2 * j], n1[2 * j + 1]};
+        m2[j] = f2{n2[2 * j], n2[2 * j + 1]};
+      }
     }
+    k2.set(k);
   }
   for (; p0 < end; p0 += step) {
     if (p0 + step < end) load(p0 + step, zn, xn);
@@ -353,26 +401,29 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
       float z[VEC], o[VEC];
       Vec<T>::to_f(zc[u], z);
       if (MODE == 0) {
+        float r[VEC];
+        if (has_x) Vec<T>::to_f(xc[u], r);
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          const float v = z[e] * k[e].A + k[e].B;
-          o[e] = a.act == DV_ACT_SILU ? silu_f(v) : v;
-        }
-        if (has_x) {
-          float r[VEC];
-          Vec<T>::to_f(xc[u], r);
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) o[e] += r[e];
+        for (int j = 0; j < VEC / 2; ++j) {
+          const f2 zz{z[2 * j], z[2 * j + 1]};
+          f2 v = zz * k2.A[j] + k2.B[j];
+          if (SILU) v *= sigmoid2(v);
+          if (has_x) v += f2{r[2 * j], r[2 * j + 1]};
+          o[2 * j] = v.x;
+          o[2 * j + 1] = v.y;
         }
       } else {
         float dy[VEC];
         Vec<T>::to_f(xc[u], dy);
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          const float v = z[e] * k[e].A + k[e].B;
-          const float dv = a.act == DV_ACT_SILU ? dy[e] * silu_grad(v) : dy[e];
-          const float zhat = z[e] * k[e].rs + k[e].zb;
-          o[e] = dv * k[e].K1 + m1[e] + zhat * m2[e];
+        for (int j = 0; j < VEC / 2; ++j) {
+          const f2 zz{z[2 * j], z[2 * j + 1]}, dd{dy[2 * j], dy[2 * j + 1]};
+          f2 dv = dd;
+          if (SILU) dv *= silu_grad2(zz * k2.A[j] + k2.B[j]);
+          const f2 zhat = zz * k2.rs[j] + k2.zb[j];
+          const f2 v = dv * k2.K1[j] + m1[j] + zhat * m2[j];
+          o[2 * j] = v.x;
+          o[2 * j + 1] = v.y;
         }
       }
       st_vec<T>((T*)a.out + (pb + p) * a.ldo + cv, o);
@@ -437,11 +488,15 @@ void gn_reduce_launch(GnArgs& a, int u, long long target, hipStream_t st) {
   a.rows_per_block = gn_rows(a, VEC, u, target);
   dim3 g((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   a.R = gn_replicas(a, (int)g.x);
+  const bool silu = a.act == DV_ACT_SILU;
+#define DV_GN_RED(UU) (silu ? gn_reduce_kernel<T, MODE, UU, true><<<g, 256, 0, st>>>(a) \
+                            : gn_reduce_kernel<T, MODE, UU, false><<<g, 256, 0, st>>>(a))
   switch (u) {
-    case 2: gn_reduce_kernel<T, MODE, 2><<<g, 256, 0, st>>>(a); break;
-    case 4: gn_reduce_kernel<T, MODE, 4><<<g, 256, 0, st>>>(a); break;
-    default: gn_reduce_kernel<T, MODE, 8><<<g, 256, 0, st>>>(a); break;
+    case 2: DV_GN_RED(2); break;
+    case 4: DV_GN_RED(4); break;
+    default: DV_GN_RED(8); break;
   }
+#undef DV_GN_RED
 }
 
 template <typename T, int MODE>
@@ -449,11 +504,15 @@ void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
   a.rows_per_block = gn_rows(a, VEC, u, target);
   dim3 g((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
+  const bool silu = a.act == DV_ACT_SILU;
+#define DV_GN_APP(UU) (silu ? gn_apply_kernel<T, MODE, UU, true><<<g, 256, 0, st>>>(a) \
+                            : gn_apply_kernel<T, MODE, UU, false><<<g, 256, 0, st>>>(a))
   switch (u) {
-    case 2: gn_apply_kernel<T, MODE, 2><<<g, 256, 0, st>>>(a); break;
-    case 8: gn_apply_kernel<T, MODE, 8><<<g, 256, 0, st>>>(a); break;
-    default: gn_apply_kernel<T, MODE, 4><<<g, 256, 0, st>>>(a); break;
+    case 2: DV_GN_APP(2); break;
+    case 8: DV_GN_APP(8); break;
+    default: DV_GN_APP(4); break;
   }
+#undef DV_GN_APP
 }
 
 template <typename T>
