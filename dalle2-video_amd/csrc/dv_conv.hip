@@ -917,13 +917,27 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
     __syncthreads();
     const int orow = taps * pad;
     const long long ob = (long long)co0 * orow;
-    for (int i = threadIdx.x; i < rn * orow; i += 256) {
-      const int rl = i / orow, j = i - rl * orow;
-      int tap, ci;
-      pack_col(j, taps, pad, chunked, tap, ci);
-      const float v = ci < cin ? sm[rl * row + ci * taps + tap] : 0.f;
-      if (bf) ((bf16*)e.out)[ob + i] = (bf16)v;
-      else ((float*)e.out)[ob + i] = v;
+    if (bf && pad % 8 == 0) {  // 8 consecutive outputs share (row, tap): one 16-B store
+      for (int i = threadIdx.x * 8; i < rn * orow; i += 256 * 8) {
+        const int rl = i / orow, j = i - rl * orow;
+        int tap, ci;
+        pack_col(j, taps, pad, chunked, tap, ci);
+        const float* r = sm + rl * row + tap;
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = ci + q < cin ? r[(ci + q) * taps] : 0.f;
+        *(bf16x8*)((bf16*)e.out + ob + i) =
+            bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+      }
+    } else {
+      for (int i = threadIdx.x; i < rn * orow; i += 256) {
+        const int rl = i / orow, j = i - rl * orow;
+        int tap, ci;
+        pack_col(j, taps, pad, chunked, tap, ci);
+        const float v = ci < cin ? sm[rl * row + ci * taps + tap] : 0.f;
+        if (bf) ((bf16*)e.out)[ob + i] = (bf16)v;
+        else ((float*)e.out)[ob + i] = v;
+      }
     }
   } else {
     int ct = PACK_TILE / (cout * taps);
@@ -937,13 +951,27 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
     __syncthreads();
     const int orow = taps * pad;
     const long long ob = (long long)ci0 * orow;
-    for (int i = threadIdx.x; i < cn * orow; i += 256) {
-      const int cl = i / orow, j = i - cl * orow;
-      int tapd, co;
-      pack_col(j, taps, pad, chunked, tapd, co);
-      const float v = co < cout ? sm[co * seg + cl * taps + (taps - 1 - tapd)] : 0.f;
-      if (bf) ((bf16*)e.out)[ob + i] = (bf16)v;
-      else ((float*)e.out)[ob + i] = v;
+    if (bf && pad % 8 == 0) {
+      for (int i = threadIdx.x * 8; i < cn * orow; i += 256 * 8) {
+        const int cl = i / orow, j = i - cl * orow;
+        int tapd, co;
+        pack_col(j, taps, pad, chunked, tapd, co);
+        const float* r = sm + cl * taps + (taps - 1 - tapd);
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = co + q < cout ? r[(co + q) * seg] : 0.f;
+        *(bf16x8*)((bf16*)e.out + ob + i) =
+            bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+      }
+    } else {
+      for (int i = threadIdx.x; i < cn * orow; i += 256) {
+        const int cl = i / orow, j = i - cl * orow;
+        int tapd, co;
+        pack_col(j, taps, pad, chunked, tapd, co);
+        const float v = co < cout ? sm[co * seg + cl * taps + (taps - 1 - tapd)] : 0.f;
+        if (bf) ((bf16*)e.out)[ob + i] = (bf16)v;
+        else ((float*)e.out)[ob + i] = v;
+      }
     }
   }
   __syncthreads();  // sm is reused by the next tile
