@@ -901,6 +901,7 @@ __device__ __forceinline__ void pack_col(int j, int taps, int pad, bool chunked,
 }
 constexpr int PACK_LDS = 8192;   // floats: the largest row / column group accepted
 constexpr int PACK_TILE = 8192;  // floats staged per tile (several rows when they are small)
+constexpr int PACK_CB = 64;      // dgrad tiles: output columns (co) per tile
 
 __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
   const int taps = e.taps, cin = e.cin, cout = e.cout, pad = e.pad_to;
@@ -940,37 +941,45 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
       }
     }
   } else {
-    int ct = PACK_TILE / (cout * taps);
-    if (ct < 1) ct = 1;
-    const int ci0 = tile * ct, cn = min(ct, cin - ci0);
-    const int seg = cn * taps;  // contiguous floats per co
-    for (int i = threadIdx.x; i < cout * seg; i += 256) {
-      const int co = i / seg, j = i - co * seg;
-      sm[i] = e.w[((long long)co * cin + ci0) * taps + j];
+    // 2-D tile: PACK_CB output columns (co) x ci_t input channels, so every
+    // co row contributes one contiguous ci_t * taps run (>= 256 B for 3x3)
+    // instead of a taps-long 36-B segment per (co, ci)
+    const int ci_t = max(1, PACK_TILE / (PACK_CB * taps));
+    const int nci = (cin + ci_t - 1) / ci_t;
+    const int co0 = (tile / nci) * PACK_CB, ci0 = (tile % nci) * ci_t;
+    const int cn = min(ci_t, cin - ci0);
+    const int con = max(0, min(PACK_CB, cout - co0));  // real co rows (0 in the pad-only tail)
+    const int seg = cn * taps;
+    for (int i = threadIdx.x; i < con * seg; i += 256) {
+      const int r = i / seg, j = i - r * seg;
+      sm[i] = e.w[((long long)(co0 + r) * cin + ci0) * taps + j];
     }
     __syncthreads();
-    const int orow = taps * pad;
-    const long long ob = (long long)ci0 * orow;
-    if (bf && pad % 8 == 0) {
-      for (int i = threadIdx.x * 8; i < cn * orow; i += 256 * 8) {
-        const int cl = i / orow, j = i - cl * orow;
-        int tapd, co;
-        pack_col(j, taps, pad, chunked, tapd, co);
+    const int cw = min(PACK_CB, pad - co0);  // columns of this tile
+    const int per_ci = taps * cw;
+    const long long orow = (long long)taps * pad;
+    auto ocol = [&](int tapd, int co) {
+      return chunked ? (co >> 4) * taps * 16 + tapd * 16 + (co & 15) : tapd * pad + co;
+    };
+    if (bf && pad % 8 == 0) {  // 8 consecutive co share (ci, tap): one 16-B store
+      for (int i = threadIdx.x * 8; i < cn * per_ci; i += 256 * 8) {
+        const int cl = i / per_ci, rem = i - cl * per_ci;
+        const int tapd = rem / cw, cc = rem - tapd * cw;
         const float* r = sm + cl * taps + (taps - 1 - tapd);
         float v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = co + q < cout ? r[(co + q) * seg] : 0.f;
-        *(bf16x8*)((bf16*)e.out + ob + i) =
+        for (int q = 0; q < 8; ++q) v[q] = cc + q < con ? r[(cc + q) * seg] : 0.f;
+        *(bf16x8*)((bf16*)e.out + (ci0 + cl) * orow + ocol(tapd, co0 + cc)) =
             bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
       }
     } else {
-      for (int i = threadIdx.x; i < cn * orow; i += 256) {
-        const int cl = i / orow, j = i - cl * orow;
-        int tapd, co;
-        pack_col(j, taps, pad, chunked, tapd, co);
-        const float v = co < cout ? sm[co * seg + cl * taps + (taps - 1 - tapd)] : 0.f;
-        if (bf) ((bf16*)e.out)[ob + i] = (bf16)v;
-        else ((float*)e.out)[ob + i] = v;
+      for (int i = threadIdx.x; i < cn * per_ci; i += 256) {
+        const int cl = i / per_ci, rem = i - cl * per_ci;
+        const int tapd = rem / cw, cc = rem - tapd * cw;
+        const float v = cc < con ? sm[cc * seg + cl * taps + (taps - 1 - tapd)] : 0.f;
+        const long long o = (ci0 + cl) * orow + ocol(tapd, co0 + cc);
+        if (bf) ((bf16*)e.out)[o] = (bf16)v;
+        else ((float*)e.out)[o] = v;
       }
     }
   }
@@ -978,11 +987,12 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
 }
 
 __device__ __forceinline__ int pack_tiles(const DvPackEntry& e) {
-  const int unit = ((e.mode & 1) == 0 ? e.cin : e.cout) * e.taps;
-  int per = PACK_TILE / unit;
-  if (per < 1) per = 1;
-  const int rows = (e.mode & 1) == 0 ? e.cout : e.cin;
-  return (rows + per - 1) / per;
+  if ((e.mode & 1) == 0) {
+    const int per = max(1, PACK_TILE / (e.cin * e.taps));
+    return (e.cout + per - 1) / per;
+  }
+  const int ci_t = max(1, PACK_TILE / (PACK_CB * e.taps));
+  return ((e.pad_to + PACK_CB - 1) / PACK_CB) * ((e.cin + ci_t - 1) / ci_t);
 }
 
 __global__ __launch_bounds__(256) void pack_weight_kernel(DvPackEntry e) {
