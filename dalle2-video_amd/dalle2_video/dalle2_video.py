@@ -485,7 +485,15 @@ class CrossEmbedLayer3D(nn.Module):
         ])
 
     def forward_cl(self, x):
-        return torch.cat([ops.conv(x, c.weight, c.bias) for c in self.convs], dim=-1)
+        # All kernels share the input: one conv with the smaller kernels
+        # zero-embedded at the centre of the largest window (same 'same'
+        # padding arithmetic) writes the channel concatenation directly. The
+        # (cout <= 64) MMA tile is then full, and the input is gathered once
+        # instead of once per kernel size.
+        kmax = max(c.weight.shape[-1] for c in self.convs)
+        w = torch.cat([F.pad(c.weight, [(kmax - c.weight.shape[-1]) // 2] * 4) for c in self.convs], dim=0)
+        b = torch.cat([c.bias for c in self.convs], dim=0)
+        return ops.conv(x, w, b, cache=False)
 
     def forward(self, x):
         b, c, t = x.shape[:3]

@@ -356,7 +356,7 @@ class PackCache:
 PACK = PackCache()
 
 
-def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int) -> torch.Tensor:
+def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int, cache: bool = True) -> torch.Tensor:
     if weight.dim() not in (2, 5) or (weight.dim() == 5 and weight.shape[-1] != weight.shape[-2]):
         raise _lib.DVError(f"conv weight must be (cout, cin) or (cout, cin, 1, k, k), got {tuple(weight.shape)}")
     cout, cin = weight.shape[0], weight.shape[1]
@@ -364,7 +364,7 @@ def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int) -> tor
     w = weight.detach()
     if w.dtype != torch.float32 or not w.is_contiguous():
         w = w.float().contiguous()
-    if PACK.enabled and w.data_ptr() == weight.data_ptr():
+    if cache and PACK.enabled and w.data_ptr() == weight.data_ptr():
         out, stale = PACK.lookup(weight, w, dtype, cout, cin, k, pad_to, mode)
         if not stale:
             return out
@@ -391,7 +391,7 @@ class ConvFn(torch.autograd.Function):
     """y = conv_(1,k,k)(cat(x0, x1)) + bias (+ res).  dalle2_video.py:107 etc."""
 
     @staticmethod
-    def forward(ctx, x0, x1, weight, bias, res, ksize, sink=None):
+    def forward(ctx, x0, x1, weight, bias, res, ksize, sink=None, cache=True):
         require_gpu(x0, x1, weight, bias, res)
         nf, h, w, c0 = x0.shape
         c1 = 0 if x1 is None else x1.shape[3]
@@ -408,13 +408,13 @@ class ConvFn(torch.autograd.Function):
         flops, nbytes = 2.0 * m * cout * cin * ksize * ksize, x0.element_size() * m * (cin + cout)
         if window_ok(x0, x1, cin, c0 if x1 is not None else cin, cout, ld0, ld1 or ld0, cout,
                      ldr, ksize, h, w, nf):
-            wp = pack_conv_weight(weight, x0.dtype, cin, 2)
+            wp = pack_conv_weight(weight, x0.dtype, cin, 2, cache)
             _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                     lambda: call("dv_conv_fwd8", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp),
                                  ptr(b), ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ACT_NONE,
                                  stream()))
         else:
-            wp = pack_conv_weight(weight, x0.dtype, cin, 0)
+            wp = pack_conv_weight(weight, x0.dtype, cin, 0, cache)
             _launch(conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
                                   max(ld0, ld1), ksize, h, w), flops, nbytes,
                     lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b),
@@ -424,6 +424,7 @@ class ConvFn(torch.autograd.Function):
         ctx.params = (weight, bias)
         ctx.meta = (ksize, c0, c1, bias is not None, res is not None)
         ctx.sink = sink
+        ctx.cache = cache
         return y
 
     @staticmethod
@@ -455,13 +456,13 @@ class ConvFn(torch.autograd.Function):
             flops = 2.0 * m * cin_real * cout8 * ksize * ksize
             nbytes = dy8.element_size() * m * (cin + cout8)
             if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, cin, 0, ksize, h, w, nf):
-                wpd = pack_conv_weight(weight, dy.dtype, cout8, 3)
+                wpd = pack_conv_weight(weight, dy.dtype, cout8, 3, ctx.cache)
                 _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                         lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd),
                                      None, rp, rld, ptr(dx), cin, nf, h, w, cout8, cin_real, ACT_NONE,
                                      stream()))
             else:
-                wpd = pack_conv_weight(weight, dy.dtype, cout8, 1)
+                wpd = pack_conv_weight(weight, dy.dtype, cout8, 1, ctx.cache)
                 _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, lddy, ksize, h, w),
                         flops, nbytes,
                         lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd), None,
@@ -520,15 +521,17 @@ class ConvFn(torch.autograd.Function):
             elif db_buf is not bslot[0]:
                 bslot[0].add_(db_buf[:cout])
         dres = dy if has_res else None
-        return dx0, dx1, dw, db, dres, None, None
+        return dx0, dx1, dw, db, dres, None, None, None
 
 
-def conv(x0, weight, bias=None, x1=None, res=None, sink=None):
+def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True):
     """(1,k,k) 'same' convolution over channels-last frames (weight in torch
     Conv3d layout (cout, cin, 1, k, k) or Linear layout (cout, cin)).
-    sink: a GradSink shared with the other conv reading (x0, x1)."""
+    sink: a GradSink shared with the other conv reading (x0, x1).
+    cache=False: the weight is rebuilt every call (not a parameter), so its
+    packed image is made on every call instead of kept in the PackCache."""
     k = weight.shape[-1] if weight.dim() == 5 else 1
-    return ConvFn.apply(x0, x1, weight, bias, res, k, sink)
+    return ConvFn.apply(x0, x1, weight, bias, res, k, sink, cache)
 
 
 # ---------------------------------------------------------------------------
