@@ -833,7 +833,11 @@ template <int BMC, int BNK>
 int launch_wgrad_glds(WgradGArgs a, hipStream_t st) {
   const int mt = (a.cout + BMC - 1) / BMC, nt = (a.K + BNK - 1) / BNK;
   static const long long target = getenv("DV_WGRAD_TARGET") ? atoll(getenv("DV_WGRAD_TARGET")) : 512;
-  long long want = target / ((long long)mt * nt);
+  // many K tiles (the 15x15 init conv: K = 1800) make the im2col gather the
+  // cost: 4x the workgroups there (measured 244 -> 179 us); a one- or two-tile
+  // output keeps 512 (more splits only add same-address atomics: 43 -> 65 us)
+  const long long tiles = (long long)mt * nt;
+  long long want = (tiles >= 8 ? 4 * target : target) / tiles;
   if (want < 1) want = 1;
   long long per = ((long long)a.M + want - 1) / want;
   per = ((per + 255) / 256) * 256;
