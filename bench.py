@@ -1,18 +1,24 @@
 #!/usr/bin/env python3
 """Unet3D denoise-steps/sec on MI355X (BASELINE.json metric).
 
-One step = one pass of the hot path over one batch: VideoDecoderTrainer
-(video, unet_number=1) + update(1), i.e. p_losses forward + backward of unet1
-(dim 64, mults 1/2/4/8) on a synthetic 16x64x64 clip batch of 4 per GPU, the
-RCCL gradient all-reduce (N>1) and the fused AdamW update — bf16 activations,
-f32 master weights.  Weights: deterministic non-zero fill; data: synthetic
-U[0,1] clips resident in HBM.
+One step = one pass of the hot path over one batch (BASELINE config 2):
+VideoDecoderTrainer(video, unet_number=1) + update(1), i.e. p_losses forward +
+backward of unet1 (dim 64, mults 1/2/4/8) on a synthetic 16x64x64 clip batch
+of 4 per GPU, the RCCL gradient all-reduce (N>1) and the fused AdamW update —
+bf16 activations, f32 master weights.  Weights: deterministic non-zero fill;
+data: synthetic U[0,1] clips resident in HBM.
 
   python bench.py --gpus N --steps K --warmup W      (N>1 under torch.distributed.run)
 
-Rank 0 prints ONE JSON line.  Extra objects: `roofline` (dominant kernel,
-timed live with HIP events on its launch stream) and `cpu_baseline` (the f32
-CPU oracle timed on the host cores, rank 0 at N=1 only).
+Rank 0 prints ONE JSON line.  Extra objects:
+  roofline      dominant kernel (HIP events on its launch stream, live)
+  conv_shapes   the same per (kernel, GEMM shape) — the actionable rows
+  attention     mid MQA QK^T/PV fwd+bwd vs the bf16 MFMA peak (north-star target)
+  fp32          the same training step in the reference's f32 arithmetic
+  sampling      DDPM denoise steps (one Unet3D forward + posterior update,
+                HIP-graph replay) at 16x64x64 bs=4 and bs=1, and the config-4
+                cascade (base 16x64x64 + SR unet2 to 256x256, 250 steps each)
+  cpu_baseline  the f32 CPU oracle on the host cores (rank 0 at N=1 only)
 """
 import argparse
 import json
@@ -30,6 +36,12 @@ METRIC = "Unet3D denoise-steps/sec, 16f×64×64 clip bs=4; 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2516.6   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 STEP_TFLOP = 3.491          # ~3x the 1,163.6 GFLOP forward contractions
+FWD_TFLOP = 1.1636          # Cfg2 forward contractions (bs=4)
+
+
+def log(*a):
+    """Progress on stderr (stdout carries only the JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
 
 
 def parse():
@@ -43,9 +55,16 @@ def parse():
     ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: torch's default, i.e. OMP_NUM_THREADS = this "
+                         "process's CPU share: 16 per GPU on the MI355X box, whose sched_getaffinity "
+                         "lists all 256 host CPUs)")
     ap.add_argument("--no-graphs", action="store_true",
                     help="launch every kernel eagerly instead of replaying the captured HIP graph")
+    ap.add_argument("--no-sampling", action="store_true")
+    ap.add_argument("--no-fp32", action="store_true")
+    ap.add_argument("--sample-steps", type=int, default=250,
+                    help="DDPM steps of the sampling legs (config 4: 250)")
     return ap.parse_args()
 
 
@@ -66,11 +85,14 @@ def build(args, device):
 
 
 def cpu_baseline(args):
-    """f32 CPU oracle (reference-equivalent op graph) — one timed train step."""
+    """f32 CPU oracle (reference-equivalent op graph, oracle/dv_ref.py) on the
+    host cores: median of 3 Cfg2 train steps (p_losses fwd+bwd+clip+AdamW)
+    after 1 warm-up, and the config-1 forward (1x3x8x32x32) median of 5."""
+    import statistics
     from oracle import dv_ref as R
     from dalle2_video.utils import deterministic_fill_
 
-    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    threads = args.cpu_threads or torch.get_num_threads()
     torch.set_num_threads(threads)
     u = R.Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
     deterministic_fill_(u)
@@ -81,15 +103,30 @@ def cpu_baseline(args):
     t = torch.randint(0, 1000, (args.batch,), generator=g)
     noise = torch.randn(x.shape, generator=g)
     R.train_step(u, sched, opt, x, t, noise)  # warm-up
-    n = 2
-    t0 = time.perf_counter()
-    for _ in range(n):
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
         R.train_step(u, sched, opt, x, t, noise)
-    dt = (time.perf_counter() - t0) / n
+        times.append(time.perf_counter() - t0)
+        log(f"cpu train step {times[-1]:.2f} s")
+    dt = statistics.median(times)
+    # config 1: a single Unet3D forward on an 8-frame 32x32 clip, bs=1
+    x1 = torch.randn(1, 3, 8, 32, 32, generator=g)
+    t1 = torch.randint(0, 1000, (1,), generator=g)
+    with torch.no_grad():
+        u(x1, t1)
+        f1 = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            u(x1, t1)
+            f1.append(time.perf_counter() - t0)
     return {"value": round(1.0 / dt, 5), "unit": "denoise-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} timed train steps (p_losses fwd+bwd+AdamW, f32) of the CPU oracle at "
-                      f"{args.frames}x{args.size}x{args.size} bs={args.batch} after 1 warm-up step "
-                      f"({dt:.2f} s each)"}
+            "sample": f"median of 3 timed train steps (p_losses fwd+bwd+clip+AdamW, f32) of the CPU "
+                      f"oracle at {args.frames}x{args.size}x{args.size} bs={args.batch} after 1 warm-up "
+                      f"step ({dt:.2f} s each; {[round(v, 2) for v in times]})",
+            "config1_forward_s": round(statistics.median(f1), 4),
+            "config1_sample": "config 1 (BASELINE configs[0]): Unet3D forward, random 1x3x8x32x32 clip, "
+                              "median of 5 after 1 warm-up"}
 
 
 def kernel_key(name):
@@ -129,6 +166,99 @@ def pmc_traffic(name):
         if kernel_key(k) == want:
             return v.get("traffic_bytes")
     return None
+
+
+def fp32_leg(args, device):
+    """The same training step in the reference's arithmetic (f32 activations,
+    exact f32 MFMA): 3 warm-up + 5 timed steps."""
+    import copy
+    a = copy.copy(args)
+    a.dtype = "fp32"
+    dec, trainer = build(a, device)
+    g = torch.Generator(device=device).manual_seed(4321)
+    video = torch.rand(a.batch, 3, a.frames, a.size, a.size, device=device, generator=g)
+
+    def step():
+        trainer(video=video, unet_number=1)
+        trainer.update(1)
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    n = 5
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    sps = n / (time.perf_counter() - t0)
+    del dec, trainer
+    return {"value": round(sps, 3), "unit": "denoise-steps/s", "dtype": "fp32", "steps": n,
+            "ms_per_step": round(1e3 / sps, 3),
+            "mfma_frac": round(STEP_TFLOP * sps / PEAK_F32_TFLOPS, 4),
+            "peak": PEAK_F32_TFLOPS, "note": "f32 activations and f32 MFMA (v_mfma_f32_32x32x2f32); "
+                                             "frac against the dense f32 MFMA peak"}
+
+
+def sampling_leg(args, device):
+    """DDPM sampling (p_sample_loop_ddpm, dalle2_video.py:1667-1755): every
+    denoise step is one Unet3D forward + the posterior update, replayed from
+    one captured HIP graph.  Times whole sample() calls (including the two
+    eager steps and the capture), bf16 autocast."""
+    from dalle2_video.dalle2_video import Unet3D, VideoDecoder
+    from dalle2_video.utils import deterministic_fill_
+
+    T = args.sample_steps
+    out = {"steps_per_loop": T, "dtype": "bf16", "unit": "denoise-steps/s",
+           "step": "one Unet3D forward + p_sample update (HIP-graph replay)"}
+    u = Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    dec = VideoDecoder(unet=(u,), frame_sizes=(args.size,), frame_numbers=(args.frames,),
+                       timesteps=T, learned_variance=False)
+    deterministic_fill_(dec.unets[0])
+    dec = dec.to(device)
+    for bs in (args.batch, 1):
+        emb = torch.randn(bs, 512, device=device)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            dec.sample(video_embed=emb, one_unet_in_gpu_at_time=False)  # warm-up loop
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            vid = dec.sample(video_embed=emb, one_unet_in_gpu_at_time=False)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+        assert torch.isfinite(vid).all(), "non-finite sample"
+        sps = T / dt
+        log(f"sampling bs={bs}: {sps:.1f} steps/s ({dt:.2f} s per {T}-step loop)")
+        fl = FWD_TFLOP * bs / 4
+        out[f"bs{bs}"] = {"value": round(sps, 2), "loop_s": round(dt, 3),
+                          "clip": [args.frames, args.size, args.size],
+                          "roofline": {"bound": "mfma", "achieved": round(fl * sps, 1),
+                                       "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                                       "frac": round(fl * sps / PEAK_BF16_TFLOPS, 4),
+                                       "flop_per_step": f"{fl:.4f}e12 (Cfg2 forward x bs/4)"}}
+    del dec, u
+    # config 4: two-stage cascade, base 16x64x64 + spatial-SR unet2 (dim 8, mults 1..16) to 256x256
+    u1 = Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    u2 = Unet3D(8, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8, 16))
+    dec = VideoDecoder(unet=(u1, u2), frame_sizes=(args.size, 256), frame_numbers=(args.frames, args.frames),
+                       timesteps=T, learned_variance=False)
+    for un in dec.unets:
+        deterministic_fill_(un)
+    dec = dec.to(device)
+    emb = torch.randn(1, 512, device=device)
+    log("cascade sampling ...")
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vid = dec.sample(video_embed=emb)  # reference defaults: one unet on the GPU at a time
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    assert vid.shape == (1, 3, args.frames, 256, 256) and torch.isfinite(vid).all()
+    out["cascade"] = {"config": f"BASELINE config 4: base {args.frames}x{args.size}x{args.size} + SR to "
+                                f"{args.frames}x256x256, bs=1, {T}-step DDPM per stage, one unet on the GPU "
+                                "at a time (the reference's sample() default)",
+                      "seconds": round(dt, 3), "value": round(2 * T / dt, 2),
+                      "unit": "denoise-steps/s (both stages)"}
+    del dec
+    return out
 
 
 def main():
@@ -172,6 +302,7 @@ def main():
 
     roof = None
     kernels = None
+    conv_shapes = None
     attention = None
     if not args.no_roofline:
         # live per-launch HIP-event timing of every conv kernel over K more steps
@@ -181,7 +312,6 @@ def main():
             step()
         summ = ops.TIMER.summary()
         event_ovh_us = ops.TIMER.event_overhead_ms * 1e3
-        ops.TIMER = None
         name, d = max(summ.items(), key=lambda kv: kv[1]["ms"])
         peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
         avg_ms = d["ms"] / d["count"]
@@ -196,9 +326,21 @@ def main():
                 "event_overhead_us_subtracted": round(event_ovh_us, 2),
                 "avg_launch_us": round(avg_ms * 1e3, 2),
                 "algorithmic_flop_per_launch": round(d["flops"] / d["count"])}
-        kernels = {k: {"ms_per_step": round(v["ms"] / max(2, min(args.steps, 5)), 3),
+        nrep = max(2, min(args.steps, 5))
+        kernels = {k: {"ms_per_step": round(v["ms"] / nrep, 3),
                        "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
                    for k, v in sorted(summ.items(), key=lambda kv: -kv[1]["ms"])}
+        # per (kernel, pass, M, N, K) rows: the roofline of every conv GEMM shape
+        conv_shapes = []
+        for (k, shp), v in sorted(ops.TIMER.summary(by_shape=True).items(), key=lambda kv: -kv[1]["ms"]):
+            if shp is None:
+                continue
+            tf = v["flops"] / (v["ms"] * 1e-3) / 1e12
+            conv_shapes.append({"kernel": k, "pass": shp[0], "M": shp[1], "N": shp[2], "K": shp[3],
+                                "launches_per_step": v["count"] // nrep,
+                                "us_per_launch": round(v["ms"] / v["count"] * 1e3, 2),
+                                "ms_per_step": round(v["ms"] / nrep, 3), "tflops": round(tf, 1),
+                                "frac": round(tf / peak, 4)})
         # north-star sub-metric: mid-attention QK^T/PV (fwd + bwd) vs the bf16 MFMA peak
         att = [v for k, v in summ.items() if k.startswith("attn:")]
         if att:
@@ -209,10 +351,22 @@ def main():
                          "flop_per_step": round(fl / nrep), "ms_per_step": round(ms / nrep, 4),
                          "achieved": round(fl / (ms * 1e-3) / 1e12, 1), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4)}
+        ops.TIMER = None
+
+    log(f"train: {args.steps / elapsed:.2f} steps/s per GPU")
+    fp32 = None
+    if not args.no_fp32 and args.dtype == "bf16" and world == 1:
+        fp32 = fp32_leg(args, device)
+        log("fp32:", fp32["value"], "steps/s")
+    sampling = None
+    if not args.no_sampling and world == 1:
+        sampling = sampling_leg(args, device)
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline on", args.cpu_threads or torch.get_num_threads(), "threads")
         base = cpu_baseline(args)
+        log("cpu baseline:", base["value"], "steps/s")
 
     if rank == 0:
         sps = args.steps / elapsed  # per GPU
@@ -222,11 +376,14 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 / sps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.dtype, "data": "synthetic",
-            "config": {"workload": "unet1 train step: p_losses fwd+bwd + RCCL grad all-reduce + fused AdamW",
+            "config": {"workload": f"BASELINE config 2: unet1 (dim 64, mults 1/2/4/8) train step on a "
+                                   f"{args.frames}x{args.size}x{args.size} clip, bs={args.batch} per GPU: "
+                                   "p_losses fwd+bwd + RCCL grad all-reduce + fused AdamW",
                        "clip": [args.frames, args.size, args.size], "batch_per_gpu": args.batch,
                        "global_batch": args.batch * world, "parallelism": f"dp{world}"},
             "step_tflops_algorithmic": round(STEP_TFLOP * sps, 1),
-            "roofline": roof, "attention": attention, "cpu_baseline": base, "kernels": kernels,
+            "roofline": roof, "attention": attention, "fp32": fp32, "sampling": sampling,
+            "cpu_baseline": base, "kernels": kernels, "conv_shapes": conv_shapes[:30] if conv_shapes else None,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

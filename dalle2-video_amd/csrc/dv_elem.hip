@@ -112,14 +112,17 @@ __global__ void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* 
 template <typename T>
 __global__ void q_sample_kernel(const float* x0, const float* noise, const long long* t,
                                 const float* sa, const float* s1m, T* y, int B, int C, int T_,
-                                int HW, int cpad, int normalize) {
+                                int HW, int cpad, int normalize, int nt) {
   const long long npix = (long long)B * T_ * HW;
   GRID_STRIDE(p, npix) {
     const int hw = (int)(p % HW);
     const long long ft = p / HW;
     const int tt = (int)(ft % T_), b = (int)(ft / T_);
     const long long ti = t[b];
-    const float a = sa[ti], s = s1m[ti];
+    // a timestep outside the schedule poisons the output (NaN) instead of
+    // reading past the table (the reference's gather raises)
+    const bool ok = ti >= 0 && ti < nt;
+    const float a = ok ? sa[ti] : __builtin_nanf(""), s = ok ? s1m[ti] : __builtin_nanf("");
     for (int c = 0; c < cpad; ++c) {
       float v = 0.f;
       if (c < C) {
@@ -462,7 +465,7 @@ template <typename T>
 __global__ void p_sample_kernel(const float* x, const T* eps, int ld, const float* noise,
                                 const long long* t, const float* sra, const float* srm1,
                                 const float* c1, const float* c2, const float* logvar, float* out,
-                                float* x0_out, int B, int C, int T_, int HW, int clip) {
+                                float* x0_out, int B, int C, int T_, int HW, int clip, int nt) {
   const long long n = (long long)B * C * T_ * HW;
   GRID_STRIDE(i, n) {
     const int hw = (int)(i % HW);
@@ -470,15 +473,17 @@ __global__ void p_sample_kernel(const float* x, const T* eps, int ld, const floa
     const int tt = (int)(r % T_);
     r /= T_;
     const int c = (int)(r % C), b = (int)(r / C);
-    const long long ti = t[b];
+    const long long ti0 = t[b];
+    const bool ok = ti0 >= 0 && ti0 < nt;  // out-of-schedule t: NaN, no OOB read
+    const long long ti = ok ? ti0 : 0;
     const long long p = ((long long)b * T_ + tt) * HW + hw;
     const float e = ld > 0 ? (float)eps[p * ld + c] : ((const float*)eps)[i];
     float x0 = sra[ti] * x[i] - srm1[ti] * e;
     if (clip) x0 = fminf(fmaxf(x0, -1.f), 1.f);
     const float mean = c1[ti] * x0 + c2[ti] * x[i];
     const float nz = ti == 0 ? 0.f : 1.f;
-    out[i] = mean + nz * expf(0.5f * logvar[ti]) * noise[i];
-    if (x0_out) x0_out[i] = x0;
+    out[i] = ok ? mean + nz * expf(0.5f * logvar[ti]) * noise[i] : __builtin_nanf("");
+    if (x0_out) x0_out[i] = ok ? x0 : __builtin_nanf("");
   }
 }
 
@@ -584,13 +589,15 @@ extern "C" int dv_shuffle(int dtype, int mode, const void* src, int lds, void* d
 
 extern "C" int dv_q_sample(int dtype, const float* x0, const float* noise, const long long* t,
                            const float* sqrt_ac, const float* sqrt_1m_ac, void* y, int B, int C,
-                           int T, int H, int W, int cpad, int normalize, void* stream) {
-  DV_REQUIRE(x0 && noise && t && sqrt_ac && sqrt_1m_ac && y && cpad >= C, "bad arguments");
+                           int T, int H, int W, int cpad, int normalize, int num_timesteps,
+                           void* stream) {
+  DV_REQUIRE(x0 && noise && t && sqrt_ac && sqrt_1m_ac && y && cpad >= C && num_timesteps > 0,
+             "bad arguments");
   const long long npix = (long long)B * T * H * W;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH(dtype,
-           (q_sample_kernel<float><<<grid_for(npix), 256, 0, st>>>(x0, noise, t, sqrt_ac, sqrt_1m_ac, (float*)y, B, C, T, H * W, cpad, normalize)),
-           (q_sample_kernel<bf16><<<grid_for(npix), 256, 0, st>>>(x0, noise, t, sqrt_ac, sqrt_1m_ac, (bf16*)y, B, C, T, H * W, cpad, normalize)));
+           (q_sample_kernel<float><<<grid_for(npix), 256, 0, st>>>(x0, noise, t, sqrt_ac, sqrt_1m_ac, (float*)y, B, C, T, H * W, cpad, normalize, num_timesteps)),
+           (q_sample_kernel<bf16><<<grid_for(npix), 256, 0, st>>>(x0, noise, t, sqrt_ac, sqrt_1m_ac, (bf16*)y, B, C, T, H * W, cpad, normalize, num_timesteps)));
   return check_launch("q_sample");
 }
 
@@ -676,13 +683,13 @@ extern "C" int dv_p_sample(int dtype, const float* x, const void* eps, int ld, c
                            const long long* t, const float* sqrt_recip_ac,
                            const float* sqrt_recipm1_ac, const float* coef1, const float* coef2,
                            const float* logvar, float* out, float* x0_out, int B, int C, int T,
-                           int H, int W, int clip, void* stream) {
-  DV_REQUIRE(x && eps && noise && t && out, "bad arguments");
+                           int H, int W, int clip, int num_timesteps, void* stream) {
+  DV_REQUIRE(x && eps && noise && t && out && num_timesteps > 0, "bad arguments");
   const long long n = (long long)B * C * T * H * W;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH(dtype,
-           (p_sample_kernel<float><<<grid_for(n), 256, 0, st>>>(x, (const float*)eps, ld, noise, t, sqrt_recip_ac, sqrt_recipm1_ac, coef1, coef2, logvar, out, x0_out, B, C, T, H * W, clip)),
-           (p_sample_kernel<bf16><<<grid_for(n), 256, 0, st>>>(x, (const bf16*)eps, ld, noise, t, sqrt_recip_ac, sqrt_recipm1_ac, coef1, coef2, logvar, out, x0_out, B, C, T, H * W, clip)));
+           (p_sample_kernel<float><<<grid_for(n), 256, 0, st>>>(x, (const float*)eps, ld, noise, t, sqrt_recip_ac, sqrt_recipm1_ac, coef1, coef2, logvar, out, x0_out, B, C, T, H * W, clip, num_timesteps)),
+           (p_sample_kernel<bf16><<<grid_for(n), 256, 0, st>>>(x, (const bf16*)eps, ld, noise, t, sqrt_recip_ac, sqrt_recipm1_ac, coef1, coef2, logvar, out, x0_out, B, C, T, H * W, clip, num_timesteps)));
   return check_launch("p_sample");
 }
 

@@ -493,7 +493,11 @@ class CrossEmbedLayer3D(nn.Module):
         kmax = max(c.weight.shape[-1] for c in self.convs)
         w = torch.cat([F.pad(c.weight, [(kmax - c.weight.shape[-1]) // 2] * 4) for c in self.convs], dim=0)
         b = torch.cat([c.bias for c in self.convs], dim=0)
-        return ops.conv(x, w, b, cache=False)
+        # algorithmic FLOPs are those of the three unpadded convs
+        cin = self.convs[0].weight.shape[1]
+        algo = sum(c.weight.shape[0] * cin * c.weight.shape[-1] ** 2 for c in self.convs)
+        executed = w.shape[0] * x.shape[-1] * kmax * kmax
+        return ops.conv(x, w, b, cache=False, algo_scale=algo / executed)
 
     def forward(self, x):
         b, c, t = x.shape[:3]
@@ -820,6 +824,62 @@ class LowresVideoConditioner(nn.Module):
 
 
 # ---------------------------------------------------------------------------
+# one DDPM denoise step as a replayable HIP graph (sampling loop, config 4)
+# ---------------------------------------------------------------------------
+
+
+class _DenoiseStepGraph:
+    """x <- p_sample(unet, x, t) in place (dalle2_video.py:1621-1664 inside the
+    loop at :1707-1735).  The loop state `x` and the timestep buffer `t` are
+    fixed device buffers; the first two calls run eagerly (every lazily
+    allocated workspace exists afterwards), the third captures the step —
+    Unet3D forward (two with classifier-free guidance), `randn_like` noise on
+    the device generator and the posterior update written back into x — and
+    every call from then on sets t and replays the graph."""
+
+    EAGER_CALLS = 2
+
+    def __init__(self, decoder, unet, x, video_embed, noise_scheduler, cond_scale, lowres_cond_vid,
+                 clip_denoised):
+        self.decoder, self.unet, self.x = decoder, unet, x
+        self.video_embed, self.sched, self.cond_scale = video_embed, noise_scheduler, cond_scale
+        self.lowres, self.clip = lowres_cond_vid, clip_denoised
+        self.t = torch.zeros(x.shape[0], dtype=torch.long, device=x.device)
+        self.calls = 0
+        self.graph = None
+
+    def _body(self):
+        x, unet = self.x, self.unet
+        if self.cond_scale == 1:
+            # forward without the NCTHW round trip: the update reads the
+            # channels-last prediction directly
+            dt = _compute_dtype(unet, x)
+            xin = torch.cat((x, self.lowres), dim=1) if exists(self.lowres) else x
+            lcl = ops.to_cl(self.lowres, dt) if exists(self.lowres) else None
+            eps = unet.forward_cl(ops.to_cl(xin, dt), self.t, batch=x.shape[0], lowres_cl=lcl)
+        else:
+            eps = unet.forward_with_cond_scale(x, self.t, video_embed=self.video_embed,
+                                               cond_scale=self.cond_scale,
+                                               lowres_cond_video=self.lowres)
+        noise = torch.randn_like(x)
+        ops.p_sample_step(x, eps, noise, self.t, self.sched, self.clip, out=x, want_x0=False)
+
+    def __call__(self, time):
+        self.t.fill_(time)
+        self.calls += 1
+        if self.calls <= self.EAGER_CALLS or ops.TIMER is not None:
+            self._body()
+            return
+        if self.graph is None:
+            torch.cuda.synchronize()
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._body()
+                ops.gn_graph_boundary(self.x.device)
+        self.graph.replay()
+
+
+# ---------------------------------------------------------------------------
 # VideoDecoder (dalle2_video.py:1169-2299)
 # ---------------------------------------------------------------------------
 
@@ -947,6 +1007,10 @@ class VideoDecoder(nn.Module):
         self.use_dynamic_thres = use_dynamic_thres
         self.dynamic_thres_percentile = dynamic_thres_percentile
         self.register_buffer("_dummy", torch.Tensor([True]), persistent=False)
+        # the DDPM loop replays one captured HIP graph per denoise step
+        # (DV_SAMPLE_GRAPHS=0: launch every step eagerly)
+        import os
+        self.sample_graphs = os.environ.get("DV_SAMPLE_GRAPHS", "1") != "0"
 
     @property
     def device(self):
@@ -1052,10 +1116,22 @@ class VideoDecoder(nn.Module):
                            predict_v=False, learned_variance=False, clip_denoised=True,
                            lowres_cond_vid=None, text_encodings=None, cond_scale=1,
                            is_latent_diffusion=False, lowres_noise_level=None):
+        """dalle2_video.py:1667-1755.  On the GPU every denoise step after the
+        first two is a replay of one captured HIP graph (_DenoiseStepGraph):
+        the Unet3D forward(s), the device-side noise draw and the in-place
+        posterior update, with no host launches in between."""
         b = shape[0]
         vid = torch.randn(shape, device=self.device)
         if not is_latent_diffusion:
             lowres_cond_vid = maybe(self.normalize_video)(lowres_cond_vid)
+        if vid.is_cuda and self.sample_graphs:
+            with ops.private_pack_cache():
+                step = _DenoiseStepGraph(self, unet, vid, video_embed, noise_scheduler, cond_scale,
+                                         lowres_cond_vid, clip_denoised)
+                for time in reversed(range(0, noise_scheduler.num_timesteps)):
+                    step(time)
+                del step
+            return self.unnormalize_video(vid)
         for time in reversed(range(0, noise_scheduler.num_timesteps)):
             times = torch.full((b,), time, device=self.device, dtype=torch.long)
             vid, _ = self.p_sample(unet, vid, times, video_embed=video_embed,

@@ -21,21 +21,21 @@ class KernelTimer:
     (bench.py uses it for the roofline of the dominant kernel)."""
 
     def __init__(self):
-        self.records = []  # (name, flops, bytes, start_event, end_event)
+        self.records = []  # (name, shape, flops, bytes, start_event, end_event)
 
     # a short device-side spin before each timed launch keeps the GPU behind the
     # host, so the start event, the kernel and the end event run back to back and
     # the elapsed time is the kernel's own (not host launch gaps)
     SPIN_CYCLES = 400_000
 
-    def run(self, name, flops, nbytes, fn):
+    def run(self, name, flops, nbytes, fn, shape=None):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         torch.cuda._sleep(self.SPIN_CYCLES)
         s.record()
         fn()
         e.record()
-        self.records.append((name, flops, nbytes, s, e))
+        self.records.append((name, shape, flops, nbytes, s, e))
 
     def overhead_ms(self, n=32):
         """Median elapsed time of an EMPTY start/end event pair recorded the
@@ -53,28 +53,32 @@ class KernelTimer:
         v = sorted(s.elapsed_time(e) for s, e in pairs)
         return v[len(v) // 2]
 
-    def summary(self):
+    def summary(self, by_shape=False):
+        """{name: totals} (or {(name, shape): totals} with by_shape=True; shape
+        is the (M, N, K) GEMM view of a conv launch)."""
         torch.cuda.synchronize()
-        ovh = self.overhead_ms()
+        if getattr(self, "event_overhead_ms", None) is None:
+            self.event_overhead_ms = self.overhead_ms()
+        ovh = self.event_overhead_ms
         out = {}
-        for name, fl, nb, s, e in self.records:
-            d = out.setdefault(name, dict(count=0, flops=0.0, bytes=0.0, ms=0.0))
+        for name, shape, fl, nb, s, e in self.records:
+            d = out.setdefault((name, shape) if by_shape else name,
+                               dict(count=0, flops=0.0, bytes=0.0, ms=0.0))
             d["count"] += 1
             d["flops"] += fl
             d["bytes"] += nb
             d["ms"] += max(s.elapsed_time(e) - ovh, 1e-4)
-        self.event_overhead_ms = ovh
         return out
 
 
 TIMER = None  # set to a KernelTimer to time kernel launches
 
 
-def _launch(name, flops, nbytes, fn):
+def _launch(name, flops, nbytes, fn, shape=None):
     if TIMER is None:
         fn()
     else:
-        TIMER.run(name, flops, nbytes, fn)
+        TIMER.run(name, flops, nbytes, fn, shape)
 
 
 def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0):
@@ -219,11 +223,18 @@ def _xattn_workspace(nb, C, device, owner=None):
     on entry, re-zeroed by dv_xattn_fold_bwd after use; mcorr [nb][32] scratch.
     `owner` (a block's parameter) gives the block its own set, for fold
     backwards deferred into one batched launch."""
+    import weakref
     key = (nb, C, str(device), None if owner is None else id(owner))
-    if key not in _XA_WS:
-        _XA_WS[key] = tuple(torch.zeros(nb, 32, C, dtype=torch.float32, device=device) for _ in range(3)) + (
-            torch.zeros(nb, 32, dtype=torch.float32, device=device),)
-    return _XA_WS[key]
+    ent = _XA_WS.get(key)
+    if ent is not None and (owner is None or ent[0]() is owner):
+        return ent[1]
+    if owner is not None:  # forget the sets of blocks that no longer exist
+        for k in [k for k, e in _XA_WS.items() if e[0] is not None and e[0]() is None]:
+            del _XA_WS[k]
+    ws = tuple(torch.zeros(nb, 32, C, dtype=torch.float32, device=device) for _ in range(3)) + (
+        torch.zeros(nb, 32, dtype=torch.float32, device=device),)
+    _XA_WS[key] = (None if owner is None else weakref.ref(owner), ws)
+    return ws
 
 
 class _GnSums:
@@ -317,13 +328,27 @@ class PackCache:
         if e is not None and e["epoch"] == self.epoch and e["version"] == weight._version:
             return e["out"], False
         if e is None:
+            import weakref
             rows = cout if mode % 2 == 0 else cin
             e = dict(out=torch.empty(rows, k * k, pad_to, dtype=dtype, device=weight.device),
-                     w=w, meta=(cout, cin, k * k, pad_to, mode))
+                     w=w, meta=(cout, cin, k * k, pad_to, mode), param=weakref.ref(weight))
             self.entries[key] = e
             self._table_key = None
         e["epoch"], e["version"] = self.epoch, weight._version
         return e["out"], True
+
+    def prune(self):
+        """Drop the entries whose parameter is gone or now lives elsewhere
+        (re-pointed into a new flat buffer, moved by `.to()`); the others —
+        e.g. another trainer's weights, whose captured graphs read these
+        images — stay.  An entry keeps its source storage alive, so a stale
+        key can never alias a newer tensor."""
+        dead = [k for k, e in self.entries.items()
+                if e["param"]() is None or e["param"]().data_ptr() != k[0]]
+        for k in dead:
+            del self.entries[k]
+        if dead:
+            self._table = self._table_key = None
 
     def refresh(self):
         """New epoch (weights were updated): repack all entries in one launch."""
@@ -333,7 +358,7 @@ class PackCache:
             return
         ents = list(self.entries.values())
         dev = ents[0]["out"].device
-        if self._table_key != len(ents) or self._table is None:
+        if self._table_key is None or self._table is None:
             rows = []
             for e in ents:
                 cout, cin, taps, pad_to, mode = e["meta"]
@@ -342,7 +367,7 @@ class PackCache:
             raw = torch.tensor([[a, b, (c | (d << 32)), (f | (g << 32)), (h | (m << 32))]
                                 for a, b, c, d, f, g, h, m in rows], dtype=torch.int64)
             self._table = raw.to(dev)
-            self._table_key = len(ents)
+            self._table_key = True
             self._max = max(e["out"].numel() for e in ents)
         call("dv_pack_conv_weights_batched", ptr(self._table), len(ents), self._max, stream())
         for e in ents:
@@ -354,6 +379,24 @@ class PackCache:
 
 
 PACK = PackCache()
+
+
+class private_pack_cache:
+    """Context: a separate, enabled PackCache for a region whose weights do not
+    change (the sampling loop).  The trainer's cache is untouched, so sampling
+    weights (e.g. the EMA unets) are never repacked by its per-update refresh."""
+
+    def __enter__(self):
+        global PACK
+        self.saved = PACK
+        PACK = PackCache()
+        PACK.enabled = True
+        return PACK
+
+    def __exit__(self, *exc):
+        global PACK
+        PACK = self.saved
+        return False
 
 
 def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int, cache: bool = True) -> torch.Tensor:
@@ -391,7 +434,7 @@ class ConvFn(torch.autograd.Function):
     """y = conv_(1,k,k)(cat(x0, x1)) + bias (+ res).  dalle2_video.py:107 etc."""
 
     @staticmethod
-    def forward(ctx, x0, x1, weight, bias, res, ksize, sink=None, cache=True):
+    def forward(ctx, x0, x1, weight, bias, res, ksize, sink=None, cache=True, algo_scale=1.0):
         require_gpu(x0, x1, weight, bias, res)
         nf, h, w, c0 = x0.shape
         c1 = 0 if x1 is None else x1.shape[3]
@@ -405,26 +448,31 @@ class ConvFn(torch.autograd.Function):
         ldr = cl_ld(res) if res is not None else 0
         b = None if bias is None else bias.detach().float().contiguous()
         m = nf * h * w
-        flops, nbytes = 2.0 * m * cout * cin * ksize * ksize, x0.element_size() * m * (cin + cout)
+        # algorithmic work: algo_scale < 1 when the executed weight is padded
+        # (CrossEmbedLayer3D's zero-embedded kernels, 3 -> 8 input channels)
+        flops = 2.0 * m * cout * cin * ksize * ksize * algo_scale
+        nbytes = x0.element_size() * m * (cin + cout)
+        shape = ("fwd", m, cout, cin * ksize * ksize)
         if window_ok(x0, x1, cin, c0 if x1 is not None else cin, cout, ld0, ld1 or ld0, cout,
                      ldr, ksize, h, w, nf):
             wp = pack_conv_weight(weight, x0.dtype, cin, 2, cache)
             _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                     lambda: call("dv_conv_fwd8", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp),
                                  ptr(b), ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ACT_NONE,
-                                 stream()))
+                                 stream()), shape)
         else:
             wp = pack_conv_weight(weight, x0.dtype, cin, 0, cache)
             _launch(conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
                                   max(ld0, ld1), ksize, h, w), flops, nbytes,
                     lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b),
                                  ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE,
-                                 stream()))
+                                 stream()), shape)
         ctx.save_for_backward(x0, x1, weight)
         ctx.params = (weight, bias)
         ctx.meta = (ksize, c0, c1, bias is not None, res is not None)
         ctx.sink = sink
         ctx.cache = cache
+        ctx.algo_scale = algo_scale
         return y
 
     @staticmethod
@@ -453,21 +501,22 @@ class ConvFn(torch.autograd.Function):
                 dx = alloc(nf, h, w, cin, dtype=dy.dtype, device=dy.device)
             rp, rld = (ptr(dx), cin) if acc is not None else (None, 0)
             m = nf * h * w
-            flops = 2.0 * m * cin_real * cout8 * ksize * ksize
+            flops = 2.0 * m * cin_real * cout8 * ksize * ksize * ctx.algo_scale
             nbytes = dy8.element_size() * m * (cin + cout8)
+            shape = ("dgrad", m, cin_real, cout8 * ksize * ksize)
             if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, cin, 0, ksize, h, w, nf):
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 3, ctx.cache)
                 _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                         lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd),
                                      None, rp, rld, ptr(dx), cin, nf, h, w, cout8, cin_real, ACT_NONE,
-                                     stream()))
+                                     stream()), shape)
             else:
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 1, ctx.cache)
                 _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, lddy, ksize, h, w),
                         flops, nbytes,
                         lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd), None,
                                      rp, rld, ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE,
-                                     stream()))
+                                     stream()), shape)
             if sink is not None and acc is None:
                 sink.dx = dx  # first reader: the other conv's backward adds into it
             else:
@@ -504,11 +553,12 @@ class ConvFn(torch.autograd.Function):
                                      max(lddy, ld0, ld1)) if (cout8 == cout and cin_real == cin)
                      else gemm_wgrad_name(dname, m, cout8, cin * ksize * ksize, max(lddy, ld0, ld1)))
             _launch(kname,
-                    2.0 * m * cout8 * cin * ksize * ksize,
+                    2.0 * m * cout8 * cin * ksize * ksize * ctx.algo_scale,
                     dy8.element_size() * m * (cin + cout8),
                     lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), lddy, ptr(x0), ld0, c0, ptr(x1), ld1,
                                  ptr(dw_t), int(acc_w), ptr(db_t), int(acc_b), ptr(ws), ws.numel(),
-                                 nf, h, w, cin, cout8, cout, cin_real, ksize, stream()))
+                                 nf, h, w, cin, cout8, cout, cin_real, ksize, stream()),
+                    ("wgrad", cout8, cin * ksize * ksize, m))
         elif want_b:
             bslot = _grad_out(bparam, zero=True)
             if bslot is None or cout8 != cout:
@@ -521,17 +571,18 @@ class ConvFn(torch.autograd.Function):
             elif db_buf is not bslot[0]:
                 bslot[0].add_(db_buf[:cout])
         dres = dy if has_res else None
-        return dx0, dx1, dw, db, dres, None, None, None
+        return dx0, dx1, dw, db, dres, None, None, None, None
 
 
-def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True):
+def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_scale=1.0):
     """(1,k,k) 'same' convolution over channels-last frames (weight in torch
     Conv3d layout (cout, cin, 1, k, k) or Linear layout (cout, cin)).
     sink: a GradSink shared with the other conv reading (x0, x1).
     cache=False: the weight is rebuilt every call (not a parameter), so its
-    packed image is made on every call instead of kept in the PackCache."""
+    packed image is made on every call instead of kept in the PackCache.
+    algo_scale: algorithmic / executed FLOPs (timing labels only)."""
     k = weight.shape[-1] if weight.dim() == 5 else 1
-    return ConvFn.apply(x0, x1, weight, bias, res, k, sink, cache)
+    return ConvFn.apply(x0, x1, weight, bias, res, k, sink, cache, algo_scale)
 
 
 # ---------------------------------------------------------------------------
@@ -1166,7 +1217,8 @@ def q_sample_cl(x_start, noise, times, sqrt_ac, sqrt_1m_ac, dtype, normalize=Tru
     cp = _pad8(C)
     y = torch.empty(B * T, H, W, cp, dtype=dtype, device=x0.device)
     call("dv_q_sample", _lib.DV_BF16 if dtype == torch.bfloat16 else _lib.DV_F32, ptr(x0), ptr(nz), ptr(t),
-         ptr(sqrt_ac), ptr(sqrt_1m_ac), ptr(y), B, C, T, H, W, cp, int(normalize), stream())
+         ptr(sqrt_ac), ptr(sqrt_1m_ac), ptr(y), B, C, T, H, W, cp, int(normalize), sqrt_ac.numel(),
+         stream())
     return y
 
 
@@ -1200,10 +1252,11 @@ def mse_loss_cl(pred_cl, target, sample_w=None):
     return MSELossFn.apply(pred_cl, target, sample_w)
 
 
-def p_sample_step(x, eps, noise, times, sched, clip_denoised=True):
+def p_sample_step(x, eps, noise, times, sched, clip_denoised=True, out=None, want_x0=True):
     """x0 = sqrt(1/ac) x - sqrt(1/ac - 1) eps -> clamp -> posterior mean + sigma z
     (p_mean_variance + p_sample, dalle2_video.py:1551-1664).  eps is an NCTHW
-    f32 tensor or a channels-last frame tensor."""
+    f32 tensor or a channels-last frame tensor.  `out` may be x itself (the
+    update is elementwise: the sampling loop advances its state in place)."""
     require_gpu(x, eps, noise, times)
     xf = x.float().contiguous()
     nz = noise.float().contiguous()
@@ -1215,12 +1268,17 @@ def p_sample_step(x, eps, noise, times, sched, clip_denoised=True):
     else:
         ef = eps
         ld, edt = cl_ld(eps), dt(eps)
-    out = torch.empty_like(xf)
-    x0 = torch.empty_like(xf)
+        if eps.shape[0] != B * T or eps.shape[-1] < C:
+            raise _lib.DVError(f"p_sample: eps {tuple(eps.shape)} does not match x {tuple(xf.shape)}")
+    if out is None:
+        out = torch.empty_like(xf)
+    elif out.dtype != torch.float32 or not out.is_contiguous() or out.shape != xf.shape:
+        raise _lib.DVError("p_sample: out must be a contiguous f32 tensor shaped like x")
+    x0 = torch.empty_like(xf) if want_x0 else None
     call("dv_p_sample", edt, ptr(xf), ptr(ef), ld, ptr(nz), ptr(t), ptr(sched.sqrt_recip_alphas_cumprod),
          ptr(sched.sqrt_recipm1_alphas_cumprod), ptr(sched.posterior_mean_coef1),
          ptr(sched.posterior_mean_coef2), ptr(sched.posterior_log_variance_clipped), ptr(out), ptr(x0),
-         B, C, T, H, W, int(clip_denoised), stream())
+         B, C, T, H, W, int(clip_denoised), sched.sqrt_recip_alphas_cumprod.numel(), stream())
     return out, x0
 
 

@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import math
 import os
-from contextlib import nullcontext
+from contextlib import contextmanager, nullcontext
 from pathlib import Path
 
 import torch
@@ -53,6 +53,10 @@ class FusedAdamW(torch.optim.Optimizer):
         self._flat = None  # (P, G, M, V, [(group, start, end)], params)
         self._clip_ws = None
         self._t = 0
+        # bumped whenever the flat buffers are (re)built: anything that holds
+        # their addresses (captured HIP graphs, packed-weight images) is stale
+        self.generation = 0
+        self._probe = ()  # (param, data offset, grad offset) spot checks of the aliasing
 
     # -- flat storage ------------------------------------------------------
     def _build_flat(self):
@@ -95,6 +99,33 @@ class FusedAdamW(torch.optim.Optimizer):
                 off += al(k)
             ranges.append((gi, start, off))
         self._flat = (P, G, M, V, ranges, [p for _, p in live])
+        self.generation += 1
+        ps = self._flat[5]
+        self._probe = tuple((p, p.data_ptr(), p.grad.data_ptr())
+                            for p in {id(q): q for q in (ps[0], ps[len(ps) // 2], ps[-1])}.values())
+
+    def _aliased(self):
+        """Do the parameters (and their grads) still live in the flat buffers?
+        `Module.to()` / `.cpu()` / `.cuda()` (e.g. VideoDecoder.one_unet_in_gpu,
+        reference dalle2_video.py:1508-1529) replace every `p.data`, so a spot
+        check of three parameters detects it."""
+        for p, dp, gp in self._probe:
+            if p.data_ptr() != dp or p.grad is None or p.grad.data_ptr() != gp:
+                return False
+        return True
+
+    def _rebuild_flat(self):
+        """Re-point the parameters into fresh flat buffers, keeping their
+        current values and gradients and the AdamW moments."""
+        P, G, M, V, ranges, params = self._flat
+        for p in params:
+            st = self.state.get(p, {})
+            st["exp_avg"] = st["exp_avg"].detach().clone()
+            st["exp_avg_sq"] = st["exp_avg_sq"].detach().clone()
+            if p.grad is None or p.grad.device != p.device:
+                p.grad = torch.zeros_like(p)
+        self._flat = None
+        self._build_flat()
 
     @property
     def flat_grad(self):
@@ -103,6 +134,8 @@ class FusedAdamW(torch.optim.Optimizer):
     def ensure_flat(self):
         if self._flat is None:
             self._build_flat()
+        elif not self._aliased():
+            self._rebuild_flat()
         return self._flat is not None
 
     @torch.no_grad()
@@ -155,7 +188,19 @@ class FusedAdamW(torch.optim.Optimizer):
         steps = [float(s["step"]) for s in self.state.values() if "step" in s]
         self._t = int(max(steps)) if steps else 0
         if self._flat is not None:
-            self._flat = None  # rebuilt (and re-pointed) on the next step
+            # keep the flat buffers (and every graph / packed image built on
+            # their addresses): copy the loaded moments into the M / V slices
+            P, G, M, V, ranges, params = self._flat
+            for p in params:
+                st = self.state.get(p)
+                if not st or "exp_avg" not in st:
+                    continue
+                off = (p.data_ptr() - P.data_ptr()) // 4
+                k = p.numel()
+                M[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                V[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                st["exp_avg"] = M[off:off + k].view_as(p)
+                st["exp_avg_sq"] = V[off:off + k].view_as(p)
 
 
 def get_optimizer(params, lr=1e-4, wd=1e-2, betas=(0.9, 0.99), eps=1e-8,
@@ -173,27 +218,40 @@ def get_optimizer(params, lr=1e-4, wd=1e-2, betas=(0.9, 0.99), eps=1e-8,
 
 
 class _LinearWarmup:
-    """pytorch_warmup.LinearWarmup stand-in: lr factor min(1, step/period)."""
+    """pytorch_warmup.LinearWarmup (the reference's `warmup.LinearWarmup`,
+    trainer.py:83-87), restated from pytorch_warmup's published BaseWarmup:
 
-    def __init__(self, optimizer, warmup_period):
+    * construction remembers the undamped lrs and dampens step 0 at once;
+    * `dampening()` restores the undamped lrs on entry (so the wrapped
+      `scheduler.step()` sees and updates the undamped values), then on exit
+      records the scheduler's new lrs as undamped and dampens the next step;
+    * factor(step) = min(1, (step + 1) / warmup_period)."""
+
+    def __init__(self, optimizer, warmup_period, last_step=-1):
         self.optimizer = optimizer
-        self.period = warmup_period
-        self.last_step = 0
+        self.warmup_period = warmup_period
+        self.last_step = last_step
+        self.lrs = [g["lr"] for g in optimizer.param_groups]
+        self.dampen()
 
+    def warmup_factor(self, step):
+        return min(1.0, (step + 1) / self.warmup_period)
+
+    def dampen(self, step=None):
+        if step is None:
+            step = self.last_step + 1
+        self.last_step = step
+        f = self.warmup_factor(step)
+        for g in self.optimizer.param_groups:
+            g["lr"] *= f
+
+    @contextmanager
     def dampening(self):
-        opt = self
-
-        class _Ctx:
-            def __enter__(self_):
-                return None
-
-            def __exit__(self_, *a):
-                opt.last_step += 1
-                f = min(1.0, opt.last_step / max(opt.period, 1))
-                for g in opt.optimizer.param_groups:
-                    g["lr"] = g["lr"] * f
-                return False
-        return _Ctx()
+        for g, lr in zip(self.optimizer.param_groups, self.lrs):
+            g["lr"] = lr
+        yield
+        self.lrs = [g["lr"] for g in self.optimizer.param_groups]
+        self.dampen()
 
 
 class EMA(nn.Module):
@@ -254,6 +312,64 @@ def split_args_and_kwargs(*args, split_size=None, **kwargs):
         yield size / batch, (cargs, ckw)
 
 
+class ShardedLoader:
+    """A DataLoader re-built over a rank-strided DistributedSampler (what
+    accelerate's `prepare` does to the reference's loaders, trainer.py:117-124):
+    rank r of N iterates samples r, r+N, ... of the (shuffled, if the original
+    loader shuffles) epoch order — disjoint across ranks, same batch size per
+    rank, so the global batch is N x batch_size.  The epoch (shuffle seed) is
+    advanced on every new iteration, as accelerate does."""
+
+    def __init__(self, loader, world, rank, seed=0):
+        from torch.utils.data import DataLoader, DistributedSampler, RandomSampler
+
+        self.original = loader
+        shuffle = isinstance(loader.sampler, RandomSampler)
+        self.sampler = DistributedSampler(loader.dataset, num_replicas=world, rank=rank,
+                                          shuffle=shuffle, seed=seed, drop_last=False)
+        kw = dict(batch_size=loader.batch_size, sampler=self.sampler, num_workers=loader.num_workers,
+                  collate_fn=loader.collate_fn, pin_memory=loader.pin_memory,
+                  drop_last=loader.drop_last, timeout=loader.timeout,
+                  worker_init_fn=loader.worker_init_fn)
+        if loader.num_workers > 0:
+            kw.update(prefetch_factor=loader.prefetch_factor,
+                      persistent_workers=loader.persistent_workers)
+        self.loader = DataLoader(loader.dataset, **kw)
+        self.epoch = 0
+
+    @property
+    def dataset(self):
+        return self.loader.dataset
+
+    @property
+    def batch_size(self):
+        return self.loader.batch_size
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        self.sampler.set_epoch(self.epoch)
+        self.epoch += 1
+        return iter(self.loader)
+
+
+def shard_loader(loader, world, rank):
+    """Per-rank view of a DataLoader (identity on one process or for objects
+    that are not map-style DataLoaders)."""
+    from torch.utils.data import DataLoader, IterableDataset
+
+    if (world <= 1 or loader is None or not isinstance(loader, DataLoader)
+            or isinstance(loader.dataset, IterableDataset) or loader.batch_sampler is None):
+        return loader
+    seed = torch.tensor([torch.initial_seed() % (1 << 31)], dtype=torch.int64)
+    if dist.is_initialized():
+        if dist.get_backend() == "nccl":  # RCCL collectives take device tensors
+            seed = seed.cuda()
+        dist.broadcast(seed, 0)  # one shuffle order for all ranks
+    return ShardedLoader(loader, world, rank, seed=int(seed.item()))
+
+
 def broadcast_parameters(module, src=0):
     """DDP's init broadcast: every rank starts from rank `src`'s weights."""
     for p in module.parameters():
@@ -312,8 +428,13 @@ class VideoDecoderTrainer(nn.Module):
                                   for i, w in enumerate(warmup_steps)]
         self.max_grad_norm = max_grad_norm
         self.register_buffer("steps", torch.tensor([0] * self.num_unets))
-        self.train_loader = dataloaders["train"] if exists(dataloaders) else None
-        self.val_loader = dataloaders["val"] if exists(dataloaders) else None
+        # accelerator.prepare(..., train, val) (trainer.py:117-124) shards the
+        # loaders per process: each rank iterates a disjoint rank-strided part
+        rank = dist.get_rank() if self.world > 1 else 0
+        self.train_loader = (shard_loader(dataloaders["train"], self.world, rank)
+                             if exists(dataloaders) else None)
+        self.val_loader = (shard_loader(dataloaders["val"], self.world, rank)
+                           if exists(dataloaders) else None)
         if self.world > 1:
             broadcast_parameters(decoder, 0)
 
@@ -343,17 +464,23 @@ class VideoDecoderTrainer(nn.Module):
         index = unet_number - 1
         opt = getattr(self, f"optim{index}")
         sched = getattr(self, f"sched{index}")
-        fresh = opt.flat_grad is None
+        gen = opt.generation
         opt.ensure_flat()
+        fresh = opt.generation != gen
+        if fresh:
+            # parameters were (re)pointed into new flat buffers: every captured
+            # graph of this unet holds the old addresses
+            self._graphs = {k: v for k, v in self._graphs.items() if k[0] != unet_number}
         allreduce_flat_grad(opt.flat_grad, self.world)
         coef = opt.clip_coefficient(self.max_grad_norm, prescale=1.0 / self.world)
         opt.step(clip_coef=coef)
         opt.zero_grad()
-        from . import ops
         if ops.PACK.enabled:
-            # the first step re-points parameters into the flat buffer: drop the
-            # images keyed on the old storage; afterwards repack in one launch
-            ops.PACK.clear() if fresh else ops.PACK.refresh()
+            # new storage: drop the images keyed on the old storage (their
+            # graphs were dropped above); otherwise repack every image in one launch
+            if fresh:
+                ops.PACK.prune()
+            ops.PACK.refresh()
         warm = self.warmup_schedulers[index]
         with (warm.dampening() if exists(warm) else nullcontext()):
             sched.step()
@@ -481,10 +608,31 @@ class VideoDecoderTrainer(nn.Module):
         return obj
 
     @torch.no_grad()
-    def sample(self, *args, **kwargs):
-        was = self.decoder.training
-        self.decoder.eval()
-        kwargs.pop("use_non_ema", None)
-        out = self.decoder.sample(*args, **kwargs)
-        self.decoder.train(was)
+    def sample(self, *args, max_batch_size=None, **kwargs):
+        """trainer.py:276-300: sample with the EMA unets swapped in (unless
+        `use_non_ema` or EMA is off); inputs are moved to the decoder's device
+        and split into `max_batch_size` chunks (decoder_sample_in_chunks)."""
+        args = tuple(self._to_device(a) for a in args)
+        kwargs = {k: self._to_device(v) for k, v in kwargs.items()}
+        kwargs["distributed"] = self.world > 1
+        use_non_ema = kwargs.pop("use_non_ema", False) or not self.use_ema
+        dec = self.decoder
+        was = dec.training
+        dec.eval()
+        trainable = dec.unets
+        if not use_non_ema:
+            dec.unets = self.unets  # swap in the exponential moving averaged unets
+        try:
+            if max_batch_size is None:
+                out = dec.sample(*args, **kwargs)
+            else:
+                outs = [dec.sample(*ca, **ck) for _, (ca, ck) in
+                        split_args_and_kwargs(*args, split_size=max_batch_size, **kwargs)]
+                out = torch.cat(outs, dim=0)
+        finally:
+            dec.unets = trainable
+            if not use_non_ema:
+                for ema in self.ema_unets:
+                    ema.restore_ema_model_device()
+            dec.train(was)
         return out

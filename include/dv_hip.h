@@ -194,7 +194,7 @@ int dv_shuffle(int dtype, int mode, const void* src, int lds, void* dst, int ldd
  * (normalize_neg_one_to_one, :1277, 1947-1956).                             */
 int dv_q_sample(int dtype, const float* x0, const float* noise, const long long* t,
                 const float* sqrt_ac, const float* sqrt_1m_ac, void* y, int B, int C, int T,
-                int H, int W, int cpad, int normalize, void* stream);
+                int H, int W, int cpad, int normalize, int num_timesteps, void* stream);
 /* loss = mean_b( w[b] * mean_(c,t,h,w) (pred - target)^2 )   (:1997-2000;
  * sample_w = p2 loss weights, NULL = 1).  loss: one f32, overwritten.        */
 int dv_mse_loss(int dtype, const void* pred, int ld, const float* target, int B, int C, int T,
@@ -209,7 +209,8 @@ int dv_mse_loss_bwd(int dtype, const void* pred, int ld, const float* target, in
 int dv_p_sample(int dtype, const float* x, const void* eps, int ld, const float* noise,
                 const long long* t, const float* sqrt_recip_ac, const float* sqrt_recipm1_ac,
                 const float* coef1, const float* coef2, const float* logvar, float* out,
-                float* x0_out, int B, int C, int T, int H, int W, int clip, void* stream);
+                float* x0_out, int B, int C, int T, int H, int W, int clip, int num_timesteps,
+                void* stream);
 
 /* ---- time conditioning MLPs (Unet3D.to_time_hiddens / to_time_tokens /
  * to_time_cond, dalle2_video.py:348-357; ResnetBlock3D.time_mlp, :152-155)

@@ -120,6 +120,54 @@ def temporal_apply(fn, x, *args, **kwargs):
 
 
 # --------------------------------------------------------------------------
+# kornia gaussian_blur2d (third-party, imported by the reference for
+# LowresVideoConditioner.blur_image, dalle2_video.py:1108).  kornia is absent
+# from this image: restated from its published algorithm — parity unpinned.
+#   gaussian(ks, sigma): x = arange(ks) - ks // 2 (+0.5 if ks even),
+#                        g = exp(-x^2 / (2 sigma^2)), g / sum(g)
+#   gaussian_blur2d(img, (ks, ks), (s, s)) with border_type="reflect":
+#     filter2d_separable = filter2d(kernel_x) then filter2d(kernel_y), each a
+#     depthwise cross-correlation after F.pad(..., mode="reflect").
+# --------------------------------------------------------------------------
+
+
+def gaussian_kernel1d(ks, sigma):
+    x = torch.arange(ks, dtype=torch.float32) - ks // 2
+    if ks % 2 == 0:
+        x = x + 0.5
+    g = torch.exp(-x.pow(2.0) / (2 * float(sigma) ** 2))
+    return g / g.sum()
+
+
+def gaussian_blur2d(img, kernel_size, sigma):
+    """img (b, c, h, w); kernel_size / sigma are (y, x) pairs."""
+    b, c, h, w = img.shape
+    ky = gaussian_kernel1d(kernel_size[0], sigma[0])
+    kx = gaussian_kernel1d(kernel_size[1], sigma[1])
+    x = img.reshape(b * c, 1, h, w)
+    px = kx.numel() // 2
+    x = F.conv2d(F.pad(x, (px, kx.numel() - 1 - px, 0, 0), mode="reflect"), kx.reshape(1, 1, 1, -1))
+    py = ky.numel() // 2
+    x = F.conv2d(F.pad(x, (0, 0, py, ky.numel() - 1 - py), mode="reflect"), ky.reshape(1, 1, -1, 1))
+    return x.reshape(b, c, h, w)
+
+
+def lowres_condition(video, *, target_frame_size, downsample_frame_size, blur, blur_sigma=0.6,
+                     blur_kernel_size=3, clamp_range=(0.0, 1.0), downsample_first=True):
+    """LowresVideoConditioner.forward (dalle2_video.py:1115-1166) with the
+    50 % blur decision made by the caller (`blur`) and no Imagen noising:
+    per-frame nearest down-resize (clamped), optional per-frame kornia blur,
+    per-frame nearest resize to the target (clamped)."""
+    if downsample_first and exists(downsample_frame_size):
+        video = temporal_apply(resize_image_to, video, downsample_frame_size, clamp_range=clamp_range,
+                               nearest=True)
+    if blur:
+        video = temporal_apply(gaussian_blur2d, video, (blur_kernel_size,) * 2, (blur_sigma,) * 2)
+    return temporal_apply(resize_image_to, video, target_frame_size, clamp_range=clamp_range,
+                          nearest=True)
+
+
+# --------------------------------------------------------------------------
 # third-party leaves (dalle2-pytorch 1.14.2) — parity unpinned
 # --------------------------------------------------------------------------
 

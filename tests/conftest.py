@@ -1,3 +1,4 @@
+import json
 import os
 import sys
 
@@ -23,3 +24,19 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture
+def parity_log(request):
+    """record(**values): prints the observed errors and, when DV_PARITY_LOG
+    names a file, appends them as one JSON line (test id + values) so the
+    worst observed error of every tolerance-checked comparison is kept."""
+    path = os.environ.get("DV_PARITY_LOG")
+
+    def record(**values):
+        line = {"test": request.node.nodeid, **values}
+        print(json.dumps(line))
+        if path:
+            with open(path, "a") as f:
+                f.write(json.dumps(line) + "\n")
+    return record

@@ -64,12 +64,23 @@ def _worker(rank, world, port, q):
         with torch.no_grad():
             for p in dec.parameters():
                 p.normal_()
-        tr = VideoDecoderTrainer(dec, lr=3e-4, use_ema=False)
+        from torch.utils.data import DataLoader, TensorDataset
+
+        dl = DataLoader(TensorDataset(torch.arange(16)), batch_size=2, shuffle=True)
+        tr = VideoDecoderTrainer(dec, lr=3e-4, use_ema=False, dataloaders={"train": dl, "val": dl})
         assert tr.world == world
         flat = torch.cat([p.detach().reshape(-1) for p in dec.parameters()])
         gathered = [torch.empty_like(flat) for _ in range(world)]
         dist.all_gather(gathered, flat)
         ok_bcast = all(torch.equal(gathered[0], t) for t in gathered)
+        # the trainer's loaders are sharded per rank (accelerate.prepare, trainer.py:117-124)
+        seen = [int(v) for (b,) in tr.train_loader for v in b]
+        allseen = [None] * world
+        dist.all_gather_object(allseen, seen)
+        if len(set(allseen[0]) & set(allseen[1])) or sorted(allseen[0] + allseen[1]) != list(range(16)):
+            raise AssertionError(f"loaders not sharded disjointly: {allseen}")
+        if len(tr.train_loader) != 4 or len(tr.val_loader) != 4:
+            raise AssertionError("per-rank loader length")
 
         # 2) DP identity with the product's all-reduce
         g = torch.Generator().manual_seed(1234)

@@ -88,17 +88,73 @@ def test_get_optimizer_groups_match_reference_rule():
 
 
 def test_linear_warmup_dampening():
+    """pytorch_warmup.LinearWarmup semantics: step 0 is dampened at
+    construction; each dampening() restores the undamped lr for the wrapped
+    scheduler step and dampens the next step by min(1, (step+1)/period)."""
     from dalle2_video.trainer import _LinearWarmup
 
     opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=1.0)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lr_lambda=lambda s: 1.0)
     w = _LinearWarmup(opt, 4)
-    lrs = []
-    for _ in range(3):
-        opt.param_groups[0]["lr"] = 1.0  # what the base scheduler restores
+    lrs = [opt.param_groups[0]["lr"]]
+    for _ in range(5):
         with w.dampening():
-            pass
+            sched.step()
         lrs.append(opt.param_groups[0]["lr"])
-    assert lrs == [0.25, 0.5, 0.75]
+    assert lrs == [0.25, 0.5, 0.75, 1.0, 1.0, 1.0]
+
+
+def test_linear_warmup_with_cosine_decay_does_not_compound():
+    """Warmup composed with CosineAnnealingLR (trainer.py:75-87): the lr seen
+    by each optimizer step is cosine(step) * warmup(step), never compounded."""
+    from dalle2_video.trainer import _LinearWarmup
+
+    base, period, tmax = 1e-4, 10, 100
+    opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=base)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=tmax)
+    w = _LinearWarmup(opt, period)
+    for step in range(40):
+        want = base * 0.5 * (1 + math.cos(math.pi * step / tmax)) * min(1.0, (step + 1) / period)
+        assert opt.param_groups[0]["lr"] == pytest.approx(want, rel=1e-9), step
+        with w.dampening():
+            sched.step()
+
+
+def test_trainer_lr_follows_warmup_and_cosine_host_side():
+    """VideoDecoderTrainer wires the same warmup/scheduler pair per unet."""
+    from dalle2_video import dalle2_video as D
+    from dalle2_video.trainer import VideoDecoderTrainer
+
+    u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    dec = D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(4,), timesteps=1000, learned_variance=False)
+    tr = VideoDecoderTrainer(dec, lr=3e-4, use_ema=False, warmup_steps=4, cosine_decay_max_steps=50)
+    assert tr.optim0.param_groups[0]["lr"] == pytest.approx(3e-4 / 4)
+    w, s = tr.warmup_schedulers[0], tr.sched0
+    for _ in range(6):
+        with w.dampening():
+            s.step()
+    want = 3e-4 * 0.5 * (1 + math.cos(math.pi * 6 / 50))
+    assert tr.optim0.param_groups[0]["lr"] == pytest.approx(want, rel=1e-9)
+
+
+def test_shard_loader_rank_strided_and_disjoint():
+    """accelerate.prepare's per-rank split of the loaders (trainer.py:117-124):
+    two ranks see disjoint samples that together cover the dataset, shuffled
+    the same way on both ranks, reshuffled per epoch."""
+    from torch.utils.data import DataLoader, TensorDataset
+
+    from dalle2_video.trainer import ShardedLoader
+
+    ds = TensorDataset(torch.arange(20))
+    for shuffle in (False, True):
+        dl = DataLoader(ds, batch_size=3, shuffle=shuffle)
+        shards = [ShardedLoader(dl, 2, r, seed=7) for r in range(2)]
+        seen = [[int(v) for (b,) in s for v in b] for s in shards]
+        assert not set(seen[0]) & set(seen[1])
+        assert sorted(seen[0] + seen[1]) == list(range(20))
+        assert len(shards[0]) == 4 and shards[0].batch_size == 3
+        again = [int(v) for (b,) in shards[0] for v in b]
+        assert (again != seen[0]) == shuffle  # set_epoch advances the shuffle order
 
 
 def test_ema_schedule():

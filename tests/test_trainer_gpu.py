@@ -66,9 +66,74 @@ def test_trainer_call_api_and_checkpoint(tmp_path):
     assert tr.optim0.param_groups[0]["lr"] == 3e-4 and tr.optim1.param_groups[0]["lr"] == 3e-4
     path = tmp_path / "ck.pt"
     tr.save(str(path))
-    tr2 = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False)
+    flat_before = [t.clone() for t in tr.optim0._flat[:4]]  # P, G, M, V
+    u1b = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    u2b = D.Unet3D(8, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8, 16))
+    dec2 = D.VideoDecoder(unet=(u1b, u2b), frame_sizes=(32, 64), frame_numbers=(4, 4), timesteps=1000,
+                          learned_variance=False).cuda()
+    tr2 = VideoDecoderTrainer(dec2, lr=3e-4, wd=1e-2, use_ema=False)
     tr2.load(str(path))
     assert tr2.steps.tolist() == [1, 1]
+    # weights and AdamW moments restored: one more identical step on both
+    # trainers gives identical flat buffers
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.rand(2, 3, 4, 32, 32, device="cuda", generator=g)
+    t = torch.tensor([3, 700], device="cuda")
+    nz = torch.randn(x.shape, device="cuda", generator=g)
+    for d, t_ in ((dec, tr), (dec2, tr2)):
+        d.p_losses(d.unets[0], x, t, video_embed=None, noise_scheduler=d.noise_schedulers[0],
+                   noise=nz).backward()
+        t_.update(1)
+    P1, _, M1, V1 = tr.optim0._flat[:4]
+    P2, _, M2, V2 = tr2.optim0._flat[:4]
+    assert not torch.equal(flat_before[0], P1)  # the extra step moved the weights
+    for a, b in ((P1, P2), (M1, M2), (V1, V2)):
+        assert ((a - b).norm() / a.norm()).item() < 1e-5
+    st = tr2.optim0.state_dict()["state"]
+    assert len(st) > 0 and all(float(v["step"]) == 2.0 for v in st.values())
+
+
+@pytest.mark.parametrize("use_ema", [False, True])
+def test_train_sample_train_keeps_training(use_ema):
+    """trainer.sample between updates (reference trainer.py:276-300) must not
+    detach the parameters from the fused optimizer's flat buffers: train ->
+    sample -> train ends on the same weights as train -> train (to 1e-4: the
+    f32 atomics of GroupNorm / split-K reductions reorder sums run to run)."""
+    from dalle2_video import dalle2_video as D
+    from dalle2_video.trainer import VideoDecoderTrainer
+    from dalle2_video.utils import deterministic_fill_
+
+    def make():
+        u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+        dec = D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(2,), timesteps=4, learned_variance=False)
+        deterministic_fill_(dec.unets[0])
+        dec = dec.cuda()
+        return dec, VideoDecoderTrainer(dec, lr=3e-4, use_ema=use_ema, ema_update_every=1,
+                                        ema_update_after_step=0)
+
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.rand(1, 3, 2, 32, 32, device="cuda", generator=g)
+    nz = torch.randn(x.shape, device="cuda", generator=g)
+    t = torch.tensor([2], device="cuda")  # within the 4-step schedule
+
+    def train(dec, tr):
+        dec.p_losses(dec.unets[0], x, t, video_embed=None, noise_scheduler=dec.noise_schedulers[0],
+                     noise=nz).backward()
+        tr.update(1)
+
+    decA, trA = make()
+    decB, trB = make()
+    train(decA, trA)
+    train(decB, trB)
+    w0 = decB.unets[0].to_out.weight.detach().clone()
+    vid = trB.sample(video_embed=torch.randn(1, 512, device="cuda"))
+    assert vid.shape == (1, 3, 2, 32, 32) and torch.isfinite(vid).all()
+    train(decA, trA)
+    train(decB, trB)
+    wA, wB = decA.unets[0].to_out.weight.detach(), decB.unets[0].to_out.weight.detach()
+    assert not torch.equal(wB, w0), "the update after sampling did not change the weights"
+    for (n, pa), pb in zip(decA.unets[0].named_parameters(), decB.unets[0].parameters()):
+        assert ((pa - pb).norm() / pa.norm().clamp_min(1e-30)).item() < 1e-4, n
 
 
 def test_graph_replay_matches_eager():
@@ -110,3 +175,40 @@ def test_graph_replay_matches_eager():
             worst = sorted(((((ge[o:o + k] - gg[o:o + k]).norm() / ge[o:o + k].norm().clamp_min(1e-30)).item(), n)
                             for n, o, k in views), reverse=True)[:8]
             raise AssertionError(f"{e} vs {gph}: rel {err:.3e}; worst params {worst}")
+
+
+def test_graph_replay_after_checkpoint_load(tmp_path):
+    """A captured graph keeps writing the live gradient buffer after
+    trainer.save/load (the flat buffers are kept): replayed calls
+    after the load give the same gradients as eager calls."""
+    from dalle2_video import dalle2_video as D
+    from dalle2_video.trainer import VideoDecoderTrainer
+    from dalle2_video.utils import deterministic_fill_
+
+    u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    dec = D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(4,), timesteps=1000, learned_variance=False)
+    deterministic_fill_(dec.unets[0])
+    dec = dec.cuda()
+    tr = VideoDecoderTrainer(dec, lr=3e-4, use_ema=False, use_graphs=True)
+    video = torch.rand(2, 3, 4, 32, 32, device="cuda")
+    for _ in range(4):  # update, eager, eager, capture+replay
+        tr(video=video, unet_number=1)
+        tr.update(1)
+    assert any("graph" in v for v in tr._graphs.values())
+    path = tmp_path / "ck.pt"
+    tr.save(str(path))
+    G = tr.optim0.flat_grad
+    tr.load(str(path))
+    assert tr.optim0.flat_grad is G
+    opt = tr.optim0
+    opt.zero_grad()
+    torch.cuda.manual_seed(11)
+    l_graph = tr(video=video, unet_number=1)  # replay
+    g_graph = opt.flat_grad.clone()
+    assert g_graph.abs().max() > 0, "replay after load wrote no gradient into the live buffer"
+    opt.zero_grad()
+    tr.use_graphs = False
+    torch.cuda.manual_seed(11)
+    l_eager = tr(video=video, unet_number=1)
+    assert abs(l_graph - l_eager) <= 1e-5 * abs(l_eager)
+    assert ((g_graph - opt.flat_grad).norm() / opt.flat_grad.norm()).item() < 1e-5
