@@ -60,7 +60,88 @@ struct ConvFwdArgs {
   int H, W, cin, cout, ks, act;
   long long M;
   int K;
+  // GroupNorm statistics epilogue (Block3D: conv -> GroupNorm, dalle2_video.py:
+  // 107-109): per-(clip, channel) sum / sum of squares of the STORED output
+  // added into gn_sums[replica][clip][cout][2] (zero on entry; replica =
+  // workgroup % gn_R, stride gn_rstride), clip = pixel / gn_P.  Null: off.
+  float* gn_sums;
+  long long gn_P;
+  int gn_R;
+  long long gn_rstride;
 };
+
+// GroupNorm statistics of a wave's tile, register-light: every lane holds
+// NV = 2 * NC values v[0..NC) = its pixels' sums of channels chan(k) and
+// v[NC..2NC) = their sums of squares (the same channels on all 32 lanes of a
+// half-wave h = lane >> 5).  Recursive halving over the 32 lanes (offsets
+// 16 .. 1, 31 shuffles for NV = 32) leaves lane r with the half-wave totals
+// of value indices r * (NV / 32) + t, which it adds for clip b: NV / 32
+// atomic instructions per wave, no arrays kept live across the tile loops.
+template <int NV, int O>
+__device__ __forceinline__ void rs_step(float (&v)[NV], int r) {
+  // current segment: v[0 .. 32 * NV / (32 * O) ... ) -- see gn_rs_reduce
+  constexpr int HALF = NV * O / 32;  // values kept after this step
+  const bool up = (r & O) != 0;
+#pragma unroll
+  for (int k = 0; k < HALF; ++k) {
+    const float send = up ? v[k] : v[k + HALF];
+    const float keep = up ? v[k + HALF] : v[k];
+    v[k] = keep + __shfl_xor(send, O, 64);
+  }
+}
+template <int NV>
+__device__ __forceinline__ void gn_rs_reduce(float (&v)[NV], int r) {
+  static_assert(NV % 32 == 0, "NV must be a multiple of 32");
+  rs_step<NV, 16>(v, r);  // 2 * NV / 32 * 16 = NV / 2 kept
+  rs_step<NV, 8>(v, r);
+  rs_step<NV, 4>(v, r);
+  rs_step<NV, 2>(v, r);
+  rs_step<NV, 1>(v, r);   // NV / 32 kept: value indices r * (NV / 32) + t
+}
+template <typename T, int NV, typename Chan>
+__device__ __forceinline__ void gn_rs_add(const ConvFwdArgs<T>& p, const float (&v)[NV],
+                                          long long b, Chan chan) {
+  constexpr int NC = NV / 2, S = NV / 32;
+  const int r = threadIdx.x & 31;
+  const int blk = blockIdx.x + gridDim.x * blockIdx.y;
+  float* base = p.gn_sums + (long long)(blk % p.gn_R) * p.gn_rstride + b * p.cout * 2;
+#pragma unroll
+  for (int t = 0; t < S; ++t) {
+    const int j = r * S + t, stat = j / NC, k = j % NC;
+    const int n = chan(k);
+    if (n < p.cout) atomicAdd(base + 2 * n + stat, v[t]);
+  }
+}
+
+// Block-level version (every wave of the workgroup calls it): the waves'
+// reduce-scattered totals are combined in LDS (ds_add_f32 into red[2 * nblk],
+// LDS that no wave still reads) and the workgroup adds ONE value per (channel,
+// statistic) of its nblk channels [n0, n0 + nblk): device-scope float
+// atomics are the expensive part (measured: 4-8x fewer of them per tile).
+template <typename T, int NV, typename Chan>
+__device__ __forceinline__ void gn_block_add(const ConvFwdArgs<T>& p, const float (&v)[NV],
+                                             long long b, Chan chan, float* red, int n0, int nblk) {
+  constexpr int NC = NV / 2, S = NV / 32;
+  __syncthreads();  // red may alias LDS the main loop read
+  for (int i = threadIdx.x; i < 2 * nblk; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  const int r = threadIdx.x & 31;
+#pragma unroll
+  for (int t = 0; t < S; ++t) {
+    const int j = r * S + t, stat = j / NC, k = j % NC;
+    const int n = chan(k);
+    if (n < p.cout) atomicAdd(red + 2 * (n - n0) + stat, v[t]);
+  }
+  __syncthreads();
+  const int blk = blockIdx.x + gridDim.x * blockIdx.y;
+  float* base = p.gn_sums + (long long)(blk % p.gn_R) * p.gn_rstride + (b * p.cout + n0) * 2;
+  for (int i = threadIdx.x; i < 2 * nblk; i += blockDim.x)
+    if (n0 + i / 2 < p.cout) atomicAdd(base + i, red[i]);
+}
+
+// value as stored (the GroupNorm reads the rounded tensor)
+template <typename T>
+__device__ __forceinline__ float stored(float v) { return (float)(T)v; }
 
 template <typename T>
 __device__ __forceinline__ void store4(T* dst, const float* v);
@@ -87,10 +168,28 @@ __device__ __forceinline__ void load4<bf16>(const bf16* src, float* v) {
 
 // epilogue: lane owns pixel column r of each 32-pixel tile; channels
 // 8g + 4h + e of each 32-channel tile.  y = act(acc + bias) + res.
-template <typename T, int TI, int TJ>
+// STATS: also the GroupNorm statistics of the stored y (gn_rs_reduce) — a
+// separate instantiation, so the plain epilogue keeps its register budget.
+template <typename T, int TI, int TJ, bool STATS = false>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32x16 (&acc)[TJ][TI],
-                                              long long mb, int nb, int r, int h) {
+                                              long long mb, int nb, int r, int h,
+                                              long long blk_m0 = 0, int blk_bm = 0, int blk_n0 = 0,
+                                              int blk_bn = 0, float* red = nullptr) {
   const bool vec_ok = ((p.ldy & 3) == 0) && (p.res == nullptr || (p.ldres & 3) == 0);
+  constexpr int NC = 16 * TJ, NV = STATS ? 2 * NC : 1;
+  float sv[NV];
+  long long clip = 0;
+  bool one_clip = true;
+  if constexpr (STATS) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) sv[k] = 0.f;
+    // the workgroup's pixel rows lie in one clip unless its tile straddles
+    // clips (small shapes only: one atomic pair per element then); decided
+    // per workgroup, so the block-level add below is block-uniform
+    const long long last = (blk_m0 + blk_bm < p.M ? blk_m0 + blk_bm : p.M) - 1;
+    clip = blk_m0 / p.gn_P;
+    one_clip = last / p.gn_P == clip;
+  }
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     const long long m = mb + 32 * i + r;
@@ -121,20 +220,48 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32
             for (int e = 0; e < 4; ++e) v[e] += rr[e];
           }
           store4<T>(p.y + m * p.ldy + n, v);
+          if constexpr (STATS) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float q = stored<T>(v[e]);
+              if (one_clip) {
+                sv[16 * j + 4 * g + e] += q;
+                sv[NC + 16 * j + 4 * g + e] += q * q;
+              } else {
+                float* sb = p.gn_sums + ((m / p.gn_P) * p.cout + n + e) * 2;
+                atomicAdd(sb, q);
+                atomicAdd(sb + 1, q * q);
+              }
+            }
+          }
         } else {
           for (int e = 0; e < 4 && n + e < p.cout; ++e) {
             float t = v[e] + (p.bias ? p.bias[n + e] : 0.f);
             if (p.act == DV_ACT_SILU) t = silu_f(t);
             if (p.res) t += (float)p.res[m * p.ldres + n + e];
             p.y[m * p.ldy + n + e] = (T)t;
+            if constexpr (STATS) {
+              const float q = stored<T>(t);
+              float* sb = p.gn_sums + ((m / p.gn_P) * p.cout + n + e) * 2;
+              atomicAdd(sb, q);
+              atomicAdd(sb + 1, q * q);
+            }
           }
         }
       }
     }
   }
+  if constexpr (STATS) {
+    if (one_clip) {  // block-uniform
+      gn_rs_reduce<NV>(sv, r);
+      gn_block_add<T, NV>(p, sv, clip, [&](int k) {
+        return nb + 32 * (k / 16) + 8 * ((k % 16) / 4) + 4 * h + (k % 4);
+      }, red, blk_n0, blk_bn);
+    }
+  }
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool STATS = false>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs<T> p) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int BK = 4 * VEC;  // K elements per 64-byte LDS row
@@ -241,7 +368,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs<T> p) {
     __syncthreads();
   }
 
-  conv_epilogue<T, TI, TJ>(p, acc, m0 + wm * 32 * TI, n0 + wn * 32 * TJ, r, h);
+  conv_epilogue<T, TI, TJ, STATS>(p, acc, m0 + wm * 32 * TI, n0 + wn * 32 * TJ, r, h, m0, BM, n0, BN,
+                                  (float*)smem);
 }
 
 
@@ -260,7 +388,7 @@ __device__ __attribute__((aligned(64))) unsigned int g_zero_line[16];
 
 __device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, int NBUF>
+template <int BM, int BN, int NBUF, bool STATS = false>
 __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p, int tiles_n) {
   constexpr int TI = BM / 64, TJ = BN / 64;
   constexpr int GB = BM / 32, GA = BN / 32;  // DMA instructions per thread per K-tile
@@ -395,7 +523,8 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p,
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
-  conv_epilogue<bf16, TI, TJ>(p, acc, m0 + wm * 32 * TI, n0 + wn * 32 * TJ, r, h);
+  conv_epilogue<bf16, TI, TJ, STATS>(p, acc, m0 + wm * 32 * TI, n0 + wn * 32 * TJ, r, h, m0, BM, n0, BN,
+                                     (float*)smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -1030,7 +1159,8 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const T* dy, int lddy, f
 template <typename T, int BM, int BN>
 int launch_fwd(const ConvFwdArgs<T>& a, hipStream_t st) {
   dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)((a.cout + BN - 1) / BN));
-  conv_fwd_kernel<T, BM, BN><<<grid, 256, 0, st>>>(a);
+  if (a.gn_sums) conv_fwd_kernel<T, BM, BN, true><<<grid, 256, 0, st>>>(a);
+  else conv_fwd_kernel<T, BM, BN, false><<<grid, 256, 0, st>>>(a);
   return check_launch("conv_fwd");
 }
 
@@ -1042,9 +1172,13 @@ int launch_fwd_glds(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   constexpr int BUF = (BM + BN) * 128;
   constexpr int DEEP = (160 * 1024) / BUF > 6 ? 6 : (160 * 1024) / BUF;
   constexpr int MID = (80 * 1024) / BUF > 3 ? 3 : (80 * 1024) / BUF;
-  if (nb <= 256) conv_fwd_glds_kernel<BM, BN, DEEP><<<(unsigned)nb, 256, 0, st>>>(a, tn);
-  else if (nb <= 512 && MID >= 3) conv_fwd_glds_kernel<BM, BN, MID><<<(unsigned)nb, 256, 0, st>>>(a, tn);
-  else conv_fwd_glds_kernel<BM, BN, 2><<<(unsigned)nb, 256, 0, st>>>(a, tn);
+  const bool stats = a.gn_sums != nullptr;
+#define DV_GL(NB) (stats ? conv_fwd_glds_kernel<BM, BN, NB, true><<<(unsigned)nb, 256, 0, st>>>(a, tn) \
+                         : conv_fwd_glds_kernel<BM, BN, NB, false><<<(unsigned)nb, 256, 0, st>>>(a, tn))
+  if (nb <= 256) DV_GL(DEEP);
+  else if (nb <= 512 && MID >= 3) DV_GL(MID);
+  else DV_GL(2);
+#undef DV_GL
   return check_launch("conv_fwd_glds");
 }
 
@@ -1092,7 +1226,7 @@ struct FsGeom {
   static constexpr int LDS = RING;
 };
 
-template <int W, bool RES>
+template <int W, bool RES, bool STATS>
 __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> p, int nstages,
                                                               int stages_per_block) {
   using G = FsGeom<W>;
@@ -1173,8 +1307,24 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   const int r = lane & 31, h = lane >> 5;
   const int px = pt * 32 + r;  // lane's pixel in the stage; window row of tap (0,0)
   const int bofs = ((px / W) * WP + (px % W)) * FS_XP + h * 16;
+  // GroupNorm statistics (STATS, compile-time like RES): each stage's 32 x 16
+  // sums / squares are reduce-scattered over the half-wave (gn_rs_reduce), so
+  // a lane carries ONE running total across stages; it is added when the
+  // stage range crosses into the next clip (128-pixel stages never straddle
+  // one: the host requires gn_P % 128 == 0) and at the end
+  float sacc[32];  // only sacc[0] is live between stages
+  sacc[0] = 0.f;
+  constexpr bool stats = STATS;
+  auto chan = [&](int k) { return co0 + ch * 32 + 8 * (k / 4) + 4 * h + (k % 4); };
 
   for (int st = 0; st < nst; ++st) {
+    if constexpr (stats) if (st > 0) {
+      const long long c_prev = (long long)(sbeg + st - 1) * 128 / p.gn_P;
+      if ((long long)(sbeg + st) * 128 / p.gn_P != c_prev) {
+        gn_rs_add<bf16, 32>(p, sacc, c_prev, chan);
+        sacc[0] = 0.f;
+      }
+    }
     const int buf = st & 3;
     // window fragments read FSD k-steps ahead of their MFMA (k-step k = tap
     // k / 4, 16 channels at (k % 4) * 16).  The reads are inline asm with
@@ -1205,6 +1355,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     });
     // epilogue: lane owns pixel m, channels 8g + 4h + e of the wave's 32
     const bool silu = p.act == DV_ACT_SILU;
+    float sv[stats ? 32 : 1];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int n = ch * 32 + 8 * g + 4 * h;
@@ -1220,6 +1371,18 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
         for (int e = 0; e < 4; ++e) v[e] += (float)rv[g][e];
       }
       store4<bf16>(p.y + m * p.ldy + co0 + n, v);
+      if constexpr (stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float q = stored<bf16>(v[e]);
+          sv[4 * g + e] = q;
+          sv[16 + 4 * g + e] = q * q;
+        }
+      }
+    }
+    if constexpr (stats) {
+      gn_rs_reduce<32>(sv, r);
+      sacc[0] += sv[0];
     }
     // stage st+1's window landed.  vmcnt retires in order over loads AND
     // stores; younger than DMA(st+1) are the previous stage's 4 stores, the
@@ -1236,6 +1399,12 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     // barrier.  Issued here, where a wave would otherwise wait at the barrier.
     if (st + 3 < nst) issue(st + 3, (st + 3) & 3);
     __builtin_amdgcn_s_barrier();
+  }
+  if constexpr (stats) {
+    // the clip of the block's last stage (block-uniform); earlier clips were
+    // added per wave at the crossing (rare: stage ranges align with clips)
+    __shared__ float red[2 * 64];
+    if (nst > 0) gn_block_add<bf16, 32>(p, sacc, (long long)(sbeg + nst - 1) * 128 / p.gn_P, chan, red, co0, 64);
   }
 }
 
@@ -1254,13 +1423,15 @@ int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   bx = (nstages + sps - 1) / sps;
   dim3 grid(bx, ct);
   const bool res = a.res != nullptr;
+  const bool stats = a.gn_sums != nullptr;
+#define DV_FS(WW, RR) (stats ? conv_fwd_stripe_kernel<WW, RR, true><<<grid, 512, 0, st>>>(a, nstages, sps) \
+                             : conv_fwd_stripe_kernel<WW, RR, false><<<grid, 512, 0, st>>>(a, nstages, sps))
   if (a.W == 64) {
-    if (res) conv_fwd_stripe_kernel<64, true><<<grid, 512, 0, st>>>(a, nstages, sps);
-    else conv_fwd_stripe_kernel<64, false><<<grid, 512, 0, st>>>(a, nstages, sps);
+    if (res) DV_FS(64, true); else DV_FS(64, false);
   } else {
-    if (res) conv_fwd_stripe_kernel<32, true><<<grid, 512, 0, st>>>(a, nstages, sps);
-    else conv_fwd_stripe_kernel<32, false><<<grid, 512, 0, st>>>(a, nstages, sps);
+    if (res) DV_FS(32, true); else DV_FS(32, false);
   }
+#undef DV_FS
   return check_launch("conv_fwd_stripe");
 }
 
@@ -1284,7 +1455,7 @@ bool stripe_geom(int h, int w, int& seg, int& nseg);
 constexpr int F2_WP = 592;  // weight row pitch: 9 taps x 32 ci bf16 + 16 B
 constexpr int F2_XP = 80;   // window pixel pitch: 32 ci bf16 + 16 B
 
-template <int W>
+template <int W, bool STATS = false>
 __global__ __launch_bounds__(512) void conv_fwd_stripe2_kernel(ConvFwdArgs<bf16> p, int seg, int nseg) {
   constexpr int WP = W + 2;
   constexpr int NWIN = W == 8 ? 200 : (128 / W + 2) * WP;   // window pixels (max over H)
@@ -1380,7 +1551,8 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe2_kernel(ConvFwdArgs<bf16>
     if (hc + 1 < nhc) store((hc + 1) & 1);
     __syncthreads();
   }
-  conv_epilogue<bf16, 1, 1>(p, acc, m0 + pt * 32, co0 + ch * 32, r, h);
+  conv_epilogue<bf16, 1, 1, STATS>(p, acc, m0 + pt * 32, co0 + ch * 32, r, h, m0, 128, co0, 64,
+                                   (float*)smem);
 }
 
 bool fwd_stripe2_ok(long long M, int h, int w, int cin, int c0, bool split, int cout, int ks, int& seg,
@@ -1396,10 +1568,13 @@ bool fwd_stripe2_ok(long long M, int h, int w, int cin, int c0, bool split, int 
 int launch_fwd_stripe2(const ConvFwdArgs<bf16>& a, int seg, int nseg, hipStream_t st) {
   dim3 grid((unsigned)(a.M / 128), a.cout / 64);
   switch (a.W) {
-    case 64: conv_fwd_stripe2_kernel<64><<<grid, 512, 0, st>>>(a, seg, nseg); break;
-    case 32: conv_fwd_stripe2_kernel<32><<<grid, 512, 0, st>>>(a, seg, nseg); break;
-    case 16: conv_fwd_stripe2_kernel<16><<<grid, 512, 0, st>>>(a, seg, nseg); break;
-    default: conv_fwd_stripe2_kernel<8><<<grid, 512, 0, st>>>(a, seg, nseg); break;
+#define DV_S2(WW) (a.gn_sums ? conv_fwd_stripe2_kernel<WW, true><<<grid, 512, 0, st>>>(a, seg, nseg) \
+                          : conv_fwd_stripe2_kernel<WW, false><<<grid, 512, 0, st>>>(a, seg, nseg))
+    case 64: DV_S2(64); break;
+    case 32: DV_S2(32); break;
+    case 16: DV_S2(16); break;
+    default: DV_S2(8); break;
+#undef DV_S2
   }
   return check_launch("conv_fwd_stripe2");
 }
@@ -1465,7 +1640,7 @@ __device__ __forceinline__ int fw_pix(int r) {
   else return (ga ? 0 : 16) + a;
 }
 
-template <int W>
+template <int W, bool STATS = false>
 __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
   using G = FwGeom<W>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
@@ -1586,6 +1761,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   }
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e
   const long long m = m0 + tpx;
+  float sv[STATS ? 64 : 1];  // STATS: [0,32) sums, [32,64) squares of the lane's 32 channels
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
 #pragma unroll
@@ -1610,7 +1786,21 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
         for (int e = 0; e < 4; ++e) v[e] += rr[e];
       }
       store4<bf16>(p.y + m * p.ldy + n, v);
+      if constexpr (STATS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float q = stored<bf16>(v[e]);
+          sv[16 * j + 4 * g + e] = q;
+          sv[32 + 16 * j + 4 * g + e] = q * q;
+        }
+      }
     }
+  }
+  if constexpr (STATS) {  // the host requires gn_P % 128 == 0: the tile is in one clip
+    gn_rs_reduce<64>(sv, r);
+    gn_block_add<bf16, 64>(p, sv, m0 / p.gn_P, [&](int k) {
+      return co0 + 32 * (k / 16) + 8 * ((k % 16) / 4) + 4 * h + (k % 4);
+    }, (float*)smem, co0, 64);
   }
 }
 
@@ -1627,10 +1817,13 @@ bool fwd_frame_ok(const ConvFwdArgs<bf16>& a, int h, int w) {
 int launch_fwd_frame(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   const int nblk = (int)(a.M / 128) * (a.cout / 64);
   switch (a.W) {
-    case 8: conv_fwd_frame_kernel<8><<<nblk, 256, 0, st>>>(a); break;
-    case 16: conv_fwd_frame_kernel<16><<<nblk, 256, 0, st>>>(a); break;
-    case 32: conv_fwd_frame_kernel<32><<<nblk, 256, 0, st>>>(a); break;
-    default: conv_fwd_frame_kernel<64><<<nblk, 256, 0, st>>>(a); break;
+#define DV_FW(WW) (a.gn_sums ? conv_fwd_frame_kernel<WW, true><<<nblk, 256, 0, st>>>(a) \
+                          : conv_fwd_frame_kernel<WW, false><<<nblk, 256, 0, st>>>(a))
+    case 8: DV_FW(8); break;
+    case 16: DV_FW(16); break;
+    case 32: DV_FW(32); break;
+    default: DV_FW(64); break;
+#undef DV_FW
   }
   return check_launch("conv_fwd_frame");
 }
@@ -1644,19 +1837,32 @@ inline void glds_tile(long long M, int cout, int& bm, int& bn) {
   if (bn == 128 && ((M + 127) / 128) * ((cout + 127) / 128) < 256) bm = 64;
 }
 
+// the statistics epilogue's fields (off when gn_sums is null)
+template <typename T>
+void set_gn(ConvFwdArgs<T>& a, float* gn_sums, long long gn_P, int gn_R) {
+  a.gn_sums = gn_sums;
+  a.gn_P = gn_sums ? gn_P : 1;
+  a.gn_R = gn_R > 0 ? gn_R : 1;
+  a.gn_rstride = gn_sums ? (a.M / a.gn_P) * a.cout * 2 : 0;
+}
+
 template <typename T>
 int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const void* w,
                const float* bias, const void* res, int ldres, void* y, int ldy, int nf, int h,
-               int wd, int cin, int cout, int ks, int act, hipStream_t st) {
+               int wd, int cin, int cout, int ks, int act, float* gn_sums, long long gn_P,
+               int gn_R, hipStream_t st) {
   ConvFwdArgs<T> a;
   a.x0 = (const T*)x0; a.x1 = (const T*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0;
   a.c0 = x1 ? c0 : cin; a.w = (const T*)w; a.bias = bias; a.res = (const T*)res;
   a.ldres = ldres; a.y = (T*)y; a.ldy = ldy; a.H = h; a.W = wd; a.cin = cin; a.cout = cout;
   a.ks = ks; a.act = act; a.M = (long long)nf * h * wd; a.K = ks * ks * cin;
+  set_gn(a, gn_sums, gn_P, gn_R);
   if (a.M == 0 || cout == 0) return DV_OK;
   if constexpr (sizeof(T) == 2) {
+    // the stripe kernel flushes statistics per 128-pixel stage: clips must
+    // be whole stages
     if (fwd_stripe_ok(a.M, h, wd, cin, x1 != nullptr, cout, ks, ld0) && (ldy & 3) == 0 &&
-        (res == nullptr || (ldres & 3) == 0))
+        (res == nullptr || (ldres & 3) == 0) && (!gn_sums || gn_P % 128 == 0))
       return launch_fwd_stripe(a, st);
     int seg, nseg;
     static const bool no_s2 = getenv("DV_NO_STRIPE2") != nullptr;  // A/B switch for profiling
@@ -2169,9 +2375,11 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
 extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
                            const void* wpack, const float* bias, const void* res, int ldres,
                            void* y, int ldy, int nf, int h, int w, int cin, int cout, int ksize,
-                           int act, void* stream) {
+                           int act, float* gn_sums, long long gn_P, int gn_R, void* stream) {
   DV_REQUIRE(x0 && wpack && y, "null pointer");
   DV_REQUIRE(cin > 0 && cin % 8 == 0, "cin must be a positive multiple of 8");
+  DV_REQUIRE(!gn_sums || (gn_P > 0 && ((long long)nf * h * w) % gn_P == 0 && gn_R >= 1),
+             "GroupNorm statistics: the pixels must be whole clips of gn_P");
   DV_REQUIRE(ld0 % 8 == 0 && (!x1 || (ld1 % 8 == 0 && c0 % 8 == 0 && c0 > 0 && c0 < cin)),
              "input strides / split must be multiples of 8");
   DV_REQUIRE(ksize >= 1 && (ksize & 1), "ksize must be odd");
@@ -2179,18 +2387,21 @@ extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const voi
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DV_F32)
     return conv_fwd_t<float>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, y, ldy, nf, h, w,
-                             cin, cout, ksize, act, st);
+                             cin, cout, ksize, act, gn_sums, gn_P, gn_R, st);
   if (dtype == DV_BF16)
     return conv_fwd_t<bf16>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, y, ldy, nf, h, w,
-                            cin, cout, ksize, act, st);
+                            cin, cout, ksize, act, gn_sums, gn_P, gn_R, st);
   DV_REQUIRE(false, "unknown dtype");
 }
 
 extern "C" int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
                             const void* wpack, const float* bias, const void* res, int ldres,
                             void* y, int ldy, int nf, int h, int w, int cin, int cout, int act,
-                            void* stream) {
+                            float* gn_sums, long long gn_P, int gn_R, void* stream) {
   DV_REQUIRE(dtype == DV_BF16, "the window conv is bf16 only");
+  DV_REQUIRE(!gn_sums || (gn_P > 0 && gn_P % 128 == 0 && ((long long)nf * h * w) % gn_P == 0 &&
+                          gn_R >= 1),
+             "GroupNorm statistics in the window conv: clips of gn_P % 128 == 0 pixels");
   DV_REQUIRE(x0 && wpack && y, "null pointer");
   DV_REQUIRE(cin > 0 && (!x1 || (c0 > 0 && c0 < cin)), "bad channel split");
   DV_REQUIRE(ldy >= cout && (!res || ldres >= cout), "bad output stride");
@@ -2199,6 +2410,7 @@ extern "C" int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const vo
   a.c0 = x1 ? c0 : cin; a.w = (const bf16*)wpack; a.bias = bias; a.res = (const bf16*)res;
   a.ldres = ldres; a.y = (bf16*)y; a.ldy = ldy; a.H = h; a.W = w; a.cin = cin; a.cout = cout;
   a.ks = 3; a.act = act; a.M = (long long)nf * h * w; a.K = 9 * cin;
+  set_gn(a, gn_sums, gn_P, gn_R);
   DV_REQUIRE(fwd_frame_ok(a, h, w), "shape/stride outside the window conv (see dv_hip.h)");
   if (a.M == 0) return DV_OK;
   return launch_fwd_frame(a, (hipStream_t)stream);

@@ -256,14 +256,16 @@ __device__ void gn_group_terms(const GnArgs& a, int b, float* cs, float* prm, fl
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cg = a.C / a.G;
   const long long sb = (long long)b * a.C * 2;
   for (int c = threadIdx.x; c < a.C; c += 256) {
-    float __attribute__((ext_vector_type(2))) v[8];  // all R (<= 8) replicas in flight at once
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-      if (r < a.R) v[r] = *(const float __attribute__((ext_vector_type(2)))*)(a.sums + r * a.rstride + sb + 2 * c);
     float v1 = 0.f, v2 = 0.f;
+    for (int r0 = 0; r0 < a.R; r0 += 8) {  // 8 replicas in flight at once (R <= 64)
+      float __attribute__((ext_vector_type(2))) v[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
-      if (r < a.R) { v1 += v[r][0]; v2 += v[r][1]; }
+      for (int r = 0; r < 8; ++r)
+        if (r0 + r < a.R) v[r] = *(const float __attribute__((ext_vector_type(2)))*)(a.sums + (r0 + r) * a.rstride + sb + 2 * c);
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (r0 + r < a.R) { v1 += v[r][0]; v2 += v[r][1]; }
+    }
     cs[c] = v1;
     cs[a.C + c] = v2;
   }
@@ -516,9 +518,10 @@ void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
 }
 
 template <typename T>
-int gn_fwd_t(GnArgs a, hipStream_t st) {
+int gn_fwd_t(GnArgs a, int sums_replicas, hipStream_t st) {
   const GnTune& t = gn_tune();
-  gn_reduce_launch<T, 0>(a, t.ur0, t.tr0, st);
+  if (sums_replicas > 0) a.R = sums_replicas;  // statistics from the conv epilogue
+  else gn_reduce_launch<T, 0>(a, t.ur0, t.tr0, st);
   gn_apply_launch<T, 0>(a, t.ua0, t.ta0, st);
   return check_launch("gn_fwd");
 }
@@ -647,8 +650,11 @@ extern "C" int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, co
                          int ldres, int nb, long long P, int C, int G, float eps,
                          const float* gamma, const float* beta, const float* ss, int act,
                          float* mean, float* rstd, float* sums, float* next, long long next_n,
-                         void* stream) {
+                         int sums_replicas, void* stream) {
   DV_REQUIRE(z && y && gamma && beta && mean && rstd && sums, "null pointer");
+  DV_REQUIRE(sums_replicas >= 0 && sums_replicas <= 64 &&
+             (sums_replicas == 0 || !next || (long long)sums_replicas * nb * C * 2 <= next_n),
+             "sums_replicas must fit the sums buffer (<= 64)");
   DV_REQUIRE(C % G == 0, "C % G != 0");
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && ldy % VEC == 0 && (!res || ldres % VEC == 0),
@@ -663,7 +669,7 @@ extern "C" int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, co
   a.R = next && a.rstride > 0 ? (int)std::min<long long>(8, std::max<long long>(1, next_n / a.rstride)) : 1;
   if (nb == 0 || P == 0) return DV_OK;
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DV_BF16 ? gn_fwd_t<bf16>(a, st) : gn_fwd_t<float>(a, st);
+  return dtype == DV_BF16 ? gn_fwd_t<bf16>(a, sums_replicas, st) : gn_fwd_t<float>(a, sums_replicas, st);
 }
 
 extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void* dz,

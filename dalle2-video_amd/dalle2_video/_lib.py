@@ -26,8 +26,10 @@ _F = ctypes.c_float
 _SIGS = {
     "dv_abi_version": [],
     "dv_zero_f32": [_P, _L, _P],
-    "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
-    "dv_conv_fwd8": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I,
+                    _P, _L, _I, _P],
+    "dv_conv_fwd8": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
+                     _P, _L, _I, _P],
     "dv_xattn_fold_batched": [_I, _P, _I, _F, _P],
     "dv_xattn_fold_bwd_batched": [_P, _I, _F, _P],
     "dv_conv_wgrad_ws": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
@@ -35,7 +37,8 @@ _SIGS = {
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
     "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "dv_pack_conv_weights_batched": [_P, _I, _L, _P],
-    "dv_gn_fwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P, _L, _P],
+    "dv_gn_fwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P, _L,
+                  _I, _P],
     "dv_gn_bwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "dv_ln_fwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _P, _F, _P, _P, _P],
     "dv_ln_bwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _F, _P, _P, _P],

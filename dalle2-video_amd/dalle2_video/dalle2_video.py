@@ -405,10 +405,15 @@ class Block3D(nn.Module):
         self.norm = nn.GroupNorm(groups, dim_out)
         self.act = nn.SiLU()
 
-    def forward_cl(self, x0, nb, x1=None, scale_shift=None, res=None, sink=None):
-        z = ops.conv(x0, self.project.weight, self.project.bias, x1=x1, sink=sink)
+    def forward_cl(self, x0, nb, x1=None, scale_shift=None, res=None, sink=None, res_sink=None):
+        # the conv's epilogue accumulates the GroupNorm statistics of z, so the
+        # norm is a single apply pass over z
+        nf, h, w = x0.shape[:3]
+        st = ops.gn_stats(nb, self.project.out_channels, (nf // nb) * h * w, x0.device)
+        z = ops.conv(x0, self.project.weight, self.project.bias, x1=x1, sink=sink, gn=st)
         return ops.group_norm_act(z, self.norm.weight, self.norm.bias, nb, self.norm.num_groups,
-                                  self.norm.eps, scale_shift=scale_shift, res=res, act=ACT_SILU)
+                                  self.norm.eps, scale_shift=scale_shift, res=res, act=ACT_SILU,
+                                  stats=st, res_sink=res_sink)
 
     def forward(self, x, scale_shift=None):
         b, c, t = x.shape[:3]
@@ -445,10 +450,14 @@ class ResnetBlock3D(nn.Module):
         # res_conv runs first so that its (cheap, 1x1) input-gradient is the
         # one that accumulates into block1's 3x3 dgrad output, not the reverse:
         # autograd runs the later-recorded node's backward first
-        if isinstance(self.res_conv, nn.Identity):
+        identity = isinstance(self.res_conv, nn.Identity)
+        if identity:
             if x1 is not None:
                 raise DVError("identity residual with a split input")
-            sink, res = None, x0
+            # block2's residual add and block1's conv both read x0: the
+            # residual gradient (block2's dy) becomes block1's dgrad
+            # accumulator (no autograd add of two full tensors)
+            sink, res = ops.GradSink(), x0
         else:
             sink = ops.GradSink()
             res = ops.conv(x0, self.res_conv.weight, self.res_conv.bias, x1=x1, sink=sink)
@@ -456,7 +465,7 @@ class ResnetBlock3D(nn.Module):
         if exists(self.cross_attn):
             assert exists(cond)
             h = self.cross_attn.forward_cl(h, cond, nb, kv=kv, fold=fold)
-        return self.block2.forward_cl(h, nb, res=res)
+        return self.block2.forward_cl(h, nb, res=res, res_sink=sink if identity else None)
 
     def forward(self, x, time_emb=None, cond=None):
         b, c, t = x.shape[:3]

@@ -81,11 +81,12 @@ def _launch(name, flops, nbytes, fn, shape=None):
         TIMER.run(name, flops, nbytes, fn, shape)
 
 
-def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0):
+def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0):
     """Kernel instantiation dv_conv_fwd dispatches to (mirror of conv_fwd_t /
     glds_tile in dv_conv.hip) — names the launch for the live roofline."""
     if (dtype_name == "bf16" and ks == 3 and cin == 64 and c0 == cin and cout % 64 == 0
-            and w in (32, 64) and h % (128 // w) == 0 and m % 128 == 0 and m * maxld < (1 << 31)):
+            and w in (32, 64) and h % (128 // w) == 0 and m % 128 == 0 and m * maxld < (1 << 31)
+            and gn_P % 128 == 0):
         return f"conv_fwd_stripe_kernel<{w}>"
     if (dtype_name == "bf16" and ks == 3 and cin % 32 == 0 and c0 % 32 == 0 and cout % 64 == 0
             and m % 128 == 0 and m * maxld < (1 << 31) and _stripe_geom_ok(h, w)
@@ -113,10 +114,12 @@ _NO_WINDOW = bool(os.environ.get("DV_NO_WINDOW"))  # A/B switch: 3x3 convs on dv
 _WINDOW_W = tuple(int(v) for v in os.environ.get("DV_WINDOW_W", "8,16").split(",") if v)
 
 
-def window_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf):
-    """Mirror of fwd_frame_ok (dv_conv.hip): the window-form 3x3 conv (dv_conv_fwd8)."""
+def window_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf, gn_P=0):
+    """Mirror of fwd_frame_ok (dv_conv.hip): the window-form 3x3 conv (dv_conv_fwd8);
+    with the GroupNorm statistics epilogue its clips must be whole 128-pixel tiles."""
     geom = (h == 8 and w == 8 and nf % 2 == 0) or (w in (16, 32, 64) and (h * w) % 128 == 0)
     return (not _NO_WINDOW and w in _WINDOW_W and x0.dtype == torch.bfloat16 and ksize == 3
+            and gn_P % 128 == 0
             and geom and cin % 16 == 0 and c0 % 16 == 0 and cout % 64 == 0
             and not (cin == 64 and c0 == cin and w in (32, 64))  # the resident-weight stripe kernel
             and ld0 % 8 == 0 and ld1 % 8 == 0 and ldy % 4 == 0 and ldres % 4 == 0
@@ -269,6 +272,28 @@ def _gn_sums(device):
     if key not in _GN_WS:
         _GN_WS[key] = _GnSums(device)
     return _GN_WS[key]
+
+
+class GnStats:
+    """The sums buffer a conv's statistics epilogue fills for the GroupNorm
+    that reads its output (Block3D: project -> norm, dalle2_video.py:107-109):
+    one take() of the alternating _GnSums pair, R replicas of [nb][C][2]."""
+
+    # replicas: the conv's device-scope atomics serialise per address (they
+    # resolve past the XCD L2s), so the statistics spread over as many
+    # replicas as the buffer holds (<= 64); the apply sums them from L2
+    MAX_R = int(os.environ.get("DV_GN_STATS_R", "8"))
+    ALL = os.environ.get("DV_GN_STATS_ALL") == "1"  # A/B switch: every conv kernel accumulates
+
+    def __init__(self, nb, C, P, device):
+        self.cur, self.nxt = _gn_sums(device).take(nb * C * 2)
+        self.R = max(1, min(self.MAX_R, self.cur.numel() // (nb * C * 2)))
+        self.P = P
+        self.used = False  # set by the conv: did its epilogue accumulate?
+
+
+def gn_stats(nb, C, P, device):
+    return GnStats(nb, C, P, device)
 
 
 def gn_graph_boundary(device):
@@ -434,7 +459,8 @@ class ConvFn(torch.autograd.Function):
     """y = conv_(1,k,k)(cat(x0, x1)) + bias (+ res).  dalle2_video.py:107 etc."""
 
     @staticmethod
-    def forward(ctx, x0, x1, weight, bias, res, ksize, sink=None, cache=True, algo_scale=1.0):
+    def forward(ctx, x0, x1, weight, bias, res, ksize, sink=None, cache=True, algo_scale=1.0,
+                gn=None):
         require_gpu(x0, x1, weight, bias, res)
         nf, h, w, c0 = x0.shape
         c1 = 0 if x1 is None else x1.shape[3]
@@ -453,20 +479,33 @@ class ConvFn(torch.autograd.Function):
         flops = 2.0 * m * cout * cin * ksize * ksize * algo_scale
         nbytes = x0.element_size() * m * (cin + cout)
         shape = ("fwd", m, cout, cin * ksize * ksize)
-        if window_ok(x0, x1, cin, c0 if x1 is not None else cin, cout, ld0, ld1 or ld0, cout,
-                     ldr, ksize, h, w, nf):
+        # GroupNorm statistics epilogue (gn: a GnStats of the GroupNorm reading y)
+        # where it measured cheaper than the GroupNorm's own reduce pass
+        # (tools/gnstats_bench.py): the resident-weight stripe kernel (stage-0/1
+        # Block3D convs) and the 8x8 window kernel; elsewhere gn.used = False
+        # and the GroupNorm reduces z itself
+        use_win = window_ok(x0, x1, cin, c0 if x1 is not None else cin, cout, ld0, ld1 or ld0, cout,
+                            ldr, ksize, h, w, nf, gn.P if gn is not None else 0)
+        if gn is not None:
+            name = (f"conv_fwd_frame_kernel<{w}>" if use_win else
+                    conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
+                                  max(ld0, ld1), ksize, h, w, gn.P))
+            gn.used = GnStats.ALL or name in ("conv_fwd_stripe_kernel<64>", "conv_fwd_stripe_kernel<32>",
+                                              "conv_fwd_frame_kernel<8>")
+        gs, gP, gR = (ptr(gn.cur), gn.P, gn.R) if gn is not None and gn.used else (None, 0, 0)
+        if use_win:
             wp = pack_conv_weight(weight, x0.dtype, cin, 2, cache)
             _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                     lambda: call("dv_conv_fwd8", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp),
                                  ptr(b), ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ACT_NONE,
-                                 stream()), shape)
+                                 gs, gP, gR, stream()), shape)
         else:
             wp = pack_conv_weight(weight, x0.dtype, cin, 0, cache)
             _launch(conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
-                                  max(ld0, ld1), ksize, h, w), flops, nbytes,
+                                  max(ld0, ld1), ksize, h, w, gP), flops, nbytes,
                     lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b),
                                  ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE,
-                                 stream()), shape)
+                                 gs, gP, gR, stream()), shape)
         ctx.save_for_backward(x0, x1, weight)
         ctx.params = (weight, bias)
         ctx.meta = (ksize, c0, c1, bias is not None, res is not None)
@@ -499,24 +538,27 @@ class ConvFn(torch.autograd.Function):
             else:
                 alloc = torch.empty if cin_real == cin else torch.zeros
                 dx = alloc(nf, h, w, cin, dtype=dy.dtype, device=dy.device)
-            rp, rld = (ptr(dx), cin) if acc is not None else (None, 0)
+            # the accumulated buffer may be a strided channel view (the dy a
+            # GroupNorm handed over): read and write it through its pixel stride
+            ldx = cl_ld(dx) if acc is not None else cin
+            rp, rld = (ptr(dx), ldx) if acc is not None else (None, 0)
             m = nf * h * w
             flops = 2.0 * m * cin_real * cout8 * ksize * ksize * ctx.algo_scale
             nbytes = dy8.element_size() * m * (cin + cout8)
             shape = ("dgrad", m, cin_real, cout8 * ksize * ksize)
-            if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, cin, 0, ksize, h, w, nf):
+            if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, ldx, rld, ksize, h, w, nf):
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 3, ctx.cache)
                 _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                         lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd),
-                                     None, rp, rld, ptr(dx), cin, nf, h, w, cout8, cin_real, ACT_NONE,
-                                     stream()), shape)
+                                     None, rp, rld, ptr(dx), ldx, nf, h, w, cout8, cin_real, ACT_NONE,
+                                     None, 0, 0, stream()), shape)
             else:
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 1, ctx.cache)
                 _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, lddy, ksize, h, w),
                         flops, nbytes,
                         lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd), None,
-                                     rp, rld, ptr(dx), cin, nf, h, w, cout8, cin_real, ksize, ACT_NONE,
-                                     stream()), shape)
+                                     rp, rld, ptr(dx), ldx, nf, h, w, cout8, cin_real, ksize, ACT_NONE,
+                                     None, 0, 0, stream()), shape)
             if sink is not None and acc is None:
                 sink.dx = dx  # first reader: the other conv's backward adds into it
             else:
@@ -571,18 +613,20 @@ class ConvFn(torch.autograd.Function):
             elif db_buf is not bslot[0]:
                 bslot[0].add_(db_buf[:cout])
         dres = dy if has_res else None
-        return dx0, dx1, dw, db, dres, None, None, None, None
+        return dx0, dx1, dw, db, dres, None, None, None, None, None
 
 
-def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_scale=1.0):
+def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_scale=1.0, gn=None):
     """(1,k,k) 'same' convolution over channels-last frames (weight in torch
     Conv3d layout (cout, cin, 1, k, k) or Linear layout (cout, cin)).
     sink: a GradSink shared with the other conv reading (x0, x1).
     cache=False: the weight is rebuilt every call (not a parameter), so its
     packed image is made on every call instead of kept in the PackCache.
-    algo_scale: algorithmic / executed FLOPs (timing labels only)."""
+    algo_scale: algorithmic / executed FLOPs (timing labels only).
+    gn: a GnStats (gn_stats()) — the kernel's epilogue accumulates the
+    GroupNorm statistics of y for the group_norm_act(stats=gn) that follows."""
     k = weight.shape[-1] if weight.dim() == 5 else 1
-    return ConvFn.apply(x0, x1, weight, bias, res, k, sink, cache, algo_scale)
+    return ConvFn.apply(x0, x1, weight, bias, res, k, sink, cache, algo_scale, gn)
 
 
 # ---------------------------------------------------------------------------
@@ -590,7 +634,7 @@ def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_s
 # ---------------------------------------------------------------------------
 class GroupNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, z, gamma, beta, ss, res, nb, groups, eps, act):
+    def forward(ctx, z, gamma, beta, ss, res, nb, groups, eps, act, stats=None, res_sink=None):
         require_gpu(z, gamma, beta, ss, res)
         nf, h, w, c = z.shape
         P = (nf // nb) * h * w
@@ -598,15 +642,23 @@ class GroupNormActFn(torch.autograd.Function):
         y = torch.empty(nf, h, w, c, dtype=z.dtype, device=dev)
         mean = torch.empty(nb * groups, dtype=torch.float32, device=dev)
         rstd = torch.empty_like(mean)
-        cur, nxt = _gn_sums(dev).take(nb * c * 2)
+        if stats is not None and stats.used:  # z's producing conv accumulated the statistics
+            if stats.P != P:
+                raise _lib.DVError("GroupNorm statistics were accumulated for another clip size")
+            cur, nxt, ready = stats.cur, stats.nxt, stats.R
+        elif stats is not None:  # the conv did not: reduce into the same (zeroed) buffer
+            cur, nxt, ready = stats.cur, stats.nxt, 0
+        else:
+            (cur, nxt), ready = _gn_sums(dev).take(nb * c * 2), 0
         g, b = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
         s = None if ss is None else ss.detach().float().contiguous()
         call("dv_gn_fwd", dt(z), ptr(z), cl_ld(z), ptr(y), c, ptr(res), cl_ld(res) if res is not None else 0,
              nb, P, c, groups, ctypes_float(eps), ptr(g), ptr(b), ptr(s), act, ptr(mean), ptr(rstd),
-             ptr(cur), ptr(nxt), nxt.numel(), stream())
+             ptr(cur), ptr(nxt), nxt.numel(), ready, stream())
         ctx.save_for_backward(z, g, b, s, mean, rstd)
         ctx.params = (gamma, beta)
         ctx.meta = (nb, groups, act, ss is not None, res is not None)
+        ctx.res_sink = res_sink
         return y
 
     @staticmethod
@@ -633,7 +685,15 @@ class GroupNormActFn(torch.autograd.Function):
              acc, stream())
         if not ret:
             dg = db = None
-        return dz, dg, db, dss, (dy if has_res else None), None, None, None, None
+        dres = dy if has_res else None
+        if dres is not None and ctx.res_sink is not None and ctx.needs_input_grad[4]:
+            # identity residual (ResnetBlock3D, dalle2_video.py:205): the
+            # residual's gradient is dy itself; block1's conv, the other
+            # reader of the same input, adds its dgrad into it in the kernel
+            # epilogue (GradSink) instead of autograd adding two tensors
+            ctx.res_sink.dx = dy
+            dres = None
+        return dz, dg, db, dss, dres, None, None, None, None, None, None
 
 
 def ctypes_float(v):
@@ -642,8 +702,11 @@ def ctypes_float(v):
 
 
 def group_norm_act(z, gamma, beta, nb, groups=8, eps=1e-5, scale_shift=None, res=None,
-                   act=_lib.ACT_SILU):
-    return GroupNormActFn.apply(z, gamma, beta, scale_shift, res, nb, groups, eps, act)
+                   act=_lib.ACT_SILU, stats=None, res_sink=None):
+    """stats: the GnStats z's conv filled (one apply launch) or None (reduce + apply).
+    res_sink: a GradSink shared with the conv that also reads `res` (the
+    residual's gradient is handed to it instead of returned to autograd)."""
+    return GroupNormActFn.apply(z, gamma, beta, scale_shift, res, nb, groups, eps, act, stats, res_sink)
 
 
 # ---------------------------------------------------------------------------

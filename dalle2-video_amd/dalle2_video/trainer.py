@@ -11,8 +11,9 @@ on the MI355X path.
 * Gradient clipping (`clip_grad_norm_(decoder.parameters(), 0.5)`,
   trainer.py:254-257) is a HIP reduction whose coefficient is applied inside
   the AdamW kernel: no host synchronisation.
-* Data parallel: one process per GPU (torchrun); the active unet's flat
-  gradient is summed with a single RCCL all-reduce over xGMI and the 1/world
+* Data parallel: one process per GPU (torchrun); the loaders are sharded per
+  rank, the active unet's flat gradient is summed with RCCL all-reduces over
+  xGMI (~25 MB buckets, back to front, async on RCCL's stream) and the 1/world
   average is folded into the update coefficient.  No other collective.
 """
 from __future__ import annotations
@@ -376,13 +377,29 @@ def broadcast_parameters(module, src=0):
         dist.broadcast(p.data, src)
 
 
-def allreduce_flat_grad(flat_grad, world):
-    """The only collective on the data path: ONE all-reduce (SUM) of the active
-    unet's flat f32 gradient (RCCL over xGMI on the GPU box).  The 1/world
-    average is not applied here: it is folded into the clip coefficient
-    (dv_grad_clip_coef's prescale), which the AdamW kernel multiplies in."""
-    if world > 1 and flat_grad is not None:
-        dist.all_reduce(flat_grad)
+BUCKET_BYTES = int(os.environ.get("DV_BUCKET_MB", "25")) * (1 << 20)
+
+
+def allreduce_flat_grad(flat_grad, world, bucket_bytes=None):
+    """The only collective on the data path: the SUM all-reduce of the active
+    unet's flat f32 gradient (RCCL over xGMI on the GPU box), in ~25 MB
+    buckets issued back to front (the flat buffer follows parameter order, so
+    the last buckets hold the output layers whose gradients the backward
+    finished first).  Every bucket is an async collective on the process
+    group's own stream (RCCL's comm stream): the buckets pipeline through the
+    7 xGMI links instead of one 200 MB ring, and the caller's stream waits
+    for all of them once.  The 1/world average is not applied here: it is
+    folded into the clip coefficient (dv_grad_clip_coef's prescale), which
+    the AdamW kernel multiplies in."""
+    if world <= 1 or flat_grad is None:
+        return flat_grad
+    n = flat_grad.numel()
+    per = max(1, (bucket_bytes or BUCKET_BYTES) // flat_grad.element_size())
+    works = []
+    for end in range(n, 0, -per):
+        works.append(dist.all_reduce(flat_grad[max(0, end - per):end], async_op=True))
+    for w in works:
+        w.wait()
     return flat_grad
 
 

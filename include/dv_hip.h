@@ -47,11 +47,17 @@ int dv_zero_f32(float* p, long long n, void* stream);
  * Input channels [0,c0) come from x0 (stride ld0), [c0,cin) from x1 (ld1);
  * c0 must be a multiple of 8 (pass c0=cin, x1=NULL for one source).
  * wpack: packed weight [cout][k*k][cin] of `dtype` (dv_pack_conv_weight).
- * Epilogue: y = act(acc + bias) + res.  cin % 8 == 0 required.            */
+ * Epilogue: y = act(acc + bias) + res.  cin % 8 == 0 required.
+ * GroupNorm statistics epilogue (Block3D conv -> GroupNorm, :107-109): when
+ * gn_sums != NULL the stored y's per-(clip, channel) sum and sum of squares
+ * are added into gn_sums[replica][nf*h*w / gn_P][cout][2] (zero on entry;
+ * gn_R replicas, clip = pixel / gn_P; nf*h*w % gn_P == 0), the `sums` a
+ * following dv_gn_fwd(..., sums_replicas = gn_R) consumes without its
+ * reduce pass.  NULL: no statistics (gn_P / gn_R ignored).                */
 int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
                 const void* wpack, const float* bias, const void* res, int ldres,
                 void* y, int ldy, int nf, int h, int w, int cin, int cout, int ksize,
-                int act, void* stream);
+                int act, float* gn_sums, long long gn_P, int gn_R, void* stream);
 
 /* Weight (and fused bias) gradient of dv_conv_fwd, written in torch layout:
  * dw (cout_real, cin_real, 1, k, k) (+)= sum_p dY[p][co] X[p + tap][ci]
@@ -75,10 +81,12 @@ int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0, 
  * needs (h, w) = (8, 8) with nf even, or w in {16, 32, 64} with
  * h * w % 128 == 0; cin % 16 == 0, c0 % 16 == 0 (split), cout % 64 == 0,
  * ld0 / ld1 % 8 == 0, ldy / ldres % 4 == 0, 16-B aligned x0 / x1 / wpack,
- * nf * h * w * ld * 2 < 2^31; returns DV_ERR_INVALID otherwise.          */
+ * nf * h * w * ld * 2 < 2^31; returns DV_ERR_INVALID otherwise.
+ * gn_sums / gn_P / gn_R as dv_conv_fwd, with gn_P % 128 == 0.             */
 int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
                  const void* wpack, const float* bias, const void* res, int ldres, void* y,
-                 int ldy, int nf, int h, int w, int cin, int cout, int act, void* stream);
+                 int ldy, int nf, int h, int w, int cin, int cout, int act, float* gn_sums,
+                 long long gn_P, int gn_R, void* stream);
 
 /* db[c] += sum_p dy[p][c]  (f32 atomics) */
 int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix, int c,
@@ -150,11 +158,14 @@ int dv_gemm_tn_batched(int dtype, const void* a, int lda, const void* b, int ldb
  * no zeroing): the buffer the caller's NEXT GroupNorm call (forward or
  * backward) will pass as `sums`.  Alternating two buffers keeps both zero on
  * entry without any memset launch.
- * C % (16 B) == 0, C <= 256 vectors, G <= 64.  act: DV_ACT_*.               */
+ * C % (16 B) == 0, C <= 256 vectors, G <= 64.  act: DV_ACT_*.
+ * sums_replicas > 0: `sums` already holds z's statistics in that many
+ * replicas, <= 64 (the producing dv_conv_fwd / dv_conv_fwd8 epilogue): the reduce
+ * launch is skipped and the call is one apply launch.                      */
 int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* res, int ldres,
               int nb, long long P, int C, int G, float eps, const float* gamma,
               const float* beta, const float* ss, int act, float* mean, float* rstd, float* sums,
-              float* next, long long next_n, void* stream);
+              float* next, long long next_n, int sums_replicas, void* stream);
 /* dz from dy (z is the pre-norm input); dgamma/dbeta [C] and dss [nb][2C]
  * (+)= their gradients (accumulate != 0 adds).  sums/next as dv_gn_fwd.      */
 int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void* dz, int lddz,

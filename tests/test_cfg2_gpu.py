@@ -157,3 +157,42 @@ def test_group_norm_act_full_size(parity_log, nb, T_, H, C, with_ss, with_res, d
     assert fwd < tol, fwd
     for k, e in errs.items():
         assert e < 2 * tol, (k, e)
+
+
+@pytest.mark.parametrize("nb,T_,H,cin,x1c,cout,dtype", [
+    (4, 16, 64, 64, 0, 64, torch.bfloat16),      # stripe kernel (stage 0)
+    (4, 16, 64, 128, 64, 64, torch.bfloat16),    # glds 256x64, dual source (up3)
+    (4, 16, 32, 192, 64, 128, torch.bfloat16),   # glds 128x128 (up2)
+    (4, 16, 16, 384, 128, 256, torch.bfloat16),  # window 16 (up1)
+    (4, 16, 8, 512, 0, 512, torch.bfloat16),     # window 8 (mid)
+    (2, 3, 6, 16, 0, 64, torch.bfloat16),        # generic kernel, clips straddle tiles (P = 108)
+    (2, 4, 8, 64, 0, 64, torch.float32),         # f32 parity kernel
+])
+def test_conv_groupnorm_statistics_epilogue(nb, T_, H, cin, x1c, cout, dtype):
+    """The conv epilogue's GroupNorm statistics (every forward kernel's STATS
+    variant, forced with GnStats.ALL) equal the per-(clip, channel) sum and
+    sum of squares of the stored output."""
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(61)
+    nf, W = nb * T_, H
+    x0 = (torch.randn(nf, H, W, cin - x1c, generator=g)).to("cuda", dtype)
+    x1 = (torch.randn(nf, H, W, x1c, generator=g)).to("cuda", dtype) if x1c else None
+    w = (torch.randn(cout, cin, 1, 3, 3, generator=g) / (9 * cin) ** 0.5).cuda()
+    b = (0.1 * torch.randn(cout, generator=g)).cuda()
+    saved = ops.GnStats.ALL
+    ops.GnStats.ALL = True
+    try:
+        st = ops.gn_stats(nb, cout, T_ * H * W, x0.device)
+        st.cur.zero_()
+        with torch.no_grad():
+            z = ops.conv(x0, w, b, x1=x1, gn=st)
+        torch.cuda.synchronize()
+    finally:
+        ops.GnStats.ALL = saved
+    assert st.used
+    got = st.cur[:st.R * nb * cout * 2].reshape(st.R, nb, cout, 2).sum(0).double().cpu()
+    zz = z.double().cpu().reshape(nb, T_ * H * W, cout)
+    want = torch.stack((zz.sum(1), (zz * zz).sum(1)), dim=-1)
+    assert ((got - want).norm() / want.norm()).item() < 1e-5
+    st.cur.zero_()  # hand the buffer back zeroed (the _GnSums contract)

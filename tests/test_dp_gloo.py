@@ -91,7 +91,12 @@ def _worker(rank, world, port, q):
         full = _grads(ou, x, times, noise)
         sl = slice(2 * rank, 2 * rank + 2)
         mine = _grads(ou, x[sl], times[sl], noise[sl])
-        allreduce_flat_grad(mine, world)
+        ref_sum = mine.clone()
+        dist.all_reduce(ref_sum)
+        # bucketed (4 MB buckets, back to front, async) == one all-reduce
+        allreduce_flat_grad(mine, world, bucket_bytes=4 << 20)
+        if not torch.equal(mine, ref_sum):
+            raise AssertionError("bucketed all-reduce differs from the single all-reduce")
         avg = mine / world
         err = ((avg - full).norm() / full.norm()).item()
         q.put((rank, ok_bcast, err))

@@ -34,12 +34,12 @@ def conv_case(nf, h, w, cin, cout, k, dtype=torch.bfloat16):
         wp = ops.pack_conv_weight(wt, dtype, cin, 2)
         def fwd():
             call("dv_conv_fwd8", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
-                 cout, nf, h, w, cin, cout, 0, stream())
+                 cout, nf, h, w, cin, cout, 0, None, 0, 0, stream())
     else:
         wp = ops.pack_conv_weight(wt, dtype, cin, 0)
         def fwd():
             call("dv_conv_fwd", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
-                 cout, nf, h, w, cin, cout, k, 0, stream())
+                 cout, nf, h, w, cin, cout, k, 0, None, 0, 0, stream())
     ms = timeit(fwd)
     dy = torch.randn_like(y)
     ws = ops._wgrad_workspace(ops._lib.dtype_name(x), nf, h, w, cin, cin, False, cout, k, x.device)
@@ -75,7 +75,7 @@ if __name__ == "__main__":
         from dalle2_video._lib import call, ptr, stream, dt
         for _ in range(20):
             call("dv_conv_fwd", dt(x), ptr(x), 64, 64, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
-                 64, 64, 64, 64, 64, 64, 3, 0, stream())
+                 64, 64, 64, 64, 64, 64, 3, 0, None, 0, 0, stream())
         torch.cuda.synchronize()
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "fwd8":  # the 8x8-stage 512->512 forward, for counter passes
@@ -87,7 +87,7 @@ if __name__ == "__main__":
         from dalle2_video._lib import call, ptr, stream, dt
         for _ in range(20):
             call("dv_conv_fwd8", dt(x), ptr(x), 512, 512, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
-                 512, 64, 8, 8, 512, 512, 0, stream())
+                 512, 64, 8, 8, 512, 512, 0, None, 0, 0, stream())
         torch.cuda.synchronize()
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "fwd":
