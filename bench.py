@@ -235,6 +235,48 @@ def sampling_leg(args, device):
                                        "frac": round(fl * sps / PEAK_BF16_TFLOPS, 4),
                                        "flop_per_step": f"{fl:.4f}e12 (Cfg2 forward x bs/4)"}}
     del dec, u
+    # config 5 shape (bf16): unet1 on a 32-frame 128x128 clip, bs=2 — the mid
+    # attention runs over 32 x 16 x 16 = 8,192 tokens (K/V-streamed flash kernel)
+    T5 = 12
+    u = Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    dec = VideoDecoder(unet=(u,), frame_sizes=(128,), frame_numbers=(32,), timesteps=T5,
+                       learned_variance=False)
+    deterministic_fill_(dec.unets[0])
+    dec = dec.to(device)
+    emb = torch.randn(2, 512, device=device)
+    from dalle2_video import ops
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        dec.sample(video_embed=emb, one_unet_in_gpu_at_time=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vid = dec.sample(video_embed=emb, one_unet_in_gpu_at_time=False)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        # one eager forward with per-launch timing: the 8,192-token attention
+        ops.TIMER = ops.KernelTimer()
+        with torch.no_grad():
+            dec.unets[0](torch.randn(2, 3, 32, 128, 128, device=device),
+                         torch.full((2,), 500, device=device, dtype=torch.long))
+        summ = ops.TIMER.summary()
+        ops.TIMER = None
+    assert torch.isfinite(vid).all()
+    att = summ.get("attn:mqa_fwd")
+    fl5 = FWD_TFLOP * (2 * 32 * 128 * 128) / (4 * 16 * 64 * 64)
+    out["config5_bf16"] = {
+        "config": "BASELINE config 5 shape, bf16 (not fp8): unet1 sampling, 32x128x128 clip, bs=2; "
+                  f"{T5}-step DDPM loop timed (per-step cost is schedule-independent)",
+        "value": round(T5 / dt, 2), "unit": "denoise-steps/s",
+        "est_1000_step_s": round(1000 * dt / T5, 1),
+        "roofline": {"bound": "mfma", "achieved": round(fl5 * T5 / dt, 1), "peak": PEAK_BF16_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(fl5 * T5 / dt / PEAK_BF16_TFLOPS, 4),
+                     "flop_per_step": f"{fl5:.3f}e12 (Cfg2 forward x 4 pixels ratio)"},
+        "mid_attention": None if att is None else {
+            "tokens": 8192, "us": round(att["ms"] / att["count"] * 1e3, 1),
+            "tflops": round(att["flops"] / (att["ms"] * 1e-3) / 1e12, 1),
+            "frac": round(att["flops"] / (att["ms"] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)},
+    }
+    log(f"config5 bf16: {T5 / dt:.2f} steps/s")
+    del dec, u
     # config 4: two-stage cascade, base 16x64x64 + spatial-SR unet2 (dim 8, mults 1..16) to 256x256
     u1 = Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
     u2 = Unet3D(8, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8, 16))

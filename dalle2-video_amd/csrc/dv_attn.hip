@@ -575,6 +575,130 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   }
 }
 
+// Long sequences (config 5: 32 x 16 x 16 = 8,192 tokens, K / V = 1 MiB per
+// clip): the same forward with K / V streamed through LDS in chunks of SCK
+// keys, double-buffered by LDS-DMA (chunk c + 1 lands while chunk c is
+// multiplied); the two key halves of the workgroup take the two halves of
+// every chunk.  LDS: 2 buffers x (K + V) x SCK x 64 B = 128 KiB.
+constexpr int SCK = 512;
+__device__ __forceinline__ void dma_kv_chunk(const __amdgpu_buffer_rsrc_t& rk,
+                                             const __amdgpu_buffer_rsrc_t& rv, char* sK, char* sV,
+                                             int row0, int nrows, int wave, int lane) {
+  const int np = nrows / 16;
+  const int rr = lane >> 2, slot = lane & 3;
+  for (int i = wave; i < 2 * np; i += NW) {
+    const bool isv = i >= np;
+    const int pc = isv ? i - np : i;
+    const int row = row0 + pc * 16 + rr;
+    const unsigned voff = row * ROW + 16 * (slot ^ ((row >> 2) & 3));
+    if (isv)
+      dma16(rv, sV + pc * 1024, voff);
+    else
+      dma16(rk, sK + pc * 1024, voff);
+  }
+}
+
+__global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* __restrict__ q,
+                                                                    const bf16* __restrict__ kp,
+                                                                    const bf16* __restrict__ vp,
+                                                                    bf16* __restrict__ o, float* lse,
+                                                                    int R, int NKP, int nkeys, float c) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int rg = wave & (RG - 1), kh = wave / RG;
+  const int b = blockIdx.y;
+  const __amdgpu_buffer_rsrc_t rk = dma_rsrc(kp + (long long)b * NKP * 32, (unsigned)NKP * ROW);
+  const __amdgpu_buffer_rsrc_t rv = dma_rsrc(vp + (long long)b * NKP * 32, (unsigned)NKP * ROW);
+  auto buf_k = [&](int i) { return smem + i * 2 * SCK * ROW; };
+  auto buf_v = [&](int i) { return smem + i * 2 * SCK * ROW + SCK * ROW; };
+  const int nch = (NKP + SCK - 1) / SCK;
+  dma_kv_chunk(rk, rv, buf_k(0), buf_v(0), 0, min(SCK, NKP), wave, lane);
+  const int row = blockIdx.x * RG * 32 + rg * 32 + r;
+  const bool rok = row < R;
+  const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
+  const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
+  const FragOff fo = frag_off(lane);
+  f32x16 acc = zero16();
+  float m = -INFINITY, l = 0.f;  // m: running max of c * s (log2 units)
+  for (int ch = 0; ch < nch; ++ch) {
+    // chunk ch landed (the only DMA in flight); every wave is done with the
+    // buffer chunk ch + 1 goes to (it held chunk ch - 1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int row0 = ch * SCK, nrows = min(SCK, NKP - row0);
+    if (ch + 1 < nch)
+      dma_kv_chunk(rk, rv, buf_k((ch + 1) & 1), buf_v((ch + 1) & 1), row0 + SCK,
+                   min(SCK, NKP - row0 - SCK), wave, lane);
+    const char* sK = buf_k(ch & 1);
+    const char* sV = buf_v(ch & 1);
+    const int nkt = nrows / 32, kmid = (nkt + 1) / 2;
+    const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid;
+    for (int kt = kbeg; kt < kend; ++kt) {
+      const int k0 = kt * 32, kg = row0 + k0;
+      f32x16 s = zero16();
+      const char* tK = sK + k0 * ROW;
+      s = mma(row_at(tK, fo, 0), qf0, s);
+      s = mma(row_at(tK, fo, 1), qf1, s);
+      if (kg + 32 > nkeys) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          if (kg + acc_row(e, h) >= nkeys) s[e] = -INFINITY;
+      }
+      float mx = max3(s[0], s[1], s[2]);
+#pragma unroll
+      for (int e = 3; e < 15; e += 2) mx = max3(mx, s[e], s[e + 1]);
+      mx = max3(mx, s[15], __shfl_xor(max3(mx, s[15], s[15]), 32, 64)) * c;
+      const bool upd = mx > m + 8.f;
+      if (__ballot(upd)) {
+        const float mn = upd ? mx : m;
+        const float alpha = ex2(m - mn);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] *= alpha;
+        l *= alpha;
+        m = mn;
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        s[e] = ex2(fmaf(s[e], c, -m));
+        l += s[e];
+      }
+      acc = mma(tr_at(sV + k0 * ROW, fo, 0), pack8(s, 0), acc);
+      acc = mma(tr_at(sV + k0 * ROW, fo, 1), pack8(s, 1), acc);
+    }
+  }
+  // merge the key halves through LDS (no chunk is read any more)
+  __syncthreads();
+  float* red = (float*)smem + rg * 18 * 64;
+  if (kh) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[e * 64 + lane] = acc[e];
+    red[16 * 64 + lane] = l;
+    red[17 * 64 + lane] = m;
+  }
+  __syncthreads();
+  if (kh) return;
+  {
+    const float m1 = red[17 * 64 + lane], mn = fmaxf(m, m1);
+    const float a0 = ex2(m - mn), a1 = ex2(m1 - mn);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = acc[e] * a0 + red[e * 64 + lane] * a1;
+    l = l * a0 + red[16 * 64 + lane] * a1;
+    m = mn;
+  }
+  l += __shfl_xor(l, 32, 64);
+  if (rok) {
+    const float inv = 1.f / l;
+    bf16* orow = o + ((long long)b * R + row) * 32;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const u32x2 v = {cvt_pk(acc[4 * g] * inv, acc[4 * g + 1] * inv),
+                       cvt_pk(acc[4 * g + 2] * inv, acc[4 * g + 3] * inv)};
+      *(u32x2*)(orow + 8 * g + 4 * h) = v;
+    }
+    if (h == 0) lse[(long long)b * R + row] = m + __log2f(l);
+  }
+}
+
 // dq (query-major, as the forward: key halves summed through LDS) and
 // D = rowsum(dO * O) for the dk/dv pass
 __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
@@ -813,6 +937,11 @@ bool eligible(int dtype, int ldq, int ldo, int H, int NKP) {
   return dtype == DV_BF16 && ldq == H * DH && ldo == H * DH &&
          (long long)NKP * 2 * ROW <= 160 * 1024;
 }
+// the streamed forward: bf16, packed rows, K / V larger than one LDS image
+bool eligible_stream(int dtype, int ldq, int ldo, int H, int NKP) {
+  return dtype == DV_BF16 && ldq == H * DH && ldo == H * DH && !eligible(dtype, ldq, ldo, H, NKP) &&
+         (long long)NKP * ROW < (1ll << 31);
+}
 
 int splits(int NKP, int B) {
   const int nkg = (NKP / 32 + 3) / 4;
@@ -867,6 +996,11 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
     const int R = N * H, lds = max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4);
     fa::set_lds((const void*)fa::mqa_fwd_fa_kernel, lds);
     fa::mqa_fwd_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
+        (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, scale * fa::LOG2E);
+  } else if (fa::eligible_stream(dtype, ldq, ldo, H, NKP)) {
+    const int R = N * H, lds = 4 * fa::SCK * fa::ROW;
+    fa::set_lds((const void*)fa::mqa_fwd_fa_stream_kernel, lds);
+    fa::mqa_fwd_fa_stream_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
         (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, scale * fa::LOG2E);
   } else if (dtype == DV_BF16)
     mqa_fwd_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)q, ldq, (const bf16*)kp, (const bf16*)vp, (bf16*)o, ldo, lse, N, NKP, N + 1, H, scale);

@@ -444,9 +444,17 @@ int grid_for(long long work, int per_block = 256) {
 
 // rows per workgroup: a multiple of one unrolled pass (rpp * U), sized for
 // about `target` workgroups over the whole call
+// DV_GN_MINB (A/B knob, default off): a floor on the bytes of z each
+// workgroup streams.  Measured on the whole step (tools/gn_ab.sh): 32 KiB
+// 78.9, 64 KiB 76.7-78.2, 128 KiB 74.3 vs 79.2 steps/s without — the small
+// 8x8 / 16x16 calls want the parallelism more than fewer prologues.
 long long gn_rows(const GnArgs& a, int vec, int u, long long target) {
+  static const long long min_bytes = getenv("DV_GN_MINB") ? atoll(getenv("DV_GN_MINB")) : 0;
   const long long pass = (long long)(256 / (a.C / vec)) * u;
   long long r = (a.P * a.nb + target - 1) / target;
+  const long long row_bytes = (long long)a.C * (16 / vec);
+  const long long rmin = min_bytes > 0 ? (min_bytes + row_bytes - 1) / row_bytes : 0;
+  if (r < rmin) r = rmin;
   r = (r + pass - 1) / pass * pass;
   return r < pass ? pass : r;
 }

@@ -297,3 +297,30 @@ def test_linear_group(act_in, ns, K):
     sum((y * gy.cuda()).sum() for y, gy in zip(yd, gys)).backward()
     grads_match([xd.grad] + [w.grad for w in wd] + [b.grad for b in bd if b is not None],
                 [xr.grad] + [w.grad for w in wr] + [b.grad for b in br if b is not None], 2e-6)
+
+
+@pytest.mark.parametrize("N,B", [(2048, 2), (4100, 1), (8192, 2)])
+def test_mqa_forward_streamed_long_sequence(parity_log, N, B):
+    """K/V-chunked flash forward (config 5: 32 x 16 x 16 = 8,192 mid tokens)
+    vs a plain f32 softmax attention computed on the GPU head by head (the
+    CPU reference would need the full (B, 16, N, N) scores)."""
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(13)
+    H, D = 16, 32
+    q = (torch.randn(B * N, H * D, generator=g) * 2).cuda().to(torch.bfloat16)
+    kv = (torch.randn(B * N, 2 * D, generator=g) * 2).cuda().to(torch.bfloat16)
+    null_kv = torch.randn(2, D, generator=g).cuda()
+    with torch.no_grad():
+        y = ops.mqa(q, kv, null_kv, B, N, H, 1.0 / D).float()
+        qf, kvf = q.float(), kv.float()
+        ref = torch.empty_like(y)
+        for b in range(B):
+            k = torch.cat((null_kv[0][None], kvf[b * N:(b + 1) * N, :D]), 0)
+            v = torch.cat((null_kv[1][None], kvf[b * N:(b + 1) * N, D:]), 0)
+            for hh in range(H):
+                qh = qf[b * N:(b + 1) * N, hh * D:(hh + 1) * D]
+                ref[b * N:(b + 1) * N, hh * D:(hh + 1) * D] = ((qh @ k.t()) / D).softmax(-1) @ v
+    e = rel(y, ref)
+    parity_log(N=N, B=B, fwd_rel=e)
+    assert e < 2.5e-2
