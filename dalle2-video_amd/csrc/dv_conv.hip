@@ -2201,20 +2201,18 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
 // LDS, so even a 256-split sum of a small gradient spreads over hundreds of
 // workgroups.  The bias partials ([S][cout], cout % 4 == 0) are reduced the
 // same way by the workgroups after the weight ones.
-__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* part, int S, int G,
-                                                            long long n4, float* dw, int acc_w,
-                                                            const float* dbpart, float* db,
-                                                            int cout, int acc_b) {
-  __shared__ f32x4 sh[256];
+__device__ __forceinline__ void reduce4_block(f32x4* sh, long long blk, const float* part, int S,
+                                              int G, long long n4, float* dw, int acc_w,
+                                              const float* dbpart, float* db, int cout, int acc_b) {
   const int cols = 256 / G;
   const long long wblocks = (n4 + cols - 1) / cols;
-  const bool bias = blockIdx.x >= wblocks;
+  const bool bias = blk >= wblocks;
   const long long n = bias ? cout / 4 : n4;
   const f32x4* src = (const f32x4*)(bias ? dbpart : part);
   float* dst = bias ? db : dw;
   const int acc = bias ? acc_b : acc_w;
   const int c = threadIdx.x % cols, grp = threadIdx.x / cols;
-  const long long i = (bias ? blockIdx.x - wblocks : blockIdx.x) * (long long)cols + c;
+  const long long i = (bias ? blk - wblocks : blk) * (long long)cols + c;
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (i < n) {
     const f32x4* p = src + i;
@@ -2234,6 +2232,43 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* part, i
   f32x4* o = (f32x4*)dst + i;
   if (acc) v += *o;
   *o = v;
+}
+
+inline long long reduce4_blocks(long long n4, int G, int cout, bool bias) {
+  const int cols = 256 / G;
+  return (n4 + cols - 1) / cols + (bias ? (cout / 4 + cols - 1) / cols : 0);
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* part, int S, int G,
+                                                            long long n4, float* dw, int acc_w,
+                                                            const float* dbpart, float* db,
+                                                            int cout, int acc_b) {
+  __shared__ f32x4 sh[256];
+  reduce4_block(sh, blockIdx.x, part, S, G, n4, dw, acc_w, dbpart, db, cout, acc_b);
+}
+
+// every pending split-K sum of a backward pass in one launch: block b belongs
+// to the last entry whose blk0 <= b (binary search over the small table)
+__global__ __launch_bounds__(256) void wgrad_reduce_batched_kernel(const DvWgradReduceEntry* table,
+                                                                   int n) {
+  __shared__ f32x4 sh[256];
+  const long long b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (table[mid].blk0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const DvWgradReduceEntry e = table[lo];
+  reduce4_block(sh, b - e.blk0, e.part, e.S, e.G, e.n4, e.dw, e.acc_w, e.dbpart, e.db, e.cout,
+                e.acc_b);
+}
+
+inline int reduce4_groups(int S) {
+  static const int gmax = getenv("DV_RED_G") ? atoi(getenv("DV_RED_G")) : 8;
+  int G = 1;
+  while (G * 2 <= gmax && G * 2 <= S) G *= 2;
+  return G;
 }
 
 // dw[co][ci][tap] (torch layout, real sizes) (+)= sum_s part[s][co][tap][ci]
@@ -2334,7 +2369,8 @@ long long wgrad_stripe_ws(int nf, int h, int w, int cin, int cout, int ks) {
 
 int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
                       int ld1, float* ws, float* dw, int acc_w, float* db, int acc_b, int nf, int h,
-                      int w, int cin, int cout, int ks, hipStream_t st) {
+                      int w, int cin, int cout, int ks, hipStream_t st,
+                      DvWgradReduceEntry* defer = nullptr) {
   WgradSArgs a;
   a.dy = (const bf16*)dy; a.lddy = lddy; a.x0 = (const bf16*)x0;
   a.x1 = (const bf16*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0; a.c0 = x1 ? c0 : cin;
@@ -2360,12 +2396,13 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   }
   if (S > 1) {
     const long long n4 = (long long)cout * a.K / 4;
-    static const int gmax = getenv("DV_RED_G") ? atoi(getenv("DV_RED_G")) : 8;
-    int G = 1;
-    while (G * 2 <= gmax && G * 2 <= S) G *= 2;
-    const long long blocks = (n4 + 256 / G - 1) / (256 / G) + (db ? (cout / 4 + 256 / G - 1) / (256 / G) : 0);
-    wgrad_reduce4_kernel<<<(unsigned)blocks, 256, 0, st>>>(ws, S, G, n4, dw, acc_w, a.dbpart, db,
-                                                            cout, acc_b);
+    const int G = reduce4_groups(S);
+    if (defer) {  // the caller sums the partials later (dv_wgrad_reduce_batched)
+      *defer = DvWgradReduceEntry{ws, a.dbpart, dw, db, n4, 0, S, G, cout, acc_w, acc_b, 0};
+    } else {
+      wgrad_reduce4_kernel<<<(unsigned)reduce4_blocks(n4, G, cout, db != nullptr), 256, 0, st>>>(
+          ws, S, G, n4, dw, acc_w, a.dbpart, db, cout, acc_b);
+    }
   }
   return check_launch("conv_wgrad_stripe");
 }
@@ -2428,11 +2465,12 @@ extern "C" int dv_conv_wgrad_ws(int dtype, int nf, int h, int w, int cin, int c0
   return DV_OK;
 }
 
-extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0,
-                             int c0, const void* x1, int ld1, float* dw, int accumulate_w,
-                             float* db, int accumulate_b, float* ws, long long ws_floats, int nf,
-                             int h, int w, int cin, int cout, int cout_real, int cin_real,
-                             int ksize, void* stream) {
+static int conv_wgrad_impl(int dtype, const void* dy, int lddy, const void* x0, int ld0, int c0,
+                           const void* x1, int ld1, float* dw, int accumulate_w, float* db,
+                           int accumulate_b, float* ws, long long ws_floats, int nf, int h, int w,
+                           int cin, int cout, int cout_real, int cin_real, int ksize,
+                           DvWgradReduceEntry* defer, void* stream) {
+  if (defer) defer->S = 0;
   DV_REQUIRE(dy && x0 && dw && ws, "null pointer");
   DV_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "cin/cout must be multiples of 8");
   DV_REQUIRE(cout_real <= cout && cin_real <= cin && cout_real > 0 && cin_real > 0,
@@ -2448,7 +2486,7 @@ extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0
   if (dtype == DV_BF16 && cout_real == cout && cin_real == cin &&
       wgrad_stripe_ok(nf, h, w, cin, c0, x1 != nullptr, cout, ksize))
     return conv_wgrad_stripe(dy, lddy, x0, ld0, c0, x1, ld1, ws, dw, accumulate_w, db, accumulate_b,
-                             nf, h, w, cin, cout, ksize, st);
+                             nf, h, w, cin, cout, ksize, st, defer);
   // general path: f32 atomics into the zeroed packed workspace, then one reduce
   const long long K = (long long)ksize * ksize * cin;
   float* dbp = db ? ws + cout * K : nullptr;
@@ -2460,6 +2498,52 @@ extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0
   launch_wgrad_reduce(ws, 1, cout, cin, ksize * ksize, dw, cout_real, cin_real, accumulate_w, dbp,
                       db, accumulate_b, st);
   return check_launch("conv_wgrad");
+}
+
+extern "C" int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0,
+                             int c0, const void* x1, int ld1, float* dw, int accumulate_w,
+                             float* db, int accumulate_b, float* ws, long long ws_floats, int nf,
+                             int h, int w, int cin, int cout, int cout_real, int cin_real,
+                             int ksize, void* stream) {
+  DV_REQUIRE(dy && x0 && dw && ws, "null pointer");
+  return conv_wgrad_impl(dtype, dy, lddy, x0, ld0, c0, x1, ld1, dw, accumulate_w, db, accumulate_b,
+                         ws, ws_floats, nf, h, w, cin, cout, cout_real, cin_real, ksize, nullptr,
+                         stream);
+}
+
+extern "C" int dv_conv_wgrad_deferred(int dtype, const void* dy, int lddy, const void* x0,
+                                      int ld0, int c0, const void* x1, int ld1, float* dw,
+                                      int accumulate_w, float* db, int accumulate_b, float* ws,
+                                      long long ws_floats, int nf, int h, int w, int cin, int cout,
+                                      int cout_real, int cin_real, int ksize,
+                                      DvWgradReduceEntry* entry, void* stream) {
+  DV_REQUIRE(entry && dy && x0 && dw && ws, "null pointer");
+  return conv_wgrad_impl(dtype, dy, lddy, x0, ld0, c0, x1, ld1, dw, accumulate_w, db, accumulate_b,
+                         ws, ws_floats, nf, h, w, cin, cout, cout_real, cin_real, ksize, entry,
+                         stream);
+}
+
+extern "C" int dv_wgrad_reduce_plan(DvWgradReduceEntry* t, int n, long long* blocks) {
+  DV_REQUIRE(t && blocks && n > 0, "bad table");
+  long long blk = 0;
+  for (int i = 0; i < n; ++i) {
+    DV_REQUIRE(t[i].S >= 1 && t[i].n4 > 0 && t[i].cout % 4 == 0 && t[i].part && t[i].dw &&
+                   (!t[i].db || t[i].dbpart),
+               "bad entry");
+    t[i].G = reduce4_groups(t[i].S);
+    t[i].blk0 = blk;
+    blk += reduce4_blocks(t[i].n4, t[i].G, t[i].cout, t[i].db != nullptr);
+  }
+  *blocks = blk;
+  return DV_OK;
+}
+
+extern "C" int dv_wgrad_reduce_batched(const DvWgradReduceEntry* table, int n, long long blocks,
+                                       void* stream) {
+  DV_REQUIRE(table && n >= 0 && blocks >= 0 && blocks < (1ll << 31), "bad table");
+  if (n == 0 || blocks == 0) return DV_OK;
+  wgrad_reduce_batched_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(table, n);
+  return check_launch("wgrad_reduce_batched");
 }
 
 extern "C" int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, long long max_elems,

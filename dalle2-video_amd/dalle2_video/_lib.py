@@ -34,6 +34,10 @@ _SIGS = {
     "dv_xattn_fold_bwd_batched": [_P, _I, _F, _P],
     "dv_conv_wgrad_ws": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_conv_wgrad": [_I, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dv_conv_wgrad_deferred": [_I, _P, _I, _P, _I, _I, _P, _I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _I, _I, _I,
+                               _I, _I, _P, _P],
+    "dv_wgrad_reduce_plan": [_P, _I, _P],
+    "dv_wgrad_reduce_batched": [_P, _I, _L, _P],
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
     "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "dv_pack_conv_weights_batched": [_P, _I, _L, _P],
@@ -68,6 +72,12 @@ _SIGS = {
     "dv_mqa_bwd_ws": [_I, _I, _I, _I, _I, _I, _I, _P],
     "dv_mqa_bwd": [_I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _L, _P, _I, _P, _I, _I, _I, _I, _F, _I, _P],
 }
+
+
+class DvWgradReduceEntry(ctypes.Structure):
+    """Mirror of DvWgradReduceEntry (include/dv_hip.h)."""
+    _fields_ = [("part", _P), ("dbpart", _P), ("dw", _P), ("db", _P), ("n4", _L), ("blk0", _L),
+                ("S", _I), ("G", _I), ("cout", _I), ("acc_w", _I), ("acc_b", _I), ("pad_", _I)]
 
 
 class DVError(RuntimeError):

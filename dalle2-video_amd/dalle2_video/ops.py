@@ -218,6 +218,102 @@ def _wgrad_workspace(dname, nf, h, w, cin, c0, split, cout, ks, device):
     return buf
 
 
+class _WgradDefer:
+    """Deferred split-K sums of the row-window wgrad (dv_conv_wgrad_deferred).
+
+    Inside `defer_wgrad()` (the trainer's forward + backward, captured or
+    eager) every conv whose weight gradient goes straight into a leaf's .grad
+    leaves its per-split partials in an arena slot instead of launching its
+    own reduce; leaving the context sums them all in ONE launch
+    (dv_wgrad_reduce_batched).  Slots are handed out in call order from the
+    start of the arena each pass, so a replayed pass sees the same addresses;
+    the device table is cached by content (built by the eager warm-up calls,
+    reused by the captured one)."""
+
+    CHUNK_FLOATS = 1 << 27  # 512 MB arena chunks (kept for the process: graphs hold their addresses)
+
+    def __init__(self):
+        self.active = 0
+        self.pending = []  # DvWgradReduceEntry
+        self.targets = set()
+        self.chunks = {}  # device -> [tensor]
+        self.cursor = (0, 0)
+        self.tables = {}  # (device, bytes) -> (device table, blocks)
+
+    def slot(self, device, floats):
+        floats = (floats + 63) // 64 * 64
+        chunks = self.chunks.setdefault(str(device), [])
+        ci, off = self.cursor
+        while True:
+            if ci == len(chunks):
+                chunks.append(torch.empty(max(self.CHUNK_FLOATS, floats), dtype=torch.float32, device=device))
+            if off + floats <= chunks[ci].numel():
+                self.cursor = (ci, off + floats)
+                return chunks[ci], off
+            ci, off = ci + 1, 0
+
+    def add(self, entry, device):
+        self.pending.append((entry, device))
+        self.targets.add(entry.dw)
+        if entry.db:
+            self.targets.add(entry.db)
+
+    def conflicts(self, *ptrs):
+        return any(p is not None and p in self.targets for p in ptrs)
+
+    def flush(self):
+        if not self.pending:
+            self.cursor = (0, 0)
+            return
+        dev = self.pending[0][1]
+        n = len(self.pending)
+        host = (_lib.DvWgradReduceEntry * n)(*[e for e, _ in self.pending])
+        nblk = ctypes.c_longlong(0)
+        call("dv_wgrad_reduce_plan", ctypes.byref(host), n, ctypes.byref(nblk))
+        blocks = nblk.value
+        key = (str(dev), bytes(host))
+        tab = self.tables.get(key)
+        if tab is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise _lib.DVError("deferred wgrad table changed inside a captured region "
+                                   "(run the same pass eagerly before capturing it)")
+            raw = torch.frombuffer(bytearray(bytes(host)), dtype=torch.uint8)
+            tab = self.tables[key] = raw.to(dev)
+        call("dv_wgrad_reduce_batched", ptr(tab), n, blocks, stream())
+        self.pending.clear()
+        self.targets.clear()
+        self.cursor = (0, 0)
+
+    def discard(self):
+        self.pending.clear()
+        self.targets.clear()
+        self.cursor = (0, 0)
+
+
+WGRAD_DEFER = _WgradDefer()
+
+
+class defer_wgrad:
+    """Context: defer the split-K sums of the convs whose backward runs inside
+    it and sum them all in one launch on exit (see _WgradDefer).  The
+    gradients are complete only after the context exits."""
+
+    def __enter__(self):
+        if WGRAD_DEFER.active == 0:
+            WGRAD_DEFER.discard()
+        WGRAD_DEFER.active += 1
+        return WGRAD_DEFER
+
+    def __exit__(self, et, ev, tb):
+        WGRAD_DEFER.active -= 1
+        if WGRAD_DEFER.active == 0:
+            if et is None:
+                WGRAD_DEFER.flush()
+            else:
+                WGRAD_DEFER.discard()
+        return False
+
+
 _XA_WS = {}
 
 
@@ -636,11 +732,32 @@ class ConvFn(torch.autograd.Function):
             ld1 = cl_ld(x1) if x1 is not None else 0
             m = nf * h * w
             dname = _lib.dtype_name(dy8)
-            ws = _wgrad_workspace(_lib.dtype_name(dy8), nf, h, w, cin, c0, x1 is not None, cout8,
-                                  ksize, dy.device)
             kname = (conv_wgrad_name(dname, m, cout8, cin, c0, x1 is not None, ksize, h, w,
                                      max(lddy, ld0, ld1)) if (cout8 == cout and cin_real == cin)
                      else gemm_wgrad_name(dname, m, cout8, cin * ksize * ksize, max(lddy, ld0, ld1)))
+            if (WGRAD_DEFER.active and dw is None and db is None and not _WgradStream.enabled
+                    and kname.startswith("conv_wgrad_stripe")):
+                # leaf .grad targets: leave the split partials for the pass-end sum
+                if WGRAD_DEFER.conflicts(dw_t.data_ptr(), db_t.data_ptr() if db_t is not None else None):
+                    WGRAD_DEFER.flush()  # a second gradient into the same target
+                need = ctypes.c_longlong(0)
+                call("dv_conv_wgrad_ws", dt(dy8), nf, h, w, cin, c0, int(x1 is not None), cout8, ksize,
+                     ctypes.byref(need))
+                arena, off = WGRAD_DEFER.slot(dy.device, need.value)
+                ent = _lib.DvWgradReduceEntry()
+                _launch(kname, 2.0 * m * cout8 * cin * ksize * ksize * ctx.algo_scale,
+                        dy8.element_size() * m * (cin + cout8),
+                        lambda: call("dv_conv_wgrad_deferred", dt(dy8), ptr(dy8), lddy, ptr(x0), ld0, c0,
+                                     ptr(x1), ld1, ptr(dw_t), int(acc_w), ptr(db_t), int(acc_b),
+                                     _lib.ctypes_vp(arena.data_ptr() + 4 * off), need.value, nf, h, w,
+                                     cin, cout8, cout, cin_real, ksize, ctypes.byref(ent), stream()),
+                        ("wgrad", cout8, cin * ksize * ksize, m))
+                if ent.S > 0:
+                    WGRAD_DEFER.add(ent, dy.device)
+                dres = dy if has_res else None
+                return dx0, dx1, dw, db, dres, None, None, None, None, None
+            ws = _wgrad_workspace(_lib.dtype_name(dy8), nf, h, w, cin, c0, x1 is not None, cout8,
+                                  ksize, dy.device)
             # on the side stream only when the results go straight into leaf
             # .grad buffers (a returned gradient is consumed by autograd on
             # this stream at once)

@@ -544,9 +544,10 @@ class VideoDecoderTrainer(nn.Module):
             with torch.cuda.graph(g):
                 ctx = (torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False)
                        if self.amp else nullcontext())
-                with ctx:
-                    loss = self.decoder(*sargs, unet_number=unet_number, **skw)
-                loss.backward()
+                with ops.defer_wgrad():  # one split-K sum launch for the whole backward
+                    with ctx:
+                        loss = self.decoder(*sargs, unet_number=unet_number, **skw)
+                    loss.backward()
                 # replays start from zeroed GroupNorm sums whatever the parity
                 # of the GroupNorm calls inside the graph (ops._GnSums)
                 ops.gn_graph_boundary(loss.device)
@@ -573,16 +574,17 @@ class VideoDecoderTrainer(nn.Module):
         cond_videos = []
         for frac, (cargs, ckw) in split_args_and_kwargs(*args, split_size=max_batch_size, **kwargs):
             ctx = torch.autocast("cuda", dtype=torch.bfloat16) if self.amp else nullcontext()
-            with ctx:
-                out = self.decoder(*cargs, unet_number=unet_number,
-                                   return_lowres_cond_video=return_lowres_cond_video, **ckw)
-            loss, cv = (out if return_lowres_cond_video else (out, None))
-            loss = loss * frac
-            if cv is not None:
-                cond_videos.append(cv)
-            total_loss += loss.item()
-            if self.training:
-                loss.backward()
+            with ops.defer_wgrad():  # the gradients are complete when it exits
+                with ctx:
+                    out = self.decoder(*cargs, unet_number=unet_number,
+                                       return_lowres_cond_video=return_lowres_cond_video, **ckw)
+                loss, cv = (out if return_lowres_cond_video else (out, None))
+                loss = loss * frac
+                if cv is not None:
+                    cond_videos.append(cv)
+                total_loss += loss.item()
+                if self.training:
+                    loss.backward()
         if return_lowres_cond_video:
             return total_loss, torch.stack(cond_videos)
         return total_loss

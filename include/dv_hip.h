@@ -74,6 +74,34 @@ int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0, 
                   int accumulate_b, float* ws, long long ws_floats, int nf, int h, int w,
                   int cin, int cout, int cout_real, int cin_real, int ksize, void* stream);
 
+/* Deferred split-K sum.  dv_conv_wgrad_deferred is dv_conv_wgrad, except that
+ * when the row-window kernel runs with several pixel splits it only writes
+ * the partials into `ws` (which must then stay untouched until the sum has
+ * run) and describes the pending sum in *entry (host memory; entry->S > 0).
+ * Otherwise the gradient is complete on return and entry->S = 0.
+ * dv_wgrad_reduce_plan fills blk0 / G of a host table of n pending sums and
+ * the launch's block count (*blocks); dv_wgrad_reduce_batched (table copied to
+ * the DEVICE) then performs all n sums in one launch.  Entries must not share
+ * a dw or db target.  The trainer defers every conv of one backward pass and
+ * sums them once at its end (replaces a reduce launch per conv).          */
+typedef struct {
+  const float* part;    /* [S][cout * K] partials                      */
+  const float* dbpart;  /* [S][cout] bias partials or NULL             */
+  float* dw;            /* (cout, cin, 1, k, k) target                 */
+  float* db;            /* [cout] target or NULL                       */
+  long long n4;         /* cout * K / 4                                */
+  long long blk0;       /* first block of this entry (plan)            */
+  int S, G, cout, acc_w, acc_b, pad_;
+} DvWgradReduceEntry;
+int dv_conv_wgrad_deferred(int dtype, const void* dy, int lddy, const void* x0, int ld0, int c0,
+                           const void* x1, int ld1, float* dw, int accumulate_w, float* db,
+                           int accumulate_b, float* ws, long long ws_floats, int nf, int h,
+                           int w, int cin, int cout, int cout_real, int cin_real, int ksize,
+                           DvWgradReduceEntry* entry, void* stream);
+int dv_wgrad_reduce_plan(DvWgradReduceEntry* host_table, int n, long long* blocks);
+int dv_wgrad_reduce_batched(const DvWgradReduceEntry* table, int n, long long blocks,
+                            void* stream);
+
 /* 3x3 forward / dgrad, window form (dalle2_video.py:107 Block3D.project at
  * the 8x8 .. 64x64 stages, and the dgrads of those convs): same contract as
  * dv_conv_fwd with ksize = 3, but `wpack` is the 16-channel-chunk-major

@@ -1,5 +1,6 @@
 """VideoDecoderTrainer (fused HIP AdamW + HIP grad-norm clip) vs the golden
 3-step training trace G4 (torch AdamW + clip_grad_norm_ on the CPU oracle)."""
+import contextlib
 import os
 
 import numpy as np
@@ -134,6 +135,47 @@ def test_train_sample_train_keeps_training(use_ema):
     assert not torch.equal(wB, w0), "the update after sampling did not change the weights"
     for (n, pa), pb in zip(decA.unets[0].named_parameters(), decB.unets[0].parameters()):
         assert ((pa - pb).norm() / pa.norm().clamp_min(1e-30)).item() < 1e-4, n
+
+
+def test_deferred_wgrad_sum_matches_per_conv_sum():
+    """ops.defer_wgrad (the trainer's forward+backward): the row-window wgrad
+    partials of every conv are summed in ONE dv_wgrad_reduce_batched launch at
+    the end of the pass instead of one reduce per conv.  Same split count and
+    summation order -> bit-identical weight and bias gradients, also when a
+    gradient accumulates (a second pass, or one weight read by two convs: the
+    pending sums are flushed before the second target write)."""
+    from dalle2_video import ops
+
+    g = torch.Generator(device="cuda").manual_seed(11)
+    shapes = [(16, 32, 32, 64, 64, 3), (64, 8, 8, 128, 256, 3), (8, 64, 64, 64, 128, 1)]
+    xs, ws, bs, dys = [], [], [], []
+    for nf, h, w, cin, cout, k in shapes:
+        xs.append(torch.randn(nf, h, w, cin, device="cuda", generator=g).bfloat16())
+        ws.append(torch.randn(cout, cin, 1, k, k, device="cuda", generator=g).div_((cin * k * k) ** 0.5)
+                  .requires_grad_())
+        bs.append(torch.randn(cout, device="cuda", generator=g).requires_grad_())
+        dys.append(torch.randn(nf, h, w, cout, device="cuda", generator=g).bfloat16())
+
+    def run(defer, passes):
+        for p in ws + bs:
+            p.grad = None
+        n_pending = []
+        for _ in range(passes):
+            with (ops.defer_wgrad() if defer else contextlib.nullcontext()):
+                outs = [ops.conv(x, w_, b_) for x, w_, b_ in zip(xs, ws, bs)]
+                outs.append(ops.conv(xs[0], ws[0], bs[0]))  # the same weight read twice
+                torch.autograd.backward(outs, dys + [dys[0]])
+                n_pending.append(len(ops.WGRAD_DEFER.pending))
+        torch.cuda.synchronize()
+        return [p.grad.clone() for p in ws + bs], n_pending
+
+    for passes in (1, 2):
+        ref, _ = run(False, passes)
+        got, n_pending = run(True, passes)
+        assert all(n >= 1 for n in n_pending), n_pending
+        assert not ops.WGRAD_DEFER.pending
+        for i, (a, b) in enumerate(zip(ref, got)):
+            assert torch.equal(a, b), (passes, i, ((a - b).norm() / a.norm()).item())
 
 
 def test_graph_replay_matches_eager():
