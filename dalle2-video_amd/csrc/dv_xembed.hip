@@ -1,0 +1,598 @@
+// CrossEmbedLayer3D (reference dalle2_video.py:208-244): the Unet3D input
+// layer, parallel (1,k,k) convolutions of the 3-channel (6 with the lowres
+// conditioning) input for k = 3, 7, 15 whose outputs are concatenated along
+// channels (dim/2, dim/4, rest).  Direct kernels on MFMA for that shape —
+// small cin, large windows — instead of one padded 15x15 implicit GEMM:
+//
+//  * K is ordered (dy, dx, c) with the pixel's channels padded to CP = 4 (or
+//    8) only, so one image row of the LDS input window, flattened as
+//    [column][CP], IS the im2col row of a pixel for one dy: operand reads are
+//    plain 8-element runs at (pixel + dx0) * CP + j.
+//  * Output channels go in tiles of 16 (v_mfma_f32_16x16x32_bf16); a tile
+//    runs only its own window (the largest kernel among its channels), so the
+//    3x3 channels do 3 dy rows of one 32-wide K step and the 15x15 ones 15
+//    rows of two.  Executed / algorithmic MACs: 1.46 (CP 4) for 3/7/15.
+//  * Weight gradient: M = 16 channels, N = 16 (dx, c) columns, K = 32 pixels
+//    of one image row; both operands come from LDS by transposed reads
+//    (ds_read_b64_tr_b16) — the im2col "rows" of consecutive pixels overlap
+//    in the window image.  Each workgroup sums a band of image rows into its
+//    own partial (plain stores); one finishing launch sums the bands and
+//    scatters them into the torch-layout gradients of every branch.
+#include "dv_common.h"
+
+#include <algorithm>
+
+using namespace dv;
+
+namespace {
+
+constexpr int XE_MAXT = 8;  // 16-channel tiles (total cout <= 128)
+
+struct XeGeom {
+  int ntiles, cout, cin, cp, kmax, nbranch;
+  int k[XE_MAXT];     // window of tile t (largest branch kernel among its channels)
+  int jw[XE_MAXT];    // forward K per dy: k*cp rounded up to 32
+  int jwp[XE_MAXT];   // LDS / image row pitch (elements) = jw + 8
+  int woff[XE_MAXT];  // element offset of tile t's [16][k][jwp] weight image
+  int boff;           // element offset of the f32 bias [cout] (16-B aligned)
+  int image_elems;    // bf16 elements incl. the bias (multiple of 8)
+  int nb16[XE_MAXT];  // wgrad 16-column blocks per dy: ceil(k*cp / 16)
+  int poff[XE_MAXT];  // float offset of tile t's partial [16][k][nb16*16]
+  int pfloats;        // floats per partial incl. the bias sums
+  int items;          // sum over tiles of k * nb16 (16x16 wgrad accumulators)
+  int bk[4], bco0[4], bcout[4];  // branches: kernel, first channel, channels
+};
+
+bool xe_geom(const DvCrossEmbed& ce, XeGeom& g) {
+  if (ce.nbranch < 1 || ce.nbranch > 4 || ce.cin < 1 || ce.cin > 8) return false;
+  g = XeGeom{};
+  g.nbranch = ce.nbranch;
+  g.cin = ce.cin;
+  g.cp = ce.cin <= 4 ? 4 : 8;
+  int co = 0, kmax = 0;
+  for (int b = 0; b < ce.nbranch; ++b) {
+    if (ce.k[b] < 1 || ce.k[b] % 2 == 0 || ce.k[b] > 15 || ce.cout[b] < 1) return false;
+    if (b && ce.k[b] < ce.k[b - 1]) return false;
+    g.bk[b] = ce.k[b];
+    g.bco0[b] = co;
+    g.bcout[b] = ce.cout[b];
+    co += ce.cout[b];
+    kmax = std::max(kmax, ce.k[b]);
+  }
+  if (co % 16 || co > 16 * XE_MAXT) return false;
+  g.cout = co;
+  g.kmax = kmax;
+  g.ntiles = co / 16;
+  int woff = 0, poff = 0;
+  for (int t = 0; t < g.ntiles; ++t) {
+    int k = 0;
+    for (int b = 0; b < ce.nbranch; ++b)
+      if (g.bco0[b] < 16 * t + 16 && g.bco0[b] + g.bcout[b] > 16 * t) k = std::max(k, g.bk[b]);
+    g.k[t] = k;
+    g.jw[t] = (k * g.cp + 31) / 32 * 32;
+    g.jwp[t] = g.jw[t] + 8;
+    g.woff[t] = woff;
+    woff += 16 * k * g.jwp[t];
+    g.nb16[t] = (k * g.cp + 15) / 16;
+    g.poff[t] = poff;
+    poff += 16 * k * g.nb16[t] * 16;
+    g.items += k * g.nb16[t];
+  }
+  g.boff = (woff + 7) / 8 * 8;
+  g.image_elems = g.boff + 2 * g.cout;  // cout % 16 == 0: stays a multiple of 8
+  g.pfloats = poff + g.cout;
+  return true;
+}
+
+__device__ __forceinline__ f32x4 mma16(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(lds_addr));
+}
+
+__device__ __forceinline__ u32x4 tr_pair(const char* lo, const char* hi) {
+  const u32x2 l2 = __builtin_bit_cast(u32x2, tr_read(lo)), h2 = __builtin_bit_cast(u32x2, tr_read(hi));
+  return u32x4{l2[0], l2[1], h2[0], h2[1]};
+}
+
+// 8 consecutive bf16 at an 8-B aligned LDS address (two b64 reads)
+__device__ __forceinline__ u32x4 lds8(const bf16* p) {
+  const u32x2 a = *(const u32x2*)p, b = *(const u32x2*)(p + 4);
+  return u32x4{a[0], a[1], b[0], b[1]};
+}
+
+__device__ __forceinline__ int branch_of(const XeGeom& g, int co) {
+  int b = 0;
+  while (b + 1 < g.nbranch && co >= g.bco0[b + 1]) ++b;
+  return b;
+}
+
+// ---------------------------------------------------------------------------
+// weight image: tile t: [16 co][k_t dy][jwp_t] bf16 with j = dx * cp + c,
+// every tap outside the channel's own (centred) window, c >= cin and
+// j >= k_t * cp zero; then the concatenated f32 bias.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void xe_pack_kernel(DvCrossEmbed ce, XeGeom g, bf16* img) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < g.boff + g.cout; i += gridDim.x * 256) {
+    if (i >= g.boff) {
+      const int co = i - g.boff, b = branch_of(g, co);
+      ((float*)(img + g.boff))[co] = ce.b[b] ? ce.b[b][co - g.bco0[b]] : 0.f;
+      continue;
+    }
+    int t = 0;
+    while (t + 1 < g.ntiles && i >= g.woff[t + 1]) ++t;
+    const int k = g.k[t], jwp = g.jwp[t];
+    const int local = i - g.woff[t];
+    float v = 0.f;
+    if (local < 16 * k * jwp) {
+      const int col = local / (k * jwp), rem = local - col * k * jwp;
+      const int dy = rem / jwp, j = rem - dy * jwp;
+      const int co = 16 * t + col, b = branch_of(g, co);
+      const int kb = g.bk[b], o = (k - kb) / 2;
+      const int dx = j / g.cp, c = j - dx * g.cp;
+      const int ky = dy - o, kx = dx - o;
+      if (j < k * g.cp && c < g.cin && (unsigned)ky < (unsigned)kb && (unsigned)kx < (unsigned)kb)
+        v = ce.w[b][(((long long)(co - g.bco0[b]) * g.cin + c) * kb + ky) * kb + kx];
+    }
+    img[i] = (bf16)v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward: a workgroup = R output rows x WB columns of one frame, all output
+// channels.  LDS: the weight image + the (R + kmax - 1) x (WB + kmax + 7)
+// input window [col][CP].  A wave job = 32 pixels of one row (two 16-pixel
+// MFMA columns sharing each weight fragment), every tile in turn.
+// D[co][px]: lane holds pixel (l & 15), channels 4 (l >> 4) .. +3 -> one
+// 8-byte store per lane per tile and pixel block.
+// ---------------------------------------------------------------------------
+constexpr int XE_R = 8;
+
+template <int CP>
+__global__ __launch_bounds__(512) void xe_fwd_kernel(XeGeom g, const bf16* img, const bf16* x,
+                                                     int ldx, bf16* y, int ldy, int H, int W,
+                                                     int WB) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cgs = W / WB, rgs = (H + XE_R - 1) / XE_R;
+  int bid = blockIdx.x;
+  const int cg = bid % cgs;
+  bid /= cgs;
+  const int rg = bid % rgs, f = bid / rgs;
+  const int y0 = rg * XE_R, x0 = cg * WB, half = g.kmax / 2;
+  const int XR = XE_R + g.kmax - 1, XC = WB + g.kmax + 7;
+  bf16* sW = (bf16*)smem;
+  bf16* sX = sW + g.image_elems;
+
+  for (int i = tid; i < g.image_elems / 8; i += 512) ((u32x4*)sW)[i] = ((const u32x4*)img)[i];
+  for (int i = tid; i < XR * XC; i += 512) {
+    const int rr = i / XC, cc = i - rr * XC;
+    const int yy = y0 + rr - half, xx = x0 + cc - half;
+    bf16 v[CP];
+#pragma unroll
+    for (int c = 0; c < CP; ++c) v[c] = (bf16)0.f;
+    if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W && cc < WB + g.kmax - 1) {
+      const bf16* src = x + ((long long)(f * H + yy) * W + xx) * ldx;
+      if (CP == 4) {
+        const u32x2 q = *(const u32x2*)src;
+        const bf16x4 e = __builtin_bit_cast(bf16x4, q);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = c < g.cin ? e[c] : (bf16)0.f;
+      } else {
+        const u32x4 q = *(const u32x4*)src;
+        const bf16x8 e = __builtin_bit_cast(bf16x8, q);
+#pragma unroll
+        for (int c = 0; c < CP; ++c) v[c] = c < g.cin ? e[c % 8] : (bf16)0.f;
+      }
+    }
+    bf16* dst = sX + (long long)i * CP;
+#pragma unroll
+    for (int c = 0; c < CP; ++c) dst[c] = v[c];
+  }
+  __syncthreads();
+
+  const float* sb = (const float*)(sW + g.boff);
+  const int jobs_per_row = WB / 32;
+  const int px = lane & 15, kg = lane >> 4;
+  for (int job = wave; job < XE_R * jobs_per_row; job += 8) {
+    const int r = job / jobs_per_row, xb = (job - r * jobs_per_row) * 32;
+    if (y0 + r >= H) break;
+    bf16* out = y + ((long long)(f * H + y0 + r) * W + x0 + xb + px) * ldy;
+    for (int t = 0; t < g.ntiles; ++t) {
+      const int k = g.k[t], jw = g.jw[t], jwp = g.jwp[t];
+      const int cofs = half - k / 2;  // the tile's window inside the kmax halo
+      const bf16* wt = sW + g.woff[t] + px * k * jwp + 8 * kg;
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      for (int dy = 0; dy < k; ++dy) {
+        const bf16* xr = sX + ((long long)(r + cofs + dy) * XC + xb + px + cofs) * CP + 8 * kg;
+        const bf16* wr = wt + dy * jwp;
+        for (int ks = 0; ks < jw; ks += 32) {
+          const u32x4 wf = *(const u32x4*)(wr + ks);
+          a0 = mma16(wf, lds8(xr + ks), a0);
+          a1 = mma16(wf, lds8(xr + 16 * CP + ks), a1);
+        }
+      }
+      const int co = 16 * t + 4 * kg;
+      bf16x4 o0, o1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o0[e] = (bf16)(a0[e] + sb[co + e]);
+        o1[e] = (bf16)(a1[e] + sb[co + e]);
+      }
+      *(bf16x4*)(out + co) = o0;
+      *(bf16x4*)(out + 16 * ldy + co) = o1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient.  Workgroup = a band of `rows` image rows of one frame;
+// per row: LDS dY row [W][cout + 8] and the kmax input rows around it
+// [kmax][W + kmax + 7][CP] (double-buffered: the next row's global loads are
+// in registers while this row's MFMAs run).  Wave w owns accumulator items
+// [w * per, w * per + per) of the flat (tile, dy, 16-column block) list.
+// ---------------------------------------------------------------------------
+template <int CP, int MAXI>
+__global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy, int lddy,
+                                                       const bf16* x, int ldx, float* part, int H,
+                                                       int W, int rows, int per) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bands = (H + rows - 1) / rows;
+  const int f = blockIdx.x / bands, yb = (blockIdx.x % bands) * rows;
+  const int yend = min(yb + rows, H);
+  const int half = g.kmax / 2, XC = W + g.kmax + 7;
+  const int DS = g.cout + 8;                 // dY row pitch (elements)
+  const int DYB = W * DS, XB = g.kmax * XC * CP;  // buffer sizes (elements)
+  bf16* sD = (bf16*)smem;                    // [2][W][DS]
+  bf16* sX = sD + 2 * DYB;                   // [2][kmax][XC][CP]
+
+  // ---- this wave's items: tile, LDS offsets ----
+  int it_t[MAXI], it_boff[MAXI];
+  const int i0 = wave * per;
+#pragma unroll
+  for (int i = 0; i < MAXI; ++i) {
+    int idx = i0 + i, t = 0;
+    it_t[i] = -1;
+    it_boff[i] = 0;
+    if (i >= per || idx >= g.items) continue;
+    while (idx >= g.k[t] * g.nb16[t]) {
+      idx -= g.k[t] * g.nb16[t];
+      ++t;
+    }
+    const int d = idx / g.nb16[t], nb = idx - d * g.nb16[t];
+    const int cofs = half - g.k[t] / 2;
+    it_t[i] = t;
+    it_boff[i] = ((d + cofs) * XC + cofs) * CP + 16 * nb;  // element offset (pixel 0)
+  }
+
+  int t_lo = XE_MAXT, t_hi = -1;
+#pragma unroll
+  for (int i = 0; i < MAXI; ++i)
+    if (it_t[i] >= 0) {
+      t_lo = min(t_lo, it_t[i]);
+      t_hi = max(t_hi, it_t[i]);
+    }
+
+  f32x4 acc[MAXI];
+#pragma unroll
+  for (int i = 0; i < MAXI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float accb = 0.f;  // bias: waves < ntiles own tile `wave`
+
+  // ---- staging: global -> registers (next row) -> LDS ----
+  const int dchunks = W * (g.cout / 8);       // 16-B dY chunks per row
+  const int xelems = g.kmax * XC;             // window pixels per row
+  constexpr int DPT = 4, XPT = 8;             // per-thread register slots
+  u32x4 dreg[DPT];
+  bf16 xreg[XPT][CP];
+  auto load_row = [&](int yy) {
+#pragma unroll
+    for (int s = 0; s < DPT; ++s) {
+      const int i = tid + 512 * s;
+      if (i < dchunks) {
+        const int p = i / (g.cout / 8), c8 = i - p * (g.cout / 8);
+        dreg[s] = *(const u32x4*)(dy + ((long long)(f * H + yy) * W + p) * lddy + 8 * c8);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < XPT; ++s) {
+      const int i = tid + 512 * s;
+#pragma unroll
+      for (int c = 0; c < CP; ++c) xreg[s][c] = (bf16)0.f;
+      if (i < xelems) {
+        const int rr = i / XC, cc = i - rr * XC;
+        const int sy = yy + rr - half, sx = cc - half;
+        if ((unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W) {
+          const bf16* src = x + ((long long)(f * H + sy) * W + sx) * ldx;
+          if (CP == 4) {
+            const bf16x4 e = __builtin_bit_cast(bf16x4, *(const u32x2*)src);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) xreg[s][c] = c < g.cin ? e[c] : (bf16)0.f;
+          } else {
+            const bf16x8 e = __builtin_bit_cast(bf16x8, *(const u32x4*)src);
+#pragma unroll
+            for (int c = 0; c < CP; ++c) xreg[s][c] = c < g.cin ? e[c % 8] : (bf16)0.f;
+          }
+        }
+      }
+    }
+  };
+  auto store_row = [&](int buf) {
+    bf16* d = sD + buf * DYB;
+#pragma unroll
+    for (int s = 0; s < DPT; ++s) {
+      const int i = tid + 512 * s;
+      if (i < dchunks) {
+        const int p = i / (g.cout / 8), c8 = i - p * (g.cout / 8);
+        *(u32x4*)(d + p * DS + 8 * c8) = dreg[s];
+      }
+    }
+    bf16* xs = sX + buf * XB;
+#pragma unroll
+    for (int s = 0; s < XPT; ++s) {
+      const int i = tid + 512 * s;
+      if (i < xelems) {
+#pragma unroll
+        for (int c = 0; c < CP; ++c) xs[i * CP + c] = xreg[s][c];
+      }
+    }
+  };
+
+  // lane parts of the transposed reads: 16-lane group kg reads pixel rows
+  // 8 kg + q (lo) and 8 kg + 4 + q (hi), 8-B chunk pp of a 32-B row
+  const int kg = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int plo = 8 * kg + q;
+
+  if (yb < yend) {
+    load_row(yb);
+    store_row(0);
+  }
+  __syncthreads();
+  for (int yy = yb; yy < yend; ++yy) {
+    const int buf = (yy - yb) & 1;
+    const bool more = yy + 1 < yend;
+    if (more) load_row(yy + 1);
+    const char* d = (const char*)(sD + buf * DYB);
+    const char* xs = (const char*)(sX + buf * XB);
+    for (int p0 = 0; p0 < W; p0 += 32) {
+      const char* arow = d + ((p0 + plo) * DS + 4 * pp) * 2;
+      if (wave < g.ntiles) {  // bias: the dY^T fragment of tile `wave` summed on the VALU
+        const char* a = arow + 32 * wave;
+        const bf16x8 e = __builtin_bit_cast(bf16x8, tr_pair(a, a + 4 * DS * 2));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) accb += (float)e[j];
+      }
+      const int lanex = ((p0 + plo) * CP + 4 * pp) * 2;
+      // items are ordered by tile: one dY^T fragment per tile this wave touches
+      for (int t = t_lo; t <= t_hi; ++t) {
+        const char* a = arow + 32 * t;
+        const u32x4 fa = tr_pair(a, a + 4 * DS * 2);
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+          if (it_t[i] != t) continue;
+          const char* b = xs + it_boff[i] * 2 + lanex;
+          acc[i] = mma16(fa, tr_pair(b, b + 4 * CP * 2), acc[i]);
+        }
+      }
+    }
+    if (more) {
+      store_row(buf ^ 1);
+    }
+    __syncthreads();
+  }
+
+  // ---- partial of this band: D[co][n]: lane n = l & 15, co = 4 kg + e ----
+  float* pp_ = part + (long long)blockIdx.x * g.pfloats;
+#pragma unroll
+  for (int i = 0; i < MAXI; ++i) {
+    if (it_t[i] < 0) continue;
+    int idx = i0 + i, t = 0;
+    while (idx >= g.k[t] * g.nb16[t]) {
+      idx -= g.k[t] * g.nb16[t];
+      ++t;
+    }
+    const int d = idx / g.nb16[t], nb = idx - d * g.nb16[t];
+    const int row = g.nb16[t] * 16;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      pp_[g.poff[t] + ((4 * kg + e) * g.k[t] + d) * row + 16 * nb + (lane & 15)] = acc[i][e];
+  }
+  if (wave < g.ntiles) {
+    accb += __shfl_xor(accb, 16, 64);
+    accb += __shfl_xor(accb, 32, 64);
+    if (lane < 16) pp_[g.pfloats - g.cout + 16 * wave + lane] = accb;
+  }
+}
+
+// sum the bands and scatter into every branch's torch-layout gradient:
+// 32 outputs x 8 split groups per workgroup, 8 loads in flight per lane
+__global__ __launch_bounds__(256) void xe_wgrad_finish_kernel(DvCrossEmbed ce, XeGeom g,
+                                                              const float* part, int S,
+                                                              long long total) {
+  __shared__ float sh[8][32];
+  const int ol = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const long long o = (long long)blockIdx.x * 32 + ol;
+  int src = -1, b = 0;
+  long long local = o;
+  float* dst = nullptr;
+  int acc = 0;
+  if (o < total) {
+    for (b = 0; b < g.nbranch; ++b) {
+      const long long nw = (long long)g.bcout[b] * g.cin * g.bk[b] * g.bk[b];
+      if (local < nw) {
+        const int kb = g.bk[b];
+        const int kx = (int)(local % kb), ky = (int)(local / kb % kb);
+        const int c = (int)(local / (kb * kb) % g.cin), col = (int)(local / ((long long)kb * kb * g.cin));
+        const int co = g.bco0[b] + col, t = co / 16, k = g.k[t], o2 = (k - kb) / 2;
+        src = g.poff[t] + ((co % 16) * k + ky + o2) * g.nb16[t] * 16 + (kx + o2) * g.cp + c;
+        dst = ce.dw[b] + local;
+        acc = ce.accumulate_w;
+        break;
+      }
+      local -= nw;
+      if (local < g.bcout[b]) {
+        src = g.pfloats - g.cout + g.bco0[b] + (int)local;
+        dst = ce.db[b] ? ce.db[b] + local : nullptr;
+        acc = ce.accumulate_b;
+        break;
+      }
+      local -= g.bcout[b];
+    }
+  }
+  float v = 0.f;
+  if (src >= 0) {
+    const float* p = part + src;
+    const long long st = g.pfloats;
+    int s = grp;
+    for (; s + 56 < S; s += 64) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = p[(long long)(s + 8 * u) * st];
+      v += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+    }
+    for (; s < S; s += 8) v += p[(long long)s * st];
+  }
+  sh[grp][ol] = v;
+  __syncthreads();
+  if (grp != 0 || !dst) return;
+  v = ((sh[0][ol] + sh[1][ol]) + (sh[2][ol] + sh[3][ol])) + ((sh[4][ol] + sh[5][ol]) + (sh[6][ol] + sh[7][ol]));
+  *dst = acc ? *dst + v : v;
+}
+
+long long xe_total_grads(const XeGeom& g) {
+  long long n = 0;
+  for (int b = 0; b < g.nbranch; ++b) n += (long long)g.bcout[b] * (g.cin * g.bk[b] * g.bk[b] + 1);
+  return n;
+}
+
+int xe_fwd_wb(int w) { return w % 64 == 0 ? 64 : 32; }
+
+size_t xe_fwd_lds(const XeGeom& g, int w) {
+  const int WB = xe_fwd_wb(w);
+  return (size_t)g.image_elems * 2 + (size_t)(XE_R + g.kmax - 1) * (WB + g.kmax + 7) * g.cp * 2;
+}
+
+size_t xe_wgrad_lds(const XeGeom& g, int w) {
+  return (size_t)2 * w * (g.cout + 8) * 2 + (size_t)2 * g.kmax * (w + g.kmax + 7) * g.cp * 2;
+}
+
+int xe_rows(int nf, int h) {
+  // ~256 bands (one 512-thread workgroup per CU)
+  long long want = (long long)nf * h / 256;
+  int rows = (int)std::max(1ll, want);
+  return std::min(rows, h);
+}
+
+bool xe_shape_ok(const XeGeom& g, int nf, int h, int w, int ldx) {
+  if (nf < 1 || h < 1 || w < 32 || w % 32 || ldx % g.cp || ldx < g.cin) return false;
+  if ((long long)nf * h * w * std::max(ldx, g.cout) >= (1ll << 31)) return false;
+  return true;
+}
+
+template <typename F>
+void xe_allow_lds(F* fn) {
+  (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+}  // namespace
+
+extern "C" int dv_cross_embed_image_elems(const DvCrossEmbed* ce, long long* elems) {
+  DV_REQUIRE(ce && elems, "null pointer");
+  XeGeom g;
+  DV_REQUIRE(xe_geom(*ce, g), "unsupported branch set (1..4 odd k <= 15 ascending, cin <= 8, "
+                              "sum(cout) % 16 == 0, <= 128)");
+  *elems = g.image_elems;
+  return DV_OK;
+}
+
+extern "C" int dv_cross_embed_pack(const DvCrossEmbed* ce, void* image, void* stream) {
+  DV_REQUIRE(ce && image, "null pointer");
+  XeGeom g;
+  DV_REQUIRE(xe_geom(*ce, g), "unsupported branch set");
+  for (int b = 0; b < g.nbranch; ++b) DV_REQUIRE(ce->w[b], "null weight");
+  const int blocks = std::min(1024, (g.boff + g.cout + 255) / 256);
+  xe_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*ce, g, (bf16*)image);
+  return check_launch("cross_embed_pack");
+}
+
+extern "C" int dv_cross_embed_fwd(const DvCrossEmbed* ce, const void* image, const void* x,
+                                  int ldx, void* y, int ldy, int nf, int h, int w, void* stream) {
+  DV_REQUIRE(ce && image && x && y, "null pointer");
+  XeGeom g;
+  DV_REQUIRE(xe_geom(*ce, g), "unsupported branch set");
+  DV_REQUIRE(xe_shape_ok(g, nf, h, w, ldx) && ldy % 4 == 0 && ldy >= g.cout,
+             "needs w % 32 == 0, ldx % (4 or 8) == 0, ldy % 4 == 0");
+  const size_t lds = xe_fwd_lds(g, w);
+  DV_REQUIRE(lds <= 160 * 1024, "LDS footprint too large");
+  const int WB = xe_fwd_wb(w);
+  const long long blocks = (long long)nf * ((h + XE_R - 1) / XE_R) * (w / WB);
+  hipStream_t st = (hipStream_t)stream;
+  static bool once = (xe_allow_lds(xe_fwd_kernel<4>), xe_allow_lds(xe_fwd_kernel<8>), true);
+  (void)once;
+  if (g.cp == 4)
+    xe_fwd_kernel<4><<<(unsigned)blocks, 512, lds, st>>>(g, (const bf16*)image, (const bf16*)x, ldx,
+                                                         (bf16*)y, ldy, h, w, WB);
+  else
+    xe_fwd_kernel<8><<<(unsigned)blocks, 512, lds, st>>>(g, (const bf16*)image, (const bf16*)x, ldx,
+                                                         (bf16*)y, ldy, h, w, WB);
+  return check_launch("cross_embed_fwd");
+}
+
+extern "C" int dv_cross_embed_wgrad_ws(const DvCrossEmbed* ce, int nf, int h, int w,
+                                       long long* floats) {
+  DV_REQUIRE(ce && floats, "null pointer");
+  XeGeom g;
+  DV_REQUIRE(xe_geom(*ce, g), "unsupported branch set");
+  DV_REQUIRE(nf > 0 && h > 0, "bad sizes");
+  const int rows = xe_rows(nf, h);
+  *floats = (long long)nf * ((h + rows - 1) / rows) * g.pfloats;
+  return DV_OK;
+}
+
+extern "C" int dv_cross_embed_wgrad(const DvCrossEmbed* ce, const void* dy, int lddy,
+                                    const void* x, int ldx, float* ws, long long ws_floats, int nf,
+                                    int h, int w, void* stream) {
+  DV_REQUIRE(ce && dy && x && ws, "null pointer");
+  XeGeom g;
+  DV_REQUIRE(xe_geom(*ce, g), "unsupported branch set");
+  for (int b = 0; b < g.nbranch; ++b) DV_REQUIRE(ce->dw[b], "null weight gradient");
+  DV_REQUIRE(xe_shape_ok(g, nf, h, w, ldx) && lddy % 8 == 0 && lddy >= g.cout,
+             "needs w % 32 == 0, ldx % (4 or 8) == 0, lddy % 8 == 0");
+  long long need = 0;
+  dv_cross_embed_wgrad_ws(ce, nf, h, w, &need);
+  DV_REQUIRE(ws_floats >= need, "workspace too small (see dv_cross_embed_wgrad_ws)");
+  const size_t lds = xe_wgrad_lds(g, w);
+  DV_REQUIRE(lds <= 160 * 1024, "LDS footprint too large");
+  // register staging slots: DPT = 4 dY chunks, XPT = 8 window pixels per thread
+  DV_REQUIRE((long long)w * (g.cout / 8) <= 4 * 512 && (long long)g.kmax * (w + g.kmax + 7) <= 8 * 512,
+             "image row too wide for the staging slots");
+  const int per = (g.items + 7) / 8;
+  DV_REQUIRE(per <= 24, "too many accumulator tiles");
+  const int rows = xe_rows(nf, h);
+  const int S = nf * ((h + rows - 1) / rows);
+  hipStream_t st = (hipStream_t)stream;
+  static bool once = (xe_allow_lds(xe_wgrad_kernel<4, 12>), xe_allow_lds(xe_wgrad_kernel<4, 24>),
+                      xe_allow_lds(xe_wgrad_kernel<8, 12>), xe_allow_lds(xe_wgrad_kernel<8, 24>), true);
+  (void)once;
+  const bf16* d = (const bf16*)dy;
+  const bf16* xx = (const bf16*)x;
+#define XE_WG(CP, MI) \
+  xe_wgrad_kernel<CP, MI><<<(unsigned)S, 512, lds, st>>>(g, d, lddy, xx, ldx, ws, h, w, rows, per)
+  if (g.cp == 4) {
+    if (per <= 12) XE_WG(4, 12);
+    else XE_WG(4, 24);
+  } else {
+    if (per <= 12) XE_WG(8, 12);
+    else XE_WG(8, 24);
+  }
+#undef XE_WG
+  const long long total = xe_total_grads(g);
+  xe_wgrad_finish_kernel<<<(unsigned)((total + 31) / 32), 256, 0, st>>>(*ce, g, ws, S, total);
+  return check_launch("cross_embed_wgrad");
+}

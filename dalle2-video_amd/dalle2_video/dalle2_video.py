@@ -494,7 +494,12 @@ class CrossEmbedLayer3D(nn.Module):
         ])
 
     def forward_cl(self, x):
-        # All kernels share the input: one conv with the smaller kernels
+        weights = [c.weight for c in self.convs]
+        if ops.cross_embed_ok(x, weights):
+            # direct kernels: each 16-channel tile runs only its own window
+            # (dv_cross_embed_fwd / _wgrad)
+            return ops.cross_embed(x, weights, [c.bias for c in self.convs])
+        # f32 / other shapes: one conv with the smaller kernels
         # zero-embedded at the centre of the largest window (same 'same'
         # padding arithmetic) writes the channel concatenation directly. The
         # (cout <= 64) MMA tile is then full, and the input is gathered once

@@ -802,6 +802,124 @@ def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_s
 
 
 # ---------------------------------------------------------------------------
+# CrossEmbedLayer3D (dalle2_video.py:208-244): direct multi-window conv
+# ---------------------------------------------------------------------------
+class DvCrossEmbed(ctypes.Structure):
+    """Mirror of DvCrossEmbed (include/dv_hip.h)."""
+    _fields_ = [("nbranch", ctypes.c_int), ("cin", ctypes.c_int), ("k", ctypes.c_int * 4),
+                ("cout", ctypes.c_int * 4), ("w", ctypes.c_void_p * 4), ("b", ctypes.c_void_p * 4),
+                ("dw", ctypes.c_void_p * 4), ("db", ctypes.c_void_p * 4),
+                ("accumulate_w", ctypes.c_int), ("accumulate_b", ctypes.c_int)]
+
+
+def _cross_embed_desc(cin, weights, biases):
+    d = DvCrossEmbed()
+    d.nbranch, d.cin = len(weights), cin
+    for i, (w, b) in enumerate(zip(weights, biases)):
+        d.k[i], d.cout[i] = w.shape[-1], w.shape[0]
+        d.w[i] = w.data_ptr()
+        d.b[i] = None if b is None else b.data_ptr()
+    return d
+
+
+def cross_embed_ok(x, weights):
+    """Shapes the direct kernels take (else the padded implicit-GEMM conv runs)."""
+    if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 4 or not 1 <= len(weights) <= 4:
+        return False
+    nf, h, w, _ = x.shape
+    cin = weights[0].shape[1]
+    ks = [wt.shape[-1] for wt in weights]
+    try:
+        ld = cl_ld(x)
+    except _lib.DVError:
+        return False
+    cout = sum(wt.shape[0] for wt in weights)
+    return (cin <= 8 and all(wt.shape[1] == cin and wt.dim() == 5 and wt.dtype == torch.float32 for wt in weights)
+            and ks == sorted(ks) and all(k % 2 == 1 and k <= 15 for k in ks)
+            and cout % 16 == 0 and cout <= 128 and w % 32 == 0
+            and ld % (4 if cin <= 4 else 8) == 0 and x.data_ptr() % 16 == 0)
+
+
+_XE_WS = {}
+
+
+class CrossEmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, nbranch, *params):
+        weights = [p.detach().float().contiguous() for p in params[:nbranch]]
+        biases = [None if p is None else p.detach().float().contiguous() for p in params[nbranch:]]
+        nf, h, w, _ = x.shape
+        cin = weights[0].shape[1]
+        desc = _cross_embed_desc(cin, weights, biases)
+        n = ctypes.c_longlong(0)
+        call("dv_cross_embed_image_elems", ctypes.byref(desc), ctypes.byref(n))
+        img = torch.empty(n.value, dtype=torch.bfloat16, device=x.device)
+        call("dv_cross_embed_pack", ctypes.byref(desc), ptr(img), stream())
+        cout = sum(wt.shape[0] for wt in weights)
+        y = torch.empty(nf, h, w, cout, dtype=x.dtype, device=x.device)
+        m = nf * h * w
+        flops = 2.0 * m * cin * sum(wt.shape[0] * wt.shape[-1] ** 2 for wt in weights)
+        _launch("cross_embed_fwd_kernel", flops, x.element_size() * m * (cin + cout),
+                lambda: call("dv_cross_embed_fwd", ctypes.byref(desc), ptr(img), ptr(x), cl_ld(x), ptr(y),
+                             cout, nf, h, w, stream()), ("fwd", m, cout, cin * max(wt.shape[-1] for wt in weights) ** 2))
+        ctx.save_for_backward(x)
+        ctx.nbranch = nbranch
+        ctx.params = params
+        ctx.flops = flops
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        nb = ctx.nbranch
+        wparams, bparams = ctx.params[:nb], ctx.params[nb:]
+        dyv, lddy = _grad_view(dy)
+        if lddy % 8:
+            dyv, lddy = dyv.contiguous(), dyv.shape[-1]
+        nf, h, w, _ = x.shape
+        cin = wparams[0].shape[1]
+        weights = [p.detach() for p in wparams]
+        desc = _cross_embed_desc(cin, weights, [None if b is None else b.detach() for b in bparams])
+        ret_w, ret_b = [None] * nb, [None] * nb
+        # gradients straight into the leaves' .grad (zero-filled when new, so
+        # every branch accumulates); otherwise returned
+        for i in range(nb):
+            slot = _grad_out(wparams[i], zero=True) if ctx.needs_input_grad[2 + i] else None
+            if slot is None:
+                ret_w[i] = torch.zeros_like(weights[i], dtype=torch.float32)
+                desc.dw[i] = ret_w[i].data_ptr()
+            else:
+                desc.dw[i] = slot[0].data_ptr()
+            b = bparams[i]
+            if b is not None and ctx.needs_input_grad[2 + nb + i]:
+                bslot = _grad_out(b, zero=True)
+                if bslot is None:
+                    ret_b[i] = torch.zeros(b.shape, dtype=torch.float32, device=dy.device)
+                    desc.db[i] = ret_b[i].data_ptr()
+                else:
+                    desc.db[i] = bslot[0].data_ptr()
+        desc.accumulate_w = desc.accumulate_b = 1
+        need = ctypes.c_longlong(0)
+        call("dv_cross_embed_wgrad_ws", ctypes.byref(desc), nf, h, w, ctypes.byref(need))
+        key = str(dy.device)
+        ws = _XE_WS.get(key)
+        if ws is None or ws.numel() < need.value:
+            ws = _XE_WS[key] = torch.empty(need.value, dtype=torch.float32, device=dy.device)
+        m = nf * h * w
+        _launch("cross_embed_wgrad_kernel", ctx.flops, dy.element_size() * m * (cin + dy.shape[-1]),
+                lambda: call("dv_cross_embed_wgrad", ctypes.byref(desc), ptr(dyv), lddy, ptr(x), cl_ld(x), ptr(ws),
+                             ws.numel(), nf, h, w, stream()), ("wgrad", dy.shape[-1], cin, m))
+        return (None, None, *ret_w, *ret_b)
+
+
+def cross_embed(x, weights, biases):
+    """Concatenated (1,k,k) 'same' convolutions of one channels-last input
+    (CrossEmbedLayer3D, stride 1): weights / biases per branch, kernel sizes
+    ascending.  x's channels beyond weights[i].shape[1] are ignored."""
+    return CrossEmbedFn.apply(x, len(weights), *weights, *biases)
+
+
+# ---------------------------------------------------------------------------
 # GroupNorm (+ per-sample scale/shift) + SiLU (+ residual)  — Block3D
 # ---------------------------------------------------------------------------
 class GroupNormActFn(torch.autograd.Function):

@@ -102,6 +102,40 @@ int dv_wgrad_reduce_plan(DvWgradReduceEntry* host_table, int n, long long* block
 int dv_wgrad_reduce_batched(const DvWgradReduceEntry* table, int n, long long blocks,
                             void* stream);
 
+/* ---- CrossEmbedLayer3D (dalle2_video.py:208-244, Unet3D.init_conv) ------
+ * nbranch parallel (1,k_b,k_b) 'same' convolutions of one small-channel
+ * input (cin <= 8: the video, + the lowres conditioning for upsampler unets),
+ * outputs concatenated along channels in branch order (dim/2, dim/4, rest).
+ * Direct MFMA kernels: each 16-channel output tile runs only its own window.
+ * w[b] / b[b]: torch Conv3d weight (cout_b, cin, 1, k_b, k_b) and bias
+ * (f32, b may be NULL).  dw / db (wgrad only): gradients of the same shapes,
+ * written or added to (accumulate_w / accumulate_b; db[b] may be NULL).
+ * Requirements: k_b odd <= 15 ascending, sum(cout_b) % 16 == 0 and <= 128;
+ * bf16 activations, w % 32 == 0, ldx % 4 == 0 (cin <= 4) or % 8 == 0,
+ * ldy % 4 == 0, lddy % 8 == 0.
+ *   dv_cross_embed_pack: weights + biases -> `image` (device, bf16 elements
+ *     from dv_cross_embed_image_elems; repack whenever the weights change);
+ *   dv_cross_embed_fwd: y[p][0..sum cout) = concat_b conv_b(x)[p] + bias;
+ *   dv_cross_embed_wgrad: weight / bias gradients from dy; ws = f32 scratch
+ *     of dv_cross_embed_wgrad_ws floats.                                    */
+typedef struct {
+  int nbranch, cin;
+  int k[4], cout[4];
+  const float* w[4];
+  const float* b[4];
+  float* dw[4];
+  float* db[4];
+  int accumulate_w, accumulate_b;
+} DvCrossEmbed;
+int dv_cross_embed_image_elems(const DvCrossEmbed* ce, long long* elems);
+int dv_cross_embed_pack(const DvCrossEmbed* ce, void* image, void* stream);
+int dv_cross_embed_fwd(const DvCrossEmbed* ce, const void* image, const void* x, int ldx,
+                       void* y, int ldy, int nf, int h, int w, void* stream);
+int dv_cross_embed_wgrad_ws(const DvCrossEmbed* ce, int nf, int h, int w, long long* floats);
+int dv_cross_embed_wgrad(const DvCrossEmbed* ce, const void* dy, int lddy, const void* x,
+                         int ldx, float* ws, long long ws_floats, int nf, int h, int w,
+                         void* stream);
+
 /* 3x3 forward / dgrad, window form (dalle2_video.py:107 Block3D.project at
  * the 8x8 .. 64x64 stages, and the dgrads of those convs): same contract as
  * dv_conv_fwd with ksize = 3, but `wpack` is the 16-channel-chunk-major
