@@ -35,6 +35,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "Unet3D denoise-steps/sec, 16f×64×64 clip bs=4; 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2516.6   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_TBS = 8.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 STEP_TFLOP = 3.491          # ~3x the 1,163.6 GFLOP forward contractions
 FWD_TFLOP = 1.1636          # Cfg2 forward contractions (bs=4)
 
@@ -378,11 +379,16 @@ def main():
             if shp is None:
                 continue
             tf = v["flops"] / (v["ms"] * 1e-3) / 1e12
+            tbs = v["bytes"] / (v["ms"] * 1e-3) / 1e12
+            # bound by arithmetic intensity (algorithmic FLOP per algorithmic
+            # byte: input read once, output written once) vs the ridge point
+            hbm = v["flops"] / max(v["bytes"], 1.0) < peak / PEAK_HBM_TBS
             conv_shapes.append({"kernel": k, "pass": shp[0], "M": shp[1], "N": shp[2], "K": shp[3],
                                 "launches_per_step": v["count"] // nrep,
                                 "us_per_launch": round(v["ms"] / v["count"] * 1e3, 2),
                                 "ms_per_step": round(v["ms"] / nrep, 3), "tflops": round(tf, 1),
-                                "frac": round(tf / peak, 4)})
+                                "tbytes_per_s": round(tbs, 2), "bound": "hbm" if hbm else "mfma",
+                                "frac": round(tbs / PEAK_HBM_TBS if hbm else tf / peak, 4)})
         # north-star sub-metric: mid-attention QK^T/PV (fwd + bwd) vs the bf16 MFMA peak
         att = [v for k, v in summ.items() if k.startswith("attn:")]
         if att:

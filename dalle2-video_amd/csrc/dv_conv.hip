@@ -1829,12 +1829,15 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a, hipStream_t st) {
 }
 
 // tile choice for the glds path (mirrored by ops.conv_tile for kernel naming)
-inline void glds_tile(long long M, int cout, int& bm, int& bn) {
+inline void glds_tile(long long M, int cout, int K, int& bm, int& bn) {
   bn = cout <= 64 ? 64 : 128;
   bm = bn == 64 ? 256 : 128;
   if (((M + bm - 1) / bm) * ((cout + bn - 1) / bn) < 512) bm = 128;
   // fewer 128-pixel tiles than CUs (8x8 stage, mid block): halve the pixel tile
   if (bn == 128 && ((M + 127) / 128) * ((cout + 127) / 128) < 256) bm = 64;
+  // (K <= 128, the memory-bound 1x1 convs: smaller tiles / more resident
+  // workgroups measured no faster, tools/k1x1.py: 4.2 TB/s either way)
+  (void)K;
 }
 
 // the statistics epilogue's fields (off when gn_sums is null)
@@ -1873,7 +1876,7 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
     const long long maxld = ld0 > (x1 ? ld1 : 0) ? ld0 : ld1;
     if (cin % 64 == 0 && a.c0 % 64 == 0 && a.M * maxld < (1ll << 31)) {
       int bm, bn;
-      glds_tile(a.M, cout, bm, bn);
+      glds_tile(a.M, cout, a.K, bm, bn);
       if (bm == 256) return launch_fwd_glds<256, 64>(a, st);
       if (bn == 64) return launch_fwd_glds<128, 64>(a, st);
       if (bm == 64) return launch_fwd_glds<64, 128>(a, st);
@@ -2353,7 +2356,9 @@ bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout
 // slower on every Cfg2 shape (tools/ab_fwd.sh): occupancy wins.
 inline void stripe_split(int nstages, int grid_xy, long long grad_floats, int& sps, int& S) {
   (void)grad_floats;
+  static const int minst = getenv("DV_WG_MINST") ? atoi(getenv("DV_WG_MINST")) : 1;  // A/B knob
   long long want = 256 / grid_xy;
+  if (minst > 1 && want > nstages / minst) want = nstages / minst;
   if (want > nstages) want = nstages;
   if (want < 1) want = 1;
   sps = (int)((nstages + want - 1) / want);

@@ -21,6 +21,7 @@
 #include "dv_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 using namespace dv;
 
@@ -839,6 +840,13 @@ extern "C" int dv_xattn_fold(int dtype, const float* wq, const float* wo, const 
   return fold_t<float>(wq, wo, kv, null_kv, g1, at, vt, Kt, KtT, Vt, VtT, colsum, nb, C, scale, st);
 }
 
+// channel-split threshold (A/B knob DV_XA_SPLIT_TILES): token tiles below it
+// run 4 waves per tile
+static long long xa_split_tiles() {
+  static const long long v = getenv("DV_XA_SPLIT_TILES") ? atoll(getenv("DV_XA_SPLIT_TILES")) : 1024;
+  return v;
+}
+
 extern "C" int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ldo, long long ntok,
                             long long P, int C, const void* Kt, const void* Vt,
                             const float* colsum, const float* g2, float eps, float* stats,
@@ -849,7 +857,7 @@ extern "C" int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ld
   DV_REQUIRE(C % VEC == 0 && ldx % VEC == 0 && ldo % 4 == 0, "C / strides must be multiples of 16 bytes");
   hipStream_t st = (hipStream_t)stream;
   const long long tiles = (ntok / P) * ((P + 31) / 32);
-  const bool split = tiles < 1024 && C >= 128;  // fewer than 256 four-wave workgroups otherwise
+  const bool split = tiles < xa_split_tiles() && C >= 128;  // fewer than 256 four-wave workgroups otherwise
   const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
   if (dtype == DV_BF16) {
     if (split) xattn_fwd_kernel<bf16, 4><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (bf16*)out, ldo, ntok, P, C, (const bf16*)Kt, (const bf16*)Vt, colsum, g2, eps, stats, (bf16*)pbuf);
@@ -872,7 +880,7 @@ extern "C" int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const vo
   DV_REQUIRE(P > 0 && ntok % P == 0 && C % 8 == 0, "bad shape");
   hipStream_t st = (hipStream_t)stream;
   const long long tiles = (ntok / P) * ((P + 31) / 32);
-  const bool split = tiles < 1024 && C >= 128;
+  const bool split = tiles < xa_split_tiles() && C >= 128;
   const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
 #define XB_ARGS(T) (const T*)dy, lddy, (const T*)x, ldx, (T*)dx, lddx, ntok, P, C, (const T*)KtT, \
     (const T*)Vt, (const T*)VtT, colsum, g2, stats, (const T*)pbuf, (T*)dobuf, (T*)dsbuf, (T*)p2buf

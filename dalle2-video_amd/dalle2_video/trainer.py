@@ -447,13 +447,22 @@ class VideoDecoderTrainer(nn.Module):
         self.register_buffer("steps", torch.tensor([0] * self.num_unets))
         # accelerator.prepare(..., train, val) (trainer.py:117-124) shards the
         # loaders per process: each rank iterates a disjoint rank-strided part
+        # and places the batches on the device (here: pinned host batches
+        # copied on a side stream one batch ahead, datasets.DeviceLoader)
         rank = dist.get_rank() if self.world > 1 else 0
-        self.train_loader = (shard_loader(dataloaders["train"], self.world, rank)
-                             if exists(dataloaders) else None)
-        self.val_loader = (shard_loader(dataloaders["val"], self.world, rank)
-                           if exists(dataloaders) else None)
+        self.train_loader = self._prepare_loader(dataloaders["train"], rank) if exists(dataloaders) else None
+        self.val_loader = self._prepare_loader(dataloaders["val"], rank) if exists(dataloaders) else None
         if self.world > 1:
             broadcast_parameters(decoder, 0)
+
+    def _prepare_loader(self, loader, rank):
+        from .datasets import DeviceLoader
+
+        loader = shard_loader(loader, self.world, rank)
+        dev = next(self.decoder.parameters()).device
+        if loader is None or dev.type != "cuda" or os.environ.get("DV_DEVICE_LOADER", "1") == "0":
+            return loader
+        return DeviceLoader(loader, dev)
 
     @property
     def device(self):
