@@ -260,7 +260,7 @@ __device__ __forceinline__ void xwave_sum(float* v, int n, float* sh, int cw, in
   }
 }
 
-template <typename T, int CS>
+template <typename T, int CS, int NCT>
 __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* out, int ldo,
                                                         long long ntok, long long P, int C,
                                                         const T* Kt, const T* Vt,
@@ -284,14 +284,31 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
   const int Cp = (C + 31) / 32 * 32;
   const T* Ktb = Kt + (long long)b * KP * Cp;
   const T* Vtb = Vt + (long long)b * Cp * KP;
+  // exact-trip bf16 path: the residual's x values (pass-3 layout) are loaded
+  // up front with the pass-1 reads of the same lines (no second round trip)
+  constexpr bool CACHE = NCT > 0 && NCT <= 4 && sizeof(T) == 2;
+  u32x2 xres[CACHE ? NCT : 1][4];
+  if constexpr (CACHE) {
+#pragma unroll
+    for (int it = 0; it < NCT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xres[it][g] = *(const u32x2*)(xr + 32 * cw + it * 32 * CS + 8 * g + 4 * h);
+  }
   // ---- scores: S^T = Kt . X^T over raw x, LN stats in the same pass ----
   f32x16 acc;
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
   float sx = 0.f, sxx = 0.f;
-  for (int c0 = 2 * VEC * cw; c0 < Cp; c0 += 2 * VEC * CS) {
+  // channel loops: NCT > 0 = exactly NCT 32-channel tiles per wave and
+  // C % 32 == 0 (checked on the host): straight-line unrolled code, so every
+  // tile's loads can issue up front; NCT == 0: bounded loop with exits
+  constexpr int NIT = NCT > 0 ? NCT : 8;
+#pragma unroll
+  for (int it = 0; it < NIT * 32 / (2 * VEC); ++it) {
+    const int c0 = 2 * VEC * cw + it * 2 * VEC * CS;
+    if (NCT == 0 && c0 >= Cp) break;
     const int c = c0 + h * VEC;
-    const u32x4 xv = c < C ? *(const u32x4*)(xr + c) : u32x4{0u, 0u, 0u, 0u};
+    const u32x4 xv = (NCT > 0 || c < C) ? *(const u32x4*)(xr + c) : u32x4{0u, 0u, 0u, 0u};
     const u32x4 kv = *(const u32x4*)(Ktb + (long long)r * Cp + c);
     float f[VEC];
     Vec<T>::to_f(xv, f);
@@ -338,7 +355,10 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
   }
   // ---- o statistics (pass 1), then the normalised output + residual (pass 2) ----
   float so = 0.f, soo = 0.f;
-  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int ct = 32 * cw + it * 32 * CS;
+    if (NCT == 0 && ct >= Cp) break;
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
@@ -357,7 +377,10 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
   const float mu2 = so / C;
   const float rs2 = rsqrtf(fmaxf(soo / C - mu2 * mu2, 0.f) + eps);
   T* orow = out + tok * ldo;
-  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int ct = 32 * cw + it * 32 * CS;
+    if (NCT == 0 && ct >= Cp) break;
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
@@ -365,9 +388,14 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = ct + 8 * g + 4 * h;
-      if (c >= C) continue;
+      if (NCT == 0 && c >= C) continue;
       float xv[4], y[4];
-      ld4<T>(xr + c, xv);
+      if constexpr (CACHE) {
+        const bf16x4 t = __builtin_bit_cast(bf16x4, xres[it][g]);
+        xv[0] = (float)t[0]; xv[1] = (float)t[1]; xv[2] = (float)t[2]; xv[3] = (float)t[3];
+      } else {
+        ld4<T>(xr + c, xv);
+      }
       const f32x4 gg = *(const f32x4*)(g2 + c);
 #pragma unroll
       for (int e = 0; e < 4; ++e) y[e] = (o[4 * g + e] - mu2) * rs2 * gg[e] + xv[e];
@@ -384,7 +412,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
 //   (the LN mean correction sum_t mu_t*rs_t*dS_tk' is NOT accumulated here:
 //    it equals (1/C) sum_c R[b][k'][c], the row sums of the R = dS'^T X GEMM)
 // ---------------------------------------------------------------------------
-template <typename T, int CS>
+template <typename T, int CS, int NCT>
 __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, const T* x, int ldx,
                                                         T* dx, int lddx, long long ntok,
                                                         long long P, int C, const T* KtT,
@@ -411,6 +439,34 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
   const T* Vtb = Vt + (long long)b * Cp * KP;
   const T* VtTb = VtT + (long long)b * KP * Cp;
   const T* KtTb = KtT + (long long)b * Cp * KP;
+  constexpr int NIT = NCT > 0 ? NCT : 8;
+  // exact-trip bf16 path: this lane's dy and x channels (16 per tile) are
+  // loaded once, up front, and serve all three passes (one global round trip
+  // instead of one per pass)
+  constexpr bool CACHE = NCT > 0 && NCT <= 4 && sizeof(T) == 2;
+  u32x2 dyc[CACHE ? NCT : 1][4], xcc[CACHE ? NCT : 1][4];
+  if constexpr (CACHE) {
+#pragma unroll
+    for (int it = 0; it < NCT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 32 * cw + it * 32 * CS + 8 * g + 4 * h;
+        dyc[it][g] = *(const u32x2*)(dyr + c);
+        xcc[it][g] = *(const u32x2*)(xr + c);
+      }
+  }
+  auto unpack4 = [](u32x2 q, float* v) {
+    const bf16x4 t = __builtin_bit_cast(bf16x4, q);
+    v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
+  };
+  auto ld_dy = [&](int it, int g, int c, float* v) {
+    if constexpr (CACHE) unpack4(dyc[it][g], v);
+    else ld4<T>(dyr + c, v);
+  };
+  auto ld_x = [&](int it, int g, int c, float* v) {
+    if constexpr (CACHE) unpack4(xcc[it][g], v);
+    else ld4<T>(xr + c, v);
+  };
   const f32x4 st = *(const f32x4*)(stats + tok * 4);
   const float mu = st[0], rs = st[1], mu2 = st[2], rs2 = st[3];
   f32x16 p;
@@ -423,7 +479,10 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
   }
   // ---- pass A: LN_out backward statistics ----
   float m1 = 0.f, m2 = 0.f;
-  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int ct = 32 * cw + it * 32 * CS;
+    if (NCT == 0 && ct >= Cp) break;
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
@@ -431,9 +490,9 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = ct + 8 * g + 4 * h;
-      if (c >= C) continue;
+      if (NCT == 0 && c >= C) continue;
       float dv[4];
-      ld4<T>(dyr + c, dv);
+      ld_dy(it, g, c, dv);
       const f32x4 gg = *(const f32x4*)(g2 + c);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -455,7 +514,10 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
   f32x16 dp;
 #pragma unroll
   for (int e = 0; e < 16; ++e) dp[e] = 0.f;
-  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int ct = 32 * cw + it * 32 * CS;
+    if (NCT == 0 && ct >= Cp) break;
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
@@ -464,13 +526,13 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = ct + 8 * g + 4 * h;
-      if (c >= C) {
+      if (NCT == 0 && c >= C) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) dO[4 * g + e] = 0.f;
         continue;
       }
       float dv[4], w[4];
-      ld4<T>(dyr + c, dv);
+      ld_dy(it, g, c, dv);
       const f32x4 gg = *(const f32x4*)(g2 + c);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -515,7 +577,10 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
   a2 = (a2 + __shfl_xor(a2, 32, 64)) / C;  // mean_c dxhat*xhat
   // ---- pass C: dXhat^T = KtT . dS^T, LN_in backward + residual ----
   T* dxr = dx + tok * lddx;
-  for (int ct = 32 * cw; ct < Cp; ct += 32 * CS) {
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int ct = 32 * cw + it * 32 * CS;
+    if (NCT == 0 && ct >= Cp) break;
     f32x16 dxh;
 #pragma unroll
     for (int e = 0; e < 16; ++e) dxh[e] = 0.f;
@@ -523,10 +588,10 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = ct + 8 * g + 4 * h;
-      if (c >= C) continue;
+      if (NCT == 0 && c >= C) continue;
       float xv[4], dv[4], w[4];
-      ld4<T>(xr + c, xv);
-      ld4<T>(dyr + c, dv);
+      ld_x(it, g, c, xv);
+      ld_dy(it, g, c, dv);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float xh = (xv[e] - mu) * rs;
@@ -847,6 +912,20 @@ static long long xa_split_tiles() {
   return v;
 }
 
+// unrolled channel-loop trips: 32-channel tiles per wave (0 if above 8)
+static int xa_nct(int C, int cs) {
+  const int cp = (C + 31) / 32 * 32;
+  const int n = (cp / 32 + cs - 1) / cs;
+  return n <= 8 ? n : 0;
+}
+// the exact-trip instantiation serves C % 32 == 0 with every wave taking the
+// same number of tiles, a power of two; anything else runs NCT = 0
+static int xa_exact(int C, int cs) {
+  const int n = xa_nct(C, cs);
+  const bool ok = C % 32 == 0 && (C / 32) % cs == 0 && (n == 1 || n == 2 || n == 4 || n == 8);
+  return ok ? n : 0;
+}
+
 extern "C" int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ldo, long long ntok,
                             long long P, int C, const void* Kt, const void* Vt,
                             const float* colsum, const float* g2, float eps, float* stats,
@@ -859,13 +938,27 @@ extern "C" int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ld
   const long long tiles = (ntok / P) * ((P + 31) / 32);
   const bool split = tiles < xa_split_tiles() && C >= 128;  // fewer than 256 four-wave workgroups otherwise
   const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
-  if (dtype == DV_BF16) {
-    if (split) xattn_fwd_kernel<bf16, 4><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (bf16*)out, ldo, ntok, P, C, (const bf16*)Kt, (const bf16*)Vt, colsum, g2, eps, stats, (bf16*)pbuf);
-    else xattn_fwd_kernel<bf16, 1><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (bf16*)out, ldo, ntok, P, C, (const bf16*)Kt, (const bf16*)Vt, colsum, g2, eps, stats, (bf16*)pbuf);
-  } else {
-    if (split) xattn_fwd_kernel<float, 4><<<blocks, 256, 0, st>>>((const float*)x, ldx, (float*)out, ldo, ntok, P, C, (const float*)Kt, (const float*)Vt, colsum, g2, eps, stats, (float*)pbuf);
-    else xattn_fwd_kernel<float, 1><<<blocks, 256, 0, st>>>((const float*)x, ldx, (float*)out, ldo, ntok, P, C, (const float*)Kt, (const float*)Vt, colsum, g2, eps, stats, (float*)pbuf);
+  const int nct = xa_nct(C, split ? 4 : 1), ex = xa_exact(C, split ? 4 : 1);
+  DV_REQUIRE(nct > 0, "C too large for the channel loop (Cp / (32 * CS) <= 8)");
+#define XF_LAUNCH(T, CS, N)                                                                         \
+  xattn_fwd_kernel<T, CS, N><<<blocks, 256, 0, st>>>((const T*)x, ldx, (T*)out, ldo, ntok, P, C,  \
+                                                     (const T*)Kt, (const T*)Vt, colsum, g2, eps,  \
+                                                     stats, (T*)pbuf)
+#define XF_DISPATCH(T)                                                                 \
+  switch ((split ? 16 : 0) + ex) {                                                     \
+    case 1: XF_LAUNCH(T, 1, 1); break;  case 2: XF_LAUNCH(T, 1, 2); break;             \
+    case 4: XF_LAUNCH(T, 1, 4); break;  case 8: XF_LAUNCH(T, 1, 8); break;             \
+    case 17: XF_LAUNCH(T, 4, 1); break; case 18: XF_LAUNCH(T, 4, 2); break;            \
+    case 20: XF_LAUNCH(T, 4, 4); break; case 24: XF_LAUNCH(T, 4, 8); break;            \
+    default: if (split) XF_LAUNCH(T, 4, 0); else XF_LAUNCH(T, 1, 0); break;            \
   }
+  if (dtype == DV_BF16) {
+    XF_DISPATCH(bf16);
+  } else {
+    XF_DISPATCH(float);
+  }
+#undef XF_LAUNCH
+#undef XF_DISPATCH
   return check_launch("xattn_fwd");
 }
 
@@ -884,13 +977,24 @@ extern "C" int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const vo
   const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
 #define XB_ARGS(T) (const T*)dy, lddy, (const T*)x, ldx, (T*)dx, lddx, ntok, P, C, (const T*)KtT, \
     (const T*)Vt, (const T*)VtT, colsum, g2, stats, (const T*)pbuf, (T*)dobuf, (T*)dsbuf, (T*)p2buf
-  if (dtype == DV_BF16) {
-    if (split) xattn_bwd_kernel<bf16, 4><<<blocks, 256, 0, st>>>(XB_ARGS(bf16));
-    else xattn_bwd_kernel<bf16, 1><<<blocks, 256, 0, st>>>(XB_ARGS(bf16));
-  } else {
-    if (split) xattn_bwd_kernel<float, 4><<<blocks, 256, 0, st>>>(XB_ARGS(float));
-    else xattn_bwd_kernel<float, 1><<<blocks, 256, 0, st>>>(XB_ARGS(float));
+  const int nct = xa_nct(C, split ? 4 : 1), ex = xa_exact(C, split ? 4 : 1);
+  DV_REQUIRE(nct > 0, "C too large for the channel loop (Cp / (32 * CS) <= 8)");
+#define XB_LAUNCH(T, CS, N) xattn_bwd_kernel<T, CS, N><<<blocks, 256, 0, st>>>(XB_ARGS(T))
+#define XB_DISPATCH(T)                                                                 \
+  switch ((split ? 16 : 0) + ex) {                                                     \
+    case 1: XB_LAUNCH(T, 1, 1); break;  case 2: XB_LAUNCH(T, 1, 2); break;             \
+    case 4: XB_LAUNCH(T, 1, 4); break;  case 8: XB_LAUNCH(T, 1, 8); break;             \
+    case 17: XB_LAUNCH(T, 4, 1); break; case 18: XB_LAUNCH(T, 4, 2); break;            \
+    case 20: XB_LAUNCH(T, 4, 4); break; case 24: XB_LAUNCH(T, 4, 8); break;            \
+    default: if (split) XB_LAUNCH(T, 4, 0); else XB_LAUNCH(T, 1, 0); break;            \
   }
+  if (dtype == DV_BF16) {
+    XB_DISPATCH(bf16);
+  } else {
+    XB_DISPATCH(float);
+  }
+#undef XB_LAUNCH
+#undef XB_DISPATCH
 #undef XB_ARGS
   return check_launch("xattn_bwd_tokens");
 }

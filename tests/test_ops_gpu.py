@@ -121,7 +121,8 @@ def _ref_cross_attention(x_tok, ctx, g1, null_kv, wq, wkv, wo, g2, eps):
 
 @pytest.mark.parametrize("dtype,tol", DTYPES)
 @pytest.mark.parametrize("C,T,H", [(64, 2, 8), (256, 2, 8), (16, 2, 4), (8, 2, 2), (48, 3, 3),
-                                   (512, 2, 8), (192, 2, 8), (128, 4, 16)])  # C >= 128: channel-split waves
+                                   (512, 2, 8), (192, 2, 8), (128, 4, 16), (32, 2, 8),
+                                   (128, 16, 32)])  # C >= 128: channel-split waves below 1024 token tiles
 def test_cross_attention(dtype, tol, C, T, H):
     # (16,2,4), (8,2,2), (48,3,3): channel counts below / not a multiple of one
     # 32-channel MFMA tile and tokens per clip (T*H*W) not a multiple of 32
