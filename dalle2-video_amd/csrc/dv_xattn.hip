@@ -74,6 +74,27 @@ __device__ f32x16 mm_acc_g<bf16>(const bf16* A, int lda, const f32x16& X, f32x16
   }
   return acc;
 }
+// mm_acc_g<bf16> split into its A-fragment loads and the MFMAs, so a kernel
+// can issue the loads early and reuse the fragments
+__device__ __forceinline__ void ld_afrag(const bf16* A, int lda, int r, int h, u32x4 (&a)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const u32x2 lo = *(const u32x2*)(A + (long long)r * lda + 16 * s + 4 * h);
+    const u32x2 hi = *(const u32x2*)(A + (long long)r * lda + 16 * s + 8 + 4 * h);
+    a[s] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+  }
+}
+__device__ __forceinline__ f32x16 mm_acc_f(const u32x4 (&a)[2], const f32x16& X, f32x16 acc) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 bx;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bx[j] = (bf16)X[8 * s + j];
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[s]), bx, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
 template <>
 __device__ f32x16 mm_acc_g<float>(const float* A, int lda, const f32x16& X, f32x16 acc, int r, int h) {
 #pragma unroll
@@ -288,11 +309,14 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
   // up front with the pass-1 reads of the same lines (no second round trip)
   constexpr bool CACHE = NCT > 0 && NCT <= 4 && sizeof(T) == 2;
   u32x2 xres[CACHE ? NCT : 1][4];
+  u32x4 vfr[CACHE ? NCT : 1][2];  // V~ fragments of passes 2 and 3
   if constexpr (CACHE) {
 #pragma unroll
-    for (int it = 0; it < NCT; ++it)
+    for (int it = 0; it < NCT; ++it) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) xres[it][g] = *(const u32x2*)(xr + 32 * cw + it * 32 * CS + 8 * g + 4 * h);
+      ld_afrag((const bf16*)(Vtb + (long long)(32 * cw + it * 32 * CS) * KP), KP, r, h, vfr[it]);
+    }
   }
   // ---- scores: S^T = Kt . X^T over raw x, LN stats in the same pass ----
   f32x16 acc;
@@ -362,7 +386,8 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
-    o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
+    if constexpr (CACHE) o = mm_acc_f(vfr[it], p, o);
+    else o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
 #pragma unroll
     for (int e = 0; e < 16; ++e) { so += o[e]; soo += o[e] * o[e]; }
   }
@@ -384,7 +409,8 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
-    o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
+    if constexpr (CACHE) o = mm_acc_f(vfr[it], p, o);
+    else o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = ct + 8 * g + 4 * h;
@@ -445,15 +471,18 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
   // instead of one per pass)
   constexpr bool CACHE = NCT > 0 && NCT <= 4 && sizeof(T) == 2;
   u32x2 dyc[CACHE ? NCT : 1][4], xcc[CACHE ? NCT : 1][4];
+  u32x4 vfr[CACHE ? NCT : 1][2];  // V~ fragments of passes A and B
   if constexpr (CACHE) {
 #pragma unroll
-    for (int it = 0; it < NCT; ++it)
+    for (int it = 0; it < NCT; ++it) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = 32 * cw + it * 32 * CS + 8 * g + 4 * h;
         dyc[it][g] = *(const u32x2*)(dyr + c);
         xcc[it][g] = *(const u32x2*)(xr + c);
       }
+      ld_afrag((const bf16*)(Vtb + (long long)(32 * cw + it * 32 * CS) * KP), KP, r, h, vfr[it]);
+    }
   }
   auto unpack4 = [](u32x2 q, float* v) {
     const bf16x4 t = __builtin_bit_cast(bf16x4, q);
@@ -486,7 +515,8 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
-    o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
+    if constexpr (CACHE) o = mm_acc_f(vfr[it], p, o);
+    else o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = ct + 8 * g + 4 * h;
@@ -521,7 +551,8 @@ __global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, c
     f32x16 o;
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[e] = 0.f;
-    o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
+    if constexpr (CACHE) o = mm_acc_f(vfr[it], p, o);
+    else o = mm_acc_g<T>(Vtb + (long long)ct * KP, KP, p, o, r, h);
     f32x16 dO;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
