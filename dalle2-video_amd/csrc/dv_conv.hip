@@ -528,6 +528,163 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p,
 }
 
 // ---------------------------------------------------------------------------
+// bf16 1x1 convolution with K = 64 * KT <= 128 input channels and cout = BN
+// (64 or 128): the res_conv / skip 1x1s of the 64x64 stage and their dgrads
+// (accumulated into the shared dX).  HBM-bound (≈ 85-170 flop/B), so the
+// shape of the glds kernel — one tile per workgroup, load / compute / store
+// in sequence — leaves the memory idle between phases.  Here a persistent
+// workgroup keeps the weights LDS-resident, streams 128-pixel tiles through
+// an NB-deep LDS-DMA ring (NB - 1 tiles in flight) and prefetches the next
+// tile's residual into registers while this tile computes; one counted
+// vmcnt per tile, every DMA issued unconditionally (tiles past the end read
+// the zero line) so the count is a constant.
+// 8 waves = 4 pixel groups of 32 x 2 channel halves of BN / 2.
+// ---------------------------------------------------------------------------
+template <int BN, int KT, int NB, bool RES>
+__global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p, int ntiles) {
+  constexpr int BM = 128;
+  constexpr int XT = BM * 128 * KT;  // one pixel tile: KT 64-channel blocks of 128-B rows
+  constexpr int WBYTES = BN * 128 * KT;
+  constexpr int TJ = BN / 64;        // 32-channel MFMA tiles per wave
+  constexpr int XD = 2 * KT;         // X-tile DMA instructions per thread (64 rows per round)
+  constexpr int WD = BN * KT / 64;   // weight DMA instructions per thread
+  constexpr int RL = RES ? 4 * TJ : 0;  // residual loads per thread per tile
+  __shared__ __attribute__((aligned(1024))) char smem[WBYTES + NB * XT];
+  char* sW = smem;
+  char* sX = smem + WBYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int chunk = lane & 7, rrow = tid >> 3;  // DMA slot: row rrow (0..63) of a round, 16-B chunk
+  const bf16* zero = (const bf16*)g_zero_line;
+
+  auto issue_x = [&](int t, int buf) {  // tile t (>= ntiles: zeros) into ring slot buf
+    const long long m0 = (long long)t * BM;
+#pragma unroll
+    for (int i = 0; i < XD; ++i) {
+      const int kb = i / 2, row = 64 * (i % 2) + rrow;
+      const int cs = chunk ^ swz8(row);
+      const long long m = m0 + row;
+      const bool first = kb * 64 < p.c0;
+      const bf16* src = (t < ntiles && m < p.M)
+                            ? (first ? p.x0 + m * p.ld0 + kb * 64 : p.x1 + m * p.ld1 + (kb * 64 - p.c0)) + cs * 8
+                            : zero;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(sX + buf * XT + kb * (BM * 128) +
+                                                                               (64 * (i % 2) + 8 * wave) * 128),
+                                       16, 0, 0);
+    }
+  };
+  // residual of this lane's outputs (pixel row r of group wm, channels n0 + 8g + 4h .. +3)
+  u32x2 rcur[RES ? 4 * TJ : 1], rnxt[RES ? 4 * TJ : 1];
+  auto load_res = [&](int t, u32x2 (&dst)[RES ? 4 * TJ : 1]) {
+    if constexpr (RES) {
+      long long m = (long long)t * BM + wm * 32 + r;
+      if (t >= ntiles || m >= p.M) m = 0;  // a valid address; the value is not stored
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = wn * (BN / 2) + 32 * j + 8 * g + 4 * h;
+          dst[4 * j + g] = *(const u32x2*)(p.res + m * p.ldres + n);
+        }
+    }
+  };
+
+  // ---- prologue: weights, NB - 1 tiles, the first residual ----
+#pragma unroll
+  for (int i = 0; i < WD; ++i) {
+    const int q = i * 512 + tid;  // 16-B chunk index over [kb][co][8]
+    const int kb = q / (BN * 8), rem = q - kb * BN * 8;
+    const int co = rem >> 3, c = rem & 7;
+    const bf16* src = p.w + (long long)co * p.K + kb * 64 + ((c ^ swz8(co)) << 3);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(sW + (long long)(i * 512 + 64 * wave) * 16),
+                                     16, 0, 0);
+  }
+  // issue order (vmcnt is in order): prologue W, X(0 .. NB-3), res(0), X(NB-2);
+  // iteration k: res(k+1), X(k+NB-1).  After res(k) come exactly X(k+NB-2),
+  // res(k+1), X(k+NB-1), so vmcnt(2 XD + RL) means res(k) — and X(k), issued
+  // before it (NB >= 3) — landed, with two X tiles still in flight.
+  static_assert(NB >= 3, "the ring needs two tiles in flight");
+  int t = blockIdx.x;
+#pragma unroll
+  for (int i = 0; i < NB - 2; ++i) issue_x(t + i * (int)gridDim.x, i);
+  load_res(t, rcur);
+  issue_x(t + (NB - 2) * (int)gridDim.x, NB - 2);
+
+  float bias[TJ][4][4];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = wn * (BN / 2) + 32 * j + 8 * g + 4 * h + e;
+        bias[j][g][e] = p.bias ? p.bias[n] : 0.f;
+      }
+
+  for (int it = 0; t < ntiles; ++it, t += gridDim.x) {
+    const int buf = it % NB;
+    load_res(t + (int)gridDim.x, rnxt);
+    issue_x(t + (NB - 1) * (int)gridDim.x, (it + NB - 1) % NB);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * XD + RL) : "memory");
+    __builtin_amdgcn_s_barrier();
+    f32x16 acc[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    const char* xs = sX + buf * XT;
+#pragma unroll
+    for (int kb = 0; kb < KT; ++kb)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int c = 2 * s + h;
+        const int xrow = wm * 32 + r;
+        const u32x4 xb = *(const u32x4*)(xs + kb * (BM * 128) + xrow * 128 + ((c ^ swz8(xrow)) << 4));
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int wrow = wn * (BN / 2) + 32 * j + r;
+          const u32x4 wa = *(const u32x4*)(sW + kb * (BN * 128) + wrow * 128 + ((c ^ swz8(wrow)) << 4));
+          acc[j] = Mma<bf16>::run(wa, xb, acc[j]);
+        }
+      }
+    // epilogue: D[co][px] — lane: pixel r, channels 8g + 4h + e of each 32-channel tile
+    const long long m = (long long)t * BM + wm * 32 + r;
+    if (m < p.M) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = wn * (BN / 2) + 32 * j + 8 * g + 4 * h;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = acc[j][4 * g + e] + bias[j][g][e];
+            if (p.act == DV_ACT_SILU) v[e] = silu_f(v[e]);
+          }
+          if constexpr (RES) {
+            const bf16x4 rv = __builtin_bit_cast(bf16x4, rcur[4 * j + g]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+          }
+          store4<bf16>(p.y + m * p.ldy + n, v);
+        }
+    }
+    if constexpr (RES) {
+#pragma unroll
+      for (int q = 0; q < 4 * TJ; ++q) rcur[q] = rnxt[q];
+    }
+    // every wave's reads of `buf` are done before the next iteration re-fills it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing DMAs (zero line) drain
+}
+
+// ---------------------------------------------------------------------------
 // wgrad
 // ---------------------------------------------------------------------------
 template <typename T>
@@ -1162,6 +1319,28 @@ int launch_fwd(const ConvFwdArgs<T>& a, hipStream_t st) {
   if (a.gn_sums) conv_fwd_kernel<T, BM, BN, true><<<grid, 256, 0, st>>>(a);
   else conv_fwd_kernel<T, BM, BN, false><<<grid, 256, 0, st>>>(a);
   return check_launch("conv_fwd");
+}
+
+// the 1x1 streaming kernel's shapes (see conv1x1_stream_kernel)
+bool conv1x1_ok(const ConvFwdArgs<bf16>& a, bool split) {
+  static const bool off = getenv("DV_NO_1X1") != nullptr;  // A/B switch
+  return !off && a.ks == 1 && (a.cin == 64 || a.cin == 128) && (!split || a.c0 == 64) &&
+         (a.cout == 64 || a.cout == 128) && a.gn_sums == nullptr && (a.ldy & 3) == 0 &&
+         (a.res == nullptr || (a.ldres & 3) == 0) && (a.ld0 & 7) == 0 && (!split || (a.ld1 & 7) == 0) &&
+         a.M * std::max(a.ld0, split ? a.ld1 : 0) < (1ll << 31) &&
+         a.M * std::max(a.ldy, a.res ? a.ldres : 0) < (1ll << 31);
+}
+
+template <int BN, int KT>
+int launch_conv1x1(const ConvFwdArgs<bf16>& a, hipStream_t st) {
+  constexpr int NB = 3;
+  constexpr int LDS = BN * 128 * KT + NB * 128 * 128 * KT;
+  constexpr int PER_CU = (160 * 1024) / LDS;
+  const int ntiles = (int)((a.M + 127) / 128);
+  const int grid = std::min(ntiles, 256 * PER_CU);
+  if (a.res) conv1x1_stream_kernel<BN, KT, NB, true><<<grid, 512, 0, st>>>(a, ntiles);
+  else conv1x1_stream_kernel<BN, KT, NB, false><<<grid, 512, 0, st>>>(a, ntiles);
+  return check_launch("conv1x1_stream");
 }
 
 template <int BM, int BN>
@@ -1873,6 +2052,10 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
         fwd_stripe2_ok(a.M, h, wd, cin, a.c0, x1 != nullptr, cout, ks, seg, nseg) &&
         a.M * std::max(ld0, x1 ? ld1 : 0) < (1ll << 31))
       return launch_fwd_stripe2(a, seg, nseg, st);
+    if (conv1x1_ok(a, x1 != nullptr)) {
+      if (cout == 64) return cin == 64 ? launch_conv1x1<64, 1>(a, st) : launch_conv1x1<64, 2>(a, st);
+      return cin == 64 ? launch_conv1x1<128, 1>(a, st) : launch_conv1x1<128, 2>(a, st);
+    }
     const long long maxld = ld0 > (x1 ? ld1 : 0) ? ld0 : ld1;
     if (cin % 64 == 0 && a.c0 % 64 == 0 && a.M * maxld < (1ll << 31)) {
       int bm, bn;

@@ -92,6 +92,9 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0):
             and m % 128 == 0 and m * maxld < (1 << 31) and _stripe_geom_ok(h, w)
             and (w == 8 or (w == 16 and cin * cout <= 256 * 256))):
         return f"conv_fwd_stripe2_kernel<{w}>"
+    if (dtype_name == "bf16" and ks == 1 and cin in (64, 128) and c0 in (cin, 64) and cout in (64, 128)
+            and gn_P == 0 and m * maxld < (1 << 31) and not _NO_1X1):
+        return f"conv1x1_stream_kernel<{cout},{cin // 64}>"
     if dtype_name == "bf16" and cin % 64 == 0 and c0 % 64 == 0 and m * maxld < (1 << 31):
         bn = 64 if cout <= 64 else 128
         bm = 256 if bn == 64 else 128
@@ -108,6 +111,7 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0):
     return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"
 
 
+_NO_1X1 = bool(os.environ.get("DV_NO_1X1"))  # A/B switch: 1x1 convs on the glds kernel
 _NO_WINDOW = bool(os.environ.get("DV_NO_WINDOW"))  # A/B switch: 3x3 convs on dv_conv_fwd only
 # measured (tools/kbench.py fwd): the window form wins at 8x8 and 16x16, the glds /
 # stripe kernels at 32x32 and 64x64
@@ -231,6 +235,9 @@ class _WgradDefer:
     reused by the captured one)."""
 
     CHUNK_FLOATS = 1 << 27  # 512 MB arena chunks (kept for the process: graphs hold their addresses)
+    # flush once this many partial bytes are pending (0 = only at the end of
+    # the pass): a smaller batch is read back while still in the 256 MB MALL
+    FLUSH_BYTES = int(os.environ.get("DV_DEFER_MB", "0")) << 20
 
     def __init__(self):
         self.active = 0
@@ -257,6 +264,9 @@ class _WgradDefer:
         self.targets.add(entry.dw)
         if entry.db:
             self.targets.add(entry.db)
+        self.pending_bytes = getattr(self, "pending_bytes", 0) + 16 * entry.S * entry.n4
+        if self.FLUSH_BYTES and self.pending_bytes >= self.FLUSH_BYTES:
+            self.flush()
 
     def conflicts(self, *ptrs):
         return any(p is not None and p in self.targets for p in ptrs)
@@ -282,11 +292,13 @@ class _WgradDefer:
         call("dv_wgrad_reduce_batched", ptr(tab), n, blocks, stream())
         self.pending.clear()
         self.targets.clear()
+        self.pending_bytes = 0
         self.cursor = (0, 0)
 
     def discard(self):
         self.pending.clear()
         self.targets.clear()
+        self.pending_bytes = 0
         self.cursor = (0, 0)
 
 
