@@ -1193,6 +1193,26 @@ constexpr int PACK_LDS = 8192;   // floats: the largest row / column group accep
 constexpr int PACK_TILE = 8192;  // floats staged per tile (several rows when they are small)
 constexpr int PACK_CB = 64;      // dgrad tiles: output columns (co) per tile
 
+// n contiguous floats -> LDS: 16-B loads (when the source is 16-B aligned),
+// 4 in flight per lane
+__device__ __forceinline__ void pack_stage(const float* src, float* sm, int n) {
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    const int n4 = n >> 2;
+    for (int i0 = threadIdx.x; i0 < n4; i0 += 1024) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + 256 * u < n4) v[u] = ((const f32x4*)src)[i0 + 256 * u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + 256 * u < n4) ((f32x4*)sm)[i0 + 256 * u] = v[u];
+    }
+    for (int i = 4 * n4 + threadIdx.x; i < n; i += 256) sm[i] = src[i];
+  } else {
+    for (int i = threadIdx.x; i < n; i += 256) sm[i] = src[i];
+  }
+}
+
 __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
   const int taps = e.taps, cin = e.cin, cout = e.cout, pad = e.pad_to;
   const bool fwd = (e.mode & 1) == 0, chunked = (e.mode & 2) != 0;
@@ -1204,7 +1224,7 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
     if (rt < 1) rt = 1;
     const int co0 = tile * rt, rn = min(rt, cout - co0);
     const float* src = e.w + (long long)co0 * row;  // rn consecutive rows: contiguous
-    for (int i = threadIdx.x; i < rn * row; i += 256) sm[i] = src[i];
+    pack_stage(src, sm, rn * row);
     __syncthreads();
     const int orow = taps * pad;
     const long long ob = (long long)co0 * orow;
@@ -1240,9 +1260,18 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
     const int cn = min(ci_t, cin - ci0);
     const int con = max(0, min(PACK_CB, cout - co0));  // real co rows (0 in the pad-only tail)
     const int seg = cn * taps;
-    for (int i = threadIdx.x; i < con * seg; i += 256) {
-      const int r = i / seg, j = i - r * seg;
-      sm[i] = e.w[((long long)(co0 + r) * cin + ci0) * taps + j];
+    // 4 loads in flight per lane (the rows' segments are not 16-B aligned)
+    for (int i0 = threadIdx.x; i0 < con * seg; i0 += 1024) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 256 * u;
+        const int r = i / seg, j = i - r * seg;
+        v[u] = i < con * seg ? e.w[((long long)(co0 + r) * cin + ci0) * taps + j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + 256 * u < con * seg) sm[i0 + 256 * u] = v[u];
     }
     __syncthreads();
     const int cw = min(PACK_CB, pad - co0);  // columns of this tile
@@ -1286,13 +1315,13 @@ __device__ __forceinline__ int pack_tiles(const DvPackEntry& e) {
 }
 
 __global__ __launch_bounds__(256) void pack_weight_kernel(DvPackEntry e) {
-  __shared__ float sm[PACK_LDS];  // one row may need up to PACK_LDS floats
+  __shared__ __attribute__((aligned(16))) float sm[PACK_LDS];  // one row may need up to PACK_LDS floats
   for (int t = blockIdx.x; t < pack_tiles(e); t += gridDim.x) pack_tile(e, t, sm);
 }
 
 // many weights in one launch: blockIdx.y selects the table entry
 __global__ __launch_bounds__(256) void pack_weight_batched_kernel(const DvPackEntry* table) {
-  __shared__ float sm[PACK_LDS];
+  __shared__ __attribute__((aligned(16))) float sm[PACK_LDS];
   const DvPackEntry e = table[blockIdx.y];
   for (int t = blockIdx.x; t < pack_tiles(e); t += gridDim.x) pack_tile(e, t, sm);
 }
@@ -2340,7 +2369,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
     __syncthreads();
   }
   // ---- torch-layout output [co][ci][tap]: each wave's 32 x 32 x 9 tile is
-  // transposed through LDS (two waves at a time, 36 KB each) so every output
+  // transposed through LDS (two tiles per round, 36 KB each) so every output
   // channel's 32 ci x 9 taps go out as 1152 contiguous bytes (float4 stores).
   // One split writes the gradient itself (accumulate honoured); several
   // splits write partials that wgrad_reduce4_kernel sums. ----
@@ -2362,15 +2391,16 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
         }
     }
     __syncthreads();
-    if (half == 0 && wm == rnd) {
-      const long long rowbase = (long long)(co0 + wm * 32) * a.K + (ci0 + wn * 32) * NT;
-      for (int idx = lane; idx < 32 * (TP / 4); idx += 64) {
-        const int col = idx / (TP / 4), j = idx - col * (TP / 4);
-        f32x4 v = *(const f32x4*)(tile + col * TP + 4 * j);
-        f32x4* o = (f32x4*)(dst + rowbase + (long long)col * a.K + 4 * j);
-        if (acc_o) v += *o;
-        *o = v;
-      }
+    // all 8 waves store the round's two tiles (the store phase is
+    // issue-bound: two storing waves left it at ~40 % of a small wgrad's time)
+    for (int idx = threadIdx.x; idx < 2 * 32 * (TP / 4); idx += 512) {
+      const int t2 = idx / (32 * (TP / 4)), rem = idx - t2 * (32 * (TP / 4));
+      const int col = rem / (TP / 4), j = rem - col * (TP / 4);
+      f32x4 v = *(const f32x4*)(red + t2 * (32 * TP) + col * TP + 4 * j);
+      const long long rowbase = (long long)(co0 + rnd * 32) * a.K + (ci0 + t2 * 32) * NT;
+      f32x4* o = (f32x4*)(dst + rowbase + (long long)col * a.K + 4 * j);
+      if (acc_o) v += *o;
+      *o = v;
     }
     __syncthreads();
   }
