@@ -309,10 +309,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DV_DIST_BACKEND=gloo + DV_SHARE_GPU=1: rehearse the N-rank path with every
+    # rank on the same GPU (a one-GPU box cannot run RCCL ranks); the driver's
+    # multi-GPU runs use the defaults (RCCL, one GPU per rank)
+    backend = os.environ.get("DV_DIST_BACKEND", "nccl")
+    if os.environ.get("DV_SHARE_GPU") == "1":
+        local = local % torch.cuda.device_count()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.manual_seed(1234 + rank)
 
