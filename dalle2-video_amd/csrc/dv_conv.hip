@@ -2228,8 +2228,10 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   const int l4 = lane >> 2, c4 = lane & 3;
   const bf16* a_src = a.dy + co0 + 8 * c4;
   const bool first = ci0 < a.c0;
-  const bf16* b_src = (first ? a.x0 + ci0 : a.x1 + (ci0 - a.c0)) + 8 * c4;
   const int xld = first ? a.ld0 : a.ld1;
+  const int b_c = (first ? ci0 : ci0 - a.c0) + 8 * c4;  // this lane's channel in its source
+  const __amdgpu_buffer_rsrc_t xrs =
+      dma_rsrc(first ? a.x0 : a.x1, (unsigned)((long long)a.nstages * 128 * xld * 2));
   int b_off[NRH], b_ry[NRH];  // b_ry: image-row offset, or a large negative for halo / junk rows
 #pragma unroll
   for (int i = 0; i < NRH; ++i) {
@@ -2261,12 +2263,12 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
 #pragma unroll
     for (int i = 0; i < NRH; ++i) {
       const bool in = KS == 1 || (unsigned)(y0 + b_ry[i]) < (unsigned)a.H;
-      const bf16* src = in ? b_src + (long long)(m0 + b_off[i]) * xld : zero;
+      // halo / pad rows load out of the raw buffer's range: 16 zero bytes
+      // without a memory access (a shared zero line is one hot L2 channel)
+      const unsigned voff = in ? (unsigned)(((m0 + b_off[i]) * xld + b_c) * 2) : DMA_OOB;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(in ? src + 32 * hh : zero),
-                                         (__attribute__((address_space(3))) void*)(sB + hh * BHALF + (128 * i + 16 * wave) * 64),
-                                         16, 0, 0);
+        dma16(xrs, sB + hh * BHALF + (128 * i + 16 * wave) * 64, in ? voff + 64 * hh : DMA_OOB);
     }
   };
 
@@ -2555,11 +2557,13 @@ bool stripe_geom(int h, int w, int& seg, int& nseg) {
   return nseg * (h + 2) * (w + 2) <= (w == 8 ? 200 : (128 / w + 2) * (w + 2));
 }
 
-bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout, int ks) {
+bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout, int ks,
+                     long long maxld = 0) {
   int seg, nseg;
   if ((ks != 3 && ks != 1) || cin % 64 || cout % 64 || (split && c0 % 64)) return false;
   const long long M = (long long)nf * h * w;
   if (M % 128 || M >= (1ll << 31)) return false;
+  if (M * maxld * 2 >= (long long)DMA_OOB) return false;  // the window's raw-buffer resource
   return ks == 1 || stripe_geom(h, w, seg, nseg);
 }
 
@@ -2702,7 +2706,7 @@ static int conv_wgrad_impl(int dtype, const void* dy, int lddy, const void* x0, 
   hipStream_t st = (hipStream_t)stream;
   if ((long long)nf * h * w == 0) return DV_OK;
   if (dtype == DV_BF16 && cout_real == cout && cin_real == cin &&
-      wgrad_stripe_ok(nf, h, w, cin, c0, x1 != nullptr, cout, ksize))
+      wgrad_stripe_ok(nf, h, w, cin, c0, x1 != nullptr, cout, ksize, std::max(ld0, x1 ? ld1 : 0)))
     return conv_wgrad_stripe(dy, lddy, x0, ld0, c0, x1, ld1, ws, dw, accumulate_w, db, accumulate_b,
                              nf, h, w, cin, cout, ksize, st, defer);
   // general path: f32 atomics into the zeroed packed workspace, then one reduce
