@@ -428,16 +428,27 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p,
     b_x[i] = rem - y * p.W;
     b_pix[i] = mi;
   }
-  const bf16* zero = (const bf16*)g_zero_line;
   const int a_rowoff = (tid >> 3);
+  // per-workgroup raw buffers over the pixels any tap of this tile can read
+  // and over this tile's weight rows: out-of-image taps, tail pixels and rows
+  // past cout load out of range (zeros without a memory access) instead of
+  // all hitting one shared zero line (a hot L2 channel)
+  const int reach = pad * p.W + pad;
+  const long long plo = m0 - reach > 0 ? m0 - reach : 0;
+  const long long phi = m0 + BM + reach < p.M ? m0 + BM + reach : p.M;
+  const __amdgpu_buffer_rsrc_t xr0 = dma_rsrc(p.x0 + plo * p.ld0, (unsigned)((phi - plo) * p.ld0 * 2));
+  const __amdgpu_buffer_rsrc_t xr1 = dma_rsrc(p.x1 + plo * p.ld1, (unsigned)((phi - plo) * p.ld1 * 2));
+  const int nrows = p.cout - n0 < BN ? p.cout - n0 : BN;
+  const __amdgpu_buffer_rsrc_t wr = dma_rsrc(p.w + (long long)n0 * p.K, (unsigned)(nrows * p.K * 2));
+  const int poff = (int)(-plo);
 
   auto issue = [&](int kt, int buf) {
     const int tap = kt / cblocks;
     const int ci = ((kt - tap * cblocks) << 6);
     const int dy = tap / p.ks - pad, dx = tap % p.ks - pad;
-    const int doff = dy * p.W + dx;
+    const int doff = dy * p.W + dx + poff;
     const bool first = ci < p.c0;  // wave-uniform: the 64-channel block never straddles c0
-    const bf16* xb = first ? p.x0 + ci : p.x1 + (ci - p.c0);
+    const int cof = first ? ci : ci - p.c0;
     const int ld = first ? p.ld0 : p.ld1;
     char* sB = smem + buf * BUF;
     char* sA = sB + BM * 128;
@@ -447,20 +458,14 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p,
       const int cs = chunk ^ swz8(row);
       const int yy = b_y[i] + dy, xx = b_x[i] + dx;
       const bool in = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-      const bf16* src = in ? xb + ((b_pix[i] + doff) * ld + cs * 8) : zero;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(sB + (32 * i + 8 * wave) * 128),
-                                       16, 0, 0);
+      const unsigned voff = in ? (unsigned)(((b_pix[i] + doff) * ld + cof + cs * 8) * 2) : DMA_OOB;
+      dma16(first ? xr0 : xr1, sB + (32 * i + 8 * wave) * 128, voff);
     }
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int row = 32 * i + a_rowoff;
       const int cs = chunk ^ swz8(row);
-      const int n = n0 + row;
-      const bf16* src = n < p.cout ? p.w + ((long long)n * p.K + (kt << 6) + cs * 8) : zero;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(sA + (32 * i + 8 * wave) * 128),
-                                       16, 0, 0);
+      dma16(wr, sA + (32 * i + 8 * wave) * 128, (unsigned)((row * p.K + (kt << 6) + cs * 8) * 2));
     }
   };
 
