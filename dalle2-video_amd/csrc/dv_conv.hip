@@ -385,6 +385,13 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs<T> p) {
 // im2col halos and all cout tiles of a pixel tile share that XCD's L2).
 // ---------------------------------------------------------------------------
 __device__ __attribute__((aligned(64))) unsigned int g_zero_line[16];
+// 16 KB of zeros: DMA lanes that must load zeros from a real address (two
+// sources per wave, no single raw buffer) spread over 1,024 16-B lines, i.e.
+// over every L2 channel, instead of all hitting one line
+__device__ __attribute__((aligned(64))) unsigned int g_zero_buf[4096];
+__device__ __forceinline__ const bf16* zero_src(unsigned salt) {
+  return (const bf16*)(g_zero_buf + (salt & 1023u) * 4);
+}
 
 __device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
 
@@ -562,7 +569,6 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
   const int wm = wave >> 1, wn = wave & 1;
   const int r = lane & 31, h = lane >> 5;
   const int chunk = lane & 7, rrow = tid >> 3;  // DMA slot: row rrow (0..63) of a round, 16-B chunk
-  const bf16* zero = (const bf16*)g_zero_line;
 
   auto issue_x = [&](int t, int buf) {  // tile t (>= ntiles: zeros) into ring slot buf
     const long long m0 = (long long)t * BM;
@@ -574,7 +580,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
       const bool first = kb * 64 < p.c0;
       const bf16* src = (t < ntiles && m < p.M)
                             ? (first ? p.x0 + m * p.ld0 + kb * 64 : p.x1 + m * p.ld1 + (kb * 64 - p.c0)) + cs * 8
-                            : zero;
+                            : zero_src(tid + 97u * blockIdx.x + 31u * i);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sX + buf * XT + kb * (BM * 128) +
                                                                                (64 * (i % 2) + 8 * wave) * 128),
@@ -980,7 +986,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
     pend = min(pbeg + p.pix_per_split, p.M);
   }
   const int pad = p.ks >> 1;
-  const bf16* zero = (const bf16*)g_zero_line;
 
   // A: this lane's fixed chunk column (channels co0 + 8*cha .. +7)
   const int a_lrow = lane / (RA / 16), a_slot = lane % (RA / 16);
@@ -1013,7 +1018,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
     for (int i = 0; i < GA; ++i) {
       const int row = (4 * i + wave) * RPI_A + a_lrow;
       const int m = pb + row;
-      const bf16* src = (a_ok && m < pend) ? a_src + m * p.lddy : zero;
+      const bf16* src = (a_ok && m < pend) ? a_src + m * p.lddy : zero_src(tid + 97u * blockIdx.x + 31u * i);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sA + (4 * i + wave) * 1024),
                                        16, 0, 0);
@@ -1027,7 +1032,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
       const int y = (int)fdiv((unsigned)rem, p.fd_w);
       const int xx = rem - y * p.W + dx, yy = y + dy;
       const bool in = b_ok && m < pend && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-      const bf16* src = in ? b_src + (m + doff) * b_ld : zero;
+      const bf16* src = in ? b_src + (m + doff) * b_ld : zero_src(tid + 97u * blockIdx.x + 31u * i + 512u);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sB + (4 * i + wave) * 1024),
                                        16, 0, 0);
@@ -2225,7 +2230,6 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   const int sbeg = blockIdx.z * a.stages_per_split;
   const int send = min(sbeg + a.stages_per_split, a.nstages);
   const int nst = send - sbeg;
-  const bf16* zero = (const bf16*)g_zero_line;
   const int HW = a.H * W, seg = a.seg, segrows = (seg + 2) * WP;
 
   // ---- static per-lane DMA slots: row 16*wave + (lane >> 2) of each 128-row
