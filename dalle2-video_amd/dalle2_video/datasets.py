@@ -147,6 +147,8 @@ class DeviceLoader:
 
     def _to_device(self, batch):
         def move(t):
+            if t.device.type != "cpu":  # already on a device: a plain (stream-ordered) move
+                return t.to(self.device, non_blocking=True)
             if not t.is_pinned():
                 t = t.pin_memory()
             return t.to(self.device, non_blocking=True)

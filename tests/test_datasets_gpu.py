@@ -28,6 +28,14 @@ def test_device_loader_delivers_identical_batches_on_gpu():
         assert n == 3
 
 
+def test_device_loader_passes_device_batches_through():
+    from dalle2_video.datasets import DeviceLoader
+
+    batches = [(torch.randn(2, 3, device="cuda"), torch.arange(2))]
+    out = list(DeviceLoader(batches, "cuda"))
+    assert len(out) == 1 and torch.equal(out[0][0], batches[0][0]) and out[0][1].is_cuda
+
+
 def test_trainer_loader_on_device_and_224_clip_path():
     from dalle2_video import dalle2_video as D
     from dalle2_video.trainer import VideoDecoderTrainer
