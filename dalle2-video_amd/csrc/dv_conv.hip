@@ -949,6 +949,13 @@ struct WgradGArgs {
   int batch_pix, splits_per_batch;
   long long ws_bstride;
   FastDiv fd_hw, fd_w, fd_cin, fd_ks;
+  // ngemm > 1: grid z holds ngemm same-shape 1x1 problems of zper blocks each,
+  // problem g reading mdy[g] / mx[g] and adding into mws[g]
+  int ngemm, zper;
+  const bf16* mdy[3];
+  const bf16* mx[3];
+  int mlddy[3], mld[3];
+  float* mws[3];
 };
 
 // byte offset of 16-B chunk `ch` of `row` in an image with RB-byte rows
@@ -974,15 +981,23 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int co0 = blockIdx.x * BMC, nk0 = blockIdx.y * BNK;
-  int pbeg, pend;
+  int pbeg, pend, bz = blockIdx.z;
   float* wsb = p.ws;
+  const bf16 *pdy = p.dy, *px0 = p.x0, *px1 = p.x1;
+  int lddy = p.lddy, ld0 = p.ld0, ld1 = p.ld1;
+  if (p.ngemm > 1) {
+    const int gi = bz / p.zper;
+    bz -= gi * p.zper;
+    pdy = p.mdy[gi]; px0 = px1 = p.mx[gi]; wsb = p.mws[gi];
+    lddy = p.mlddy[gi]; ld0 = ld1 = p.mld[gi];
+  }
   if (p.batch_pix > 0) {
-    const int bi = blockIdx.z / p.splits_per_batch, lz = blockIdx.z % p.splits_per_batch;
+    const int bi = bz / p.splits_per_batch, lz = bz % p.splits_per_batch;
     pbeg = bi * p.batch_pix + lz * p.pix_per_split;
     pend = min(pbeg + p.pix_per_split, (bi + 1) * p.batch_pix);
-    wsb = p.ws + bi * p.ws_bstride;
+    wsb += bi * p.ws_bstride;
   } else {
-    pbeg = blockIdx.z * p.pix_per_split;
+    pbeg = bz * p.pix_per_split;
     pend = min(pbeg + p.pix_per_split, p.M);
   }
   const int pad = p.ks >> 1;
@@ -994,7 +1009,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
   const int a_x = RA == 128 ? (((a_row0 >> 1) & 1) << 2) : ((a_row0 & 3) << 2);
   const int cha = a_slot ^ a_x;
   const bool a_ok = co0 + 8 * cha < p.cout;
-  const bf16* a_src = p.dy + co0 + 8 * cha;
+  const bf16* a_src = pdy + co0 + 8 * cha;
   // B: fixed chunk column -> (tap, ci)
   const int b_lrow = lane / (RB / 16), b_slot = lane % (RB / 16);
   const int b_row0 = wave * RPI_B + b_lrow;
@@ -1007,8 +1022,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
   const int ty = b_ok ? (int)fdiv((unsigned)tap, p.fd_ks) : 0;
   const int dy = ty - pad, dx = tap - ty * p.ks - pad;
   const bool first = ci < p.c0;
-  const bf16* b_src = first ? p.x0 + ci : p.x1 + (ci - p.c0);
-  const int b_ld = first ? p.ld0 : p.ld1;
+  const bf16* b_src = first ? px0 + ci : px1 + (ci - p.c0);
+  const int b_ld = first ? ld0 : ld1;
   const int doff = dy * p.W + dx;
 
   auto issue = [&](int pb, int buf) {
@@ -1018,7 +1033,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
     for (int i = 0; i < GA; ++i) {
       const int row = (4 * i + wave) * RPI_A + a_lrow;
       const int m = pb + row;
-      const bf16* src = (a_ok && m < pend) ? a_src + m * p.lddy : zero_src(tid + 97u * blockIdx.x + 31u * i);
+      const bf16* src = (a_ok && m < pend) ? a_src + m * lddy : zero_src(tid + 97u * blockIdx.x + 31u * i);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sA + (4 * i + wave) * 1024),
                                        16, 0, 0);
@@ -1156,8 +1171,18 @@ int launch_wgrad_glds(WgradGArgs a, hipStream_t st) {
     splits = (unsigned)((a.M + per - 1) / per);
   }
   a.pix_per_split = (int)per;
+  a.zper = (int)splits;
+  if (a.ngemm > 1) splits *= (unsigned)a.ngemm;
   conv_wgrad_glds_kernel<BMC, BNK><<<dim3(mt, nt, splits), 256, 0, st>>>(a);
   return check_launch("conv_wgrad_glds");
+}
+
+static int launch_wgrad_glds_any(WgradGArgs& a, hipStream_t st) {
+  if (a.cout <= 64) {
+    if (a.K >= 2048 || a.K % 256 == 0) return launch_wgrad_glds<64, 256>(a, st);
+    return launch_wgrad_glds<64, 128>(a, st);
+  }
+  return launch_wgrad_glds<128, 128>(a, st);
 }
 
 int conv_wgrad_glds(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
@@ -1172,12 +1197,34 @@ int conv_wgrad_glds(const void* dy, int lddy, const void* x0, int ld0, int c0, c
   a.ws_bstride = (long long)cout * a.K;
   a.fd_hw = make_fastdiv((unsigned)(h * w)); a.fd_w = make_fastdiv((unsigned)w);
   a.fd_cin = make_fastdiv((unsigned)cin); a.fd_ks = make_fastdiv((unsigned)ks);
+  a.ngemm = 1; a.zper = 0;
   if (a.M == 0) return DV_OK;
-  if (cout <= 64) {
-    if (a.K >= 2048 || a.K % 256 == 0) return launch_wgrad_glds<64, 256>(a, st);
-    return launch_wgrad_glds<64, 128>(a, st);
+  return launch_wgrad_glds_any(a, st);
+}
+
+// ngemm same-shape batched TN GEMMs out_g[b][i][j] += sum_r A_g[r][i] B_g[r][j]
+// in ONE launch (the three cross-attention token reductions of a block share
+// rows, m and n: one launch fills the chip three times as wide as each alone)
+static int gemm_tn_multi_glds(int ngemm, const void* const* a, const int* lda, const void* const* b,
+                              const int* ldb, float* const* out, long long batch_rows, int nbatch,
+                              int m, int n, hipStream_t st) {
+  WgradGArgs g;
+  g.dy = (const bf16*)a[0]; g.lddy = lda[0]; g.x0 = g.x1 = (const bf16*)b[0];
+  g.ld0 = g.ld1 = ldb[0]; g.c0 = n; g.ws = out[0]; g.db = nullptr;
+  g.H = 1; g.W = 1; g.cin = n; g.cout = m; g.ks = 1; g.K = n;
+  g.M = (int)(batch_rows * nbatch);
+  g.batch_pix = (int)batch_rows; g.splits_per_batch = 1; g.pix_per_split = 0;
+  g.ws_bstride = (long long)m * n;
+  g.fd_hw = make_fastdiv(1u); g.fd_w = make_fastdiv(1u);
+  g.fd_cin = make_fastdiv((unsigned)n); g.fd_ks = make_fastdiv(1u);
+  g.ngemm = ngemm; g.zper = 0;
+  for (int i = 0; i < 3; ++i) {
+    const int j = i < ngemm ? i : 0;
+    g.mdy[i] = (const bf16*)a[j]; g.mx[i] = (const bf16*)b[j];
+    g.mlddy[i] = lda[j]; g.mld[i] = ldb[j]; g.mws[i] = out[j];
   }
-  return launch_wgrad_glds<128, 128>(a, st);
+  if (g.M == 0) return DV_OK;
+  return launch_wgrad_glds_any(g, st);
 }
 
 // Weight packing, LDS-staged so both the torch-layout reads and the packed
@@ -2833,4 +2880,28 @@ extern "C" int dv_gemm_tn_batched(int dtype, const void* a, int lda, const void*
   if (dtype == DV_BF16)
     return conv_wgrad_t<bf16>(a, lda, b, ldb, n, nullptr, 0, out, nullptr, 1, 1, W, n, m, 1, st, batch_rows);
   DV_REQUIRE(false, "unknown dtype");
+}
+
+extern "C" int dv_gemm_tn_batched_multi(int dtype, int ngemm, const void* const* a, const int* lda,
+                                        const void* const* b, const int* ldb, float* const* out,
+                                        long long batch_rows, int nbatch, int m, int n, void* stream) {
+  // ngemm (1..3) dv_gemm_tn_batched problems of one shape, one launch when bf16
+  DV_REQUIRE(a && lda && b && ldb && out && ngemm >= 1 && ngemm <= 3, "bad ngemm / null arrays");
+  long long maxld = 0;
+  for (int i = 0; i < ngemm; ++i) {
+    DV_REQUIRE(a[i] && b[i] && out[i] && lda[i] % 8 == 0 && ldb[i] % 8 == 0,
+               "null operand or stride not a multiple of 8");
+    maxld = std::max<long long>(maxld, std::max(lda[i], ldb[i]));
+  }
+  DV_REQUIRE(m % 8 == 0 && n % 8 == 0, "m, n and strides must be multiples of 8");
+  if (nbatch <= 0 || batch_rows <= 0) return DV_OK;
+  const long long rows = batch_rows * nbatch;
+  if (dtype == DV_BF16 && rows * maxld < (1ll << 31))
+    return gemm_tn_multi_glds(ngemm, a, lda, b, ldb, out, batch_rows, nbatch, m, n, (hipStream_t)stream);
+  for (int i = 0; i < ngemm; ++i) {
+    const int rc = dv_gemm_tn_batched(dtype, a[i], lda[i], b[i], ldb[i], out[i], batch_rows, nbatch,
+                                      m, n, stream);
+    if (rc != DV_OK) return rc;
+  }
+  return DV_OK;
 }

@@ -70,6 +70,7 @@ _SIGS = {
     "dv_xattn_bwd_tokens": [_I, _P, _I, _P, _I, _P, _I, _L, _L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "dv_xattn_fold_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _I, _P],
     "dv_gemm_tn_batched": [_I, _P, _I, _P, _I, _P, _L, _I, _I, _I, _P],
+    "dv_gemm_tn_batched_multi": [_I, _I, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P],
     "dv_resize_nearest": [_P, _P, _L, _I, _I, _I, _I, _I, _F, _F, _P],
     "dv_gaussian_blur": [_P, _P, _L, _I, _I, _I, _P, _P],
     "dv_mqa_prep": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _P],

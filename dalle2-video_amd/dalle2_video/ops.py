@@ -112,6 +112,8 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0):
 
 
 _NO_1X1 = bool(os.environ.get("DV_NO_1X1"))  # A/B switch: 1x1 convs on the glds kernel
+# A/B switch: the cross-attention token reductions as three launches, not one
+_NO_GEMM_MULTI = os.environ.get("DV_NO_GEMM_MULTI", "0") not in ("", "0")
 _NO_WINDOW = bool(os.environ.get("DV_NO_WINDOW"))  # A/B switch: 3x3 convs on dv_conv_fwd only
 # measured (tools/kbench.py fwd): the window form wins at 8x8 and 16x16, the glds /
 # stripe kernels at 32x32 and 64x64
@@ -1352,13 +1354,26 @@ class CrossAttnFn(torch.autograd.Function):
         call("dv_xattn_bwd_tokens", dt(x), ptr(dy), lddy, ptr(x), ldx, ptr(dx), C, ntok, P, C,
              ptr(KtT), ptr(Vt), ptr(VtT), ptr(colsum), ptr(g2f), ptr(stats), ptr(pbuf), ptr(dobuf),
              ptr(dsbuf), ptr(p2buf), stream())
-        # per-batch token reductions: R = dS'^T X, V' = P^T dO, Q = P'^T dY (one batched GEMM each)
-        for a_, b_, ldb, o_ in ((dsbuf, x, ldx, wsR), (pbuf, dobuf, C, wsV), (p2buf, dy, lddy, wsQ)):
-            _launch(gemm_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldb)),
-                    2.0 * ntok * 32 * C, 0,
-                    lambda a_=a_, b_=b_, ldb=ldb, o_=o_: call(
-                        "dv_gemm_tn_batched", dt(x), ptr(a_), 32, ptr(b_), ldb, ptr(o_), P, nb, 32, C,
-                        stream()))
+        # per-batch token reductions: R = dS'^T X, V' = P^T dO, Q = P'^T dY (three batched
+        # GEMMs of one shape, one launch)
+        probs = ((dsbuf, x, ldx, wsR), (pbuf, dobuf, C, wsV), (p2buf, dy, lddy, wsQ))
+        if _NO_GEMM_MULTI:
+            for a_, b_, ldb, o_ in probs:
+                _launch(gemm_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldb)),
+                        2.0 * ntok * 32 * C, 0,
+                        lambda a_=a_, b_=b_, ldb=ldb, o_=o_: call(
+                            "dv_gemm_tn_batched", dt(x), ptr(a_), 32, ptr(b_), ldb, ptr(o_), P, nb, 32,
+                            C, stream()))
+        else:
+            pa = (ctypes.c_void_p * 3)(*(a_.data_ptr() for a_, _, _, _ in probs))
+            la = (ctypes.c_int * 3)(32, 32, 32)
+            pb = (ctypes.c_void_p * 3)(*(b_.data_ptr() for _, b_, _, _ in probs))
+            lb = (ctypes.c_int * 3)(*(ldb for _, _, ldb, _ in probs))
+            po = (ctypes.c_void_p * 3)(*(o_.data_ptr() for _, _, _, o_ in probs))
+            _launch(gemm_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldx, C, lddy)),
+                    3 * 2.0 * ntok * 32 * C, 0,
+                    lambda: call("dv_gemm_tn_batched_multi", dt(x), 3, pa, la, pb, lb, po, P, nb, 32, C,
+                                 stream()))
         dat = torch.empty(nb, C, 24, dtype=torch.float32, device=dev)
         dvt = torch.empty_like(dat)
         s1, s2 = _grad_out(g1p), _grad_out(g2p)

@@ -206,6 +206,11 @@ int dv_linear_group_bwd(const float* x, int B, int K, int act_in, const DvLinEnt
  * Used for the token reductions of the cross-attention backward.           */
 int dv_gemm_tn_batched(int dtype, const void* a, int lda, const void* b, int ldb, float* out,
                        long long batch_rows, int nbatch, int m, int n, void* stream);
+/* ngemm (1..3) dv_gemm_tn_batched problems sharing batch_rows, nbatch, m, n
+ * (host arrays of operand pointers / strides / outputs): one launch in bf16.  */
+int dv_gemm_tn_batched_multi(int dtype, int ngemm, const void* const* a, const int* lda,
+                             const void* const* b, const int* ldb, float* const* out,
+                             long long batch_rows, int nbatch, int m, int n, void* stream);
 
 /* ---- GroupNorm (+ FiLM scale/shift, SiLU, residual) -----------------------
  * Block3D.norm/act with ResnetBlock3D's scale_shift (dalle2_video.py:109-133,

@@ -325,3 +325,33 @@ def test_mqa_forward_streamed_long_sequence(parity_log, N, B):
     e = rel(y, ref)
     parity_log(N=N, B=B, fwd_rel=e)
     assert e < 2.5e-2
+
+
+@pytest.mark.parametrize("ngemm,nb,P,n", [(3, 4, 1000, 64), (3, 2, 4096, 128), (2, 1, 77, 256), (1, 3, 300, 64)])
+def test_gemm_tn_batched_multi(ngemm, nb, P, n):
+    """The one-launch form of the cross-attention token reductions: problem g,
+    batch b gets out_g[b] += A_g[b rows]^T B_g[b rows] (f32 atomics on a
+    pre-filled output), for operands of different leading dimensions."""
+    import ctypes
+
+    from dalle2_video._lib import call, stream
+
+    g = torch.Generator().manual_seed(11)
+    dev, m = "cuda", 32
+    lds_a = [32, 40, 32][:ngemm]
+    lds_b = [n, n + 8, 2 * n][:ngemm]
+    A = [torch.randn(nb * P, la, generator=g).to(torch.bfloat16) for la in lds_a]
+    B = [torch.randn(nb * P, lb, generator=g).to(torch.bfloat16) for lb in lds_b]
+    O = [torch.randn(nb, m, n, generator=g) for _ in range(ngemm)]
+    Ad = [t.to(dev) for t in A]
+    Bd = [t.to(dev) for t in B]
+    Od = [t.to(dev) for t in O]
+    arr = lambda T, xs: (T * 3)(*(list(xs) + [xs[0]] * (3 - len(xs))))
+    call("dv_gemm_tn_batched_multi", 1, ngemm, arr(ctypes.c_void_p, [t.data_ptr() for t in Ad]),
+         arr(ctypes.c_int, lds_a), arr(ctypes.c_void_p, [t.data_ptr() for t in Bd]),
+         arr(ctypes.c_int, lds_b), arr(ctypes.c_void_p, [t.data_ptr() for t in Od]), P, nb, m, n, stream())
+    torch.cuda.synchronize()
+    for a, b, o, od in zip(A, B, O, Od):
+        ref = o.double() + torch.einsum("bri,brj->bij", a[:, :m].double().reshape(nb, P, m),
+                                        b[:, :n].double().reshape(nb, P, n))
+        assert rel(od, ref) < 1e-5
