@@ -227,16 +227,43 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
         for (int u = 0; u < U; ++u) cur[l][u] = nxt[l][u];
     }
   }
-  // block reduce over the row slots ([rpp][C] in LDS), then one atomic per channel
+  // block reduce over the row slots, then one atomic per channel.  Narrow rows
+  // (tpr a power of two < 64: C = 8 .. 256 bf16) first fold the wave's rows
+  // with lane shuffles (lanes tpr apart hold the same channels), leaving 4
+  // wave partials per channel in LDS; otherwise [rpp][C] rows are summed in LDS
+  // (a serial rpp-long loop per channel: 256 rows at C = 8).
+  const int lane = tid & 63, wv = tid >> 6;
+  const bool shfl = tpr < 64 && (tpr & (tpr - 1)) == 0;
+  int nrow = rpp;
+  if (shfl) {
 #pragma unroll
-  for (int e = 0; e < VEC; ++e) {
-    sh[0][tid * VEC + e] = (rr < rpp) ? s1[e / 2][e % 2] : 0.f;
-    sh[1][tid * VEC + e] = (rr < rpp) ? s2[e / 2][e % 2] : 0.f;
+    for (int j = 0; j < VEC / 2; ++j) {
+      for (int o = tpr; o < 64; o <<= 1) {
+        s1[j].x += __shfl_xor(s1[j].x, o, 64);
+        s1[j].y += __shfl_xor(s1[j].y, o, 64);
+        s2[j].x += __shfl_xor(s2[j].x, o, 64);
+        s2[j].y += __shfl_xor(s2[j].y, o, 64);
+      }
+    }
+    if (lane < tpr) {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        sh[0][wv * a.C + cv + e] = s1[e / 2][e % 2];
+        sh[1][wv * a.C + cv + e] = s2[e / 2][e % 2];
+      }
+    }
+    nrow = 4;
+  } else {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      sh[0][tid * VEC + e] = (rr < rpp) ? s1[e / 2][e % 2] : 0.f;
+      sh[1][tid * VEC + e] = (rr < rpp) ? s2[e / 2][e % 2] : 0.f;
+    }
   }
   __syncthreads();
   for (int c = tid; c < a.C; c += 256) {
     float t1 = 0.f, t2 = 0.f;
-    for (int r = 0; r < rpp; ++r) {
+    for (int r = 0; r < nrow; ++r) {
       t1 += sh[0][r * a.C + c];
       t2 += sh[1][r * a.C + c];
     }

@@ -21,6 +21,7 @@
 #include "dv_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 using namespace dv;
 
@@ -30,6 +31,7 @@ constexpr int XE_MAXT = 8;  // 16-channel tiles (total cout <= 128)
 
 struct XeGeom {
   int ntiles, cout, cin, cp, kmax, nbranch;
+  int cpad;           // 16 * ntiles: cout padded to whole tiles (zero weights / bias)
   int k[XE_MAXT];     // window of tile t (largest branch kernel among its channels)
   int jw[XE_MAXT];    // forward K per dy: k*cp rounded up to 32
   int jwp[XE_MAXT];   // LDS / image row pitch (elements) = jw + 8
@@ -43,12 +45,13 @@ struct XeGeom {
   int bk[4], bco0[4], bcout[4];  // branches: kernel, first channel, channels
 };
 
-bool xe_geom(const DvCrossEmbed& ce, XeGeom& g) {
-  if (ce.nbranch < 1 || ce.nbranch > 4 || ce.cin < 1 || ce.cin > 8) return false;
+// fwd_only: also cin 9..16 (CP = 16; the weight-gradient kernel stages CP <= 8)
+bool xe_geom(const DvCrossEmbed& ce, XeGeom& g, bool fwd_only = false) {
+  if (ce.nbranch < 1 || ce.nbranch > 4 || ce.cin < 1 || ce.cin > (fwd_only ? 16 : 8)) return false;
   g = XeGeom{};
   g.nbranch = ce.nbranch;
   g.cin = ce.cin;
-  g.cp = ce.cin <= 4 ? 4 : 8;
+  g.cp = ce.cin <= 4 ? 4 : ce.cin <= 8 ? 8 : 16;
   int co = 0, kmax = 0;
   for (int b = 0; b < ce.nbranch; ++b) {
     if (ce.k[b] < 1 || ce.k[b] % 2 == 0 || ce.k[b] > 15 || ce.cout[b] < 1) return false;
@@ -59,10 +62,11 @@ bool xe_geom(const DvCrossEmbed& ce, XeGeom& g) {
     co += ce.cout[b];
     kmax = std::max(kmax, ce.k[b]);
   }
-  if (co % 16 || co > 16 * XE_MAXT) return false;
+  if (co % 8 || co > 16 * XE_MAXT) return false;
   g.cout = co;
   g.kmax = kmax;
-  g.ntiles = co / 16;
+  g.ntiles = (co + 15) / 16;
+  g.cpad = 16 * g.ntiles;
   int woff = 0, poff = 0;
   for (int t = 0; t < g.ntiles; ++t) {
     int k = 0;
@@ -79,8 +83,8 @@ bool xe_geom(const DvCrossEmbed& ce, XeGeom& g) {
     g.items += k * g.nb16[t];
   }
   g.boff = (woff + 7) / 8 * 8;
-  g.image_elems = g.boff + 2 * g.cout;  // cout % 16 == 0: stays a multiple of 8
-  g.pfloats = poff + g.cout;
+  g.image_elems = g.boff + 2 * g.cpad;  // f32 bias [cpad]: stays a multiple of 8
+  g.pfloats = poff + g.cpad;
   return true;
 }
 
@@ -117,10 +121,10 @@ __device__ __forceinline__ int branch_of(const XeGeom& g, int co) {
 // j >= k_t * cp zero; then the concatenated f32 bias.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void xe_pack_kernel(DvCrossEmbed ce, XeGeom g, bf16* img) {
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < g.boff + g.cout; i += gridDim.x * 256) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < g.boff + g.cpad; i += gridDim.x * 256) {
     if (i >= g.boff) {
       const int co = i - g.boff, b = branch_of(g, co);
-      ((float*)(img + g.boff))[co] = ce.b[b] ? ce.b[b][co - g.bco0[b]] : 0.f;
+      ((float*)(img + g.boff))[co] = co < g.cout && ce.b[b] ? ce.b[b][co - g.bco0[b]] : 0.f;
       continue;
     }
     int t = 0;
@@ -135,7 +139,8 @@ __global__ __launch_bounds__(256) void xe_pack_kernel(DvCrossEmbed ce, XeGeom g,
       const int kb = g.bk[b], o = (k - kb) / 2;
       const int dx = j / g.cp, c = j - dx * g.cp;
       const int ky = dy - o, kx = dx - o;
-      if (j < k * g.cp && c < g.cin && (unsigned)ky < (unsigned)kb && (unsigned)kx < (unsigned)kb)
+      if (co < g.cout && j < k * g.cp && c < g.cin && (unsigned)ky < (unsigned)kb &&
+          (unsigned)kx < (unsigned)kb)
         v = ce.w[b][(((long long)(co - g.bco0[b]) * g.cin + c) * kb + ky) * kb + kx];
     }
     img[i] = (bf16)v;
@@ -150,12 +155,17 @@ __global__ __launch_bounds__(256) void xe_pack_kernel(DvCrossEmbed ce, XeGeom g,
 // D[co][px]: lane holds pixel (l & 15), channels 4 (l >> 4) .. +3 -> one
 // 8-byte store per lane per tile and pixel block.
 // ---------------------------------------------------------------------------
-constexpr int XE_R = 8;
+// rows per forward workgroup; DV_XE_R / DV_XE_WB: A/B knobs (rows, columns)
+int xe_r() {
+  static const int r = getenv("DV_XE_R") ? std::max(1, atoi(getenv("DV_XE_R"))) : 8;
+  return r;
+}
 
 template <int CP>
 __global__ __launch_bounds__(512) void xe_fwd_kernel(XeGeom g, const bf16* img, const bf16* x,
-                                                     int ldx, bf16* y, int ldy, int H, int W,
-                                                     int WB) {
+                                                     int ldx, const bf16* x1, int ld1, int c0,
+                                                     const bf16* res, int ldres, bf16* y, int ldy,
+                                                     int H, int W, int WB, int XE_R) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -169,30 +179,83 @@ __global__ __launch_bounds__(512) void xe_fwd_kernel(XeGeom g, const bf16* img, 
   bf16* sW = (bf16*)smem;
   bf16* sX = sW + g.image_elems;
 
-  for (int i = tid; i < g.image_elems / 8; i += 512) ((u32x4*)sW)[i] = ((const u32x4*)img)[i];
-  for (int i = tid; i < XR * XC; i += 512) {
+  // window staging: XS pixels per thread, every global load issued before any
+  // LDS store (one memory round trip per workgroup, not one per pixel slot)
+  constexpr int XS = 4, NJ = CP == 4 ? 1 : CP / 8;
+  const int npx = XR * XC;
+  u32x4 wreg = {};
+  const bool wld = tid < g.image_elems / 8;
+  if (wld) wreg = ((const u32x4*)img)[tid];
+  u32x4 xv[XS][NJ];
+#pragma unroll
+  for (int s = 0; s < XS; ++s) {
+    const int i = tid + 512 * s;
     const int rr = i / XC, cc = i - rr * XC;
     const int yy = y0 + rr - half, xx = x0 + cc - half;
-    bf16 v[CP];
+    const bool in = i < npx && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W &&
+                    cc < WB + g.kmax - 1;
+    const long long pix = (long long)(f * H + yy) * W + xx;
 #pragma unroll
-    for (int c = 0; c < CP; ++c) v[c] = (bf16)0.f;
-    if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W && cc < WB + g.kmax - 1) {
-      const bf16* src = x + ((long long)(f * H + yy) * W + xx) * ldx;
+    for (int j = 0; j < NJ; ++j) {
+      xv[s][j] = u32x4{0u, 0u, 0u, 0u};
       if (CP == 4) {
-        const u32x2 q = *(const u32x2*)src;
-        const bf16x4 e = __builtin_bit_cast(bf16x4, q);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = c < g.cin ? e[c] : (bf16)0.f;
-      } else {
-        const u32x4 q = *(const u32x4*)src;
-        const bf16x8 e = __builtin_bit_cast(bf16x8, q);
-#pragma unroll
-        for (int c = 0; c < CP; ++c) v[c] = c < g.cin ? e[c % 8] : (bf16)0.f;
+        if (in) {
+          const u32x2 q = *(const u32x2*)(x + pix * ldx);
+          xv[s][j] = u32x4{q[0], q[1], 0u, 0u};
+        }
+      } else if (in && 8 * j < g.cin) {
+        // 8-channel chunks: channels [0, c0) of x, [c0, cin) of x1 (c0 % 8 == 0)
+        const bf16* src = 8 * j < c0 ? x + pix * ldx + 8 * j : x1 + pix * ld1 + (8 * j - c0);
+        xv[s][j] = *(const u32x4*)src;
       }
     }
-    bf16* dst = sX + (long long)i * CP;
+  }
+  if (wld) ((u32x4*)sW)[tid] = wreg;
+  for (int i = tid + 512; i < g.image_elems / 8; i += 512) ((u32x4*)sW)[i] = ((const u32x4*)img)[i];
 #pragma unroll
-    for (int c = 0; c < CP; ++c) dst[c] = v[c];
+  for (int s = 0; s < XS; ++s) {
+    const int i = tid + 512 * s;
+    if (i >= npx) break;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      bf16x8 e = __builtin_bit_cast(bf16x8, xv[s][j]);
+      const int cl = CP == 4 ? 4 : 8;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (c >= cl || 8 * j + c >= g.cin) e[c] = (bf16)0.f;
+      if (CP == 4) {
+        *(bf16x4*)(sX + (long long)i * 4) = bf16x4{e[0], e[1], e[2], e[3]};
+      } else {
+        *(bf16x8*)(sX + (long long)i * CP + 8 * j) = e;
+      }
+    }
+  }
+  for (int i = tid + 512 * XS; i < npx; i += 512) {  // windows beyond XS slots (wide kmax)
+    const int rr = i / XC, cc = i - rr * XC;
+    const int yy = y0 + rr - half, xx = x0 + cc - half;
+    const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W && cc < WB + g.kmax - 1;
+    const long long pix = (long long)(f * H + yy) * W + xx;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      bf16x8 e = {};
+      if (CP == 4) {
+        if (in) {
+          const bf16x4 q = __builtin_bit_cast(bf16x4, *(const u32x2*)(x + pix * ldx));
+#pragma unroll
+          for (int c = 0; c < 4; ++c) e[c] = c < g.cin ? q[c] : (bf16)0.f;
+        }
+        *(bf16x4*)(sX + (long long)i * 4) = bf16x4{e[0], e[1], e[2], e[3]};
+      } else {
+        if (in && 8 * j < g.cin) {
+          const bf16* src = 8 * j < c0 ? x + pix * ldx + 8 * j : x1 + pix * ld1 + (8 * j - c0);
+          e = __builtin_bit_cast(bf16x8, *(const u32x4*)src);
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            if (8 * j + c >= g.cin) e[c] = (bf16)0.f;
+        }
+        *(bf16x8*)(sX + (long long)i * CP + 8 * j) = e;
+      }
+    }
   }
   __syncthreads();
 
@@ -202,7 +265,7 @@ __global__ __launch_bounds__(512) void xe_fwd_kernel(XeGeom g, const bf16* img, 
   for (int job = wave; job < XE_R * jobs_per_row; job += 8) {
     const int r = job / jobs_per_row, xb = (job - r * jobs_per_row) * 32;
     if (y0 + r >= H) break;
-    bf16* out = y + ((long long)(f * H + y0 + r) * W + x0 + xb + px) * ldy;
+    const long long p = (long long)(f * H + y0 + r) * W + x0 + xb + px;
     for (int t = 0; t < g.ntiles; ++t) {
       const int k = g.k[t], jw = g.jw[t], jwp = g.jwp[t];
       const int cofs = half - k / 2;  // the tile's window inside the kmax halo
@@ -218,14 +281,22 @@ __global__ __launch_bounds__(512) void xe_fwd_kernel(XeGeom g, const bf16* img, 
         }
       }
       const int co = 16 * t + 4 * kg;
+      if (co >= g.cout) continue;  // padded channels of the last tile
+      float r0[4] = {0.f, 0.f, 0.f, 0.f}, r1[4] = {0.f, 0.f, 0.f, 0.f};
+      if (res) {
+        const bf16x4 q0 = *(const bf16x4*)(res + p * ldres + co);
+        const bf16x4 q1 = *(const bf16x4*)(res + (p + 16) * ldres + co);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { r0[e] = (float)q0[e]; r1[e] = (float)q1[e]; }
+      }
       bf16x4 o0, o1;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        o0[e] = (bf16)(a0[e] + sb[co + e]);
-        o1[e] = (bf16)(a1[e] + sb[co + e]);
+        o0[e] = (bf16)(a0[e] + sb[co + e] + r0[e]);
+        o1[e] = (bf16)(a1[e] + sb[co + e] + r1[e]);
       }
-      *(bf16x4*)(out + co) = o0;
-      *(bf16x4*)(out + 16 * ldy + co) = o1;
+      *(bf16x4*)(y + p * ldy + co) = o0;
+      *(bf16x4*)(y + (p + 16) * ldy + co) = o1;
     }
   }
 }
@@ -248,7 +319,7 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
   const int f = blockIdx.x / bands, yb = (blockIdx.x % bands) * rows;
   const int yend = min(yb + rows, H);
   const int half = g.kmax / 2, XC = W + g.kmax + 7;
-  const int DS = g.cout + 8;                 // dY row pitch (elements)
+  const int DS = g.cpad + 8;                 // dY row pitch (elements)
   const int DYB = W * DS, XB = g.kmax * XC * CP;  // buffer sizes (elements)
   bf16* sD = (bf16*)smem;                    // [2][W][DS]
   bf16* sX = sD + 2 * DYB;                   // [2][kmax][XC][CP]
@@ -288,7 +359,7 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
   // ---- staging: global -> registers (next row) -> LDS ----
   const int dchunks = W * (g.cout / 8);       // 16-B dY chunks per row
   const int xelems = g.kmax * XC;             // window pixels per row
-  constexpr int DPT = 4, XPT = 8;             // per-thread register slots
+  constexpr int DPT = 4, XPT = 9;             // per-thread register slots (w = 256, k = 15: 4170 pixels)
   u32x4 dreg[DPT];
   bf16 xreg[XPT][CP];
   auto load_row = [&](int yy) {
@@ -349,6 +420,11 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
   const int kg = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   const int plo = 8 * kg + q;
 
+  if (g.cpad != g.cout) {  // channels [cout, cpad) of both dY buffers stay zero
+    for (int i = tid; i < 2 * W; i += 512)
+      for (int c = g.cout; c < g.cpad; c += 8) *(u32x4*)(sD + i * DS + c) = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+  }
   if (yb < yend) {
     load_row(yb);
     store_row(0);
@@ -406,7 +482,7 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
   if (wave < g.ntiles) {
     accb += __shfl_xor(accb, 16, 64);
     accb += __shfl_xor(accb, 32, 64);
-    if (lane < 16) pp_[g.pfloats - g.cout + 16 * wave + lane] = accb;
+    if (lane < 16) pp_[g.pfloats - g.cpad + 16 * wave + lane] = accb;
   }
 }
 
@@ -437,7 +513,7 @@ __global__ __launch_bounds__(256) void xe_wgrad_finish_kernel(DvCrossEmbed ce, X
       }
       local -= nw;
       if (local < g.bcout[b]) {
-        src = g.pfloats - g.cout + g.bco0[b] + (int)local;
+        src = g.pfloats - g.cpad + g.bco0[b] + (int)local;
         dst = ce.db[b] ? ce.db[b] + local : nullptr;
         acc = ce.accumulate_b;
         break;
@@ -471,15 +547,19 @@ long long xe_total_grads(const XeGeom& g) {
   return n;
 }
 
-int xe_fwd_wb(int w) { return w % 64 == 0 ? 64 : 32; }
+int xe_fwd_wb(int w) {
+  static const int forced = getenv("DV_XE_WB") ? atoi(getenv("DV_XE_WB")) : 0;
+  if (forced >= 32 && forced % 32 == 0 && w % forced == 0) return forced;
+  return w % 64 == 0 ? 64 : 32;
+}
 
 size_t xe_fwd_lds(const XeGeom& g, int w) {
   const int WB = xe_fwd_wb(w);
-  return (size_t)g.image_elems * 2 + (size_t)(XE_R + g.kmax - 1) * (WB + g.kmax + 7) * g.cp * 2;
+  return (size_t)g.image_elems * 2 + (size_t)(xe_r() + g.kmax - 1) * (WB + g.kmax + 7) * g.cp * 2;
 }
 
 size_t xe_wgrad_lds(const XeGeom& g, int w) {
-  return (size_t)2 * w * (g.cout + 8) * 2 + (size_t)2 * g.kmax * (w + g.kmax + 7) * g.cp * 2;
+  return (size_t)2 * w * (g.cpad + 8) * 2 + (size_t)2 * g.kmax * (w + g.kmax + 7) * g.cp * 2;
 }
 
 int xe_rows(int nf, int h) {
@@ -490,7 +570,8 @@ int xe_rows(int nf, int h) {
 }
 
 bool xe_shape_ok(const XeGeom& g, int nf, int h, int w, int ldx) {
-  if (nf < 1 || h < 1 || w < 32 || w % 32 || ldx % g.cp || ldx < g.cin) return false;
+  if (nf < 1 || h < 1 || w < 32 || w % 32 || ldx % std::min(g.cp, 8) || ldx < std::min(g.cin, 8))
+    return false;
   if ((long long)nf * h * w * std::max(ldx, g.cout) >= (1ll << 31)) return false;
   return true;
 }
@@ -521,27 +602,94 @@ extern "C" int dv_cross_embed_pack(const DvCrossEmbed* ce, void* image, void* st
   return check_launch("cross_embed_pack");
 }
 
+namespace {
+int xe_fwd_launch(const XeGeom& g, const void* image, const void* x, int ldx, const void* x1, int ld1,
+                  int c0, const void* res, int ldres, void* y, int ldy, int nf, int h, int w,
+                  hipStream_t st) {
+  const size_t lds = xe_fwd_lds(g, w);
+  DV_REQUIRE(lds <= 160 * 1024, "LDS footprint too large");
+  const int WB = xe_fwd_wb(w);
+  const int R = xe_r();
+  const long long blocks = (long long)nf * ((h + R - 1) / R) * (w / WB);
+  static bool once = (xe_allow_lds(xe_fwd_kernel<4>), xe_allow_lds(xe_fwd_kernel<8>),
+                      xe_allow_lds(xe_fwd_kernel<16>), true);
+  (void)once;
+#define XE_FW(CP)                                                                                \
+  xe_fwd_kernel<CP><<<(unsigned)blocks, 512, lds, st>>>(g, (const bf16*)image, (const bf16*)x, ldx, \
+                                                        (const bf16*)x1, ld1, c0, (const bf16*)res, \
+                                                        ldres, (bf16*)y, ldy, h, w, WB, R)
+  if (g.cp == 4) XE_FW(4);
+  else if (g.cp == 8) XE_FW(8);
+  else XE_FW(16);
+#undef XE_FW
+  return DV_OK;
+}
+
+DvCrossEmbed small_desc(const float* wt, const float* b, int cin, int cout, int ksize) {
+  DvCrossEmbed ce{};
+  ce.nbranch = 1;
+  ce.cin = cin;
+  ce.k[0] = ksize;
+  ce.cout[0] = cout;
+  ce.w[0] = wt;
+  ce.b[0] = b;
+  return ce;
+}
+}  // namespace
+
 extern "C" int dv_cross_embed_fwd(const DvCrossEmbed* ce, const void* image, const void* x,
                                   int ldx, void* y, int ldy, int nf, int h, int w, void* stream) {
   DV_REQUIRE(ce && image && x && y, "null pointer");
   XeGeom g;
   DV_REQUIRE(xe_geom(*ce, g), "unsupported branch set");
-  DV_REQUIRE(xe_shape_ok(g, nf, h, w, ldx) && ldy % 4 == 0 && ldy >= g.cout,
+  DV_REQUIRE(xe_shape_ok(g, nf, h, w, ldx) && ldx >= g.cin && ldy % 4 == 0 && ldy >= g.cout,
              "needs w % 32 == 0, ldx % (4 or 8) == 0, ldy % 4 == 0");
-  const size_t lds = xe_fwd_lds(g, w);
-  DV_REQUIRE(lds <= 160 * 1024, "LDS footprint too large");
-  const int WB = xe_fwd_wb(w);
-  const long long blocks = (long long)nf * ((h + XE_R - 1) / XE_R) * (w / WB);
-  hipStream_t st = (hipStream_t)stream;
-  static bool once = (xe_allow_lds(xe_fwd_kernel<4>), xe_allow_lds(xe_fwd_kernel<8>), true);
-  (void)once;
-  if (g.cp == 4)
-    xe_fwd_kernel<4><<<(unsigned)blocks, 512, lds, st>>>(g, (const bf16*)image, (const bf16*)x, ldx,
-                                                         (bf16*)y, ldy, h, w, WB);
-  else
-    xe_fwd_kernel<8><<<(unsigned)blocks, 512, lds, st>>>(g, (const bf16*)image, (const bf16*)x, ldx,
-                                                         (bf16*)y, ldy, h, w, WB);
+  const int rc = xe_fwd_launch(g, image, x, ldx, nullptr, 0, g.cin, nullptr, 0, y, ldy, nf, h, w,
+                               (hipStream_t)stream);
+  if (rc != DV_OK) return rc;
   return check_launch("cross_embed_fwd");
+}
+
+extern "C" int dv_conv_small_image_elems(int cin, int cout, int ksize, long long* elems) {
+  DV_REQUIRE(elems, "null pointer");
+  XeGeom g;
+  DV_REQUIRE(xe_geom(small_desc(nullptr, nullptr, cin, cout, ksize), g, true),
+             "unsupported shape (cin <= 16, cout % 8 == 0 <= 128, odd k <= 15)");
+  *elems = g.image_elems;
+  return DV_OK;
+}
+
+extern "C" int dv_conv_small_pack(const float* wt, const float* bias, int cin, int cout, int ksize,
+                                  void* image, void* stream) {
+  DV_REQUIRE(wt && image, "null pointer");
+  const DvCrossEmbed ce = small_desc(wt, bias, cin, cout, ksize);
+  XeGeom g;
+  DV_REQUIRE(xe_geom(ce, g, true), "unsupported shape");
+  const int blocks = std::min(1024, (g.boff + g.cpad + 255) / 256);
+  xe_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(ce, g, (bf16*)image);
+  return check_launch("conv_small_pack");
+}
+
+extern "C" int dv_conv_small_fwd(const void* x0, int ld0, int c0, const void* x1, int ld1,
+                                 const void* image, const void* res, int ldres, void* y, int ldy,
+                                 int nf, int h, int w, int cin, int cout, int ksize, void* stream) {
+  DV_REQUIRE(x0 && image && y, "null pointer");
+  XeGeom g;
+  DV_REQUIRE(xe_geom(small_desc(nullptr, nullptr, cin, cout, ksize), g, true),
+             "unsupported shape (cin <= 16, cout % 8 == 0 <= 128, odd k <= 15)");
+  const bool two = x1 != nullptr;
+  DV_REQUIRE(!two || (g.cp >= 8 && c0 % 8 == 0 && c0 > 0 && c0 < cin && ld1 % 8 == 0 && ld1 >= cin - c0),
+             "second input needs c0 % 8 == 0 and ld1 % 8 == 0");
+  const int cx0 = two ? c0 : cin;
+  DV_REQUIRE(xe_shape_ok(g, nf, h, w, ld0) && ld0 >= cx0 && (g.cp == 4 || ld0 % 8 == 0),
+             "needs w % 32 == 0 and 16-B aligned pixel rows");
+  DV_REQUIRE(ldy % 4 == 0 && ldy >= cout && (!res || (ldres % 4 == 0 && ldres >= cout)),
+             "ldy / ldres must be multiples of 4");
+  DV_REQUIRE((long long)nf * h * w * std::max({ld0, ld1, ldy, ldres}) < (1ll << 31), "tensor too large");
+  const int rc = xe_fwd_launch(g, image, x0, ld0, x1, ld1, cx0, res, ldres, y, ldy, nf, h, w,
+                               (hipStream_t)stream);
+  if (rc != DV_OK) return rc;
+  return check_launch("conv_small_fwd");
 }
 
 extern "C" int dv_cross_embed_wgrad_ws(const DvCrossEmbed* ce, int nf, int h, int w,
@@ -562,15 +710,15 @@ extern "C" int dv_cross_embed_wgrad(const DvCrossEmbed* ce, const void* dy, int 
   XeGeom g;
   DV_REQUIRE(xe_geom(*ce, g), "unsupported branch set");
   for (int b = 0; b < g.nbranch; ++b) DV_REQUIRE(ce->dw[b], "null weight gradient");
-  DV_REQUIRE(xe_shape_ok(g, nf, h, w, ldx) && lddy % 8 == 0 && lddy >= g.cout,
+  DV_REQUIRE(xe_shape_ok(g, nf, h, w, ldx) && ldx >= g.cin && lddy % 8 == 0 && lddy >= g.cout,
              "needs w % 32 == 0, ldx % (4 or 8) == 0, lddy % 8 == 0");
   long long need = 0;
   dv_cross_embed_wgrad_ws(ce, nf, h, w, &need);
   DV_REQUIRE(ws_floats >= need, "workspace too small (see dv_cross_embed_wgrad_ws)");
   const size_t lds = xe_wgrad_lds(g, w);
   DV_REQUIRE(lds <= 160 * 1024, "LDS footprint too large");
-  // register staging slots: DPT = 4 dY chunks, XPT = 8 window pixels per thread
-  DV_REQUIRE((long long)w * (g.cout / 8) <= 4 * 512 && (long long)g.kmax * (w + g.kmax + 7) <= 8 * 512,
+  // register staging slots: DPT = 4 dY chunks, XPT = 9 window pixels per thread
+  DV_REQUIRE((long long)w * (g.cout / 8) <= 4 * 512 && (long long)g.kmax * (w + g.kmax + 7) <= 9 * 512,
              "image row too wide for the staging slots");
   const int per = (g.items + 7) / 8;
   DV_REQUIRE(per <= 24, "too many accumulator tiles");

@@ -43,6 +43,9 @@ _SIGS = {
     "dv_cross_embed_fwd": [_P, _P, _P, _I, _P, _I, _I, _I, _I, _P],
     "dv_cross_embed_wgrad_ws": [_P, _I, _I, _I, _P],
     "dv_cross_embed_wgrad": [_P, _P, _I, _P, _I, _P, _L, _I, _I, _I, _P],
+    "dv_conv_small_image_elems": [_I, _I, _I, _P],
+    "dv_conv_small_pack": [_P, _P, _I, _I, _I, _P, _P],
+    "dv_conv_small_fwd": [_P, _I, _I, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
     "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "dv_pack_conv_weights_batched": [_P, _I, _L, _P],

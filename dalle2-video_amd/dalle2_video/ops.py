@@ -450,8 +450,10 @@ class PackCache:
 
     def __init__(self):
         self.enabled = False
+        self.static = False  # weights do not change while this cache is current (sampling)
         self.epoch = 0
         self.entries = {}  # key -> dict(out, w, meta, epoch, version)
+        self.small = {}  # small-channel conv images (_small_image)
         self._table = None
         self._table_key = None
 
@@ -526,6 +528,7 @@ class private_pack_cache:
         self.saved = PACK
         PACK = PackCache()
         PACK.enabled = True
+        PACK.static = True
         return PACK
 
     def __exit__(self, *exc):
@@ -641,16 +644,25 @@ class ConvFn(torch.autograd.Function):
         # (tools/gnstats_bench.py): the resident-weight stripe kernel (stage-0/1
         # Block3D convs) and the 8x8 window kernel; elsewhere gn.used = False
         # and the GroupNorm reduces z itself
-        use_win = window_ok(x0, x1, cin, c0 if x1 is not None else cin, cout, ld0, ld1 or ld0, cout,
-                            ldr, ksize, h, w, nf, gn.P if gn is not None else 0)
-        if gn is not None:
+        use_small = small_conv_ok(x0, x1, cin, cin_real, cout, ld0, ld1, ldr, ksize, w)
+        use_win = not use_small and window_ok(x0, x1, cin, c0 if x1 is not None else cin, cout, ld0,
+                                              ld1 or ld0, cout, ldr, ksize, h, w, nf,
+                                              gn.P if gn is not None else 0)
+        if gn is not None and use_small:
+            gn.used = False
+        elif gn is not None:
             name = (f"conv_fwd_frame_kernel<{w}>" if use_win else
                     conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
                                   max(ld0, ld1), ksize, h, w, gn.P))
             gn.used = GnStats.ALL or name in ("conv_fwd_stripe_kernel<64>", "conv_fwd_stripe_kernel<32>",
                                               "conv_fwd_frame_kernel<8>")
         gs, gP, gR = (ptr(gn.cur), gn.P, gn.R) if gn is not None and gn.used else (None, 0, 0)
-        if use_win:
+        if use_small:
+            img = _small_image(weight, b, cin_real, cout, ksize, cache)
+            _launch("xe_fwd_kernel", flops, nbytes,
+                    lambda: call("dv_conv_small_fwd", ptr(x0), ld0, c0, ptr(x1), ld1, ptr(img), ptr(res),
+                                 ldr, ptr(y), cout, nf, h, w, cin_real, cout, ksize, stream()), shape)
+        elif use_win:
             wp = pack_conv_weight(weight, x0.dtype, cin, 2, cache)
             _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                     lambda: call("dv_conv_fwd8", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp),
@@ -802,6 +814,51 @@ class ConvFn(torch.autograd.Function):
         return dx0, dx1, dw, db, dres, None, None, None, None, None
 
 
+# small-channel forward (cin <= 16, cout <= 32: the cascade's 256x256 unet at
+# dim 8) on the direct kernel of dv_xembed.hip; DV_NO_SMALL=1 keeps the
+# implicit GEMM (A/B switch)
+_NO_SMALL = os.environ.get("DV_NO_SMALL", "0") not in ("", "0")
+
+
+def small_conv_ok(x0, x1, cin, cin_real, cout, ld0, ld1, ldr, ksize, w):
+    if _NO_SMALL or x0.dtype != torch.bfloat16 or not x0.is_cuda:
+        return False
+    if not (cin_real <= 16 and cout <= 32 and cout % 8 == 0 and ksize % 2 == 1 and ksize <= 15
+            and w % 32 == 0 and ldr % 4 == 0):
+        return False
+    if x1 is not None:
+        c0 = x0.shape[3]
+        return cin_real == cin and c0 % 8 == 0 and ld0 % 8 == 0 and ld1 % 8 == 0 and cin > 8
+    return ld0 % (4 if cin_real <= 4 else 8) == 0
+
+
+def _small_image(weight, bias, cin, cout, k, cache):
+    """Packed image of a small-channel conv (weights + bias), kept in the
+    current PackCache (torch version counters checked) while its weights
+    cannot change behind torch's back: a sampling region's private cache, or
+    no trainer at all.  Under a trainer's cache (AdamW writes the weights in
+    place) it is rebuilt by every call, so a captured graph repacks on
+    replay."""
+    w = weight.detach()
+    if w.dtype != torch.float32 or not w.is_contiguous():
+        w = w.float().contiguous()
+    keep = cache and (PACK.static or not PACK.enabled) and w.data_ptr() == weight.data_ptr()
+    key = (weight.data_ptr(), tuple(weight.shape), None if bias is None else bias.data_ptr())
+    ver = (weight._version, None if bias is None else bias._version)
+    cache_d = PACK.small
+    if keep:
+        e = cache_d.get(key)
+        if e is not None and e[0] == ver and e[2] is weight:
+            return e[1]
+    n = ctypes.c_longlong(0)
+    call("dv_conv_small_image_elems", cin, cout, k, ctypes.byref(n))
+    img = torch.empty(n.value, dtype=torch.bfloat16, device=weight.device)
+    call("dv_conv_small_pack", ptr(w), ptr(bias), cin, cout, k, ptr(img), stream())
+    if keep:
+        cache_d[key] = (ver, img, weight)
+    return img
+
+
 def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_scale=1.0, gn=None):
     """(1,k,k) 'same' convolution over channels-last frames (weight in torch
     Conv3d layout (cout, cin, 1, k, k) or Linear layout (cout, cin)).
@@ -848,9 +905,13 @@ def cross_embed_ok(x, weights):
     except _lib.DVError:
         return False
     cout = sum(wt.shape[0] for wt in weights)
+    kmax, cp, cpad = max(ks), 4 if cin <= 4 else 8, (cout + 15) // 16 * 16
+    # the weight-gradient kernel's staging slots and LDS (dv_xembed.hip)
+    wgrad_fits = (kmax * (w + kmax + 7) <= 9 * 512 and w * (cout // 8) <= 4 * 512
+                  and 4 * w * (cpad + 8) + 4 * kmax * (w + kmax + 7) * cp <= 160 * 1024)
     return (cin <= 8 and all(wt.shape[1] == cin and wt.dim() == 5 and wt.dtype == torch.float32 for wt in weights)
             and ks == sorted(ks) and all(k % 2 == 1 and k <= 15 for k in ks)
-            and cout % 16 == 0 and cout <= 128 and w % 32 == 0
+            and cout % 8 == 0 and cout <= 128 and w % 32 == 0 and wgrad_fits
             and ld % (4 if cin <= 4 else 8) == 0 and x.data_ptr() % 16 == 0)
 
 

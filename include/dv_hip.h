@@ -110,7 +110,8 @@ int dv_wgrad_reduce_batched(const DvWgradReduceEntry* table, int n, long long bl
  * w[b] / b[b]: torch Conv3d weight (cout_b, cin, 1, k_b, k_b) and bias
  * (f32, b may be NULL).  dw / db (wgrad only): gradients of the same shapes,
  * written or added to (accumulate_w / accumulate_b; db[b] may be NULL).
- * Requirements: k_b odd <= 15 ascending, sum(cout_b) % 16 == 0 and <= 128;
+ * Requirements: k_b odd <= 15 ascending, sum(cout_b) % 8 == 0 and <= 128
+ * (the last 16-channel tile is zero-padded);
  * bf16 activations, w % 32 == 0, ldx % 4 == 0 (cin <= 4) or % 8 == 0,
  * ldy % 4 == 0, lddy % 8 == 0.
  *   dv_cross_embed_pack: weights + biases -> `image` (device, bf16 elements
@@ -135,6 +136,21 @@ int dv_cross_embed_wgrad_ws(const DvCrossEmbed* ce, int nf, int h, int w, long l
 int dv_cross_embed_wgrad(const DvCrossEmbed* ce, const void* dy, int lddy, const void* x,
                          int ldx, float* ws, long long ws_floats, int nf, int h, int w,
                          void* stream);
+
+/* Small-channel (1,k,k) convolution forward on the same direct kernel (the
+ * cascade's 256x256 unet, dim 8: Block3D.project / res_conv with cin <= 16,
+ * cout <= 128, dalle2_video.py:107, 170 — an implicit GEMM with N = 8 runs
+ * its MFMA tiles 1/8 full).  y = conv(cat(x0[:, :c0], x1)) + bias (+ res);
+ * x1 may be NULL (then c0 is ignored), else c0 % 8 == 0.  bf16, w % 32 == 0,
+ * ld0 / ld1 % 8 == 0 (ld0 % 4 with cin <= 4), ldy / ldres % 4 == 0, cout % 8.
+ *   dv_conv_small_pack: torch weight (cout, cin, 1, k, k) f32 + bias (NULL:
+ *     zero) -> image of dv_conv_small_image_elems bf16 elements.           */
+int dv_conv_small_image_elems(int cin, int cout, int ksize, long long* elems);
+int dv_conv_small_pack(const float* w, const float* bias, int cin, int cout, int ksize,
+                       void* image, void* stream);
+int dv_conv_small_fwd(const void* x0, int ld0, int c0, const void* x1, int ld1, const void* image,
+                      const void* res, int ldres, void* y, int ldy, int nf, int h, int w, int cin,
+                      int cout, int ksize, void* stream);
 
 /* 3x3 forward / dgrad, window form (dalle2_video.py:107 Block3D.project at
  * the 8x8 .. 64x64 stages, and the dgrads of those convs): same contract as

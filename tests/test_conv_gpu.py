@@ -36,6 +36,13 @@ CASES = [
     (3, 9, 11, 64, 64, 64, 1),      # dual source, 297 pixels (ragged last tile)
     (2, 6, 6, 64, 0, 128, 1),       # fewer pixels than one tile
     (64, 64, 64, 64, 64, 64, 1),    # the 64x64 up-path res_conv: 2,048 tiles over persistent workgroups
+    # small-channel direct forward (bf16, cin <= 16, cout <= 32, w % 32 == 0: dv_conv_small_fwd)
+    (2, 8, 64, 8, 0, 8, 3),         # the 256x256 unet's dim-8 Block3D conv
+    (2, 5, 32, 8, 8, 8, 3),         # up-path skip concat 8 + 8 (CP 16), 5 rows < one 8-row band
+    (1, 9, 96, 8, 8, 16, 3),        # concat 8 + 8 -> 16, 96 = 3 x 32-column blocks
+    (2, 4, 64, 16, 0, 8, 1),        # 1x1 16 -> 8
+    (1, 6, 32, 16, 0, 24, 7),       # cin 16 (CP 16), second output tile half padded
+    (2, 8, 64, 8, 0, 8, 15),        # 15x15 window
 ]
 
 

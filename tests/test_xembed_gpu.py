@@ -29,6 +29,8 @@ CASES = [
     (8, 32, 32, 3, 8, ((3, 8), (7, 4), (15, 4))),       # Cfg1 (dim 16)
     (4, 64, 128, 6, 8, ((3, 16), (7, 8), (15, 8))),     # upsampler unet: video + lowres cond (CP 8)
     (2, 16, 32, 3, 4, ((3, 64), (7, 32), (15, 32))),    # dim 128, 4-channel pixel stride
+    (4, 16, 256, 6, 8, ((3, 4), (7, 2), (15, 2))),      # Cfg4 unet2 (dim 8): one zero-padded tile
+    (2, 8, 64, 3, 4, ((3, 16), (7, 8))),                # 24 channels: second tile half padded
 ]
 
 
