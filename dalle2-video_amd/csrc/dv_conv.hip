@@ -68,6 +68,9 @@ struct ConvFwdArgs {
   long long gn_P;
   int gn_R;
   long long gn_rstride;
+  // window kernel: output-channel groups the 8 XCDs split into (the other
+  // factor of 8 splits the pixel tiles); 0: one channel block per XCD
+  int xcd_c;
 };
 
 // GroupNorm statistics of a wave's tile, register-light: every lane holds
@@ -1914,9 +1917,20 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int npx = (int)(p.M / 128), nblk = npx * (p.cout / 64);
   int L = blockIdx.x;
-  if (nblk % 8 == 0) L = (L % 8) * (nblk / 8) + L / 8;  // consecutive blocks share an XCD
-  const int co0 = (L / npx) * 64;
-  const long long m0 = (long long)(L % npx) * 128;
+  int co0;
+  long long m0;
+  if (p.xcd_c > 0) {
+    // XCD x = block % 8 takes channel group x / xp and pixel group x % xp: its
+    // L2 holds 1/xc of the weights and 1/xp of the input (host-checked splits)
+    const int xc = p.xcd_c, xp = 8 / xc, x = L % 8, j = L / 8;
+    const int tpc = (p.cout / 64) / xc, ppg = npx / xp;
+    co0 = ((x / xp) * tpc + j / ppg) * 64;
+    m0 = (long long)((x % xp) * ppg + j % ppg) * 128;
+  } else {
+    if (nblk % 8 == 0) L = (L % 8) * (nblk / 8) + L / 8;  // consecutive blocks share an XCD
+    co0 = (L / npx) * 64;
+    m0 = (long long)(L % npx) * 128;
+  }
   const int nch = p.cin / 16;
   const int HW = p.H * W;
   const int y0 = W == 8 ? 0 : (int)((m0 % HW) / W);        // tile's first image row
@@ -2079,7 +2093,29 @@ bool fwd_frame_ok(const ConvFwdArgs<bf16>& a, int h, int w) {
          ((uintptr_t)a.x0 & 15) == 0 && ((uintptr_t)a.x1 & 15) == 0 && ((uintptr_t)a.w & 15) == 0;
 }
 
-int launch_fwd_frame(const ConvFwdArgs<bf16>& a, hipStream_t st) {
+// channel x pixel split of the window conv's tiles over the 8 XCDs that
+// minimises the L2 fill traffic xp * |w| + xc * |x| (each XCD's L2 reads its
+// 1/xc of the weights and 1/xp of the input once); DV_FRAME_XC forces xc
+int frame_xcd_split(const ConvFwdArgs<bf16>& a) {
+  static const int forced = getenv("DV_FRAME_XC") ? atoi(getenv("DV_FRAME_XC")) : -1;
+  const int ntco = a.cout / 64, npx = (int)(a.M / 128);
+  auto ok = [&](int xc) { return ntco % xc == 0 && npx % (8 / xc) == 0; };
+  if (forced == 0) return 0;
+  if (forced > 0) return (forced <= 8 && 8 % forced == 0 && ok(forced)) ? forced : 0;
+  const double wb = (double)a.cout * a.K, xb = (double)a.M * a.cin;
+  int best = 0;
+  double bc = 0;
+  for (int xc = 1; xc <= 8; xc *= 2) {
+    if (!ok(xc)) continue;
+    const double c = (8 / xc) * wb + xc * xb;
+    if (!best || c < bc) { best = xc; bc = c; }
+  }
+  return best;
+}
+
+int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
+  ConvFwdArgs<bf16> a = a0;
+  a.xcd_c = frame_xcd_split(a);
   const int nblk = (int)(a.M / 128) * (a.cout / 64);
   switch (a.W) {
 #define DV_FW(WW) (a.gn_sums ? conv_fwd_frame_kernel<WW, true><<<nblk, 256, 0, st>>>(a) \
