@@ -898,6 +898,64 @@ class _DenoiseStepGraph:
 # ---------------------------------------------------------------------------
 
 
+def _move_module(module, device):
+    """`module.to(device)` for the host <-> GPU moves of one_unet_in_gpu, as ONE
+    copy per dtype through a pinned host buffer kept on the module: the
+    parameters, their gradients and the buffers become views of one flat
+    tensor on the target device (pinned host memory, or a fresh GPU buffer).
+    Module.to() moves ~440 tensors through pageable memory one by one.
+    Other devices / mixed layouts fall back to Module.to()."""
+    device = torch.device(device)
+    ts = []
+    for p in module.parameters():
+        ts.append(p)
+        if p.grad is not None:
+            ts.append(p.grad)
+    ts += [b for b in module.buffers()]
+    if not ts or all(t.device == device for t in ts) or \
+            (device.type == "cuda" and device.index is None and all(t.is_cuda for t in ts)):
+        return
+    src_dev = ts[0].device
+    if device.type not in ("cpu", "cuda") or any(t.device != src_dev for t in ts) or \
+            not torch.cuda.is_available() or (src_dev.type == "cpu") == (device.type == "cpu"):
+        module.to(device)
+        return
+    groups = {}
+    for t in ts:
+        groups.setdefault(t.dtype, []).append(t)
+    cache = module.__dict__.setdefault("_dv_pinned", {})
+    for dt, group in groups.items():
+        n = sum(t.numel() for t in group)
+        if device.type == "cpu":
+            flat = cache.get(dt)
+            if flat is None or flat.numel() != n:
+                flat = cache[dt] = torch.empty(n, dtype=dt, pin_memory=True)
+            gflat = torch.empty(n, dtype=dt, device=src_dev)
+            off = 0
+            for t in group:
+                gflat[off:off + t.numel()].copy_(t.data.reshape(-1))
+                off += t.numel()
+            flat.copy_(gflat, non_blocking=True)
+        else:
+            flat = torch.empty(n, dtype=dt, device=device)
+            cpu_flat = cache.get(dt)
+            if cpu_flat is None or cpu_flat.numel() != n or any(
+                    not _views_of(t, cpu_flat) for t in group):
+                module.to(device)  # not laid out by a previous host move
+                return
+            flat.copy_(cpu_flat, non_blocking=True)
+        off = 0
+        for t in group:
+            t.data = flat[off:off + t.numel()].view(t.shape)
+            off += t.numel()
+    if device.type == "cpu":
+        torch.cuda.current_stream(src_dev).synchronize()  # host views are read-ready
+
+
+def _views_of(t, flat):
+    return t.device.type == "cpu" and t.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr()
+
+
 class VideoDecoder(nn.Module):
     def __init__(self, unet, *, clip=None, frame_size=None, channels=3, vae=tuple(),
                  timesteps=1000, sample_timesteps=None, video_cond_drop_prob=0.1,
@@ -1047,11 +1105,12 @@ class VideoDecoder(nn.Module):
         cuda, cpu = torch.device(cuda), torch.device("cpu")
         self.to(cuda)
         devices = [next(u.parameters()).device for u in self.unets]
-        self.unets.to(cpu)
-        unet.to(cuda)
+        for u in self.unets:
+            _move_module(u, cpu)
+        _move_module(unet, cuda)
         yield
         for u, d in zip(self.unets, devices):
-            u.to(d)
+            _move_module(u, d)
 
     # ---- training (p_losses, dalle2_video.py:1908-2006) -------------------
     def p_losses(self, unet, x_start, times, *, video_embed, noise_scheduler,
