@@ -172,6 +172,24 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
     }
   };
   long long p0 = beg + rr;
+  // MODE 1: the parameter / statistics loads go out BEFORE the data batch
+  // (global loads return in order: issued after it they would wait for it)
+  const bool pre = MODE == 1 && a.C <= 512;
+  float pg[2] = {0.f, 0.f}, pbt[2] = {0.f, 0.f}, psc[2] = {1.f, 1.f}, psh[2] = {0.f, 0.f};
+  float mu_r = 0.f, rs_r = 0.f;
+  if (pre) {
+    const float* ssb = a.ss ? a.ss + (long long)b * 2 * a.C : nullptr;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = tid + 256 * k;
+      if (c < a.C) {
+        pg[k] = a.gamma[c];
+        pbt[k] = a.beta[c];
+        if (ssb) { psc[k] = 1.f + ssb[c]; psh[k] = ssb[a.C + c]; }
+      }
+    }
+    if (tid < a.G) { mu_r = a.mean[b * a.G + tid]; rs_r = a.rstd[b * a.G + tid]; }
+  }
   load(p0, cur);  // in flight across the prologue
   if (MODE == 1 && !a.accumulate && blockIdx.x == 0 && b == 0) {  // the apply atomically adds
     for (int c = tid; c < a.C; c += 256) {
@@ -180,8 +198,22 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
     }
   }
   if (MODE == 1) {
-    stage_params(a, b, prm);
-    for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
+    if (pre) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int c = tid + 256 * k;
+        if (c < a.C) {
+          prm[c] = pg[k];
+          prm[a.C + c] = pbt[k];
+          prm[2 * a.C + c] = psc[k];
+          prm[3 * a.C + c] = psh[k];
+        }
+      }
+      if (tid < a.G) { smu[tid] = mu_r; srs[tid] = rs_r; }
+    } else {
+      stage_params(a, b, prm);
+      for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
+    }
     __syncthreads();
   }
   f2 s1[VEC / 2], s2[VEC / 2];
@@ -280,8 +312,10 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
 // then one wave per group (channel sums combined in double for the variance).
 //   MODE 0: t1 = mean, t2 = rstd      MODE 1: t1 = m1, t2 = m2
 template <int MODE>
+__device__ void gn_group_math(const GnArgs& a, const float* cs, const float* prm, float* t1, float* t2);
+
+template <int MODE>
 __device__ void gn_group_terms(const GnArgs& a, int b, float* cs, float* prm, float* t1, float* t2) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cg = a.C / a.G;
   const long long sb = (long long)b * a.C * 2;
   for (int c = threadIdx.x; c < a.C; c += 256) {
     float v1 = 0.f, v2 = 0.f;
@@ -299,6 +333,64 @@ __device__ void gn_group_terms(const GnArgs& a, int b, float* cs, float* prm, fl
   }
   stage_params(a, b, prm);
   __syncthreads();
+  gn_group_math<MODE>(a, cs, prm, t1, t2);
+}
+
+// The same prologue in two halves (C <= 512, R <= 8): gn_terms_issue puts the
+// sums / parameter loads in flight BEFORE the caller issues its first data
+// batch, gn_terms_finish consumes them.  Global loads return in order, so
+// issued after the data batch they would wait for it (~2.5 us per apply
+// launch measured with the prologue stubbed out).
+struct GnTermRegs {
+  f2 s[2][8];
+  float gm[2], bt[2], sc[2], sh[2];
+};
+__device__ __forceinline__ bool gn_terms_split_ok(const GnArgs& a) { return a.C <= 512 && a.R <= 8; }
+
+__device__ __forceinline__ void gn_terms_issue(const GnArgs& a, int b, GnTermRegs& r) {
+  const long long sb = (long long)b * a.C * 2;
+  const float* ssb = a.ss ? a.ss + (long long)b * 2 * a.C : nullptr;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    if (c < a.C) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < a.R) r.s[k][q] = *(const f2*)(a.sums + q * a.rstride + sb + 2 * c);
+      r.gm[k] = a.gamma[c];
+      r.bt[k] = a.beta[c];
+      r.sc[k] = ssb ? 1.f + ssb[c] : 1.f;
+      r.sh[k] = ssb ? ssb[a.C + c] : 0.f;
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void gn_terms_finish(const GnArgs& a, const GnTermRegs& r, float* cs, float* prm,
+                                                float* t1, float* t2) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    if (c < a.C) {
+      float v1 = 0.f, v2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < a.R) { v1 += r.s[k][q][0]; v2 += r.s[k][q][1]; }
+      cs[c] = v1;
+      cs[a.C + c] = v2;
+      prm[c] = r.gm[k];
+      prm[a.C + c] = r.bt[k];
+      prm[2 * a.C + c] = r.sc[k];
+      prm[3 * a.C + c] = r.sh[k];
+    }
+  }
+  __syncthreads();
+  gn_group_math<MODE>(a, cs, prm, t1, t2);
+}
+
+template <int MODE>
+__device__ void gn_group_math(const GnArgs& a, const float* cs, const float* prm, float* t1, float* t2) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cg = a.C / a.G;
   for (int g = wave; g < a.G; g += 4) {
     if (MODE == 0) {
       double s1 = 0.0, s2 = 0.0;
@@ -367,10 +459,15 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
     }
   };
   long long p0 = beg + rr;
+  const bool split = gn_terms_split_ok(a);
+  GnTermRegs tr;
+  float mu_r = 0.f, rs_r = 0.f;
+  if (split) gn_terms_issue(a, b, tr);  // older than the data batch: returns first
+  if (MODE == 1 && tid < a.G) { mu_r = a.mean[b * a.G + tid]; rs_r = a.rstd[b * a.G + tid]; }
   load(p0, zc, xc);  // the first batch is in flight across the prologue
-  gn_group_terms<MODE>(a, b, cs, prm, t1, t2);
-  if (MODE == 1)
-    for (int g = tid; g < a.G; g += 256) { smu[g] = a.mean[b * a.G + g]; srs[g] = a.rstd[b * a.G + g]; }
+  if (split) gn_terms_finish<MODE>(a, tr, cs, prm, t1, t2);
+  else gn_group_terms<MODE>(a, b, cs, prm, t1, t2);
+  if (MODE == 1 && tid < a.G) { smu[tid] = mu_r; srs[tid] = rs_r; }
   __syncthreads();
   if (blockIdx.x == 0) {
     if (MODE == 0) {  // saved for the backward
