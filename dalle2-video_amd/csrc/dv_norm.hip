@@ -59,6 +59,7 @@ struct GnArgs {
   float *dgamma, *dbeta, *dss;
   int accumulate;
   long long rows_per_block;
+  int exp;  // timing experiments only (DV_GN_EXP): 1 no prologue math, 2 no `next` zeroing, 4 no block-0 section
 };
 
 // Per-thread fixed channel vector [cv, cv+VEC) of batch b = blockIdx.y; the
@@ -159,16 +160,19 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   const T* zb = (const T*)a.z + (long long)b * a.P * a.ldz + cv;
   const T* dyb = (const T*)a.dy + (long long)b * a.P * a.lddy + cv;
   const bool act_rows = rr < rpp;
-  // batch loads (rows p0 + u*rpp), issued one batch ahead of their use
+  // batch loads (rows p0 + u*rpp), issued one batch ahead of their use.
+  // Unconditional, with the row clamped to the last one: a load under a
+  // per-lane branch makes the compiler wait for ALL outstanding loads
+  // (vmcnt(0)) at the branch join, which serialised the U rows in flight.
+  // Clamped lanes read the same line (coalesced, ~free) and are not summed.
   u32x4 cur[NL][U], nxt[NL][U];
   auto load = [&](long long p0, u32x4 (&buf)[NL][U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long long p = p0 + (long long)u * rpp;
-      if (act_rows && p < end) {
-        buf[0][u] = *(const u32x4*)(zb + p * a.ldz);
-        if (MODE == 1) buf[NL - 1][u] = *(const u32x4*)(dyb + p * a.lddy);
-      }
+      long long p = p0 + (long long)u * rpp;
+      p = p < end ? p : end - 1;
+      buf[0][u] = *(const u32x4*)(zb + p * a.ldz);
+      if (MODE == 1) buf[NL - 1][u] = *(const u32x4*)(dyb + p * a.lddy);
     }
   };
   long long p0 = beg + rr;
@@ -177,18 +181,22 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   const bool pre = MODE == 1 && a.C <= 512;
   float pg[2] = {0.f, 0.f}, pbt[2] = {0.f, 0.f}, psc[2] = {1.f, 1.f}, psh[2] = {0.f, 0.f};
   float mu_r = 0.f, rs_r = 0.f;
-  if (pre) {
-    const float* ssb = a.ss ? a.ss + (long long)b * 2 * a.C : nullptr;
+  if (pre) {  // unconditional loads from clamped indices (see load() below)
+    const bool has_ss = a.ss != nullptr;
+    const float* scp = has_ss ? a.ss + (long long)b * 2 * a.C : a.gamma;
+    const float* shp = has_ss ? scp + a.C : a.gamma;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const int c = tid + 256 * k;
-      if (c < a.C) {
-        pg[k] = a.gamma[c];
-        pbt[k] = a.beta[c];
-        if (ssb) { psc[k] = 1.f + ssb[c]; psh[k] = ssb[a.C + c]; }
-      }
+      int c = tid + 256 * k;
+      c = c < a.C ? c : a.C - 1;
+      pg[k] = a.gamma[c];
+      pbt[k] = a.beta[c];
+      psc[k] = scp[c];  // raw (selected after the data batch is issued)
+      psh[k] = shp[c];
     }
-    if (tid < a.G) { mu_r = a.mean[b * a.G + tid]; rs_r = a.rstd[b * a.G + tid]; }
+    const int g = tid < a.G ? tid : a.G - 1;
+    mu_r = a.mean[b * a.G + g];
+    rs_r = a.rstd[b * a.G + g];
   }
   load(p0, cur);  // in flight across the prologue
   if (MODE == 1 && !a.accumulate && blockIdx.x == 0 && b == 0) {  // the apply atomically adds
@@ -205,8 +213,8 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
         if (c < a.C) {
           prm[c] = pg[k];
           prm[a.C + c] = pbt[k];
-          prm[2 * a.C + c] = psc[k];
-          prm[3 * a.C + c] = psh[k];
+          prm[2 * a.C + c] = a.ss ? 1.f + psc[k] : 1.f;
+          prm[3 * a.C + c] = a.ss ? psh[k] : 0.f;
         }
       }
       if (tid < a.G) { smu[tid] = mu_r; srs[tid] = rs_r; }
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
       k2.set(k);
     }
     for (; p0 < end; p0 += step) {
-      if (p0 + step < end) load(p0 + step, nxt);
+      load(p0 + step, nxt);  // past the end: clamped re-reads of the last row
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (p0 + (long long)u * rpp >= end) break;
@@ -347,21 +355,28 @@ struct GnTermRegs {
 };
 __device__ __forceinline__ bool gn_terms_split_ok(const GnArgs& a) { return a.C <= 512 && a.R <= 8; }
 
+// Every load is unconditional (channel and replica indices clamped, the FiLM
+// pointer swapped for a dummy when absent): a load under a lane branch makes
+// the compiler wait for all outstanding loads at the join, which held the
+// data batch's issue behind these loads' full latency.
 __device__ __forceinline__ void gn_terms_issue(const GnArgs& a, int b, GnTermRegs& r) {
   const long long sb = (long long)b * a.C * 2;
-  const float* ssb = a.ss ? a.ss + (long long)b * 2 * a.C : nullptr;
+  const bool has_ss = a.ss != nullptr;
+  const float* scp = has_ss ? a.ss + (long long)b * 2 * a.C : a.gamma;
+  const float* shp = has_ss ? scp + a.C : a.gamma;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const int c = threadIdx.x + 256 * k;
-    if (c < a.C) {
+    int c = threadIdx.x + 256 * k;
+    c = c < a.C ? c : a.C - 1;
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (q < a.R) r.s[k][q] = *(const f2*)(a.sums + q * a.rstride + sb + 2 * c);
-      r.gm[k] = a.gamma[c];
-      r.bt[k] = a.beta[c];
-      r.sc[k] = ssb ? 1.f + ssb[c] : 1.f;
-      r.sh[k] = ssb ? ssb[a.C + c] : 0.f;
+    for (int q = 0; q < 8; ++q) {
+      const int qq = q < a.R ? q : a.R - 1;
+      r.s[k][q] = *(const f2*)(a.sums + qq * a.rstride + sb + 2 * c);
     }
+    r.gm[k] = a.gamma[c];
+    r.bt[k] = a.beta[c];
+    r.sc[k] = scp[c];  // raw: any arithmetic here would wait for the load before
+    r.sh[k] = shp[c];  // the caller's data batch is issued (gn_terms_finish selects)
   }
 }
 
@@ -380,8 +395,8 @@ __device__ __forceinline__ void gn_terms_finish(const GnArgs& a, const GnTermReg
       cs[a.C + c] = v2;
       prm[c] = r.gm[k];
       prm[a.C + c] = r.bt[k];
-      prm[2 * a.C + c] = r.sc[k];
-      prm[3 * a.C + c] = r.sh[k];
+      prm[2 * a.C + c] = a.ss ? 1.f + r.sc[k] : 1.f;
+      prm[3 * a.C + c] = a.ss ? r.sh[k] : 0.f;
     }
   }
   __syncthreads();
@@ -426,9 +441,179 @@ __device__ void gn_group_math(const GnArgs& a, const float* cs, const float* prm
   }
 }
 
+// --------------------------------------------------------------------------
+// Register-only apply prologue (DIRECT): no LDS, no workgroup barrier.
+// A thread owns the VEC channels [cv, cv+VEC) of one group.  The lanes of a
+// wave that hold the same channel vector (row slots, tpr lanes apart) split
+// the R sums replicas between them; xor shuffles then fold the replicas
+// (offsets tpr .. 32) and the group's tpc = cg/VEC channel vectors (offsets
+// 1 .. tpc/2).  Valid when tpr = C/VEC is a power of two <= 64, cg % VEC == 0
+// and R <= GN_DQ * (64 / tpr).  Every load is issued by gn_direct_issue
+// before the caller's first data batch (loads return in order).
+// --------------------------------------------------------------------------
+constexpr int GN_DQ = 4;  // sums replicas loaded per thread (at most)
+template <int VEC, int DQ>
+struct GnDirRegs {
+  f32x4 s[DQ][VEC / 2];     // (sum1, sum2) of VEC channels, DQ replicas
+  f32x4 gm[VEC / 4], bt[VEC / 4], sc[VEC / 4], sh[VEC / 4];
+  float mu, rs;             // MODE 1: the forward's group statistics
+};
+
+__host__ __device__ inline bool gn_direct_ok(const GnArgs& a, int vec) {
+  const int tpr = a.C / vec, cg = a.C / a.G;
+  return tpr <= 64 && (tpr & (tpr - 1)) == 0 && cg % vec == 0 && a.R <= GN_DQ * (64 / tpr);
+}
+
+// replicas each thread loads: ceil(R / (64 / tpr)), as 1, 2 or 4
+__host__ __device__ inline int gn_direct_dq(const GnArgs& a, int vec) {
+  const int rw = 64 / (a.C / vec), nq = (a.R + rw - 1) / rw;
+  return nq <= 1 ? 1 : nq <= 2 ? 2 : 4;
+}
+
+template <int VEC, int MODE, int DQ>
+__device__ __forceinline__ void gn_direct_issue(const GnArgs& a, int b, int cv, GnDirRegs<VEC, DQ>& r) {
+  const int lane = threadIdx.x & 63, tpr = a.C / VEC, rw = 64 / tpr, qi = lane / tpr;
+  const float* sb = a.sums + ((long long)b * a.C + cv) * 2;
+#pragma unroll
+  for (int i = 0; i < DQ; ++i) {
+    int q = qi + rw * i;
+    q = q < a.R ? q : a.R - 1;  // clamped (weighted 0 in finish): unconditional loads
+#pragma unroll
+    for (int v = 0; v < VEC / 2; ++v) r.s[i][v] = *(const f32x4*)(sb + q * a.rstride + 4 * v);
+  }
+  const bool has_ss = a.ss != nullptr;
+  const float* scp = has_ss ? a.ss + (long long)b * 2 * a.C + cv : a.gamma + cv;
+  const float* shp = has_ss ? scp + a.C : a.gamma + cv;
+#pragma unroll
+  for (int v = 0; v < VEC / 4; ++v) {
+    r.gm[v] = *(const f32x4*)(a.gamma + cv + 4 * v);
+    r.bt[v] = *(const f32x4*)(a.beta + cv + 4 * v);
+    r.sc[v] = *(const f32x4*)(scp + 4 * v);
+    r.sh[v] = *(const f32x4*)(shp + 4 * v);
+  }
+  if (MODE == 1) {
+    const int g = cv / (a.C / a.G);
+    r.mu = a.mean[b * a.G + g];
+    r.rs = a.rstd[b * a.G + g];
+  }
+}
+
+// xor-fold over lanes `lo, 2lo, .. < hi`
+template <typename V>
+__device__ __forceinline__ V lane_fold(V v, int lo, int hi) {
+  for (int o = lo; o < hi; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Per-channel coefficients of the thread's VEC channels (and, MODE 1, the
+// negated m1/m2 terms); block 0 of each clip also writes the saved statistics
+// (MODE 0) or this clip's FiLM gradients and its dgamma/dbeta share (MODE 1).
+template <int VEC, int MODE, int DQ>
+__device__ __forceinline__ void gn_direct_finish(const GnArgs& a, int b, int cv, int rr,
+                                                 const GnDirRegs<VEC, DQ>& r, ChanCoef* k, f2* m1, f2* m2) {
+  const int lane = threadIdx.x & 63, tpr = a.C / VEC, rw = 64 / tpr, qi = lane / tpr;
+  const int cg = a.C / a.G, tpc = cg / VEC, g = cv / cg;
+  // this lane's replica slice, per channel
+  float s1[VEC], s2[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) s1[e] = s2[e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < DQ; ++i) {
+    const float w = qi + rw * i < a.R ? 1.f : 0.f;
+#pragma unroll
+    for (int v = 0; v < VEC / 2; ++v) {
+      s1[2 * v] += w * r.s[i][v][0];
+      s2[2 * v] += w * r.s[i][v][1];
+      s1[2 * v + 1] += w * r.s[i][v][2];
+      s2[2 * v + 1] += w * r.s[i][v][3];
+    }
+  }
+  float gm[VEC], bt[VEC], sc[VEC], sh[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    gm[e] = r.gm[e / 4][e % 4];
+    bt[e] = r.bt[e / 4][e % 4];
+    sc[e] = a.ss ? 1.f + r.sc[e / 4][e % 4] : 1.f;
+    sh[e] = a.ss ? r.sh[e / 4][e % 4] : 0.f;
+  }
+  const double n = (double)a.P * cg;
+  float mu, rs;
+  if (MODE == 0) {
+    double d1 = 0.0, d2 = 0.0;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) { d1 += s1[e]; d2 += s2[e]; }
+    d1 = lane_fold(lane_fold(d1, tpr, 64), 1, tpc);
+    d2 = lane_fold(lane_fold(d2, tpr, 64), 1, tpc);
+    const double m = d1 / n;
+    double var = d2 / n - m * m;
+    if (var < 0) var = 0;
+    mu = (float)m;
+    rs = (float)(1.0 / sqrt(var + (double)a.eps));
+    if (blockIdx.x == 0 && !(a.exp & 4) && rr == 0 && (lane % tpr) % tpc == 0) {
+      a.mean[b * a.G + g] = mu;
+      a.rstd[b * a.G + g] = rs;
+    }
+  } else {
+    mu = r.mu;
+    rs = r.rs;
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const float kk = gm[e] * sc[e];
+      t1 += kk * s1[e];
+      t2 += kk * s2[e];
+    }
+    t1 = lane_fold(lane_fold(t1, tpr, 64), 1, tpc) / (float)n;
+    t2 = lane_fold(lane_fold(t2, tpr, 64), 1, tpc) / (float)n;
+#pragma unroll
+    for (int j = 0; j < VEC / 2; ++j) {
+      m1[j] = f2{-rs * t1, -rs * t1};
+      m2[j] = f2{-rs * t2, -rs * t2};
+    }
+    if (blockIdx.x == 0 && !(a.exp & 4)) {  // wave-uniform: every lane joins the folds
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        s1[e] = lane_fold(s1[e], tpr, 64);
+        s2[e] = lane_fold(s2[e], tpr, 64);
+      }
+      if (rr == 0) {  // one lane per channel vector of the clip
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const int c = cv + e;
+          if (a.dss) {
+            a.dss[(long long)b * 2 * a.C + c] = gm[e] * s2[e] + bt[e] * s1[e];  // d scale
+            a.dss[(long long)b * 2 * a.C + a.C + c] = s1[e];                    // d shift
+          }
+          if (a.dgamma) atomicAdd(a.dgamma + c, sc[e] * s2[e]);
+          if (a.dbeta) atomicAdd(a.dbeta + c, sc[e] * s1[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    k[e].A = rs * gm[e] * sc[e];
+    k[e].B = (bt[e] - mu * rs * gm[e]) * sc[e] + sh[e];
+    k[e].rs = rs;
+    k[e].zb = -mu * rs;
+    k[e].K1 = rs * sc[e] * gm[e];
+  }
+}
+
+// the next GroupNorm call's sums start at zero (spread over the grid)
+__device__ __forceinline__ void gn_zero_next(const GnArgs& a) {
+  const long long nblk = (long long)gridDim.x * gridDim.y;
+  const long long per = ((a.next_n + nblk - 1) / nblk + 3) / 4 * 4;
+  const long long i0 = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * per;
+  for (long long i = i0 + threadIdx.x * 4; i < i0 + per && i < a.next_n; i += 1024) {
+    if (i + 4 <= a.next_n) *(f32x4*)(a.next + i) = f32x4{0.f, 0.f, 0.f, 0.f};
+    else for (long long j = i; j < a.next_n; ++j) a.next[j] = 0.f;
+  }
+}
+
 // MODE 0: forward apply  out = act(v) (+ res)
 // MODE 1: backward apply out = dz = rs*(dv*(1+s)*g - m1 - zhat*m2)
-template <typename T, int MODE, int U, bool SILU>
+template <typename T, int MODE, int U, bool SILU, bool RES, int DQ>  // DQ 0: LDS prologue
 __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float t1[64], t2[64], smu[64], srs[64];
@@ -444,32 +629,59 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   const long long pb = (long long)b * a.P;
   const long long step = (long long)rpp * U;
   const bool act_rows = rr < rpp;
-  const bool has_x = MODE == 1 || a.res != nullptr;  // second stream: dy (bwd) or res (fwd)
+  constexpr bool has_x = MODE == 1 || RES;  // second stream: dy (bwd) or res (fwd)
   const T* xsrc = MODE == 1 ? (const T*)a.dy : (const T*)a.res;
   const int ldx = MODE == 1 ? a.lddy : a.ldres;
   u32x4 zc[U], xc[U], zn[U], xn[U];
+  // unconditional loads, row clamped to the last one (see gn_reduce_kernel):
+  // no lane branch around a load, so the U rows really are in flight at once
   auto load = [&](long long p0, u32x4 (&zb)[U], u32x4 (&xb)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long long p = p0 + (long long)u * rpp;
-      if (act_rows && p < end) {
-        zb[u] = *(const u32x4*)((const T*)a.z + (pb + p) * a.ldz + cv);
-        if (has_x) xb[u] = *(const u32x4*)(xsrc + (pb + p) * ldx + cv);
-      }
+      long long p = p0 + (long long)u * rpp;
+      p = p < end ? p : end - 1;
+      zb[u] = *(const u32x4*)((const T*)a.z + (pb + p) * a.ldz + cv);
+      if (has_x) xb[u] = *(const u32x4*)(xsrc + (pb + p) * ldx + cv);
     }
   };
   long long p0 = beg + rr;
+  Coef2<VEC> k2;
+  f2 m1[VEC / 2], m2[VEC / 2];
+  if constexpr (DQ > 0) {
+    GnDirRegs<VEC, DQ> dr;
+    gn_direct_issue<VEC, MODE, DQ>(a, b, cv, dr);
+    __builtin_amdgcn_sched_barrier(0);  // prologue loads ahead of the data batch
+    load(p0, zc, xc);
+    ChanCoef k[VEC];
+    if (!(a.exp & 1)) gn_direct_finish<VEC, MODE, DQ>(a, b, cv, rr, dr, k, m1, m2);
+    k2.set(k);
+    if (a.next && !(a.exp & 2)) gn_zero_next(a);
+    if (!act_rows) return;
+  } else {
   const bool split = gn_terms_split_ok(a);
   GnTermRegs tr;
   float mu_r = 0.f, rs_r = 0.f;
-  if (split) gn_terms_issue(a, b, tr);  // older than the data batch: returns first
-  if (MODE == 1 && tid < a.G) { mu_r = a.mean[b * a.G + tid]; rs_r = a.rstd[b * a.G + tid]; }
+  // older than the data batch: returns first.  Issued unconditionally (indices
+  // clamped; unused when !split): under a branch, its join waited for them.
+  gn_terms_issue(a, b, tr);
+  if (MODE == 1) {
+    const int g = tid < a.G ? tid : a.G - 1;
+    mu_r = a.mean[b * a.G + g];
+    rs_r = a.rstd[b * a.G + g];
+  }
+  // keep the prologue loads ahead of the data batch in the machine schedule
+  // (they return in order), and consume them on every path so the IR cannot
+  // sink them into the `split` branch below the batch either
+  __builtin_amdgcn_sched_barrier(0);
   load(p0, zc, xc);  // the first batch is in flight across the prologue
-  if (split) gn_terms_finish<MODE>(a, tr, cs, prm, t1, t2);
-  else gn_group_terms<MODE>(a, b, cs, prm, t1, t2);
+  if (!(a.exp & 1)) gn_terms_finish<MODE>(a, tr, cs, prm, t1, t2);
+  if (!split) {  // C > 512 or R > 8: redo from all replicas (not on the Cfg2 path)
+    __syncthreads();
+    gn_group_terms<MODE>(a, b, cs, prm, t1, t2);
+  }
   if (MODE == 1 && tid < a.G) { smu[tid] = mu_r; srs[tid] = rs_r; }
   __syncthreads();
-  if (blockIdx.x == 0) {
+  if (blockIdx.x == 0 && !(a.exp & 4)) {
     if (MODE == 0) {  // saved for the backward
       for (int g = tid; g < a.G; g += 256) { a.mean[b * a.G + g] = t1[g]; a.rstd[b * a.G + g] = t2[g]; }
     } else {  // this sample's FiLM gradients; its share of dgamma / dbeta (zeroed by the reduce)
@@ -486,18 +698,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
       }
     }
   }
-  if (a.next) {  // the next GroupNorm call's sums start at zero (spread over the grid)
-    const long long nblk = (long long)gridDim.x * gridDim.y;
-    const long long per = ((a.next_n + nblk - 1) / nblk + 3) / 4 * 4;
-    const long long i0 = ((long long)b * gridDim.x + blockIdx.x) * per;
-    for (long long i = i0 + tid * 4; i < i0 + per && i < a.next_n; i += 1024) {
-      if (i + 4 <= a.next_n) *(f32x4*)(a.next + i) = f32x4{0.f, 0.f, 0.f, 0.f};
-      else for (long long j = i; j < a.next_n; ++j) a.next[j] = 0.f;
-    }
-  }
+  if (a.next && !(a.exp & 2)) gn_zero_next(a);
   if (!act_rows) return;
-  Coef2<VEC> k2;
-  f2 m1[VEC / 2], m2[VEC / 2];
   {
     ChanCoef k[VEC];
     float n1[VEC], n2[VEC];
@@ -519,8 +721,9 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
     }
     k2.set(k);
   }
+  }  // DQ == 0
   for (; p0 < end; p0 += step) {
-    if (p0 + step < end) load(p0 + step, zn, xn);
+    load(p0 + step, zn, xn);  // past the end: clamped re-reads of the last row
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long p = p0 + (long long)u * rpp;
@@ -637,17 +840,29 @@ void gn_reduce_launch(GnArgs& a, int u, long long target, hipStream_t st) {
 template <typename T, int MODE>
 void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
+  static const int exp = getenv("DV_GN_EXP") ? atoi(getenv("DV_GN_EXP")) : 0;
+  a.exp = exp;
   a.rows_per_block = gn_rows(a, VEC, u, target);
   dim3 g((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   const bool silu = a.act == DV_ACT_SILU;
-#define DV_GN_APP(UU) (silu ? gn_apply_kernel<T, MODE, UU, true><<<g, 256, 0, st>>>(a) \
-                            : gn_apply_kernel<T, MODE, UU, false><<<g, 256, 0, st>>>(a))
+  const bool res = MODE == 0 && a.res != nullptr;
+  // A/B: DV_GN_DIRECT bit 0 forward, bit 1 backward (register prologue; else LDS)
+  static const int dflag = getenv("DV_GN_DIRECT") ? atoi(getenv("DV_GN_DIRECT")) : 1;
+  const int dq = sizeof(T) == 2 && (dflag >> MODE & 1) && gn_direct_ok(a, VEC) ? gn_direct_dq(a, VEC) : 0;
+#define DV_GN_APP2(UU, D)                                                            \
+  (silu ? (res ? gn_apply_kernel<T, MODE, UU, true, true, D><<<g, 256, 0, st>>>(a)    \
+               : gn_apply_kernel<T, MODE, UU, true, false, D><<<g, 256, 0, st>>>(a))  \
+        : (res ? gn_apply_kernel<T, MODE, UU, false, true, D><<<g, 256, 0, st>>>(a)   \
+               : gn_apply_kernel<T, MODE, UU, false, false, D><<<g, 256, 0, st>>>(a)))
+#define DV_GN_APP(UU) \
+  (dq == 1 ? DV_GN_APP2(UU, 1) : dq == 2 ? DV_GN_APP2(UU, 2) : dq == 4 ? DV_GN_APP2(UU, 4) : DV_GN_APP2(UU, 0))
   switch (u) {
     case 2: DV_GN_APP(2); break;
     case 8: DV_GN_APP(8); break;
     default: DV_GN_APP(4); break;
   }
 #undef DV_GN_APP
+#undef DV_GN_APP2
 }
 
 template <typename T>
