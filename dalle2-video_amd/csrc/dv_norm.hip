@@ -141,7 +141,7 @@ __device__ __forceinline__ float silu_grad(float v) {
 // stay lightly contended.
 constexpr int GN_U = 4;
 
-template <typename T, int MODE, int U, bool SILU>
+template <typename T, int MODE, int U, bool SILU, bool DIR>  // DIR: MODE 1 register prologue
 __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int NL = MODE == 1 ? 2 : 1;  // tensors streamed (z, dy)
@@ -178,6 +178,43 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
   long long p0 = beg + rr;
   // MODE 1: the parameter / statistics loads go out BEFORE the data batch
   // (global loads return in order: issued after it they would wait for it)
+  ChanCoef kd[VEC];  // DIR: this thread's coefficients, straight from registers
+  if constexpr (MODE == 1 && DIR) {
+    // the VEC channels [cv, cv+VEC) lie in one group (cg % VEC == 0): the
+    // thread loads its own parameters and its group's statistics -- no LDS
+    // staging, no barrier
+    const bool has_ss = a.ss != nullptr;
+    const float* scp = has_ss ? a.ss + (long long)b * 2 * a.C + cv : a.gamma + cv;
+    const float* shp = has_ss ? scp + a.C : a.gamma + cv;
+    f32x4 gm[VEC / 4], bt[VEC / 4], sc[VEC / 4], sh[VEC / 4];
+#pragma unroll
+    for (int v = 0; v < VEC / 4; ++v) {
+      gm[v] = *(const f32x4*)(a.gamma + cv + 4 * v);
+      bt[v] = *(const f32x4*)(a.beta + cv + 4 * v);
+      sc[v] = *(const f32x4*)(scp + 4 * v);
+      sh[v] = *(const f32x4*)(shp + 4 * v);
+    }
+    const int g = cv / (a.C / a.G);
+    const float mu = a.mean[b * a.G + g], rs = a.rstd[b * a.G + g];
+    __builtin_amdgcn_sched_barrier(0);
+    load(p0, cur);  // in flight across the prologue
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const float gme = gm[e / 4][e % 4], bte = bt[e / 4][e % 4];
+      const float sce = has_ss ? 1.f + sc[e / 4][e % 4] : 1.f, she = has_ss ? sh[e / 4][e % 4] : 0.f;
+      kd[e].A = rs * gme * sce;
+      kd[e].B = (bte - mu * rs * gme) * sce + she;
+      kd[e].rs = rs;
+      kd[e].zb = -mu * rs;
+      kd[e].K1 = 0.f;
+    }
+    if (!a.accumulate && blockIdx.x == 0 && b == 0) {  // the apply atomically adds
+      for (int c = tid; c < a.C; c += 256) {
+        if (a.dgamma) a.dgamma[c] = 0.f;
+        if (a.dbeta) a.dbeta[c] = 0.f;
+      }
+    }
+  } else {
   const bool pre = MODE == 1 && a.C <= 512;
   float pg[2] = {0.f, 0.f}, pbt[2] = {0.f, 0.f}, psc[2] = {1.f, 1.f}, psh[2] = {0.f, 0.f};
   float mu_r = 0.f, rs_r = 0.f;
@@ -224,12 +261,15 @@ __global__ __launch_bounds__(256) void gn_reduce_kernel(GnArgs a) {
     }
     __syncthreads();
   }
+  }
   f2 s1[VEC / 2], s2[VEC / 2];
 #pragma unroll
   for (int j = 0; j < VEC / 2; ++j) s1[j] = s2[j] = f2{0.f, 0.f};
   if (act_rows) {
     Coef2<VEC> k2;
-    if (MODE == 1) {
+    if constexpr (MODE == 1 && DIR) {
+      k2.set(kd);
+    } else if (MODE == 1) {
       ChanCoef k[VEC];
       load_coef<VEC>(a, cv, smu, srs, prm, k);
       k2.set(k);
@@ -827,14 +867,19 @@ void gn_reduce_launch(GnArgs& a, int u, long long target, hipStream_t st) {
   dim3 g((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   a.R = gn_replicas(a, (int)g.x);
   const bool silu = a.act == DV_ACT_SILU;
-#define DV_GN_RED(UU) (silu ? gn_reduce_kernel<T, MODE, UU, true><<<g, 256, 0, st>>>(a) \
-                            : gn_reduce_kernel<T, MODE, UU, false><<<g, 256, 0, st>>>(a))
+  // A/B: DV_GN_DIRECT bit 2 (default on): the backward reduce's register prologue
+  static const int dflag = getenv("DV_GN_DIRECT") ? atoi(getenv("DV_GN_DIRECT")) : 5;
+  const bool dir = MODE == 1 && (dflag & 4) && (a.C / a.G) % VEC == 0;
+#define DV_GN_RED2(UU, D) (silu ? gn_reduce_kernel<T, MODE, UU, true, D><<<g, 256, 0, st>>>(a) \
+                                : gn_reduce_kernel<T, MODE, UU, false, D><<<g, 256, 0, st>>>(a))
+#define DV_GN_RED(UU) (dir ? DV_GN_RED2(UU, true) : DV_GN_RED2(UU, false))
   switch (u) {
     case 2: DV_GN_RED(2); break;
     case 4: DV_GN_RED(4); break;
     default: DV_GN_RED(8); break;
   }
 #undef DV_GN_RED
+#undef DV_GN_RED2
 }
 
 template <typename T, int MODE>
@@ -846,8 +891,8 @@ void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
   dim3 g((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   const bool silu = a.act == DV_ACT_SILU;
   const bool res = MODE == 0 && a.res != nullptr;
-  // A/B: DV_GN_DIRECT bit 0 forward, bit 1 backward (register prologue; else LDS)
-  static const int dflag = getenv("DV_GN_DIRECT") ? atoi(getenv("DV_GN_DIRECT")) : 1;
+  // A/B: DV_GN_DIRECT bit 0 forward, bit 1 backward apply (register prologue; else LDS)
+  static const int dflag = getenv("DV_GN_DIRECT") ? atoi(getenv("DV_GN_DIRECT")) : 5;
   const int dq = sizeof(T) == 2 && (dflag >> MODE & 1) && gn_direct_ok(a, VEC) ? gn_direct_dq(a, VEC) : 0;
 #define DV_GN_APP2(UU, D)                                                            \
   (silu ? (res ? gn_apply_kernel<T, MODE, UU, true, true, D><<<g, 256, 0, st>>>(a)    \
