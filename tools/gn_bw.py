@@ -63,14 +63,14 @@ def case(nb, T, H, C, iters=50):
     dz = torch.empty_like(z)
     dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
     dss = torch.empty(nb, 2 * C, device=dev)
-    sums2 = torch.zeros(2, nb * C * 2, device=dev)
+    sums2 = torch.zeros(2, ops._GnSums.CAP, device=dev)  # the step's buffers: R = min(8, CAP / (nb*C*2))
 
     def bwd():  # reduce + apply; the two buffers alternate as in ops._GnSums
         call("dv_gn_bwd", dt(z), ptr(dy), C, ptr(z), C, ptr(dz), C, nb, P, C, 8, ptr(g), ptr(b), ptr(ss), 1,
-             ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(sums2[0]), ptr(sums2[1]), nb * C * 2, 1,
+             ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(sums2[0]), ptr(sums2[1]), sums2.shape[1], 1,
              stream())
         call("dv_gn_bwd", dt(z), ptr(dy), C, ptr(z), C, ptr(dz), C, nb, P, C, 8, ptr(g), ptr(b), ptr(ss), 1,
-             ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(sums2[1]), ptr(sums2[0]), nb * C * 2, 1,
+             ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(sums2[1]), ptr(sums2[0]), sums2.shape[1], 1,
              stream())
 
     n = z.numel() * 2  # bytes of one bf16 tensor
