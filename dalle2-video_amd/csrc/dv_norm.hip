@@ -928,74 +928,92 @@ int gn_bwd_t(GnArgs a, hipStream_t st) {
 }
 
 // --------------------------------------------------------------------------
-// row LayerNorm: y = (x - mean) * rstd * g (+ b) (+ res); one wave per row
+// row LayerNorm: y = (x - mean) * rstd * g (+ b) (+ res); one wave per row,
+// NV 16-byte vectors per lane (C <= 64 * VEC * NV).  Every load is
+// unconditional (vector index clamped, out-of-row lanes masked to zero): a
+// load under a lane branch made the compiler wait for all outstanding loads
+// at the join, so x, res and dy of a row went out one after another.
+// The backward writes per-block column partials of dg / db (plain stores) and
+// ln_colsum_kernel sums them: 1,024 blocks adding 2C floats each into the
+// same few lines with atomics serialised (33 us for 4,096 x 512 rows).
 // --------------------------------------------------------------------------
-template <typename T, int MODE>  // MODE 0 fwd, 1 bwd
+template <typename T, int MODE, int NV>  // MODE 0 fwd, 1 bwd
 __global__ __launch_bounds__(256) void ln_kernel(const T* x, int ldx, const T* dy, int lddy, T* out,
                                                  int ldo, const T* res, int ldres, long long rows,
                                                  int C, const float* g, const float* bias,
-                                                 float eps, float* mean, float* rstd, float* dg,
-                                                 float* db) {
+                                                 float eps, float* mean, float* rstd, float* part,
+                                                 float* dg, float* db) {
   constexpr int VEC = 16 / sizeof(T);
-  constexpr int MAXV = 4;  // C <= 64 * VEC * MAXV, C % VEC == 0
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float pg[MAXV][VEC], pb[MAXV][VEC];
+  int c0[NV];
+  bool live[NV];
+  float gv[NV][VEC];
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k)
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * VEC;
+    live[k] = c < C;
+    c0[k] = live[k] ? c : C - VEC;  // clamped: a valid address, masked below
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) gv[k][e] = g[c0[k] + e];
+  }
+  float pg[NV][VEC], pb[NV][VEC];
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
 #pragma unroll
     for (int e = 0; e < VEC; ++e) pg[k][e] = pb[k][e] = 0.f;
   for (long long row = (long long)blockIdx.x * 4 + wave; row < rows; row += (long long)gridDim.x * 4) {
-    float xv[MAXV][VEC];
+    u32x4 xr[NV], yr[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      xr[k] = *(const u32x4*)(x + row * ldx + c0[k]);
+      if (MODE == 1) yr[k] = *(const u32x4*)(dy + row * lddy + c0[k]);
+      else if (res) yr[k] = *(const u32x4*)(res + row * ldres + c0[k]);
+    }
+    float xv[NV][VEC];
     float s = 0.f, q = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-      const int c0 = (k * 64 + lane) * VEC;
-      if (c0 < C) ld_vec<T>(x + row * ldx + c0, xv[k]);
+    for (int k = 0; k < NV; ++k) {
+      Vec<T>::to_f(xr[k], xv[k]);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        if (c0 >= C) xv[k][e] = 0.f;
+        if (!live[k]) xv[k][e] = 0.f;
         s += xv[k][e];
       }
     }
     const float mu = wave_sum(s) / C;
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k)
+    for (int k = 0; k < NV; ++k)
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        const float d = (k * 64 + lane) * VEC < C ? xv[k][e] - mu : 0.f;
+        const float d = live[k] ? xv[k][e] - mu : 0.f;
         q += d * d;
       }
     const float rs = rsqrtf(wave_sum(q) / C + eps);
     if (MODE == 0) {
       if (lane == 0 && mean) { mean[row] = mu; rstd[row] = rs; }
 #pragma unroll
-      for (int k = 0; k < MAXV; ++k) {
-        const int c0 = (k * 64 + lane) * VEC;
-        if (c0 >= C) continue;
-        float o[VEC];
+      for (int k = 0; k < NV; ++k) {
+        float o[VEC], r[VEC];
+        if (res) Vec<T>::to_f(yr[k], r);
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) o[e] = (xv[k][e] - mu) * rs * g[c0 + e] + (bias ? bias[c0 + e] : 0.f);
-        if (res) {
-          float r[VEC];
-          ld_vec<T>(res + row * ldres + c0, r);
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) o[e] += r[e];
+        for (int e = 0; e < VEC; ++e) {
+          o[e] = (xv[k][e] - mu) * rs * gv[k][e] + (bias ? bias[c0[k] + e] : 0.f);
+          if (res) o[e] += r[e];
         }
-        st_vec<T>(out + row * ldo + c0, o);
+        if (live[k]) st_vec<T>(out + row * ldo + c0[k], o);
       }
     } else {
       // dxhat = dy*g; dx = rs*(dxhat - mean(dxhat) - xhat*mean(dxhat*xhat))
-      float dyv[MAXV][VEC];
+      float dyv[NV][VEC];
       float m1 = 0.f, m2 = 0.f;
 #pragma unroll
-      for (int k = 0; k < MAXV; ++k) {
-        const int c0 = (k * 64 + lane) * VEC;
-        if (c0 >= C) continue;
-        ld_vec<T>(dy + row * lddy + c0, dyv[k]);
+      for (int k = 0; k < NV; ++k) {
+        Vec<T>::to_f(yr[k], dyv[k]);
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
+          if (!live[k]) dyv[k][e] = 0.f;
           const float xh = (xv[k][e] - mu) * rs;
-          const float dxh = dyv[k][e] * g[c0 + e];
+          const float dxh = dyv[k][e] * gv[k][e];
           m1 += dxh;
           m2 += dxh * xh;
           pg[k][e] += dyv[k][e] * xh;
@@ -1005,23 +1023,21 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* x, int ldx, const T* d
       m1 = wave_sum(m1) / C;
       m2 = wave_sum(m2) / C;
 #pragma unroll
-      for (int k = 0; k < MAXV; ++k) {
-        const int c0 = (k * 64 + lane) * VEC;
-        if (c0 >= C) continue;
+      for (int k = 0; k < NV; ++k) {
         float o[VEC];
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
           const float xh = (xv[k][e] - mu) * rs;
-          o[e] = rs * (dyv[k][e] * g[c0 + e] - m1 - xh * m2);
+          o[e] = rs * (dyv[k][e] * gv[k][e] - m1 - xh * m2);
         }
-        st_vec<T>(out + row * ldo + c0, o);
+        if (live[k]) st_vec<T>(out + row * ldo + c0[k], o);
       }
     }
   }
-  if (MODE == 1) {
-    __shared__ float red[2][4][64 * VEC * MAXV];
+  if (MODE == 1) {  // this block's column partials: part[blk][0..C) dg, [C..2C) db
+    __shared__ float red[2][4][64 * VEC * NV];
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k)
+    for (int k = 0; k < NV; ++k)
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
         red[0][wave][(k * 64 + lane) * VEC + e] = pg[k][e];
@@ -1031,10 +1047,57 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* x, int ldx, const T* d
     for (int c = threadIdx.x; c < C; c += 256) {
       const float tg = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
       const float tb = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
-      if (dg) atomicAdd(dg + c, tg);
-      if (db) atomicAdd(db + c, tb);
+      if (part) {  // many blocks: partials, summed by ln_colsum_kernel
+        part[(long long)blockIdx.x * 2 * C + c] = tg;
+        part[(long long)blockIdx.x * 2 * C + C + c] = tb;
+      } else {     // a few blocks: atomics are uncontended, no second launch
+        if (dg) atomicAdd(dg + c, tg);
+        if (db) atomicAdd(db + c, tb);
+      }
     }
   }
+}
+
+// dg[c] (+)= sum_b part[b][c], db[c] (+)= sum_b part[b][C + c]: block
+// (x, y) owns 64 columns and every gridDim.y-th block row; its 4 waves take
+// every 4th of those (8 loads in flight per lane), meet in LDS, and add their
+// total with one atomic per column (gridDim.y adds per address)
+__global__ __launch_bounds__(256) void ln_colsum_kernel(const float* part, int nblk, int C, float* dg,
+                                                        float* db) {
+  __shared__ float sh[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  const int n2 = 2 * C, rs = 4 * gridDim.y;
+  float v = 0.f;
+  if (col < n2) {
+    int r = blockIdx.y * 4 + grp;
+    for (; r + 7 * rs < nblk; r += 8 * rs) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = part[(long long)(r + u * rs) * n2 + col];
+      v += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+    }
+    for (; r < nblk; r += rs) v += part[(long long)r * n2 + col];
+  }
+  sh[grp][threadIdx.x & 63] = v;
+  __syncthreads();
+  if (grp != 0 || col >= n2) return;
+  v = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
+  float* o = col < C ? (dg ? dg + col : nullptr) : (db ? db + col - C : nullptr);
+  if (o) atomicAdd(o, v);  // dg / db accumulate (the caller zeroes fresh buffers)
+}
+
+template <typename T, int MODE>
+void ln_launch(int nv, int blocks, const T* x, int ldx, const T* dy, int lddy, T* out, int ldo,
+               const T* res, int ldres, long long rows, int C, const float* g, const float* bias,
+               float eps, float* mean, float* rstd, float* part, float* dg, float* db, hipStream_t st) {
+#define DV_LN(NVV) ln_kernel<T, MODE, NVV><<<blocks, 256, 0, st>>>(x, ldx, dy, lddy, out, ldo, res, ldres, \
+                                                                  rows, C, g, bias, eps, mean, rstd, part, dg, db)
+  switch (nv) {
+    case 1: DV_LN(1); break;
+    case 2: DV_LN(2); break;
+    default: DV_LN(4); break;
+  }
+#undef DV_LN
 }
 
 }  // namespace
@@ -1088,6 +1151,12 @@ extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int
   return dtype == DV_BF16 ? gn_bwd_t<bf16>(a, st) : gn_bwd_t<float>(a, st);
 }
 
+// 16-byte vectors per lane of one row (1, 2 or 4)
+static int ln_nv(int C, int vec) {
+  const int n = (C + 64 * vec - 1) / (64 * vec);
+  return n <= 1 ? 1 : n <= 2 ? 2 : 4;
+}
+
 extern "C" int dv_ln_fwd(int dtype, const void* x, int ldx, void* y, int ldy, const void* res,
                          int ldres, long long rows, int C, const float* g, const float* b,
                          float eps, float* mean, float* rstd, void* stream) {
@@ -1100,34 +1169,41 @@ extern "C" int dv_ln_fwd(int dtype, const void* x, int ldx, void* y, int ldy, co
   const int blocks = grid_for(rows, 4);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DV_BF16)
-    ln_kernel<bf16, 0><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, nullptr, 0, (bf16*)y, ldy,
-                                               (const bf16*)res, ldres, rows, C, g, b, eps, mean,
-                                               rstd, nullptr, nullptr);
+    ln_launch<bf16, 0>(ln_nv(C, VEC), blocks, (const bf16*)x, ldx, nullptr, 0, (bf16*)y, ldy,
+                       (const bf16*)res, ldres, rows, C, g, b, eps, mean, rstd, nullptr, nullptr, nullptr, st);
   else
-    ln_kernel<float, 0><<<blocks, 256, 0, st>>>((const float*)x, ldx, nullptr, 0, (float*)y, ldy,
-                                                (const float*)res, ldres, rows, C, g, b, eps, mean,
-                                                rstd, nullptr, nullptr);
+    ln_launch<float, 0>(ln_nv(C, VEC), blocks, (const float*)x, ldx, nullptr, 0, (float*)y, ldy,
+                        (const float*)res, ldres, rows, C, g, b, eps, mean, rstd, nullptr, nullptr, nullptr, st);
   return check_launch("ln_fwd");
+}
+
+extern "C" int dv_ln_bwd_ws(long long rows, int C, long long* need) {
+  DV_REQUIRE(need && rows >= 0 && C > 0, "bad arguments");
+  *need = (long long)std::max(1, std::min(grid_for(rows, 4), 1024)) * 2 * C;
+  return DV_OK;
 }
 
 extern "C" int dv_ln_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, void* dx,
                          int lddx, long long rows, int C, const float* g, float eps, float* dg,
-                         float* db, void* stream) {
-  DV_REQUIRE(dy && x && dx && g, "null pointer");
+                         float* db, float* ws, long long ws_n, void* stream) {
+  DV_REQUIRE(dy && x && dx && g && ws, "null pointer");
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C <= 64 * VEC * 4 && C % VEC == 0, "C must be a multiple of 16 bytes, <= 256 vectors");
   DV_REQUIRE(ldx % VEC == 0 && lddy % VEC == 0 && lddx % VEC == 0, "strides must be multiples of 16 bytes");
   if (rows == 0) return DV_OK;
-  int blocks = grid_for(rows, 4);
-  if (blocks > 1024) blocks = 1024;  // bounds the dg/db atomics
+  const int blocks = std::min(grid_for(rows, 4), 1024);
+  DV_REQUIRE(ws_n >= (long long)blocks * 2 * C, "workspace smaller than dv_ln_bwd_ws");
   hipStream_t st = (hipStream_t)stream;
+  float* part = blocks > 8 ? ws : nullptr;  // <= 8 blocks: direct atomics
   if (dtype == DV_BF16)
-    ln_kernel<bf16, 1><<<blocks, 256, 0, st>>>((const bf16*)x, ldx, (const bf16*)dy, lddy,
-                                               (bf16*)dx, lddx, nullptr, 0, rows, C, g, nullptr,
-                                               eps, nullptr, nullptr, dg, db);
+    ln_launch<bf16, 1>(ln_nv(C, VEC), blocks, (const bf16*)x, ldx, (const bf16*)dy, lddy, (bf16*)dx, lddx,
+                       nullptr, 0, rows, C, g, nullptr, eps, nullptr, nullptr, part, dg, db, st);
   else
-    ln_kernel<float, 1><<<blocks, 256, 0, st>>>((const float*)x, ldx, (const float*)dy, lddy,
-                                                (float*)dx, lddx, nullptr, 0, rows, C, g, nullptr,
-                                                eps, nullptr, nullptr, dg, db);
+    ln_launch<float, 1>(ln_nv(C, VEC), blocks, (const float*)x, ldx, (const float*)dy, lddy, (float*)dx,
+                        lddx, nullptr, 0, rows, C, g, nullptr, eps, nullptr, nullptr, part, dg, db, st);
+  if (part && (dg || db)) {
+    const unsigned ys = (unsigned)std::max(1, std::min(16, blocks / 32));  // >= 32 rows per block
+    ln_colsum_kernel<<<dim3((2 * C + 63) / 64, ys), 256, 0, st>>>(ws, blocks, C, dg, db);
+  }
   return check_launch("ln_bwd");
 }

@@ -53,7 +53,8 @@ _SIGS = {
                   _I, _P],
     "dv_gn_bwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "dv_ln_fwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _P, _F, _P, _P, _P],
-    "dv_ln_bwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _F, _P, _P, _P],
+    "dv_ln_bwd_ws": [_L, _I, _P],
+    "dv_ln_bwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _F, _P, _P, _P, _L, _P],
     "dv_ncthw_to_cl": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_cl_to_ncthw": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P],
     "dv_shuffle": [_I, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P],

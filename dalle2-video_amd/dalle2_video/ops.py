@@ -1108,9 +1108,27 @@ class LayerNormFn(torch.autograd.Function):
         bs = _grad_out(ctx.params[1], zero=True) if has_b else None
         dg = gs[0] if gs else torch.zeros(c, dtype=torch.float32, device=xc.device)
         db = (bs[0] if bs else torch.zeros(c, dtype=torch.float32, device=xc.device)) if has_b else None
+        import ctypes
+        need = ctypes.c_longlong(0)
+        call("dv_ln_bwd_ws", rows, c, ctypes.byref(need))
+        ws = _ln_workspace(need.value, xc.device)
         call("dv_ln_bwd", dt(xc), ptr(dy), c, ptr(xc), c, ptr(dx), c, rows, c, ptr(gf),
-             ctypes_float(eps), ptr(dg), ptr(db), stream())
+             ctypes_float(eps), ptr(dg), ptr(db), ptr(ws), ws.numel(), stream())
         return dx, (None if gs else dg), (None if bs else db), (dy if has_res else None), None
+
+
+_LN_WS = {}
+
+
+def _ln_workspace(n, device):
+    """Per-device f32 scratch for dv_ln_bwd's per-block column partials (grown
+    on demand; kernels on the stream use it one after another)."""
+    key = str(device)
+    if key not in _LN_WS or _LN_WS[key].numel() < n:
+        # sized for every LayerNorm of the path at once (C <= 1,024: 8 MB), so
+        # it is never re-allocated between the eager warm-up and graph capture
+        _LN_WS[key] = torch.empty(max(n, 1 << 21), dtype=torch.float32, device=device)
+    return _LN_WS[key]
 
 
 def layer_norm(x, g, b=None, res=None, eps=1e-5):

@@ -264,8 +264,12 @@ int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void*
 int dv_ln_fwd(int dtype, const void* x, int ldx, void* y, int ldy, const void* res, int ldres,
               long long rows, int C, const float* g, const float* b, float eps, float* mean,
               float* rstd, void* stream);
+/* dg / db (+)= column sums (accumulated: zero fresh buffers).  ws: caller-owned
+ * f32 scratch of *need (dv_ln_bwd_ws) floats for the per-block partials. */
+int dv_ln_bwd_ws(long long rows, int C, long long* need);
 int dv_ln_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, void* dx, int lddx,
-              long long rows, int C, const float* g, float eps, float* dg, float* db, void* stream);
+              long long rows, int C, const float* g, float eps, float* dg, float* db, float* ws,
+              long long ws_n, void* stream);
 
 /* ---- layout, space-to-depth / pixel shuffle --------------------------------
  * NCTHW f32 <-> channels-last frames (cpad: padded channel stride, zeros).  */

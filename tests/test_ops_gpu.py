@@ -75,11 +75,11 @@ def test_group_norm_act(dtype, tol, with_ss, with_res, nb, C):
 
 @pytest.mark.parametrize("dtype,tol", DTYPES)
 @pytest.mark.parametrize("C,bias,res", [(512, False, True), (64, True, False)])
-def test_layer_norm(dtype, tol, C, bias, res):
+@pytest.mark.parametrize("rows", [8, 300, 4096])  # direct atomics / block partials / split column sum
+def test_layer_norm(dtype, tol, C, bias, res, rows):
     from dalle2_video import ops
 
     g = torch.Generator().manual_seed(5)
-    rows = 300
     x = torch.randn(rows, C, generator=g) * 3 + 1
     w = 1 + 0.1 * torch.randn(C, generator=g)
     b = 0.1 * torch.randn(C, generator=g) if bias else None
