@@ -1259,21 +1259,29 @@ __device__ __forceinline__ void pack_stage(const float* src, float* sm, int n) {
   if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
     const int n4 = n >> 2;
     for (int i0 = threadIdx.x; i0 < n4; i0 += 1024) {
+      // unconditional loads (index clamped): a load under a lane branch makes
+      // the compiler wait for every outstanding load at the join
       f32x4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (i0 + 256 * u < n4) v[u] = ((const f32x4*)src)[i0 + 256 * u];
+      for (int u = 0; u < 4; ++u) v[u] = ((const f32x4*)src)[min(i0 + 256 * u, n4 - 1)];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (i0 + 256 * u < n4) ((f32x4*)sm)[i0 + 256 * u] = v[u];
     }
     for (int i = 4 * n4 + threadIdx.x; i < n; i += 256) sm[i] = src[i];
-  } else {
-    for (int i = threadIdx.x; i < n; i += 256) sm[i] = src[i];
+  } else {  // unaligned (a weight after an odd-sized one in the flat buffer): 8 loads in flight
+    for (int i0 = threadIdx.x; i0 < n; i0 += 2048) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[min(i0 + 256 * u, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + 256 * u < n) sm[i0 + 256 * u] = v[u];
+    }
   }
 }
 
-__device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
+__device__ __forceinline__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {  // inlined: sm stays an LDS pointer (ds_ ops, not flat)
   const int taps = e.taps, cin = e.cin, cout = e.cout, pad = e.pad_to;
   const bool fwd = (e.mode & 1) == 0, chunked = (e.mode & 2) != 0;
   if ((long long)(fwd ? cin : cout) * taps > PACK_LDS) return;  // rejected on the host
@@ -1296,7 +1304,10 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
         const float* r = sm + rl * row + tap;
         float v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = ci + q < cin ? r[(ci + q) * taps] : 0.f;
+        for (int q = 0; q < 8; ++q) {  // clamped index: unconditional reads, then select
+          const float t = r[min(ci + q, cin - 1) * taps];
+          v[q] = ci + q < cin ? t : 0.f;
+        }
         *(bf16x8*)((bf16*)e.out + ob + i) =
             bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
       }
@@ -1325,9 +1336,9 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
       float v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int i = i0 + 256 * u;
+        const int i = min(i0 + 256 * u, con * seg - 1);  // clamped: unconditional loads
         const int r = i / seg, j = i - r * seg;
-        v[u] = i < con * seg ? e.w[((long long)(co0 + r) * cin + ci0) * taps + j] : 0.f;
+        v[u] = e.w[((long long)(co0 + r) * cin + ci0) * taps + j];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -1347,7 +1358,10 @@ __device__ void pack_tile(const DvPackEntry& e, int tile, float* sm) {
         const float* r = sm + cl * taps + (taps - 1 - tapd);
         float v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = cc + q < con ? r[(cc + q) * seg] : 0.f;
+        for (int q = 0; q < 8; ++q) {  // clamped index: unconditional reads, then select
+          const float t = r[max(0, min(cc + q, con - 1)) * seg];
+          v[q] = cc + q < con ? t : 0.f;
+        }
         *(bf16x8*)((bf16*)e.out + (ci0 + cl) * orow + ocol(tapd, co0 + cc)) =
             bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
       }
