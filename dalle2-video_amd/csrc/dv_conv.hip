@@ -14,6 +14,8 @@
 //   f32 atomics into a packed [co][tap][ci] workspace (coalesced rows).
 #include "dv_common.h"
 
+#include <type_traits>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -193,6 +195,38 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32
     clip = blk_m0 / p.gn_P;
     one_clip = last / p.gn_P == clip;
   }
+  // Bias and residual of the whole tile are loaded BEFORE the first store:
+  // vmcnt counts loads and stores in order, so a load issued behind a store
+  // waits for that store's write (one write round trip per 4-channel group,
+  // TI*TJ*4 of them per tile, when loads and stores interleaved).  Indices are
+  // clamped (unconditional loads); lanes past M / cout skip the store.
+  f32x4 bv[TJ][4];
+  using RV = typename std::conditional<sizeof(T) == 2, u32x2, f32x4>::type;
+  RV rv[TI][TJ][4];
+  if (vec_ok && p.cout >= 4) {
+    if (p.bias) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = min(nb + 32 * j + 8 * g + 4 * h, p.cout - 4);
+          bv[j][g] = *(const f32x4*)(p.bias + n);
+        }
+    }
+    if (p.res) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const long long m = min(mb + 32 * i + r, p.M - 1);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = min(nb + 32 * j + 8 * g + 4 * h, p.cout - 4);
+            rv[i][j][g] = *(const RV*)(p.res + m * p.ldres + n);
+          }
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     const long long m = mb + 32 * i + r;
@@ -208,9 +242,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32
         for (int e = 0; e < 4; ++e) v[e] = acc[j][i][4 * g + e];
         if (vec_ok && n + 3 < p.cout) {
           if (p.bias) {
-            f32x4 b = *(const f32x4*)(p.bias + n);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += b[e];
+            for (int e = 0; e < 4; ++e) v[e] += bv[j][g][e];
           }
           if (p.act == DV_ACT_SILU) {
 #pragma unroll
@@ -218,7 +251,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32
           }
           if (p.res) {
             float rr[4];
-            load4<T>(p.res + m * p.ldres + n, rr);
+            if constexpr (sizeof(T) == 2) {
+              const bf16x4 t4 = __builtin_bit_cast(bf16x4, rv[i][j][g]);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) rr[e] = (float)t4[e];
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) rr[e] = rv[i][j][g][e];
+            }
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += rr[e];
           }
@@ -2052,9 +2092,26 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
-  // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e
+  // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e.  Bias and
+  // residual are loaded for all 8 channel groups BEFORE the first store (vmcnt
+  // retires loads and stores in order: a load behind a store waits for the
+  // write, one round trip per group when they interleaved)
   const long long m = m0 + tpx;
   float sv[STATS ? 64 : 1];  // STATS: [0,32) sums, [32,64) squares of the lane's 32 channels
+  f32x4 bb[2][4];
+  u32x2 rq[2][4];
+  if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bb[j][g] = *(const f32x4*)(p.bias + co0 + 32 * j + 8 * g + 4 * h);
+  }
+  if (p.res) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) rq[j][g] = *(const u32x2*)(p.res + m * p.ldres + co0 + 32 * j + 8 * g + 4 * h);
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
 #pragma unroll
@@ -2064,19 +2121,17 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = j ? acc1[4 * g + e] + acc3[4 * g + e] : acc0[4 * g + e] + acc2[4 * g + e];
       if (p.bias) {
-        const f32x4 bb = *(const f32x4*)(p.bias + n);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += bb[e];
+        for (int e = 0; e < 4; ++e) v[e] += bb[j][g][e];
       }
       if (p.act == DV_ACT_SILU) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
       }
       if (p.res) {
-        float rr[4];
-        load4<bf16>(p.res + m * p.ldres + n, rr);
+        const bf16x4 t4 = __builtin_bit_cast(bf16x4, rq[j][g]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += rr[e];
+        for (int e = 0; e < 4; ++e) v[e] += (float)t4[e];
       }
       store4<bf16>(p.y + m * p.ldy + n, v);
       if constexpr (STATS) {
