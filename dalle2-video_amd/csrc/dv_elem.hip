@@ -408,21 +408,83 @@ __global__ __launch_bounds__(256) void linear_group_bwd_kernel(LinGroupArgs a) {
   }
 }
 
+__device__ __forceinline__ void adamw_elem(float& pi, float gi, float& mi, float& vi, bool decay, float lr,
+                                           float b1, float b2, float eps, float wd, float step,
+                                           float bc2_sqrt) {
+  if (decay) pi *= 1.f - lr * wd;
+  mi = mi + (1.f - b1) * (gi - mi);
+  vi = vi * b2 + (1.f - b2) * gi * gi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  pi = pi - step * (mi / denom);
+}
+
+// scalar form (any alignment)
 __global__ void adamw_kernel(float* p, const float* g, float* m, float* v, long long n,
                              long long n_wd, float lr, float b1, float b2, float eps, float wd,
                              float bc1, float bc2_sqrt, const float* clip) {
   const float cc = clip ? clip[0] : 1.f;
   const float step = lr / bc1;
   GRID_STRIDE(i, n) {
-    const float gi = g[i] * cc;
-    float pi = p[i];
-    if (i < n_wd) pi *= 1.f - lr * wd;
-    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
-    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_elem(pi, g[i] * cc, mi, vi, i < n_wd, lr, b1, b2, eps, wd, step, bc2_sqrt);
     m[i] = mi;
     v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = pi - step * (mi / denom);
+    p[i] = pi;
+  }
+}
+
+// 16-B vectors, two per thread per trip: all eight loads of a trip are issued
+// before its six stores (vmcnt retires loads and stores in order, so a load
+// issued behind a store would also wait for that store's write)
+__global__ void adamw_vec_kernel(float* p, const float* g, float* m, float* v, long long n,
+                             long long n_wd, float lr, float b1, float b2, float eps, float wd,
+                             float bc1, float bc2_sqrt, const float* clip) {
+  const float cc = clip ? clip[0] : 1.f;
+  const float step = lr / bc1;
+  const long long n4 = n / 4;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  f32x4* P4 = (f32x4*)p;
+  const f32x4* G4 = (const f32x4*)g;
+  f32x4* M4 = (f32x4*)m;
+  f32x4* V4 = (f32x4*)v;
+  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += 2 * stride) {
+    long long ix[2] = {i0, i0 + stride};
+    const bool live1 = ix[1] < n4;
+    if (!live1) ix[1] = i0;  // clamped: unconditional loads, store skipped
+    f32x4 pv[2], gv[2], mv[2], vv[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      gv[k] = G4[ix[k]];
+      pv[k] = P4[ix[k]];
+      mv[k] = M4[ix[k]];
+      vv[k] = V4[ix[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pi = pv[k][e], mi = mv[k][e], vi = vv[k][e];
+        adamw_elem(pi, gv[k][e] * cc, mi, vi, 4 * ix[k] + e < n_wd, lr, b1, b2, eps, wd, step, bc2_sqrt);
+        pv[k][e] = pi;
+        mv[k][e] = mi;
+        vv[k][e] = vi;
+      }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && !live1) break;
+      M4[ix[k]] = mv[k];
+      V4[ix[k]] = vv[k];
+      P4[ix[k]] = pv[k];
+    }
+  }
+  // the n % 4 tail
+  const long long t = 4 * n4 + (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) {
+    float pi = p[t], mi = m[t], vi = v[t];
+    adamw_elem(pi, g[t] * cc, mi, vi, t < n_wd, lr, b1, b2, eps, wd, step, bc2_sqrt);
+    m[t] = mi;
+    v[t] = vi;
+    p[t] = pi;
   }
 }
 
@@ -664,7 +726,13 @@ extern "C" int dv_adamw(float* p, const float* g, float* m, float* v, long long 
                         float lr, float beta1, float beta2, float eps, float wd, float bc1,
                         float bc2_sqrt, const float* clip_coef, void* stream) {
   DV_REQUIRE(p && g && m && v, "null pointer");
-  adamw_kernel<<<grid_for(n, 256, 8192), 256, 0, (hipStream_t)stream>>>(p, g, m, v, n, n_wd, lr, beta1, beta2, eps, wd, bc1, bc2_sqrt, clip_coef);
+  const bool al16 = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                      reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+  if (al16)
+    adamw_vec_kernel<<<grid_for((n + 7) / 8, 256, 8192), 256, 0, (hipStream_t)stream>>>(
+        p, g, m, v, n, n_wd, lr, beta1, beta2, eps, wd, bc1, bc2_sqrt, clip_coef);
+  else
+    adamw_kernel<<<grid_for(n, 256, 8192), 256, 0, (hipStream_t)stream>>>(p, g, m, v, n, n_wd, lr, beta1, beta2, eps, wd, bc1, bc2_sqrt, clip_coef);
   return check_launch("adamw");
 }
 
