@@ -500,10 +500,12 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* x, long long n,
     n4 = n / 4;
     const f32x4* x4 = (const f32x4*)x;
     long long i = t0;
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-      const f32x4 v0 = x4[i], v1 = x4[i + stride], v2 = x4[i + 2 * stride], v3 = x4[i + 3 * stride];
-      a += v0 * v0 + v1 * v1;
-      b += v2 * v2 + v3 * v3;
+    for (; i + 7 * stride < n4; i += 8 * stride) {  // 8 x 16 B in flight per lane
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = x4[i + u * stride];
+      a += (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+      b += (v[4] * v[4] + v[5] * v[5]) + (v[6] * v[6] + v[7] * v[7]);
     }
     for (; i < n4; i += stride) a += x4[i] * x4[i];
   }
@@ -742,7 +744,9 @@ extern "C" int dv_grad_clip_coef(const float* g, long long n, float max_norm, fl
   DV_REQUIRE(g && ws, "null pointer");
   hipStream_t st = (hipStream_t)stream;
   zero_f32(ws, 1, st);
-  sumsq_kernel<<<grid_for(n, 256, 2048), 256, 0, st>>>(g, n, ws);
+  // 512 blocks: their one atomic each lands on ONE word, which serialises at
+  // ~11 ns per add (2,048 blocks left a ~20 us tail)
+  sumsq_kernel<<<grid_for(n, 256, 512), 256, 0, st>>>(g, n, ws);
   clip_coef_kernel<<<1, 1, 0, st>>>(ws, max_norm, prescale, ws + 1);
   return check_launch("grad_clip_coef");
 }
