@@ -141,15 +141,32 @@ __global__ __launch_bounds__(256) void mse_kernel(const T* pred, int ld, const f
                                                   float* loss, float scale) {
   __shared__ float sh[4];
   const long long npix = (long long)B * T_ * HW;
+  const long long stride = (long long)gridDim.x * blockDim.x;
   float acc = 0.f;
-  GRID_STRIDE(p, npix) {
-    const int hw = (int)(p % HW);
-    const long long ft = p / HW;
-    const int tt = (int)(ft % T_), b = (int)(ft / T_);
-    const float wb = w ? w[b] : 1.f;
+  // 4 pixels per trip, their loads independent of each other (few blocks: every
+  // block ends in ONE atomic on the loss word, and same-word atomics serialise)
+  for (long long p0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; p0 < npix; p0 += 4 * stride) {
+    long long pp[4];
+    long long tb[4];
+    float wb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long p = p0 + u * stride;
+      const bool live = p < npix;
+      pp[u] = live ? p : p0;
+      const int hw = (int)(pp[u] % HW);
+      const long long ft = pp[u] / HW;
+      const int tt = (int)(ft % T_), b = (int)(ft / T_);
+      tb[u] = ((long long)b * C * T_ + tt) * HW + hw;  // channel 0 of this pixel in the NCTHW target
+      wb[u] = live ? (w ? w[b] : 1.f) : 0.f;
+    }
     for (int c = 0; c < C; ++c) {
-      const float d = (float)pred[p * ld + c] - target[(((long long)b * C + c) * T_ + tt) * HW + hw];
-      acc += wb * d * d;
+      float d[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        d[u] = (float)pred[pp[u] * ld + c] - target[tb[u] + (long long)c * T_ * HW];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += wb[u] * d[u] * d[u];
     }
   }
   acc = block_sum<256>(acc, sh);
@@ -672,7 +689,7 @@ extern "C" int dv_mse_loss(int dtype, const void* pred, int ld, const float* tar
   const float scale = 1.f / (float)((double)B * C * T * H * W);
   hipStream_t st = (hipStream_t)stream;
   zero_f32(loss, 1, st);
-  const int g = grid_for(npix, 256, 1024);
+  const int g = grid_for((npix + 3) / 4, 256, 256);
   DISPATCH(dtype,
            (mse_kernel<float><<<g, 256, 0, st>>>((const float*)pred, ld, target, B, C, T, H * W, sample_w, loss, scale)),
            (mse_kernel<bf16><<<g, 256, 0, st>>>((const bf16*)pred, ld, target, B, C, T, H * W, sample_w, loss, scale)));
