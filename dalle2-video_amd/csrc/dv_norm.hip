@@ -853,7 +853,7 @@ const GnTune& gn_tune() {
     GnTune g;
     g.ur0 = (int)env("DV_GN_UR0", 2 * GN_U); g.ua0 = (int)env("DV_GN_UA0", GN_U);
     g.ur1 = (int)env("DV_GN_UR1", GN_U);     g.ua1 = (int)env("DV_GN_UA1", 2);
-    g.tr0 = env("DV_GN_TR0", 768);  g.ta0 = env("DV_GN_TA0", 1024);
+    g.tr0 = env("DV_GN_TR0", 768);  g.ta0 = env("DV_GN_TA0", 512);  // ta0: 1024 before the register prologue
     g.tr1 = env("DV_GN_TR1", 768);  g.ta1 = env("DV_GN_TA1", 768);
     return g;
   }();
