@@ -73,16 +73,24 @@ def case(nb, T, H, C, iters=50):
              ptr(mean), ptr(rstd), ptr(dg), ptr(db), ptr(dss), ptr(sums2[1]), ptr(sums2[0]), sums2.shape[1], 1,
              stream())
 
+    sums3 = torch.zeros(2, ops._GnSums.CAP, device=dev)
+
+    def fwd_full():  # reduce + apply (no conv statistics epilogue); buffers alternate
+        for i in (0, 1):
+            call("dv_gn_fwd", dt(z), ptr(z), C, ptr(y), C, None, 0, nb, P, C, 8, f, ptr(g), ptr(b), ptr(ss), 1,
+                 ptr(mean), ptr(rstd), ptr(sums3[i]), ptr(sums3[1 - i]), sums3.shape[1], 0, stream())
+
     n = z.numel() * 2  # bytes of one bf16 tensor
     t_app = timeit(lambda: apply(None), iters)
     t_appr = timeit(lambda: apply(r), iters)
     t_bwd = timeit(bwd, iters) / 2
+    t_fwd = timeit(fwd_full, iters) / 2
     t_cp = timeit(lambda: y.copy_(z), iters)
     t_add = timeit(lambda: torch.add(z, r, out=y), iters)
     gb = lambda nbytes, ms: nbytes / ms / 1e9
     print(f"nb={nb} T={T} {H:3d}x{H:<3d} C={C:3d} {n/1e6:6.1f} MB | apply {t_app*1e3:6.1f} us "
           f"{gb(2*n, t_app):5.2f} TB/s | apply+res {t_appr*1e3:6.1f} us {gb(3*n, t_appr):5.2f} | "
-          f"bwd(red+app) {t_bwd*1e3:6.1f} us {gb(5*n, t_bwd):5.2f} | copy {t_cp*1e3:6.1f} us "
+          f"bwd(red+app) {t_bwd*1e3:6.1f} us {gb(5*n, t_bwd):5.2f} | fwd(red+app) {t_fwd*1e3:6.1f} us | copy {t_cp*1e3:6.1f} us "
           f"{gb(2*n, t_cp):5.2f} | add {t_add*1e3:6.1f} us {gb(3*n, t_add):5.2f}", flush=True)
 
 
