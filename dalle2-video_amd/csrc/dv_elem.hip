@@ -505,9 +505,13 @@ __global__ void adamw_vec_kernel(float* p, const float* g, float* m, float* v, l
   }
 }
 
-// sum of squares of the flat gradient: 16-B loads, 4 independent loads in
-// flight per lane (the scalar grid-stride loop was latency-bound at ~2.7 TB/s)
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* x, long long n, float* out) {
+// sum of squares of the flat gradient: 16-B loads, 8 independent loads in
+// flight per lane (the scalar grid-stride loop was latency-bound at ~2.7 TB/s).
+// Each block writes its partial to part[blockIdx.x]; clip_coef_kernel sums
+// the partials in a fixed order, so the norm — and the clipped update — is
+// bit-identical run to run and on every data-parallel rank (an atomic sum
+// made the ranks' weights drift apart by an ulp per step)
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* x, long long n, float* part) {
   __shared__ float sh[4];
   const long long stride = (long long)gridDim.x * blockDim.x;
   const long long t0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -530,13 +534,20 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* x, long long n,
   float acc = (a[0] + a[1]) + (a[2] + a[3]);
   for (long long i = n4 * 4 + t0; i < n; i += stride) acc += x[i] * x[i];
   acc = block_sum<256>(acc, sh);
-  if (threadIdx.x == 0) atomicAdd(out, acc);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
 
 // coef = prescale * min(max_norm / (||prescale * g|| + 1e-6), 1)  (prescale = 1/world
-// folds the DDP average into the update; torch.nn.utils.clip_grad_norm_ semantics)
-__global__ void clip_coef_kernel(const float* sumsq, float max_norm, float prescale, float* coef) {
-  const float norm = prescale * sqrtf(sumsq[0]);
+// folds the DDP average into the update; torch.nn.utils.clip_grad_norm_ semantics).
+// One block: thread t sums partials t, t + 256, ... then a fixed-shape block sum.
+__global__ __launch_bounds__(256) void clip_coef_kernel(const float* part, int nparts, float max_norm,
+                                                        float prescale, float* coef) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+  s = block_sum<256>(s, sh);
+  if (threadIdx.x != 0) return;
+  const float norm = prescale * sqrtf(s);
   float c = max_norm > 0.f ? max_norm / (norm + 1e-6f) : 1.f;
   coef[0] = prescale * (c < 1.f ? c : 1.f);
   coef[1] = norm;
@@ -757,14 +768,13 @@ extern "C" int dv_adamw(float* p, const float* g, float* m, float* v, long long 
 
 extern "C" int dv_grad_clip_coef(const float* g, long long n, float max_norm, float prescale,
                                  float* ws, void* stream) {
-  // ws[0] = sum of squares, ws[1] = update coefficient, ws[2] = gradient norm
+  // ws[1] = update coefficient, ws[2] = gradient norm, ws[4 ..] = per-block
+  // partial sums (DV_CLIP_WS_FLOATS in all)
   DV_REQUIRE(g && ws, "null pointer");
   hipStream_t st = (hipStream_t)stream;
-  zero_f32(ws, 1, st);
-  // 512 blocks: their one atomic each lands on ONE word, which serialises at
-  // ~11 ns per add (2,048 blocks left a ~20 us tail)
-  sumsq_kernel<<<grid_for(n, 256, 512), 256, 0, st>>>(g, n, ws);
-  clip_coef_kernel<<<1, 1, 0, st>>>(ws, max_norm, prescale, ws + 1);
+  const unsigned nb = grid_for(n, 256, DV_CLIP_WS_FLOATS - 4);
+  sumsq_kernel<<<nb, 256, 0, st>>>(g, n, ws + 4);
+  clip_coef_kernel<<<1, 256, 0, st>>>(ws + 4, (int)nb, max_norm, prescale, ws + 1);
   return check_launch("grad_clip_coef");
 }
 

@@ -1205,11 +1205,14 @@ class VideoDecoder(nn.Module):
                     step(time)
                 del step
             return self.unnormalize_video(vid)
-        for time in reversed(range(0, noise_scheduler.num_timesteps)):
-            times = torch.full((b,), time, device=self.device, dtype=torch.long)
-            vid, _ = self.p_sample(unet, vid, times, video_embed=video_embed,
-                                   cond_scale=cond_scale, lowres_cond_vid=lowres_cond_vid,
-                                   noise_scheduler=noise_scheduler, clip_denoised=clip_denoised)
+        # the eager loop packs its (unchanging) weights into a private cache too, so
+        # sampling never adds entries the trainer's per-update refresh would repack
+        with (ops.private_pack_cache() if vid.is_cuda else nullcontext()):
+            for time in reversed(range(0, noise_scheduler.num_timesteps)):
+                times = torch.full((b,), time, device=self.device, dtype=torch.long)
+                vid, _ = self.p_sample(unet, vid, times, video_embed=video_embed,
+                                       cond_scale=cond_scale, lowres_cond_vid=lowres_cond_vid,
+                                       noise_scheduler=noise_scheduler, clip_denoised=clip_denoised)
         return self.unnormalize_video(vid)
 
     @torch.no_grad()

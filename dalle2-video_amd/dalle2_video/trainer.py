@@ -80,6 +80,7 @@ class FusedAdamW(torch.optim.Optimizer):
         V = torch.zeros(n, dtype=torch.float32, device=dev)
         ranges = []
         off = 0
+        self._offsets = {}
         for gi in range(len(self.param_groups)):
             start = off
             for g2, p in live:
@@ -97,6 +98,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 self.state[p] = dict(step=torch.tensor(float(self._t)),
                                      exp_avg=M[off:off + k].view_as(p),
                                      exp_avg_sq=V[off:off + k].view_as(p))
+                self._offsets[id(p)] = off
                 off += al(k)
             ranges.append((gi, start, off))
         self._flat = (P, G, M, V, ranges, [p for _, p in live])
@@ -121,8 +123,9 @@ class FusedAdamW(torch.optim.Optimizer):
         P, G, M, V, ranges, params = self._flat
         for p in params:
             st = self.state.get(p, {})
-            st["exp_avg"] = st["exp_avg"].detach().clone()
-            st["exp_avg_sq"] = st["exp_avg_sq"].detach().clone()
+            for k in ("exp_avg", "exp_avg_sq"):
+                if k in st:
+                    st[k] = st[k].detach().clone()
             if p.grad is None or p.grad.device != p.device:
                 p.grad = torch.zeros_like(p)
         self._flat = None
@@ -179,27 +182,35 @@ class FusedAdamW(torch.optim.Optimizer):
             return None
         G = self._flat[1]
         if self._clip_ws is None:
-            self._clip_ws = torch.zeros(4, dtype=torch.float32, device=G.device)
+            self._clip_ws = torch.zeros(516, dtype=torch.float32, device=G.device)  # DV_CLIP_WS_FLOATS
         call("dv_grad_clip_coef", ptr(G), G.numel(), ctypes_float(max_norm if max_norm else 0.0),
              ctypes_float(prescale), ptr(self._clip_ws), stream())
         return self._clip_ws[1:2]
 
     def load_state_dict(self, state_dict):
+        if self._flat is not None:
+            self.ensure_flat()  # parameters moved since the last step: re-point them first
         super().load_state_dict(state_dict)
         steps = [float(s["step"]) for s in self.state.values() if "step" in s]
         self._t = int(max(steps)) if steps else 0
         if self._flat is not None:
             # keep the flat buffers (and every graph / packed image built on
             # their addresses): copy the loaded moments into the M / V slices
+            # (offsets recorded by _build_flat); a live parameter the
+            # checkpoint has no moments for starts from zero moments, as a
+            # fresh torch AdamW state would
             P, G, M, V, ranges, params = self._flat
             for p in params:
-                st = self.state.get(p)
-                if not st or "exp_avg" not in st:
-                    continue
-                off = (p.data_ptr() - P.data_ptr()) // 4
+                st = self.state.setdefault(p, {})
+                off = self._offsets[id(p)]
                 k = p.numel()
-                M[off:off + k].copy_(st["exp_avg"].reshape(-1))
-                V[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                if "exp_avg" in st:
+                    M[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                    V[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                else:
+                    M[off:off + k].zero_()
+                    V[off:off + k].zero_()
+                    st["step"] = torch.tensor(float(self._t))
                 st["exp_avg"] = M[off:off + k].view_as(p)
                 st["exp_avg_sq"] = V[off:off + k].view_as(p)
 
@@ -363,12 +374,58 @@ def shard_loader(loader, world, rank):
     if (world <= 1 or loader is None or not isinstance(loader, DataLoader)
             or isinstance(loader.dataset, IterableDataset) or loader.batch_sampler is None):
         return loader
+    if loader.batch_size is None:
+        # a custom batch_sampler (automatic batching off in the rebuilt form):
+        # keep its batches and give rank r every world-th one
+        return _BatchStridedLoader(loader, world, rank)
     seed = torch.tensor([torch.initial_seed() % (1 << 31)], dtype=torch.int64)
     if dist.is_initialized():
         if dist.get_backend() == "nccl":  # RCCL collectives take device tensors
             seed = seed.cuda()
         dist.broadcast(seed, 0)  # one shuffle order for all ranks
     return ShardedLoader(loader, world, rank, seed=int(seed.item()))
+
+
+class _BatchStridedLoader:
+    """Per-rank view of a DataLoader driven by a custom batch_sampler: rank r
+    of N takes batches r, r+N, ... (the sampler's own batches, unchanged).
+    The sampler must produce the same batch order on every rank (seeded)."""
+
+    def __init__(self, loader, world, rank):
+        from torch.utils.data import DataLoader
+
+        class _Strided:
+            def __init__(self, bs):
+                self.bs = bs
+
+            def __iter__(self):
+                for i, b in enumerate(self.bs):
+                    if i % world == rank:
+                        yield b
+
+            def __len__(self):
+                n = len(self.bs)
+                return n // world + (1 if rank < n % world else 0)
+
+        self.original = loader
+        kw = dict(batch_sampler=_Strided(loader.batch_sampler), num_workers=loader.num_workers,
+                  collate_fn=loader.collate_fn, pin_memory=loader.pin_memory, timeout=loader.timeout,
+                  worker_init_fn=loader.worker_init_fn)
+        self.loader = DataLoader(loader.dataset, **kw)
+
+    @property
+    def dataset(self):
+        return self.loader.dataset
+
+    @property
+    def batch_size(self):
+        return None
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        return iter(self.loader)
 
 
 def broadcast_parameters(module, src=0):
@@ -485,28 +542,33 @@ class VideoDecoderTrainer(nn.Module):
         self.steps[unet_number - 1] += 1
 
     # -- one optimizer step (trainer.py:247-274) ----------------------------
+    def _check_flat(self, unet_number):
+        """Re-point the unet's parameters into fresh flat buffers if they moved
+        (Module.to / one_unet_in_gpu, e.g. trainer.sample with use_non_ema);
+        True when that happened — every captured graph of this unet and every
+        packed image keyed on the old storage is then dropped."""
+        opt = getattr(self, f"optim{unet_number - 1}")
+        gen = opt.generation
+        opt.ensure_flat()
+        if opt.generation == gen:
+            return False
+        self._graphs = {k: v for k, v in self._graphs.items() if k[0] != unet_number}
+        if ops.PACK.enabled:
+            ops.PACK.prune()
+        return True
+
     def update(self, unet_number=None):
         unet_number = self.validate_and_return_unet_number(unet_number)
         index = unet_number - 1
         opt = getattr(self, f"optim{index}")
         sched = getattr(self, f"sched{index}")
-        gen = opt.generation
-        opt.ensure_flat()
-        fresh = opt.generation != gen
-        if fresh:
-            # parameters were (re)pointed into new flat buffers: every captured
-            # graph of this unet holds the old addresses
-            self._graphs = {k: v for k, v in self._graphs.items() if k[0] != unet_number}
+        self._check_flat(unet_number)
         allreduce_flat_grad(opt.flat_grad, self.world)
         coef = opt.clip_coefficient(self.max_grad_norm, prescale=1.0 / self.world)
         opt.step(clip_coef=coef)
         opt.zero_grad()
         if ops.PACK.enabled:
-            # new storage: drop the images keyed on the old storage (their
-            # graphs were dropped above); otherwise repack every image in one launch
-            if fresh:
-                ops.PACK.prune()
-            ops.PACK.refresh()
+            ops.PACK.refresh()  # repack every cached image in one launch
         warm = self.warmup_schedulers[index]
         with (warm.dampening() if exists(warm) else nullcontext()):
             sched.step()
@@ -575,6 +637,11 @@ class VideoDecoderTrainer(nn.Module):
         unet_number = self.validate_and_return_unet_number(unet_number)
         args = tuple(self._to_device(a) for a in args)
         kwargs = {k: self._to_device(v) for k, v in kwargs.items()}
+        if self.training and getattr(self, f"optim{unet_number - 1}").flat_grad is not None:
+            # a moved unet (sampling without EMA moves the trainable unets through
+            # host memory) is re-pointed into fresh flat buffers BEFORE anything
+            # runs: a captured graph must never replay against the old storage
+            self._check_flat(unet_number)
         if self._graphable(unet_number, max_batch_size, return_lowres_cond_video):
             out = self._graphed_call(unet_number, args, kwargs)
             if out is not None:

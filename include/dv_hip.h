@@ -335,7 +335,10 @@ int dv_adamw(float* p, const float* g, float* m, float* v, long long n, long lon
              const float* clip_coef, void* stream);
 /* ws[1] = prescale * min(max_norm / (||prescale*g|| + 1e-6), 1), ws[2] = the
  * norm (torch clip_grad_norm_ semantics; prescale = 1/world after the RCCL
- * sum).  ws: 4 floats, ws[0] scratch.  max_norm <= 0: no clipping.          */
+ * sum).  ws: DV_CLIP_WS_FLOATS floats (per-block partials summed in a fixed
+ * order: the result is bit-identical on every rank and run).  max_norm <= 0:
+ * no clipping.                                                              */
+#define DV_CLIP_WS_FLOATS 516
 int dv_grad_clip_coef(const float* g, long long n, float max_norm, float prescale, float* ws,
                       void* stream);
 

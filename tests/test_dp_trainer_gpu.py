@@ -1,0 +1,72 @@
+"""Data parallelism through the real trainer (reference
+trainer.py:117-124 prepare / :360 DDP backward / :247-274 update): two ranks
+(gloo, both on the box's one GPU — the RCCL path needs one GPU per rank) each
+run VideoDecoderTrainer.__call__ + update on half of a global batch, with the
+HIP-graph capture on (steps 3-4 replay), vs one rank on the whole batch.
+
+Checked (tests/dp_trainer_worker.py writes what each rank saw):
+  * the init broadcast: rank 1 starts from a different local init and ends up
+    with rank 0's weights;
+  * step-0 local gradients: the mean over ranks == the whole-batch gradient
+    (rel <= 1e-5, f32);
+  * losses: the mean of the ranks' losses == the whole-batch loss every step
+    (rel <= 1e-5);
+  * after 5 updates (all-reduce, clip, AdamW): both ranks hold bit-identical
+    weights, == the world-1 weights (rel <= 1e-5).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dp_trainer_worker.py")
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return str(s.getsockname()[1])
+
+
+def _run(out, world):
+    port = _port()
+    env = dict(os.environ)
+    procs = [subprocess.Popen([sys.executable, WORKER, str(out), str(world), str(r), port], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(world)]
+    logs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        logs.append(o.decode(errors="replace"))
+    for p, lg in zip(procs, logs):
+        assert p.returncode == 0, lg[-3000:]
+    return [torch.load(os.path.join(out, f"w{world}_r{r}.pt"), weights_only=True) for r in range(world)]
+
+
+def rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm()).item()
+
+
+def test_two_rank_trainer_matches_one_rank(tmp_path, parity_log):
+    one = _run(tmp_path, 1)[0]
+    two = _run(tmp_path, 2)
+    assert one["graphed"] and all(r["graphed"] for r in two), "the replayed path did not run"
+    init_err = rel(two[1]["init"], two[0]["init"])
+    g_err = rel((two[0]["grad0"] + two[1]["grad0"]) / 2, one["grad0"])
+    l_err = max(abs((a + b) / 2 - c) / abs(c) for a, b, c in zip(two[0]["losses"], two[1]["losses"], one["losses"]))
+    p_err = rel(two[0]["params"], one["params"])
+    parity_log(config="2-rank gloo trainer (dim 16, 4x3x4x32x32 global, 5 steps, graphs)", init_rel=init_err,
+               grad0_rel=g_err, loss_rel_max=l_err, params_rel=p_err)
+    assert init_err == 0.0, "init broadcast did not give rank 1 rank 0's weights"
+    assert g_err <= 1e-5, g_err
+    assert l_err <= 1e-5, l_err
+    assert torch.equal(two[0]["params"], two[1]["params"]), "ranks diverged after the all-reduced updates"
+    assert p_err <= 1e-5, p_err

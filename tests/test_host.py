@@ -193,3 +193,24 @@ def test_sinusoid_freqs_match_torch_expression():
         half = dim // 2
         ref = torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1)))
         assert torch.equal(ops.sinusoid_freqs(dim, "cpu"), ref.float())
+
+
+def test_shard_loader_keeps_custom_batch_sampler_batches():
+    """a DataLoader built with a custom batch_sampler (batch_size
+    None) is sharded by batches — rank r of N gets batches r, r+N, ... as the
+    sampler made them — instead of being rebuilt with automatic batching off."""
+    from torch.utils.data import DataLoader, TensorDataset
+
+    from dalle2_video.trainer import shard_loader
+
+    ds = TensorDataset(torch.arange(20))
+    batches = [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9, 10, 11], [12, 13]]
+    loader = DataLoader(ds, batch_sampler=batches)
+    assert loader.batch_size is None
+    got = []
+    for r in range(2):
+        sh = shard_loader(loader, 2, r)
+        got.append([b[0].tolist() for b in sh])
+        assert len(sh) == len(got[-1])
+    assert got[0] == [batches[0], batches[2], batches[4]]
+    assert got[1] == [batches[1], batches[3]]

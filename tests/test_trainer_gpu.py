@@ -254,3 +254,48 @@ def test_graph_replay_after_checkpoint_load(tmp_path):
     l_eager = tr(video=video, unet_number=1)
     assert abs(l_graph - l_eager) <= 1e-5 * abs(l_eager)
     assert ((g_graph - opt.flat_grad).norm() / opt.flat_grad.norm()).item() < 1e-5
+
+
+def test_graphs_survive_sampling_the_trainable_unet():
+    """trainer.sample with use_ema=False samples the
+    trainable unet, and one_unet_in_gpu moves its parameters through host
+    memory (new storage for every p.data / p.grad).  The next training call
+    must not replay the graph captured on the old storage: the trainer
+    re-points the unet into fresh flat buffers first and drops its graphs, so
+    the gradients of the call after sampling land in the live buffer and
+    equal an eager call's."""
+    from dalle2_video import dalle2_video as D
+    from dalle2_video.trainer import VideoDecoderTrainer
+    from dalle2_video.utils import deterministic_fill_
+
+    u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    dec = D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(2,), timesteps=4, learned_variance=False)
+    deterministic_fill_(dec.unets[0])
+    dec = dec.cuda()
+    tr = VideoDecoderTrainer(dec, lr=3e-4, use_ema=False, use_graphs=True)
+    video = torch.rand(2, 3, 2, 32, 32, device="cuda")
+    for _ in range(5):  # update, eager, eager, capture, replay
+        tr(video=video, unet_number=1)
+        tr.update(1)
+    assert any("graph" in v for v in tr._graphs.values())
+    opt = tr.optim0
+    G_old = opt.flat_grad
+    vid = tr.sample(video_embed=torch.randn(2, 512, device="cuda"))
+    assert torch.isfinite(vid).all()
+    opt.zero_grad()
+    torch.cuda.manual_seed(21)
+    l1 = tr(video=video, unet_number=1)
+    torch.cuda.synchronize()
+    assert opt._aliased(), "parameters are not views of the optimizer's flat buffers after sampling"
+    assert opt.flat_grad is not G_old
+    g1 = opt.flat_grad.clone()
+    assert g1.abs().max() > 0, "the call after sampling wrote no gradient into the live buffer"
+    opt.zero_grad()
+    tr.use_graphs = False
+    torch.cuda.manual_seed(21)
+    l2 = tr(video=video, unet_number=1)
+    assert abs(l1 - l2) <= 1e-5 * abs(l2)
+    assert ((g1 - opt.flat_grad).norm() / opt.flat_grad.norm()).item() < 1e-5
+    w0 = dec.unets[0].to_out.weight.detach().clone()
+    tr.update(1)
+    assert not torch.equal(dec.unets[0].to_out.weight.detach(), w0), "the update did not move the weights"
