@@ -30,6 +30,10 @@ _SIGS = {
                     _P, _L, _I, _P],
     "dv_conv_fwd8": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
                      _P, _L, _I, _P],
+    "dv_mx8_quant": [_P, _I, _I, _L, _P, _P, _P],
+    "dv_mx8_image_bytes": [_I, _I, _P],
+    "dv_mx8_pack_conv_weight": [_P, _I, _I, _P, _P],
+    "dv_conv_fwd_mx8": [_P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
     "dv_xattn_fold_batched": [_I, _P, _I, _F, _P],
     "dv_xattn_fold_bwd_batched": [_P, _I, _F, _P],
     "dv_conv_wgrad_ws": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P],

@@ -642,6 +642,11 @@ class Unet3D(nn.Module):
         self.to_out = nn.Conv3d(out_dim_in, self.channels_out, kernel_size=(1, 1, 1))
         zero_init_(self.to_out)
         self.checkpoint_during_training = checkpoint_during_training
+        # sampling precision switch (not a reference argument): True runs the
+        # eligible 3x3 convs of a no-grad forward in MX-fp8 (BASELINE config 5,
+        # ops.mx8_convs); training always stays bf16 / f32.  DV_FP8=1 sets it.
+        import os
+        self.fp8 = os.environ.get("DV_FP8", "0") == "1"
 
     # dalle2_video.py:652-681 — `cond_on_image_embeds` is swallowed by **kwargs
     # so the rebuilt unet keeps cond_on_video_embeds=False.
@@ -728,6 +733,17 @@ class Unet3D(nn.Module):
                    text_cond_drop_prob=0.0):
         """Core denoiser on channels-last frames x (batch*T, H, W, C8); returns
         channels-last (batch*T, H, W, channels_out)."""
+        if getattr(self, "fp8", False) and not torch.is_grad_enabled():
+            with ops.mx8_convs():
+                return self._forward_cl(x, time, batch=batch, lowres_cl=lowres_cl,
+                                        video_cond_drop_prob=video_cond_drop_prob,
+                                        text_cond_drop_prob=text_cond_drop_prob)
+        return self._forward_cl(x, time, batch=batch, lowres_cl=lowres_cl,
+                                video_cond_drop_prob=video_cond_drop_prob,
+                                text_cond_drop_prob=text_cond_drop_prob)
+
+    def _forward_cl(self, x, time, *, batch, lowres_cl=None, video_cond_drop_prob=0.0,
+                    text_cond_drop_prob=0.0):
         x = self.init_conv.forward_cl(x)
         r = x
         t, c, mid_c = self._conditioning(time, batch, x.device, video_cond_drop_prob,

@@ -615,6 +615,105 @@ class GradSink:
         self.dx = None
 
 
+# ---------------------------------------------------------------------------
+# MX-fp8 3x3 convs for sampling (BASELINE config 5; dv_mx8.hip)
+# ---------------------------------------------------------------------------
+class _Mx8State:
+    active = 0  # > 0 inside mx8_convs()
+
+
+class mx8_convs:
+    """Context: eligible 3x3 convs run in MX-fp8 (e4m3 operands with a power-
+    of-two scale per 32 channels, f32 accumulation, bf16 output) — forward
+    only: ignored while autograd records (training stays bf16 / f32).
+    Unet3D.forward_cl enters it when the unet's `fp8` flag is set."""
+
+    def __enter__(self):
+        _Mx8State.active += 1
+        return self
+
+    def __exit__(self, *exc):
+        _Mx8State.active -= 1
+        return False
+
+
+def mx8_ok(x0, x1, weight, res, ksize, h, w, nf):
+    """Mirror of dv_conv_fwd_mx8's contract (dv_hip.h)."""
+    if not _Mx8State.active or torch.is_grad_enabled() or ksize != 3 or x0.dtype != torch.bfloat16:
+        return False
+    c0 = x0.shape[3]
+    c1 = 0 if x1 is None else x1.shape[3]
+    cout, cin_real = weight.shape[0], weight.shape[1]
+    if cin_real != c0 + c1 or c0 % 64 or c1 % 64 or cout % 64:
+        return False
+    geom = (h == 8 and w == 8) or (w in (16, 32, 64, 128) and h % (128 // w) == 0)
+    if not geom or (nf * h * w) % 128:
+        return False
+    for t in (x0, x1, res):
+        if t is not None:
+            try:
+                ld = cl_ld(t)
+            except _lib.DVError:
+                return False
+            if ld % 8 or t.data_ptr() % 16:
+                return False
+    return True
+
+
+def mx8_quant(x):
+    """bf16 channels-last (NF, H, W, C) -> (q uint8 [M * C], s int32 [C/64 * M]):
+    MX-fp8 e4m3 bytes and the per-32-channel scale pairs (dv_mx8_quant)."""
+    nf, h, w, c = x.shape
+    m = nf * h * w
+    q = torch.empty(m * c, dtype=torch.uint8, device=x.device)
+    sc = torch.empty((c // 64) * m, dtype=torch.int32, device=x.device)
+    call("dv_mx8_quant", ptr(x), cl_ld(x), c, m, ptr(q), ptr(sc), stream())
+    return q, sc
+
+
+def mx8_weight_image(weight):
+    """The conv kernel's MX-fp8 image of a (cout, cin, 1, 3, 3) f32 weight, kept
+    in the current PackCache (trainer epoch + torch version checked; a sampling
+    region's private cache is fresh per sample() call)."""
+    w = weight.detach()
+    if w.dtype != torch.float32 or not w.is_contiguous():
+        w = w.float().contiguous()
+    cache = PACK.__dict__.setdefault("mx8", {})
+    key = (weight.data_ptr(), tuple(weight.shape))
+    ver = (PACK.epoch, weight._version)
+    e = cache.get(key)
+    if e is not None and e[0] == ver and e[2]() is weight:
+        return e[1]
+    import weakref
+    cout, cin = weight.shape[0], weight.shape[1]
+    n = ctypes.c_longlong(0)
+    call("dv_mx8_image_bytes", cout, cin, ctypes.byref(n))
+    img = torch.empty(n.value, dtype=torch.uint8, device=weight.device)
+    call("dv_mx8_pack_conv_weight", ptr(w), cout, cin, ptr(img), stream())
+    if PACK.enabled:
+        cache[key] = (ver, img, weakref.ref(weight))
+    return img
+
+
+def conv_mx8(x0, weight, bias=None, x1=None, res=None):
+    """y = conv3x3(cat(x0, x1)) + bias (+ res) in MX-fp8 (bf16 channels-last in / out)."""
+    require_gpu(x0, x1, weight, bias, res)
+    nf, h, w, c0 = x0.shape
+    c1 = 0 if x1 is None else x1.shape[3]
+    cout = weight.shape[0]
+    q0, s0 = mx8_quant(x0)
+    q1, s1 = mx8_quant(x1) if x1 is not None else (None, None)
+    img = mx8_weight_image(weight)
+    y = torch.empty(nf, h, w, cout, dtype=torch.bfloat16, device=x0.device)
+    b = None if bias is None else bias.detach().float().contiguous()
+    m = nf * h * w
+    _launch(f"conv_fwd_mx8_kernel<{w}>", 2.0 * m * cout * (c0 + c1) * 9, m * (c0 + c1 + 2 * cout),
+            lambda: call("dv_conv_fwd_mx8", ptr(q0), ptr(s0), c0, ptr(q1), ptr(s1), c1, ptr(img), ptr(b),
+                         ptr(res), cl_ld(res) if res is not None else 0, ptr(y), cout, nf, h, w, cout,
+                         stream()), ("fwd", m, cout, 9 * (c0 + c1)))
+    return y
+
+
 class ConvFn(torch.autograd.Function):
     """y = conv_(1,k,k)(cat(x0, x1)) + bias (+ res).  dalle2_video.py:107 etc."""
 
@@ -628,6 +727,10 @@ class ConvFn(torch.autograd.Function):
         cout, cin_real = weight.shape[0], weight.shape[1]
         if cin_real > cin:
             raise _lib.DVError(f"conv: weight expects {cin_real} input channels, got {cin}")
+        if mx8_ok(x0, x1, weight, res, ksize, h, w, nf):
+            if gn is not None:
+                gn.used = False  # the GroupNorm reduces z itself
+            return conv_mx8(x0, weight, bias, x1=x1, res=res)
         y = torch.empty(nf, h, w, cout, dtype=x0.dtype, device=x0.device)
         ld0 = cl_ld(x0)
         ld1 = cl_ld(x1) if x1 is not None else 0

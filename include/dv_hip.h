@@ -166,6 +166,29 @@ int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int
                  int ldy, int nf, int h, int w, int cin, int cout, int act, float* gn_sums,
                  long long gn_P, int gn_R, void* stream);
 
+/* ---- MX-fp8 3x3 forward (sampling; BASELINE config 5 — Block3D.project,
+ * dalle2_video.py:107, no autograd).  OCP MX-fp8: e4m3 elements, one e8m0
+ * power-of-two scale per 32 consecutive channels, on the block-scaled
+ * v_mfma_scale_f32_32x32x64_f8f6f4 (f32 accumulation).
+ *   dv_mx8_quant: bf16 channels-last x[M][ld] (C channels) -> q[M][C] e4m3
+ *     bytes + s[C/64][M] u32 (byte h = scale of channels [64c + 32h, +32)).
+ *     Scale 2^E with E the smallest power keeping the block max <= 448 in its
+ *     top binade; round to nearest even.  C % 64 == 0, ld % 8 == 0.
+ *   dv_mx8_image_bytes / dv_mx8_pack_conv_weight: f32 weight (cout, cin, 1,
+ *     3, 3) -> the kernel's swizzled image of e4m3 rows + scales,
+ *     [cout/64][cin/64][38,912 B].  cout, cin % 64 == 0.
+ *   dv_conv_fwd_mx8: y = conv3x3(cat(x0, x1)) + bias (+ res), y bf16.  x0 =
+ *     (q0, s0) with c0 channels, x1 = (q1, s1) with c1 (0: none), both % 64;
+ *     (h, w) = (8, 8), or w in {16, 32, 64, 128} with h % (128 / w) == 0;
+ *     nf * h * w % 128 == 0; cout % 64 == 0; ldy, ldres % 4 == 0; 16-B
+ *     aligned q / wimg.                                                     */
+int dv_mx8_quant(const void* x, int ld, int C, long long M, void* q, void* s, void* stream);
+int dv_mx8_image_bytes(int cout, int cin, long long* bytes);
+int dv_mx8_pack_conv_weight(const float* w, int cout, int cin, void* img, void* stream);
+int dv_conv_fwd_mx8(const void* q0, const void* s0, int c0, const void* q1, const void* s1, int c1,
+                    const void* wimg, const float* bias, const void* res, int ldres, void* y,
+                    int ldy, int nf, int h, int w, int cout, void* stream);
+
 /* db[c] += sum_p dy[p][c]  (f32 atomics) */
 int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix, int c,
                  void* stream);

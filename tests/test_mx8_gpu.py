@@ -1,0 +1,169 @@
+"""MX-fp8 sampling convs (BASELINE config 5: "fp8 MFMA ... conv", dv_mx8.hip)
+against exact restatements in torch.
+
+  quantisation   dv_mx8_quant vs a torch restatement of the rule (per 32
+                 channels: E = the power of two putting the block max in the
+                 top binade <= 448, e4m3 round-to-nearest-even): bit-exact
+                 bytes and scales
+  conv kernel    dv_conv_fwd_mx8 vs an f64 conv of the DEQUANTISED operands
+                 (the same e4m3 values and scales): the kernel's only error is
+                 f32 accumulation order and the bf16 output rounding —
+                 norm-wise <= 2e-3
+  quantisation error (logged, and bounded): vs the f64 conv of the original
+                 bf16 input and f32 weights, <= 8e-2
+  whole unet     unet1 forward in fp8 at a config-5 sub-shape (1x3x8x128x128:
+                 every frame width 128 .. 16 runs through the fp8 kernel) vs the
+                 CPU oracle (reference Unet3D.forward, dalle2_video.py:694-952),
+                 <= 0.15 (fp8 is a sampling performance mode; the bf16 forward of
+                 the same call is logged beside it)
+The observed values are printed and appended to $DV_PARITY_LOG.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import dv_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+
+def ref_quant(x):
+    """(..., C) float -> (e4m3 bytes (..., C), E (..., C/32)) by the MX rule."""
+    blk = x.float().reshape(*x.shape[:-1], x.shape[-1] // 32, 32)
+    bits = blk.abs().amax(-1).contiguous().view(torch.int32)
+    E = ((bits >> 23) & 255) - 135 + ((bits & 0x7FFFFF) > 0x600000).int()
+    E = E.clamp_min(-127)
+    scaled = torch.ldexp(blk, -E[..., None].float())
+    q = scaled.to(torch.float8_e4m3fn).view(torch.uint8).reshape(x.shape)
+    return q, E
+
+
+def dequant(q, E):
+    blk = q.reshape(*q.shape[:-1], q.shape[-1] // 32, 32).view(torch.float8_e4m3fn).double()
+    return (blk * torch.pow(2.0, E[..., None].double())).reshape(q.shape)
+
+
+def test_mx8_quant_bit_exact():
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(8)
+    nf, h, w, c = 3, 8, 16, 192
+    x = torch.randn(nf, h, w, c, generator=g)
+    # block magnitudes over 2^-30 .. 2^30, a zero block and a block at 448
+    x = x * torch.pow(2.0, torch.randint(-30, 31, (nf, h, w, c // 32, 1), generator=g).float()).repeat_interleave(32, -1).reshape(nf, h, w, c)
+    x[0, 0, 0, :32] = 0
+    x[0, 0, 1, :32] = 448.0
+    xb = x.to(torch.bfloat16)
+    wide = torch.zeros(nf, h, w, c + 64, dtype=torch.bfloat16)
+    wide[..., :c] = xb
+    xd = wide.cuda()[..., :c]  # a channel slice of a wider buffer (ld = C + 64)
+    q, s = ops.mx8_quant(xd)
+    torch.cuda.synchronize()
+    qr, Er = ref_quant(xb.float())
+    q = q.cpu().reshape(nf, h, w, c)
+    s = s.cpu().view(torch.uint8).reshape(c // 64, nf * h * w, 4)
+    got_E = torch.stack((s[..., 0], s[..., 1]), -1).permute(1, 0, 2).reshape(nf, h, w, c // 32).int() - 127
+    assert torch.equal(got_E, Er.int()), (got_E != Er).sum()
+    assert torch.equal(q, qr), (q != qr).sum()
+    assert (s[..., 2:] == 0).all()
+
+
+SHAPES = [  # nf, h, w, c0, c1, cout, with residual
+    (2, 8, 8, 64, 0, 64, False),
+    (1, 16, 16, 128, 0, 128, True),
+    (1, 8, 32, 64, 64, 64, False),
+    (2, 4, 64, 64, 0, 128, True),
+    (1, 3, 128, 64, 0, 64, True),
+    (1, 2, 128, 128, 64, 64, False),
+    (1, 16, 16, 512, 256, 512, True),
+]
+
+
+@pytest.mark.parametrize("nf,h,w,c0,c1,cout,with_res", SHAPES)
+def test_mx8_conv_vs_dequantised_reference(parity_log, nf, h, w, c0, c1, cout, with_res):
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(100 + w + c0 + c1)
+    cin = c0 + c1
+    x0 = torch.randn(nf, h, w, c0, generator=g).bfloat16()
+    x1 = torch.randn(nf, h, w, c1, generator=g).bfloat16() if c1 else None
+    wt = torch.randn(cout, cin, 1, 3, 3, generator=g) / (9 * cin) ** 0.5
+    b = 0.1 * torch.randn(cout, generator=g)
+    res = torch.randn(nf, h, w, cout, generator=g).bfloat16() if with_res else None
+    dev = lambda t: None if t is None else t.cuda()
+    with torch.no_grad(), ops.mx8_convs():
+        assert ops.mx8_ok(dev(x0), dev(x1), dev(wt), dev(res), 3, h, w, nf)
+        y = ops.conv(dev(x0), dev(wt), dev(b), x1=dev(x1), res=dev(res))
+        q0, s0 = ops.mx8_quant(dev(x0))
+        q1, s1 = ops.mx8_quant(dev(x1)) if c1 else (None, None)
+    torch.cuda.synchronize()
+    assert y.dtype == torch.bfloat16 and y.shape == (nf, h, w, cout)
+
+    def deq_x(q, s, c):
+        s = s.cpu().view(torch.uint8).reshape(c // 64, nf * h * w, 4)
+        E = torch.stack((s[..., 0], s[..., 1]), -1).permute(1, 0, 2).reshape(nf, h, w, c // 32).int() - 127
+        return dequant(q.cpu().reshape(nf, h, w, c), E)
+
+    xq = deq_x(q0, s0, c0)
+    if c1:
+        xq = torch.cat((xq, deq_x(q1, s1, c1)), -1)
+    wq_b, wE = ref_quant(wt[:, :, 0].permute(0, 2, 3, 1))  # (cout, 3, 3, cin): blocks along cin
+    wq = dequant(wq_b, wE).permute(0, 3, 1, 2)  # (cout, cin, 3, 3)
+
+    def conv64(x, wgt):
+        xin = x.double().permute(0, 3, 1, 2)
+        out = F.conv2d(xin, wgt.double(), b.double(), padding=1).permute(0, 2, 3, 1)
+        return out + (res.double() if with_res else 0)
+
+    ref_q = conv64(xq, wq)
+    xfull = x0.float() if not c1 else torch.cat((x0.float(), x1.float()), -1)
+    ref_full = conv64(xfull, wt[:, :, 0])
+    e_kernel = rel(y.float(), ref_q.to(torch.bfloat16).float())
+    e_quant = rel(y.float(), ref_full)
+    parity_log(shape=[nf, h, w, c0, c1, cout], res=with_res, kernel_rel=e_kernel, fp8_vs_exact_rel=e_quant)
+    assert e_kernel <= 2e-3, e_kernel
+    assert e_quant <= 8e-2, e_quant
+
+
+def test_unet1_fp8_forward_config5_subshape(parity_log):
+    """unet1 at 1x3x8x128x128 with every eligible 3x3 conv in MX-fp8 (128², 64²,
+    32², 16² stages) vs the f32 CPU oracle; the bf16 forward is logged beside."""
+    from dalle2_video import dalle2_video as D, ops
+
+    def build(mod):
+        u = mod.Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+        return u.cast_model_parameters(lowres_cond=False, lowres_noise_cond=False, channels=3,
+                                       channels_out=3, cond_on_image_embeds=True, cond_on_text_encodings=False)
+
+    torch.set_num_threads(min(16, torch.get_num_threads() * 2))
+    ou = R.deterministic_fill_(build(R))
+    g = torch.Generator().manual_seed(55)
+    x = torch.randn(1, 3, 8, 128, 128, generator=g)
+    t = torch.tensor([421])
+    with torch.no_grad():
+        yr = ou(x, t, video_embed=None)
+    u = build(D)
+    u.load_state_dict(ou.state_dict(), strict=True)
+    u = u.cuda()
+    ops.TIMER = ops.KernelTimer()
+    try:
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16), ops.private_pack_cache():
+            y16 = u(x.cuda(), t.cuda(), video_embed=None)
+            n_bf16 = len(ops.TIMER.records)
+            u.fp8 = True
+            y8 = u(x.cuda(), t.cuda(), video_embed=None)
+        n_mx8 = sum(1 for r in ops.TIMER.records if r[0].startswith("conv_fwd_mx8"))
+    finally:
+        ops.TIMER = None
+        u.fp8 = False
+    e16, e8 = rel(y16.float(), yr), rel(y8.float(), yr)
+    parity_log(config="unet1 fwd 1x3x8x128x128", bf16_rel=e16, fp8_rel=e8, mx8_convs=n_mx8,
+               launches_bf16=n_bf16)
+    assert n_mx8 >= 40, n_mx8  # every Block3D conv of the 4 stages + mid
+    assert torch.isfinite(y8).all()
+    assert e8 <= 0.15, e8
