@@ -35,6 +35,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "Unet3D denoise-steps/sec, 16f×64×64 clip bs=4; 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2516.6   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+PEAK_FP8_TFLOPS = 5033.2    # dense MX-fp8 MFMA, 2x bf16 per clock (MI355X_MICROARCH.md)
 PEAK_HBM_TBS = 8.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 STEP_TFLOP = 3.491          # ~3x the 1,163.6 GFLOP forward contractions
 FWD_TFLOP = 1.1636          # Cfg2 forward contractions (bs=4)
@@ -277,6 +278,42 @@ def sampling_leg(args, device):
             "frac": round(att["flops"] / (att["ms"] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)},
     }
     log(f"config5 bf16: {T5 / dt:.2f} steps/s")
+    # the same loop with the MX-fp8 convs (Unet3D.fp8: e4m3 operands with a
+    # power-of-two scale per 32 channels on v_mfma_scale_f32_32x32x64_f8f6f4)
+    dec.unets[0].fp8 = True
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        dec.sample(video_embed=emb, one_unet_in_gpu_at_time=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vid = dec.sample(video_embed=emb, one_unet_in_gpu_at_time=False)
+        torch.cuda.synchronize()
+        dt8 = time.perf_counter() - t0
+        ops.TIMER = ops.KernelTimer()
+        with torch.no_grad(), ops.private_pack_cache():
+            xin = torch.randn(2, 3, 32, 128, 128, device=device)
+            tin = torch.full((2,), 500, device=device, dtype=torch.long)
+            dec.unets[0](xin, tin)  # packs the fp8 weight images
+            ops.TIMER.records.clear()
+            dec.unets[0](xin, tin)
+        summ8 = ops.TIMER.summary()
+        ops.TIMER = None
+    dec.unets[0].fp8 = False
+    assert torch.isfinite(vid).all()
+    mx = {k: v for k, v in summ8.items() if k.startswith("conv_fwd_mx8")}
+    kname, kd = max(mx.items(), key=lambda kv: kv[1]["ms"])
+    k_tf = kd["flops"] / (kd["ms"] * 1e-3) / 1e12
+    out["config5_fp8"] = {
+        "config": "BASELINE config 5: unet1 sampling, 32x128x128 clip, bs=2, the 3x3 convs of the 32² / 16² "
+                  f"stages in MX-fp8 (e4m3 + e8m0 per 32 channels); {T5}-step DDPM loop timed",
+        "value": round(T5 / dt8, 2), "unit": "denoise-steps/s", "speedup_vs_bf16": round(dt / dt8, 3),
+        "est_1000_step_s": round(1000 * dt8 / T5, 1), "fp8_convs_per_step": sum(v["count"] for v in mx.values()),
+        "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(k_tf, 1), "peak": PEAK_FP8_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(k_tf / PEAK_FP8_TFLOPS, 4),
+                     "avg_launch_us": round(kd["ms"] / kd["count"] * 1e3, 2),
+                     "note": "dominant MX-fp8 conv kernel, HIP events per launch; peak = dense MX-fp8 MFMA"},
+        "kernels_ms_per_step": {k: round(v["ms"], 3) for k, v in sorted(mx.items(), key=lambda kv: -kv[1]["ms"])},
+    }
+    log(f"config5 fp8: {T5 / dt8:.2f} steps/s")
     del dec, u
     # config 4: two-stage cascade, base 16x64x64 + spatial-SR unet2 (dim 8, mults 1..16) to 256x256
     u1 = Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))

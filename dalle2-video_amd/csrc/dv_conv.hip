@@ -2929,6 +2929,16 @@ extern "C" int dv_wgrad_reduce_batched(const DvWgradReduceEntry* table, int n, l
   return check_launch("wgrad_reduce_batched");
 }
 
+extern "C" int dv_wgrad_reduce_one(const DvWgradReduceEntry* e, void* stream) {
+  DV_REQUIRE(e && e->S >= 1 && e->n4 > 0 && e->cout % 4 == 0 && e->part && e->dw && (!e->db || e->dbpart),
+             "bad entry");
+  const int G = reduce4_groups(e->S);
+  wgrad_reduce4_kernel<<<(unsigned)reduce4_blocks(e->n4, G, e->cout, e->db != nullptr), 256, 0,
+                         (hipStream_t)stream>>>(e->part, e->S, G, e->n4, e->dw, e->acc_w, e->dbpart, e->db,
+                                                e->cout, e->acc_b);
+  return check_launch("wgrad_reduce_one");
+}
+
 extern "C" int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, long long max_elems,
                                             void* stream) {
   DV_REQUIRE(table && n >= 0 && n <= 65535, "bad table");

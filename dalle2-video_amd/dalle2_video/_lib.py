@@ -42,6 +42,7 @@ _SIGS = {
                                _I, _I, _P, _P],
     "dv_wgrad_reduce_plan": [_P, _I, _P],
     "dv_wgrad_reduce_batched": [_P, _I, _L, _P],
+    "dv_wgrad_reduce_one": [_P, _P],
     "dv_cross_embed_image_elems": [_P, _P],
     "dv_cross_embed_pack": [_P, _P, _P],
     "dv_cross_embed_fwd": [_P, _P, _P, _I, _P, _I, _I, _I, _I, _P],

@@ -750,8 +750,11 @@ class Unet3D(nn.Module):
                                          text_cond_drop_prob)
         pre = self._grouped_projections(t, c, mid_c, batch, x.dtype)
 
+        mark = ops.backward_mark  # backward progress marks (trainer's overlapped all-reduce)
+
         def run(blk, x, cond, x1=None):
             ss, kv, fold = pre.get(id(blk), (None, None, None))
+            mark(x)
             return blk.forward_cl(x, t, cond, batch, x1=x1, ss=ss, kv=kv, fold=fold)
 
         hiddens = []
@@ -761,9 +764,11 @@ class Unet3D(nn.Module):
                 x = run(blk, x, c)
                 hiddens.append(x)
             hiddens.append(x)  # after the Identity attention
+            mark(x)
             x = post.forward_cl(x)
         x = run(self.mid_block1, x, mid_c)
         if exists(self.mid_attn):
+            mark(x)
             x = self.mid_attn.forward_cl(x, batch)
         x = run(self.mid_block2, x, mid_c)
         for init_block, blocks, attn, up in self.ups:
@@ -771,8 +776,10 @@ class Unet3D(nn.Module):
             for blk in blocks:
                 x = run(blk, x, c, x1=hiddens.pop())
             if not isinstance(up, nn.Identity):
+                mark(x)
                 x = up.forward_cl(x)
         x = run(self.final_resnet_block, x, None, x1=r)
+        mark(x)
         return ops.conv(x, self.to_out.weight, self.to_out.bias, x1=lowres_cl)
 
     def forward(self, x, time, *, video_embed=None, lowres_cond_video=None,

@@ -240,6 +240,16 @@ class _WgradDefer:
     # flush once this many partial bytes are pending (0 = only at the end of
     # the pass): a smaller batch is read back while still in the 256 MB MALL
     FLUSH_BYTES = int(os.environ.get("DV_DEFER_MB", "0")) << 20
+    # streamed sums (DV_DEFER_STREAM=1): each conv's split-K sum is launched
+    # on a side stream right after its wgrad, to overlap the memory-bound sum
+    # with the MFMA / LDS-bound convs of the rest of the backward; the side
+    # stream is joined when the pass ends (and before any other kernel writes
+    # a gradient a pending sum targets).  Measured slower on the whole step
+    # (same box, tools/gpu_r03e.sh: 84.7 vs 95.3 steps/s — the side-stream
+    # sums take CU slots and HBM from the 1-workgroup-per-CU convs), so the
+    # default is one batched sum at the end of the pass.
+    STREAM = os.environ.get("DV_DEFER_STREAM", "0") == "1"
+    _sides = {}
 
     def __init__(self):
         self.active = 0
@@ -248,6 +258,30 @@ class _WgradDefer:
         self.chunks = {}  # device -> [tensor]
         self.cursor = (0, 0)
         self.tables = {}  # (device, bytes) -> (device table, blocks)
+        self.streamed = None  # device whose side stream holds unjoined sums
+        self.added = 0  # entries deferred in this pass (streamed or pending)
+
+    def _side(self, device):
+        key = str(device)
+        if key not in self._sides:
+            self._sides[key] = torch.cuda.Stream(device=device)
+        return self._sides[key]
+
+    def join(self):
+        """The current stream waits for every streamed sum launched so far."""
+        if self.streamed is not None:
+            torch.cuda.current_stream(self.streamed).wait_stream(self._side(self.streamed))
+            self.streamed = None
+            self.targets.clear()
+
+    def before_write(self, *ptrs):
+        """Call before a kernel outside the deferral writes a gradient buffer:
+        a pending (batched) or in-flight (streamed) sum into it lands first."""
+        if any(p is not None and p in self.targets for p in ptrs):
+            if self.streamed is not None:
+                self.join()
+            else:
+                self.flush()
 
     def slot(self, device, floats):
         floats = (floats + 63) // 64 * 64
@@ -262,6 +296,18 @@ class _WgradDefer:
             ci, off = ci + 1, 0
 
     def add(self, entry, device):
+        self.added += 1
+        if self.STREAM:
+            main = torch.cuda.current_stream(device)
+            side = self._side(device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                call("dv_wgrad_reduce_one", ctypes.byref(entry), stream())
+            self.streamed = device
+            self.targets.add(entry.dw)
+            if entry.db:
+                self.targets.add(entry.db)
+            return
         self.pending.append((entry, device))
         self.targets.add(entry.dw)
         if entry.db:
@@ -274,6 +320,7 @@ class _WgradDefer:
         return any(p is not None and p in self.targets for p in ptrs)
 
     def flush(self):
+        self.join()
         if not self.pending:
             self.cursor = (0, 0)
             return
@@ -298,6 +345,8 @@ class _WgradDefer:
         self.cursor = (0, 0)
 
     def discard(self):
+        self.join()
+        self.added = 0
         self.pending.clear()
         self.targets.clear()
         self.pending_bytes = 0
@@ -348,6 +397,20 @@ def _xattn_workspace(nb, C, device, owner=None):
         torch.zeros(nb, 32, dtype=torch.float32, device=device),)
     _XA_WS[key] = (None if owner is None else weakref.ref(owner), ws)
     return ws
+
+
+class _BackwardMarks:
+    """Module-boundary marks for the trainer's overlapped gradient all-reduce:
+    while a tracker is set, Unet3D's forward registers a hook on each block's
+    input, so the tracker is called (in a fixed order) as the backward
+    finishes each block."""
+    tracker = None
+
+
+def backward_mark(x):
+    t = _BackwardMarks.tracker
+    if t is not None and torch.is_grad_enabled() and x.requires_grad:
+        x.register_hook(t.on_hit)
 
 
 class _GnSums:
@@ -637,9 +700,21 @@ class mx8_convs:
         return False
 
 
+# where the MX-fp8 conv runs (tools/cfg5_profile.py, same-box rocprof-free
+# per-launch timing at the config-5 shapes): frame widths <= 32 — the 16² / 32²
+# stages with 128 .. 768 input channels run 1.1-2.0x faster than their bf16
+# kernels (512 -> 512 at 16²: 114 -> 59 us) — while at 64² / 128² with 64-192
+# input channels (one or two 64-channel chunks per tile: no pipelining over K,
+# the operand DMA latency exposed) the bf16 stripe / glds kernels win and the
+# quantisation pass would cost more.  DV_FP8_ALL=1 puts every eligible conv on it.
+_MX8_MAX_W = 128 if os.environ.get("DV_FP8_ALL", "0") == "1" else 32
+
+
 def mx8_ok(x0, x1, weight, res, ksize, h, w, nf):
-    """Mirror of dv_conv_fwd_mx8's contract (dv_hip.h)."""
-    if not _Mx8State.active or torch.is_grad_enabled() or ksize != 3 or x0.dtype != torch.bfloat16:
+    """Mirror of dv_conv_fwd_mx8's contract (dv_hip.h), restricted to the
+    frame widths where it measured faster (_MX8_MAX_W)."""
+    if (not _Mx8State.active or torch.is_grad_enabled() or ksize != 3 or x0.dtype != torch.bfloat16
+            or w > _MX8_MAX_W):
         return False
     c0 = x0.shape[3]
     c1 = 0 if x1 is None else x1.shape[3]
@@ -867,8 +942,9 @@ class ConvFn(torch.autograd.Function):
             if (WGRAD_DEFER.active and dw is None and db is None and not _WgradStream.enabled
                     and kname.startswith("conv_wgrad_stripe")):
                 # leaf .grad targets: leave the split partials for the pass-end sum
-                if WGRAD_DEFER.conflicts(dw_t.data_ptr(), db_t.data_ptr() if db_t is not None else None):
-                    WGRAD_DEFER.flush()  # a second gradient into the same target
+                if (not WGRAD_DEFER.STREAM
+                        and WGRAD_DEFER.conflicts(dw_t.data_ptr(), db_t.data_ptr() if db_t is not None else None)):
+                    WGRAD_DEFER.flush()  # a second gradient into the same target (streamed sums stay ordered)
                 need = ctypes.c_longlong(0)
                 call("dv_conv_wgrad_ws", dt(dy8), nf, h, w, cin, c0, int(x1 is not None), cout8, ksize,
                      ctypes.byref(need))
@@ -885,6 +961,7 @@ class ConvFn(torch.autograd.Function):
                     WGRAD_DEFER.add(ent, dy.device)
                 dres = dy if has_res else None
                 return dx0, dx1, dw, db, dres, None, None, None, None, None
+            WGRAD_DEFER.before_write(dw_t.data_ptr(), db_t.data_ptr() if db_t is not None else None)
             ws = _wgrad_workspace(_lib.dtype_name(dy8), nf, h, w, cin, c0, x1 is not None, cout8,
                                   ksize, dy.device)
             # on the side stream only when the results go straight into leaf
@@ -905,6 +982,7 @@ class ConvFn(torch.autograd.Function):
                 db_buf = torch.zeros(cout8, dtype=torch.float32, device=dy.device)
             else:
                 db_buf = bslot[0]
+            WGRAD_DEFER.before_write(bslot[0].data_ptr() if bslot is not None else None)
             run = (_WgradStream.run if bslot is not None and db_buf is bslot[0]
                    else (lambda dev, f, ts: f()))
             run(dy.device, lambda: call("dv_bias_grad", dt(dy8), ptr(dy8), lddy, ptr(db_buf),

@@ -58,6 +58,7 @@ class FusedAdamW(torch.optim.Optimizer):
         # their addresses (captured HIP graphs, packed-weight images) is stale
         self.generation = 0
         self._probe = ()  # (param, data offset, grad offset) spot checks of the aliasing
+        self.order_key = None  # optional sort key of the parameters within a group
 
     # -- flat storage ------------------------------------------------------
     def _build_flat(self):
@@ -81,11 +82,13 @@ class FusedAdamW(torch.optim.Optimizer):
         ranges = []
         off = 0
         self._offsets = {}
+        key = self.order_key  # flat order within a group (the all-reduce buckets follow it)
         for gi in range(len(self.param_groups)):
             start = off
-            for g2, p in live:
-                if g2 != gi:
-                    continue
+            members = [p for g2, p in live if g2 == gi]
+            if key is not None:
+                members.sort(key=key)
+            for p in members:
                 k = p.numel()
                 st = self.state.get(p, {})
                 P[off:off + k].copy_(p.detach().reshape(-1))
@@ -437,7 +440,7 @@ def broadcast_parameters(module, src=0):
 BUCKET_BYTES = int(os.environ.get("DV_BUCKET_MB", "25")) * (1 << 20)
 
 
-def allreduce_flat_grad(flat_grad, world, bucket_bytes=None):
+def allreduce_flat_grad(flat_grad, world, bucket_bytes=None, force=False):
     """The only collective on the data path: the SUM all-reduce of the active
     unet's flat f32 gradient (RCCL over xGMI on the GPU box), in ~25 MB
     buckets issued back to front (the flat buffer follows parameter order, so
@@ -448,7 +451,7 @@ def allreduce_flat_grad(flat_grad, world, bucket_bytes=None):
     for all of them once.  The 1/world average is not applied here: it is
     folded into the clip coefficient (dv_grad_clip_coef's prescale), which
     the AdamW kernel multiplies in."""
-    if world <= 1 or flat_grad is None:
+    if (world <= 1 and not force) or flat_grad is None:
         return flat_grad
     n = flat_grad.numel()
     per = max(1, (bucket_bytes or BUCKET_BYTES) // flat_grad.element_size())
@@ -458,6 +461,141 @@ def allreduce_flat_grad(flat_grad, world, bucket_bytes=None):
     for w in works:
         w.wait()
     return flat_grad
+
+
+class OverlappedAllReduce:
+    """The gradient all-reduce of one unet overlapped with its backward — what
+    DDP's bucket hooks do inside the reference's accelerator.backward
+    (trainer.py:360).
+
+    * The first training call RECORDS the backward order: Unet3D's forward
+      marks every block input (ops.backward_mark) and, at each mark's
+      gradient hook, the parameters whose .grad exists by then get that hook's
+      index (their gradient kernels — or streamed split-K sums — have been
+      launched).  Parameters never seen before the end rank last.
+    * The optimizer's flat buffer is laid out in that order within each
+      weight-decay group (FusedAdamW.order_key), and cut into ~BUCKET_BYTES
+      buckets of whole parameters; a bucket is ready at the largest index of
+      its parameters.
+      (Each Unet3D parameter's gradient comes from ONE backward op — no
+      weight is applied twice — so its first appearance is its completion.)
+    * Every later call: at hook k, each bucket ready by k is all-reduced (SUM)
+      on a comm stream that first waits for the compute stream and the
+      streamed-wgrad-sum stream; the rest go at the end of the backward.
+      update() waits for them (a captured call joins them inside the graph).
+    The 1/world average stays in the clip coefficient, as before."""
+
+    def __init__(self, opt, world):
+        self.opt, self.world = opt, world
+        self.ranks = None      # id(param) -> backward index
+        self.mode = None       # "record" / "run" during a call
+        self.hit = 0
+        self.plan = None       # (generation, [(start, end, ready)])
+        self.launched = 0
+        self.works = []
+        self.comm = None
+        self.params = None
+
+    def attach(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        big = 1 << 30
+        self.opt.order_key = lambda p: (self.ranks or {}).get(id(p), big)
+
+    def _buckets(self):
+        gen = self.opt.generation
+        if self.plan is not None and self.plan[0] == gen:
+            return self.plan[1]
+        P, G, M, V, ranges, params = self.opt._flat
+        big = 1 << 30
+        per = max(1, BUCKET_BYTES // 4)
+        spans = sorted((self.opt._offsets[id(p)], p.numel(), self.ranks.get(id(p), big) if self.ranks else big)
+                       for p in params)
+        out, cur = [], None
+        for gi, gstart, gend in ranges:  # buckets never straddle a group boundary
+            for off, n, rk in spans:
+                if not gstart <= off < gend:
+                    continue
+                if cur is None or (off + n) - cur[0] > per:
+                    if cur is not None:
+                        out.append(tuple(cur))
+                    cur = [off, off + n, rk]
+                else:
+                    cur[1], cur[2] = off + n, max(cur[2], rk)
+            if cur is not None:
+                cur[1] = gend  # include the alignment gap
+                out.append(tuple(cur))
+                cur = None
+        self.plan = (gen, out)
+        return out
+
+    def begin(self):
+        """Before a training call's forward: arm the hooks."""
+        self.hit = 0
+        self.launched = 0
+        if self.ranks is None:
+            self.mode = "record"
+            self.ranks = {}
+            # a gradient that exists before the backward (accumulating into an
+            # earlier one) says nothing about the order: those rank last
+            self._pre = {id(p) for p in self.params if p.grad is not None}
+        elif self.opt._flat is not None and self.opt._aliased():
+            self.mode = "run"
+            self.comm = self.comm or torch.cuda.Stream(device=self.opt._flat[1].device)
+        else:
+            self.mode = None
+            return
+        ops._BackwardMarks.tracker = self
+
+    def on_hit(self, grad):
+        self.hit += 1
+        if self.mode == "record":
+            for p in self.params:
+                if id(p) not in self.ranks and p.grad is not None and id(p) not in self._pre:
+                    self.ranks[id(p)] = self.hit
+        elif self.mode == "run":
+            self._launch(self.hit)
+        return None
+
+    def _launch(self, upto):
+        buckets = self._buckets()
+        G = self.opt.flat_grad
+        if (self.launched < len(buckets) and buckets[self.launched][2] <= upto
+                and ops.WGRAD_DEFER.pending):
+            # batched split-K sums pending: land them before the bucket goes out
+            ops.WGRAD_DEFER.flush()
+        while self.launched < len(buckets) and buckets[self.launched][2] <= upto:
+            start, end, _ = buckets[self.launched]
+            dev = G.device
+            self.comm.wait_stream(torch.cuda.current_stream(dev))
+            side = ops.WGRAD_DEFER.streamed
+            if side is not None:
+                self.comm.wait_stream(ops.WGRAD_DEFER._side(side))
+            with torch.cuda.stream(self.comm):
+                self.works.append(dist.all_reduce(G[start:end], async_op=True))
+            self.launched += 1
+
+    def end(self, join):
+        """After the backward (the deferred-wgrad sums joined): the remaining
+        buckets; join=True waits for every bucket here (a captured call)."""
+        ops._BackwardMarks.tracker = None
+        mode, self.mode = self.mode, None
+        if mode == "record":
+            return False
+        if mode != "run":
+            return False
+        self._launch(1 << 31)
+        if join:
+            self.wait()
+        return True
+
+    def abort(self):
+        ops._BackwardMarks.tracker = None
+        self.mode = None
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
 
 
 class VideoDecoderTrainer(nn.Module):
@@ -502,6 +640,19 @@ class VideoDecoderTrainer(nn.Module):
                                   for i, w in enumerate(warmup_steps)]
         self.max_grad_norm = max_grad_norm
         self.register_buffer("steps", torch.tensor([0] * self.num_unets))
+        # gradient all-reduce overlapped with the backward (N > 1; DV_OVERLAP=0
+        # turns it off; DV_FORCE_ALLREDUCE=1 runs the collective path on a
+        # one-rank group too, for tests)
+        self.force_allreduce = (os.environ.get("DV_FORCE_ALLREDUCE", "0") == "1"
+                                and dist.is_available() and dist.is_initialized())
+        self.overlap = None
+        if (self.world > 1 or self.force_allreduce) and os.environ.get("DV_OVERLAP", "1") != "0":
+            self.overlap = []
+            for i, unet in enumerate(decoder.unets):
+                ov = OverlappedAllReduce(getattr(self, f"optim{i}"), self.world)
+                ov.attach(unet.parameters())
+                self.overlap.append(ov)
+        self._reduced = [False] * self.num_unets  # the last call's gradient is already all-reduced
         # accelerator.prepare(..., train, val) (trainer.py:117-124) shards the
         # loaders per process: each rank iterates a disjoint rank-strided part
         # and places the batches on the device (here: pinned host batches
@@ -562,8 +713,13 @@ class VideoDecoderTrainer(nn.Module):
         index = unet_number - 1
         opt = getattr(self, f"optim{index}")
         sched = getattr(self, f"sched{index}")
-        self._check_flat(unet_number)
-        allreduce_flat_grad(opt.flat_grad, self.world)
+        if self._check_flat(unet_number):
+            self._reduced[index] = False  # re-pointed buffers: reduce the copied gradient again
+        if self._reduced[index]:
+            self.overlap[index].wait()  # the overlapped buckets (a captured call joined them already)
+        else:
+            allreduce_flat_grad(opt.flat_grad, self.world, force=self.force_allreduce)
+        self._reduced[index] = False
         coef = opt.clip_coefficient(self.max_grad_norm, prescale=1.0 / self.world)
         opt.step(clip_coef=coef)
         opt.zero_grad()
@@ -586,6 +742,9 @@ class VideoDecoderTrainer(nn.Module):
             else:
                 return v
         return v.to(self.device)
+
+    def _overlap_for(self, unet_number):
+        return None if self.overlap is None else self.overlap[unet_number - 1]
 
     def _graphable(self, unet_number, max_batch_size, return_lowres_cond_video):
         from . import ops
@@ -610,19 +769,34 @@ class VideoDecoderTrainer(nn.Module):
         if "graph" not in ent:
             sargs = tuple(a.clone() if torch.is_tensor(a) else a for a in args)
             skw = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in kwargs.items()}
+            # the overlapped all-reduce goes into the graph only where the
+            # collective can be captured (RCCL); with gloo the update reduces
+            ov = self._overlap_for(unet_number)
+            if ov is not None and not (dist.get_backend() == "nccl"):
+                ov = None
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
+            overlapped = False
             with torch.cuda.graph(g):
                 ctx = (torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False)
                        if self.amp else nullcontext())
-                with ops.defer_wgrad():  # one split-K sum launch for the whole backward
-                    with ctx:
-                        loss = self.decoder(*sargs, unet_number=unet_number, **skw)
-                    loss.backward()
+                if ov is not None:
+                    ov.begin()
+                try:
+                    with ops.defer_wgrad():  # split-K sums streamed (or batched) inside the pass
+                        with ctx:
+                            loss = self.decoder(*sargs, unet_number=unet_number, **skw)
+                        loss.backward()
+                except BaseException:
+                    if ov is not None:
+                        ov.abort()
+                    raise
+                if ov is not None:
+                    overlapped = ov.end(join=True)  # collectives captured and joined
                 # replays start from zeroed GroupNorm sums whatever the parity
                 # of the GroupNorm calls inside the graph (ops._GnSums)
                 ops.gn_graph_boundary(loss.device)
-            ent.update(graph=g, args=sargs, kwargs=skw, loss=loss.detach())
+            ent.update(graph=g, args=sargs, kwargs=skw, loss=loss.detach(), overlapped=overlapped)
         for dst, src in zip(ent["args"], args):
             if torch.is_tensor(dst):
                 dst.copy_(src)
@@ -630,6 +804,7 @@ class VideoDecoderTrainer(nn.Module):
             if torch.is_tensor(v):
                 ent["kwargs"][k].copy_(v)
         ent["graph"].replay()
+        self._reduced[unet_number - 1] = ent["overlapped"]
         return ent["loss"].item()
 
     def forward(self, *args, unet_number=None, max_batch_size=None, return_lowres_cond_video=False,
@@ -648,19 +823,32 @@ class VideoDecoderTrainer(nn.Module):
                 return out
         total_loss = 0.0
         cond_videos = []
-        for frac, (cargs, ckw) in split_args_and_kwargs(*args, split_size=max_batch_size, **kwargs):
+        chunks = list(split_args_and_kwargs(*args, split_size=max_batch_size, **kwargs))
+        # overlap only a single-chunk call (chunks accumulate into the same buffer)
+        ov = self._overlap_for(unet_number) if (self.training and len(chunks) == 1) else None
+        self._reduced[unet_number - 1] = False
+        for frac, (cargs, ckw) in chunks:
             ctx = torch.autocast("cuda", dtype=torch.bfloat16) if self.amp else nullcontext()
-            with ops.defer_wgrad():  # the gradients are complete when it exits
-                with ctx:
-                    out = self.decoder(*cargs, unet_number=unet_number,
-                                       return_lowres_cond_video=return_lowres_cond_video, **ckw)
-                loss, cv = (out if return_lowres_cond_video else (out, None))
-                loss = loss * frac
-                if cv is not None:
-                    cond_videos.append(cv)
-                total_loss += loss.item()
-                if self.training:
-                    loss.backward()
+            if ov is not None:
+                ov.begin()
+            try:
+                with ops.defer_wgrad():  # the gradients are complete when it exits
+                    with ctx:
+                        out = self.decoder(*cargs, unet_number=unet_number,
+                                           return_lowres_cond_video=return_lowres_cond_video, **ckw)
+                    loss, cv = (out if return_lowres_cond_video else (out, None))
+                    loss = loss * frac
+                    if cv is not None:
+                        cond_videos.append(cv)
+                    total_loss += loss.item()
+                    if self.training:
+                        loss.backward()
+            except BaseException:
+                if ov is not None:
+                    ov.abort()
+                raise
+            if ov is not None:
+                self._reduced[unet_number - 1] = ov.end(join=False)
         if return_lowres_cond_video:
             return total_loss, torch.stack(cond_videos)
         return total_loss

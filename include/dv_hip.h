@@ -101,6 +101,9 @@ int dv_conv_wgrad_deferred(int dtype, const void* dy, int lddy, const void* x0, 
 int dv_wgrad_reduce_plan(DvWgradReduceEntry* host_table, int n, long long* blocks);
 int dv_wgrad_reduce_batched(const DvWgradReduceEntry* table, int n, long long blocks,
                             void* stream);
+/* One pending entry (a HOST pointer: the fields ride in the kernel arguments,
+ * no device table), e.g. on a side stream right after its wgrad.          */
+int dv_wgrad_reduce_one(const DvWgradReduceEntry* entry, void* stream);
 
 /* ---- CrossEmbedLayer3D (dalle2_video.py:208-244, Unet3D.init_conv) ------
  * nbranch parallel (1,k_b,k_b) 'same' convolutions of one small-channel

@@ -2,7 +2,11 @@
 (__call__ + update, HIP-graph capture on) under torch.distributed (gloo, every
 rank on cuda:0), training on its rank-strided share of one fixed global batch.
 
-  python tests/dp_trainer_worker.py OUT_DIR WORLD RANK PORT
+  python tests/dp_trainer_worker.py OUT_DIR WORLD RANK PORT [BACKEND]
+
+BACKEND gloo (default) or nccl (one rank only on the one-GPU box: with
+DV_FORCE_ALLREDUCE=1 the trainer's overlapped all-reduce then runs on a
+one-rank RCCL group, captured into the HIP graph).
 
 The decoder's two random draws — `times` (torch.randint, reference
 dalle2_video.py:2229) and `noise` (torch.randn_like in p_losses, :1946) — are
@@ -25,11 +29,15 @@ GLOBAL_B, T, S, STEPS = 4, 4, 32, 5
 
 def main():
     out_dir, world, rank, port = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-    if world > 1:
+    backend = sys.argv[5] if len(sys.argv) > 5 else "gloo"
+    torch.cuda.set_device(0)
+    if world > 1 or backend == "nccl":
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = port
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     from dalle2_video.dalle2_video import Unet3D, VideoDecoder
     from dalle2_video.trainer import VideoDecoderTrainer
     from dalle2_video.utils import deterministic_fill_
@@ -81,10 +89,12 @@ def main():
         tr.update(1)
     torch.cuda.synchronize()
     graphed = any("graph" in v for v in tr._graphs.values())
+    overlapped = any(v.get("overlapped", False) for v in tr._graphs.values())
     params = torch.cat([p.detach().reshape(-1) for p in dec.unets[0].parameters()]).cpu()
-    torch.save(dict(losses=losses, grad0=grad0, params=params, init=init, graphed=graphed, per=per),
-               os.path.join(out_dir, f"w{world}_r{rank}.pt"))
-    if world > 1:
+    torch.save(dict(losses=losses, grad0=grad0, params=params, init=init, graphed=graphed, per=per,
+                    overlapped=overlapped, buckets=0 if tr.overlap is None else len(tr.overlap[0]._buckets())),
+               os.path.join(out_dir, f"w{world}_r{rank}_{backend}.pt"))
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -13,6 +13,12 @@ Checked (tests/dp_trainer_worker.py writes what each rank saw):
     (rel <= 1e-5);
   * after 5 updates (all-reduce, clip, AdamW): both ranks hold bit-identical
     weights, == the world-1 weights (rel <= 1e-5).
+The two eager calls after the first run the all-reduce OVERLAPPED with the
+backward (bucket all-reduces launched from backward progress hooks,
+trainer.OverlappedAllReduce): a bucket reduced before its last gradient
+landed would break the match.  A second test runs the overlapped path on a
+one-rank RCCL group (DV_FORCE_ALLREDUCE=1) where the collectives are captured
+into the HIP graph, and checks it against the plain run.
 """
 import os
 import socket
@@ -32,10 +38,12 @@ def _port():
         return str(s.getsockname()[1])
 
 
-def _run(out, world):
+def _run(out, world, backend="gloo", env_extra=None):
     port = _port()
-    env = dict(os.environ)
-    procs = [subprocess.Popen([sys.executable, WORKER, str(out), str(world), str(r), port], env=env,
+    # 1 MB buckets: the small test unet (12.5 MB of gradient) spans a dozen,
+    # so the overlapped all-reduce launches most of them mid-backward
+    env = dict(os.environ, DV_BUCKET_MB="1", **(env_extra or {}))
+    procs = [subprocess.Popen([sys.executable, WORKER, str(out), str(world), str(r), port, backend], env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(world)]
     logs = []
     for p in procs:
@@ -48,7 +56,7 @@ def _run(out, world):
         logs.append(o.decode(errors="replace"))
     for p, lg in zip(procs, logs):
         assert p.returncode == 0, lg[-3000:]
-    return [torch.load(os.path.join(out, f"w{world}_r{r}.pt"), weights_only=True) for r in range(world)]
+    return [torch.load(os.path.join(out, f"w{world}_r{r}_{backend}.pt"), weights_only=True) for r in range(world)]
 
 
 def rel(a, b):
@@ -70,3 +78,18 @@ def test_two_rank_trainer_matches_one_rank(tmp_path, parity_log):
     assert l_err <= 1e-5, l_err
     assert torch.equal(two[0]["params"], two[1]["params"]), "ranks diverged after the all-reduced updates"
     assert p_err <= 1e-5, p_err
+
+
+def test_overlapped_allreduce_captured_on_one_rank_rccl(tmp_path, parity_log):
+    """The overlapped bucket all-reduces inside the captured training graph
+    (RCCL, one rank: the sums are identities) leave the training identical to
+    the run without a process group."""
+    plain = _run(tmp_path, 1)[0]
+    rccl = _run(tmp_path, 1, "nccl", {"DV_FORCE_ALLREDUCE": "1"})[0]
+    assert rccl["graphed"] and rccl["overlapped"], "the captured call did not include the all-reduce"
+    assert rccl["buckets"] >= 8, rccl["buckets"]
+    p_err = rel(rccl["params"], plain["params"])
+    l_err = max(abs(a - b) / abs(b) for a, b in zip(rccl["losses"], plain["losses"]))
+    parity_log(config="1-rank RCCL, overlapped all-reduce captured", params_rel=p_err, loss_rel_max=l_err,
+               buckets=rccl["buckets"])
+    assert p_err <= 1e-5 and l_err <= 1e-5, (p_err, l_err)

@@ -12,7 +12,7 @@ against exact restatements in torch.
   quantisation error (logged, and bounded): vs the f64 conv of the original
                  bf16 input and f32 weights, <= 8e-2
   whole unet     unet1 forward in fp8 at a config-5 sub-shape (1x3x8x128x128:
-                 every frame width 128 .. 16 runs through the fp8 kernel) vs the
+                 the 32² / 16² stage convs run in fp8 — ops._MX8_MAX_W) vs the
                  CPU oracle (reference Unet3D.forward, dalle2_video.py:694-952),
                  <= 0.15 (fp8 is a sampling performance mode; the bf16 forward of
                  the same call is logged beside it)
@@ -96,11 +96,13 @@ def test_mx8_conv_vs_dequantised_reference(parity_log, nf, h, w, c0, c1, cout, w
     b = 0.1 * torch.randn(cout, generator=g)
     res = torch.randn(nf, h, w, cout, generator=g).bfloat16() if with_res else None
     dev = lambda t: None if t is None else t.cuda()
+    saved, ops._MX8_MAX_W = ops._MX8_MAX_W, 128  # the kernel at every frame width
     with torch.no_grad(), ops.mx8_convs():
         assert ops.mx8_ok(dev(x0), dev(x1), dev(wt), dev(res), 3, h, w, nf)
         y = ops.conv(dev(x0), dev(wt), dev(b), x1=dev(x1), res=dev(res))
         q0, s0 = ops.mx8_quant(dev(x0))
         q1, s1 = ops.mx8_quant(dev(x1)) if c1 else (None, None)
+    ops._MX8_MAX_W = saved
     torch.cuda.synchronize()
     assert y.dtype == torch.bfloat16 and y.shape == (nf, h, w, cout)
 
@@ -131,8 +133,8 @@ def test_mx8_conv_vs_dequantised_reference(parity_log, nf, h, w, c0, c1, cout, w
 
 
 def test_unet1_fp8_forward_config5_subshape(parity_log):
-    """unet1 at 1x3x8x128x128 with every eligible 3x3 conv in MX-fp8 (128², 64²,
-    32², 16² stages) vs the f32 CPU oracle; the bf16 forward is logged beside."""
+    """unet1 at 1x3x8x128x128 with the 32² / 16² stage convs in MX-fp8 vs the
+    f32 CPU oracle; the bf16 forward is logged beside."""
     from dalle2_video import dalle2_video as D, ops
 
     def build(mod):
@@ -164,6 +166,6 @@ def test_unet1_fp8_forward_config5_subshape(parity_log):
     e16, e8 = rel(y16.float(), yr), rel(y8.float(), yr)
     parity_log(config="unet1 fwd 1x3x8x128x128", bf16_rel=e16, fp8_rel=e8, mx8_convs=n_mx8,
                launches_bf16=n_bf16)
-    assert n_mx8 >= 40, n_mx8  # every Block3D conv of the 4 stages + mid
+    assert n_mx8 >= 24, n_mx8  # the Block3D convs of the 32² / 16² stages and the mid block
     assert torch.isfinite(y8).all()
     assert e8 <= 0.15, e8

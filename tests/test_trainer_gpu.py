@@ -137,13 +137,16 @@ def test_train_sample_train_keeps_training(use_ema):
         assert ((pa - pb).norm() / pa.norm().clamp_min(1e-30)).item() < 1e-4, n
 
 
-def test_deferred_wgrad_sum_matches_per_conv_sum():
+@pytest.mark.parametrize("streamed", [True, False])
+def test_deferred_wgrad_sum_matches_per_conv_sum(streamed):
     """ops.defer_wgrad (the trainer's forward+backward): the row-window wgrad
-    partials of every conv are summed in ONE dv_wgrad_reduce_batched launch at
-    the end of the pass instead of one reduce per conv.  Same split count and
-    summation order -> bit-identical weight and bias gradients, also when a
-    gradient accumulates (a second pass, or one weight read by two convs: the
-    pending sums are flushed before the second target write)."""
+    partials of every conv are summed either on a side stream right after
+    each wgrad (streamed, the default) or in ONE dv_wgrad_reduce_batched
+    launch at the end of the pass, instead of one reduce per conv on the main
+    stream.  Same split count and summation order -> bit-identical weight and
+    bias gradients, also when a gradient accumulates (a second pass, or one
+    weight read by two convs: streamed sums stay ordered on their stream,
+    pending batched sums are flushed before the second target write)."""
     from dalle2_video import ops
 
     g = torch.Generator(device="cuda").manual_seed(11)
@@ -165,17 +168,22 @@ def test_deferred_wgrad_sum_matches_per_conv_sum():
                 outs = [ops.conv(x, w_, b_) for x, w_, b_ in zip(xs, ws, bs)]
                 outs.append(ops.conv(xs[0], ws[0], bs[0]))  # the same weight read twice
                 torch.autograd.backward(outs, dys + [dys[0]])
-                n_pending.append(len(ops.WGRAD_DEFER.pending))
+                n_pending.append(ops.WGRAD_DEFER.added)
         torch.cuda.synchronize()
         return [p.grad.clone() for p in ws + bs], n_pending
 
-    for passes in (1, 2):
-        ref, _ = run(False, passes)
-        got, n_pending = run(True, passes)
-        assert all(n >= 1 for n in n_pending), n_pending
-        assert not ops.WGRAD_DEFER.pending
-        for i, (a, b) in enumerate(zip(ref, got)):
-            assert torch.equal(a, b), (passes, i, ((a - b).norm() / a.norm()).item())
+    saved = ops.WGRAD_DEFER.STREAM
+    ops.WGRAD_DEFER.STREAM = streamed
+    try:
+        for passes in (1, 2):
+            ref, _ = run(False, passes)
+            got, n_pending = run(True, passes)
+            assert all(n >= 1 for n in n_pending), n_pending
+            assert not ops.WGRAD_DEFER.pending and ops.WGRAD_DEFER.streamed is None
+            for i, (a, b) in enumerate(zip(ref, got)):
+                assert torch.equal(a, b), (passes, i, ((a - b).norm() / a.norm()).item())
+    finally:
+        ops.WGRAD_DEFER.STREAM = saved
 
 
 def test_graph_replay_matches_eager():
