@@ -478,7 +478,8 @@ class OverlappedAllReduce:
       buckets of whole parameters; a bucket is ready at the largest index of
       its parameters.
       (Each Unet3D parameter's gradient comes from ONE backward op — no
-      weight is applied twice — so its first appearance is its completion.)
+      weight is applied twice — so its first appearance is its completion,
+      once the writes the backward defers are flushed: see _launch.)
     * Every later call: at hook k, each bucket ready by k is all-reduced (SUM)
       on a comm stream that first waits for the compute stream and the
       streamed-wgrad-sum stream; the rest go at the end of the backward.
@@ -559,10 +560,15 @@ class OverlappedAllReduce:
     def _launch(self, upto):
         buckets = self._buckets()
         G = self.opt.flat_grad
-        if (self.launched < len(buckets) and buckets[self.launched][2] <= upto
-                and ops.WGRAD_DEFER.pending):
-            # batched split-K sums pending: land them before the bucket goes out
-            ops.WGRAD_DEFER.flush()
+        if self.launched < len(buckets) and buckets[self.launched][2] <= upto:
+            # gradient writes the backward defers (batched split-K sums, the
+            # cross-attention fold backwards) land before a bucket goes out: a
+            # parameter ranks where its .grad was allocated, which is where its
+            # deferred write was queued
+            if ops.WGRAD_DEFER.pending:
+                ops.WGRAD_DEFER.flush()
+            if ops._FOLD_BWD_PENDING:
+                ops.flush_fold_bwd()
         while self.launched < len(buckets) and buckets[self.launched][2] <= upto:
             start, end, _ = buckets[self.launched]
             dev = G.device
