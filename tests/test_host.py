@@ -214,3 +214,31 @@ def test_shard_loader_keeps_custom_batch_sampler_batches():
         assert len(sh) == len(got[-1])
     assert got[0] == [batches[0], batches[2], batches[4]]
     assert got[1] == [batches[1], batches[3]]
+
+
+def test_decoder_state_dict_keys_match_the_reference_layout():
+    """VideoDecoder's checkpoint keys (what train_decoder.py:177-184 saves):
+    the reference module tree (dalle2_video.py:1169-1506) registers, per unet
+    i, `unets.i.*` (the Unet3D keys, pinned to the reference by golden G2),
+    `noise_schedulers.i.*` (NoiseScheduler's persistent buffers — restated
+    from dalle2-pytorch 1.14.2, so this part is pinned to the oracle's
+    restatement, not to the package), nothing for `vaes` (NullVQGanVAE) or
+    `lowres_conds` (LowresVideoConditioner without noising), and `_dummy` is
+    non-persistent.  Values of the schedule buffers match the oracle's."""
+    from dalle2_video import dalle2_video as D
+
+    u1 = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    u2 = D.Unet3D(8, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8, 16))
+    dec = D.VideoDecoder((u1, u2), frame_sizes=(64, 128), frame_numbers=(16, 16), timesteps=1000,
+                         learned_variance=False)
+    sd = dec.state_dict()
+    want = set()
+    for i, u in enumerate(dec.unets):
+        want |= {f"unets.{i}.{k}" for k in u.state_dict()}
+    scheds = [R.NoiseScheduler(beta_schedule=b, timesteps=1000, loss_type="l2") for b in ("cosine", "linear")]
+    for i, s in enumerate(scheds):
+        want |= {f"noise_schedulers.{i}.{k}" for k in s.state_dict()}
+    assert set(sd) == want, (sorted(set(sd) - want)[:5], sorted(want - set(sd))[:5])
+    for i, s in enumerate(scheds):
+        for k, v in s.state_dict().items():
+            assert torch.allclose(sd[f"noise_schedulers.{i}.{k}"], v, rtol=1e-6, atol=0), (i, k)
