@@ -1962,7 +1962,7 @@ __device__ __forceinline__ int fw_pix(int r) {
   else return (ga ? 0 : 16) + a;
 }
 
-template <int W, bool STATS = false>
+template <int W, bool STATS = false, int PF = 2, int DEFER = 0>
 __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
   using G = FwGeom<W>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
@@ -2055,31 +2055,44 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   f32x16 acc0, acc1, acc2, acc3;
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc0[e] = acc1[e] = acc2[e] = acc3[e] = 0.f;
+  // DEFER: the last tap's MFMAs of chunk c run after the chunk's barrier, while
+  // chunk c+1's first fragment reads are in flight (its operands are in
+  // registers before the barrier, so the buffer may be refilled under them)
+  u32x4 lb, la0, la1;
   for (int c = 0; c < nch; ++c) {
     const char* b = smem + (c % NBUF) * BUF;
-    // fragments of tap d + 2 are read while tap d multiplies (one wave per
-    // SIMD: the LDS latency is hidden by this wave's own MFMAs)
-    u32x4 bq[3], aq0[3], aq1[3];
+    // fragments of tap d + PF are read while tap d multiplies (one wave per
+    // SIMD: the LDS latency is hidden by this wave's own MFMAs only)
+    constexpr int NS = PF + 1;
+    u32x4 bq[NS], aq0[NS], aq1[NS];
     auto rd = [&](int d, int s) {
       const int T = ((d / 3) * WQ + (d % 3)) * 48;
       bq[s] = *(const u32x4*)(b + bofs + T);
       aq0[s] = *(const u32x4*)(b + aofs + d * 32);
       aq1[s] = *(const u32x4*)(b + aofs + 32 * F8_WROW * 16 + d * 32);
     };
-    rd(0, 0);
-    rd(1, 1);
+#pragma unroll
+    for (int d = 0; d < PF; ++d) rd(d, d);
+    if (DEFER && c > 0) {  // tap 8 of chunk c-1 (even tap: chains 0 / 1)
+      acc0 = Mma<bf16>::run(la0, lb, acc0);
+      acc1 = Mma<bf16>::run(la1, lb, acc1);
+    }
     // chunk c+AHEAD's pieces go out one per tap, in the MFMA shadow: its
     // buffer was last read in chunk c-1, before the last barrier
     const bool pre = c + AHEAD < nch;
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
-      if (d + 2 < 9) rd(d + 2, (d + 2) % 3);
-      if (d & 1) {
-        acc2 = Mma<bf16>::run(aq0[d % 3], bq[d % 3], acc2);
-        acc3 = Mma<bf16>::run(aq1[d % 3], bq[d % 3], acc3);
+      if (d + PF < 9) rd(d + PF, (d + PF) % NS);
+      if (DEFER && d == 8) {
+        lb = bq[d % NS];
+        la0 = aq0[d % NS];
+        la1 = aq1[d % NS];
+      } else if (d & 1) {
+        acc2 = Mma<bf16>::run(aq0[d % NS], bq[d % NS], acc2);
+        acc3 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc3);
       } else {
-        acc0 = Mma<bf16>::run(aq0[d % 3], bq[d % 3], acc0);
-        acc1 = Mma<bf16>::run(aq1[d % 3], bq[d % 3], acc1);
+        acc0 = Mma<bf16>::run(aq0[d % NS], bq[d % NS], acc0);
+        acc1 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc1);
       }
       if (d < NPW && pre) issue1(c + AHEAD, d);
       __builtin_amdgcn_sched_barrier(0);
@@ -2090,7 +2103,12 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     else if (young == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
     else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0), "+v"(la1)::"memory");
     __builtin_amdgcn_s_barrier();
+  }
+  if (DEFER && nch > 0) {
+    acc0 = Mma<bf16>::run(la0, lb, acc0);
+    acc1 = Mma<bf16>::run(la1, lb, acc1);
   }
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e.  Bias and
   // residual are loaded for all 8 channel groups BEFORE the first store (vmcnt
@@ -2186,14 +2204,22 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   ConvFwdArgs<bf16> a = a0;
   a.xcd_c = frame_xcd_split(a);
   const int nblk = (int)(a.M / 128) * (a.cout / 64);
+  // A/B: DV_FRAME_PF = fragment prefetch distance in taps (2, 3 or 4)
+  // and DV_FRAME_DEFER = 1: the last tap's MFMAs after the chunk barrier
+  static const int pf = getenv("DV_FRAME_PF") ? atoi(getenv("DV_FRAME_PF")) : 2;
+  static const int df = getenv("DV_FRAME_DEFER") ? atoi(getenv("DV_FRAME_DEFER")) : 0;
   switch (a.W) {
-#define DV_FW(WW) (a.gn_sums ? conv_fwd_frame_kernel<WW, true><<<nblk, 256, 0, st>>>(a) \
-                          : conv_fwd_frame_kernel<WW, false><<<nblk, 256, 0, st>>>(a))
+#define DV_FW3(WW, P, D) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, P, D><<<nblk, 256, 0, st>>>(a) \
+                                : conv_fwd_frame_kernel<WW, false, P, D><<<nblk, 256, 0, st>>>(a))
+#define DV_FW2(WW, P) (df ? DV_FW3(WW, P, 1) : DV_FW3(WW, P, 0))
+#define DV_FW(WW) (pf == 3 ? DV_FW2(WW, 3) : DV_FW2(WW, 2))
     case 8: DV_FW(8); break;
     case 16: DV_FW(16); break;
     case 32: DV_FW(32); break;
     default: DV_FW(64); break;
 #undef DV_FW
+#undef DV_FW2
+#undef DV_FW3
   }
   return check_launch("conv_fwd_frame");
 }

@@ -374,6 +374,228 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_mx8_kernel(Mx8Args p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent form for the wide frames (W = 64 / 128) with one or two input
+// chunks (cin <= 128: the 64² / 128² stage convs of config 5), where the
+// per-tile kernel above re-fetched the whole weight image for one chunk of
+// work and exposed the operand DMA latency of every tile.  The block's
+// weight image (NCH chunks) stays resident in LDS for the workgroup's life;
+// the workgroup walks a contiguous range of 128-pixel tiles of ONE
+// output-channel block (consecutive tiles share two of their three window
+// rows in this XCD's L2) as a sequence of (tile, chunk) steps whose pixel
+// windows stream through a 3-deep LDS ring: the window of step s + 2 is in
+// flight while step s multiplies, and the finished tile's stores go out at
+// the start of the next tile.  No residual (the Block3D convs take none).
+// ---------------------------------------------------------------------------
+template <int W>
+struct MxPGeom {
+  using G = MxGeom<W, 128>;
+  static constexpr int WBUF = G::NDP * 1024 + G::NSP * 256;  // one step's window (data + scales)
+  static constexpr int NWB = 3;
+};
+
+template <int W, int NCH>
+constexpr int mxp_lds() { return NCH * MX_WIMG + MxPGeom<W>::NWB * MxPGeom<W>::WBUF; }
+
+template <int W, int NCH>
+__global__ __launch_bounds__(256) void conv_fwd_mx8p_kernel(Mx8Args p, int tiles_per_wg, int wg_per_cb) {
+  constexpr int NW = 4, TP = 128;
+  using G = MxGeom<W, TP>;
+  using PG = MxPGeom<W>;
+  constexpr int WQ = G::WQ, WBUF = PG::WBUF, NWB = PG::NWB, RES = NCH * MX_WIMG;
+  static_assert(W >= 16 && TP % W == 0, "whole-row tiles");
+  __shared__ __attribute__((aligned(1024))) char smem[mxp_lds<W, NCH>()];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cb = blockIdx.x / wg_per_cb, g = blockIdx.x % wg_per_cb;
+  const int co0 = cb * 64;
+  const int npx = (int)(p.M / TP);
+  const int t0 = g * tiles_per_wg, t1 = min(npx, t0 + tiles_per_wg);
+  if (t0 >= t1) return;  // (uniform per workgroup)
+  const int nsteps = (t1 - t0) * NCH;
+  const int nch0 = p.c0 / 64;
+  const int HW = p.H * W;
+
+  // resident weights: the block's NCH chunk images, one DMA pass
+  const __amdgpu_buffer_rsrc_t wr = dma_rsrc(p.w + (long long)cb * NCH * MX_WIMG, (unsigned)(NCH * MX_WIMG));
+#pragma unroll
+  for (int k = wave; k < NCH * MX_WPIECES; k += NW) dma16s(wr, smem + k * 1024, (unsigned)(k * 1024 + lane * 16), 0u);
+
+  // per-lane window geometry (tile-relative): data pieces, then scale pieces
+  constexpr int NXP = (G::NDP + NW - 1) / NW, NSPW = (G::NSP + NW - 1) / NW;
+  int xoff[NXP], xwy[NXP], xt[NXP], soff[NSPW], swy[NSPW];
+#pragma unroll
+  for (int i = 0; i < NXP; ++i) {
+    const int slot = min(wave + NW * i, G::NDP - 1) * 64 + lane, wp = slot >> 2;
+    const int wy = wp / WQ, wx = wp - wy * WQ;
+    const bool ok = wp < G::WPIX && wx >= 1 && wx <= W;
+    xt[i] = ((slot & 3) ^ ((wp >> 2) & 3)) * 16;
+    xoff[i] = (wy - 1) * W + (wx - 1);
+    xwy[i] = ok ? wy : -(1 << 20);
+  }
+#pragma unroll
+  for (int i = 0; i < NSPW; ++i) {
+    const int wp = min(wave + NW * i, G::NSP - 1) * 64 + lane;
+    const int wy = wp / WQ, wx = wp - wy * WQ;
+    const bool ok = wp < G::WPIX && wx >= 1 && wx <= W;
+    soff[i] = (wy - 1) * W + (wx - 1);
+    swy[i] = ok ? wy : -(1 << 20);
+  }
+  const __amdgpu_buffer_rsrc_t qr0 = dma_rsrc(p.q0, (unsigned)(p.M * p.c0));
+  const __amdgpu_buffer_rsrc_t sr0 = dma_rsrc(p.s0, (unsigned)(p.M * 4 * nch0));
+  const __amdgpu_buffer_rsrc_t qr1 = dma_rsrc(p.q1, (unsigned)(p.M * p.c1));
+  const __amdgpu_buffer_rsrc_t sr1 = dma_rsrc(p.s1, (unsigned)(p.M * 4 * (NCH - nch0)));
+  // the window of step s into ring slot s % NWB (piece j of this wave)
+  auto issue1 = [&](int st, int j) {
+    const int tile = t0 + st / NCH, c = st % NCH;
+    const long long m0 = (long long)tile * TP;
+    const int y0 = (int)((m0 % HW) / W);
+    char* b = smem + RES + (st % NWB) * WBUF;
+    const bool first = c < nch0;
+    const int cc = first ? c : c - nch0;
+    if (j < NXP) {
+      const int k = min(wave + NW * j, G::NDP - 1);
+      const int yy = y0 + xwy[j] - 1;
+      const bool ok = (unsigned)yy < (unsigned)p.H;
+      const long long pix = m0 + xoff[j];
+      const unsigned vo = ok ? (unsigned)(pix * (first ? p.c0 : p.c1) + xt[j]) : DMA_OOB;
+      if (first) dma16s(qr0, b + k * 1024, vo, (unsigned)(cc * 64));
+      else dma16s(qr1, b + k * 1024, vo, (unsigned)(cc * 64));
+    } else {
+      const int jj = j - NXP, k = min(wave + NW * jj, G::NSP - 1);
+      const int yy = y0 + swy[jj] - 1;
+      const bool ok = (unsigned)yy < (unsigned)p.H;
+      const unsigned vo = ok ? (unsigned)((m0 + soff[jj]) * 4) : DMA_OOB;
+      const unsigned so = (unsigned)((long long)cc * p.M * 4);
+      char* dst = b + G::NDP * 1024 + k * 256;
+      if (first) dma4s(sr0, dst, vo, so);
+      else dma4s(sr1, dst, vo, so);
+    }
+  };
+  constexpr int NPWX = NXP + NSPW;
+  // prologue: steps 0 and 1 in flight with the weights; wait for everything
+#pragma unroll
+  for (int st = 0; st < NWB - 1; ++st)
+    if (st < nsteps) {
+#pragma unroll
+      for (int j = 0; j < NPWX; ++j) issue1(st, j);
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  const int r = lane & 31, h = lane >> 5;
+  const int tpx = wave * 32 + mx_pix<W>(r);
+  const int wb = (tpx / W) * WQ + tpx % W;
+  const int xr = (r >> 2) & 3;
+  const int aoff0 = r * MX_WROW + ((h ^ xr) << 4), aoff1 = r * MX_WROW + (((2 + h) ^ xr) << 4);
+  unsigned as[NCH][2][3];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const unsigned* sp = (const unsigned*)(smem + c * MX_WIMG + MX_WDATA + (32 * j + r) * 32 + 16 * h);
+      as[c][j][0] = sp[0];
+      as[c][j][1] = sp[1];
+      as[c][j][2] = sp[2];
+    }
+  f32x4 bb[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg)
+      bb[j][gg] = p.bias ? *(const f32x4*)(p.bias + co0 + 32 * j + 8 * gg + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][0][e] = acc[j][1][e] = 0.f;
+  auto epilogue = [&](int tile) {
+    const long long m = (long long)tile * TP + tpx;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[j][0][4 * gg + e] + acc[j][1][4 * gg + e] + bb[j][gg][e];
+        *(bf16x4*)(p.y + m * p.ldy + co0 + 32 * j + 8 * gg + 4 * h) =
+            bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][0][e] = acc[j][1][e] = 0.f;
+  };
+
+  for (int st = 0; st < nsteps; ++st) {
+    const int c = st % NCH;
+    const bool tile_start = c == 0 && st > 0;
+    if (tile_start) epilogue(t0 + st / NCH - 1);  // 8 stores, before this step's DMA
+    const char* wimg = smem + c * MX_WIMG;
+    const char* win = smem + RES + (st % NWB) * WBUF;
+    u32x4 bq[3][2], aq[3][2][2];
+    unsigned bs[3];
+    auto rd = [&](int d, int sl) {
+      const int pw = wb + (d / 3) * WQ + (d % 3);
+      const int xp = (pw >> 2) & 3;
+      const char* pb = win + pw * 64;
+      bq[sl][0] = *(const u32x4*)(pb + ((h ^ xp) << 4));
+      bq[sl][1] = *(const u32x4*)(pb + (((2 + h) ^ xp) << 4));
+      bs[sl] = *(const uint8_t*)(win + G::NDP * 1024 + pw * 4 + h);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        aq[sl][j][0] = *(const u32x4*)(wimg + 32 * j * MX_WROW + aoff0 + d * 64);
+        aq[sl][j][1] = *(const u32x4*)(wimg + 32 * j * MX_WROW + aoff1 + d * 64);
+      }
+    };
+    rd(0, 0);
+    rd(1, 1);
+    const bool pre = st + NWB - 1 < nsteps;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      if (d + 2 < 9) rd(d + 2, (d + 2) % 3);
+      const int sl = d % 3;
+      const v8i bf = cat8(bq[sl][0], bq[sl][1]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const v8i af = cat8(aq[sl][j][0], aq[sl][j][1]);
+        const int sa = (int)((as[c][j][d / 4] >> (8 * (d % 4))) & 255u);
+        acc[j][d & 1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af, bf, acc[j][d & 1], 0, 0, 0, sa, 0,
+                                                                       (int)bs[sl]);
+      }
+      if (pre) {
+#pragma unroll
+        for (int j = d; j < NPWX; j += 9) issue1(st + NWB - 1, j);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // step st + 1's window landed: younger than its DMA are this step's
+    // stores (8 when it began a tile) and this step's DMA for st + 2
+    if (tile_start) {
+      if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + NPWX) : "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPWX) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  epilogue(t1 - 1);
+}
+
+template <int W, int NCH>
+int launch_mx8p(const Mx8Args& a, hipStream_t st) {
+  const int ncb = a.cout / 64, npx = (int)(a.M / 128);
+  int g = 256 / ncb;  // one workgroup per CU (the LDS holds one)
+  if (g < 1) g = 1;
+  if (g > npx) g = npx;
+  const int per = (npx + g - 1) / g;
+  g = (npx + per - 1) / per;
+  conv_fwd_mx8p_kernel<W, NCH><<<ncb * g, 256, 0, st>>>(a, per, g);
+  return check_launch("conv_fwd_mx8p");
+}
+
 template <int W>
 int launch_mx8(const Mx8Args& a, hipStream_t st) {
   constexpr int NW = MX_NW;
@@ -436,6 +658,12 @@ extern "C" int dv_conv_fwd_mx8(const void* q0, const void* s0, int c0, const voi
   a.c0 = c0; a.c1 = c1; a.w = (const uint8_t*)wimg; a.bias = bias; a.res = (const bf16*)res; a.ldres = ldres;
   a.y = (bf16*)y; a.ldy = ldy; a.H = h; a.cin = cin; a.cout = cout; a.M = M;
   hipStream_t st = (hipStream_t)stream;
+  // the persistent resident-weight form for the wide frames with <= 2 chunks
+  static const bool no_p = getenv("DV_MX8_NO_PERSIST") != nullptr;  // A/B switch
+  if (!no_p && !res && (w == 64 || w == 128) && cin <= 128) {
+    if (w == 128) return cin == 64 ? launch_mx8p<128, 1>(a, st) : launch_mx8p<128, 2>(a, st);
+    return cin == 64 ? launch_mx8p<64, 1>(a, st) : launch_mx8p<64, 2>(a, st);
+  }
   switch (w) {
     case 8: return launch_mx8<8>(a, st);
     case 16: return launch_mx8<16>(a, st);

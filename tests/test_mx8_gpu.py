@@ -81,6 +81,11 @@ SHAPES = [  # nf, h, w, c0, c1, cout, with residual
     (1, 3, 128, 64, 0, 64, True),
     (1, 2, 128, 128, 64, 64, False),
     (1, 16, 16, 512, 256, 512, True),
+    # persistent resident-weight form (W 64 / 128, <= 2 chunks, no residual):
+    # several tiles per workgroup, two output-channel blocks, dual source
+    (8, 64, 128, 64, 0, 64, False),
+    (16, 64, 64, 64, 64, 128, False),
+    (2, 16, 64, 128, 0, 64, False),
 ]
 
 
