@@ -910,7 +910,7 @@ class _DenoiseStepGraph:
         if self.graph is None:
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self._body()
                 ops.gn_graph_boundary(self.x.device)
         self.graph.replay()

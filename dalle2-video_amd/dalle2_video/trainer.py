@@ -783,7 +783,10 @@ class VideoDecoderTrainer(nn.Module):
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             overlapped = False
-            with torch.cuda.graph(g):
+            # thread-local capture: the process group's watchdog thread polls
+            # the events of earlier (eager) collectives while this thread
+            # captures, which the default global mode turns into an error
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 ctx = (torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False)
                        if self.amp else nullcontext())
                 if ov is not None:
