@@ -2367,11 +2367,11 @@ struct WgradSArgs {
   const bf16* x0;
   const bf16* x1;
   int ld0, ld1, c0;
-  float* part;    // [S][cout][cin][9] partials (S > 1)
-  float* dbpart;  // [S][cout] or null
+  float* part;    // [S][cout][cin][9] partials (S > 1): f32, or bf16 when part_bf16
+  float* dbpart;  // [S][cout] or null (f32)
   float* dw;      // (cout, cin, 1, 3, 3) gradient (S == 1)
   float* db;      // [cout] or null
-  int acc_w, acc_b;
+  int acc_w, acc_b, part_bf16;
   int H, cin, cout, K;
   int nstages, stages_per_split;
   int seg, nseg;  // image rows per window segment, segments per stage
@@ -2563,7 +2563,9 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   // One split writes the gradient itself (accumulate honoured); several
   // splits write partials that wgrad_reduce4_kernel sums. ----
   const bool direct = gridDim.z == 1;
-  float* dst = direct ? a.dw : a.part + (long long)blockIdx.z * a.cout * a.K;
+  const bool pbf = !direct && a.part_bf16;  // bf16 partials: half the split-K bytes
+  float* dst = direct ? a.dw : a.part + (pbf ? 0 : (long long)blockIdx.z * a.cout * a.K);
+  bf16* dstb = (bf16*)a.part + (long long)blockIdx.z * a.cout * a.K;
   const int acc_o = direct && a.acc_w;
   const int r = lane & 31, h = lane >> 5;
   constexpr int TP = 32 * NT;  // floats per output channel in a tile
@@ -2587,7 +2589,13 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
       const int col = rem / (TP / 4), j = rem - col * (TP / 4);
       f32x4 v = *(const f32x4*)(red + t2 * (32 * TP) + col * TP + 4 * j);
       const long long rowbase = (long long)(co0 + rnd * 32) * a.K + (ci0 + t2 * 32) * NT;
-      f32x4* o = (f32x4*)(dst + rowbase + (long long)col * a.K + 4 * j);
+      const long long oi = rowbase + (long long)col * a.K + 4 * j;
+      if (pbf) {
+        const float t4[4] = {v[0], v[1], v[2], v[3]};
+        store4<bf16>(dstb + oi, t4);
+        continue;
+      }
+      f32x4* o = (f32x4*)(dst + oi);
       if (acc_o) v += *o;
       *o = v;
     }
@@ -2606,29 +2614,36 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
 // LDS, so even a 256-split sum of a small gradient spreads over hundreds of
 // workgroups.  The bias partials ([S][cout], cout % 4 == 0) are reduced the
 // same way by the workgroups after the weight ones.
+__device__ __forceinline__ f32x4 part4(const void* p, bool pbf, long long i) {
+  if (!pbf) return ((const f32x4*)p)[i];
+  const bf16x4 t = __builtin_bit_cast(bf16x4, ((const u32x2*)p)[i]);
+  return f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
+}
+
 __device__ __forceinline__ void reduce4_block(f32x4* sh, long long blk, const float* part, int S,
                                               int G, long long n4, float* dw, int acc_w,
-                                              const float* dbpart, float* db, int cout, int acc_b) {
+                                              const float* dbpart, float* db, int cout, int acc_b,
+                                              int part_bf16) {
   const int cols = 256 / G;
   const long long wblocks = (n4 + cols - 1) / cols;
   const bool bias = blk >= wblocks;
   const long long n = bias ? cout / 4 : n4;
-  const f32x4* src = (const f32x4*)(bias ? dbpart : part);
+  const void* src = bias ? (const void*)dbpart : (const void*)part;
+  const bool pbf = part_bf16 && !bias;  // the bias partials stay f32
   float* dst = bias ? db : dw;
   const int acc = bias ? acc_b : acc_w;
   const int c = threadIdx.x % cols, grp = threadIdx.x / cols;
   const long long i = (bias ? blk - wblocks : blk) * (long long)cols + c;
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (i < n) {
-    const f32x4* p = src + i;
     int s = grp;
     for (; s + 7 * G < S; s += 8 * G) {
       f32x4 t[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = p[(long long)(s + u * G) * n];
+      for (int u = 0; u < 8; ++u) t[u] = part4(src, pbf, (long long)(s + u * G) * n + i);
       v += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
     }
-    for (; s < S; s += G) v += p[(long long)s * n];
+    for (; s < S; s += G) v += part4(src, pbf, (long long)s * n + i);
   }
   sh[threadIdx.x] = v;
   __syncthreads();
@@ -2647,9 +2662,9 @@ inline long long reduce4_blocks(long long n4, int G, int cout, bool bias) {
 __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* part, int S, int G,
                                                             long long n4, float* dw, int acc_w,
                                                             const float* dbpart, float* db,
-                                                            int cout, int acc_b) {
+                                                            int cout, int acc_b, int part_bf16) {
   __shared__ f32x4 sh[256];
-  reduce4_block(sh, blockIdx.x, part, S, G, n4, dw, acc_w, dbpart, db, cout, acc_b);
+  reduce4_block(sh, blockIdx.x, part, S, G, n4, dw, acc_w, dbpart, db, cout, acc_b, part_bf16);
 }
 
 // every pending split-K sum of a backward pass in one launch: block b belongs
@@ -2666,7 +2681,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_batched_kernel(const DvWgrad
   }
   const DvWgradReduceEntry e = table[lo];
   reduce4_block(sh, b - e.blk0, e.part, e.S, e.G, e.n4, e.dw, e.acc_w, e.dbpart, e.db, e.cout,
-                e.acc_b);
+                e.acc_b, e.part_bf16);
 }
 
 inline int reduce4_groups(int S) {
@@ -2769,11 +2784,19 @@ inline void stripe_split(int nstages, int grid_xy, long long grad_floats, int& s
   S = (nstages + sps - 1) / sps;
 }
 
+// split-K partials in bf16 (halves their write and the sum's read; the sum
+// and the gradient stay f32).  DV_WG_F32PART=1 keeps f32 partials (A/B).
+inline bool stripe_part_bf16() {
+  static const bool f32 = getenv("DV_WG_F32PART") && atoi(getenv("DV_WG_F32PART"));
+  return !f32;
+}
+
 long long wgrad_stripe_ws(int nf, int h, int w, int cin, int cout, int ks) {
   const int nstages = (int)((long long)nf * h * w / 128);
   int sps, S;
   stripe_split(nstages, (cout / 64) * (cin / 64), (long long)cout * ks * ks * cin, sps, S);
-  return (long long)S * cout * ((long long)ks * ks * cin + 1);
+  const long long wpart = (long long)S * cout * ks * ks * cin;  // cout % 64 == 0: even
+  return (stripe_part_bf16() ? wpart / 2 : wpart) + (long long)S * cout;
 }
 
 int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0, const void* x1,
@@ -2790,7 +2813,8 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   int S;
   stripe_split(a.nstages, (cout / 64) * (cin / 64), (long long)cout * a.K, a.stages_per_split, S);
   a.part = ws;
-  a.dbpart = db ? ws + (long long)S * cout * a.K : nullptr;
+  a.part_bf16 = S > 1 && stripe_part_bf16();
+  a.dbpart = db ? ws + (long long)S * cout * a.K / (a.part_bf16 ? 2 : 1) : nullptr;
   a.dw = dw; a.db = db; a.acc_w = acc_w; a.acc_b = acc_b;
   dim3 grid(cout / 64, cin / 64, S);
   if (ks == 1) {
@@ -2807,10 +2831,10 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
     const long long n4 = (long long)cout * a.K / 4;
     const int G = reduce4_groups(S);
     if (defer) {  // the caller sums the partials later (dv_wgrad_reduce_batched)
-      *defer = DvWgradReduceEntry{ws, a.dbpart, dw, db, n4, 0, S, G, cout, acc_w, acc_b, 0};
+      *defer = DvWgradReduceEntry{ws, a.dbpart, dw, db, n4, 0, S, G, cout, acc_w, acc_b, a.part_bf16};
     } else {
       wgrad_reduce4_kernel<<<(unsigned)reduce4_blocks(n4, G, cout, db != nullptr), 256, 0, st>>>(
-          ws, S, G, n4, dw, acc_w, a.dbpart, db, cout, acc_b);
+          ws, S, G, n4, dw, acc_w, a.dbpart, db, cout, acc_b, a.part_bf16);
     }
   }
   return check_launch("conv_wgrad_stripe");
@@ -2961,7 +2985,7 @@ extern "C" int dv_wgrad_reduce_one(const DvWgradReduceEntry* e, void* stream) {
   const int G = reduce4_groups(e->S);
   wgrad_reduce4_kernel<<<(unsigned)reduce4_blocks(e->n4, G, e->cout, e->db != nullptr), 256, 0,
                          (hipStream_t)stream>>>(e->part, e->S, G, e->n4, e->dw, e->acc_w, e->dbpart, e->db,
-                                                e->cout, e->acc_b);
+                                                e->cout, e->acc_b, e->part_bf16);
   return check_launch("wgrad_reduce_one");
 }
 

@@ -92,7 +92,7 @@ _SIGS = {
 class DvWgradReduceEntry(ctypes.Structure):
     """Mirror of DvWgradReduceEntry (include/dv_hip.h)."""
     _fields_ = [("part", _P), ("dbpart", _P), ("dw", _P), ("db", _P), ("n4", _L), ("blk0", _L),
-                ("S", _I), ("G", _I), ("cout", _I), ("acc_w", _I), ("acc_b", _I), ("pad_", _I)]
+                ("S", _I), ("G", _I), ("cout", _I), ("acc_w", _I), ("acc_b", _I), ("part_bf16", _I)]
 
 
 class DVError(RuntimeError):

@@ -85,13 +85,14 @@ int dv_conv_wgrad(int dtype, const void* dy, int lddy, const void* x0, int ld0, 
  * a dw or db target.  The trainer defers every conv of one backward pass and
  * sums them once at its end (replaces a reduce launch per conv).          */
 typedef struct {
-  const float* part;    /* [S][cout * K] partials                      */
+  const float* part;    /* [S][cout * K] partials (f32, or bf16 below) */
   const float* dbpart;  /* [S][cout] bias partials or NULL             */
   float* dw;            /* (cout, cin, 1, k, k) target                 */
   float* db;            /* [cout] target or NULL                       */
   long long n4;         /* cout * K / 4                                */
   long long blk0;       /* first block of this entry (plan)            */
-  int S, G, cout, acc_w, acc_b, pad_;
+  int S, G, cout, acc_w, acc_b;
+  int part_bf16;        /* 1: part holds bf16 values (bias partials f32) */
 } DvWgradReduceEntry;
 int dv_conv_wgrad_deferred(int dtype, const void* dy, int lddy, const void* x0, int ld0, int c0,
                            const void* x1, int ld1, float* dw, int accumulate_w, float* db,

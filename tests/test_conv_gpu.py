@@ -107,3 +107,36 @@ def test_linear_weight_as_1x1_conv(dtype, tol):
     (y.float() * gy.cuda()).sum().backward()
     assert rel(xd.grad.float(), xr.grad) < tol * 2
     assert rel(wd.grad, wr.grad) < tol * 2
+
+
+@pytest.mark.parametrize("case", [(32, 64, 64, 64, 0, 64, 3), (16, 32, 32, 128, 0, 128, 3),
+                                  (64, 8, 8, 512, 0, 512, 3), (64, 64, 64, 64, 64, 64, 1)])
+def test_stripe_wgrad_bf16_partials(case, parity_log):
+    """The row-window wgrad's split-K partials are stored in bf16 and summed
+    in f32 (half the partial bytes).  Rounding each of S partials is an error
+    of the order of ONE bf16 rounding of the gradient (random-sign partials:
+    rms 2^-8/sqrt(12) relative, whatever S) -- the rounding the reference's
+    autocast gradient itself carries (its conv weight gradient is a bf16
+    tensor cast to f32).  Checked against fp64 on the same bf16 x and dY."""
+    from dalle2_video import ops
+
+    nf, h, w, c0, c1, cout, k = case
+    g = torch.Generator().manual_seed(7)
+    cin = c0 + c1
+    x = torch.randn(nf, h, w, cin, generator=g).bfloat16()
+    wt = torch.randn(cout, cin, 1, k, k, generator=g) / (cin * k * k) ** 0.5
+    gy = torch.randn(nf, h, w, cout, generator=g).bfloat16()
+    xr = x.double()
+    wr = wt.bfloat16().double().requires_grad_()
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr[:, :, 0], padding=k // 2).permute(0, 2, 3, 1)
+    (yr * gy.double()).sum().backward()
+    xd = x.cuda()
+    x0 = xd[..., :c0].contiguous() if c1 else xd
+    x1 = xd[..., c0:].contiguous() if c1 else None
+    wd = wt.cuda().requires_grad_()
+    y = ops.conv(x0, wd, None, x1=x1)
+    y.backward(gy.cuda())
+    err = rel(wd.grad, wr.grad)
+    parity_log(config=f"stripe wgrad bf16 partials {case}", dw_rel=err)
+    # one bf16 rounding is 2^-9 relative at most, 1.1e-3 rms
+    assert err < 2.5e-3, err
