@@ -143,4 +143,16 @@ template <> struct Vec<bf16> {
   }
 };
 
+// ---- OCP MX-fp8 (e4m3 elements, one e8m0 scale per 32 channels): shared by
+// the quantiser (dv_mx8.hip) and the GroupNorm apply's fused quantiser ----
+// scale exponent E of a block with max |v| = amax: every v * 2^-E lies in the
+// e4m3 range (<= 448) and the largest uses its top binade where it fits
+__device__ __forceinline__ int mx_exp(float amax) {
+  const unsigned b = __float_as_uint(amax);
+  const int eb = (int)((b >> 23) & 255);
+  const int E = eb - 135 + ((b & 0x7fffffu) > 0x600000u ? 1 : 0);
+  return E < -127 ? -127 : E;
+}
+__device__ __forceinline__ float mx_inv(int E) { return __uint_as_float((unsigned)(127 - E) << 23); }
+
 }  // namespace dv

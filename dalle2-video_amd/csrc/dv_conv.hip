@@ -1930,7 +1930,11 @@ int launch_fwd_stripe2(const ConvFwdArgs<bf16>& a, int seg, int nseg, hipStream_
 // 128 / W rows of one frame when H*W % 128 == 0): window rows NWR of WQ pixel
 // slots (W + 2 used; W = 8 pads to 12 so the residues work out, see above),
 // three 16-B slots per pixel.
-template <int W>
+constexpr int F8_WROW = 19;                                // 16-B slots per weight row
+// CO output channels per tile: 64 (two 32x32 accumulators per wave), or 32
+// for the grids that would leave CUs idle (M = 4,096 at 256 channels: 128
+// tiles of 64 channels for 256 CUs)
+template <int W, int CO = 64>
 struct FwGeom {
   static constexpr int NF = W == 8 ? 2 : 1;                  // frames per tile
   static constexpr int NWR = W == 8 ? 10 : 128 / W + 2;      // window rows per frame
@@ -1938,13 +1942,12 @@ struct FwGeom {
   static constexpr int FPIX = NWR * WQ;                      // window pixels per frame
   static constexpr int WPIX = NF * FPIX;
   static constexpr int XPIECES = (WPIX * 3 + 63) / 64;
-  static constexpr int PIECES = 19 + XPIECES;                // + 64 weight rows x 19 slots
+  static constexpr int WPC = (CO * F8_WROW + 63) / 64;       // CO weight rows x 19 slots
+  static constexpr int PIECES = WPC + XPIECES;
   static constexpr int NPW = (PIECES + 3) / 4;
   static constexpr int BUF = PIECES * 1024;
   static constexpr int NBUF = 5 * BUF <= 160 * 1024 - 1024 ? 5 : 4;
 };
-constexpr int F8_WROW = 19;                                // 16-B slots per weight row
-constexpr int F8_WPIECES = F8_WROW;                        // 64 rows x 19 slots = 19 KiB
 
 // lane r -> pixel (row * W + col) of the wave's 32-pixel tile so that the
 // ds_read_b128 16-lane group {0-3, 12-15, 20-27} and its complement each take
@@ -1962,14 +1965,15 @@ __device__ __forceinline__ int fw_pix(int r) {
   else return (ga ? 0 : 16) + a;
 }
 
-template <int W, bool STATS = false, int PF = 2, int DEFER = 0>
+template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64>
 __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
-  using G = FwGeom<W>;
+  using G = FwGeom<W, CO>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
+  constexpr int WPC = G::WPC, NJ = CO / 32;
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int npx = (int)(p.M / 128), nblk = npx * (p.cout / 64);
+  const int npx = (int)(p.M / 128), nblk = npx * (p.cout / CO);
   int L = blockIdx.x;
   int co0;
   long long m0;
@@ -1977,12 +1981,12 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     // XCD x = block % 8 takes channel group x / xp and pixel group x % xp: its
     // L2 holds 1/xc of the weights and 1/xp of the input (host-checked splits)
     const int xc = p.xcd_c, xp = 8 / xc, x = L % 8, j = L / 8;
-    const int tpc = (p.cout / 64) / xc, ppg = npx / xp;
-    co0 = ((x / xp) * tpc + j / ppg) * 64;
+    const int tpc = (p.cout / CO) / xc, ppg = npx / xp;
+    co0 = ((x / xp) * tpc + j / ppg) * CO;
     m0 = (long long)((x % xp) * ppg + j % ppg) * 128;
   } else {
     if (nblk % 8 == 0) L = (L % 8) * (nblk / 8) + L / 8;  // consecutive blocks share an XCD
-    co0 = (L / npx) * 64;
+    co0 = (L / npx) * CO;
     m0 = (long long)(L % npx) * 128;
   }
   const int nch = p.cin / 16;
@@ -1997,12 +2001,12 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   for (int i = 0; i < NPW; ++i) {
     const int k = min(wave + 4 * i, PIECES - 1);
     voff0[i] = voff1[i] = DMA_OOB;
-    if (k < F8_WPIECES) {
+    if (k < WPC) {
       // chunk-major packed row (mode 2/3): [cin / 16][9 taps][16]; slot c = 2 tap + half
       const int slot = k * 64 + lane, row = slot / F8_WROW, c = slot - row * F8_WROW;
-      if (c < 18) voff0[i] = (unsigned)((((long long)co0 + row) * p.K + c * 8) * 2);
+      if (c < 18 && row < CO) voff0[i] = (unsigned)((((long long)co0 + row) * p.K + c * 8) * 2);
     } else {
-      const int slot = (k - F8_WPIECES) * 64 + lane, px = slot / 3, s = slot - px * 3;
+      const int slot = (k - WPC) * 64 + lane, px = slot / 3, s = slot - px * 3;
       const int f = px / G::FPIX, rem = px - f * G::FPIX, wy = rem / WQ, wx = rem - wy * WQ;
       const int y = y0 + wy - 1;  // image row (W = 8: within frame f of the tile)
       if (px < G::WPIX && s < 2 && wx >= 1 && wx <= W && y >= 0 && y < p.H &&
@@ -2022,7 +2026,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     const bool first = ci0 < p.c0;
     char* b = smem + (c % NBUF) * BUF;
     const int k = min(wave + 4 * i, PIECES - 1);
-    if (k < F8_WPIECES) dma16s(wr, b + k * 1024, voff0[i], (unsigned)ci0 * 18);
+    if (k < WPC) dma16s(wr, b + k * 1024, voff0[i], (unsigned)ci0 * 18);
     else if (first) dma16s(xr0, b + k * 1024, voff0[i], (unsigned)ci0 * 2);
     else dma16s(xr1, b + k * 1024, voff1[i], (unsigned)(ci0 - p.c0) * 2);
   };
@@ -2048,7 +2052,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   const int tpx = wave * 32 + pix;                 // within the 128-pixel tile
   const int wb = W == 8 ? (tpx >> 6) * G::FPIX + ((tpx & 63) >> 3) * WQ + (tpx & 7)
                         : (tpx / W) * WQ + tpx % W;  // window pixel of tap (0, 0)
-  const int bofs = F8_WPIECES * 1024 + (wb * 3 + h) * 16;
+  const int bofs = WPC * 1024 + (wb * 3 + h) * 16;
   const int aofs = r * (F8_WROW * 16) + h * 16;
   // two accumulator chains per channel half (even / odd taps): four
   // independent MFMA chains, summed in the epilogue
@@ -2069,13 +2073,13 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
       const int T = ((d / 3) * WQ + (d % 3)) * 48;
       bq[s] = *(const u32x4*)(b + bofs + T);
       aq0[s] = *(const u32x4*)(b + aofs + d * 32);
-      aq1[s] = *(const u32x4*)(b + aofs + 32 * F8_WROW * 16 + d * 32);
+      if (CO == 64) aq1[s] = *(const u32x4*)(b + aofs + 32 * F8_WROW * 16 + d * 32);
     };
 #pragma unroll
     for (int d = 0; d < PF; ++d) rd(d, d);
     if (DEFER && c > 0) {  // tap 8 of chunk c-1 (even tap: chains 0 / 1)
       acc0 = Mma<bf16>::run(la0, lb, acc0);
-      acc1 = Mma<bf16>::run(la1, lb, acc1);
+      if (CO == 64) acc1 = Mma<bf16>::run(la1, lb, acc1);
     }
     // chunk c+AHEAD's pieces go out one per tap, in the MFMA shadow: its
     // buffer was last read in chunk c-1, before the last barrier
@@ -2086,13 +2090,13 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
       if (DEFER && d == 8) {
         lb = bq[d % NS];
         la0 = aq0[d % NS];
-        la1 = aq1[d % NS];
+        if (CO == 64) la1 = aq1[d % NS];
       } else if (d & 1) {
         acc2 = Mma<bf16>::run(aq0[d % NS], bq[d % NS], acc2);
-        acc3 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc3);
+        if (CO == 64) acc3 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc3);
       } else {
         acc0 = Mma<bf16>::run(aq0[d % NS], bq[d % NS], acc0);
-        acc1 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc1);
+        if (CO == 64) acc1 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc1);
       }
       if (d < NPW && pre) issue1(c + AHEAD, d);
       __builtin_amdgcn_sched_barrier(0);
@@ -2103,35 +2107,36 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     else if (young == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
     else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0), "+v"(la1)::"memory");
+    if (DEFER && CO == 64) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0), "+v"(la1)::"memory");
+    else if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0)::"memory");
     __builtin_amdgcn_s_barrier();
   }
   if (DEFER && nch > 0) {
     acc0 = Mma<bf16>::run(la0, lb, acc0);
-    acc1 = Mma<bf16>::run(la1, lb, acc1);
+    if (CO == 64) acc1 = Mma<bf16>::run(la1, lb, acc1);
   }
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e.  Bias and
   // residual are loaded for all 8 channel groups BEFORE the first store (vmcnt
   // retires loads and stores in order: a load behind a store waits for the
   // write, one round trip per group when they interleaved)
   const long long m = m0 + tpx;
-  float sv[STATS ? 64 : 1];  // STATS: [0,32) sums, [32,64) squares of the lane's 32 channels
-  f32x4 bb[2][4];
-  u32x2 rq[2][4];
+  float sv[STATS ? 2 * CO : 1];  // STATS: [0,CO) sums, [CO,2CO) squares of the lane's CO/2 channels
+  f32x4 bb[NJ][4];
+  u32x2 rq[NJ][4];
   if (p.bias) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) bb[j][g] = *(const f32x4*)(p.bias + co0 + 32 * j + 8 * g + 4 * h);
   }
   if (p.res) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) rq[j][g] = *(const u32x2*)(p.res + m * p.ldres + co0 + 32 * j + 8 * g + 4 * h);
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NJ; ++j) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int n = co0 + 32 * j + 8 * g + 4 * h;
@@ -2157,16 +2162,16 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
         for (int e = 0; e < 4; ++e) {
           const float q = stored<bf16>(v[e]);
           sv[16 * j + 4 * g + e] = q;
-          sv[32 + 16 * j + 4 * g + e] = q * q;
+          sv[CO / 2 + 16 * j + 4 * g + e] = q * q;
         }
       }
     }
   }
   if constexpr (STATS) {  // the host requires gn_P % 128 == 0: the tile is in one clip
-    gn_rs_reduce<64>(sv, r);
-    gn_block_add<bf16, 64>(p, sv, m0 / p.gn_P, [&](int k) {
+    gn_rs_reduce<2 * CO>(sv, r);
+    gn_block_add<bf16, 2 * CO>(p, sv, m0 / p.gn_P, [&](int k) {
       return co0 + 32 * (k / 16) + 8 * ((k % 16) / 4) + 4 * h + (k % 4);
-    }, (float*)smem, co0, 64);
+    }, (float*)smem, co0, CO);
   }
 }
 
@@ -2183,9 +2188,9 @@ bool fwd_frame_ok(const ConvFwdArgs<bf16>& a, int h, int w) {
 // channel x pixel split of the window conv's tiles over the 8 XCDs that
 // minimises the L2 fill traffic xp * |w| + xc * |x| (each XCD's L2 reads its
 // 1/xc of the weights and 1/xp of the input once); DV_FRAME_XC forces xc
-int frame_xcd_split(const ConvFwdArgs<bf16>& a) {
+int frame_xcd_split(const ConvFwdArgs<bf16>& a, int co) {
   static const int forced = getenv("DV_FRAME_XC") ? atoi(getenv("DV_FRAME_XC")) : -1;
-  const int ntco = a.cout / 64, npx = (int)(a.M / 128);
+  const int ntco = a.cout / co, npx = (int)(a.M / 128);
   auto ok = [&](int xc) { return ntco % xc == 0 && npx % (8 / xc) == 0; };
   if (forced == 0) return 0;
   if (forced > 0) return (forced <= 8 && 8 % forced == 0 && ok(forced)) ? forced : 0;
@@ -2202,24 +2207,25 @@ int frame_xcd_split(const ConvFwdArgs<bf16>& a) {
 
 int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   ConvFwdArgs<bf16> a = a0;
-  a.xcd_c = frame_xcd_split(a);
-  const int nblk = (int)(a.M / 128) * (a.cout / 64);
-  // A/B: DV_FRAME_PF = fragment prefetch distance in taps (2, 3 or 4)
-  // and DV_FRAME_DEFER = 1: the last tap's MFMAs after the chunk barrier
-  static const int pf = getenv("DV_FRAME_PF") ? atoi(getenv("DV_FRAME_PF")) : 2;
-  static const int df = getenv("DV_FRAME_DEFER") ? atoi(getenv("DV_FRAME_DEFER")) : 0;
+  // 32-channel tiles when 64-channel ones leave CUs idle (DV_FRAME_CO32=0: off)
+  static const bool co32_ok = !(getenv("DV_FRAME_CO32") && atoi(getenv("DV_FRAME_CO32")) == 0);
+  const int co = co32_ok && (a.M / 128) * (a.cout / 64) <= 128 ? 32 : 64;
+  a.xcd_c = frame_xcd_split(a, co);
+  const int nblk = (int)(a.M / 128) * (a.cout / co);
+  // fragment prefetch distance PF = 3 taps and DEFER (the last tap's MFMAs
+  // after the chunk barrier): same-box per-launch A/B (tools/frame_ab.py,
+  // profiles/r03_frame_ab.txt) put PF 3 + DEFER 1 1-3 % ahead of PF 2 without
+  // the deferral; the template keeps both knobs
   switch (a.W) {
-#define DV_FW3(WW, P, D) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, P, D><<<nblk, 256, 0, st>>>(a) \
-                                : conv_fwd_frame_kernel<WW, false, P, D><<<nblk, 256, 0, st>>>(a))
-#define DV_FW2(WW, P) (df ? DV_FW3(WW, P, 1) : DV_FW3(WW, P, 0))
-#define DV_FW(WW) (pf == 3 ? DV_FW2(WW, 3) : DV_FW2(WW, 2))
+#define DV_FW4(WW, C) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, C><<<nblk, 256, 0, st>>>(a) \
+                             : conv_fwd_frame_kernel<WW, false, 3, 1, C><<<nblk, 256, 0, st>>>(a))
+#define DV_FW(WW) (co == 32 ? DV_FW4(WW, 32) : DV_FW4(WW, 64))
     case 8: DV_FW(8); break;
     case 16: DV_FW(16); break;
     case 32: DV_FW(32); break;
     default: DV_FW(64); break;
 #undef DV_FW
-#undef DV_FW2
-#undef DV_FW3
+#undef DV_FW4
   }
   return check_launch("conv_fwd_frame");
 }

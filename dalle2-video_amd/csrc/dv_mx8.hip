@@ -37,15 +37,7 @@ constexpr int MX_WDATA = 64 * MX_WROW;               // 36,864
 constexpr int MX_WIMG = MX_WDATA + 64 * 32;          // + per-row scales [h][16]: 38,912 B
 constexpr int MX_WPIECES = MX_WIMG / 1024;           // 38 DMA pieces of 64 lanes x 16 B
 
-// scale exponent E of a block with max |v| = amax: every v * 2^-E lies in the
-// e4m3 range (<= 448) and the largest uses its top binade where it fits
-__device__ __forceinline__ int mx_exp(float amax) {
-  const unsigned b = __float_as_uint(amax);
-  const int eb = (int)((b >> 23) & 255);
-  const int E = eb - 135 + ((b & 0x7fffffu) > 0x600000u ? 1 : 0);
-  return E < -127 ? -127 : E;
-}
-__device__ __forceinline__ float mx_inv(int E) { return __uint_as_float((unsigned)(127 - E) << 23); }
+// mx_exp / mx_inv (the block scale exponent): dv_common.h
 
 // 16 floats (already scaled) -> 16 e4m3 bytes, element i at byte i
 __device__ __forceinline__ u32x4 mx_cvt16(const float* v, float inv) {

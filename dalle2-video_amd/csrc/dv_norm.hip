@@ -59,6 +59,8 @@ struct GnArgs {
   float *dgamma, *dbeta, *dss;
   int accumulate;
   long long rows_per_block;
+  uint8_t* q;       // fwd, bf16: the output also as MX-fp8 (see QNT), or null
+  unsigned* qs;
   int exp;  // timing experiments only (DV_GN_EXP): 1 no prologue math, 2 no `next` zeroing, 4 no block-0 section
 };
 
@@ -653,7 +655,11 @@ __device__ __forceinline__ void gn_zero_next(const GnArgs& a) {
 
 // MODE 0: forward apply  out = act(v) (+ res)
 // MODE 1: backward apply out = dz = rs*(dv*(1+s)*g - m1 - zhat*m2)
-template <typename T, int MODE, int U, bool SILU, bool RES, int DQ>  // DQ 0: LDS prologue
+// QNT (MODE 0, bf16, C % 64 == 0): the stored output is also written as the
+// MX-fp8 operand of the 3x3 conv that reads it (dv_mx8_quant's layout and
+// rounding, bit for bit: q [M][C] e4m3, qs [C/64][M] scale pairs): the 4
+// lanes holding one 32-channel block fold their amax with two lane xors
+template <typename T, int MODE, int U, bool SILU, bool RES, int DQ, bool QNT = false>  // DQ 0: LDS prologue
 __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float t1[64], t2[64], smu[64], srs[64];
@@ -782,6 +788,30 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
           o[2 * j] = v.x;
           o[2 * j + 1] = v.y;
         }
+        if constexpr (QNT) {
+          float ob[VEC], am = 0.f;
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            ob[e] = (float)(T)o[e];  // the value stored below
+            am = fmaxf(am, fabsf(ob[e]));
+          }
+          am = fmaxf(am, __shfl_xor(am, 1, 64));
+          am = fmaxf(am, __shfl_xor(am, 2, 64));
+          const int E = mx_exp(am);
+          const float inv = mx_inv(E);
+          u32x2 w;
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            unsigned t = __builtin_amdgcn_cvt_pk_fp8_f32(ob[4 * i] * inv, ob[4 * i + 1] * inv, 0, false);
+            w[i] = __builtin_amdgcn_cvt_pk_fp8_f32(ob[4 * i + 2] * inv, ob[4 * i + 3] * inv, t, true);
+          }
+          const long long m = pb + p;
+          *(u32x2*)(a.q + m * a.C + cv) = w;
+          const int E1 = __shfl_xor(E, 4, 64);  // the chunk's second 32-channel block
+          if ((cv & 63) == 0)
+            a.qs[(long long)(cv >> 6) * ((long long)a.nb * a.P) + m] =
+                (unsigned)(E + 127) | ((unsigned)(E1 + 127) << 8);
+        }
       } else {
         float dy[VEC];
         Vec<T>::to_f(xc[u], dy);
@@ -882,6 +912,17 @@ void gn_reduce_launch(GnArgs& a, int u, long long target, hipStream_t st) {
 #undef DV_GN_RED2
 }
 
+template <typename T, int MODE, int U, bool SILU, bool RES, int DQ>
+void gn_apply_go(const GnArgs& a, dim3 g, hipStream_t st) {
+  if constexpr (MODE == 0 && sizeof(T) == 2) {
+    if (a.q) {
+      gn_apply_kernel<T, MODE, U, SILU, RES, DQ, true><<<g, 256, 0, st>>>(a);
+      return;
+    }
+  }
+  gn_apply_kernel<T, MODE, U, SILU, RES, DQ><<<g, 256, 0, st>>>(a);
+}
+
 template <typename T, int MODE>
 void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
@@ -894,11 +935,11 @@ void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
   // A/B: DV_GN_DIRECT bit 0 forward, bit 1 backward apply (register prologue; else LDS)
   static const int dflag = getenv("DV_GN_DIRECT") ? atoi(getenv("DV_GN_DIRECT")) : 5;
   const int dq = sizeof(T) == 2 && (dflag >> MODE & 1) && gn_direct_ok(a, VEC) ? gn_direct_dq(a, VEC) : 0;
-#define DV_GN_APP2(UU, D)                                                            \
-  (silu ? (res ? gn_apply_kernel<T, MODE, UU, true, true, D><<<g, 256, 0, st>>>(a)    \
-               : gn_apply_kernel<T, MODE, UU, true, false, D><<<g, 256, 0, st>>>(a))  \
-        : (res ? gn_apply_kernel<T, MODE, UU, false, true, D><<<g, 256, 0, st>>>(a)   \
-               : gn_apply_kernel<T, MODE, UU, false, false, D><<<g, 256, 0, st>>>(a)))
+#define DV_GN_APP2(UU, D)                                                 \
+  (silu ? (res ? gn_apply_go<T, MODE, UU, true, true, D>(a, g, st)         \
+               : gn_apply_go<T, MODE, UU, true, false, D>(a, g, st))       \
+        : (res ? gn_apply_go<T, MODE, UU, false, true, D>(a, g, st)        \
+               : gn_apply_go<T, MODE, UU, false, false, D>(a, g, st)))
 #define DV_GN_APP(UU) \
   (dq == 1 ? DV_GN_APP2(UU, 1) : dq == 2 ? DV_GN_APP2(UU, 2) : dq == 4 ? DV_GN_APP2(UU, 4) : DV_GN_APP2(UU, 0))
   switch (u) {
@@ -1102,30 +1143,61 @@ void ln_launch(int nv, int blocks, const T* x, int ldx, const T* dy, int lddy, T
 
 }  // namespace
 
-extern "C" int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* res,
-                         int ldres, int nb, long long P, int C, int G, float eps,
-                         const float* gamma, const float* beta, const float* ss, int act,
-                         float* mean, float* rstd, float* sums, float* next, long long next_n,
-                         int sums_replicas, void* stream) {
-  DV_REQUIRE(z && y && gamma && beta && mean && rstd && sums, "null pointer");
-  DV_REQUIRE(sums_replicas >= 0 && sums_replicas <= 64 &&
+// DV_REQUIRE reporting the C entry point's name
+#define DV_REQUIRE_AS(fn, cond, msg)                         \
+  do {                                                       \
+    if (!(cond)) {                                           \
+      ::dv::set_error(std::string(fn) + ": " + (msg));       \
+      return DV_ERR_INVALID;                                 \
+    }                                                        \
+  } while (0)
+
+static int gn_fwd_impl(int dtype, const void* z, int ldz, void* y, int ldy, const void* res,
+                       int ldres, int nb, long long P, int C, int G, float eps,
+                       const float* gamma, const float* beta, const float* ss, int act,
+                       float* mean, float* rstd, float* sums, float* next, long long next_n,
+                       int sums_replicas, void* q, void* qs, void* stream, const char* fn) {
+  DV_REQUIRE_AS(fn, z && y && gamma && beta && mean && rstd && sums, "null pointer");
+  DV_REQUIRE_AS(fn, !q || (qs && dtype == DV_BF16 && C % 64 == 0 && ((uintptr_t)q & 7) == 0),
+             "the MX-fp8 copy needs bf16, C % 64 == 0 and 8-B aligned q (with qs)");
+  DV_REQUIRE_AS(fn, sums_replicas >= 0 && sums_replicas <= 64 &&
              (sums_replicas == 0 || !next || (long long)sums_replicas * nb * C * 2 <= next_n),
              "sums_replicas must fit the sums buffer (<= 64)");
-  DV_REQUIRE(C % G == 0, "C % G != 0");
+  DV_REQUIRE_AS(fn, C % G == 0, "C % G != 0");
   const int VEC = dtype == DV_BF16 ? 8 : 4;
-  DV_REQUIRE(C % VEC == 0 && ldz % VEC == 0 && ldy % VEC == 0 && (!res || ldres % VEC == 0),
+  DV_REQUIRE_AS(fn, C % VEC == 0 && ldz % VEC == 0 && ldy % VEC == 0 && (!res || ldres % VEC == 0),
              "channel counts / strides must be multiples of 16 bytes");
-  DV_REQUIRE(C <= GN_CMAX && G <= 64, "C > 1024 or G > 64");
-  DV_REQUIRE(next != sums || !next, "next must not alias sums");
+  DV_REQUIRE_AS(fn, C <= GN_CMAX && G <= 64, "C > 1024 or G > 64");
+  DV_REQUIRE_AS(fn, next != sums || !next, "next must not alias sums");
   GnArgs a{};
   a.z = z; a.ldz = ldz; a.out = y; a.ldo = ldy; a.res = res; a.ldres = ldres; a.nb = nb;
   a.P = P; a.C = C; a.G = G; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta;
   a.ss = ss; a.act = act; a.sums = sums; a.next = next; a.next_n = next ? next_n : 0; a.eps = eps;
   a.rstride = (long long)nb * C * 2;
   a.R = next && a.rstride > 0 ? (int)std::min<long long>(8, std::max<long long>(1, next_n / a.rstride)) : 1;
+  a.q = (uint8_t*)q; a.qs = (unsigned*)qs;
   if (nb == 0 || P == 0) return DV_OK;
   hipStream_t st = (hipStream_t)stream;
   return dtype == DV_BF16 ? gn_fwd_t<bf16>(a, sums_replicas, st) : gn_fwd_t<float>(a, sums_replicas, st);
+}
+
+extern "C" int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* res,
+                         int ldres, int nb, long long P, int C, int G, float eps,
+                         const float* gamma, const float* beta, const float* ss, int act,
+                         float* mean, float* rstd, float* sums, float* next, long long next_n,
+                         int sums_replicas, void* stream) {
+  return gn_fwd_impl(dtype, z, ldz, y, ldy, res, ldres, nb, P, C, G, eps, gamma, beta, ss, act, mean,
+                     rstd, sums, next, next_n, sums_replicas, nullptr, nullptr, stream, __func__);
+}
+
+extern "C" int dv_gn_fwd_mx8(const void* z, int ldz, void* y, int ldy, const void* res, int ldres,
+                             int nb, long long P, int C, int G, float eps, const float* gamma,
+                             const float* beta, const float* ss, int act, float* mean, float* rstd,
+                             float* sums, float* next, long long next_n, int sums_replicas, void* q,
+                             void* qs, void* stream) {
+  DV_REQUIRE(q && qs, "null pointer");
+  return gn_fwd_impl(DV_BF16, z, ldz, y, ldy, res, ldres, nb, P, C, G, eps, gamma, beta, ss, act, mean,
+                     rstd, sums, next, next_n, sums_replicas, q, qs, stream, __func__);
 }
 
 extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void* dz,

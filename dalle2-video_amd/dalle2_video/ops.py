@@ -700,14 +700,20 @@ class mx8_convs:
         return False
 
 
-# where the MX-fp8 conv runs (tools/cfg5_profile.py, same-box rocprof-free
-# per-launch timing at the config-5 shapes): frame widths <= 32 — the 16² / 32²
-# stages with 128 .. 768 input channels run 1.1-2.0x faster than their bf16
-# kernels (512 -> 512 at 16²: 114 -> 59 us) — while at 64² / 128² with 64-192
-# input channels (one or two 64-channel chunks per tile: no pipelining over K,
-# the operand DMA latency exposed) the bf16 stripe / glds kernels win and the
-# quantisation pass would cost more.  DV_FP8_ALL=1 puts every eligible conv on it.
-_MX8_MAX_W = 128 if os.environ.get("DV_FP8_ALL", "0") == "1" else 32
+# where the MX-fp8 conv runs: every eligible 3x3 conv (cin, cout % 64 == 0).
+# Same-box config-5 forward (tools/cfg5_profile.py, graph replay, r03i): fp8
+# at W <= 32 only 9.57 ms, at every width 9.00 ms with the GroupNorm-fused
+# quantisation (9.56 without it: the separate quantisation pass of the wide
+# 64² / 128² activations ate the conv gain), bf16 9.74-9.99 ms.
+# DV_FP8_MAX_W=32 restricts it to the 8² .. 32² stages.
+_MX8_MAX_W = int(os.environ.get("DV_FP8_MAX_W", "128"))
+# the GroupNorm apply writes the fp8 copy of its output (dv_gn_fwd_mx8) so the
+# consuming conv skips its quantisation pass; DV_FP8_FUSE=0 turns it off (A/B)
+_MX8_FUSE = os.environ.get("DV_FP8_FUSE", "1") != "0"
+
+
+def _mx8_geom(nf, h, w):
+    return ((h == 8 and w == 8) or (w in (16, 32, 64, 128) and h % (128 // w) == 0)) and (nf * h * w) % 128 == 0
 
 
 def mx8_ok(x0, x1, weight, res, ksize, h, w, nf):
@@ -721,8 +727,7 @@ def mx8_ok(x0, x1, weight, res, ksize, h, w, nf):
     cout, cin_real = weight.shape[0], weight.shape[1]
     if cin_real != c0 + c1 or c0 % 64 or c1 % 64 or cout % 64:
         return False
-    geom = (h == 8 and w == 8) or (w in (16, 32, 64, 128) and h % (128 // w) == 0)
-    if not geom or (nf * h * w) % 128:
+    if not _mx8_geom(nf, h, w):
         return False
     for t in (x0, x1, res):
         if t is not None:
@@ -776,8 +781,9 @@ def conv_mx8(x0, weight, bias=None, x1=None, res=None):
     nf, h, w, c0 = x0.shape
     c1 = 0 if x1 is None else x1.shape[3]
     cout = weight.shape[0]
-    q0, s0 = mx8_quant(x0)
-    q1, s1 = mx8_quant(x1) if x1 is not None else (None, None)
+    # a GroupNorm output already carries its MX-fp8 copy (dv_gn_fwd_mx8)
+    q0, s0 = getattr(x0, "_dv_mx8", None) or mx8_quant(x0)
+    q1, s1 = (getattr(x1, "_dv_mx8", None) or mx8_quant(x1)) if x1 is not None else (None, None)
     img = mx8_weight_image(weight)
     y = torch.empty(nf, h, w, cout, dtype=torch.bfloat16, device=x0.device)
     b = None if bias is None else bias.detach().float().contiguous()
@@ -1178,29 +1184,44 @@ def cross_embed(x, weights, biases):
 # ---------------------------------------------------------------------------
 # GroupNorm (+ per-sample scale/shift) + SiLU (+ residual)  — Block3D
 # ---------------------------------------------------------------------------
+def _gn_forward(z, gamma, beta, ss, res, nb, groups, eps, act, stats, mx8=False):
+    """dv_gn_fwd; mx8: y also as the MX-fp8 operand of its 3x3 consumer
+    (dv_gn_fwd_mx8), attached to y as `_dv_mx8` for conv_mx8."""
+    require_gpu(z, gamma, beta, ss, res)
+    nf, h, w, c = z.shape
+    P = (nf // nb) * h * w
+    dev = z.device
+    y = torch.empty(nf, h, w, c, dtype=z.dtype, device=dev)
+    mean = torch.empty(nb * groups, dtype=torch.float32, device=dev)
+    rstd = torch.empty_like(mean)
+    if stats is not None and stats.used:  # z's producing conv accumulated the statistics
+        if stats.P != P:
+            raise _lib.DVError("GroupNorm statistics were accumulated for another clip size")
+        cur, nxt, ready = stats.cur, stats.nxt, stats.R
+    elif stats is not None:  # the conv did not: reduce into the same (zeroed) buffer
+        cur, nxt, ready = stats.cur, stats.nxt, 0
+    else:
+        (cur, nxt), ready = _gn_sums(dev).take(nb * c * 2), 0
+    g, b = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
+    s = None if ss is None else ss.detach().float().contiguous()
+    args = (ptr(z), cl_ld(z), ptr(y), c, ptr(res), cl_ld(res) if res is not None else 0,
+            nb, P, c, groups, ctypes_float(eps), ptr(g), ptr(b), ptr(s), act, ptr(mean), ptr(rstd),
+            ptr(cur), ptr(nxt), nxt.numel(), ready)
+    if mx8:
+        m = nf * h * w
+        q = torch.empty(m * c, dtype=torch.uint8, device=dev)
+        qs = torch.empty((c // 64) * m, dtype=torch.int32, device=dev)
+        call("dv_gn_fwd_mx8", *args, ptr(q), ptr(qs), stream())
+        y._dv_mx8 = (q, qs)
+    else:
+        call("dv_gn_fwd", dt(z), *args, stream())
+    return y, g, b, s, mean, rstd
+
+
 class GroupNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, gamma, beta, ss, res, nb, groups, eps, act, stats=None, res_sink=None):
-        require_gpu(z, gamma, beta, ss, res)
-        nf, h, w, c = z.shape
-        P = (nf // nb) * h * w
-        dev = z.device
-        y = torch.empty(nf, h, w, c, dtype=z.dtype, device=dev)
-        mean = torch.empty(nb * groups, dtype=torch.float32, device=dev)
-        rstd = torch.empty_like(mean)
-        if stats is not None and stats.used:  # z's producing conv accumulated the statistics
-            if stats.P != P:
-                raise _lib.DVError("GroupNorm statistics were accumulated for another clip size")
-            cur, nxt, ready = stats.cur, stats.nxt, stats.R
-        elif stats is not None:  # the conv did not: reduce into the same (zeroed) buffer
-            cur, nxt, ready = stats.cur, stats.nxt, 0
-        else:
-            (cur, nxt), ready = _gn_sums(dev).take(nb * c * 2), 0
-        g, b = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
-        s = None if ss is None else ss.detach().float().contiguous()
-        call("dv_gn_fwd", dt(z), ptr(z), cl_ld(z), ptr(y), c, ptr(res), cl_ld(res) if res is not None else 0,
-             nb, P, c, groups, ctypes_float(eps), ptr(g), ptr(b), ptr(s), act, ptr(mean), ptr(rstd),
-             ptr(cur), ptr(nxt), nxt.numel(), ready, stream())
+        y, g, b, s, mean, rstd = _gn_forward(z, gamma, beta, ss, res, nb, groups, eps, act, stats)
         ctx.save_for_backward(z, g, b, s, mean, rstd)
         ctx.params = (gamma, beta)
         ctx.meta = (nb, groups, act, ss is not None, res is not None)
@@ -1251,7 +1272,14 @@ def group_norm_act(z, gamma, beta, nb, groups=8, eps=1e-5, scale_shift=None, res
                    act=_lib.ACT_SILU, stats=None, res_sink=None):
     """stats: the GnStats z's conv filled (one apply launch) or None (reduce + apply).
     res_sink: a GradSink shared with the conv that also reads `res` (the
-    residual's gradient is handed to it instead of returned to autograd)."""
+    residual's gradient is handed to it instead of returned to autograd).
+    Inside mx8_convs() without autograd, an output an MX-fp8 conv can read
+    (bf16, C % 64 == 0, a frame width it runs at) also gets its fp8 copy from
+    the same launch: the conv then skips its quantisation pass."""
+    if _MX8_FUSE and _Mx8State.active and not torch.is_grad_enabled() and z.dtype == torch.bfloat16:
+        nf, h, w, c = z.shape
+        if c % 64 == 0 and w <= _MX8_MAX_W and _mx8_geom(nf, h, w):
+            return _gn_forward(z, gamma, beta, scale_shift, res, nb, groups, eps, act, stats, mx8=True)[0]
     return GroupNormActFn.apply(z, gamma, beta, scale_shift, res, nb, groups, eps, act, stats, res_sink)
 
 

@@ -276,6 +276,13 @@ int dv_gn_fwd(int dtype, const void* z, int ldz, void* y, int ldy, const void* r
               int nb, long long P, int C, int G, float eps, const float* gamma,
               const float* beta, const float* ss, int act, float* mean, float* rstd, float* sums,
               float* next, long long next_n, int sums_replicas, void* stream);
+/* dv_gn_fwd (bf16) that also writes y as the MX-fp8 operand of the 3x3 conv
+ * reading it (sampling in fp8, BASELINE config 5): q [nb*P][C] e4m3 and qs
+ * [C/64][nb*P] scale pairs, bit-identical to dv_mx8_quant(y); C % 64 == 0. */
+int dv_gn_fwd_mx8(const void* z, int ldz, void* y, int ldy, const void* res, int ldres, int nb,
+                  long long P, int C, int G, float eps, const float* gamma, const float* beta,
+                  const float* ss, int act, float* mean, float* rstd, float* sums, float* next,
+                  long long next_n, int sums_replicas, void* q, void* qs, void* stream);
 /* dz from dy (z is the pre-norm input); dgamma/dbeta [C] and dss [nb][2C]
  * (+)= their gradients (accumulate != 0 adds).  sums/next as dv_gn_fwd.      */
 int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void* dz, int lddz,

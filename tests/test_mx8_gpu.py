@@ -174,3 +174,63 @@ def test_unet1_fp8_forward_config5_subshape(parity_log):
     assert n_mx8 >= 24, n_mx8  # the Block3D convs of the 32² / 16² stages and the mid block
     assert torch.isfinite(y8).all()
     assert e8 <= 0.15, e8
+
+
+@pytest.mark.parametrize("nb,frames,h,w,c,ss,res", [(2, 4, 16, 16, 128, True, False), (1, 8, 32, 32, 64, False, True),
+                                                     (2, 2, 8, 8, 512, True, True), (1, 3, 5, 128, 192, False, False)])
+def test_gn_fwd_mx8_bit_exact(nb, frames, h, w, c, ss, res):
+    """dv_gn_fwd_mx8 (the GroupNorm apply writing its output's MX-fp8 copy):
+    its e4m3 bytes and scale pairs == dv_mx8_quant of its own stored output,
+    bit for bit; the output == dv_gn_fwd's within the GroupNorm's run-to-run
+    noise (the statistics are f32 atomic sums: a last-bit change of the mean
+    flips an occasional bf16 rounding)."""
+    from dalle2_video import _lib, ops
+
+    g = torch.Generator().manual_seed(c + h)
+    nf = nb * frames
+    z = (3 * torch.randn(nf, h, w, c, generator=g)).bfloat16().cuda()
+    gamma, beta = (1 + 0.2 * torch.randn(c, generator=g)).cuda(), (0.2 * torch.randn(c, generator=g)).cuda()
+    sc = (0.3 * torch.randn(nb, 2 * c, generator=g)).cuda() if ss else None
+    r = torch.randn(nf, h, w, c, generator=g).bfloat16().cuda() if res else None
+    with torch.no_grad():
+        y0 = ops.group_norm_act(z, gamma, beta, nb, groups=8, scale_shift=sc, res=r)
+        y1 = ops._gn_forward(z, gamma, beta, sc, r, nb, 8, 1e-5, _lib.ACT_SILU, None, mx8=True)[0]
+        q0, s0 = ops.mx8_quant(y1)
+    q1, s1 = y1._dv_mx8
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q0), (q1 != q0).sum().item()
+    assert torch.equal(s1, s0), (s1 != s0).sum().item()
+    assert rel(y1, y0) <= 1e-3, rel(y1, y0)
+
+
+def test_unet1_fp8_fused_quant_matches_unfused(parity_log):
+    """The fp8 unet forward with the GroupNorm-fused quantisation vs the same
+    forward quantising every conv input in its own pass: equal up to the
+    run-to-run noise of the fp8 forward, measured beside as two unfused runs
+    (the GroupNorm statistics are f32 atomic sums; a last-bit change flips an
+    occasional e4m3 rounding downstream: ~1e-2 at this shape)."""
+    from dalle2_video import dalle2_video as D, ops
+    from dalle2_video.utils import deterministic_fill_
+
+    u = D.Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    deterministic_fill_(u)
+    u = u.cuda()
+    u.fp8 = True
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(1, 3, 8, 64, 64, generator=g).cuda()
+    emb = torch.randn(1, 512, generator=g).cuda()
+    t = torch.tensor([300]).cuda()
+    saved = ops._MX8_FUSE
+    try:
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16), ops.private_pack_cache():
+            ops._MX8_FUSE = True
+            ya = u(x, t, video_embed=emb)
+            ops._MX8_FUSE = False
+            yb = u(x, t, video_embed=emb)
+            yc = u(x, t, video_embed=emb)
+    finally:
+        ops._MX8_FUSE = saved
+    assert torch.isfinite(ya).all()
+    e, floor = rel(ya.float(), yb.float()), rel(yc.float(), yb.float())
+    parity_log(config="unet1 fp8 fwd 1x3x8x64x64, fused vs unfused quantisation", rel=e, unfused_run_to_run=floor)
+    assert e <= 2 * floor + 5e-3, (e, floor)
