@@ -2120,7 +2120,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   // retires loads and stores in order: a load behind a store waits for the
   // write, one round trip per group when they interleaved)
   const long long m = m0 + tpx;
-  float sv[STATS ? 2 * CO : 1];  // STATS: [0,CO) sums, [CO,2CO) squares of the lane's CO/2 channels
+  float sv[STATS ? CO : 1];  // STATS: [0,CO/2) sums, [CO/2,CO) squares of the lane's CO/2 channels
   f32x4 bb[NJ][4];
   u32x2 rq[NJ][4];
   if (p.bias) {
@@ -2168,8 +2168,8 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     }
   }
   if constexpr (STATS) {  // the host requires gn_P % 128 == 0: the tile is in one clip
-    gn_rs_reduce<2 * CO>(sv, r);
-    gn_block_add<bf16, 2 * CO>(p, sv, m0 / p.gn_P, [&](int k) {
+    gn_rs_reduce<CO>(sv, r);
+    gn_block_add<bf16, CO>(p, sv, m0 / p.gn_P, [&](int k) {
       return co0 + 32 * (k / 16) + 8 * ((k % 16) / 4) + 4 * h + (k % 4);
     }, (float*)smem, co0, CO);
   }
@@ -2620,64 +2620,94 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
 // LDS, so even a 256-split sum of a small gradient spreads over hundreds of
 // workgroups.  The bias partials ([S][cout], cout % 4 == 0) are reduced the
 // same way by the workgroups after the weight ones.
-__device__ __forceinline__ f32x4 part4(const void* p, bool pbf, long long i) {
-  if (!pbf) return ((const f32x4*)p)[i];
-  const bf16x4 t = __builtin_bit_cast(bf16x4, ((const u32x2*)p)[i]);
-  return f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
+// One lane handles 8 consecutive elements: a 16-B load of bf16 partials (or
+// two 16-B loads of f32 ones) per split, so the loads in flight per lane carry
+// twice the bytes of a float4 column and a workgroup covers 2,048 / G elements
+// (the big gradients have S = 4: one float4 per lane left the blocks mostly
+// overhead).
+struct F8 {
+  f32x4 lo, hi;
+};
+
+__device__ __forceinline__ F8 part8(const void* p, bool pbf, long long i) {
+  if (!pbf) return F8{((const f32x4*)p)[2 * i], ((const f32x4*)p)[2 * i + 1]};
+  const u32x4 t = ((const u32x4*)p)[i];
+  F8 r;
+  r.lo = f32x4{__builtin_bit_cast(float, t[0] << 16), __builtin_bit_cast(float, t[0] & 0xffff0000u),
+               __builtin_bit_cast(float, t[1] << 16), __builtin_bit_cast(float, t[1] & 0xffff0000u)};
+  r.hi = f32x4{__builtin_bit_cast(float, t[2] << 16), __builtin_bit_cast(float, t[2] & 0xffff0000u),
+               __builtin_bit_cast(float, t[3] << 16), __builtin_bit_cast(float, t[3] & 0xffff0000u)};
+  return r;
 }
 
-__device__ __forceinline__ void reduce4_block(f32x4* sh, long long blk, const float* part, int S,
-                                              int G, long long n4, float* dw, int acc_w,
+__device__ __forceinline__ void reduce8_block(F8* sh, long long blk, const float* part, int S,
+                                              int G, long long n8, float* dw, int acc_w,
                                               const float* dbpart, float* db, int cout, int acc_b,
                                               int part_bf16) {
   const int cols = 256 / G;
-  const long long wblocks = (n4 + cols - 1) / cols;
+  const long long wblocks = (n8 + cols - 1) / cols;
   const bool bias = blk >= wblocks;
-  const long long n = bias ? cout / 4 : n4;
+  const long long n = bias ? cout / 8 : n8;
   const void* src = bias ? (const void*)dbpart : (const void*)part;
   const bool pbf = part_bf16 && !bias;  // the bias partials stay f32
   float* dst = bias ? db : dw;
   const int acc = bias ? acc_b : acc_w;
   const int c = threadIdx.x % cols, grp = threadIdx.x / cols;
   const long long i = (bias ? blk - wblocks : blk) * (long long)cols + c;
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  if (i < n) {
-    int s = grp;
-    for (; s + 7 * G < S; s += 8 * G) {
-      f32x4 t[8];
+  const long long ic = i < n ? i : n - 1;  // clamped: every load unconditional
+  F8 v = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  int s = grp;
+  for (; s + 3 * G < S; s += 4 * G) {
+    F8 t[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = part4(src, pbf, (long long)(s + u * G) * n + i);
-      v += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
-    }
-    for (; s < S; s += G) v += part4(src, pbf, (long long)s * n + i);
+    for (int u = 0; u < 4; ++u) t[u] = part8(src, pbf, (long long)(s + u * G) * n + ic);
+    v.lo += (t[0].lo + t[1].lo) + (t[2].lo + t[3].lo);
+    v.hi += (t[0].hi + t[1].hi) + (t[2].hi + t[3].hi);
   }
-  sh[threadIdx.x] = v;
-  __syncthreads();
-  if (grp != 0 || i >= n) return;
-  for (int gg = 1; gg < G; ++gg) v += sh[gg * cols + c];
-  f32x4* o = (f32x4*)dst + i;
-  if (acc) v += *o;
-  *o = v;
+  for (; s < S; s += G) {
+    const F8 t = part8(src, pbf, (long long)s * n + ic);
+    v.lo += t.lo;
+    v.hi += t.hi;
+  }
+  if (G > 1) {
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    if (grp != 0) return;
+    for (int gg = 1; gg < G; ++gg) {
+      v.lo += sh[gg * cols + c].lo;
+      v.hi += sh[gg * cols + c].hi;
+    }
+  }
+  if (i >= n) return;
+  f32x4* o = (f32x4*)dst + 2 * i;
+  if (acc) {
+    v.lo += o[0];
+    v.hi += o[1];
+  }
+  o[0] = v.lo;
+  o[1] = v.hi;
 }
 
+// n4 = gradient elements / 4 (the table's unit); every stripe-wgrad gradient
+// and bias has a multiple of 8 elements (cin, cout % 64 == 0)
 inline long long reduce4_blocks(long long n4, int G, int cout, bool bias) {
   const int cols = 256 / G;
-  return (n4 + cols - 1) / cols + (bias ? (cout / 4 + cols - 1) / cols : 0);
+  return (n4 / 2 + cols - 1) / cols + (bias ? (cout / 8 + cols - 1) / cols : 0);
 }
 
 __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* part, int S, int G,
                                                             long long n4, float* dw, int acc_w,
                                                             const float* dbpart, float* db,
                                                             int cout, int acc_b, int part_bf16) {
-  __shared__ f32x4 sh[256];
-  reduce4_block(sh, blockIdx.x, part, S, G, n4, dw, acc_w, dbpart, db, cout, acc_b, part_bf16);
+  __shared__ F8 sh[256];
+  reduce8_block(sh, blockIdx.x, part, S, G, n4 / 2, dw, acc_w, dbpart, db, cout, acc_b, part_bf16);
 }
 
 // every pending split-K sum of a backward pass in one launch: block b belongs
 // to the last entry whose blk0 <= b (binary search over the small table)
 __global__ __launch_bounds__(256) void wgrad_reduce_batched_kernel(const DvWgradReduceEntry* table,
                                                                    int n) {
-  __shared__ f32x4 sh[256];
+  __shared__ F8 sh[256];
   const long long b = blockIdx.x;
   int lo = 0, hi = n - 1;
   while (lo < hi) {
@@ -2686,14 +2716,15 @@ __global__ __launch_bounds__(256) void wgrad_reduce_batched_kernel(const DvWgrad
     else hi = mid - 1;
   }
   const DvWgradReduceEntry e = table[lo];
-  reduce4_block(sh, b - e.blk0, e.part, e.S, e.G, e.n4, e.dw, e.acc_w, e.dbpart, e.db, e.cout,
+  reduce8_block(sh, b - e.blk0, e.part, e.S, e.G, e.n4 / 2, e.dw, e.acc_w, e.dbpart, e.db, e.cout,
                 e.acc_b, e.part_bf16);
 }
 
+// split groups per workgroup: each lane keeps >= 4 splits (4 loads in flight)
 inline int reduce4_groups(int S) {
   static const int gmax = getenv("DV_RED_G") ? atoi(getenv("DV_RED_G")) : 8;
   int G = 1;
-  while (G * 2 <= gmax && G * 2 <= S) G *= 2;
+  while (G * 2 <= gmax && G * 8 <= S) G *= 2;
   return G;
 }
 
@@ -2966,7 +2997,7 @@ extern "C" int dv_wgrad_reduce_plan(DvWgradReduceEntry* t, int n, long long* blo
   DV_REQUIRE(t && blocks && n > 0, "bad table");
   long long blk = 0;
   for (int i = 0; i < n; ++i) {
-    DV_REQUIRE(t[i].S >= 1 && t[i].n4 > 0 && t[i].cout % 4 == 0 && t[i].part && t[i].dw &&
+    DV_REQUIRE(t[i].S >= 1 && t[i].n4 > 0 && t[i].n4 % 2 == 0 && t[i].cout % 8 == 0 && t[i].part && t[i].dw &&
                    (!t[i].db || t[i].dbpart),
                "bad entry");
     t[i].G = reduce4_groups(t[i].S);
@@ -2986,7 +3017,7 @@ extern "C" int dv_wgrad_reduce_batched(const DvWgradReduceEntry* table, int n, l
 }
 
 extern "C" int dv_wgrad_reduce_one(const DvWgradReduceEntry* e, void* stream) {
-  DV_REQUIRE(e && e->S >= 1 && e->n4 > 0 && e->cout % 4 == 0 && e->part && e->dw && (!e->db || e->dbpart),
+  DV_REQUIRE(e && e->S >= 1 && e->n4 > 0 && e->n4 % 2 == 0 && e->cout % 8 == 0 && e->part && e->dw && (!e->db || e->dbpart),
              "bad entry");
   const int G = reduce4_groups(e->S);
   wgrad_reduce4_kernel<<<(unsigned)reduce4_blocks(e->n4, G, e->cout, e->db != nullptr), 256, 0,

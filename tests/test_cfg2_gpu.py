@@ -165,6 +165,8 @@ def test_group_norm_act_full_size(parity_log, nb, T_, H, C, with_ss, with_res, d
     (4, 16, 32, 192, 64, 128, torch.bfloat16),   # glds 128x128 (up2)
     (4, 16, 16, 384, 128, 256, torch.bfloat16),  # window 16 (up1)
     (4, 16, 8, 512, 0, 512, torch.bfloat16),     # window 8 (mid)
+    (4, 16, 8, 256, 0, 256, torch.bfloat16),     # window 8, 32-channel tiles (M = 4,096: 128 tiles of 64)
+    (4, 16, 16, 128, 0, 256, torch.bfloat16),    # window 16, 8 channel chunks (down2 block1)
     (2, 3, 6, 16, 0, 64, torch.bfloat16),        # generic kernel, clips straddle tiles (P = 108)
     (2, 4, 8, 64, 0, 64, torch.float32),         # f32 parity kernel
 ])
