@@ -245,9 +245,18 @@ def sampling_leg(args, device):
     # spread over a short loop; est_1000_step_s adds it back once.
     T5A, T5B = 8, 24
     u = Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    # VideoDecoder rebuilds the unet it is given (cast_model_parameters, quirk
+    # Q3: a fresh instance, as the reference's Decoder): the first decoder's unet
+    # is the one filled and timed, and the second decoder is pointed at it
+    d0 = VideoDecoder(unet=(u,), frame_sizes=(128,), frame_numbers=(32,), timesteps=T5A,
+                      learned_variance=False)
+    u = d0.unets[0]
     deterministic_fill_(u)
-    decs = [VideoDecoder(unet=(u,), frame_sizes=(128,), frame_numbers=(32,), timesteps=T5,
-                         learned_variance=False).to(device) for T5 in (T5A, T5B)]
+    d1 = VideoDecoder(unet=(u,), frame_sizes=(128,), frame_numbers=(32,), timesteps=T5B,
+                      learned_variance=False)
+    d1.unets[0] = u
+    decs = [d0.to(device), d1.to(device)]
+    assert next(u.parameters()).is_cuda
     emb = torch.randn(2, 512, device=device)
     from dalle2_video import ops
 

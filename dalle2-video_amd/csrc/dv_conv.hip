@@ -21,6 +21,29 @@
 
 using namespace dv;
 
+// Diagnostic build only (make stamp): per-workgroup s_memrealtime stamps of
+// a kernel's phases into a device array read back by dv_debug_stamps
+// (tools/wgrad_stamp.py).  The product build compiles none of it.
+#ifdef DV_STAMP
+constexpr int DV_NSTAMP = 8;
+__device__ unsigned long long g_dv_stamp[16384 * DV_NSTAMP];
+#define DV_STAMP_AT(i)                                                                  \
+  do {                                                                                  \
+    if (threadIdx.x == 0) {                                                             \
+      const long long blin = blockIdx.x + (long long)gridDim.x * (blockIdx.y + (long long)gridDim.y * blockIdx.z); \
+      if (blin < 16384) g_dv_stamp[blin * DV_NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                   \
+  } while (0)
+extern "C" int dv_debug_stamps(unsigned long long* host, long long n) {
+  if (n > 16384 * DV_NSTAMP) n = 16384 * DV_NSTAMP;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dv_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#else
+#define DV_STAMP_AT(i) \
+  do {                 \
+  } while (0)
+#endif
+
 namespace {
 
 __device__ __forceinline__ int sw_off(int row, int chunk) {
@@ -1971,6 +1994,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
   constexpr int WPC = G::WPC, NJ = CO / 32;
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
+  DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int npx = (int)(p.M / 128), nblk = npx * (p.cout / CO);
@@ -2046,6 +2070,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   else if (pro == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  DV_STAMP_AT(1);
 
   const int r = lane & 31, h = lane >> 5;
   const int pix = fw_pix<W>(r);                    // within the wave's 32 pixels
@@ -2115,6 +2140,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     acc0 = Mma<bf16>::run(la0, lb, acc0);
     if (CO == 64) acc1 = Mma<bf16>::run(la1, lb, acc1);
   }
+  DV_STAMP_AT(2);
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e.  Bias and
   // residual are loaded for all 8 channel groups BEFORE the first store (vmcnt
   // retires loads and stores in order: a load behind a store waits for the
@@ -2173,6 +2199,10 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
       return co0 + 32 * (k / 16) + 8 * ((k % 16) / 4) + 4 * h + (k % 4);
     }, (float*)smem, co0, CO);
   }
+#ifdef DV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  DV_STAMP_AT(4);
 }
 
 bool fwd_frame_ok(const ConvFwdArgs<bf16>& a, int h, int w) {
@@ -2407,6 +2437,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   constexpr int DPS = 2 + 2 * NRH;  // DMAs per thread per stage
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * STG];
 
+  DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int half = wave >> 2, wq = wave & 3, wm = wq >> 1, wn = wq & 1;
@@ -2509,6 +2540,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
+    if (st == 0) DV_STAMP_AT(1);
     const char* sA = smem + buf * STG + wm * (AIMG / 2);
     const char* sB = smem + buf * STG + AIMG + wn * BHALF;
 #pragma unroll
@@ -2538,6 +2570,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
+  DV_STAMP_AT(2);
   accb += __shfl_xor(accb, 32, 64);  // both k-halves of the channel
 
   // ---- sum the two pixel halves through LDS (two passes over the taps) ----
@@ -2563,6 +2596,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
     }
     __syncthreads();
   }
+  DV_STAMP_AT(3);
   // ---- torch-layout output [co][ci][tap]: each wave's 32 x 32 x 9 tile is
   // transposed through LDS (two tiles per round, 36 KB each) so every output
   // channel's 32 ci x 9 taps go out as 1152 contiguous bytes (float4 stores).
@@ -2607,6 +2641,10 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
     }
     __syncthreads();
   }
+#ifdef DV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial stores written
+#endif
+  DV_STAMP_AT(4);
   if (do_bias && half == 0 && lane < 32) {
     const int co = co0 + wm * 32 + lane;
     if (direct) a.db[co] = a.acc_b ? a.db[co] + accb : accb;

@@ -152,7 +152,14 @@ def dtype_name(t):
 
 
 def ptr(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    """Device address of a tensor for the C-ABI.  Every pointer the library
+    takes is a device pointer: a host tensor here would be dereferenced by a
+    kernel (a GPU memory fault), so it is rejected before any launch."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise DVError("the HIP path runs on the GPU only (got a CPU tensor)")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def require_gpu(*ts):

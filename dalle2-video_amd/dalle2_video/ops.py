@@ -1108,6 +1108,9 @@ _XE_WS = {}
 class CrossEmbedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, nbranch, *params):
+        # the descriptor carries raw weight addresses: a host weight would be
+        # read by the pack kernel (memory fault), so check before any launch
+        require_gpu(x, *[p for p in params if p is not None])
         weights = [p.detach().float().contiguous() for p in params[:nbranch]]
         biases = [None if p is None else p.detach().float().contiguous() for p in params[nbranch:]]
         nf, h, w, _ = x.shape

@@ -150,6 +150,7 @@ class FusedAdamW(torch.optim.Optimizer):
         if not self.ensure_flat():
             return None
         P, G, M, V, ranges, _ = self._flat
+        _lib.require_gpu(P, G, M, V)  # raw addresses below: never a host buffer
         self._t += 1
         for gi, start, end in ranges:
             if end <= start:
@@ -463,6 +464,10 @@ def allreduce_flat_grad(flat_grad, world, bucket_bytes=None, force=False):
     return flat_grad
 
 
+# collectives captured into HIP graphs (see OverlappedAllReduce.wait)
+_CAPTURED_WORKS = []
+
+
 class OverlappedAllReduce:
     """The gradient all-reduce of one unet overlapped with its backward — what
     DDP's bucket hooks do inside the reference's accelerator.backward
@@ -601,6 +606,13 @@ class OverlappedAllReduce:
     def wait(self):
         for w in self.works:
             w.wait()
+        if self.works and torch.cuda.is_current_stream_capturing():
+            # the captured works' events were recorded in the capturing stream;
+            # ProcessGroupNCCL returns a released work's events to its event
+            # cache, and an eager collective that re-records such an event makes
+            # the watchdog's hipEventQuery fail (hipErrorCapturedEvent, process
+            # abort): captured works are kept for the life of the process
+            _CAPTURED_WORKS.extend(self.works)
         self.works = []
 
 
