@@ -787,6 +787,16 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (__attribute__((address_space(3))) s16x4*)(lds_addr));
 }
+// LDS byte address (32-bit) of a shared-memory pointer, and a transposed read
+// at base + a compile-time offset (the ds_read's immediate field)
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ unsigned lds_u32(const char* p) {
+  return (unsigned)(size_t)(const lds_char*)p;
+}
+__device__ __forceinline__ s16x4 tr_read_at(unsigned base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)((lds_char*)(size_t)base + off));
+}
 
 template <typename T, int BMC, int BNK>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs<T> p) {
@@ -2543,29 +2553,53 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
     if (st == 0) DV_STAMP_AT(1);
     const char* sA = smem + buf * STG + wm * (AIMG / 2);
     const char* sB = smem + buf * STG + AIMG + wn * BHALF;
+    // This stage's operand addresses: one VGPR per (k-step, pixel half), the
+    // tap offset an immediate of the ds_read.  The empty asm makes the lane
+    // offsets opaque per stage: otherwise the (offset + tap) sums are hoisted
+    // out of the stage loop as 36 loop-invariant registers, each read then
+    // costs two VALU, and the registers left no room for a prefetch.
+    unsigned wl[4], wh[4];
+    const unsigned sBu = lds_u32(sB);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int R0 = half * 64 + 16 * s + 8 * (g >> 1);
-      u32x4 fa;
-      {
-        const s16x4 lo = tr_read(sA + (R0 + q) * 64 + colb);
-        const s16x4 hi = tr_read(sA + (R0 + 4 + q) * 64 + colb);
-        const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
-        fa = u32x4{l2[0], l2[1], h2[0], h2[1]};
-      }
+      wl[s] = sBu + wlo[s];
+      wh[s] = sBu + whi[s];
+      asm volatile("" : "+v"(wl[s]), "+v"(wh[s]));
+    }
+    const int a0 = ((half * 64 + 8 * (g >> 1) + q) * 64 + colb);
+    // the 4 A fragments (dY) of the stage up front; B (window) fragments of
+    // tap j + WPF are read while tap j multiplies (flattened k-step x tap)
+    u32x4 fa[4];
 #pragma unroll
-      for (int d = 0; d < NT; ++d) {
-        const int toff = KS == 1 ? 0 : ((d / 3) * WP + (d % 3)) * 64;
-        const s16x4 lo = tr_read(sB + wlo[s] + toff);
-        const s16x4 hi = tr_read(sB + whi[s] + toff);
-        const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
-        acc[d] = Mma<bf16>::run(fa, u32x4{l2[0], l2[1], h2[0], h2[1]}, acc[d]);
-      }
-      if (do_bias) {
+    for (int s = 0; s < 4; ++s) {
+      const s16x4 lo = tr_read(sA + a0 + s * 1024);
+      const s16x4 hi = tr_read(sA + a0 + s * 1024 + 256);
+      const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+      fa[s] = u32x4{l2[0], l2[1], h2[0], h2[1]};
+    }
+    constexpr int NJ = 4 * NT, WPF = NT >= 3 ? 3 : NT, NR = WPF + 1;
+    u32x4 fb[NR];
+    auto rdB = [&](int j) {
+      const int s = j / NT, d = j % NT;
+      const int toff = KS == 1 ? 0 : ((d / 3) * WP + (d % 3)) * 64;
+      const s16x4 lo = tr_read_at(wl[s], toff);
+      const s16x4 hi = tr_read_at(wh[s], toff);
+      const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+      fb[j % NR] = u32x4{l2[0], l2[1], h2[0], h2[1]};
+    };
+#pragma unroll
+    for (int j = 0; j < WPF; ++j) rdB(j);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if (j + WPF < NJ) rdB(j + WPF);
+      const int s = j / NT, d = j % NT;
+      acc[d] = Mma<bf16>::run(fa[s], fb[j % NR], acc[d]);
+      if (d == NT - 1 && do_bias) {
         float t[8];
-        Vec<bf16>::to_f(fa, t);
+        Vec<bf16>::to_f(fa[s], t);
         accb += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
