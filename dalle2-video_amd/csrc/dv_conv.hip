@@ -1998,7 +1998,7 @@ __device__ __forceinline__ int fw_pix(int r) {
   else return (ga ? 0 : 16) + a;
 }
 
-template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64>
+template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true>
 __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
   using G = FwGeom<W, CO>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
@@ -2006,7 +2006,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
   DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6) & 3;  // & 3: the DMA piece type folds per (wave, i)
   const int npx = (int)(p.M / 128), nblk = npx * (p.cout / CO);
   int L = blockIdx.x;
   int co0;
@@ -2061,7 +2061,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     char* b = smem + (c % NBUF) * BUF;
     const int k = min(wave + 4 * i, PIECES - 1);
     if (k < WPC) dma16s(wr, b + k * 1024, voff0[i], (unsigned)ci0 * 18);
-    else if (first) dma16s(xr0, b + k * 1024, voff0[i], (unsigned)ci0 * 2);
+    else if (!SPLIT || first) dma16s(xr0, b + k * 1024, voff0[i], (unsigned)ci0 * 2);
     else dma16s(xr1, b + k * 1024, voff1[i], (unsigned)(ci0 - p.c0) * 2);
   };
   auto issue = [&](int c) {
@@ -2098,7 +2098,10 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   // chunk c+1's first fragment reads are in flight (its operands are in
   // registers before the barrier, so the buffer may be refilled under them)
   u32x4 lb, la0, la1;
-  for (int c = 0; c < nch; ++c) {
+  // one chunk; PRE (compile-time): chunk c + AHEAD exists and is issued here.
+  // The loop is split into the chunks that issue and the AHEAD tail, so the
+  // main loop carries no per-piece branch and a constant vmcnt
+  auto chunk = [&](int c, auto PRE) {
     const char* b = smem + (c % NBUF) * BUF;
     // fragments of tap d + PF are read while tap d multiplies (one wave per
     // SIMD: the LDS latency is hidden by this wave's own MFMAs only)
@@ -2118,7 +2121,6 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     }
     // chunk c+AHEAD's pieces go out one per tap, in the MFMA shadow: its
     // buffer was last read in chunk c-1, before the last barrier
-    const bool pre = c + AHEAD < nch;
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
       if (d + PF < 9) rd(d + PF, (d + PF) % NS);
@@ -2133,19 +2135,28 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
         acc0 = Mma<bf16>::run(aq0[d % NS], bq[d % NS], acc0);
         if (CO == 64) acc1 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc1);
       }
-      if (d < NPW && pre) issue1(c + AHEAD, d);
+      if constexpr (decltype(PRE)::value) {
+        if (d < NPW) issue1(c + AHEAD, d);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     // chunk c+1 landed: younger are the pieces of chunks c+2 .. c+AHEAD
-    const int young = min(c + AHEAD, nch - 1) - (c + 1);
-    if (young >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
-    else if (young == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
-    else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (decltype(PRE)::value) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((AHEAD - 1) * NPW) : "memory");
+    } else {
+      const int young = min(c + AHEAD, nch - 1) - (c + 1);
+      if (young >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
+      else if (young == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
+      else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (DEFER && CO == 64) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0), "+v"(la1)::"memory");
     else if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0)::"memory");
     __builtin_amdgcn_s_barrier();
-  }
+  };
+  int c = 0;
+  for (; c + AHEAD < nch; ++c) chunk(c, std::true_type{});
+  for (; c < nch; ++c) chunk(c, std::false_type{});
   if (DEFER && nch > 0) {
     acc0 = Mma<bf16>::run(la0, lb, acc0);
     if (CO == 64) acc1 = Mma<bf16>::run(la1, lb, acc1);
@@ -2257,8 +2268,10 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   // profiles/r03_frame_ab.txt) put PF 3 + DEFER 1 1-3 % ahead of PF 2 without
   // the deferral; the template keeps both knobs
   switch (a.W) {
-#define DV_FW4(WW, C) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, C><<<nblk, 256, 0, st>>>(a) \
-                             : conv_fwd_frame_kernel<WW, false, 3, 1, C><<<nblk, 256, 0, st>>>(a))
+#define DV_FW5(WW, C, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, C, SP><<<nblk, 256, 0, st>>>(a) \
+                                 : conv_fwd_frame_kernel<WW, false, 3, 1, C, SP><<<nblk, 256, 0, st>>>(a))
+  // SPLIT: the input is a channel concat of two sources (the up-path skips)
+#define DV_FW4(WW, C) (a.c0 < a.cin ? DV_FW5(WW, C, true) : DV_FW5(WW, C, false))
 #define DV_FW(WW) (co == 32 ? DV_FW4(WW, 32) : DV_FW4(WW, 64))
     case 8: DV_FW(8); break;
     case 16: DV_FW(16); break;
@@ -2266,6 +2279,7 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
     default: DV_FW(64); break;
 #undef DV_FW
 #undef DV_FW4
+#undef DV_FW5
   }
   return check_launch("conv_fwd_frame");
 }
