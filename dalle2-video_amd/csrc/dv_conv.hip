@@ -515,31 +515,55 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p,
   const __amdgpu_buffer_rsrc_t wr = dma_rsrc(p.w + (long long)n0 * p.K, (unsigned)(nrows * p.K * 2));
   const int poff = (int)(-plo);
 
+  // per-row DMA state, computed once: the row pixel's byte offset in each
+  // source (relative to the raw buffer base plo, with the row's swizzled
+  // chunk) and the mask of the taps whose input pixel is inside the frame;
+  // per K-tile each DMA then adds one uniform tap offset (no multiply and no
+  // exec-masked block per DMA: 10+ VALU per DMA before), and the weight DMAs
+  // take the K-tile offset in the instruction's soffset (no VALU at all)
+  unsigned rb0[GB], rb1[GB], tmask[GB], ab[GA];
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int row = 32 * i + (tid >> 3);
+    const int cs = chunk ^ swz8(row);
+    rb0[i] = (unsigned)(((b_pix[i] + poff) * p.ld0 + cs * 8) * 2);
+    rb1[i] = (unsigned)(((b_pix[i] + poff) * p.ld1 + cs * 8) * 2);
+    // ks is 1 or 3 (host-checked); tap t = 3 (dy + 1) + dx + 1
+    const int y = b_y[i], x = b_x[i];
+    const unsigned H = (unsigned)p.H, Wd = (unsigned)p.W;
+    if (p.ks == 1) {
+      tmask[i] = (unsigned)y < H ? 1u : 0u;
+    } else {
+      const unsigned ym = ((unsigned)(y - 1) < H ? 1u : 0u) | ((unsigned)y < H ? 2u : 0u) |
+                          ((unsigned)(y + 1) < H ? 4u : 0u);
+      const unsigned xm = ((unsigned)(x - 1) < Wd ? 1u : 0u) | 2u | ((unsigned)(x + 1) < Wd ? 4u : 0u);
+      tmask[i] = ((ym & 1u) ? xm : 0u) | ((ym & 2u) ? xm << 3 : 0u) | ((ym & 4u) ? xm << 6 : 0u);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int row = 32 * i + a_rowoff;
+    ab[i] = (unsigned)((row * p.K + (chunk ^ swz8(row)) * 8) * 2);
+  }
+
   auto issue = [&](int kt, int buf) {
     const int tap = kt / cblocks;
     const int ci = ((kt - tap * cblocks) << 6);
     const int dy = tap / p.ks - pad, dx = tap % p.ks - pad;
-    const int doff = dy * p.W + dx + poff;
     const bool first = ci < p.c0;  // wave-uniform: the 64-channel block never straddles c0
     const int cof = first ? ci : ci - p.c0;
     const int ld = first ? p.ld0 : p.ld1;
+    const unsigned toff = (unsigned)(((dy * p.W + dx) * ld + cof) * 2);  // mod 2^32 (dy, dx < 0)
     char* sB = smem + buf * BUF;
     char* sA = sB + BM * 128;
 #pragma unroll
     for (int i = 0; i < GB; ++i) {
-      const int row = 32 * i + (tid >> 3);
-      const int cs = chunk ^ swz8(row);
-      const int yy = b_y[i] + dy, xx = b_x[i] + dx;
-      const bool in = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-      const unsigned voff = in ? (unsigned)(((b_pix[i] + doff) * ld + cof + cs * 8) * 2) : DMA_OOB;
+      const bool in = (tmask[i] >> tap) & 1u;
+      const unsigned voff = in ? (first ? rb0[i] : rb1[i]) + toff : DMA_OOB;
       dma16(first ? xr0 : xr1, sB + (32 * i + 8 * wave) * 128, voff);
     }
 #pragma unroll
-    for (int i = 0; i < GA; ++i) {
-      const int row = 32 * i + a_rowoff;
-      const int cs = chunk ^ swz8(row);
-      dma16(wr, sA + (32 * i + 8 * wave) * 128, (unsigned)((row * p.K + (kt << 6) + cs * 8) * 2));
-    }
+    for (int i = 0; i < GA; ++i) dma16s(wr, sA + (32 * i + 8 * wave) * 128, ab[i], (unsigned)kt * 128);
   };
 
   f32x16 acc[TJ][TI];
@@ -1530,8 +1554,10 @@ int launch_fwd_glds(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   const bool stats = a.gn_sums != nullptr;
 #define DV_GL(NB) (stats ? conv_fwd_glds_kernel<BM, BN, NB, true><<<(unsigned)nb, 256, 0, st>>>(a, tn) \
                          : conv_fwd_glds_kernel<BM, BN, NB, false><<<(unsigned)nb, 256, 0, st>>>(a, tn))
-  if (nb <= 256) DV_GL(DEEP);
-  else if (nb <= 512 && MID >= 3) DV_GL(MID);
+  // DV_GLDS_RING=deep|mid|2 forces one ring depth (A/B)
+  static const int force = getenv("DV_GLDS_RING") ? (getenv("DV_GLDS_RING")[0] == 'd' ? 3 : getenv("DV_GLDS_RING")[0] == 'm' ? 2 : 1) : 0;
+  if (force == 3 || (!force && nb <= 256)) DV_GL(DEEP);
+  else if (force == 2 || (!force && nb <= 512 && MID >= 3)) DV_GL(MID);
   else DV_GL(2);
 #undef DV_GL
   return check_launch("conv_fwd_glds");
@@ -2334,7 +2360,7 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
       return cin == 64 ? launch_conv1x1<128, 1>(a, st) : launch_conv1x1<128, 2>(a, st);
     }
     const long long maxld = ld0 > (x1 ? ld1 : 0) ? ld0 : ld1;
-    if (cin % 64 == 0 && a.c0 % 64 == 0 && a.M * maxld < (1ll << 31)) {
+    if (cin % 64 == 0 && a.c0 % 64 == 0 && a.M * maxld < (1ll << 31) && (ks == 1 || ks == 3)) {  // the kernel's tap mask
       int bm, bn;
       glds_tile(a.M, cout, a.K, bm, bn);
       if (bm == 256) return launch_fwd_glds<256, 64>(a, st);
