@@ -2485,7 +2485,10 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   constexpr int WP = G::WP, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF, NT = G::NT;
   constexpr int AIMG = G::AIMG, BHALF = G::BHALF;
   constexpr int DPS = 2 + 2 * NRH;  // DMAs per thread per stage
-  __shared__ __attribute__((aligned(1024))) char smem[NBUF * STG];
+  // the bf16-partial epilogue sums the pixel halves in one pass (4 waves x
+  // (NT x 16 + 1) x 64 floats), which can exceed the stage ring
+  constexpr int RED1 = 4 * (NT * 16 + 1) * 64 * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * STG > RED1 ? NBUF * STG : RED1];
 
   DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2647,30 +2650,66 @@ __global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   DV_STAMP_AT(2);
   accb += __shfl_xor(accb, 32, 64);  // both k-halves of the channel
 
-  // ---- sum the two pixel halves through LDS (two passes over the taps) ----
+  // ---- sum the two pixel halves through LDS in one pass (16-B rows per lane) ----
   float* red = (float*)smem;
+  constexpr int PERW = (NT * 16 + 1) * 64;  // floats per wave
+  if (half == 1) {
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    constexpr int PER = (5 * 16 + 1) * 64;  // <= 5 taps + the bias sums per wave
-    const int d0 = pass == 0 ? 0 : (NT < 5 ? NT : 5), d1 = pass == 0 ? (NT < 5 ? NT : 5) : NT;
-    if (half == 1) {
+    for (int d = 0; d < NT; ++d)
 #pragma unroll
-      for (int d = d0; d < d1; ++d)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) red[wq * PER + ((d - d0) * 16 + e) * 64 + lane] = acc[d][e];
-      if (pass == 0) red[wq * PER + 5 * 16 * 64 + lane] = accb;
-    }
-    __syncthreads();
-    if (half == 0) {
-#pragma unroll
-      for (int d = d0; d < d1; ++d)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[d][e] += red[wq * PER + ((d - d0) * 16 + e) * 64 + lane];
-      if (pass == 0) accb += red[wq * PER + 5 * 16 * 64 + lane];
-    }
-    __syncthreads();
+      for (int e4 = 0; e4 < 4; ++e4)
+        *(f32x4*)(red + wq * PERW + (d * 4 + e4) * 256 + lane * 4) =
+            f32x4{acc[d][4 * e4], acc[d][4 * e4 + 1], acc[d][4 * e4 + 2], acc[d][4 * e4 + 3]};
+    red[wq * PERW + NT * 16 * 64 + lane] = accb;
   }
+  __syncthreads();
+  if (half == 0) {
+#pragma unroll
+    for (int d = 0; d < NT; ++d)
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const f32x4 v = *(const f32x4*)(red + wq * PERW + (d * 4 + e4) * 256 + lane * 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[d][4 * e4 + k] += v[k];
+        __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight (else they all hoist: spills)
+      }
+    accb += red[wq * PERW + NT * 16 * 64 + lane];
+  }
+  __syncthreads();
   DV_STAMP_AT(3);
+  if (gridDim.z > 1 && a.part_bf16) {
+    // ---- bf16 split partials: the four half-0 waves round their 32 x 32 x 9
+    // tiles to bf16 and transpose them into the torch layout in LDS together
+    // (one round), and all 8 waves write the block's 64 x 576 partial as 16-B
+    // stores ----
+    constexpr int TP = 32 * NT;  // bf16 per output channel of a wave tile
+    bf16* tiles = (bf16*)smem;
+    const int r = lane & 31, h = lane >> 5;
+    if (half == 0) {
+      bf16* tb = tiles + wq * 32 * TP;
+#pragma unroll
+      for (int d = 0; d < NT; ++d)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) tb[((e & 3) + 8 * (e >> 2) + 4 * h) * TP + r * NT + d] = (bf16)acc[d][e];
+    }
+    __syncthreads();
+    bf16* dstb = (bf16*)a.part + (long long)blockIdx.z * a.cout * a.K;
+    constexpr int CPR = TP / 8;  // 16-B chunks per output-channel row of a tile
+    for (int idx = threadIdx.x; idx < 4 * 32 * CPR; idx += 512) {
+      const int t4 = idx / (32 * CPR), rem = idx - t4 * (32 * CPR);
+      const int col = rem / CPR, j = rem - col * CPR;
+      const u32x4 v = *(const u32x4*)(tiles + (t4 * 32 + col) * TP + 8 * j);
+      const long long oi = (long long)(co0 + (t4 >> 1) * 32 + col) * a.K + (ci0 + (t4 & 1) * 32) * NT + 8 * j;
+      *(u32x4*)(dstb + oi) = v;
+    }
+#ifdef DV_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    DV_STAMP_AT(4);
+    if (do_bias && half == 0 && lane < 32) a.dbpart[(long long)blockIdx.z * a.cout + co0 + wm * 32 + lane] = accb;
+    return;
+  }
+
   // ---- torch-layout output [co][ci][tap]: each wave's 32 x 32 x 9 tile is
   // transposed through LDS (two tiles per round, 36 KB each) so every output
   // channel's 32 ci x 9 taps go out as 1152 contiguous bytes (float4 stores).
