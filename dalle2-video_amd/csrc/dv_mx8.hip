@@ -176,14 +176,14 @@ __device__ __forceinline__ void dma4s(__amdgpu_buffer_rsrc_t r, void* lds, unsig
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, (int)voff, (int)soff, 0, 0);
 }
 
-template <int W, int NW>
+template <int W, int NW, bool SPLIT = true>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_mx8_kernel(Mx8Args p) {
   constexpr int TP = 32 * NW;
   using G = MxGeom<W, TP>;
   constexpr int BUF = G::BUF, WQ = G::WQ;
   __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6) & (NW - 1);  // masked: piece types fold
   const int npx = (int)(p.M / TP), ncb = p.cout / 64;
   // consecutive blocks (one XCD each, round robin) take the pixel tiles of one
   // output-channel block: an XCD's L2 keeps that block's weights
@@ -244,13 +244,13 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_mx8_kernel(Mx8Args p) {
     } else if (i < NWP + NXP) {
       const int j = i - NWP, k = min(wave + NW * j, G::NDP - 1);
       char* dst = b + G::XOFF + k * 1024;
-      if (first) dma16s(qr0, dst, xo0[j], (unsigned)(cc * 64));
+      if (!SPLIT || first) dma16s(qr0, dst, xo0[j], (unsigned)(cc * 64));
       else dma16s(qr1, dst, xo1[j], (unsigned)(cc * 64));
     } else {
       const int j = i - NWP - NXP, k = min(wave + NW * j, G::NSP - 1);
       char* dst = b + G::SOFF + k * 256;
-      const unsigned sof = (unsigned)((long long)cc * p.M * 4);
-      if (first) dma4s(sr0, dst, so[j], sof);
+      const unsigned sof = (unsigned)(cc * (int)p.M * 4);  // < 2^31: host-checked
+      if (!SPLIT || first) dma4s(sr0, dst, so[j], sof);
       else dma4s(sr1, dst, so[j], sof);
     }
   };
@@ -273,7 +273,10 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_mx8_kernel(Mx8Args p) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[j][0][e] = acc[j][1][e] = 0.f;
 
-  for (int c = 0; c < nch; ++c) {
+  // one chunk; PRE (compile-time): chunk c + 1 exists and is issued here (the
+  // loop is split into the chunks that issue and the last one: no per-piece
+  // branch between the MFMAs)
+  auto chunk = [&](int c, auto PRE) {
     const char* b = smem + (c & 1) * BUF;
     // the lane's A scales of both 32-row halves: 9 tap bytes of K-block h
     unsigned as[2][3];
@@ -301,7 +304,6 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_mx8_kernel(Mx8Args p) {
     };
     rd(0, 0);
     rd(1, 1);
-    const bool pre = c + 1 < nch;
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
       if (d + 2 < 9) rd(d + 2, (d + 2) % 3);
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_mx8_kernel(Mx8Args p) {
       }
       // chunk c + 1's pieces go out in the MFMA shadow (its buffer was last
       // read in chunk c - 1, before the last barrier)
-      if (pre) {
+      if constexpr (decltype(PRE)::value) {
 #pragma unroll
         for (int i = d; i < NPW; i += 9) issue1(c + 1, i);
       }
@@ -325,7 +327,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_mx8_kernel(Mx8Args p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-  }
+  };
+  for (int c = 0; c + 1 < nch; ++c) chunk(c, std::true_type{});
+  if (nch > 0) chunk(nch - 1, std::false_type{});
 
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e; bias and
   // residual loaded for the whole tile before the first store
@@ -389,7 +393,7 @@ struct MxPGeom {
 template <int W, int NCH>
 constexpr int mxp_lds() { return NCH * MX_WIMG + MxPGeom<W>::NWB * MxPGeom<W>::WBUF; }
 
-template <int W, int NCH>
+template <int W, int NCH, bool SPLIT = true>
 __global__ __launch_bounds__(256) void conv_fwd_mx8p_kernel(Mx8Args p, int tiles_per_wg, int wg_per_cb) {
   constexpr int NW = 4, TP = 128;
   using G = MxGeom<W, TP>;
@@ -437,30 +441,42 @@ __global__ __launch_bounds__(256) void conv_fwd_mx8p_kernel(Mx8Args p, int tiles
   const __amdgpu_buffer_rsrc_t sr0 = dma_rsrc(p.s0, (unsigned)(p.M * 4 * nch0));
   const __amdgpu_buffer_rsrc_t qr1 = dma_rsrc(p.q1, (unsigned)(p.M * p.c1));
   const __amdgpu_buffer_rsrc_t sr1 = dma_rsrc(p.s1, (unsigned)(p.M * 4 * (NCH - nch0)));
-  // the window of step s into ring slot s % NWB (piece j of this wave)
-  auto issue1 = [&](int st, int j) {
+  // the window of step s into ring slot s % NWB (piece j of this wave).  The
+  // step's tile row, source and chunk are worked out once per step in 32-bit
+  // arithmetic (M * C < 2^31, host-checked): a 64-bit modulo per DMA piece
+  // was a ~150-instruction scalar division in front of every DMA.
+  struct StepDma {
+    int m0, y0, cc, buf;
+    bool first;
+  };
+  auto step_dma = [&](int st) {
+    StepDma sd;
     const int tile = t0 + st / NCH, c = st % NCH;
-    const long long m0 = (long long)tile * TP;
-    const int y0 = (int)((m0 % HW) / W);
-    char* b = smem + RES + (st % NWB) * WBUF;
-    const bool first = c < nch0;
-    const int cc = first ? c : c - nch0;
+    sd.m0 = tile * TP;
+    sd.y0 = (sd.m0 % HW) / W;
+    sd.first = c < nch0;
+    sd.cc = sd.first ? c : c - nch0;
+    sd.buf = st % NWB;
+    return sd;
+  };
+  auto issue1 = [&](const StepDma& sd, int j) {
+    char* b = smem + RES + sd.buf * WBUF;
     if (j < NXP) {
       const int k = min(wave + NW * j, G::NDP - 1);
-      const int yy = y0 + xwy[j] - 1;
+      const int yy = sd.y0 + xwy[j] - 1;
       const bool ok = (unsigned)yy < (unsigned)p.H;
-      const long long pix = m0 + xoff[j];
-      const unsigned vo = ok ? (unsigned)(pix * (first ? p.c0 : p.c1) + xt[j]) : DMA_OOB;
-      if (first) dma16s(qr0, b + k * 1024, vo, (unsigned)(cc * 64));
-      else dma16s(qr1, b + k * 1024, vo, (unsigned)(cc * 64));
+      const int pix = sd.m0 + xoff[j];
+      const unsigned vo = ok ? (unsigned)(pix * ((!SPLIT || sd.first) ? p.c0 : p.c1) + xt[j]) : DMA_OOB;
+      if (!SPLIT || sd.first) dma16s(qr0, b + k * 1024, vo, (unsigned)(sd.cc * 64));
+      else dma16s(qr1, b + k * 1024, vo, (unsigned)(sd.cc * 64));
     } else {
       const int jj = j - NXP, k = min(wave + NW * jj, G::NSP - 1);
-      const int yy = y0 + swy[jj] - 1;
+      const int yy = sd.y0 + swy[jj] - 1;
       const bool ok = (unsigned)yy < (unsigned)p.H;
-      const unsigned vo = ok ? (unsigned)((m0 + soff[jj]) * 4) : DMA_OOB;
-      const unsigned so = (unsigned)((long long)cc * p.M * 4);
+      const unsigned vo = ok ? (unsigned)((sd.m0 + soff[jj]) * 4) : DMA_OOB;
+      const unsigned so = (unsigned)(sd.cc * (int)p.M * 4);
       char* dst = b + G::NDP * 1024 + k * 256;
-      if (first) dma4s(sr0, dst, vo, so);
+      if (!SPLIT || sd.first) dma4s(sr0, dst, vo, so);
       else dma4s(sr1, dst, vo, so);
     }
   };
@@ -469,8 +485,9 @@ __global__ __launch_bounds__(256) void conv_fwd_mx8p_kernel(Mx8Args p, int tiles
 #pragma unroll
   for (int st = 0; st < NWB - 1; ++st)
     if (st < nsteps) {
+      const StepDma sd = step_dma(st);
 #pragma unroll
-      for (int j = 0; j < NPWX; ++j) issue1(st, j);
+      for (int j = 0; j < NPWX; ++j) issue1(sd, j);
     }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -519,7 +536,8 @@ __global__ __launch_bounds__(256) void conv_fwd_mx8p_kernel(Mx8Args p, int tiles
       for (int e = 0; e < 16; ++e) acc[j][0][e] = acc[j][1][e] = 0.f;
   };
 
-  for (int st = 0; st < nsteps; ++st) {
+  // one step; PRE (compile-time): step st + NWB - 1 exists and is issued here
+  auto step = [&](int st, auto PRE) {
     const int c = st % NCH;
     const bool tile_start = c == 0 && st > 0;
     if (tile_start) epilogue(t0 + st / NCH - 1);  // 8 stores, before this step's DMA
@@ -542,7 +560,9 @@ __global__ __launch_bounds__(256) void conv_fwd_mx8p_kernel(Mx8Args p, int tiles
     };
     rd(0, 0);
     rd(1, 1);
-    const bool pre = st + NWB - 1 < nsteps;
+    constexpr bool pre = decltype(PRE)::value;
+    StepDma sdn;
+    if constexpr (pre) sdn = step_dma(st + NWB - 1);
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
       if (d + 2 < 9) rd(d + 2, (d + 2) % 3);
@@ -555,24 +575,27 @@ __global__ __launch_bounds__(256) void conv_fwd_mx8p_kernel(Mx8Args p, int tiles
         acc[j][d & 1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af, bf, acc[j][d & 1], 0, 0, 0, sa, 0,
                                                                        (int)bs[sl]);
       }
-      if (pre) {
+      if constexpr (pre) {
 #pragma unroll
-        for (int j = d; j < NPWX; j += 9) issue1(st + NWB - 1, j);
+        for (int j = d; j < NPWX; j += 9) issue1(sdn, j);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     // step st + 1's window landed: younger than its DMA are this step's
     // stores (8 when it began a tile) and this step's DMA for st + 2
     if (tile_start) {
-      if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + NPWX) : "memory");
+      if constexpr (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + NPWX) : "memory");
       else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
-      if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPWX) : "memory");
+      if constexpr (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPWX) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-  }
+  };
+  int st = 0;
+  for (; st + NWB - 1 < nsteps; ++st) step(st, std::true_type{});
+  for (; st < nsteps; ++st) step(st, std::false_type{});
   epilogue(t1 - 1);
 }
 
@@ -584,7 +607,8 @@ int launch_mx8p(const Mx8Args& a, hipStream_t st) {
   if (g > npx) g = npx;
   const int per = (npx + g - 1) / g;
   g = (npx + per - 1) / per;
-  conv_fwd_mx8p_kernel<W, NCH><<<ncb * g, 256, 0, st>>>(a, per, g);
+  if (a.c1 > 0) conv_fwd_mx8p_kernel<W, NCH, true><<<ncb * g, 256, 0, st>>>(a, per, g);
+  else conv_fwd_mx8p_kernel<W, NCH, false><<<ncb * g, 256, 0, st>>>(a, per, g);
   return check_launch("conv_fwd_mx8p");
 }
 
@@ -592,7 +616,8 @@ template <int W>
 int launch_mx8(const Mx8Args& a, hipStream_t st) {
   constexpr int NW = MX_NW;
   const int nblk = (int)(a.M / (32 * NW)) * (a.cout / 64);
-  conv_fwd_mx8_kernel<W, NW><<<nblk, NW * 64, 0, st>>>(a);
+  if (a.c1 > 0) conv_fwd_mx8_kernel<W, NW, true><<<nblk, NW * 64, 0, st>>>(a);
+  else conv_fwd_mx8_kernel<W, NW, false><<<nblk, NW * 64, 0, st>>>(a);
   return check_launch("conv_fwd_mx8");
 }
 
