@@ -1993,19 +1993,20 @@ constexpr int F8_WROW = 19;                                // 16-B slots per wei
 // CO output channels per tile: 64 (two 32x32 accumulators per wave), or 32
 // for the grids that would leave CUs idle (M = 4,096 at 256 channels: 128
 // tiles of 64 channels for 256 CUs)
-template <int W, int CO = 64>
+template <int W, int CO = 64, int NWV = 4>
 struct FwGeom {
+  static constexpr int CG = CO * (NWV / 4);                  // channels per workgroup
   static constexpr int NF = W == 8 ? 2 : 1;                  // frames per tile
   static constexpr int NWR = W == 8 ? 10 : 128 / W + 2;      // window rows per frame
   static constexpr int WQ = W == 8 ? 12 : W + 2;             // pixel slots per window row
   static constexpr int FPIX = NWR * WQ;                      // window pixels per frame
   static constexpr int WPIX = NF * FPIX;
   static constexpr int XPIECES = (WPIX * 3 + 63) / 64;
-  static constexpr int WPC = (CO * F8_WROW + 63) / 64;       // CO weight rows x 19 slots
+  static constexpr int WPC = (CG * F8_WROW + 63) / 64;       // CG weight rows x 19 slots
   static constexpr int PIECES = WPC + XPIECES;
-  static constexpr int NPW = (PIECES + 3) / 4;
+  static constexpr int NPW = (PIECES + NWV - 1) / NWV;
   static constexpr int BUF = PIECES * 1024;
-  static constexpr int NBUF = 5 * BUF <= 160 * 1024 - 1024 ? 5 : 4;
+  static constexpr int NBUF = (160 * 1024 - 1024) / BUF >= 5 ? 5 : (160 * 1024 - 1024) / BUF;
 };
 
 // lane r -> pixel (row * W + col) of the wave's 32-pixel tile so that the
@@ -2024,16 +2025,23 @@ __device__ __forceinline__ int fw_pix(int r) {
   else return (ga ? 0 : 16) + a;
 }
 
-template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true>
-__global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
-  using G = FwGeom<W, CO>;
+// NWV = 8: a 128-pixel x 2*CO-channel tile per workgroup, waves 4-7 on the
+// second channel half (the pixel window is staged once for both halves): for
+// the grids whose CO-channel tiles would run in two rounds on the 256 CUs.
+template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
+  using G = FwGeom<W, CO, NWV>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
-  constexpr int WPC = G::WPC, NJ = CO / 32;
+  constexpr int WPC = G::WPC, NJ = CO / 32, CG = G::CG;
+  static_assert(NWV == 4 || (NWV == 8 && !STATS), "the 8-wave tile has no statistics epilogue");
+  static_assert(NPW <= 9, "one DMA piece per tap");
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
   DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6) & 3;  // & 3: the DMA piece type folds per (wave, i)
-  const int npx = (int)(p.M / 128), nblk = npx * (p.cout / CO);
+  // masked: the DMA piece type folds per (wave, i) at compile time
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6) & (NWV - 1);
+  const int wq = wave & 3, chh = wave >> 2;  // pixel sub-tile, channel half
+  const int npx = (int)(p.M / 128), nblk = npx * (p.cout / CG);
   int L = blockIdx.x;
   int co0;
   long long m0;
@@ -2041,12 +2049,12 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     // XCD x = block % 8 takes channel group x / xp and pixel group x % xp: its
     // L2 holds 1/xc of the weights and 1/xp of the input (host-checked splits)
     const int xc = p.xcd_c, xp = 8 / xc, x = L % 8, j = L / 8;
-    const int tpc = (p.cout / CO) / xc, ppg = npx / xp;
-    co0 = ((x / xp) * tpc + j / ppg) * CO;
+    const int tpc = (p.cout / CG) / xc, ppg = npx / xp;
+    co0 = ((x / xp) * tpc + j / ppg) * CG;
     m0 = (long long)((x % xp) * ppg + j % ppg) * 128;
   } else {
     if (nblk % 8 == 0) L = (L % 8) * (nblk / 8) + L / 8;  // consecutive blocks share an XCD
-    co0 = (L / npx) * CO;
+    co0 = (L / npx) * CG;
     m0 = (long long)(L % npx) * 128;
   }
   const int nch = p.cin / 16;
@@ -2059,12 +2067,12 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   unsigned voff0[NPW], voff1[NPW];
 #pragma unroll
   for (int i = 0; i < NPW; ++i) {
-    const int k = min(wave + 4 * i, PIECES - 1);
+    const int k = min(wave + NWV * i, PIECES - 1);
     voff0[i] = voff1[i] = DMA_OOB;
     if (k < WPC) {
       // chunk-major packed row (mode 2/3): [cin / 16][9 taps][16]; slot c = 2 tap + half
       const int slot = k * 64 + lane, row = slot / F8_WROW, c = slot - row * F8_WROW;
-      if (c < 18 && row < CO) voff0[i] = (unsigned)((((long long)co0 + row) * p.K + c * 8) * 2);
+      if (c < 18 && row < CG) voff0[i] = (unsigned)((((long long)co0 + row) * p.K + c * 8) * 2);
     } else {
       const int slot = (k - WPC) * 64 + lane, px = slot / 3, s = slot - px * 3;
       const int f = px / G::FPIX, rem = px - f * G::FPIX, wy = rem / WQ, wx = rem - wy * WQ;
@@ -2085,7 +2093,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
     const int ci0 = c * 16;
     const bool first = ci0 < p.c0;
     char* b = smem + (c % NBUF) * BUF;
-    const int k = min(wave + 4 * i, PIECES - 1);
+    const int k = min(wave + NWV * i, PIECES - 1);
     if (k < WPC) dma16s(wr, b + k * 1024, voff0[i], (unsigned)ci0 * 18);
     else if (!SPLIT || first) dma16s(xr0, b + k * 1024, voff0[i], (unsigned)ci0 * 2);
     else dma16s(xr1, b + k * 1024, voff1[i], (unsigned)(ci0 - p.c0) * 2);
@@ -2110,11 +2118,11 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
 
   const int r = lane & 31, h = lane >> 5;
   const int pix = fw_pix<W>(r);                    // within the wave's 32 pixels
-  const int tpx = wave * 32 + pix;                 // within the 128-pixel tile
+  const int tpx = wq * 32 + pix;                   // within the 128-pixel tile
   const int wb = W == 8 ? (tpx >> 6) * G::FPIX + ((tpx & 63) >> 3) * WQ + (tpx & 7)
                         : (tpx / W) * WQ + tpx % W;  // window pixel of tap (0, 0)
   const int bofs = WPC * 1024 + (wb * 3 + h) * 16;
-  const int aofs = r * (F8_WROW * 16) + h * 16;
+  const int aofs = (chh * CO + r) * (F8_WROW * 16) + h * 16;
   // two accumulator chains per channel half (even / odd taps): four
   // independent MFMA chains, summed in the epilogue
   f32x16 acc0, acc1, acc2, acc3;
@@ -2193,6 +2201,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
   // retires loads and stores in order: a load behind a store waits for the
   // write, one round trip per group when they interleaved)
   const long long m = m0 + tpx;
+  const int cw = co0 + chh * CO;  // this wave's first output channel
   float sv[STATS ? CO : 1];  // STATS: [0,CO/2) sums, [CO/2,CO) squares of the lane's CO/2 channels
   f32x4 bb[NJ][4];
   u32x2 rq[NJ][4];
@@ -2200,19 +2209,19 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) bb[j][g] = *(const f32x4*)(p.bias + co0 + 32 * j + 8 * g + 4 * h);
+      for (int g = 0; g < 4; ++g) bb[j][g] = *(const f32x4*)(p.bias + cw + 32 * j + 8 * g + 4 * h);
   }
   if (p.res) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) rq[j][g] = *(const u32x2*)(p.res + m * p.ldres + co0 + 32 * j + 8 * g + 4 * h);
+      for (int g = 0; g < 4; ++g) rq[j][g] = *(const u32x2*)(p.res + m * p.ldres + cw + 32 * j + 8 * g + 4 * h);
   }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const int n = co0 + 32 * j + 8 * g + 4 * h;
+      const int n = cw + 32 * j + 8 * g + 4 * h;
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = j ? acc1[4 * g + e] + acc3[4 * g + e] : acc0[4 * g + e] + acc2[4 * g + e];
@@ -2287,8 +2296,18 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   // 32-channel tiles when 64-channel ones leave CUs idle (DV_FRAME_CO32=0: off)
   static const bool co32_ok = !(getenv("DV_FRAME_CO32") && atoi(getenv("DV_FRAME_CO32")) == 0);
   const int co = co32_ok && (a.M / 128) * (a.cout / 64) <= 128 ? 32 : 64;
-  a.xcd_c = frame_xcd_split(a, co);
-  const int nblk = (int)(a.M / 128) * (a.cout / co);
+  // 8 waves on 128 channels for the 16-wide frames whose 64-channel tiles
+  // would take two rounds of the 256 CUs (DV_FRAME_W8=0: off)
+  static const bool w8_ok = !(getenv("DV_FRAME_W8") && atoi(getenv("DV_FRAME_W8")) == 0);
+  const bool w8 = w8_ok && a.W == 16 && co == 64 && !a.gn_sums && a.cout % 128 == 0 &&
+                  (a.M / 128) * (a.cout / 64) > 256;
+  a.xcd_c = frame_xcd_split(a, w8 ? 128 : co);
+  const int nblk = (int)(a.M / 128) * (a.cout / (w8 ? 128 : co));
+  if (w8) {
+    if (a.c0 < a.cin) conv_fwd_frame_kernel<16, false, 3, 1, 64, true, 8><<<nblk, 512, 0, st>>>(a);
+    else conv_fwd_frame_kernel<16, false, 3, 1, 64, false, 8><<<nblk, 512, 0, st>>>(a);
+    return check_launch("conv_fwd_frame");
+  }
   // fragment prefetch distance PF = 3 taps and DEFER (the last tap's MFMAs
   // after the chunk barrier): same-box per-launch A/B (tools/frame_ab.py,
   // profiles/r03_frame_ab.txt) put PF 3 + DEFER 1 1-3 % ahead of PF 2 without
