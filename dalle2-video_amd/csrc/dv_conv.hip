@@ -602,24 +602,32 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p,
     __builtin_amdgcn_s_barrier();
     const char* sB = smem + buf * BUF;
     const char* sA = sB + BM * 128;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    // fragments of k-step s + 1 are read before the MFMAs of k-step s (with
+    // the reads issued just ahead of their own MFMAs every k-step exposed the
+    // LDS latency)
+    u32x4 wa[2][TJ], xb[2][TI];
+    auto rd = [&](int s, int sl) {
       const int c = 2 * s + h;
-      u32x4 wa[TJ], xb[TI];
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int row = wn * 32 * TJ + 32 * j + r;
-        wa[j] = *(const u32x4*)(sA + row * 128 + ((c ^ swz8(row)) << 4));
+        wa[sl][j] = *(const u32x4*)(sA + row * 128 + ((c ^ swz8(row)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int row = wm * 32 * TI + 32 * i + r;
-        xb[i] = *(const u32x4*)(sB + row * 128 + ((c ^ swz8(row)) << 4));
+        xb[sl][i] = *(const u32x4*)(sB + row * 128 + ((c ^ swz8(row)) << 4));
       }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s + 1 < 4) rd(s + 1, (s + 1) & 1);
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int i = 0; i < TI; ++i) acc[j][i] = Mma<bf16>::run(wa[j], xb[i], acc[j][i]);
+        for (int i = 0; i < TI; ++i) acc[j][i] = Mma<bf16>::run(wa[s & 1][j], xb[s & 1][i], acc[j][i]);
+      __builtin_amdgcn_sched_barrier(0);
     }
     // every wave's reads of `buf` are done before the next iteration re-fills it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
