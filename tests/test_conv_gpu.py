@@ -140,3 +140,35 @@ def test_stripe_wgrad_bf16_partials(case, parity_log):
     parity_log(config=f"stripe wgrad bf16 partials {case}", dw_rel=err)
     # one bf16 rounding is 2^-9 relative at most, 1.1e-3 rms
     assert err < 2.5e-3, err
+
+
+def test_batched_repack_matches_single_packs():
+    """PackCache.refresh (one flat-tile launch over every cached image) writes the
+    same bytes as packing each weight alone, for both layouts and both dtypes,
+    a row-tiled 1x1 / 3x3 mix and an entry larger than the rest."""
+    from dalle2_video import ops
+    shapes = [(64, 64, 3), (512, 768, 3), (3, 64, 3), (128, 256, 1), (40, 24, 3), (256, 256, 1), (16, 8, 15)]
+    cache = ops.PackCache()
+    cache.enabled = True
+    g = torch.Generator(device="cuda").manual_seed(3)
+    wts, imgs = [], []
+    for co, ci, k in shapes:
+        w = torch.randn(co, ci, 1, k, k, device="cuda", generator=g)
+        wts.append(w)
+        for dtype in (torch.bfloat16, torch.float32):
+            for mode in (0, 1, 2, 3):
+                if k == 15 and mode >= 2:
+                    continue
+                pad = ((ci if mode % 2 == 0 else co) + 15) // 16 * 16
+                out, stale = cache.lookup(w, w, dtype, co, ci, k, pad, mode)
+                assert stale
+                imgs.append((w, dtype, pad, mode, out))
+    for w in wts:  # new weights, then one batched repack
+        w.copy_(torch.randn(w.shape, device="cuda", generator=g))
+    cache.refresh()
+    torch.cuda.synchronize()
+    for w, dtype, pad, mode, out in imgs:
+        ref = ops.pack_conv_weight(w, dtype, pad, mode, cache=False)
+        assert torch.equal(out.view(torch.int16) if dtype == torch.bfloat16 else out.view(torch.int32),
+                           ref.view(torch.int16) if dtype == torch.bfloat16 else ref.view(torch.int32)), \
+            (tuple(w.shape), dtype, mode)
