@@ -84,7 +84,11 @@ def frame_case(nf, h, w, cin, cout):
     f()
     m = nf * h * w
     co = 32 if (m // 128) * (cout // 64) <= 128 else 64
-    report(f"frame fwd ({nf},{h},{w}) {cin}->{cout} co{co}", stamps((m // 128) * (cout // co)), [0, 1, 2, 4])
+    # 8 waves on 128 channels where 64-channel tiles would take two rounds (dv_conv.hip, DV_FRAME_W8)
+    w8 = w == 16 and co == 64 and cout % 128 == 0 and (m // 128) * (cout // 64) > 256
+    cw = 128 if w8 else co
+    report(f"frame fwd ({nf},{h},{w}) {cin}->{cout} {'8 waves x ' if w8 else ''}co{cw}",
+           stamps((m // 128) * (cout // cw)), [0, 1, 2, 4])
 
 
 for shp in [(64, 64, 64, 64, 64), (64, 32, 32, 128, 128), (64, 16, 16, 256, 256), (64, 8, 8, 512, 512)]:
