@@ -2490,6 +2490,9 @@ struct WgradSArgs {
   int seg, nseg;  // image rows per window segment, segments per stage
 };
 
+#ifndef DV_WG1_NBUF
+#define DV_WG1_NBUF 2
+#endif
 template <int W, int KS> struct StripeGeom {
   static constexpr int WP = W + 2;
   // window rows (max over H): KS == 1 stages the 128 pixels themselves
@@ -2498,7 +2501,10 @@ template <int W, int KS> struct StripeGeom {
   static constexpr int AIMG = 2 * 128 * 64;                     // dY image: 2 co halves x 128 rows x 64 B
   static constexpr int BHALF = NRH * 128 * 64;                  // window image of one ci half
   static constexpr int STG = AIMG + 2 * BHALF;
-  static constexpr int NBUF = STG * 3 <= 160 * 1024 ? 3 : 2;
+  // 1x1: a 2-deep ring (64 KB) so that two workgroups share a CU -- a stage
+  // holds one tap's MFMAs only, too little to cover the next stage's DMA
+  // latency inside one workgroup
+  static constexpr int NBUF = KS == 1 ? DV_WG1_NBUF : (STG * 3 <= 160 * 1024 ? 3 : 2);
   static constexpr int NT = KS * KS;                            // taps
 };
 
@@ -2507,7 +2513,7 @@ template <int W, int KS> struct StripeGeom {
 // conflict-free WITHOUT a swizzle, and an operand address is linear in the
 // row — every tap's window offset folds into the ds_read immediate.
 template <int W, int KS>
-__global__ __launch_bounds__(512) void conv_wgrad_stripe_kernel(WgradSArgs a) {
+__global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   using G = StripeGeom<W, KS>;
   constexpr int WP = G::WP, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF, NT = G::NT;
   constexpr int AIMG = G::AIMG, BHALF = G::BHALF;
@@ -2988,10 +2994,11 @@ bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout
 // split count: ~256 workgroups (one per CU: the stage ring takes up to 147 KB
 // of LDS).  Capping the splits by stages or by partial bytes was measured
 // slower on every Cfg2 shape (tools/ab_fwd.sh): occupancy wins.
-inline void stripe_split(int nstages, int grid_xy, long long grad_floats, int& sps, int& S) {
+inline void stripe_split(int nstages, int grid_xy, long long grad_floats, int ks, int& sps, int& S) {
   (void)grad_floats;
   static const int minst = getenv("DV_WG_MINST") ? atoi(getenv("DV_WG_MINST")) : 1;  // A/B knob
-  long long want = 256 / grid_xy;
+  // 1x1 with the 2-deep ring: two workgroups per CU
+  long long want = (ks == 1 && DV_WG1_NBUF == 2 ? 512 : 256) / grid_xy;
   if (minst > 1 && want > nstages / minst) want = nstages / minst;
   if (want > nstages) want = nstages;
   if (want < 1) want = 1;
@@ -3009,7 +3016,7 @@ inline bool stripe_part_bf16() {
 long long wgrad_stripe_ws(int nf, int h, int w, int cin, int cout, int ks) {
   const int nstages = (int)((long long)nf * h * w / 128);
   int sps, S;
-  stripe_split(nstages, (cout / 64) * (cin / 64), (long long)cout * ks * ks * cin, sps, S);
+  stripe_split(nstages, (cout / 64) * (cin / 64), (long long)cout * ks * ks * cin, ks, sps, S);
   const long long wpart = (long long)S * cout * ks * ks * cin;  // cout % 64 == 0: even
   return (stripe_part_bf16() ? wpart / 2 : wpart) + (long long)S * cout;
 }
@@ -3026,7 +3033,7 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   if (ks == 3) stripe_geom(h, w, a.seg, a.nseg);
   a.nstages = (int)((long long)nf * h * w / 128);
   int S;
-  stripe_split(a.nstages, (cout / 64) * (cin / 64), (long long)cout * a.K, a.stages_per_split, S);
+  stripe_split(a.nstages, (cout / 64) * (cin / 64), (long long)cout * a.K, ks, a.stages_per_split, S);
   a.part = ws;
   a.part_bf16 = S > 1 && stripe_part_bf16();
   a.dbpart = db ? ws + (long long)S * cout * a.K / (a.part_bf16 ? 2 : 1) : nullptr;
