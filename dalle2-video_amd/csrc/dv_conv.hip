@@ -1073,7 +1073,10 @@ __device__ __forceinline__ int img_off(int row, int ch) {
   return row * RB + ((ch ^ x) << 4);
 }
 
-template <int BMC, int BNK>
+// K1: 1x1 (ks == 1: the 1x1 wgrads and the batched token GEMMs) -- a B row is
+// the pixel itself, so the per-DMA (frame, row, column) divisions and the
+// window bounds test drop out of the stage loop (PMC: 31-36 VALU per MFMA)
+template <int BMC, int BNK, bool K1>
 __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
   constexpr int BP = 64;
   constexpr int RA = BMC * 2, RB = BNK * 2;  // row bytes
@@ -1125,10 +1128,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
   const int chb = b_slot ^ b_x;
   const int n = nk0 + 8 * chb;
   const bool b_ok = n < p.K;
-  const int tap = b_ok ? (int)fdiv((unsigned)n, p.fd_cin) : 0;
+  const int tap = K1 ? 0 : (b_ok ? (int)fdiv((unsigned)n, p.fd_cin) : 0);
   const int ci = n - tap * p.cin;
-  const int ty = b_ok ? (int)fdiv((unsigned)tap, p.fd_ks) : 0;
-  const int dy = ty - pad, dx = tap - ty * p.ks - pad;
+  const int ty = K1 ? 0 : (b_ok ? (int)fdiv((unsigned)tap, p.fd_ks) : 0);
+  const int dy = K1 ? 0 : ty - pad, dx = K1 ? 0 : tap - ty * p.ks - pad;
   const bool first = ci < p.c0;
   const bf16* b_src = first ? px0 + ci : px1 + (ci - p.c0);
   const int b_ld = first ? ld0 : ld1;
@@ -1150,11 +1153,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
     for (int i = 0; i < GB; ++i) {
       const int row = (4 * i + wave) * RPI_B + b_lrow;
       const int m = pb + row;
-      const int f = (int)fdiv((unsigned)m, p.fd_hw);
-      const int rem = m - f * p.H * p.W;
-      const int y = (int)fdiv((unsigned)rem, p.fd_w);
-      const int xx = rem - y * p.W + dx, yy = y + dy;
-      const bool in = b_ok && m < pend && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      bool in = b_ok && m < pend;
+      if (!K1) {
+        const int f = (int)fdiv((unsigned)m, p.fd_hw);
+        const int rem = m - f * p.H * p.W;
+        const int y = (int)fdiv((unsigned)rem, p.fd_w);
+        const int xx = rem - y * p.W + dx, yy = y + dy;
+        in = in && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      }
       const bf16* src = in ? b_src + (m + doff) * b_ld : zero_src(tid + 97u * blockIdx.x + 31u * i + 512u);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sB + (4 * i + wave) * 1024),
@@ -1281,7 +1287,8 @@ int launch_wgrad_glds(WgradGArgs a, hipStream_t st) {
   a.pix_per_split = (int)per;
   a.zper = (int)splits;
   if (a.ngemm > 1) splits *= (unsigned)a.ngemm;
-  conv_wgrad_glds_kernel<BMC, BNK><<<dim3(mt, nt, splits), 256, 0, st>>>(a);
+  if (a.ks == 1) conv_wgrad_glds_kernel<BMC, BNK, true><<<dim3(mt, nt, splits), 256, 0, st>>>(a);
+  else conv_wgrad_glds_kernel<BMC, BNK, false><<<dim3(mt, nt, splits), 256, 0, st>>>(a);
   return check_launch("conv_wgrad_glds");
 }
 
