@@ -46,20 +46,22 @@ __global__ void cl_to_ncthw_kernel(const T* y, int ld, float* x, int B, int C, i
   }
 }
 
-// unit = (frame, low-res y, x, group of VEC high-res channels)
+// unit = (frame, low-res y, x, group of VEC high-res channels); grid y walks the
+// low-res rows (f, y), grid x a row's (x, channel group) units: one 32-bit
+// division per unit (a flat 64-bit index took four 64-bit divisions, each a
+// ~150-instruction sequence, and left the pass VALU-bound)
 template <typename T, int MODE>
 __global__ void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* z, int ldz, int nf,
                                int H, int W, int C, int act) {
   constexpr int VEC = 16 / sizeof(T);
   const int cg = C / VEC;
-  const long long total = (long long)nf * H * W * cg;
-  GRID_STRIDE(idx, total) {
-    const int g = (int)(idx % cg);
-    const long long lp = idx / cg;  // low-res pixel
-    const int x = (int)(lp % W);
-    const long long fy = lp / W;
-    const int y = (int)(fy % H);
-    const long long f = fy / H;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= W * cg) return;
+  const int x = t / cg, g = t - x * cg;
+  for (int row = blockIdx.y; row < nf * H; row += gridDim.y) {
+    const long long f = row / H;
+    const int y = row - (int)f * H;
+    const long long lp = (long long)row * W + x;  // low-res pixel
     const int c0 = g * VEC;
     float lo[4 * VEC];  // low-res span, element (c - c0)*4 + i*2 + j
     if (MODE == 1) {
@@ -667,14 +669,16 @@ extern "C" int dv_shuffle(int dtype, int mode, const void* src, int lds, void* d
   const int VEC = dtype == DV_BF16 ? 8 : 4;
   DV_REQUIRE(C % VEC == 0 && lds % VEC == 0 && ldd % VEC == 0 && (!z || ldz % VEC == 0),
              "channels / strides must be multiples of 16 bytes");
-  const long long units = (long long)nf * H * W * (C / VEC);
+  if ((long long)nf * H * W * C == 0) return DV_OK;
+  DV_REQUIRE((long long)W * (C / VEC) < (1ll << 31) && (long long)nf * H < (1ll << 31), "shape too large");
+  const dim3 grid((unsigned)((W * (C / VEC) + 255) / 256), (unsigned)std::min(nf * H, 65535));
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DV_F32) {
-    if (mode == 0) shuffle_kernel<float, 0><<<grid_for(units), 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, nf, H, W, C, act);
-    else shuffle_kernel<float, 1><<<grid_for(units), 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, nf, H, W, C, act);
+    if (mode == 0) shuffle_kernel<float, 0><<<grid, 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, nf, H, W, C, act);
+    else shuffle_kernel<float, 1><<<grid, 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, nf, H, W, C, act);
   } else {
-    if (mode == 0) shuffle_kernel<bf16, 0><<<grid_for(units), 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, nf, H, W, C, act);
-    else shuffle_kernel<bf16, 1><<<grid_for(units), 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, nf, H, W, C, act);
+    if (mode == 0) shuffle_kernel<bf16, 0><<<grid, 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, nf, H, W, C, act);
+    else shuffle_kernel<bf16, 1><<<grid, 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, nf, H, W, C, act);
   }
   return check_launch("shuffle");
 }
