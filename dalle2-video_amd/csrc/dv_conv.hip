@@ -1512,6 +1512,76 @@ __global__ __launch_bounds__(256) void pack_weight_batched_kernel(const DvPackEn
   for (int t = blockIdx.x; t < pack_tiles(e); t += gridDim.x) pack_tile(e, t, sm);
 }
 
+// Both images of a bf16 3x3 weight from one staged (64 co) x (16 ci) x 9 tile:
+// the forward rows co0..co0+63 (16 input channels each) and the dgrad rows
+// ci0..ci0+15 (64 output channels each) -- the f32 weight is read once, not
+// once per image, and a tile is 36 KB (the per-image forward tile of a
+// 512-channel weight held one 18 KB row)
+constexpr int PP_CO = 64, PP_CI = 16, PP_T = 9, PP_SROW = PP_CI * PP_T + 1;
+__global__ __launch_bounds__(256) void pack_pair_kernel(const DvPackPair* table, const int* tile_entry) {
+  __shared__ float sm[PP_CO * PP_SROW];
+  const int tid = threadIdx.x;
+  const int ei = tile_entry[blockIdx.x];
+  const DvPackPair e = table[ei];
+  const int t = (int)(blockIdx.x - e.tile0);
+  const int nci = e.cin / PP_CI;
+  const int co0 = (t / nci) * PP_CO, ci0 = (t - (t / nci) * nci) * PP_CI;
+  constexpr int SEG = PP_CI * PP_T;  // 144 contiguous floats per co row
+  const float* src = e.w + ((long long)co0 * e.cin + ci0) * PP_T;
+  const long long rstride = (long long)e.cin * PP_T;
+  // 64 x 144 floats, 9 loads in flight per lane (index clamped: unconditional loads)
+  constexpr int N = PP_CO * SEG, U = 9;
+  for (int i0 = tid; i0 < N; i0 += 256 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + 256 * u, N - 1);
+      const int r = i / SEG, j = i - r * SEG;
+      v[u] = src[r * rstride + j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 256 * u;
+      if (i < N) {
+        const int r = i / SEG, j = i - r * SEG;
+        sm[r * PP_SROW + j] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  const int mf = e.modes & 255, md = e.modes >> 8;
+  // forward image: row co, tap, 8 input channels per 16-B store
+  {
+    bf16* out = (bf16*)e.out_fwd;
+    const long long orow = (long long)PP_T * e.cin;
+    for (int idx = tid; idx < PP_CO * PP_T * 2; idx += 256) {
+      const int co = idx / (PP_T * 2), rem = idx - co * (PP_T * 2);
+      const int tap = rem >> 1, h8 = (rem & 1) * 8;
+      const float* r = sm + co * PP_SROW + h8 * PP_T + tap;
+      const long long o = (long long)(co0 + co) * orow +
+                          (mf == 2 ? (ci0 / 16) * (PP_T * 16) + tap * 16 + h8 : (long long)tap * e.cin + ci0 + h8);
+      *(bf16x8*)(out + o) = bf16x8{(bf16)r[0], (bf16)r[PP_T], (bf16)r[2 * PP_T], (bf16)r[3 * PP_T],
+                                   (bf16)r[4 * PP_T], (bf16)r[5 * PP_T], (bf16)r[6 * PP_T], (bf16)r[7 * PP_T]};
+    }
+  }
+  // dgrad image: row ci, flipped tap, 8 output channels per 16-B store
+  {
+    bf16* out = (bf16*)e.out_dgrad;
+    const long long orow = (long long)PP_T * e.cout;
+    for (int idx = tid; idx < PP_CI * PP_T * (PP_CO / 8); idx += 256) {
+      const int ci = idx / (PP_T * 8), rem = idx - ci * (PP_T * 8);
+      const int tpd = rem >> 3, g8 = rem & 7;
+      const float* r = sm + (g8 * 8) * PP_SROW + ci * PP_T + (PP_T - 1 - tpd);
+      const int co = co0 + g8 * 8;
+      const long long o = (long long)(ci0 + ci) * orow +
+                          (md == 3 ? (co >> 4) * (PP_T * 16) + tpd * 16 + (co & 15) : (long long)tpd * e.cout + co);
+      *(bf16x8*)(out + o) = bf16x8{(bf16)r[0], (bf16)r[PP_SROW], (bf16)r[2 * PP_SROW], (bf16)r[3 * PP_SROW],
+                                   (bf16)r[4 * PP_SROW], (bf16)r[5 * PP_SROW], (bf16)r[6 * PP_SROW],
+                                   (bf16)r[7 * PP_SROW]};
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void bias_grad_kernel(const T* dy, int lddy, float* db,
                                                         long long npix, int c, long long rows_per) {
@@ -3226,6 +3296,14 @@ extern "C" int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, lon
   if (bx > 128) bx = 128;
   pack_weight_batched_kernel<<<dim3((unsigned)bx, (unsigned)n), 256, 0, (hipStream_t)stream>>>(table);
   return check_launch("pack_conv_weights_batched");
+}
+
+extern "C" int dv_pack_conv_weight_pairs(const DvPackPair* table, const int* tile_entry, long long total_tiles,
+                                         void* stream) {
+  DV_REQUIRE(table && tile_entry && total_tiles >= 0 && total_tiles < (1ll << 31), "bad table");
+  if (total_tiles == 0) return DV_OK;
+  pack_pair_kernel<<<(unsigned)total_tiles, 256, 0, (hipStream_t)stream>>>(table, tile_entry);
+  return check_launch("pack_conv_weight_pairs");
 }
 
 extern "C" int dv_bias_grad(int dtype, const void* dy, int lddy, float* db, long long npix, int c,

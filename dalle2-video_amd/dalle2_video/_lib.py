@@ -54,6 +54,7 @@ _SIGS = {
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
     "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "dv_pack_conv_weights_batched": [_P, _I, _L, _P],
+    "dv_pack_conv_weight_pairs": [_P, _P, _L, _P],
     "dv_gn_fwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P, _L,
                   _I, _P],
     "dv_gn_fwd_mx8": [_P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P, _L, _I, _P, _P, _P],

@@ -559,19 +559,64 @@ class PackCache:
         ents = list(self.entries.values())
         dev = ents[0]["out"].device
         if self._table_key is None or self._table is None:
+            pairs, rest = self._pair(ents)
             rows = []
-            for e in ents:
+            for e in rest:
                 cout, cin, taps, pad_to, mode = e["meta"]
                 dtc = _lib.DV_BF16 if e["out"].dtype == torch.bfloat16 else _lib.DV_F32
                 rows.append((e["w"].data_ptr(), e["out"].data_ptr(), dtc, cout, cin, taps, pad_to, mode))
             raw = torch.tensor([[a, b, (c | (d << 32)), (f | (g << 32)), (h | (m << 32))]
-                                for a, b, c, d, f, g, h, m in rows], dtype=torch.int64)
+                                for a, b, c, d, f, g, h, m in rows], dtype=torch.int64).reshape(-1, 5)
             self._table = raw.to(dev)
             self._table_key = True
-            self._max = max(e["out"].numel() for e in ents)
-        call("dv_pack_conv_weights_batched", ptr(self._table), len(ents), self._max, stream())
+            self._nrest = len(rest)
+            self._max = max((e["out"].numel() for e in rest), default=0)
+            # pairs: DvPackPair rows (w, out_fwd, out_dgrad, cout | cin << 32, taps | modes << 32, tile0)
+            prow, tmap, t0 = [], [], 0
+            for i, (ef, ed) in enumerate(pairs):
+                cout, cin = ef["meta"][0], ef["meta"][1]
+                n = (cout // 64) * (cin // 16)
+                modes = ef["meta"][4] | (ed["meta"][4] << 8)
+                prow.append([ef["w"].data_ptr(), ef["out"].data_ptr(), ed["out"].data_ptr(),
+                             cout | (cin << 32), 9 | (modes << 32), t0])
+                tmap.append(torch.full((n,), i, dtype=torch.int32))
+                t0 += n
+            self._pairs = torch.tensor(prow, dtype=torch.int64).reshape(-1, 6).to(dev)
+            self._tmap = torch.cat(tmap).to(dev) if tmap else None
+            self._ntiles = t0
+        if self._nrest:
+            call("dv_pack_conv_weights_batched", ptr(self._table), self._nrest, self._max, stream())
+        if self._ntiles:
+            call("dv_pack_conv_weight_pairs", ptr(self._pairs), ptr(self._tmap), self._ntiles, stream())
         for e in ents:
             e["epoch"] = self.epoch
+
+    @staticmethod
+    def _pair(ents):
+        """(forward, dgrad) entry pairs of the bf16 3x3 weights that
+        dv_pack_conv_weight_pairs packs from one read of the weight
+        (cout % 64 == 0, cin % 16 == 0, unpadded rows, exactly one image of
+        each kind), and the rest.  DV_PACK_PAIRS=0: no pairs (A/B)."""
+        if os.environ.get("DV_PACK_PAIRS", "1") == "0":
+            return [], ents
+        by_w = {}
+        for e in ents:
+            by_w.setdefault(e["w"].data_ptr(), []).append(e)
+        pairs, rest = [], []
+        for group in by_w.values():
+            f = [e for e in group if e["meta"][4] in (0, 2)]
+            d = [e for e in group if e["meta"][4] in (1, 3)]
+            ok = len(f) == 1 and len(d) == 1 and len(group) == 2
+            if ok:
+                (cout, cin, taps, padf, _), padd = f[0]["meta"], d[0]["meta"][3]
+                ok = (taps == 9 and cout % 64 == 0 and cin % 16 == 0 and padf == cin and padd == cout
+                      and f[0]["out"].dtype == torch.bfloat16 and d[0]["out"].dtype == torch.bfloat16
+                      and d[0]["meta"][:3] == (cout, cin, taps) and f[0]["w"].is_contiguous())
+            if ok:
+                pairs.append((f[0], d[0]))
+            else:
+                rest.extend(group)
+        return pairs, rest
 
     def clear(self):
         self.entries.clear()

@@ -218,6 +218,21 @@ typedef struct {
 int dv_pack_conv_weights_batched(const DvPackEntry* table, int n, long long max_elems,
                                  void* stream);
 
+/* Both images of each bf16 3x3 weight from ONE read of it: the forward image
+ * (mode 0 or 2, pad = cin) and the dgrad image (mode 1 or 3, pad = cout),
+ * cout % 64 == 0, cin % 16 == 0.  Tile t of entry e is (64 co) x (16 ci);
+ * entries own consecutive tile ranges starting at tile0, and `tile_entry`
+ * (DEVICE, total_tiles ints) maps every tile to its entry.                 */
+typedef struct {
+  const float* w;   /* f32 torch weight (cout, cin, 1, 3, 3) */
+  void* out_fwd;    /* bf16 image, mode = modes & 255 (0 or 2) */
+  void* out_dgrad;  /* bf16 image, mode = modes >> 8 (1 or 3) */
+  int cout, cin, taps, modes;
+  long long tile0;
+} DvPackPair;
+int dv_pack_conv_weight_pairs(const DvPackPair* table, const int* tile_entry, long long total_tiles,
+                              void* stream);
+
 /* ---- grouped small linears ------------------------------------------------
  * Many nn.Linear layers over the SAME f32 input rows x [B][K] in ONE launch:
  * y_e [B][n_e] = act_in(x) W_e^T (+ bias_e) for every entry e.  Serves the

@@ -172,3 +172,33 @@ def test_batched_repack_matches_single_packs():
         assert torch.equal(out.view(torch.int16) if dtype == torch.bfloat16 else out.view(torch.int32),
                            ref.view(torch.int16) if dtype == torch.bfloat16 else ref.view(torch.int32)), \
             (tuple(w.shape), dtype, mode)
+
+
+def test_paired_repack_matches_single_packs():
+    """The bf16 3x3 weights whose cache holds exactly one forward and one dgrad
+    image are repacked by dv_pack_conv_weight_pairs (one read of the weight for
+    both images); every (forward, dgrad) mode combination, beside a weight the
+    pairing rejects (cout % 64 != 0), writes the same bytes as single packs."""
+    from dalle2_video import ops
+    cases = [((64, 64, 3), 2, 3), ((512, 768, 3), 2, 3), ((128, 48, 3), 0, 1), ((64, 16, 3), 0, 3),
+             ((192, 64, 3), 2, 1), ((40, 24, 3), 0, 1)]
+    cache = ops.PackCache()
+    cache.enabled = True
+    g = torch.Generator(device="cuda").manual_seed(5)
+    imgs = []
+    for (co, ci, k), mf, md in cases:
+        w = torch.randn(co, ci, 1, k, k, device="cuda", generator=g)
+        for mode in (mf, md):
+            pad = ci if mode % 2 == 0 else co
+            out, stale = cache.lookup(w, w, torch.bfloat16, co, ci, k, pad, mode)
+            assert stale
+            imgs.append((w, pad, mode, out))
+    pairs, rest = cache._pair(list(cache.entries.values()))
+    assert len(pairs) == 5 and len(rest) == 2
+    for w, _, _, _ in imgs:
+        w.copy_(torch.randn(w.shape, device="cuda", generator=g))
+    cache.refresh()
+    torch.cuda.synchronize()
+    for w, pad, mode, out in imgs:
+        ref = ops.pack_conv_weight(w, torch.bfloat16, pad, mode, cache=False)
+        assert torch.equal(out.view(torch.int16), ref.view(torch.int16)), (tuple(w.shape), mode)
