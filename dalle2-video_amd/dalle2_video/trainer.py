@@ -20,6 +20,13 @@ from __future__ import annotations
 
 import math
 import os
+
+# ProcessGroupNCCL's event cache hands an event of a finished eager collective
+# to a collective recorded inside a HIP-graph capture; the watchdog thread can
+# still query the eager work's event, which HIP refuses for an event last
+# recorded in a capturing stream (hipErrorCapturedEvent -> watchdog abort).
+# Fresh events per collective: set before the process group is created.
+os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 from contextlib import contextmanager, nullcontext
 from pathlib import Path
 

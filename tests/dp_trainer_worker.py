@@ -16,6 +16,10 @@ losses, the step-0 local gradient, the flat parameters after the last update,
 and the parameters after the init broadcast to OUT_DIR/w{WORLD}_r{RANK}.pt.
 """
 import os
+
+# RCCL collectives captured into the training graph: no event reuse between
+# eager and captured collectives (dalle2_video/trainer.py explains)
+os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
