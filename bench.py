@@ -24,9 +24,6 @@ import argparse
 import json
 import os
 
-# RCCL collectives captured into the training graph: no event reuse between
-# eager and captured collectives (dalle2_video/trainer.py explains)
-os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 import sys
 import time
 

@@ -88,6 +88,11 @@ _SIGS = {
     "dv_mqa_fwd": [_I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _F, _P],
     "dv_mqa_bwd_ws": [_I, _I, _I, _I, _I, _I, _I, _P],
     "dv_mqa_bwd": [_I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _L, _P, _I, _P, _I, _I, _I, _I, _F, _I, _P],
+    "dv_comm_unique_id": [_P],
+    "dv_comm_init": [_P, _I, _I, _I, _P],
+    "dv_comm_allreduce": [_P, _P, _L, _I, _I, _P],
+    "dv_comm_async_error": [_P],
+    "dv_comm_destroy": [_P],
 }
 
 

@@ -517,6 +517,7 @@ class PackCache:
         self.epoch = 0
         self.entries = {}  # key -> dict(out, w, meta, epoch, version)
         self.small = {}  # small-channel conv images (_small_image)
+        self.mx8 = {}  # MX-fp8 conv weight images (mx8_weight_image)
         self._table = None
         self._table_key = None
 
@@ -549,6 +550,9 @@ class PackCache:
             del self.entries[k]
         if dead:
             self._table = self._table_key = None
+        gone = [k for k, e in self.mx8.items() if e[2]() is None or e[2]().data_ptr() != k[0]]
+        for k in gone:
+            del self.mx8[k]
 
     def refresh(self):
         """New epoch (weights were updated): repack all entries in one launch."""
@@ -620,6 +624,7 @@ class PackCache:
 
     def clear(self):
         self.entries.clear()
+        self.mx8.clear()
         self._table = self._table_key = None
 
 
@@ -803,7 +808,7 @@ def mx8_weight_image(weight):
     w = weight.detach()
     if w.dtype != torch.float32 or not w.is_contiguous():
         w = w.float().contiguous()
-    cache = PACK.__dict__.setdefault("mx8", {})
+    cache = PACK.mx8
     key = (weight.data_ptr(), tuple(weight.shape))
     ver = (PACK.epoch, weight._version)
     e = cache.get(key)

@@ -12,21 +12,14 @@ on the MI355X path.
   trainer.py:254-257) is a HIP reduction whose coefficient is applied inside
   the AdamW kernel: no host synchronisation.
 * Data parallel: one process per GPU (torchrun); the loaders are sharded per
-  rank, the active unet's flat gradient is summed with RCCL all-reduces over
-  xGMI (~25 MB buckets, back to front, async on RCCL's stream) and the 1/world
-  average is folded into the update coefficient.  No other collective.
+  rank, the active unet's flat gradient is averaged with RCCL all-reduces over
+  xGMI (~25 MB buckets overlapped with the backward, on a communicator the
+  HIP library owns: GradComm).  No other collective on the data path.
 """
 from __future__ import annotations
 
 import math
 import os
-
-# ProcessGroupNCCL's event cache hands an event of a finished eager collective
-# to a collective recorded inside a HIP-graph capture; the watchdog thread can
-# still query the eager work's event, which HIP refuses for an event last
-# recorded in a capturing stream (hipErrorCapturedEvent -> watchdog abort).
-# Fresh events per collective: set before the process group is created.
-os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 from contextlib import contextmanager, nullcontext
 from pathlib import Path
 
@@ -385,25 +378,32 @@ def shard_loader(loader, world, rank):
     if (world <= 1 or loader is None or not isinstance(loader, DataLoader)
             or isinstance(loader.dataset, IterableDataset) or loader.batch_sampler is None):
         return loader
-    if loader.batch_size is None:
-        # a custom batch_sampler (automatic batching off in the rebuilt form):
-        # keep its batches and give rank r every world-th one
-        return _BatchStridedLoader(loader, world, rank)
     seed = torch.tensor([torch.initial_seed() % (1 << 31)], dtype=torch.int64)
     if dist.is_initialized():
         if dist.get_backend() == "nccl":  # RCCL collectives take device tensors
             seed = seed.cuda()
         dist.broadcast(seed, 0)  # one shuffle order for all ranks
-    return ShardedLoader(loader, world, rank, seed=int(seed.item()))
+    seed = int(seed.item())
+    if loader.batch_size is None:
+        # a custom batch_sampler (automatic batching off in the rebuilt form):
+        # keep its batches and give rank r every world-th one
+        return _BatchStridedLoader(loader, world, rank, seed)
+    return ShardedLoader(loader, world, rank, seed=seed)
 
 
 class _BatchStridedLoader:
     """Per-rank view of a DataLoader driven by a custom batch_sampler: rank r
     of N takes batches r, r+N, ... (the sampler's own batches, unchanged).
-    The sampler must produce the same batch order on every rank (seeded)."""
+    Every rank must draw the same batch order: a batch sampler over an
+    unseeded RandomSampler gets a generator seeded with the broadcast seed;
+    any other source of randomness is the caller's to seed."""
 
-    def __init__(self, loader, world, rank):
-        from torch.utils.data import DataLoader
+    def __init__(self, loader, world, rank, seed=0):
+        from torch.utils.data import DataLoader, RandomSampler
+
+        inner = getattr(loader.batch_sampler, "sampler", None)
+        if isinstance(inner, RandomSampler) and inner.generator is None:
+            inner.generator = torch.Generator().manual_seed(seed)
 
         class _Strided:
             def __init__(self, bs):
@@ -421,7 +421,10 @@ class _BatchStridedLoader:
         self.original = loader
         kw = dict(batch_sampler=_Strided(loader.batch_sampler), num_workers=loader.num_workers,
                   collate_fn=loader.collate_fn, pin_memory=loader.pin_memory, timeout=loader.timeout,
-                  worker_init_fn=loader.worker_init_fn)
+                  worker_init_fn=loader.worker_init_fn, generator=loader.generator)
+        if loader.num_workers > 0:
+            kw.update(prefetch_factor=loader.prefetch_factor,
+                      persistent_workers=loader.persistent_workers)
         self.loader = DataLoader(loader.dataset, **kw)
 
     @property
@@ -447,32 +450,90 @@ def broadcast_parameters(module, src=0):
 
 BUCKET_BYTES = int(os.environ.get("DV_BUCKET_MB", "25")) * (1 << 20)
 
+_NATIVE_COMMS = {}  # process group -> RCCL communicator of libdv_hip (one per process)
+_COMM_SERIAL = [0]
 
-def allreduce_flat_grad(flat_grad, world, bucket_bytes=None, force=False):
-    """The only collective on the data path: the SUM all-reduce of the active
-    unet's flat f32 gradient (RCCL over xGMI on the GPU box), in ~25 MB
-    buckets issued back to front (the flat buffer follows parameter order, so
-    the last buckets hold the output layers whose gradients the backward
-    finished first).  Every bucket is an async collective on the process
-    group's own stream (RCCL's comm stream): the buckets pipeline through the
-    7 xGMI links instead of one 200 MB ring, and the caller's stream waits
-    for all of them once.  The 1/world average is not applied here: it is
-    folded into the clip coefficient (dv_grad_clip_coef's prescale), which
-    the AdamW kernel multiplies in."""
+
+class GradComm:
+    """The data path's one collective: the gradient all-reduce, as a MEAN
+    over ranks (DDP's bucket semantics: averaging an already averaged bucket
+    again is the identity, so gradients that accumulate over several trainer
+    calls before update() stay correct however often a part is reduced).
+
+    * RCCL (`nccl` process group, CUDA tensors): a communicator owned by
+      libdv_hip (dv_comm_*), made once per process; the id travels through
+      the torch.distributed store.  The all-reduce is enqueued on the CURRENT
+      stream — eagerly, or inside a HIP-graph capture of the backward — with
+      no c10d work object: ProcessGroupNCCL's watchdog polls the events of
+      its works from another thread, and one recorded in a capturing stream
+      aborts the process (hipErrorCapturedEvent), so captured collectives
+      never go through it.
+    * anything else (gloo: the CPU tests, the shared-GPU rehearsals): c10d
+      SUM then a 1/world scale."""
+
+    def __init__(self, world, device=None):
+        self.world = world
+        self.native = None
+        if (device is not None and device.type == "cuda" and dist.is_initialized()
+                and dist.get_backend() == "nccl"):
+            self.native = self._native(device)
+
+    @staticmethod
+    def _native(device):
+        import ctypes
+
+        key = id(dist.distributed_c10d._get_default_group())
+        if key in _NATIVE_COMMS:
+            return _NATIVE_COMMS[key]
+        rank, world = dist.get_rank(), dist.get_world_size()
+        _COMM_SERIAL[0] += 1  # every rank makes its communicators in the same order
+        name = f"dv_comm/{_COMM_SERIAL[0]}"
+        store = dist.distributed_c10d._get_default_store()
+        buf = ctypes.create_string_buffer(128)
+        if rank == 0:
+            call("dv_comm_unique_id", buf)
+            store.set(name, buf.raw)
+        else:
+            raw = store.get(name)
+            ctypes.memmove(buf, raw, 128)
+        handle = ctypes.c_void_p()
+        call("dv_comm_init", buf, world, rank, device.index if device.index is not None
+             else torch.cuda.current_device(), ctypes.byref(handle))
+        _NATIVE_COMMS[key] = handle
+        return handle
+
+    def allreduce_mean_(self, t):
+        """Mean over ranks, in place, on the current stream.  Returns None
+        (stream-ordered: RCCL) or a pending c10d work for finish()."""
+        if self.native is not None:
+            call("dv_comm_allreduce", self.native, ptr(t), t.numel(), _lib.dt(t), 1, stream())
+            return None
+        return (dist.all_reduce(t, async_op=True), t)
+
+    def finish(self, pending):
+        work, t = pending
+        work.wait()
+        if self.world > 1:
+            t.mul_(1.0 / self.world)
+
+
+def allreduce_flat_grad(flat_grad, world, bucket_bytes=None, force=False, comm=None):
+    """Average the active unet's flat f32 gradient over the ranks (in place).
+    RCCL: one stream-ordered collective (RCCL pipelines a 200 MB buffer over
+    the xGMI links itself).  c10d: ~bucket_bytes buckets issued back to front
+    (async), then the 1/world scale."""
     if (world <= 1 and not force) or flat_grad is None:
+        return flat_grad
+    comm = comm or GradComm(world, flat_grad.device)
+    if comm.native is not None:
+        comm.allreduce_mean_(flat_grad)
         return flat_grad
     n = flat_grad.numel()
     per = max(1, (bucket_bytes or BUCKET_BYTES) // flat_grad.element_size())
-    works = []
-    for end in range(n, 0, -per):
-        works.append(dist.all_reduce(flat_grad[max(0, end - per):end], async_op=True))
-    for w in works:
-        w.wait()
+    pend = [comm.allreduce_mean_(flat_grad[max(0, end - per):end]) for end in range(n, 0, -per)]
+    for p in pend:
+        comm.finish(p)
     return flat_grad
-
-
-# collectives captured into HIP graphs (see OverlappedAllReduce.wait)
-_CAPTURED_WORKS = []
 
 
 class OverlappedAllReduce:
@@ -492,20 +553,23 @@ class OverlappedAllReduce:
       (Each Unet3D parameter's gradient comes from ONE backward op — no
       weight is applied twice — so its first appearance is its completion,
       once the writes the backward defers are flushed: see _launch.)
-    * Every later call: at hook k, each bucket ready by k is all-reduced (SUM)
-      on a comm stream that first waits for the compute stream and the
-      streamed-wgrad-sum stream; the rest go at the end of the backward.
-      update() waits for them (a captured call joins them inside the graph).
-    The 1/world average stays in the clip coefficient, as before."""
+    * Every later call: at hook k, each bucket ready by k is averaged over
+      the ranks (GradComm: RCCL on libdv_hip's communicator) on a comm stream
+      that first waits for every stream writing gradients; the rest go at the
+      end of the backward.  update() waits for them (a captured call joins
+      them inside the graph).  The mean is idempotent, so a second call
+      before update() (gradient accumulation, the reference's val loop in
+      train_decoder.py:146-151) re-averages the already averaged part to
+      itself, as DDP does."""
 
-    def __init__(self, opt, world):
-        self.opt, self.world = opt, world
+    def __init__(self, opt, world, gcomm):
+        self.opt, self.world, self.gcomm = opt, world, gcomm
         self.ranks = None      # id(param) -> backward index
         self.mode = None       # "record" / "run" during a call
         self.hit = 0
         self.plan = None       # (generation, [(start, end, ready)])
         self.launched = 0
-        self.works = []
+        self.pending = []      # c10d works (gloo) still to finish
         self.comm = None
         self.params = None
 
@@ -584,12 +648,18 @@ class OverlappedAllReduce:
         while self.launched < len(buckets) and buckets[self.launched][2] <= upto:
             start, end, _ = buckets[self.launched]
             dev = G.device
+            # every stream that may still write gradients of this bucket: the
+            # compute stream, the streamed split-K sums, the side-stream wgrads
             self.comm.wait_stream(torch.cuda.current_stream(dev))
             side = ops.WGRAD_DEFER.streamed
             if side is not None:
                 self.comm.wait_stream(ops.WGRAD_DEFER._side(side))
+            if ops._WgradStream.enabled and str(dev) in ops._WgradStream._streams:
+                self.comm.wait_stream(ops._WgradStream._streams[str(dev)])
             with torch.cuda.stream(self.comm):
-                self.works.append(dist.all_reduce(G[start:end], async_op=True))
+                pend = self.gcomm.allreduce_mean_(G[start:end])
+            if pend is not None:
+                self.pending.append(pend)
             self.launched += 1
 
     def end(self, join):
@@ -611,16 +681,13 @@ class OverlappedAllReduce:
         self.mode = None
 
     def wait(self):
-        for w in self.works:
-            w.wait()
-        if self.works and torch.cuda.is_current_stream_capturing():
-            # the captured works' events were recorded in the capturing stream;
-            # ProcessGroupNCCL returns a released work's events to its event
-            # cache, and an eager collective that re-records such an event makes
-            # the watchdog's hipEventQuery fail (hipErrorCapturedEvent, process
-            # abort): captured works are kept for the life of the process
-            _CAPTURED_WORKS.extend(self.works)
-        self.works = []
+        """The caller's stream waits for every launched bucket (inside a
+        capture this is the join of the comm stream back into the graph)."""
+        for p in self.pending:
+            self.gcomm.finish(p)
+        self.pending = []
+        if self.comm is not None:
+            torch.cuda.current_stream(self.comm.device).wait_stream(self.comm)
 
 
 class VideoDecoderTrainer(nn.Module):
@@ -671,13 +738,17 @@ class VideoDecoderTrainer(nn.Module):
         self.force_allreduce = (os.environ.get("DV_FORCE_ALLREDUCE", "0") == "1"
                                 and dist.is_available() and dist.is_initialized())
         self.overlap = None
+        self.gcomm = None
+        if self.world > 1 or self.force_allreduce:
+            self.gcomm = GradComm(self.world, next(decoder.parameters()).device)
         if (self.world > 1 or self.force_allreduce) and os.environ.get("DV_OVERLAP", "1") != "0":
             self.overlap = []
             for i, unet in enumerate(decoder.unets):
-                ov = OverlappedAllReduce(getattr(self, f"optim{i}"), self.world)
+                ov = OverlappedAllReduce(getattr(self, f"optim{i}"), self.world, self.gcomm)
                 ov.attach(unet.parameters())
                 self.overlap.append(ov)
         self._reduced = [False] * self.num_unets  # the last call's gradient is already all-reduced
+        self._gen_seen = [getattr(self, f"optim{i}").generation for i in range(self.num_unets)]
         # accelerator.prepare(..., train, val) (trainer.py:117-124) shards the
         # loaders per process: each rank iterates a disjoint rank-strided part
         # and places the batches on the device (here: pinned host batches
@@ -724,10 +795,12 @@ class VideoDecoderTrainer(nn.Module):
         True when that happened — every captured graph of this unet and every
         packed image keyed on the old storage is then dropped."""
         opt = getattr(self, f"optim{unet_number - 1}")
-        gen = opt.generation
         opt.ensure_flat()
-        if opt.generation == gen:
+        # against the last generation THIS trainer saw: a rebuild can also
+        # happen inside FusedAdamW.load_state_dict
+        if opt.generation == self._gen_seen[unet_number - 1]:
             return False
+        self._gen_seen[unet_number - 1] = opt.generation
         self._graphs = {k: v for k, v in self._graphs.items() if k[0] != unet_number}
         if ops.PACK.enabled:
             ops.PACK.prune()
@@ -743,9 +816,9 @@ class VideoDecoderTrainer(nn.Module):
         if self._reduced[index]:
             self.overlap[index].wait()  # the overlapped buckets (a captured call joined them already)
         else:
-            allreduce_flat_grad(opt.flat_grad, self.world, force=self.force_allreduce)
+            allreduce_flat_grad(opt.flat_grad, self.world, force=self.force_allreduce, comm=self.gcomm)
         self._reduced[index] = False
-        coef = opt.clip_coefficient(self.max_grad_norm, prescale=1.0 / self.world)
+        coef = opt.clip_coefficient(self.max_grad_norm)  # the gradient is already the mean over ranks
         opt.step(clip_coef=coef)
         opt.zero_grad()
         if ops.PACK.enabled:
@@ -845,6 +918,11 @@ class VideoDecoderTrainer(nn.Module):
             # host memory) is re-pointed into fresh flat buffers BEFORE anything
             # runs: a captured graph must never replay against the old storage
             self._check_flat(unet_number)
+        ov = self._overlap_for(unet_number)
+        if ov is not None:
+            # a previous call's buckets may still be in flight on the comm
+            # stream: this call's backward accumulates into the same buffer
+            ov.wait()
         if self._graphable(unet_number, max_batch_size, return_lowres_cond_video):
             out = self._graphed_call(unet_number, args, kwargs)
             if out is not None:

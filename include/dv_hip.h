@@ -508,6 +508,25 @@ int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int ldo, const 
                float* D, float* ws, long long ws_floats, void* dkv, int lddkv, float* dnull, int B,
                int N, int NKP, int H, float scale, int accumulate, void* stream);
 
+/* ---- gradient exchange over RCCL (xGMI) -----------------------------------
+ * Replaces the bucket all-reduces DDP issues from its gradient hooks inside
+ * accelerator.backward (reference trainer.py:360; accelerate wraps the
+ * decoder in DistributedDataParallel at trainer.py:117-124).  One process per
+ * GPU; the communicator belongs to this library, so a collective enqueued
+ * inside a HIP-graph capture has no host-side work object that another thread
+ * could poll.  RCCL is resolved at run time (the instance torch loaded, else
+ * /opt/rocm/lib); without it these return DV_ERR_UNSUPPORTED.
+ * unique_id: 128 opaque bytes made on one rank and handed to every rank
+ * (the trainer uses the torch.distributed store).  init: blocking, every rank
+ * at once, on `device`.  allreduce: in place on `stream`, `average` != 0 ->
+ * mean over ranks (idempotent on data every rank already holds, as DDP's
+ * averaged buckets are), else sum.                                          */
+int dv_comm_unique_id(void* id_out);
+int dv_comm_init(const void* id, int nranks, int rank, int device, void** comm_out);
+int dv_comm_allreduce(void* comm, void* buf, long long count, int dtype, int average, void* stream);
+int dv_comm_async_error(void* comm);
+int dv_comm_destroy(void* comm);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,7 +6,10 @@ rank on cuda:0), training on its rank-strided share of one fixed global batch.
 
 BACKEND gloo (default) or nccl (one rank only on the one-GPU box: with
 DV_FORCE_ALLREDUCE=1 the trainer's overlapped all-reduce then runs on a
-one-rank RCCL group, captured into the HIP graph).
+one-rank RCCL communicator, captured into the HIP graph).
+DV_TEST_ACCUM=2: two trainer calls per update (gradient accumulation; the
+second call uses the next step's data).  DV_TEST_GRAPHS=0: no graph capture
+(every call eager, so every call after the first two overlaps its buckets).
 
 The decoder's two random draws — `times` (torch.randint, reference
 dalle2_video.py:2229) and `noise` (torch.randn_like in p_losses, :1946) — are
@@ -17,9 +20,6 @@ and the parameters after the init broadcast to OUT_DIR/w{WORLD}_r{RANK}.pt.
 """
 import os
 
-# RCCL collectives captured into the training graph: no event reuse between
-# eager and captured collectives (dalle2_video/trainer.py explains)
-os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -54,7 +54,9 @@ def main():
             for p in dec.unets[0].parameters():
                 p.mul_(1.5)
     dec = dec.cuda()
-    tr = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False, use_graphs=True)
+    accum = int(os.environ.get("DV_TEST_ACCUM", "1"))
+    tr = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False,
+                             use_graphs=os.environ.get("DV_TEST_GRAPHS", "1") == "1")
     init = torch.cat([p.detach().reshape(-1) for p in dec.unets[0].parameters()]).cpu()
 
     g = torch.Generator().manual_seed(2024)
@@ -83,10 +85,12 @@ def main():
     losses, grad0 = [], None
     opt = tr.optim0
     for s in range(STEPS):
-        video_d.copy_(video_all[s, sl])
-        times_d.copy_(times_all[s, sl])
-        noise_d.copy_(noise_all[s, sl])
-        losses.append(tr(video=video_d, unet_number=1))
+        for a in range(accum):
+            src = (s + a) % STEPS
+            video_d.copy_(video_all[src, sl])
+            times_d.copy_(times_all[src, sl])
+            noise_d.copy_(noise_all[src, sl])
+            losses.append(tr(video=video_d, unet_number=1))
         if s == 0:
             grad0 = torch.cat([p.grad.detach().reshape(-1) for p in dec.unets[0].parameters()
                                if p.grad is not None]).cpu()
@@ -97,7 +101,7 @@ def main():
     params = torch.cat([p.detach().reshape(-1) for p in dec.unets[0].parameters()]).cpu()
     torch.save(dict(losses=losses, grad0=grad0, params=params, init=init, graphed=graphed, per=per,
                     overlapped=overlapped, buckets=0 if tr.overlap is None else len(tr.overlap[0]._buckets())),
-               os.path.join(out_dir, f"w{world}_r{rank}_{backend}.pt"))
+               os.path.join(out_dir, f"w{world}_r{rank}_{backend}_a{accum}.pt"))
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

@@ -2,9 +2,10 @@
 
 Checks the two collectives the trainer uses (trainer.broadcast_parameters at
 init, trainer.allreduce_flat_grad per update) and the DP identity they
-implement: the 1/world-scaled SUM of per-rank gradients over disjoint halves
-of a batch equals the single-process gradient of the whole batch (p_losses is
-a batch mean).  Gradients come from the CPU oracle unet (the product forward
+implement: the MEAN over ranks of per-rank gradients over disjoint halves of
+a batch equals the single-process gradient of the whole batch (p_losses is a
+batch mean), and averaging an already averaged gradient again is the
+identity (DDP's bucket semantics, which gradient accumulation relies on).  Gradients come from the CPU oracle unet (the product forward
 is GPU-only); the exchange code is the product's.
 """
 import os
@@ -93,12 +94,16 @@ def _worker(rank, world, port, q):
         mine = _grads(ou, x[sl], times[sl], noise[sl])
         ref_sum = mine.clone()
         dist.all_reduce(ref_sum)
-        # bucketed (4 MB buckets, back to front, async) == one all-reduce
+        # bucketed (4 MB buckets, back to front, async) == one all-reduce / world
         allreduce_flat_grad(mine, world, bucket_bytes=4 << 20)
-        if not torch.equal(mine, ref_sum):
+        if not torch.equal(mine, ref_sum * (1.0 / world)):
             raise AssertionError("bucketed all-reduce differs from the single all-reduce")
-        avg = mine / world
-        err = ((avg - full).norm() / full.norm()).item()
+        # idempotent: the mean of identical per-rank values is that value
+        again = mine.clone()
+        allreduce_flat_grad(again, world, bucket_bytes=4 << 20)
+        if not torch.equal(again, mine):
+            raise AssertionError("re-averaging an averaged gradient changed it")
+        err = ((mine - full).norm() / full.norm()).item()
         q.put((rank, ok_bcast, err))
     except BaseException as e:  # report instead of leaving the parent waiting
         import traceback

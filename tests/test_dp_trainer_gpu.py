@@ -17,8 +17,12 @@ The two eager calls after the first run the all-reduce OVERLAPPED with the
 backward (bucket all-reduces launched from backward progress hooks,
 trainer.OverlappedAllReduce): a bucket reduced before its last gradient
 landed would break the match.  A second test runs the overlapped path on a
-one-rank RCCL group (DV_FORCE_ALLREDUCE=1) where the collectives are captured
-into the HIP graph, and checks it against the plain run.
+one-rank RCCL communicator (DV_FORCE_ALLREDUCE=1) where the collectives are
+captured into the HIP graph, and checks it against the plain run.  A third
+accumulates two calls per update (eager, so both calls overlap their bucket
+all-reduces): the second call re-averages the part the first one already
+averaged, which must leave it unchanged (a SUM there grew the
+gradient by world^(calls-1)).
 """
 import os
 import socket
@@ -43,6 +47,7 @@ def _run(out, world, backend="gloo", env_extra=None):
     # 1 MB buckets: the small test unet (12.5 MB of gradient) spans a dozen,
     # so the overlapped all-reduce launches most of them mid-backward
     env = dict(os.environ, DV_BUCKET_MB="1", **(env_extra or {}))
+    accum = env.get("DV_TEST_ACCUM", "1")
     procs = [subprocess.Popen([sys.executable, WORKER, str(out), str(world), str(r), port, backend], env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(world)]
     logs = []
@@ -56,7 +61,8 @@ def _run(out, world, backend="gloo", env_extra=None):
         logs.append(o.decode(errors="replace"))
     for p, lg in zip(procs, logs):
         assert p.returncode == 0, lg[-3000:]
-    return [torch.load(os.path.join(out, f"w{world}_r{r}_{backend}.pt"), weights_only=True) for r in range(world)]
+    return [torch.load(os.path.join(out, f"w{world}_r{r}_{backend}_a{accum}.pt"), weights_only=True)
+            for r in range(world)]
 
 
 def rel(a, b):
@@ -93,3 +99,29 @@ def test_overlapped_allreduce_captured_on_one_rank_rccl(tmp_path, parity_log):
     parity_log(config="1-rank RCCL, overlapped all-reduce captured", params_rel=p_err, loss_rel_max=l_err,
                buckets=rccl["buckets"])
     assert p_err <= 1e-5 and l_err <= 1e-5, (p_err, l_err)
+
+
+def test_two_rank_gradient_accumulation_matches_one_rank(tmp_path, parity_log):
+    env = {"DV_TEST_ACCUM": "2", "DV_TEST_GRAPHS": "0"}
+    one = _run(tmp_path, 1, env_extra=env)[0]
+    two = _run(tmp_path, 2, env_extra=env)
+    p_err = rel(two[0]["params"], one["params"])
+    l_err = max(abs((a + b) / 2 - c) / abs(c) for a, b, c in zip(two[0]["losses"], two[1]["losses"], one["losses"]))
+    parity_log(config="2-rank gloo trainer, 2 calls per update, eager overlapped", params_rel=p_err,
+               loss_rel_max=l_err)
+    assert torch.equal(two[0]["params"], two[1]["params"]), "ranks diverged"
+    assert l_err <= 1e-5, l_err
+    assert p_err <= 1e-5, p_err
+
+
+def test_rccl_captured_accumulation_matches_plain(tmp_path, parity_log):
+    """Two calls per update on the one-rank RCCL communicator, graphs on: the
+    second call of each update replays the captured graph into a gradient
+    that already holds the first call's (averaged) buckets."""
+    env = {"DV_TEST_ACCUM": "2"}
+    plain = _run(tmp_path, 1, env_extra=env)[0]
+    rccl = _run(tmp_path, 1, "nccl", dict(env, DV_FORCE_ALLREDUCE="1"))[0]
+    assert rccl["graphed"] and rccl["overlapped"]
+    p_err = rel(rccl["params"], plain["params"])
+    parity_log(config="1-rank RCCL, 2 calls per update, captured overlap", params_rel=p_err)
+    assert p_err <= 1e-5, p_err
