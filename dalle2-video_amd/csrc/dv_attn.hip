@@ -308,10 +308,12 @@ __global__ __launch_bounds__(256) void mqa_dkdv_kernel(const T* q, int ldq, cons
   }
 }
 
-// K/V with the null key/value at index 0, zero-padded to NKP keys
+// K/V with the null key/value at index 0, zero-padded to NKP keys; keys
+// multiplied by kscale (1, or the bf16 path's scale * log2 e: scores then come
+// out of the MFMA in log2 units)
 template <typename T>
 __global__ void mqa_prep_kernel(const T* kv, int ldkv, const float* null_kv, T* kp, T* vp, int B,
-                                int N, int NKP) {
+                                int N, int NKP, float kscale) {
   const long long n = (long long)B * NKP * DH;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -327,7 +329,7 @@ __global__ void mqa_prep_kernel(const T* kv, int ldkv, const float* null_kv, T* 
       kv_k = (float)kv[tok * ldkv + d];
       kv_v = (float)kv[tok * ldkv + DH + d];
     }
-    kp[i] = (T)kv_k;
+    kp[i] = (T)(kv_k * kscale);
     vp[i] = (T)kv_v;
   }
 }
@@ -481,17 +483,136 @@ __device__ __forceinline__ bf16x8 load_row8(const bf16* p, bool ok) {
   return *(const bf16x8*)p;
 }
 
+// ---- forward --------------------------------------------------------------
+// Keys are stored pre-multiplied by c = scale * log2 e (dv_mqa_prep), so S^T =
+// K Q^T is the logit in log2 units, and the running max enters as the MFMA's
+// C operand (negm = 16 copies of -m per lane: every element a lane holds
+// belongs to its one query row): the tile leaves the MFMA as c s - m and
+// p = exp2 of it, one VALU op per score.  The next tile's scores are issued
+// before this tile's softmax, so its MFMAs run under the exp / sum VALU.
+struct Soft {
+  f32x16 acc, negm;
+  float m, l;
+};
+
+__device__ __forceinline__ f32x16 bcast16(float v) {
+  f32x16 z;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) z[e] = v;
+  return z;
+}
+__device__ __forceinline__ f32x16 score(const char* tK, const FragOff& fo, bf16x8 q0, bf16x8 q1, f32x16 c) {
+  c = mma(row_at(tK, fo, 0), q0, c);
+  return mma(row_at(tK, fo, 1), q1, c);
+}
+// keys >= nkeys of the tile at global key kg -> -inf (the last tile only)
+__device__ __forceinline__ void mask_keys(f32x16& s, int kg, int nkeys, int h) {
+  if (kg + 32 > nkeys) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if (kg + acc_row(e, h) >= nkeys) s[e] = -INFINITY;
+  }
+}
+// max over the 32 keys of a lane's query column (both half-waves)
+__device__ __forceinline__ float col_max(const f32x16& s) {
+  float mx = max3(s[0], s[1], s[2]);
+#pragma unroll
+  for (int e = 3; e < 15; e += 2) mx = max3(mx, s[e], s[e + 1]);
+  mx = max3(mx, s[15], s[15]);
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+  return max3(mx, __uint_as_float(sw[0]), __uint_as_float(sw[1]));
+}
+// first tile of a key range: m = its max
+__device__ __forceinline__ void soft_init(Soft& st, f32x16& s) {
+  st.m = col_max(s);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) s[e] -= st.m;
+  st.negm = bcast16(-st.m);
+  st.acc = zero16();
+  st.l = 0.f;
+}
+// softmax + PV of the tile in s (= c s - m); sn (the next tile's, same m) is
+// shifted with it when the max is raised (lazily: only past m + 8)
+__device__ __forceinline__ void soft_tile(Soft& st, f32x16& s, f32x16& sn, const char* tV, const FragOff& fo) {
+  const float mx = col_max(s);
+  const bool upd = mx > 8.f;
+  if (__builtin_amdgcn_ballot_w64(upd)) {
+    const float d = upd ? mx : 0.f;
+    const float a = ex2(-d);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      s[e] -= d;
+      sn[e] -= d;
+      st.acc[e] *= a;
+    }
+    st.l *= a;
+    st.m += d;
+    st.negm = bcast16(-st.m);
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) s[e] = ex2(s[e]);
+  float t[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = s[2 * j] + s[2 * j + 1];
+  st.l += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+  st.acc = mma(tr_at(tV, fo, 0), pack8(s, 0), st.acc);
+  st.acc = mma(tr_at(tV, fo, 1), pack8(s, 1), st.acc);
+}
+// key tiles [kbeg, kend) of LDS images sK / sV (tile t at t * 32 rows; global
+// key of tile t = kg0 + 32 t), pipelined one tile ahead; `first` starts the state
+__device__ __forceinline__ void soft_range(Soft& st, bool first, const char* sK, const char* sV, int kbeg, int kend,
+                                           int kg0, int nkeys, const FragOff& fo, bf16x8 q0, bf16x8 q1, int h) {
+  if (kbeg >= kend) return;
+  f32x16 s = score(sK + kbeg * 32 * ROW, fo, q0, q1, first ? zero16() : st.negm);
+  mask_keys(s, kg0 + kbeg * 32, nkeys, h);
+  if (first) soft_init(st, s);
+  for (int kt = kbeg; kt < kend; ++kt) {
+    const int kn = kt + 1 < kend ? kt + 1 : kt;  // the last trip re-scores its own tile (discarded)
+    f32x16 sn = score(sK + kn * 32 * ROW, fo, q0, q1, st.negm);
+    soft_tile(st, s, sn, sV + kt * 32 * ROW, fo);
+    mask_keys(sn, kg0 + kn * 32, nkeys, h);
+    s = sn;
+  }
+}
+// merge the two key halves (half 1 parks its state in LDS at `red`) and store
+// O (bf16) and lse (log2 units); returns with only half 0 alive
+__device__ __forceinline__ void soft_finish(Soft& st, float* red, int kh, int lane, int h, bool rok,
+                                            bf16* orow, float* lsep) {
+  __syncthreads();
+  if (kh) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[e * 64 + lane] = st.acc[e];
+    red[16 * 64 + lane] = st.l;
+    red[17 * 64 + lane] = st.m;
+  }
+  __syncthreads();
+  if (kh) return;
+  const float m1 = red[17 * 64 + lane], mn = fmaxf(st.m, m1);
+  const float a0 = ex2(st.m - mn), a1 = ex2(m1 - mn);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) st.acc[e] = st.acc[e] * a0 + red[e * 64 + lane] * a1;
+  float l = st.l * a0 + red[16 * 64 + lane] * a1;
+  l += __shfl_xor(l, 32, 64);
+  if (rok) {
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const u32x2 v = {cvt_pk(st.acc[4 * g] * inv, st.acc[4 * g + 1] * inv),
+                       cvt_pk(st.acc[4 * g + 2] * inv, st.acc[4 * g + 3] * inv)};
+      *(u32x2*)(orow + 8 * g + 4 * h) = v;
+    }
+    if (h == 0) *lsep = mn + __log2f(l);
+  }
+}
+
 // grid (ceil(R / 256), B), 1024 threads, dynamic LDS 2 * NKP * 64 B.
-// Wave w: 32 query rows (group w & 7) against key half w >> 3; the halves
-// merge (m, l, O) through LDS at the end.  Per key tile: S^T = K Q^T (rows
-// keys, column = this lane's query row), the running max on raw scores
-// (c > 0), p = exp2(c s - m) by one fma, then O^T += V^T P^T with P^T as
-// the B operand straight from the accumulator.
+// Wave w: 32 query rows (group w & 7) against key half w >> 3 of the whole
+// clip's K / V, staged once by LDS-DMA; the halves merge through LDS.
 __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restrict__ q,
                                                              const bf16* __restrict__ kp,
                                                              const bf16* __restrict__ vp,
                                                              bf16* __restrict__ o, float* lse,
-                                                             int R, int NKP, int nkeys, float c) {
+                                                             int R, int NKP, int nkeys) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sK = smem;
   char* sV = smem + NKP * ROW;
@@ -506,73 +627,11 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const FragOff fo = frag_off(lane);
-  f32x16 acc = zero16();
-  float m = -INFINITY, l = 0.f;  // m: running max of c * s (log2 units)
   const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
-  const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid;
-  for (int kt = kbeg; kt < kend; ++kt) {
-    const int k0 = kt * 32;
-    f32x16 s = zero16();
-    const char* tK = sK + k0 * ROW;
-    s = mma(row_at(tK, fo, 0), qf0, s);
-    s = mma(row_at(tK, fo, 1), qf1, s);
-    if (k0 + 32 > nkeys) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-        if (k0 + acc_row(e, h) >= nkeys) s[e] = -INFINITY;
-    }
-    float mx = max3(s[0], s[1], s[2]);
-#pragma unroll
-    for (int e = 3; e < 15; e += 2) mx = max3(mx, s[e], s[e + 1]);
-    mx = max3(mx, s[15], __shfl_xor(max3(mx, s[15], s[15]), 32, 64)) * c;
-    const bool upd = mx > m + 8.f;
-    if (__ballot(upd)) {
-      const float mn = upd ? mx : m;
-      const float alpha = ex2(m - mn);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[e] *= alpha;
-      l *= alpha;
-      m = mn;
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      s[e] = ex2(fmaf(s[e], c, -m));
-      l += s[e];
-    }
-    acc = mma(tr_at(sV + k0 * ROW, fo, 0), pack8(s, 0), acc);
-    acc = mma(tr_at(sV + k0 * ROW, fo, 1), pack8(s, 1), acc);
-  }
-  // merge the key halves: half 1 parks (acc, l, m) in LDS (K/V no longer read)
-  __syncthreads();
-  float* red = (float*)smem + rg * 18 * 64;
-  if (kh) {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) red[e * 64 + lane] = acc[e];
-    red[16 * 64 + lane] = l;
-    red[17 * 64 + lane] = m;
-  }
-  __syncthreads();
-  if (kh) return;
-  {
-    const float m1 = red[17 * 64 + lane], mn = fmaxf(m, m1);
-    const float a0 = ex2(m - mn), a1 = ex2(m1 - mn);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = acc[e] * a0 + red[e * 64 + lane] * a1;
-    l = l * a0 + red[16 * 64 + lane] * a1;
-    m = mn;
-  }
-  l += __shfl_xor(l, 32, 64);
-  if (rok) {
-    const float inv = 1.f / l;
-    bf16* orow = o + ((long long)b * R + row) * 32;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const u32x2 v = {cvt_pk(acc[4 * g] * inv, acc[4 * g + 1] * inv),
-                       cvt_pk(acc[4 * g + 2] * inv, acc[4 * g + 3] * inv)};
-      *(u32x2*)(orow + 8 * g + 4 * h) = v;
-    }
-    if (h == 0) lse[(long long)b * R + row] = m + __log2f(l);
-  }
+  Soft st;
+  soft_range(st, true, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
+  soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
+              lse + (long long)b * R + row);
 }
 
 // Long sequences (config 5: 32 x 16 x 16 = 8,192 tokens, K / V = 1 MiB per
@@ -602,7 +661,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
                                                                     const bf16* __restrict__ kp,
                                                                     const bf16* __restrict__ vp,
                                                                     bf16* __restrict__ o, float* lse,
-                                                                    int R, int NKP, int nkeys, float c) {
+                                                                    int R, int NKP, int nkeys) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int rg = wave & (RG - 1), kh = wave / RG;
@@ -618,8 +677,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
   const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
   const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
   const FragOff fo = frag_off(lane);
-  f32x16 acc = zero16();
-  float m = -INFINITY, l = 0.f;  // m: running max of c * s (log2 units)
+  Soft st;
   for (int ch = 0; ch < nch; ++ch) {
     // chunk ch landed (the only DMA in flight); every wave is done with the
     // buffer chunk ch + 1 goes to (it held chunk ch - 1)
@@ -629,82 +687,23 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
     if (ch + 1 < nch)
       dma_kv_chunk(rk, rv, buf_k((ch + 1) & 1), buf_v((ch + 1) & 1), row0 + SCK,
                    min(SCK, NKP - row0 - SCK), wave, lane);
-    const char* sK = buf_k(ch & 1);
-    const char* sV = buf_v(ch & 1);
     const int nkt = nrows / 32, kmid = (nkt + 1) / 2;
-    const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid;
-    for (int kt = kbeg; kt < kend; ++kt) {
-      const int k0 = kt * 32, kg = row0 + k0;
-      f32x16 s = zero16();
-      const char* tK = sK + k0 * ROW;
-      s = mma(row_at(tK, fo, 0), qf0, s);
-      s = mma(row_at(tK, fo, 1), qf1, s);
-      if (kg + 32 > nkeys) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e)
-          if (kg + acc_row(e, h) >= nkeys) s[e] = -INFINITY;
-      }
-      float mx = max3(s[0], s[1], s[2]);
-#pragma unroll
-      for (int e = 3; e < 15; e += 2) mx = max3(mx, s[e], s[e + 1]);
-      mx = max3(mx, s[15], __shfl_xor(max3(mx, s[15], s[15]), 32, 64)) * c;
-      const bool upd = mx > m + 8.f;
-      if (__ballot(upd)) {
-        const float mn = upd ? mx : m;
-        const float alpha = ex2(m - mn);
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] *= alpha;
-        l *= alpha;
-        m = mn;
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        s[e] = ex2(fmaf(s[e], c, -m));
-        l += s[e];
-      }
-      acc = mma(tr_at(sV + k0 * ROW, fo, 0), pack8(s, 0), acc);
-      acc = mma(tr_at(sV + k0 * ROW, fo, 1), pack8(s, 1), acc);
-    }
+    soft_range(st, ch == 0, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo,
+               qf0, qf1, h);
   }
-  // merge the key halves through LDS (no chunk is read any more)
-  __syncthreads();
-  float* red = (float*)smem + rg * 18 * 64;
-  if (kh) {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) red[e * 64 + lane] = acc[e];
-    red[16 * 64 + lane] = l;
-    red[17 * 64 + lane] = m;
-  }
-  __syncthreads();
-  if (kh) return;
-  {
-    const float m1 = red[17 * 64 + lane], mn = fmaxf(m, m1);
-    const float a0 = ex2(m - mn), a1 = ex2(m1 - mn);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = acc[e] * a0 + red[e * 64 + lane] * a1;
-    l = l * a0 + red[16 * 64 + lane] * a1;
-    m = mn;
-  }
-  l += __shfl_xor(l, 32, 64);
-  if (rok) {
-    const float inv = 1.f / l;
-    bf16* orow = o + ((long long)b * R + row) * 32;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const u32x2 v = {cvt_pk(acc[4 * g] * inv, acc[4 * g + 1] * inv),
-                       cvt_pk(acc[4 * g + 2] * inv, acc[4 * g + 3] * inv)};
-      *(u32x2*)(orow + 8 * g + 4 * h) = v;
-    }
-    if (h == 0) lse[(long long)b * R + row] = m + __log2f(l);
-  }
+  soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
+              lse + (long long)b * R + row);
 }
 
 // dq (query-major, as the forward: key halves summed through LDS) and
-// D = rowsum(dO * O) for the dk/dv pass
+// D = rowsum(dO * O) for the dk/dv pass.  Both per-row constants enter as C
+// operands: S^T arrives as c s - L (keys pre-scaled by c), dP^T as dP - D, so
+// dS = exp2(.) * (.) is two VALU ops per score.  dq = (K^T dS^T) / log2 e
+// (the keys carry c = scale * log2 e; dq needs scale).
 __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
-    bf16* __restrict__ dq, float* __restrict__ D, int R, int NKP, int nkeys, float c, float scale) {
+    bf16* __restrict__ dq, float* __restrict__ D, int R, int NKP, int nkeys) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sK = smem;
   char* sV = smem + NKP * ROW;
@@ -724,20 +723,19 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const FragOff fo = frag_off(lane);
+  const f32x16 negL = bcast16(-L2), negD = bcast16(-dd);
   f32x16 acc = zero16();
   const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
   const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid;
   for (int kt = kbeg; kt < kend; ++kt) {
     const int k0 = kt * 32;
-    f32x16 s = zero16(), dp = zero16();
     const char* tK = sK + k0 * ROW;
     const char* tV = sV + k0 * ROW;
-    s = mma(row_at(tK, fo, 0), qf0, s);
-    dp = mma(row_at(tV, fo, 0), df0, dp);
-    s = mma(row_at(tK, fo, 1), qf1, s);
+    f32x16 s = score(tK, fo, qf0, qf1, negL);
+    f32x16 dp = mma(row_at(tV, fo, 0), df0, negD);
     dp = mma(row_at(tV, fo, 1), df1, dp);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) s[e] = ex2(fmaf(s[e], c, -L2)) * (dp[e] - dd);
+    for (int e = 0; e < 16; ++e) s[e] = ex2(s[e]) * dp[e];
     if (k0 + 32 > nkeys) {
 #pragma unroll
       for (int e = 0; e < 16; ++e)
@@ -757,11 +755,12 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] += red[e * 64 + lane];
   if (rok) {
+    constexpr float INV_LOG2E = 0.6931471805599453f;
     bf16* qrow = dq + ((long long)b * R + row) * 32;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const u32x2 v = {cvt_pk(acc[4 * g] * scale, acc[4 * g + 1] * scale),
-                       cvt_pk(acc[4 * g + 2] * scale, acc[4 * g + 3] * scale)};
+      const u32x2 v = {cvt_pk(acc[4 * g] * INV_LOG2E, acc[4 * g + 1] * INV_LOG2E),
+                       cvt_pk(acc[4 * g + 2] * INV_LOG2E, acc[4 * g + 3] * INV_LOG2E)};
       *(u32x2*)(qrow + 8 * g + 4 * h) = v;
     }
   }
@@ -770,7 +769,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
 // dk/dv, key-major.  grid (ceil(nkt / 4), S, B); wave w: key tile
 // blockIdx.x * 4 + (w & 3), query-tile parity w >> 2 (four tiles per step).
 // Partials ws[split][b][NKP][64] = (scale * dK | dV) over the split's rows.
-// Rows past the slice load a clamped row with L = +inf (p = 0), so every
+// Rows past the slice load a clamped row with -L = -inf (p = 0), so every
 // step issues the same loads (exact vmcnt accounting, no exec branches).
 constexpr int TB = 2 * 32 * ROW + 2 * 32 * 4;  // one tile: Q, dO images, L, -D
 constexpr int QP = NW / 4;                      // query-tile parities
@@ -778,7 +777,7 @@ constexpr int RED = 2 * 4 * 2 * 16 * 64 * 4;    // parity combine (two parities 
 __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ D, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
-    float* __restrict__ ws, int R, int NKP, int nkeys, int rows_per_split, float c, float scale) {
+    float* __restrict__ ws, int R, int NKP, int nkeys, int rows_per_split, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[2 * QP * TB > RED ? 2 * QP * TB : RED];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int b = blockIdx.z, split = blockIdx.y;
@@ -809,7 +808,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     char* t = smem + (QP * buf + sp) * TB;
     *(u32x4*)(t + (u < 128 ? 0 : 32 * ROW) + img(crow, cch)) = cv;
     if (u < 32) {
-      ((float*)(t + 2 * 32 * ROW))[u] = lrow < r1 ? lv : INFINITY;
+      ((float*)(t + 2 * 32 * ROW))[u] = lrow < r1 ? -lv : -INFINITY;
       ((float*)(t + 2 * 32 * ROW))[32 + u] = -dv;
     }
   };
@@ -831,26 +830,27 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
       const char* sdO = t + 32 * ROW;
       const float* sL = (const float*)(t + 2 * 32 * ROW);
       const float* sD = sL + 32;
-      f32x16 s = zero16(), dp;
+      // C operands: -L (S arrives as c s - L, keys pre-scaled) and -D
+      f32x16 s, dp;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 d4 = *(const f32x4*)(sD + 8 * g + 4 * h);
+        const f32x4 l4 = *(const f32x4*)(sL + 8 * g + 4 * h);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dp[4 * g + e] = d4[e];
+        for (int e = 0; e < 4; ++e) {
+          dp[4 * g + e] = d4[e];
+          s[4 * g + e] = l4[e];
+        }
       }
       s = mma(row_frag(sQ, 0, r, h), kf0, s);
       dp = mma(row_frag(sdO, 0, r, h), vf0, dp);
       s = mma(row_frag(sQ, 1, r, h), kf1, s);
       dp = mma(row_frag(sdO, 1, r, h), vf1, dp);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 l4 = *(const f32x4*)(sL + 8 * g + 4 * h);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float p = ex2(fmaf(s[4 * g + e], c, -l4[e]));
-          s[4 * g + e] = p;
-          dp[4 * g + e] *= p;
-        }
+      for (int e = 0; e < 16; ++e) {
+        const float p = ex2(s[e]);
+        s[e] = p;
+        dp[e] *= p;
       }
       dvv = mma(tr_frag(sdO, 0, lane), pack8(s, 0), dvv);
       dk = mma(tr_frag(sQ, 0, lane), pack8(dp, 0), dk);
@@ -974,14 +974,16 @@ int grid_for(long long work) {
 }  // namespace
 
 extern "C" int dv_mqa_prep(int dtype, const void* kv, int ldkv, const float* null_kv, void* kp,
-                           void* vp, int B, int N, int NKP, void* stream) {
+                           void* vp, int B, int N, int NKP, float scale, void* stream) {
   DV_REQUIRE(kv && null_kv && kp && vp && NKP >= N + 1 && NKP % 32 == 0, "bad arguments");
   hipStream_t st = (hipStream_t)stream;
   const long long n = (long long)B * NKP * DH;
-  if (dtype == DV_BF16)
-    mqa_prep_kernel<bf16><<<grid_for(n), 256, 0, st>>>((const bf16*)kv, ldkv, null_kv, (bf16*)kp, (bf16*)vp, B, N, NKP);
+  if (dtype == DV_BF16)  // keys in log2 units of the logit (the fa kernels' contract)
+    mqa_prep_kernel<bf16><<<grid_for(n), 256, 0, st>>>((const bf16*)kv, ldkv, null_kv, (bf16*)kp, (bf16*)vp, B, N, NKP,
+                                                      scale * fa::LOG2E);
   else
-    mqa_prep_kernel<float><<<grid_for(n), 256, 0, st>>>((const float*)kv, ldkv, null_kv, (float*)kp, (float*)vp, B, N, NKP);
+    mqa_prep_kernel<float><<<grid_for(n), 256, 0, st>>>((const float*)kv, ldkv, null_kv, (float*)kp, (float*)vp, B, N,
+                                                       NKP, 1.f);
   return check_launch("mqa_prep");
 }
 
@@ -990,22 +992,28 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
                           void* stream) {
   DV_REQUIRE(q && kp && vp && o && lse && H % 4 == 0 && NKP % 32 == 0, "bad arguments");
   DV_REQUIRE(ldq % 8 == 0 && ldo >= H * DH, "bad strides");
-  dim3 grid((N + 31) / 32, H / 4, B);
   hipStream_t st = (hipStream_t)stream;
-  if (fa::eligible(dtype, ldq, ldo, H, NKP)) {
-    const int R = N * H, lds = max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4);
-    fa::set_lds((const void*)fa::mqa_fwd_fa_kernel, lds);
-    fa::mqa_fwd_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
-        (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, scale * fa::LOG2E);
-  } else if (fa::eligible_stream(dtype, ldq, ldo, H, NKP)) {
-    const int R = N * H, lds = 4 * fa::SCK * fa::ROW;
-    fa::set_lds((const void*)fa::mqa_fwd_fa_stream_kernel, lds);
-    fa::mqa_fwd_fa_stream_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
-        (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, scale * fa::LOG2E);
-  } else if (dtype == DV_BF16)
-    mqa_fwd_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)q, ldq, (const bf16*)kp, (const bf16*)vp, (bf16*)o, ldo, lse, N, NKP, N + 1, H, scale);
-  else
-    mqa_fwd_kernel<float><<<grid, 256, 0, st>>>((const float*)q, ldq, (const float*)kp, (const float*)vp, (float*)o, ldo, lse, N, NKP, N + 1, H, scale);
+  if (dtype == DV_BF16) {
+    // bf16 keys come from dv_mqa_prep pre-scaled: only the fa kernels read them
+    DV_REQUIRE(ldq == H * DH && ldo == H * DH, "bf16 path needs dense q / o rows");
+    const int R = N * H;
+    if (fa::eligible(dtype, ldq, ldo, H, NKP)) {
+      const int lds = max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4);
+      fa::set_lds((const void*)fa::mqa_fwd_fa_kernel, lds);
+      fa::mqa_fwd_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
+          (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1);
+    } else {
+      DV_REQUIRE(fa::eligible_stream(dtype, ldq, ldo, H, NKP), "sequence too long");
+      const int lds = 4 * fa::SCK * fa::ROW;
+      fa::set_lds((const void*)fa::mqa_fwd_fa_stream_kernel, lds);
+      fa::mqa_fwd_fa_stream_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
+          (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1);
+    }
+  } else {
+    dim3 grid((N + 31) / 32, H / 4, B);
+    mqa_fwd_kernel<float><<<grid, 256, 0, st>>>((const float*)q, ldq, (const float*)kp, (const float*)vp, (float*)o,
+                                                ldo, lse, N, NKP, N + 1, H, scale);
+  }
   return check_launch("mqa_fwd");
 }
 
@@ -1034,35 +1042,28 @@ extern "C" int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int 
     DV_REQUIRE(lddo == H * DH && lddq == H * DH, "bf16 path needs dense dout/dq rows");
     const int R = N * H, lds = max(NKP * 2 * fa::ROW, fa::RG * 16 * 64 * 4), S = fa::splits(NKP, B);
     const int rps = ((R + S - 1) / S + 63) / 64 * 64;
-    const float c = scale * fa::LOG2E;
     fa::set_lds((const void*)fa::mqa_dq_fa_kernel, lds);
     fa::mqa_dq_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
         (const bf16*)q, (const bf16*)o, (const bf16*)dout, lse, (const bf16*)kp, (const bf16*)vp,
-        (bf16*)dq, D, R, NKP, N + 1, c, scale);
+        (bf16*)dq, D, R, NKP, N + 1);
     fa::mqa_dkdv_fa_kernel<<<dim3((NKP / 32 + 3) / 4, S, B), fa::NW * 64, 0, st>>>(
         (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP,
-        N + 1, rps, c, scale);
+        N + 1, rps, scale);
     DV_REQUIRE(S >= 1 && S <= 16, "split count out of range");
     fa::launch_finish<16>(S, grid_for((long long)B * N * 16), st, ws, B, N, NKP, (bf16*)dkv, lddkv,
                           dnull, accumulate);
 
     return check_launch("mqa_bwd");
   }
+  DV_REQUIRE(dtype == DV_F32, "bf16 backward needs the whole clip's K / V in LDS (NKP <= 1280)");
   float* dkp = ws;
   float* dvp = ws + (long long)B * NKP * DH;
   zero_f32(dkp, (long long)B * NKP * DH, st);
   zero_f32(dvp, (long long)B * NKP * DH, st);
   const int hg = 2, hpg = H / hg;
-  if (dtype == DV_BF16) {
-    mqa_bwd_d_kernel<bf16><<<grid_for((long long)B * N * H), 256, 0, st>>>((const bf16*)o, ldo, (const bf16*)dout, lddo, D, B, N, H);
-    mqa_dq_kernel<bf16><<<dim3((N + 31) / 32, H / 4, B), 256, 0, st>>>((const bf16*)q, ldq, (const bf16*)dout, lddo, lse, D, (const bf16*)kp, (const bf16*)vp, (bf16*)dq, lddq, N, NKP, N + 1, H, scale);
-    mqa_dkdv_kernel<bf16><<<dim3(NKP / 32, hg, B), 256, 0, st>>>((const bf16*)q, ldq, (const bf16*)dout, lddo, lse, D, (const bf16*)kp, (const bf16*)vp, dkp, dvp, N, NKP, N + 1, H, hpg, scale);
-    mqa_finish_kernel<bf16><<<grid_for((long long)B * N * DH), 256, 0, st>>>(dkp, dvp, (bf16*)dkv, lddkv, dnull, B, N, NKP, accumulate);
-  } else {
-    mqa_bwd_d_kernel<float><<<grid_for((long long)B * N * H), 256, 0, st>>>((const float*)o, ldo, (const float*)dout, lddo, D, B, N, H);
-    mqa_dq_kernel<float><<<dim3((N + 31) / 32, H / 4, B), 256, 0, st>>>((const float*)q, ldq, (const float*)dout, lddo, lse, D, (const float*)kp, (const float*)vp, (float*)dq, lddq, N, NKP, N + 1, H, scale);
-    mqa_dkdv_kernel<float><<<dim3(NKP / 32, hg, B), 256, 0, st>>>((const float*)q, ldq, (const float*)dout, lddo, lse, D, (const float*)kp, (const float*)vp, dkp, dvp, N, NKP, N + 1, H, hpg, scale);
-    mqa_finish_kernel<float><<<grid_for((long long)B * N * DH), 256, 0, st>>>(dkp, dvp, (float*)dkv, lddkv, dnull, B, N, NKP, accumulate);
-  }
+  mqa_bwd_d_kernel<float><<<grid_for((long long)B * N * H), 256, 0, st>>>((const float*)o, ldo, (const float*)dout, lddo, D, B, N, H);
+  mqa_dq_kernel<float><<<dim3((N + 31) / 32, H / 4, B), 256, 0, st>>>((const float*)q, ldq, (const float*)dout, lddo, lse, D, (const float*)kp, (const float*)vp, (float*)dq, lddq, N, NKP, N + 1, H, scale);
+  mqa_dkdv_kernel<float><<<dim3(NKP / 32, hg, B), 256, 0, st>>>((const float*)q, ldq, (const float*)dout, lddo, lse, D, (const float*)kp, (const float*)vp, dkp, dvp, N, NKP, N + 1, H, hpg, scale);
+  mqa_finish_kernel<float><<<grid_for((long long)B * N * DH), 256, 0, st>>>(dkp, dvp, (float*)dkv, lddkv, dnull, B, N, NKP, accumulate);
   return check_launch("mqa_bwd");
 }

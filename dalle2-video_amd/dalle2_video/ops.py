@@ -1777,7 +1777,8 @@ class MQAFn(torch.autograd.Function):
         kp = torch.empty(B, NKP, MQA_DH, dtype=q.dtype, device=dev)
         vp = torch.empty_like(kp)
         nkv = null_kv.detach().float().contiguous()
-        call("dv_mqa_prep", dt(q), ptr(kvc), kvc.shape[-1], ptr(nkv), ptr(kp), ptr(vp), B, N, NKP, stream())
+        call("dv_mqa_prep", dt(q), ptr(kvc), kvc.shape[-1], ptr(nkv), ptr(kp), ptr(vp), B, N, NKP,
+             ctypes_float(scale), stream())
         o = torch.empty(B * N, H * MQA_DH, dtype=q.dtype, device=dev)
         lse = torch.empty(B, H, N, dtype=torch.float32, device=dev)
         _launch("attn:mqa_fwd", 4.0 * B * H * N * (N + 1) * MQA_DH, 0,

@@ -488,21 +488,25 @@ int dv_xattn_fold_bwd(float* wsR, float* wsV, float* wsQ, float* mcorr,
  * ONE shared k/v head (multi-query), learned null k/v at key 0, q scaled
  * twice by 32^-0.5 with cosine-sim off -> logit factor 1/32).
  * prep: kv [B][N][*] (k at 0, v at 32, stride ldkv) -> kp/vp [B][NKP][32]
- * (row 0 null, rows > N zero; NKP = roundup(N+1, 32)).                      */
+ * (row 0 null, rows > N zero; NKP = roundup(N+1, 32)).  `scale` is the
+ * logit factor later passed to dv_mqa_fwd / dv_mqa_bwd: on the bf16 path kp
+ * holds k * scale * log2(e) (the MFMA then yields the logit in log2 units);
+ * f32 kp holds k.                                                          */
 int dv_mqa_prep(int dtype, const void* kv, int ldkv, const float* null_kv, void* kp, void* vp,
-                int B, int N, int NKP, void* stream);
+                int B, int N, int NKP, float scale, void* stream);
 /* o[b][n][h*32+d] = softmax_j(scale * q.k_j) v_j; lse f32 saved (opaque to the
  * caller, B*H*N floats: [B][N*H] log2 units on the bf16 path, [B][H][N]
- * natural-log otherwise).  bf16 with dense rows (ldq == ldo == H*32) and
- * NKP <= 1280 runs the whole-clip-K/V-in-LDS kernels.                       */
+ * natural-log otherwise).  bf16 needs dense rows (ldq == ldo == H*32): NKP
+ * <= 1280 runs the whole-clip-K/V-in-LDS kernel, longer clips the K/V-
+ * streamed one.                                                             */
 int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, const void* vp, void* o, int ldo,
                float* lse, int B, int N, int NKP, int H, float scale, void* stream);
 /* f32 scratch dv_mqa_bwd needs (floats); same path choice as dv_mqa_fwd.     */
 int dv_mqa_bwd_ws(int dtype, int ldq, int ldo, int B, int N, int NKP, int H, long long* floats);
 /* dq, dkv (k at 0, v at 32, stride lddkv) and dnull (+)= (accumulate);
  * D (B*H*N floats) and ws (>= dv_mqa_bwd_ws floats, no zeroing needed) are
- * scratch.  bf16 path: dq (query-major) writes D, dk/dv (key-major) writes
- * per-slice partials to ws, a finish launch sums them.                      */
+ * scratch.  bf16 path (NKP <= 1280): dq (query-major) writes D, dk/dv
+ * (key-major) writes per-slice partials to ws, a finish launch sums them.   */
 int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int ldo, const void* dout,
                int lddo, const float* lse, const void* kp, const void* vp, void* dq, int lddq,
                float* D, float* ws, long long ws_floats, void* dkv, int lddkv, float* dnull, int B,
