@@ -11,6 +11,8 @@
 //   O^T += V^T P^T     (P^T accumulator reused as the B operand)
 //   dkdv: S = Q K^T, dP = dO V^T, dV^T += dO^T P, dK^T += Q^T dS
 //   dq:   S^T, dP^T = V dO^T, dQ^T += K^T dS^T
+#include <cstdlib>
+
 #include "dv_common.h"
 
 using namespace dv;
@@ -423,6 +425,37 @@ __device__ __forceinline__ bf16x8 tr_at(const char* tile, const FragOff& f, int 
   return cat8(tr_read(tile + f.tr[s][0]), tr_read(tile + f.tr[s][1]));
 }
 
+// V^T fragments (both k-steps) of a 32-key tile by ds_read_b64_tr_b16 from
+// inline asm, waiting for its own reads only: the builtin carries no memory
+// operand, so hipcc drains vmcnt before it — i.e. waits for the NEXT chunk's
+// LDS-DMA in the streamed kernel on every tile.
+__device__ __forceinline__ unsigned lds_off(const char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+// issue: the four reads, no wait; tr_wait: lgkmcnt(0) tied to the results
+// (the consumer cannot be scheduled above it)
+struct TrFrag {
+  s16x4 x[4];
+};
+__device__ __forceinline__ TrFrag tr_issue(const char* tile, const FragOff& f) {
+  TrFrag t;
+  const unsigned b = lds_off(tile);
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %4\n\t"
+      "ds_read_b64_tr_b16 %1, %5\n\t"
+      "ds_read_b64_tr_b16 %2, %6\n\t"
+      "ds_read_b64_tr_b16 %3, %7"
+      : "=&v"(t.x[0]), "=&v"(t.x[1]), "=&v"(t.x[2]), "=&v"(t.x[3])
+      : "v"(b + f.tr[0][0]), "v"(b + f.tr[0][1]), "v"(b + f.tr[1][0]), "v"(b + f.tr[1][1])
+      : "memory");
+  return t;
+}
+__device__ __forceinline__ void tr_wait(TrFrag& t, bf16x8& a0, bf16x8& a1) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t.x[0]), "+v"(t.x[1]), "+v"(t.x[2]), "+v"(t.x[3])::"memory");
+  a0 = cat8(t.x[0], t.x[1]);
+  a1 = cat8(t.x[2], t.x[3]);
+}
+
 __device__ __forceinline__ unsigned cvt_pk(float lo, float hi) {
   unsigned r;
   asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
@@ -513,12 +546,22 @@ __device__ __forceinline__ void mask_keys(f32x16& s, int kg, int nkeys, int h) {
       if (kg + acc_row(e, h) >= nkeys) s[e] = -INFINITY;
   }
 }
-// max over the 32 keys of a lane's query column (both half-waves)
+// max over the 32 keys of a lane's query column (both half-waves); the
+// chain is one asm block (hipcc pads every separate inline-asm VALU op with
+// an s_nop)
 __device__ __forceinline__ float col_max(const f32x16& s) {
-  float mx = max3(s[0], s[1], s[2]);
-#pragma unroll
-  for (int e = 3; e < 15; e += 2) mx = max3(mx, s[e], s[e + 1]);
-  mx = max3(mx, s[15], s[15]);
+  float mx;
+  asm("v_max3_f32 %0, %1, %2, %3\n\t"
+      "v_max3_f32 %0, %0, %4, %5\n\t"
+      "v_max3_f32 %0, %0, %6, %7\n\t"
+      "v_max3_f32 %0, %0, %8, %9\n\t"
+      "v_max3_f32 %0, %0, %10, %11\n\t"
+      "v_max3_f32 %0, %0, %12, %13\n\t"
+      "v_max3_f32 %0, %0, %14, %15\n\t"
+      "v_max_f32 %0, %0, %16"
+      : "=&v"(mx)
+      : "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(s[4]), "v"(s[5]), "v"(s[6]), "v"(s[7]), "v"(s[8]),
+        "v"(s[9]), "v"(s[10]), "v"(s[11]), "v"(s[12]), "v"(s[13]), "v"(s[14]), "v"(s[15]));
   const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
   return max3(mx, __uint_as_float(sw[0]), __uint_as_float(sw[1]));
 }
@@ -534,6 +577,7 @@ __device__ __forceinline__ void soft_init(Soft& st, f32x16& s) {
 // softmax + PV of the tile in s (= c s - m); sn (the next tile's, same m) is
 // shifted with it when the max is raised (lazily: only past m + 8)
 __device__ __forceinline__ void soft_tile(Soft& st, f32x16& s, f32x16& sn, const char* tV, const FragOff& fo) {
+  TrFrag vt = tr_issue(tV, fo);  // V^T of this tile: in flight under the max / exp
   const float mx = col_max(s);
   const bool upd = mx > 8.f;
   if (__builtin_amdgcn_ballot_w64(upd)) {
@@ -555,8 +599,10 @@ __device__ __forceinline__ void soft_tile(Soft& st, f32x16& s, f32x16& sn, const
 #pragma unroll
   for (int j = 0; j < 8; ++j) t[j] = s[2 * j] + s[2 * j + 1];
   st.l += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
-  st.acc = mma(tr_at(tV, fo, 0), pack8(s, 0), st.acc);
-  st.acc = mma(tr_at(tV, fo, 1), pack8(s, 1), st.acc);
+  bf16x8 v0, v1;
+  tr_wait(vt, v0, v1);
+  st.acc = mma(v0, pack8(s, 0), st.acc);
+  st.acc = mma(v1, pack8(s, 1), st.acc);
 }
 // key tiles [kbeg, kend) of LDS images sK / sV (tile t at t * 32 rows; global
 // key of tile t = kg0 + 32 t), pipelined one tile ahead; `first` starts the state
@@ -574,6 +620,131 @@ __device__ __forceinline__ void soft_range(Soft& st, bool first, const char* sK,
     s = sn;
   }
 }
+// Two key tiles per step (64 keys): one max chain, 32 independent exps and
+// 4 PV MFMAs per dependency round — the per-wave chain max -> exp -> PV is
+// the bound at 4 waves / SIMD, so a step carries twice the keys.
+__device__ __forceinline__ float col_max2(const f32x16& a, const f32x16& b) {
+  float mx;
+  asm("v_max3_f32 %0, %1, %2, %3\n\t"
+      "v_max3_f32 %0, %0, %4, %5\n\t"
+      "v_max3_f32 %0, %0, %6, %7\n\t"
+      "v_max3_f32 %0, %0, %8, %9\n\t"
+      "v_max3_f32 %0, %0, %10, %11\n\t"
+      "v_max3_f32 %0, %0, %12, %13\n\t"
+      "v_max3_f32 %0, %0, %14, %15\n\t"
+      "v_max_f32 %0, %0, %16"
+      : "=&v"(mx)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),
+        "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12]), "v"(a[13]), "v"(a[14]), "v"(a[15]));
+  asm("v_max3_f32 %0, %0, %1, %2\n\t"
+      "v_max3_f32 %0, %0, %3, %4\n\t"
+      "v_max3_f32 %0, %0, %5, %6\n\t"
+      "v_max3_f32 %0, %0, %7, %8\n\t"
+      "v_max3_f32 %0, %0, %9, %10\n\t"
+      "v_max3_f32 %0, %0, %11, %12\n\t"
+      "v_max3_f32 %0, %0, %13, %14\n\t"
+      "v_max3_f32 %0, %0, %15, %16"
+      : "+v"(mx)
+      : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]), "v"(b[8]),
+        "v"(b[9]), "v"(b[10]), "v"(b[11]), "v"(b[12]), "v"(b[13]), "v"(b[14]), "v"(b[15]));
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+  return max3(mx, __uint_as_float(sw[0]), __uint_as_float(sw[1]));
+}
+__device__ __forceinline__ float sum16(const f32x16& s) {
+  float t[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = s[2 * j] + s[2 * j + 1];
+  return ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+}
+// one step over the key tiles in s0 / s1 (raw log2-unit scores, masked):
+// max, lazy rescale, p = exp2(s - m), row sums, then the NEXT pair is scored
+// into the dead s0 / s1 registers (its MFMAs overlap this step's PV MFMAs and
+// the tail VALU) before this pair's PV.  No C-operand max here: 16 fewer
+// VGPRs (the pair step needs them) for one v_sub per score.
+__device__ __forceinline__ void soft_step2(Soft& st, f32x16& s0, f32x16& s1, const char* tV0, const char* tV1,
+                                           const char* tKn0, const char* tKn1, const FragOff& fo, bf16x8 q0,
+                                           bf16x8 q1) {
+  TrFrag vt0 = tr_issue(tV0, fo), vt1 = tr_issue(tV1, fo);
+  const float mx = col_max2(s0, s1);
+  const bool upd = mx > st.m + 8.f;
+  if (__builtin_amdgcn_ballot_w64(upd)) {
+    const float mn = upd ? mx : st.m;
+    const float a = ex2(st.m - mn);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) st.acc[e] *= a;
+    st.l *= a;
+    st.m = mn;
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    s0[e] = ex2(s0[e] - st.m);
+    s1[e] = ex2(s1[e] - st.m);
+  }
+  st.l += sum16(s0) + sum16(s1);
+  const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
+  s0 = score(tKn0, fo, q0, q1, zero16());
+  s1 = score(tKn1, fo, q0, q1, zero16());
+  bf16x8 a0, a1, b0, b1;
+  tr_wait(vt0, a0, a1);
+  tr_wait(vt1, b0, b1);
+  st.acc = mma(a0, p00, st.acc);
+  st.acc = mma(a1, p01, st.acc);
+  st.acc = mma(b0, p10, st.acc);
+  st.acc = mma(b1, p11, st.acc);
+}
+// soft_range with two tiles per step; the state's m is a plain running max
+// here (negm unused; the caller starts it at -inf, l = 0, acc = 0); an odd
+// range starts with one single-tile step
+__device__ __forceinline__ void soft_range2(Soft& st, bool first, const char* sK, const char* sV, int kbeg, int kend,
+                                            int kg0, int nkeys, const FragOff& fo, bf16x8 q0, bf16x8 q1, int h) {
+  if (kbeg >= kend) return;
+  int kt = kbeg;
+  if ((kend - kbeg) & 1) {  // single tile: raw scores through the pair step's rules
+    f32x16 s = score(sK + kt * 32 * ROW, fo, q0, q1, zero16());
+    mask_keys(s, kg0 + kt * 32, nkeys, h);
+    TrFrag vt = tr_issue(sV + kt * 32 * ROW, fo);
+    const float mx = col_max(s);
+    const bool upd = mx > st.m + 8.f;
+    if (__builtin_amdgcn_ballot_w64(upd)) {
+      const float mn = upd ? mx : st.m;
+      const float a = st.m == -INFINITY ? 0.f : ex2(st.m - mn);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) st.acc[e] *= a;
+      st.l *= a;
+      st.m = mn;
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s[e] = ex2(s[e] - st.m);
+    st.l += sum16(s);
+    bf16x8 a0, a1;
+    tr_wait(vt, a0, a1);
+    st.acc = mma(a0, pack8(s, 0), st.acc);
+    st.acc = mma(a1, pack8(s, 1), st.acc);
+    ++kt;
+  }
+  if (kt >= kend) return;
+  f32x16 s0 = score(sK + kt * 32 * ROW, fo, q0, q1, zero16());
+  f32x16 s1 = score(sK + (kt + 1) * 32 * ROW, fo, q0, q1, zero16());
+  mask_keys(s0, kg0 + kt * 32, nkeys, h);
+  mask_keys(s1, kg0 + (kt + 1) * 32, nkeys, h);
+  if (st.m == -INFINITY) st.m = col_max2(s0, s1);  // the first step: m = the pair's max
+  for (; kt < kend; kt += 2) {
+    const int kn0 = kt + 2 < kend ? kt + 2 : kt, kn1 = kn0 + 1;  // the last step re-scores its own pair
+    soft_step2(st, s0, s1, sV + kt * 32 * ROW, sV + (kt + 1) * 32 * ROW, sK + kn0 * 32 * ROW,
+               sK + kn1 * 32 * ROW, fo, q0, q1);
+    mask_keys(s0, kg0 + kn0 * 32, nkeys, h);
+    mask_keys(s1, kg0 + kn1 * 32, nkeys, h);
+  }
+}
+template <bool PAIR>
+__device__ __forceinline__ void soft_range_t(Soft& st, bool first, const char* sK, const char* sV, int kbeg, int kend,
+                                             int kg0, int nkeys, const FragOff& fo, bf16x8 q0, bf16x8 q1, int h) {
+  if constexpr (PAIR)
+    soft_range2(st, first, sK, sV, kbeg, kend, kg0, nkeys, fo, q0, q1, h);
+  else
+    soft_range(st, first, sK, sV, kbeg, kend, kg0, nkeys, fo, q0, q1, h);
+}
+
 // merge the two key halves (half 1 parks its state in LDS at `red`) and store
 // O (bf16) and lse (log2 units); returns with only half 0 alive
 __device__ __forceinline__ void soft_finish(Soft& st, float* red, int kh, int lane, int h, bool rok,
@@ -608,6 +779,7 @@ __device__ __forceinline__ void soft_finish(Soft& st, float* red, int kh, int la
 // grid (ceil(R / 256), B), 1024 threads, dynamic LDS 2 * NKP * 64 B.
 // Wave w: 32 query rows (group w & 7) against key half w >> 3 of the whole
 // clip's K / V, staged once by LDS-DMA; the halves merge through LDS.
+template <bool PAIR>
 __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restrict__ q,
                                                              const bf16* __restrict__ kp,
                                                              const bf16* __restrict__ vp,
@@ -616,7 +788,8 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sK = smem;
   char* sV = smem + NKP * ROW;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int rg = wave & (RG - 1), kh = wave / RG;
   const int b = blockIdx.y;
   dma_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, wave, lane);
@@ -628,8 +801,8 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   __syncthreads();
   const FragOff fo = frag_off(lane);
   const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
-  Soft st;
-  soft_range(st, true, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
+  Soft st{zero16(), zero16(), -INFINITY, 0.f};
+  soft_range_t<PAIR>(st, true, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
   soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
               lse + (long long)b * R + row);
 }
@@ -657,13 +830,15 @@ __device__ __forceinline__ void dma_kv_chunk(const __amdgpu_buffer_rsrc_t& rk,
   }
 }
 
+template <bool PAIR>
 __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* __restrict__ q,
                                                                     const bf16* __restrict__ kp,
                                                                     const bf16* __restrict__ vp,
                                                                     bf16* __restrict__ o, float* lse,
                                                                     int R, int NKP, int nkeys) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int rg = wave & (RG - 1), kh = wave / RG;
   const int b = blockIdx.y;
   const __amdgpu_buffer_rsrc_t rk = dma_rsrc(kp + (long long)b * NKP * 32, (unsigned)NKP * ROW);
@@ -677,7 +852,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
   const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
   const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
   const FragOff fo = frag_off(lane);
-  Soft st;
+  Soft st{zero16(), zero16(), -INFINITY, 0.f};
   for (int ch = 0; ch < nch; ++ch) {
     // chunk ch landed (the only DMA in flight); every wave is done with the
     // buffer chunk ch + 1 goes to (it held chunk ch - 1)
@@ -688,7 +863,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
       dma_kv_chunk(rk, rv, buf_k((ch + 1) & 1), buf_v((ch + 1) & 1), row0 + SCK,
                    min(SCK, NKP - row0 - SCK), wave, lane);
     const int nkt = nrows / 32, kmid = (nkt + 1) / 2;
-    soft_range(st, ch == 0, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo,
+    soft_range_t<PAIR>(st, ch == 0, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo,
                qf0, qf1, h);
   }
   soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
@@ -707,7 +882,8 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sK = smem;
   char* sV = smem + NKP * ROW;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int rg = wave & (RG - 1), kh = wave / RG;
   const int b = blockIdx.y;
   dma_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, wave, lane);
@@ -779,7 +955,8 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     const float* __restrict__ D, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
     float* __restrict__ ws, int R, int NKP, int nkeys, int rows_per_split, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[2 * QP * TB > RED ? 2 * QP * TB : RED];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int b = blockIdx.z, split = blockIdx.y;
   const int kt = blockIdx.x * 4 + (wave & 3), qp = wave >> 2;
   const bool kvalid = kt < NKP / 32;
@@ -997,17 +1174,33 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
     // bf16 keys come from dv_mqa_prep pre-scaled: only the fa kernels read them
     DV_REQUIRE(ldq == H * DH && ldo == H * DH, "bf16 path needs dense q / o rows");
     const int R = N * H;
-    if (fa::eligible(dtype, ldq, ldo, H, NKP)) {
+    // DV_MQA_STREAM=1: the K/V-streamed kernel at every length; DV_MQA_PAIR=0:
+    // one key tile per softmax step (A/B)
+    static const bool force_stream = getenv("DV_MQA_STREAM") && atoi(getenv("DV_MQA_STREAM")) != 0;
+    static const bool pair = !getenv("DV_MQA_PAIR") || atoi(getenv("DV_MQA_PAIR")) != 0;
+    const dim3 grid((R + 255) / 256, B);
+    if (fa::eligible(dtype, ldq, ldo, H, NKP) && !force_stream) {
       const int lds = max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4);
-      fa::set_lds((const void*)fa::mqa_fwd_fa_kernel, lds);
-      fa::mqa_fwd_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
-          (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1);
+      const void* fn = pair ? (const void*)fa::mqa_fwd_fa_kernel<true> : (const void*)fa::mqa_fwd_fa_kernel<false>;
+      fa::set_lds(fn, lds);
+      if (pair)
+        fa::mqa_fwd_fa_kernel<true><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
+                                                                   (bf16*)o, lse, R, NKP, N + 1);
+      else
+        fa::mqa_fwd_fa_kernel<false><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
+                                                                    (bf16*)o, lse, R, NKP, N + 1);
     } else {
-      DV_REQUIRE(fa::eligible_stream(dtype, ldq, ldo, H, NKP), "sequence too long");
+      DV_REQUIRE((long long)NKP * fa::ROW < (1ll << 31), "sequence too long");
       const int lds = 4 * fa::SCK * fa::ROW;
-      fa::set_lds((const void*)fa::mqa_fwd_fa_stream_kernel, lds);
-      fa::mqa_fwd_fa_stream_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
-          (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1);
+      const void* fn = pair ? (const void*)fa::mqa_fwd_fa_stream_kernel<true>
+                            : (const void*)fa::mqa_fwd_fa_stream_kernel<false>;
+      fa::set_lds(fn, lds);
+      if (pair)
+        fa::mqa_fwd_fa_stream_kernel<true><<<grid, fa::NW * 64, lds, st>>>(
+            (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1);
+      else
+        fa::mqa_fwd_fa_stream_kernel<false><<<grid, fa::NW * 64, lds, st>>>(
+            (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1);
     }
   } else {
     dim3 grid((N + 31) / 32, H / 4, B);

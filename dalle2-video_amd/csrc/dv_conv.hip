@@ -96,6 +96,11 @@ struct ConvFwdArgs {
   // window kernel: output-channel groups the 8 XCDs split into (the other
   // factor of 8 splits the pixel tiles); 0: one channel block per XCD
   int xcd_c;
+  // window kernel, K split in two (KSPL = 2): each tile's two halves hand
+  // their f32 partial sums through ks_part (32 KB per half) and a per-tile
+  // ticket in ks_flag (zero between launches)
+  float* ks_part;
+  int* ks_flag;
 };
 
 // GroupNorm statistics of a wave's tile, register-light: every lane holds
@@ -2113,7 +2118,14 @@ __device__ __forceinline__ int fw_pix(int r) {
 // NWV = 8: a 128-pixel x 2*CO-channel tile per workgroup, waves 4-7 on the
 // second channel half (the pixel window is staged once for both halves): for
 // the grids whose CO-channel tiles would run in two rounds on the 256 CUs.
-template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4>
+// KSPL = 2: the 16-channel chunks are split in two halves over two
+// workgroups per tile (grid doubled) for grids whose tiles leave half the
+// CUs idle; the last of the two to finish adds the other's partial sums
+// (written to p.ks_part, agent-scope release / acquire around a per-tile
+// ticket: no spin, the halves may sit on different XCDs) and runs the
+// epilogue.
+template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4,
+          int KSPL = 1>
 __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
   using G = FwGeom<W, CO, NWV>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
@@ -2128,6 +2140,12 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   const int wq = wave & 3, chh = wave >> 2;  // pixel sub-tile, channel half
   const int npx = (int)(p.M / 128), nblk = npx * (p.cout / CG);
   int L = blockIdx.x;
+  int kh = 0;  // K half (KSPL = 2): blocks b and b + 8 (one XCD) take the two halves of tile L
+  if constexpr (KSPL == 2) {
+    kh = (L >> 3) & 1;
+    L = ((L >> 4) << 3) | (L & 7);
+  }
+  const int tile = L;
   int co0;
   long long m0;
   if (p.xcd_c > 0) {
@@ -2142,7 +2160,10 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     co0 = (L / npx) * CG;
     m0 = (long long)(L % npx) * 128;
   }
-  const int nch = p.cin / 16;
+  const int nch_all = p.cin / 16;
+  const int cbeg = KSPL == 2 ? kh * (nch_all / 2) : 0;
+  const int cend = KSPL == 2 ? cbeg + nch_all / 2 : nch_all;
+  const int nch = cend - cbeg;  // chunks of this workgroup
   const int HW = p.H * W;
   const int y0 = W == 8 ? 0 : (int)((m0 % HW) / W);        // tile's first image row
   const long long fb = W == 8 ? m0 : m0 - (m0 % HW) + (long long)y0 * W;  // pixel of (y0, 0)
@@ -2189,10 +2210,10 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   };
   constexpr int AHEAD = NBUF - 1;  // chunks in flight beyond the one being read
 
-  // prologue: chunks 0 .. AHEAD-1 in flight, wait for chunk 0
+  // prologue: chunks cbeg .. cbeg+AHEAD-1 in flight, wait for chunk cbeg
 #pragma unroll
   for (int c = 0; c < AHEAD; ++c)
-    if (c < nch) issue(c);
+    if (c < nch) issue(cbeg + c);
   const int pro = min(AHEAD, nch) - 1;  // younger chunks than chunk 0
   if (pro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
   else if (pro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
@@ -2234,7 +2255,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     };
 #pragma unroll
     for (int d = 0; d < PF; ++d) rd(d, d);
-    if (DEFER && c > 0) {  // tap 8 of chunk c-1 (even tap: chains 0 / 1)
+    if (DEFER && c > cbeg) {  // tap 8 of chunk c-1 (even tap: chains 0 / 1)
       acc0 = Mma<bf16>::run(la0, lb, acc0);
       if (CO == 64) acc1 = Mma<bf16>::run(la1, lb, acc1);
     }
@@ -2263,7 +2284,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     if constexpr (decltype(PRE)::value) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"((AHEAD - 1) * NPW) : "memory");
     } else {
-      const int young = min(c + AHEAD, nch - 1) - (c + 1);
+      const int young = min(c + AHEAD, cend - 1) - (c + 1);
       if (young >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
       else if (young == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
       else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
@@ -2273,14 +2294,54 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     else if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0)::"memory");
     __builtin_amdgcn_s_barrier();
   };
-  int c = 0;
-  for (; c + AHEAD < nch; ++c) chunk(c, std::true_type{});
-  for (; c < nch; ++c) chunk(c, std::false_type{});
+  int c = cbeg;
+  for (; c + AHEAD < cend; ++c) chunk(c, std::true_type{});
+  for (; c < cend; ++c) chunk(c, std::false_type{});
   if (DEFER && nch > 0) {
     acc0 = Mma<bf16>::run(la0, lb, acc0);
     if (CO == 64) acc1 = Mma<bf16>::run(la1, lb, acc1);
   }
   DV_STAMP_AT(2);
+  if constexpr (KSPL == 2) {
+    // hand-off: both halves write their partial (lane-linear, 1 KB per wave
+    // store), release, take a ticket; the second adds the first's partial
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      acc0[e] += acc2[e];
+      if (CO == 64) acc1[e] += acc3[e];
+      acc2[e] = acc3[e] = 0.f;
+    }
+    constexpr int PART = NWV * 2 * 16 * 64;  // floats per half
+    float* mine = p.ks_part + ((long long)tile * 2 + kh) * PART + wave * (2 * 16 * 64);
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      *(f32x4*)(mine + e4 * 256 + lane * 4) = f32x4{acc0[4 * e4], acc0[4 * e4 + 1], acc0[4 * e4 + 2], acc0[4 * e4 + 3]};
+      if (CO == 64)
+        *(f32x4*)(mine + 1024 + e4 * 256 + lane * 4) =
+            f32x4{acc1[4 * e4], acc1[4 * e4 + 1], acc1[4 * e4 + 2], acc1[4 * e4 + 3]};
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's stores out of its L2
+    __syncthreads();
+    int* tk = (int*)smem;
+    if (threadIdx.x == 0) *tk = __hip_atomic_fetch_add(p.ks_flag + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*tk == 0) return;  // the other half finishes the tile
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const float* other = p.ks_part + ((long long)tile * 2 + (kh ^ 1)) * PART + wave * (2 * 16 * 64);
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      const f32x4 o0 = *(const f32x4*)(other + e4 * 256 + lane * 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc0[4 * e4 + k] += o0[k];
+      if (CO == 64) {
+        const f32x4 o1 = *(const f32x4*)(other + 1024 + e4 * 256 + lane * 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc1[4 * e4 + k] += o1[k];
+      }
+    }
+    if (threadIdx.x == 0) p.ks_flag[tile] = 0;  // ready for the next launch
+    __syncthreads();  // the ticket word is LDS the statistics epilogue reuses
+  }
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e.  Bias and
   // residual are loaded for all 8 channel groups BEFORE the first store (vmcnt
   // retires loads and stores in order: a load behind a store waits for the
@@ -2376,11 +2437,51 @@ int frame_xcd_split(const ConvFwdArgs<bf16>& a, int co) {
   return best;
 }
 
+// caller-owned scratch of the window conv's K split (dv_conv_scratch), per device
+struct KsScratch {
+  float* part = nullptr;
+  long long bytes = 0;
+  int* flags = nullptr;
+  int nflags = 0;
+};
+KsScratch g_ks[64];
+
+KsScratch* ks_scratch() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  return g_ks[dev].part ? &g_ks[dev] : nullptr;
+}
+
 int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   ConvFwdArgs<bf16> a = a0;
-  // 32-channel tiles when 64-channel ones leave CUs idle (DV_FRAME_CO32=0: off)
+  const int tiles64 = (int)(a.M / 128) * (a.cout / 64);
+  // grids of <= 128 64-channel tiles (half the CUs): the chunk loop split in
+  // two workgroups per tile (KSPL = 2) when the caller registered scratch
+  // (DV_FRAME_KSPLIT=0: off); otherwise 32-channel tiles (DV_FRAME_CO32=0: off)
+  static const bool ks_ok = !(getenv("DV_FRAME_KSPLIT") && atoi(getenv("DV_FRAME_KSPLIT")) == 0);
+  if (ks_ok && tiles64 <= 128 && tiles64 % 8 == 0 && (a.cin / 16) % 2 == 0) {
+    KsScratch* ks = ks_scratch();
+    if (ks && ks->nflags >= tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {
+      a.ks_part = ks->part;
+      a.ks_flag = ks->flags;
+      a.xcd_c = frame_xcd_split(a, 64);
+      const int nb2 = 2 * tiles64;
+#define DV_FK(WW, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, 64, SP, 4, 2><<<nb2, 256, 0, st>>>(a) \
+                              : conv_fwd_frame_kernel<WW, false, 3, 1, 64, SP, 4, 2><<<nb2, 256, 0, st>>>(a))
+#define DV_FK2(WW) (a.c0 < a.cin ? DV_FK(WW, true) : DV_FK(WW, false))
+      switch (a.W) {
+        case 8: DV_FK2(8); break;
+        case 16: DV_FK2(16); break;
+        case 32: DV_FK2(32); break;
+        default: DV_FK2(64); break;
+      }
+#undef DV_FK2
+#undef DV_FK
+      return check_launch("conv_fwd_frame");
+    }
+  }
   static const bool co32_ok = !(getenv("DV_FRAME_CO32") && atoi(getenv("DV_FRAME_CO32")) == 0);
-  const int co = co32_ok && (a.M / 128) * (a.cout / 64) <= 128 ? 32 : 64;
+  const int co = co32_ok && tiles64 <= 128 ? 32 : 64;
   // 8 waves on 128 channels for the 16-wide frames whose 64-channel tiles
   // would take two rounds of the 256 CUs (DV_FRAME_W8=0: off)
   static const bool w8_ok = !(getenv("DV_FRAME_W8") && atoi(getenv("DV_FRAME_W8")) == 0);
@@ -3161,6 +3262,17 @@ extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const voi
     return conv_fwd_t<bf16>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, y, ldy, nf, h, w,
                             cin, cout, ksize, act, gn_sums, gn_P, gn_R, st);
   DV_REQUIRE(false, "unknown dtype");
+}
+
+extern "C" int dv_conv_scratch(void* part, long long bytes, int* flags, int nflags) {
+  DV_REQUIRE((part && flags && bytes > 0 && nflags > 0) || (!part && !flags), "bad scratch");
+  int dev = 0;
+  DV_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "no current device");
+  g_ks[dev].part = (float*)part;
+  g_ks[dev].bytes = part ? bytes : 0;
+  g_ks[dev].flags = flags;
+  g_ks[dev].nflags = flags ? nflags : 0;
+  return DV_OK;
 }
 
 extern "C" int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,

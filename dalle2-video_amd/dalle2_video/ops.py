@@ -208,6 +208,20 @@ def _grad_out(p, zero=False):
 
 
 _WS = {}
+_KS_SCRATCH = {}
+
+
+def _conv_scratch(device):
+    """The window conv's K-split hand-off scratch (dv_conv_scratch), registered
+    once per device before its first launch (so a captured graph replays on
+    the same addresses): 16 MB of f32 partials, 1,024 zeroed tile tickets."""
+    key = str(device)
+    if key not in _KS_SCRATCH:
+        part = torch.empty(4 << 20, dtype=torch.float32, device=device)
+        flags = torch.zeros(1024, dtype=torch.int32, device=device)
+        call("dv_conv_scratch", ptr(part), part.numel() * 4, ptr(flags), flags.numel())
+        _KS_SCRATCH[key] = (part, flags)
+    return _KS_SCRATCH[key]
 
 
 def _wgrad_workspace(dname, nf, h, w, cin, c0, split, cout, ks, device):
@@ -898,6 +912,7 @@ class ConvFn(torch.autograd.Function):
                                  ldr, ptr(y), cout, nf, h, w, cin_real, cout, ksize, stream()), shape)
         elif use_win:
             wp = pack_conv_weight(weight, x0.dtype, cin, 2, cache)
+            _conv_scratch(x0.device)
             _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                     lambda: call("dv_conv_fwd8", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp),
                                  ptr(b), ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ACT_NONE,
@@ -951,6 +966,7 @@ class ConvFn(torch.autograd.Function):
             shape = ("dgrad", m, cin_real, cout8 * ksize * ksize)
             if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, ldx, rld, ksize, h, w, nf):
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 3, ctx.cache)
+                _conv_scratch(dy8.device)
                 _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                         lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd),
                                      None, rp, rld, ptr(dx), ldx, nf, h, w, cout8, cin_real, ACT_NONE,

@@ -32,6 +32,10 @@ CASES = [
     # 8x8-frame forward / dgrad (H = W = 8, 16-channel chunks, two frames per block)
     (4, 8, 8, 48, 16, 64, 3),       # dual source at a 16-channel boundary, dgrad 64 -> 48 + 16
     (6, 8, 8, 128, 0, 192, 3),      # three channel blocks (no XCD regrouping), 8 chunks
+    # window conv with the chunk loop split over two workgroups per tile (<= 128
+    # 64-channel tiles: the halves hand partial sums over through dv_conv_scratch)
+    (64, 8, 8, 512, 0, 256, 3),     # the Cfg2 8x8 512 -> 256 shape (dgrad 256 -> 512: no split)
+    (16, 16, 16, 64, 64, 64, 3),    # W=16, dual source, 32 tiles (dgrad 64 -> 128: split too)
     # 1x1 streaming kernel (K = 64 / 128, cout = 64 / 128): ragged / tiny / persistent
     (3, 9, 11, 64, 64, 64, 1),      # dual source, 297 pixels (ragged last tile)
     (2, 6, 6, 64, 0, 128, 1),       # fewer pixels than one tile
