@@ -432,8 +432,10 @@ __device__ __forceinline__ bf16x8 tr_at(const char* tile, const FragOff& f, int 
 __device__ __forceinline__ unsigned lds_off(const char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
-// issue: the four reads, no wait; tr_wait: lgkmcnt(0) tied to the results
-// (the consumer cannot be scheduled above it)
+// The reads and their wait are ONE asm statement: the compiler takes an asm
+// output as written when the statement ends, so a split issue / wait lets the
+// register allocator copy a fragment before its data has landed (measured:
+// nondeterministic NaN rows).  tr_issue returns with the data in registers.
 struct TrFrag {
   s16x4 x[4];
 };
@@ -444,22 +446,38 @@ __device__ __forceinline__ TrFrag tr_issue(const char* tile, const FragOff& f) {
       "ds_read_b64_tr_b16 %0, %4\n\t"
       "ds_read_b64_tr_b16 %1, %5\n\t"
       "ds_read_b64_tr_b16 %2, %6\n\t"
-      "ds_read_b64_tr_b16 %3, %7"
+      "ds_read_b64_tr_b16 %3, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
       : "=&v"(t.x[0]), "=&v"(t.x[1]), "=&v"(t.x[2]), "=&v"(t.x[3])
       : "v"(b + f.tr[0][0]), "v"(b + f.tr[0][1]), "v"(b + f.tr[1][0]), "v"(b + f.tr[1][1])
       : "memory");
   return t;
 }
-__device__ __forceinline__ void tr_wait(TrFrag& t, bf16x8& a0, bf16x8& a1) {
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t.x[0]), "+v"(t.x[1]), "+v"(t.x[2]), "+v"(t.x[3])::"memory");
+__device__ __forceinline__ void tr_wait(const TrFrag& t, bf16x8& a0, bf16x8& a1) {
   a0 = cat8(t.x[0], t.x[1]);
   a1 = cat8(t.x[2], t.x[3]);
 }
 
+// f32 pair -> packed bf16 (hipcc emits v_cvt_pk_bf16_f32).  Compiler-visible on
+// purpose: an inline-asm VALU op that reads a v_exp result or an MFMA result
+// gets no hazard wait states from hipcc (it reads the register stale).
 __device__ __forceinline__ unsigned cvt_pk(float lo, float hi) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, v);
+}
+// the same as one inline-asm op with its own trans-result wait state (s_nop 0:
+// hipcc adds none in front of an asm consumer of v_exp): the dk/dv loop keeps
+// its register allocation (no spill at 128 VGPRs) with it
+__device__ __forceinline__ unsigned cvt_pk_asm(float lo, float hi) {
   unsigned r;
-  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  asm("s_nop 0\n\tv_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
   return r;
+}
+__device__ __forceinline__ bf16x8 pack8a(const f32x16& x, int s) {
+  const u32x4 v = {cvt_pk_asm(x[8 * s], x[8 * s + 1]), cvt_pk_asm(x[8 * s + 2], x[8 * s + 3]),
+                   cvt_pk_asm(x[8 * s + 4], x[8 * s + 5]), cvt_pk_asm(x[8 * s + 6], x[8 * s + 7])};
+  return __builtin_bit_cast(bf16x8, v);
 }
 __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
   const u32x4 v = {cvt_pk(x[8 * s], x[8 * s + 1]), cvt_pk(x[8 * s + 2], x[8 * s + 3]),
@@ -476,11 +494,10 @@ __device__ __forceinline__ float dot8(bf16x8 a, bf16x8 b) {
   for (int j = 0; j < 8; ++j) s += (float)a[j] * (float)b[j];
   return s;
 }
-// v_max3_f32 without the NaN-canonicalising moves fmaxf costs (scores are finite or -inf)
+// max of three (hipcc folds chains of fmaxf into v_max3_f32 and inserts the
+// MFMA-result wait states an inline-asm form does not get)
 __device__ __forceinline__ float max3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return __builtin_fmaxf(__builtin_fmaxf(a, b), c);
 }
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
@@ -546,25 +563,18 @@ __device__ __forceinline__ void mask_keys(f32x16& s, int kg, int nkeys, int h) {
       if (kg + acc_row(e, h) >= nkeys) s[e] = -INFINITY;
   }
 }
-// max over the 32 keys of a lane's query column (both half-waves); the
-// chain is one asm block (hipcc pads every separate inline-asm VALU op with
-// an s_nop)
-__device__ __forceinline__ float col_max(const f32x16& s) {
-  float mx;
-  asm("v_max3_f32 %0, %1, %2, %3\n\t"
-      "v_max3_f32 %0, %0, %4, %5\n\t"
-      "v_max3_f32 %0, %0, %6, %7\n\t"
-      "v_max3_f32 %0, %0, %8, %9\n\t"
-      "v_max3_f32 %0, %0, %10, %11\n\t"
-      "v_max3_f32 %0, %0, %12, %13\n\t"
-      "v_max3_f32 %0, %0, %14, %15\n\t"
-      "v_max_f32 %0, %0, %16"
-      : "=&v"(mx)
-      : "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(s[4]), "v"(s[5]), "v"(s[6]), "v"(s[7]), "v"(s[8]),
-        "v"(s[9]), "v"(s[10]), "v"(s[11]), "v"(s[12]), "v"(s[13]), "v"(s[14]), "v"(s[15]));
+// max over the 32 keys of a lane's query column (both half-waves)
+__device__ __forceinline__ float half_max(const f32x16& s) {
+  float mx = max3(s[0], s[1], s[2]);
+#pragma unroll
+  for (int e = 3; e < 15; e += 2) mx = max3(mx, s[e], s[e + 1]);
+  return __builtin_fmaxf(mx, s[15]);
+}
+__device__ __forceinline__ float cross_half(float mx) {
   const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
   return max3(mx, __uint_as_float(sw[0]), __uint_as_float(sw[1]));
 }
+__device__ __forceinline__ float col_max(const f32x16& s) { return cross_half(half_max(s)); }
 // first tile of a key range: m = its max
 __device__ __forceinline__ void soft_init(Soft& st, f32x16& s) {
   st.m = col_max(s);
@@ -624,31 +634,7 @@ __device__ __forceinline__ void soft_range(Soft& st, bool first, const char* sK,
 // 4 PV MFMAs per dependency round — the per-wave chain max -> exp -> PV is
 // the bound at 4 waves / SIMD, so a step carries twice the keys.
 __device__ __forceinline__ float col_max2(const f32x16& a, const f32x16& b) {
-  float mx;
-  asm("v_max3_f32 %0, %1, %2, %3\n\t"
-      "v_max3_f32 %0, %0, %4, %5\n\t"
-      "v_max3_f32 %0, %0, %6, %7\n\t"
-      "v_max3_f32 %0, %0, %8, %9\n\t"
-      "v_max3_f32 %0, %0, %10, %11\n\t"
-      "v_max3_f32 %0, %0, %12, %13\n\t"
-      "v_max3_f32 %0, %0, %14, %15\n\t"
-      "v_max_f32 %0, %0, %16"
-      : "=&v"(mx)
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),
-        "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12]), "v"(a[13]), "v"(a[14]), "v"(a[15]));
-  asm("v_max3_f32 %0, %0, %1, %2\n\t"
-      "v_max3_f32 %0, %0, %3, %4\n\t"
-      "v_max3_f32 %0, %0, %5, %6\n\t"
-      "v_max3_f32 %0, %0, %7, %8\n\t"
-      "v_max3_f32 %0, %0, %9, %10\n\t"
-      "v_max3_f32 %0, %0, %11, %12\n\t"
-      "v_max3_f32 %0, %0, %13, %14\n\t"
-      "v_max3_f32 %0, %0, %15, %16"
-      : "+v"(mx)
-      : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]), "v"(b[8]),
-        "v"(b[9]), "v"(b[10]), "v"(b[11]), "v"(b[12]), "v"(b[13]), "v"(b[14]), "v"(b[15]));
-  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-  return max3(mx, __uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  return cross_half(__builtin_fmaxf(half_max(a), half_max(b)));
 }
 __device__ __forceinline__ float sum16(const f32x16& s) {
   float t[8];
@@ -1007,32 +993,32 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
       const char* sdO = t + 32 * ROW;
       const float* sL = (const float*)(t + 2 * 32 * ROW);
       const float* sD = sL + 32;
-      // C operands: -L (S arrives as c s - L, keys pre-scaled) and -D
-      f32x16 s, dp;
+      // dP arrives as dP - D (C operand -D); S in log2 units (keys pre-scaled)
+      f32x16 s = zero16(), dp;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 d4 = *(const f32x4*)(sD + 8 * g + 4 * h);
-        const f32x4 l4 = *(const f32x4*)(sL + 8 * g + 4 * h);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          dp[4 * g + e] = d4[e];
-          s[4 * g + e] = l4[e];
-        }
+        for (int e = 0; e < 4; ++e) dp[4 * g + e] = d4[e];
       }
       s = mma(row_frag(sQ, 0, r, h), kf0, s);
       dp = mma(row_frag(sdO, 0, r, h), vf0, dp);
       s = mma(row_frag(sQ, 1, r, h), kf1, s);
       dp = mma(row_frag(sdO, 1, r, h), vf1, dp);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const float p = ex2(s[e]);
-        s[e] = p;
-        dp[e] *= p;
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 l4 = *(const f32x4*)(sL + 8 * g + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = ex2(s[4 * g + e] + l4[e]);  // the staged value is -L
+          s[4 * g + e] = p;
+          dp[4 * g + e] *= p;
+        }
       }
-      dvv = mma(tr_frag(sdO, 0, lane), pack8(s, 0), dvv);
-      dk = mma(tr_frag(sQ, 0, lane), pack8(dp, 0), dk);
-      dvv = mma(tr_frag(sdO, 1, lane), pack8(s, 1), dvv);
-      dk = mma(tr_frag(sQ, 1, lane), pack8(dp, 1), dk);
+      dvv = mma(tr_frag(sdO, 0, lane), pack8a(s, 0), dvv);
+      dk = mma(tr_frag(sQ, 0, lane), pack8a(dp, 0), dk);
+      dvv = mma(tr_frag(sdO, 1, lane), pack8a(s, 1), dvv);
+      dk = mma(tr_frag(sQ, 1, lane), pack8a(dp, 1), dk);
     }
     if (more) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -2083,7 +2083,7 @@ constexpr int F8_WROW = 19;                                // 16-B slots per wei
 // CO output channels per tile: 64 (two 32x32 accumulators per wave), or 32
 // for the grids that would leave CUs idle (M = 4,096 at 256 channels: 128
 // tiles of 64 channels for 256 CUs)
-template <int W, int CO = 64, int NWV = 4>
+template <int W, int CO = 64, int NWV = 4, int NB = 0>
 struct FwGeom {
   static constexpr int CG = CO * (NWV / 4);                  // channels per workgroup
   static constexpr int NF = W == 8 ? 2 : 1;                  // frames per tile
@@ -2096,7 +2096,7 @@ struct FwGeom {
   static constexpr int PIECES = WPC + XPIECES;
   static constexpr int NPW = (PIECES + NWV - 1) / NWV;
   static constexpr int BUF = PIECES * 1024;
-  static constexpr int NBUF = (160 * 1024 - 1024) / BUF >= 5 ? 5 : (160 * 1024 - 1024) / BUF;
+  static constexpr int NBUF = NB ? NB : ((160 * 1024 - 1024) / BUF >= 5 ? 5 : (160 * 1024 - 1024) / BUF);
 };
 
 // lane r -> pixel (row * W + col) of the wave's 32-pixel tile so that the
@@ -2124,10 +2124,13 @@ __device__ __forceinline__ int fw_pix(int r) {
 // (written to p.ks_part, agent-scope release / acquire around a per-tile
 // ticket: no spin, the halves may sit on different XCDs) and runs the
 // epilogue.
+// NB > 0: a shallower ring (NB chunk buffers) so that two workgroups share a
+// CU (the K-split 256-tile grids: two waves per SIMD from two workgroups, one
+// hiding the other's LDS-DMA issue)
 template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4,
-          int KSPL = 1>
+          int KSPL = 1, int NB = 0>
 __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
-  using G = FwGeom<W, CO, NWV>;
+  using G = FwGeom<W, CO, NWV, NB>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
   constexpr int WPC = G::WPC, NJ = CO / 32, CG = G::CG;
   static_assert(NWV == 4 || (NWV == 8 && !STATS), "the 8-wave tile has no statistics epilogue");
@@ -2458,7 +2461,28 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   // grids of <= 128 64-channel tiles (half the CUs): the chunk loop split in
   // two workgroups per tile (KSPL = 2) when the caller registered scratch
   // (DV_FRAME_KSPLIT=0: off); otherwise 32-channel tiles (DV_FRAME_CO32=0: off)
-  static const bool ks_ok = !(getenv("DV_FRAME_KSPLIT") && atoi(getenv("DV_FRAME_KSPLIT")) == 0);
+  // opt-in: measured 104.0 -> 100.6 steps/s on (gpurun_out/ks_r04a): the agent-scope release of
+  // the partial (an L2 write-back) costs more than the idle CUs it fills
+  static const bool ks_ok = getenv("DV_FRAME_KSPLIT") && atoi(getenv("DV_FRAME_KSPLIT")) != 0;
+  // DV_FRAME_KS256=1: also split the 256-tile grids, two workgroups per CU on
+  // a 2-deep ring (A/B)
+  static const bool ks256 = getenv("DV_FRAME_KS256") && atoi(getenv("DV_FRAME_KS256")) != 0;
+  if (ks_ok && ks256 && tiles64 == 256 && a.W == 8 && (a.cin / 16) % 2 == 0) {
+    KsScratch* ks = ks_scratch();
+    if (ks && ks->nflags >= tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {
+      a.ks_part = ks->part;
+      a.ks_flag = ks->flags;
+      a.xcd_c = frame_xcd_split(a, 64);
+      const int nb2 = 2 * tiles64;
+      if (a.c0 < a.cin)
+        a.gn_sums ? conv_fwd_frame_kernel<8, true, 3, 1, 64, true, 4, 2, 2><<<nb2, 256, 0, st>>>(a)
+                  : conv_fwd_frame_kernel<8, false, 3, 1, 64, true, 4, 2, 2><<<nb2, 256, 0, st>>>(a);
+      else
+        a.gn_sums ? conv_fwd_frame_kernel<8, true, 3, 1, 64, false, 4, 2, 2><<<nb2, 256, 0, st>>>(a)
+                  : conv_fwd_frame_kernel<8, false, 3, 1, 64, false, 4, 2, 2><<<nb2, 256, 0, st>>>(a);
+      return check_launch("conv_fwd_frame");
+    }
+  }
   if (ks_ok && tiles64 <= 128 && tiles64 % 8 == 0 && (a.cin / 16) % 2 == 0) {
     KsScratch* ks = ks_scratch();
     if (ks && ks->nflags >= tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {

@@ -35,6 +35,7 @@ CASES = [
     # window conv with the chunk loop split over two workgroups per tile (<= 128
     # 64-channel tiles: the halves hand partial sums over through dv_conv_scratch)
     (64, 8, 8, 512, 0, 256, 3),     # the Cfg2 8x8 512 -> 256 shape (dgrad 256 -> 512: no split)
+    (64, 8, 8, 512, 0, 512, 3),     # Cfg2 8x8 512 -> 512: 256 tiles (split only with DV_FRAME_KS256=1)
     (16, 16, 16, 64, 64, 64, 3),    # W=16, dual source, 32 tiles (dgrad 64 -> 128: split too)
     # 1x1 streaming kernel (K = 64 / 128, cout = 64 / 128): ragged / tiny / persistent
     (3, 9, 11, 64, 64, 64, 1),      # dual source, 297 pixels (ragged last tile)

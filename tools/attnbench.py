@@ -47,8 +47,15 @@ def case(B, N, H, bwd, it):
     gy = torch.randn(B * N, H * D, device="cuda", generator=g).bfloat16()
     flop = 4.0 * B * H * N * (N + 1) * D
     with torch.no_grad():
-        err = ((ops.mqa(q, kv, nkv, B, N, H, 1.0 / D).float() - reference(q, kv, nkv, B, N, H)).norm()
-               / reference(q, kv, nkv, B, N, H).norm()).item()
+        o = ops.mqa(q, kv, nkv, B, N, H, 1.0 / D).float()
+        ref = reference(q, kv, nkv, B, N, H)
+        err = ((o - ref).norm() / ref.norm()).item()
+        bad = ~torch.isfinite(o)
+        if bad.any():
+            rows = bad.reshape(B * N * H, D).any(-1).nonzero().flatten()
+            print(f"  non-finite: {bad.sum().item()} values in {rows.numel()} of {B * N * H} rows; "
+                  f"first rows {rows[:8].tolist()}; row % 256 histogram "
+                  f"{torch.bincount((rows % 256) // 32, minlength=8).tolist()}", flush=True)
 
     def fwd():
         with torch.no_grad():
