@@ -856,6 +856,172 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
               lse + (long long)b * R + row);
 }
 
+// ---- forward, ping-pong (round 4) ------------------------------------------
+// At d = 32 a key tile costs a wave as much VALU (16 v_exp at 8 issue cycles
+// each + the max / sum / pack) as MFMA (4 x 32 cycles), and the two do not
+// overlap inside one wave.  Here the two key halves of a workgroup are two
+// wave GROUPS that sit on every SIMD (waves w and w + 8 share one) and run
+// half an iteration apart, separated by workgroup barriers: while group 0 is
+// in its MFMA phase (score the next tile, PV of the current one), group 1 is
+// in its softmax phase (max, exp2, row sums, bf16 pack), then they swap.
+//   M(x): S_{x+1} = K_{x+1} Q^T (C operand -m: log2 units minus the max),
+//         O^T += V_x^T P_x^T
+//   V(x+1): mask, max, lazy rescale, P = exp2(S), l += sum, pack
+// Group 1 enters one barrier late; both run the same number of iterations
+// (the half with fewer tiles runs fully masked dummies).  STREAM: K / V
+// arrive in 512-key chunks by LDS-DMA into a double buffer (each wave issues
+// its pieces of chunk c + 1 at its first M phase of chunk c, when both groups
+// are past chunk c - 1, and drains them in the last two iterations of chunk
+// c); otherwise the whole clip's K / V are staged once.
+struct PPState {
+  f32x16 acc, negm, s;
+  bf16x8 p0, p1;
+  float m, l;
+};
+// kg: the tile's first key (a dummy passes kg = nkeys: every key masked)
+__device__ __forceinline__ void pp_softmax(PPState& st, int kg, int nkeys, int h) {
+  mask_keys(st.s, kg, nkeys, h);
+  const float mx = col_max(st.s);
+  const bool upd = mx > 8.f;
+  if (__builtin_amdgcn_ballot_w64(upd)) {
+    const float d = upd ? mx : 0.f;
+    const float a = ex2(-d);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      st.s[e] -= d;
+      st.acc[e] *= a;
+    }
+    st.l *= a;
+    st.m += d;
+    st.negm = bcast16(-st.m);
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) st.s[e] = ex2(st.s[e]);
+  st.l += sum16(st.s);
+  st.p0 = pack8(st.s, 0);
+  st.p1 = pack8(st.s, 1);
+}
+__device__ __forceinline__ void pp_mfma(PPState& st, const char* tKn, const char* tV, const FragOff& fo, bf16x8 q0,
+                                        bf16x8 q1) {
+  const bf16x8 k0 = row_at(tKn, fo, 0), k1 = row_at(tKn, fo, 1);
+  TrFrag vt = tr_issue(tV, fo);
+  bf16x8 v0, v1;
+  tr_wait(vt, v0, v1);
+  st.s = mma(k0, q0, st.negm);
+  st.acc = mma(v0, st.p0, st.acc);
+  st.s = mma(k1, q1, st.s);
+  st.acc = mma(v1, st.p1, st.acc);
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(NW * 64) void mqa_fwd_pp_kernel(const bf16* __restrict__ q,
+                                                             const bf16* __restrict__ kp,
+                                                             const bf16* __restrict__ vp,
+                                                             bf16* __restrict__ o, float* lse,
+                                                             int R, int NKP, int nkeys) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rg = wave & (RG - 1), g = wave / RG;  // g: key half = ping-pong group
+  const int b = blockIdx.y;
+  const int CK = STREAM ? SCK : NKP;  // keys per chunk
+  const int nch = (NKP + CK - 1) / CK;
+  const __amdgpu_buffer_rsrc_t rk = dma_rsrc(kp + (long long)b * NKP * 32, (unsigned)NKP * ROW);
+  const __amdgpu_buffer_rsrc_t rv = dma_rsrc(vp + (long long)b * NKP * 32, (unsigned)NKP * ROW);
+  auto buf_k = [&](int c) { return smem + (STREAM ? (c & 1) * 2 * SCK * ROW : 0); };
+  auto buf_v = [&](int c) { return smem + (STREAM ? (c & 1) * 2 * SCK * ROW : 0) + CK * ROW; };
+  dma_kv_chunk(rk, rv, buf_k(0), buf_v(0), 0, min(CK, NKP), wave, lane);
+  const int row = blockIdx.x * RG * 32 + rg * 32 + r;
+  const bool rok = row < R;
+  const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
+  const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const FragOff fo = frag_off(lane);
+  // this group's tiles of chunk c: [tb(c), tb(c) + it(c)), valid below te(c)
+  auto nkt_of = [&](int c) { return min(CK, NKP - c * CK) / 32; };
+  auto it_of = [&](int c) { return (nkt_of(c) + 1) / 2; };
+  auto tb_of = [&](int c) { return g ? it_of(c) : 0; };
+  auto te_of = [&](int c) { return g ? nkt_of(c) : it_of(c); };
+  // prologue: score + softmax of the group's first tile (chunk 0)
+  PPState st;
+  st.acc = zero16();
+  st.l = 0.f;
+  {
+    const int t0 = tb_of(0);
+    const bool dummy = t0 >= te_of(0);
+    const int tt = dummy ? te_of(0) - 1 : t0;
+    st.s = score(buf_k(0) + tt * 32 * ROW, fo, qf0, qf1, zero16());
+    mask_keys(st.s, dummy ? nkeys : tt * 32, nkeys, h);
+    st.m = col_max(st.s);  // the first tile is never a dummy for NKP >= 64
+#pragma unroll
+    for (int e = 0; e < 16; ++e) st.s[e] = ex2(st.s[e] - st.m);
+    st.l = sum16(st.s);
+    st.p0 = pack8(st.s, 0);
+    st.p1 = pack8(st.s, 1);
+    st.negm = bcast16(-st.m);
+  }
+  static_assert(NW == 16, "two groups of 8 waves");
+  if (g) {
+    __builtin_amdgcn_s_setprio(1);  // the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD" 4)
+    __builtin_amdgcn_s_barrier();   // half a step behind group 0
+  }
+  for (int c = 0; c < nch; ++c) {
+    const int its = it_of(c), tb = tb_of(c), te = te_of(c);
+    const char* sK = buf_k(c);
+    const char* sV = buf_v(c);
+    for (int i = 0; i < its; ++i) {
+      const int tcur = min(tb + i, te - 1);  // a dummy re-reads a valid tile (its P is zero)
+      // the next tile: this chunk's next, or the next chunk's first
+      const bool last_in_chunk = i + 1 == its;
+      const bool has_next_chunk = c + 1 < nch;
+      int tn;
+      const char* sKn;
+      bool ndummy;
+      int kgn;
+      if (!last_in_chunk) {
+        tn = tb + i + 1;
+        ndummy = tn >= te;
+        tn = ndummy ? te - 1 : tn;
+        sKn = sK;
+        kgn = c * CK + tn * 32;
+      } else if (has_next_chunk) {
+        const int tb2 = tb_of(c + 1), te2 = te_of(c + 1);
+        ndummy = tb2 >= te2;
+        tn = ndummy ? te2 - 1 : tb2;
+        sKn = buf_k(c + 1);
+        kgn = (c + 1) * CK + tn * 32;
+      } else {
+        tn = tcur;  // past the end: scored and discarded
+        ndummy = true;
+        sKn = sK;
+        kgn = 0;
+      }
+      if (STREAM && i == 0 && has_next_chunk)  // chunk c - 1 is read by nobody now
+        dma_kv_chunk(rk, rv, buf_k(c + 1), buf_v(c + 1), (c + 1) * CK, min(CK, NKP - (c + 1) * CK), wave, lane);
+      const bool drain = STREAM && has_next_chunk && i + 2 >= its;
+      // ---- M phase ----  (sched_barrier: hipcc would move MFMAs / VALU across s_barrier)
+      pp_mfma(st, sKn + tn * 32 * ROW, sV + tcur * 32 * ROW, fo, qf0, qf1);
+      if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- V phase (the next tile's softmax) ----
+      pp_softmax(st, ndummy ? nkeys : kgn, nkeys, h);
+      if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (!g) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_s_setprio(0);
+  // the last V phase scored a tile past the end: its P was never used
+  Soft fin{st.acc, st.negm, st.m, st.l};
+  soft_finish(fin, (float*)smem + rg * 18 * 64, g, lane, h, rok, o + ((long long)b * R + row) * 32,
+              lse + (long long)b * R + row);
+}
+
 // dq (query-major, as the forward: key halves summed through LDS) and
 // D = rowsum(dO * O) for the dk/dv pass.  Both per-row constants enter as C
 // operands: S^T arrives as c s - L (keys pre-scaled by c), dP^T as dP - D, so
@@ -1165,6 +1331,22 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
     static const bool force_stream = getenv("DV_MQA_STREAM") && atoi(getenv("DV_MQA_STREAM")) != 0;
     static const bool pair = !getenv("DV_MQA_PAIR") || atoi(getenv("DV_MQA_PAIR")) != 0;
     const dim3 grid((R + 255) / 256, B);
+    // DV_MQA_PP=1: the ping-pong kernel (two wave groups per SIMD) instead of the single-group ones
+    static const bool pp = getenv("DV_MQA_PP") && atoi(getenv("DV_MQA_PP")) != 0;
+    if (pp && NKP >= 64) {
+      const bool whole = fa::eligible(dtype, ldq, ldo, H, NKP) && !force_stream;
+      DV_REQUIRE((long long)NKP * fa::ROW < (1ll << 31), "sequence too long");
+      const int lds = whole ? max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4) : 4 * fa::SCK * fa::ROW;
+      const void* fn = whole ? (const void*)fa::mqa_fwd_pp_kernel<false> : (const void*)fa::mqa_fwd_pp_kernel<true>;
+      fa::set_lds(fn, lds);
+      if (whole)
+        fa::mqa_fwd_pp_kernel<false><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
+                                                                    (bf16*)o, lse, R, NKP, N + 1);
+      else
+        fa::mqa_fwd_pp_kernel<true><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
+                                                                   (bf16*)o, lse, R, NKP, N + 1);
+      return check_launch("mqa_fwd");
+    }
     if (fa::eligible(dtype, ldq, ldo, H, NKP) && !force_stream) {
       const int lds = max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4);
       const void* fn = pair ? (const void*)fa::mqa_fwd_fa_kernel<true> : (const void*)fa::mqa_fwd_fa_kernel<false>;
