@@ -101,6 +101,8 @@ struct ConvFwdArgs {
   // ticket in ks_flag (zero between launches)
   float* ks_part;
   int* ks_flag;
+  int* ks_err;   // count of hand-offs whose halves sat on different XCDs (must stay 0)
+  int ks_local;  // 1: XCD-local hand-off (no L2 write-back; blocks b, b + 8 share an L2)
 };
 
 // GroupNorm statistics of a wave's tile, register-light: every lane holds
@@ -2323,13 +2325,35 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
         *(f32x4*)(mine + 1024 + e4 * 256 + lane * 4) =
             f32x4{acc1[4 * e4], acc1[4 * e4 + 1], acc1[4 * e4 + 2], acc1[4 * e4 + 3]};
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's stores out of its L2
-    __syncthreads();
     int* tk = (int*)smem;
-    if (threadIdx.x == 0) *tk = __hip_atomic_fetch_add(p.ks_flag + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (*tk == 0) return;  // the other half finishes the tile
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (p.ks_local) {
+      // XCD-local: round-robin dispatch puts blocks b and b + 8 on one XCD, so
+      // the partner reads this partial from the L2 both share; waiting for the
+      // stores' acknowledgement replaces the agent-scope release (a write-back
+      // of the whole L2, which cost more than the split gained).  The ticket
+      // carries the XCD id: a partner elsewhere is counted in ks_err.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        x &= 15;
+        const int t = __hip_atomic_fetch_add(p.ks_flag + tile, 1 + (x << 4), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        if (t != 0 && (t >> 4) != x) __hip_atomic_fetch_add(p.ks_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *tk = t;
+      }
+      __syncthreads();
+      if (*tk == 0) return;  // the other half finishes the tile
+      asm volatile("buffer_inv sc0" ::: "memory");  // no stale L1 line of the partner's partial
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's stores out of its L2
+      __syncthreads();
+      if (threadIdx.x == 0) *tk = __hip_atomic_fetch_add(p.ks_flag + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (*tk == 0) return;  // the other half finishes the tile
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
     const float* other = p.ks_part + ((long long)tile * 2 + (kh ^ 1)) * PART + wave * (2 * 16 * 64);
 #pragma unroll
     for (int e4 = 0; e4 < 4; ++e4) {
@@ -2342,7 +2366,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
         for (int k = 0; k < 4; ++k) acc1[4 * e4 + k] += o1[k];
       }
     }
-    if (threadIdx.x == 0) p.ks_flag[tile] = 0;  // ready for the next launch
+    if (threadIdx.x == 0) __hip_atomic_store(p.ks_flag + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();  // the ticket word is LDS the statistics epilogue reuses
   }
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e.  Bias and
@@ -2461,17 +2485,24 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   // grids of <= 128 64-channel tiles (half the CUs): the chunk loop split in
   // two workgroups per tile (KSPL = 2) when the caller registered scratch
   // (DV_FRAME_KSPLIT=0: off); otherwise 32-channel tiles (DV_FRAME_CO32=0: off)
-  // opt-in: measured 104.0 -> 100.6 steps/s on (gpurun_out/ks_r04a): the agent-scope release of
-  // the partial (an L2 write-back) costs more than the idle CUs it fills
+  // opt-in: measured 104.0 -> 100.6 steps/s (gpurun_out/ks_r04a): the agent-scope release of
+  // the partial (an L2 write-back) costs more than the idle CUs it fills; the XCD-local
+  // hand-off (=2) removes that cost and still loses per launch to the 32-channel tiles
+  // (13.7 vs 11.1 us, 16.3 vs 13.2 us with statistics; step 102.8 vs 102.9,
+  // profiles/r04f_ksplit_xcd_local_ab.txt)
   static const bool ks_ok = getenv("DV_FRAME_KSPLIT") && atoi(getenv("DV_FRAME_KSPLIT")) != 0;
+  // DV_FRAME_KSPLIT=2: the XCD-local hand-off (no agent-scope release)
+  static const int ks_local = ks_ok && atoi(getenv("DV_FRAME_KSPLIT")) == 2 ? 1 : 0;
   // DV_FRAME_KS256=1: also split the 256-tile grids, two workgroups per CU on
   // a 2-deep ring (A/B)
   static const bool ks256 = getenv("DV_FRAME_KS256") && atoi(getenv("DV_FRAME_KS256")) != 0;
   if (ks_ok && ks256 && tiles64 == 256 && a.W == 8 && (a.cin / 16) % 2 == 0) {
     KsScratch* ks = ks_scratch();
-    if (ks && ks->nflags >= tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {
+    if (ks && ks->nflags > tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {
       a.ks_part = ks->part;
       a.ks_flag = ks->flags;
+      a.ks_err = ks->flags + ks->nflags - 1;
+      a.ks_local = ks_local;
       a.xcd_c = frame_xcd_split(a, 64);
       const int nb2 = 2 * tiles64;
       if (a.c0 < a.cin)
@@ -2485,9 +2516,11 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   }
   if (ks_ok && tiles64 <= 128 && tiles64 % 8 == 0 && (a.cin / 16) % 2 == 0) {
     KsScratch* ks = ks_scratch();
-    if (ks && ks->nflags >= tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {
+    if (ks && ks->nflags > tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {
       a.ks_part = ks->part;
       a.ks_flag = ks->flags;
+      a.ks_err = ks->flags + ks->nflags - 1;
+      a.ks_local = ks_local;
       a.xcd_c = frame_xcd_split(a, 64);
       const int nb2 = 2 * tiles64;
 #define DV_FK(WW, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, 64, SP, 4, 2><<<nb2, 256, 0, st>>>(a) \

@@ -63,11 +63,12 @@ class KernelTimer:
         out = {}
         for name, shape, fl, nb, s, e in self.records:
             d = out.setdefault((name, shape) if by_shape else name,
-                               dict(count=0, flops=0.0, bytes=0.0, ms=0.0))
+                               dict(count=0, flops=0.0, bytes=0.0, ms=0.0, ms_raw=0.0))
             d["count"] += 1
             d["flops"] += fl
             d["bytes"] += nb
             d["ms"] += max(s.elapsed_time(e) - ovh, 1e-4)
+            d["ms_raw"] += s.elapsed_time(e)
         return out
 
 

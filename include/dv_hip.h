@@ -160,7 +160,9 @@ int dv_conv_small_fwd(const void* x0, int ld0, int c0, const void* x1, int ld1, 
  * device, registered once before its first launch: grids of <= 128 64-channel
  * tiles split the chunk loop over two workgroups per tile, which hand their
  * f32 partial sums through `part` (64 KB per tile) and a per-tile ticket in
- * `flags` (zeroed by the caller at registration; the kernel leaves them zero).
+ * `flags` (zeroed by the caller at registration; the kernel leaves them zero;
+ * the LAST flag counts XCD-local hand-offs whose halves ran on different XCDs,
+ * DV_FRAME_KSPLIT=2, and must stay 0).  The split is opt-in (DV_FRAME_KSPLIT).
  * Launches using it must be ordered (one stream).  part = flags = NULL
  * unregisters (no K split).                                                */
 int dv_conv_scratch(void* part, long long bytes, int* flags, int nflags);

@@ -91,6 +91,10 @@ def test_conv_fwd_bwd(case, dtype, tol):
     assert rel(dx.float(), xr.grad) < tol * 2
     assert rel(wd.grad, wr.grad) < tol * 2
     assert rel(bd.grad, br.grad) < tol
+    # the window conv's K split (DV_FRAME_KSPLIT=2): no hand-off across XCDs
+    ks = ops._KS_SCRATCH.get(str(torch.device(dev, torch.cuda.current_device())))
+    if ks is not None:
+        assert int(ks[1][-1]) == 0, "K-split halves on different XCDs"
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
