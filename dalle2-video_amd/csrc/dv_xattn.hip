@@ -25,6 +25,26 @@
 
 using namespace dv;
 
+// Diagnostic build only (make stamp): per-workgroup s_memrealtime stamps of
+// the cross-attention kernels' phases (tools/xattn_stamp.py)
+#ifdef DV_STAMP
+constexpr int XA_NSTAMP = 8;
+__device__ unsigned long long g_xa_stamp[16384 * XA_NSTAMP];
+#define XA_STAMP_AT(i)                                                                         \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 16384)                                                \
+      g_xa_stamp[blockIdx.x * XA_NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime();             \
+  } while (0)
+extern "C" int dv_debug_stamps_xattn(unsigned long long* host, long long n) {
+  if (n > 16384 * XA_NSTAMP) n = 16384 * XA_NSTAMP;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_xa_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#else
+#define XA_STAMP_AT(i) \
+  do {                 \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr int NH = 8, DH = 64, NK = 3, HK = NH * NK;  // 24 folded columns
@@ -282,7 +302,7 @@ __device__ __forceinline__ void xwave_sum(float* v, int n, float* sh, int cw, in
 }
 
 template <typename T, int CS, int NCT>
-__global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* out, int ldo,
+__global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_fwd_kernel(const T* x, int ldx, T* out, int ldo,
                                                         long long ntok, long long P, int C,
                                                         const T* Kt, const T* Vt,
                                                         const float* colsum, const float* g2,
@@ -301,6 +321,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
   const bool valid = tin < P;
   const bool lead = cw == 0;  // stores the per-token outputs shared by the channel groups
   const long long tok = (long long)b * P + (valid ? tin : P - 1);
+  XA_STAMP_AT(0);
   const T* xr = x + tok * ldx;
   const int Cp = (C + 31) / 32 * 32;
   const T* Ktb = Kt + (long long)b * KP * Cp;
@@ -340,6 +361,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
     for (int e = 0; e < VEC; ++e) { sx += f[e]; sxx += f[e] * f[e]; }
     acc = Mma<T>::run(kv, xv, acc);
   }
+  XA_STAMP_AT(1);
   if (CS > 1) {
     float v[XRS];
 #pragma unroll
@@ -352,6 +374,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
     sx = v[16];
     sxx = v[17];
   }
+  XA_STAMP_AT(2);
   sx += __shfl_xor(sx, 32, 64);
   sxx += __shfl_xor(sxx, 32, 64);
   const float mu = sx / C;
@@ -377,6 +400,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
     float pw[4] = {(float)pt[0], (float)pt[1], (float)pt[2], (float)pt[3]};
     if (valid && lead) st4<T>(pbuf + tok * KP + 8 * m + 4 * h, pw);
   }
+  XA_STAMP_AT(3);
   // ---- o statistics (pass 1), then the normalised output + residual (pass 2) ----
   float so = 0.f, soo = 0.f;
 #pragma unroll
@@ -397,6 +421,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
     so = v[0];
     soo = v[1];
   }
+  XA_STAMP_AT(4);
   so += __shfl_xor(so, 32, 64);
   soo += __shfl_xor(soo, 32, 64);
   const float mu2 = so / C;
@@ -429,6 +454,12 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
     }
   }
   if (h == 0 && valid && lead) *(f32x4*)(stats + tok * 4) = f32x4{mu, rs, mu2, rs2};
+  XA_STAMP_AT(5);
+#ifdef DV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  XA_STAMP_AT(6);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -439,7 +470,7 @@ __global__ __launch_bounds__(256) void xattn_fwd_kernel(const T* x, int ldx, T* 
 //    it equals (1/C) sum_c R[b][k'][c], the row sums of the R = dS'^T X GEMM)
 // ---------------------------------------------------------------------------
 template <typename T, int CS, int NCT>
-__global__ __launch_bounds__(256) void xattn_bwd_kernel(const T* dy, int lddy, const T* x, int ldx,
+__global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T* dy, int lddy, const T* x, int ldx,
                                                         T* dx, int lddx, long long ntok,
                                                         long long P, int C, const T* KtT,
                                                         const T* Vt, const T* VtT,
@@ -942,6 +973,14 @@ static long long xa_split_tiles() {
   static const long long v = getenv("DV_XA_SPLIT_TILES") ? atoll(getenv("DV_XA_SPLIT_TILES")) : 1024;
   return v;
 }
+// 8 waves per tile (512-thread workgroups) for the grids of <= 256 tiles whose
+// channels split 8 ways (the 8x8 stage at 256 / 512 channels: each wave's serial
+// channel chain halves; DV_XA_CS8=0: 4 waves)
+static int xa_cs(long long tiles, int C, bool split) {
+  static const bool cs8 = !(getenv("DV_XA_CS8") && atoi(getenv("DV_XA_CS8")) == 0);
+  if (!split) return 1;
+  return cs8 && tiles <= 256 && C % 256 == 0 ? 8 : 4;
+}
 
 // unrolled channel-loop trips: 32-channel tiles per wave (0 if above 8)
 static int xa_nct(int C, int cs) {
@@ -968,20 +1007,22 @@ extern "C" int dv_xattn_fwd(int dtype, const void* x, int ldx, void* out, int ld
   hipStream_t st = (hipStream_t)stream;
   const long long tiles = (ntok / P) * ((P + 31) / 32);
   const bool split = tiles < xa_split_tiles() && C >= 128;  // fewer than 256 four-wave workgroups otherwise
+  const int cs = xa_cs(tiles, C, split);
   const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
-  const int nct = xa_nct(C, split ? 4 : 1), ex = xa_exact(C, split ? 4 : 1);
+  const int nct = xa_nct(C, cs), ex = xa_exact(C, cs);
   DV_REQUIRE(nct > 0, "C too large for the channel loop (Cp / (32 * CS) <= 8)");
 #define XF_LAUNCH(T, CS, N)                                                                         \
-  xattn_fwd_kernel<T, CS, N><<<blocks, 256, 0, st>>>((const T*)x, ldx, (T*)out, ldo, ntok, P, C,  \
-                                                     (const T*)Kt, (const T*)Vt, colsum, g2, eps,  \
-                                                     stats, (T*)pbuf)
+  xattn_fwd_kernel<T, CS, N><<<blocks, CS == 8 ? 512 : 256, 0, st>>>(                              \
+      (const T*)x, ldx, (T*)out, ldo, ntok, P, C, (const T*)Kt, (const T*)Vt, colsum, g2, eps,      \
+      stats, (T*)pbuf)
 #define XF_DISPATCH(T)                                                                 \
-  switch ((split ? 16 : 0) + ex) {                                                     \
+  switch ((cs == 8 ? 32 : split ? 16 : 0) + ex) {                                      \
     case 1: XF_LAUNCH(T, 1, 1); break;  case 2: XF_LAUNCH(T, 1, 2); break;             \
     case 4: XF_LAUNCH(T, 1, 4); break;  case 8: XF_LAUNCH(T, 1, 8); break;             \
     case 17: XF_LAUNCH(T, 4, 1); break; case 18: XF_LAUNCH(T, 4, 2); break;            \
     case 20: XF_LAUNCH(T, 4, 4); break; case 24: XF_LAUNCH(T, 4, 8); break;            \
-    default: if (split) XF_LAUNCH(T, 4, 0); else XF_LAUNCH(T, 1, 0); break;            \
+    case 33: XF_LAUNCH(T, 8, 1); break; case 34: XF_LAUNCH(T, 8, 2); break;            \
+    default: if (cs == 8) XF_LAUNCH(T, 8, 0); else if (split) XF_LAUNCH(T, 4, 0); else XF_LAUNCH(T, 1, 0); break; \
   }
   if (dtype == DV_BF16) {
     XF_DISPATCH(bf16);
@@ -1005,19 +1046,21 @@ extern "C" int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const vo
   hipStream_t st = (hipStream_t)stream;
   const long long tiles = (ntok / P) * ((P + 31) / 32);
   const bool split = tiles < xa_split_tiles() && C >= 128;
+  const int cs = xa_cs(tiles, C, split);
   const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
 #define XB_ARGS(T) (const T*)dy, lddy, (const T*)x, ldx, (T*)dx, lddx, ntok, P, C, (const T*)KtT, \
     (const T*)Vt, (const T*)VtT, colsum, g2, stats, (const T*)pbuf, (T*)dobuf, (T*)dsbuf, (T*)p2buf
-  const int nct = xa_nct(C, split ? 4 : 1), ex = xa_exact(C, split ? 4 : 1);
+  const int nct = xa_nct(C, cs), ex = xa_exact(C, cs);
   DV_REQUIRE(nct > 0, "C too large for the channel loop (Cp / (32 * CS) <= 8)");
-#define XB_LAUNCH(T, CS, N) xattn_bwd_kernel<T, CS, N><<<blocks, 256, 0, st>>>(XB_ARGS(T))
+#define XB_LAUNCH(T, CS, N) xattn_bwd_kernel<T, CS, N><<<blocks, CS == 8 ? 512 : 256, 0, st>>>(XB_ARGS(T))
 #define XB_DISPATCH(T)                                                                 \
-  switch ((split ? 16 : 0) + ex) {                                                     \
+  switch ((cs == 8 ? 32 : split ? 16 : 0) + ex) {                                      \
     case 1: XB_LAUNCH(T, 1, 1); break;  case 2: XB_LAUNCH(T, 1, 2); break;             \
     case 4: XB_LAUNCH(T, 1, 4); break;  case 8: XB_LAUNCH(T, 1, 8); break;             \
     case 17: XB_LAUNCH(T, 4, 1); break; case 18: XB_LAUNCH(T, 4, 2); break;            \
     case 20: XB_LAUNCH(T, 4, 4); break; case 24: XB_LAUNCH(T, 4, 8); break;            \
-    default: if (split) XB_LAUNCH(T, 4, 0); else XB_LAUNCH(T, 1, 0); break;            \
+    case 33: XB_LAUNCH(T, 8, 1); break; case 34: XB_LAUNCH(T, 8, 2); break;            \
+    default: if (cs == 8) XB_LAUNCH(T, 8, 0); else if (split) XB_LAUNCH(T, 4, 0); else XB_LAUNCH(T, 1, 0); break; \
   }
   if (dtype == DV_BF16) {
     XB_DISPATCH(bf16);
