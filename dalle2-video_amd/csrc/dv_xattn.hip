@@ -104,6 +104,15 @@ __device__ __forceinline__ void ld_afrag(const bf16* A, int lda, int r, int h, u
     a[s] = u32x4{lo[0], lo[1], hi[0], hi[1]};
   }
 }
+// ld_afrag from an LDS image (row stride lda bf16)
+__device__ __forceinline__ void ld_afrag_lds(const bf16* A, int lda, int r, int h, u32x4 (&a)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const u32x2 lo = *(const u32x2*)(A + r * lda + 16 * s + 4 * h);
+    const u32x2 hi = *(const u32x2*)(A + r * lda + 16 * s + 8 + 4 * h);
+    a[s] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+  }
+}
 __device__ __forceinline__ f32x16 mm_acc_f(const u32x4 (&a)[2], const f32x16& X, f32x16 acc) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -312,6 +321,11 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_fwd_kernel(const T*
   // waves tile each batch element's P tokens; lanes past P mirror token P-1
   // (their MFMA columns are independent) and store nothing
   __shared__ float xred[CS == 1 ? 1 : CS * XRS * 64];
+  // LN_out gain staged in LDS: a global load between the output stores would
+  // wait for every earlier store (vmcnt retires in order); LDS reads do not
+  __shared__ float g2s[256 * CS];  // C <= 32 * 8 * CS (host-checked)
+  for (int i = threadIdx.x; i < C; i += 64 * (CS == 8 ? 8 : 4)) g2s[i] = g2[i];
+  __syncthreads();
   const int cw = CS == 1 ? 0 : (threadIdx.x >> 6);  // channel group of this wave
   const long long wpb = (P + 31) / 32;
   const long long wv = CS == 1 ? (long long)blockIdx.x * 4 + (threadIdx.x >> 6) : (long long)blockIdx.x;
@@ -322,6 +336,12 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_fwd_kernel(const T*
   const bool lead = cw == 0;  // stores the per-token outputs shared by the channel groups
   const long long tok = (long long)b * P + (valid ? tin : P - 1);
   XA_STAMP_AT(0);
+  // the colsum terms of the softmax, loaded with the first batch (before any store)
+  float csr[4][3];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) csr[m][j] = colsum[b * KP + 8 * m + 4 * h + j];
   const T* xr = x + tok * ldx;
   const int Cp = (C + 31) / 32 * 32;
   const T* Ktb = Kt + (long long)b * KP * Cp;
@@ -386,8 +406,7 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_fwd_kernel(const T*
     float s3[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const int kp = 8 * m + 4 * h + j;
-      s3[j] = rs * (acc[4 * m + j] - mu * colsum[b * KP + kp]);
+      s3[j] = rs * (acc[4 * m + j] - mu * csr[m][j]);
     }
     const float mx = fmaxf(s3[0], fmaxf(s3[1], s3[2]));
     const float e0 = __expf(s3[0] - mx), e1 = __expf(s3[1] - mx), e2 = __expf(s3[2] - mx);
@@ -447,7 +466,7 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_fwd_kernel(const T*
       } else {
         ld4<T>(xr + c, xv);
       }
-      const f32x4 gg = *(const f32x4*)(g2 + c);
+      const f32x4 gg = *(const f32x4*)(g2s + c);
 #pragma unroll
       for (int e = 0; e < 4; ++e) y[e] = (o[4 * g + e] - mu2) * rs2 * gg[e] + xv[e];
       if (valid) st4<T>(orow + c, y);
@@ -470,7 +489,7 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_fwd_kernel(const T*
 //    it equals (1/C) sum_c R[b][k'][c], the row sums of the R = dS'^T X GEMM)
 // ---------------------------------------------------------------------------
 template <typename T, int CS, int NCT>
-__global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T* dy, int lddy, const T* x, int ldx,
+__global__ __launch_bounds__(CS == 8 ? 512 : 256, CS == 8 ? 1 : 2) void xattn_bwd_kernel(const T* dy, int lddy, const T* x, int ldx,
                                                         T* dx, int lddx, long long ntok,
                                                         long long P, int C, const T* KtT,
                                                         const T* Vt, const T* VtT,
@@ -481,15 +500,49 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
   // waves tile each batch element's P tokens; lanes past P mirror token P-1
   // (their MFMA columns are independent) and store nothing
   __shared__ float xred[CS == 1 ? 1 : CS * XRS * 64];
-  const int cw = CS == 1 ? 0 : (threadIdx.x >> 6);  // channel group of this wave
+  __shared__ float g2s[256 * CS];  // LN_out gain in LDS (see the forward)
+  constexpr int NTH = 64 * (CS == 8 ? 8 : 4);
+  for (int i = threadIdx.x; i < C; i += NTH) g2s[i] = g2[i];
   const long long wpb = (P + 31) / 32;
-  const long long wv = CS == 1 ? (long long)blockIdx.x * 4 + (threadIdx.x >> 6) : (long long)blockIdx.x;
-  if (wv >= (ntok / P) * wpb) return;  // uniform per workgroup when CS > 1
-  const int b = (int)(wv / wpb);
-  const long long tin = (wv % wpb) * 32 + r;
+  // workgroups never straddle two clips: CS = 1 takes 4 consecutive tiles of
+  // one clip (bpc workgroups per clip), CS > 1 one tile
+  const long long bpc = CS == 1 ? (wpb + 3) / 4 : wpb;
+  const int b = (int)(blockIdx.x / bpc);
+  const long long tic = CS == 1 ? (blockIdx.x % bpc) * 4 + (threadIdx.x >> 6) : blockIdx.x % bpc;
+  const bool clip_ok = b < ntok / P;
+  // exact-trip bf16: the clip's Vt^T (KP x Cp) and Kt^T (Cp x KP) operand
+  // images and its colsum staged in LDS once per workgroup (rows padded
+  // against bank conflicts)
+  constexpr bool STAGE = NCT > 0 && NCT <= 4 && sizeof(T) == 2;  // the CACHE path below
+  constexpr int CPS = 32 * (NCT > 0 ? NCT : 1) * CS;  // Cp of the exact path
+  constexpr int SV_LD = CPS + 8, SK_LD = KP + 8;      // bf16 row strides
+  __shared__ __attribute__((aligned(16))) bf16 sfr[STAGE ? KP * SV_LD + CPS * SK_LD : 8];
+  __shared__ float scs[KP];
+  bf16* const sVtT = sfr;
+  bf16* const sKtT = sfr + KP * SV_LD;
+  if (clip_ok) {
+    if (threadIdx.x < KP) scs[threadIdx.x] = colsum[b * KP + threadIdx.x];
+    if constexpr (STAGE) {
+      const bf16* gv = (const bf16*)VtT + (long long)b * KP * CPS;
+      const bf16* gk = (const bf16*)KtT + (long long)b * CPS * KP;
+      for (int i = threadIdx.x; i < KP * CPS / 8; i += NTH) {  // 16-B pieces
+        const int row = i / (CPS / 8), col = (i % (CPS / 8)) * 8;
+        *(u32x4*)(sVtT + row * SV_LD + col) = *(const u32x4*)(gv + (long long)row * CPS + col);
+      }
+      for (int i = threadIdx.x; i < CPS * KP / 8; i += NTH) {
+        const int row = i / (KP / 8), col = (i % (KP / 8)) * 8;
+        *(u32x4*)(sKtT + row * SK_LD + col) = *(const u32x4*)(gk + (long long)row * KP + col);
+      }
+    }
+  }
+  __syncthreads();
+  const int cw = CS == 1 ? 0 : (threadIdx.x >> 6);  // channel group of this wave
+  if (!clip_ok || tic >= wpb) return;  // uniform per wave (per workgroup when CS > 1)
+  const long long tin = tic * 32 + r;
   const bool valid = tin < P;
   const bool lead = cw == 0;
   const long long tok = (long long)b * P + (valid ? tin : P - 1);
+  XA_STAMP_AT(0);
   const T* xr = x + tok * ldx;
   const T* dyr = dy + tok * lddy;
   const int Cp = (C + 31) / 32 * 32;
@@ -554,7 +607,7 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
       if (NCT == 0 && c >= C) continue;
       float dv[4];
       ld_dy(it, g, c, dv);
-      const f32x4 gg = *(const f32x4*)(g2 + c);
+      const f32x4 gg = *(const f32x4*)(g2s + c);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float doh = dv[e] * gg[e];
@@ -571,7 +624,10 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
   }
   m1 = (m1 + __shfl_xor(m1, 32, 64)) / C;
   m2 = (m2 + __shfl_xor(m2, 32, 64)) / C;
+  XA_STAMP_AT(1);
   // ---- pass B: dO (stored) and dP^T = Vt^T . dO^T ----
+  // (staged: the Vt^T fragments come from LDS -- a global load behind the dO
+  // stores would wait for them, vmcnt retiring in order)
   f32x16 dp;
 #pragma unroll
   for (int e = 0; e < 16; ++e) dp[e] = 0.f;
@@ -595,7 +651,7 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
       }
       float dv[4], w[4];
       ld_dy(it, g, c, dv);
-      const f32x4 gg = *(const f32x4*)(g2 + c);
+      const f32x4 gg = *(const f32x4*)(g2s + c);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float oh = (o[4 * g + e] - mu2) * rs2;
@@ -605,7 +661,13 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
       }
       if (valid) st4<T>(dobuf + tok * C + c, w);
     }
-    dp = mm_acc_g<T>(VtTb + ct, Cp, dO, dp, r, h);
+    if constexpr (STAGE) {
+      u32x4 a[2];
+      ld_afrag_lds(sVtT + ct, SV_LD, r, h, a);
+      dp = mm_acc_f(a, dO, dp);
+    } else {
+      dp = mm_acc_g<T>(VtTb + ct, Cp, dO, dp, r, h);
+    }
   }
   if (CS > 1) {
     float v[16];
@@ -615,6 +677,7 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
 #pragma unroll
     for (int e = 0; e < 16; ++e) dp[e] = v[e];
   }
+  XA_STAMP_AT(2);
   // ---- softmax backward (lane-local heads) ----
   f32x16 ds;
   float a1 = 0.f, a2 = 0.f;
@@ -627,7 +690,7 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
       const int kp = 8 * m + 4 * h + j;
       const float d = j < 3 ? p[4 * m + j] * (dp[4 * m + j] - sd) : 0.f;
       ds[4 * m + j] = d;
-      a1 += d * colsum[b * KP + kp];
+      a1 += d * scs[kp];  // d = 0 at j = 3
       if (j < 3 && p[4 * m + j] > 0.f) a2 += d * __logf(p[4 * m + j]);
       w[j] = rs * d;
       q[j] = j < 3 ? rs2 * p[4 * m + j] : (kp == 3 ? mu2 * rs2 : 0.f);
@@ -637,6 +700,7 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
   }
   a1 = (a1 + __shfl_xor(a1, 32, 64)) / C;  // mean_c dxhat
   a2 = (a2 + __shfl_xor(a2, 32, 64)) / C;  // mean_c dxhat*xhat
+  XA_STAMP_AT(3);
   // ---- pass C: dXhat^T = KtT . dS^T, LN_in backward + residual ----
   T* dxr = dx + tok * lddx;
 #pragma unroll
@@ -646,7 +710,13 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
     f32x16 dxh;
 #pragma unroll
     for (int e = 0; e < 16; ++e) dxh[e] = 0.f;
-    dxh = mm_acc_g<T>(KtTb + (long long)ct * KP, KP, ds, dxh, r, h);
+    if constexpr (STAGE) {
+      u32x4 a[2];
+      ld_afrag_lds(sKtT + ct * SK_LD, SK_LD, r, h, a);
+      dxh = mm_acc_f(a, ds, dxh);
+    } else {
+      dxh = mm_acc_g<T>(KtTb + (long long)ct * KP, KP, ds, dxh, r, h);
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = ct + 8 * g + 4 * h;
@@ -662,6 +732,12 @@ __global__ __launch_bounds__(CS == 8 ? 512 : 256) void xattn_bwd_kernel(const T*
       if (valid) st4<T>(dxr + c, w);
     }
   }
+  XA_STAMP_AT(4);
+#ifdef DV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  XA_STAMP_AT(5);
+#endif
 }
 
 // mcorr[b][k'] = (1/C) sum_c R[b][k'][c]  (= sum_t mu_t * dS'_tk', mu_t the
@@ -1047,7 +1123,8 @@ extern "C" int dv_xattn_bwd_tokens(int dtype, const void* dy, int lddy, const vo
   const long long tiles = (ntok / P) * ((P + 31) / 32);
   const bool split = tiles < xa_split_tiles() && C >= 128;
   const int cs = xa_cs(tiles, C, split);
-  const int blocks = (int)(split ? tiles : (tiles + 3) / 4);
+  // one clip per workgroup (the kernel stages the clip's operand images)
+  const int blocks = (int)(split ? tiles : (ntok / P) * (((P + 31) / 32 + 3) / 4));
 #define XB_ARGS(T) (const T*)dy, lddy, (const T*)x, ldx, (T*)dx, lddx, ntok, P, C, (const T*)KtT, \
     (const T*)Vt, (const T*)VtT, colsum, g2, stats, (const T*)pbuf, (T*)dobuf, (T*)dsbuf, (T*)p2buf
   const int nct = xa_nct(C, cs), ex = xa_exact(C, cs);

@@ -4,9 +4,10 @@ dalle2-video_amd/csrc stamp; DV_STAMP in dv_xattn.hip):
 
   DV_HIP_LIB=dalle2-video_amd/csrc/build_stamp/libdv_hip_stamp.so python tools/xattn_stamp.py
 
-Stamps: 0 entry, 1 channel loop (scores + LN sums) issued, 2 cross-wave sums
-done, 3 softmax + P stored, 4 output statistics summed, 5 output stores
-issued, 6 stores drained.  s_memrealtime ticks at 100 MHz."""
+Forward stamps: 0 entry, 1 channel loop (scores + LN sums) issued, 2 cross-wave
+sums done, 3 softmax + P stored, 4 output statistics summed, 5 output stores
+issued, 6 stores drained.  Backward: 0 entry, 1 pass A (LN_out statistics),
+2 pass B (dO stored, dP), 3 softmax backward, 4 pass C (dx stored), 5 drained.  s_memrealtime ticks at 100 MHz."""
 import ctypes
 import os
 import sys
@@ -54,9 +55,15 @@ def case(nf, h, w, C, nb):
     wkv = torch.randn(1024, 64, device="cuda", generator=g) / 8
     wo = torch.randn(C, 512, device="cuda", generator=g) / 512 ** 0.5
 
+    xg = x.clone().requires_grad_()
+    gy = torch.randn_like(x)
+
     def run():
         with torch.no_grad():
             ops.cross_attention(x, ctx, g1, null_kv, wq, wkv, wo, g2, nb, 1e-5)
+
+    def run_bwd():
+        ops.cross_attention(xg, ctx, g1, null_kv, wq, wkv, wo, g2, nb, 1e-5).backward(gy)
 
     for _ in range(3):
         run()
@@ -71,6 +78,9 @@ def case(nf, h, w, C, nb):
     split = tiles < 1024 and C >= 128
     nblk = tiles if split else (tiles + 3) // 4
     report(f"xattn fwd {nf}x{h}x{w}x{C}", stamps(nblk), [0, 1, 2, 3, 4, 5, 6], s0.elapsed_time(s1) * 1e3)
+    for _ in range(2):
+        run_bwd()
+    report(f"xattn bwd {nf}x{h}x{w}x{C}", stamps(nblk), [0, 1, 2, 3, 4, 5], 0.0)
 
 
 if __name__ == "__main__":
