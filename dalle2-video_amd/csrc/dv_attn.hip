@@ -336,6 +336,58 @@ __global__ void mqa_prep_kernel(const T* kv, int ldkv, const float* null_kv, T* 
   }
 }
 
+// bf16 prep, grid (ceil(NKP / 64), B): 64 key rows per block, 4 threads per
+// row (8 dims of k and of v each, 16-B loads when the kv rows allow them):
+// the rows of mqa_prep_kernel plus each block's largest key norm |k'| (log2
+// units) in kmax[b * gridDim.x + block] -- the forward bounds every score by
+// |q| max|k'|
+constexpr int PREP_KEYS = 64;
+__global__ __launch_bounds__(256) void mqa_prep_rows_kernel(const bf16* kv, int ldkv, const float* null_kv,
+                                                            bf16* kp, bf16* vp, int N, int NKP, float kscale,
+                                                            float* kmax) {
+  __shared__ float red[4];
+  const int b = blockIdx.y, key = blockIdx.x * PREP_KEYS + (threadIdx.x >> 2), d0 = (threadIdx.x & 3) * 8;
+  float n2 = 0.f;
+  if (key < NKP) {
+    float kf[8], vf[8];
+    if (key == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { kf[j] = null_kv[d0 + j]; vf[j] = null_kv[DH + d0 + j]; }
+    } else if (key <= N) {
+      const bf16* row = kv + ((long long)b * N + key - 1) * ldkv;
+      if ((reinterpret_cast<unsigned long long>(row + d0) & 15) == 0) {  // 16-B aligned rows
+        const bf16x8 k8 = *(const bf16x8*)(row + d0), v8 = *(const bf16x8*)(row + DH + d0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { kf[j] = (float)k8[j]; vf[j] = (float)v8[j]; }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { kf[j] = (float)row[d0 + j]; vf[j] = (float)row[DH + d0 + j]; }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[j] = vf[j] = 0.f;
+    }
+    bf16x8 ko, vo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ko[j] = (bf16)(kf[j] * kscale);
+      vo[j] = (bf16)vf[j];
+      n2 += (float)ko[j] * (float)ko[j];
+    }
+    const long long o = ((long long)b * NKP + key) * DH + d0;
+    *(bf16x8*)(kp + o) = ko;
+    *(bf16x8*)(vp + o) = vo;
+  }
+  n2 += __shfl_xor(n2, 1, 64);  // the row's 4 threads
+  n2 += __shfl_xor(n2, 2, 64);
+#pragma unroll
+  for (int o = 4; o <= 32; o <<= 1) n2 = fmaxf(n2, __shfl_xor(n2, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n2;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    kmax[(long long)b * gridDim.x + blockIdx.x] = sqrtf(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
 template <typename T>
 __global__ void mqa_finish_kernel(const float* dkp, const float* dvp, T* dkv, int lddkv,
                                   float* dnull, int B, int N, int NKP, int accumulate) {
@@ -555,12 +607,17 @@ __device__ __forceinline__ f32x16 score(const char* tK, const FragOff& fo, bf16x
   c = mma(row_at(tK, fo, 0), q0, c);
   return mma(row_at(tK, fo, 1), q1, c);
 }
-// keys >= nkeys of the tile at global key kg -> -inf (the last tile only)
+// keys >= nkeys of the tile at global key kg -> -inf (the last tile only).
+// The tail test is a scalar branch; the per-element selects sit inside it
+// (written as per-element ifs, hipcc evaluated all 16 lane compares and an
+// s_or chain on EVERY tile to form the branch mask: ~45 VALU per key pair).
 __device__ __forceinline__ void mask_keys(f32x16& s, int kg, int nkeys, int h) {
-  if (kg + 32 > nkeys) {
+  const int lim = __builtin_amdgcn_readfirstlane(nkeys - kg);  // keys of this tile still valid
+  if (lim < 32) {
+    asm volatile("" ::: "memory");  // a side effect: keeps the branch (no if-conversion into selects)
+    const int lh = lim - 4 * h;  // acc_row(e, h) = 4 h + an immediate per e
 #pragma unroll
-    for (int e = 0; e < 16; ++e)
-      if (kg + acc_row(e, h) >= nkeys) s[e] = -INFINITY;
+    for (int e = 0; e < 16; ++e) s[e] = ((e & 3) + 8 * (e >> 2)) >= lh ? -INFINITY : s[e];
   }
 }
 // max over the 32 keys of a lane's query column (both half-waves)
@@ -722,6 +779,65 @@ __device__ __forceinline__ void soft_range2(Soft& st, bool first, const char* sK
     mask_keys(s1, kg0 + kn1 * 32, nkeys, h);
   }
 }
+// Bounded scores (round 4): when every score of a wave's rows satisfies
+// |s| <= |q| max|k'| <= FIX_BOUND (log2 units), p = exp2(s) itself is a
+// normal f32 / bf16 number (2^-64 .. 2^64) and the row sums stay far below
+// f32's range, so the softmax needs no running max at all: m = 0, no max
+// chain, no rescale, one exp2 per score -- the same softmax, exactly.
+constexpr float FIX_BOUND = 64.f;
+__device__ __forceinline__ void soft_step2_fixed(Soft& st, f32x16& s0, f32x16& s1, const char* tV0, const char* tV1,
+                                                 const char* tKn0, const char* tKn1, const FragOff& fo, bf16x8 q0,
+                                                 bf16x8 q1) {
+  TrFrag vt0 = tr_issue(tV0, fo), vt1 = tr_issue(tV1, fo);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    s0[e] = ex2(s0[e]);
+    s1[e] = ex2(s1[e]);
+  }
+  st.l += sum16(s0) + sum16(s1);
+  const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
+  s0 = score(tKn0, fo, q0, q1, zero16());
+  s1 = score(tKn1, fo, q0, q1, zero16());
+  bf16x8 a0, a1, b0, b1;
+  tr_wait(vt0, a0, a1);
+  tr_wait(vt1, b0, b1);
+  st.acc = mma(a0, p00, st.acc);
+  st.acc = mma(a1, p01, st.acc);
+  st.acc = mma(b0, p10, st.acc);
+  st.acc = mma(b1, p11, st.acc);
+}
+// soft_range2 for a bounded wave (st.m stays 0)
+__device__ __forceinline__ void soft_range2_fixed(Soft& st, const char* sK, const char* sV, int kbeg, int kend, int kg0,
+                                                  int nkeys, const FragOff& fo, bf16x8 q0, bf16x8 q1, int h) {
+  st.m = 0.f;
+  if (kbeg >= kend) return;
+  int kt = kbeg;
+  if ((kend - kbeg) & 1) {
+    f32x16 s = score(sK + kt * 32 * ROW, fo, q0, q1, zero16());
+    mask_keys(s, kg0 + kt * 32, nkeys, h);
+    TrFrag vt = tr_issue(sV + kt * 32 * ROW, fo);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s[e] = ex2(s[e]);
+    st.l += sum16(s);
+    bf16x8 a0, a1;
+    tr_wait(vt, a0, a1);
+    st.acc = mma(a0, pack8(s, 0), st.acc);
+    st.acc = mma(a1, pack8(s, 1), st.acc);
+    ++kt;
+  }
+  if (kt >= kend) return;
+  f32x16 s0 = score(sK + kt * 32 * ROW, fo, q0, q1, zero16());
+  f32x16 s1 = score(sK + (kt + 1) * 32 * ROW, fo, q0, q1, zero16());
+  mask_keys(s0, kg0 + kt * 32, nkeys, h);
+  mask_keys(s1, kg0 + (kt + 1) * 32, nkeys, h);
+  for (; kt < kend; kt += 2) {
+    const int kn0 = kt + 2 < kend ? kt + 2 : kt, kn1 = kn0 + 1;
+    soft_step2_fixed(st, s0, s1, sV + kt * 32 * ROW, sV + (kt + 1) * 32 * ROW, sK + kn0 * 32 * ROW,
+                     sK + kn1 * 32 * ROW, fo, q0, q1);
+    mask_keys(s0, kg0 + kn0 * 32, nkeys, h);
+    mask_keys(s1, kg0 + kn1 * 32, nkeys, h);
+  }
+}
 template <bool PAIR>
 __device__ __forceinline__ void soft_range_t(Soft& st, bool first, const char* sK, const char* sV, int kbeg, int kend,
                                              int kg0, int nkeys, const FragOff& fo, bf16x8 q0, bf16x8 q1, int h) {
@@ -729,6 +845,21 @@ __device__ __forceinline__ void soft_range_t(Soft& st, bool first, const char* s
     soft_range2(st, first, sK, sV, kbeg, kend, kg0, nkeys, fo, q0, q1, h);
   else
     soft_range(st, first, sK, sV, kbeg, kend, kg0, nkeys, fo, q0, q1, h);
+}
+// wave-uniform: every score of this wave's rows within FIX_BOUND?  (kmax:
+// the prep's per-block key norms of clip b; NULL = unknown -> online max)
+__device__ __forceinline__ bool scores_bounded(const float* kmax, int nkb, int b, int lane, bf16x8 q0, bf16x8 q1) {
+  if (kmax == nullptr) return false;
+  float km = 0.f;
+  for (int i = lane; i < nkb; i += 64) km = fmaxf(km, kmax[(long long)b * nkb + i]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) km = fmaxf(km, __shfl_xor(km, o, 64));
+  float q2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q2 += (float)q0[j] * (float)q0[j] + (float)q1[j] * (float)q1[j];
+  q2 += __shfl_xor(q2, 32, 64);
+  const bool over = sqrtf(q2) * km > FIX_BOUND;
+  return __builtin_amdgcn_readfirstlane((int)(__builtin_amdgcn_ballot_w64(over) == 0)) != 0;
 }
 
 // merge the two key halves (half 1 parks its state in LDS at `red`) and store
@@ -770,7 +901,8 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
                                                              const bf16* __restrict__ kp,
                                                              const bf16* __restrict__ vp,
                                                              bf16* __restrict__ o, float* lse,
-                                                             int R, int NKP, int nkeys) {
+                                                             int R, int NKP, int nkeys, const float* kmax,
+                                                             int nkb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sK = smem;
   char* sV = smem + NKP * ROW;
@@ -788,7 +920,11 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   const FragOff fo = frag_off(lane);
   const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
   Soft st{zero16(), zero16(), -INFINITY, 0.f};
-  soft_range_t<PAIR>(st, true, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
+  const bool fixed = PAIR && scores_bounded(kmax, nkb, b, lane, qf0, qf1);
+  if (fixed)
+    soft_range2_fixed(st, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
+  else
+    soft_range_t<PAIR>(st, true, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
   soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
               lse + (long long)b * R + row);
 }
@@ -821,7 +957,8 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
                                                                     const bf16* __restrict__ kp,
                                                                     const bf16* __restrict__ vp,
                                                                     bf16* __restrict__ o, float* lse,
-                                                                    int R, int NKP, int nkeys) {
+                                                                    int R, int NKP, int nkeys, const float* kmax,
+                                                                    int nkb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
@@ -839,18 +976,33 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
   const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
   const FragOff fo = frag_off(lane);
   Soft st{zero16(), zero16(), -INFINITY, 0.f};
-  for (int ch = 0; ch < nch; ++ch) {
-    // chunk ch landed (the only DMA in flight); every wave is done with the
-    // buffer chunk ch + 1 goes to (it held chunk ch - 1)
+  const bool fixed = PAIR && scores_bounded(kmax, nkb, b, lane, qf0, qf1);
+  // chunk ch landed (the only DMA in flight); every wave is done with the
+  // buffer chunk ch + 1 goes to (it held chunk ch - 1)
+  auto next_chunk = [&](int ch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int row0 = ch * SCK, nrows = min(SCK, NKP - row0);
+    const int row0 = ch * SCK;
     if (ch + 1 < nch)
       dma_kv_chunk(rk, rv, buf_k((ch + 1) & 1), buf_v((ch + 1) & 1), row0 + SCK,
                    min(SCK, NKP - row0 - SCK), wave, lane);
-    const int nkt = nrows / 32, kmid = (nkt + 1) / 2;
-    soft_range_t<PAIR>(st, ch == 0, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo,
-               qf0, qf1, h);
+  };
+  // two chunk loops (bounded / online): one loop holding both range bodies
+  // spilled at the 128-VGPR cap
+  if (fixed) {
+    for (int ch = 0; ch < nch; ++ch) {
+      next_chunk(ch);
+      const int row0 = ch * SCK, nkt = min(SCK, NKP - row0) / 32, kmid = (nkt + 1) / 2;
+      soft_range2_fixed(st, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo, qf0,
+                        qf1, h);
+    }
+  } else {
+    for (int ch = 0; ch < nch; ++ch) {
+      next_chunk(ch);
+      const int row0 = ch * SCK, nkt = min(SCK, NKP - row0) / 32, kmid = (nkt + 1) / 2;
+      soft_range_t<PAIR>(st, ch == 0, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys,
+                         fo, qf0, qf1, h);
+    }
   }
   soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
               lse + (long long)b * R + row);
@@ -1064,10 +1216,12 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
     dp = mma(row_at(tV, fo, 1), df1, dp);
 #pragma unroll
     for (int e = 0; e < 16; ++e) s[e] = ex2(s[e]) * dp[e];
-    if (k0 + 32 > nkeys) {
+    const int lim = __builtin_amdgcn_readfirstlane(nkeys - k0);  // valid keys of this tile
+    if (lim < 32) {  // the last tile only: a scalar branch (see mask_keys)
+      asm volatile("" ::: "memory");
+      const int lh = lim - 4 * h;
 #pragma unroll
-      for (int e = 0; e < 16; ++e)
-        if (k0 + acc_row(e, h) >= nkeys) s[e] = 0.f;
+      for (int e = 0; e < 16; ++e) s[e] = ((e & 3) + 8 * (e >> 2)) >= lh ? 0.f : s[e];
     }
     acc = mma(tr_at(tK, fo, 0), pack8(s, 0), acc);
     acc = mma(tr_at(tK, fo, 1), pack8(s, 1), acc);
@@ -1303,11 +1457,14 @@ int grid_for(long long work) {
 }  // namespace
 
 extern "C" int dv_mqa_prep(int dtype, const void* kv, int ldkv, const float* null_kv, void* kp,
-                           void* vp, int B, int N, int NKP, float scale, void* stream) {
+                           void* vp, int B, int N, int NKP, float scale, float* kmax, void* stream) {
   DV_REQUIRE(kv && null_kv && kp && vp && NKP >= N + 1 && NKP % 32 == 0, "bad arguments");
   hipStream_t st = (hipStream_t)stream;
   const long long n = (long long)B * NKP * DH;
-  if (dtype == DV_BF16)  // keys in log2 units of the logit (the fa kernels' contract)
+  if (dtype == DV_BF16 && kmax)  // keys in log2 units of the logit + the key-norm bound
+    mqa_prep_rows_kernel<<<dim3((NKP + PREP_KEYS - 1) / PREP_KEYS, B), 256, 0, st>>>((const bf16*)kv, ldkv, null_kv, (bf16*)kp,
+                                                                    (bf16*)vp, N, NKP, scale * fa::LOG2E, kmax);
+  else if (dtype == DV_BF16)  // keys in log2 units of the logit (the fa kernels' contract)
     mqa_prep_kernel<bf16><<<grid_for(n), 256, 0, st>>>((const bf16*)kv, ldkv, null_kv, (bf16*)kp, (bf16*)vp, B, N, NKP,
                                                       scale * fa::LOG2E);
   else
@@ -1318,7 +1475,11 @@ extern "C" int dv_mqa_prep(int dtype, const void* kv, int ldkv, const float* nul
 
 extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, const void* vp,
                           void* o, int ldo, float* lse, int B, int N, int NKP, int H, float scale,
-                          void* stream) {
+                          const float* kmax, void* stream) {
+  // kmax: dv_mqa_prep's key-norm bound (NULL: online max everywhere)
+  static const bool no_fixed = getenv("DV_MQA_FIXED") && atoi(getenv("DV_MQA_FIXED")) == 0;  // A/B
+  if (no_fixed) kmax = nullptr;
+  const int nkb = (NKP + PREP_KEYS - 1) / PREP_KEYS;
   DV_REQUIRE(q && kp && vp && o && lse && H % 4 == 0 && NKP % 32 == 0, "bad arguments");
   DV_REQUIRE(ldq % 8 == 0 && ldo >= H * DH, "bad strides");
   hipStream_t st = (hipStream_t)stream;
@@ -1353,10 +1514,10 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
       fa::set_lds(fn, lds);
       if (pair)
         fa::mqa_fwd_fa_kernel<true><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
-                                                                   (bf16*)o, lse, R, NKP, N + 1);
+                                                                   (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
       else
         fa::mqa_fwd_fa_kernel<false><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
-                                                                    (bf16*)o, lse, R, NKP, N + 1);
+                                                                    (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
     } else {
       DV_REQUIRE((long long)NKP * fa::ROW < (1ll << 31), "sequence too long");
       const int lds = 4 * fa::SCK * fa::ROW;
@@ -1365,10 +1526,10 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
       fa::set_lds(fn, lds);
       if (pair)
         fa::mqa_fwd_fa_stream_kernel<true><<<grid, fa::NW * 64, lds, st>>>(
-            (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1);
+            (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
       else
         fa::mqa_fwd_fa_stream_kernel<false><<<grid, fa::NW * 64, lds, st>>>(
-            (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1);
+            (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
     }
   } else {
     dim3 grid((N + 31) / 32, H / 4, B);

@@ -1794,13 +1794,16 @@ class MQAFn(torch.autograd.Function):
         kp = torch.empty(B, NKP, MQA_DH, dtype=q.dtype, device=dev)
         vp = torch.empty_like(kp)
         nkv = null_kv.detach().float().contiguous()
+        # bf16: per-64-key-block key norms, the forward's score bound (no running max when it holds)
+        kmax = (torch.empty(B * ((NKP + 63) // 64), dtype=torch.float32, device=dev)
+                if q.dtype == torch.bfloat16 else None)
         call("dv_mqa_prep", dt(q), ptr(kvc), kvc.shape[-1], ptr(nkv), ptr(kp), ptr(vp), B, N, NKP,
-             ctypes_float(scale), stream())
+             ctypes_float(scale), ptr(kmax), stream())
         o = torch.empty(B * N, H * MQA_DH, dtype=q.dtype, device=dev)
         lse = torch.empty(B, H, N, dtype=torch.float32, device=dev)
         _launch("attn:mqa_fwd", 4.0 * B * H * N * (N + 1) * MQA_DH, 0,
                 lambda: call("dv_mqa_fwd", dt(q), ptr(qc), qc.shape[-1], ptr(kp), ptr(vp), ptr(o),
-                             o.shape[-1], ptr(lse), B, N, NKP, H, ctypes_float(scale), stream()))
+                             o.shape[-1], ptr(lse), B, N, NKP, H, ctypes_float(scale), ptr(kmax), stream()))
         ctx.save_for_backward(qc, kp, vp, o, lse)
         ctx.params = (null_kv,)
         ctx.meta = (B, N, H, NKP, scale, kvc.shape[-1])

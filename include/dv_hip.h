@@ -501,16 +501,19 @@ int dv_xattn_fold_bwd(float* wsR, float* wsV, float* wsQ, float* mcorr,
  * (row 0 null, rows > N zero; NKP = roundup(N+1, 32)).  `scale` is the
  * logit factor later passed to dv_mqa_fwd / dv_mqa_bwd: on the bf16 path kp
  * holds k * scale * log2(e) (the MFMA then yields the logit in log2 units);
- * f32 kp holds k.                                                          */
+ * f32 kp holds k.  kmax (bf16 path, may be NULL): B * ceil(NKP / 64) floats,
+ * receives the largest |k * scale * log2(e)| of every 64-key block, the
+ * bound dv_mqa_fwd uses to drop the running max when |q| max|k| <= 64.     */
 int dv_mqa_prep(int dtype, const void* kv, int ldkv, const float* null_kv, void* kp, void* vp,
-                int B, int N, int NKP, float scale, void* stream);
+                int B, int N, int NKP, float scale, float* kmax, void* stream);
 /* o[b][n][h*32+d] = softmax_j(scale * q.k_j) v_j; lse f32 saved (opaque to the
  * caller, B*H*N floats: [B][N*H] log2 units on the bf16 path, [B][H][N]
  * natural-log otherwise).  bf16 needs dense rows (ldq == ldo == H*32): NKP
  * <= 1280 runs the whole-clip-K/V-in-LDS kernel, longer clips the K/V-
- * streamed one.                                                             */
+ * streamed one.  kmax: dv_mqa_prep's key-norm blocks (NULL: every wave
+ * keeps the online running max).                                           */
 int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, const void* vp, void* o, int ldo,
-               float* lse, int B, int N, int NKP, int H, float scale, void* stream);
+               float* lse, int B, int N, int NKP, int H, float scale, const float* kmax, void* stream);
 /* f32 scratch dv_mqa_bwd needs (floats); same path choice as dv_mqa_fwd.     */
 int dv_mqa_bwd_ws(int dtype, int ldq, int ldo, int B, int N, int NKP, int H, long long* floats);
 /* dq, dkv (k at 0, v at 32, stride lddkv) and dnull (+)= (accumulate);
