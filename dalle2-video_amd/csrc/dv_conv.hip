@@ -2538,7 +2538,11 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
     }
   }
   static const bool co32_ok = !(getenv("DV_FRAME_CO32") && atoi(getenv("DV_FRAME_CO32")) == 0);
-  const int co = co32_ok && tiles64 <= 128 ? 32 : 64;
+  // DV_FRAME_CO32R=1: 32-channel tiles also where the 64-channel grid ends in a
+  // half-empty round (384 tiles = 1.5 rounds: the 8x8 dgrad 768 -> 512)
+  static const bool co32r = getenv("DV_FRAME_CO32R") && atoi(getenv("DV_FRAME_CO32R")) != 0;
+  const bool ragged = co32r && tiles64 > 256 && tiles64 % 256 != 0 && tiles64 % 256 <= 128;
+  const int co = co32_ok && (tiles64 <= 128 || ragged) ? 32 : 64;
   // 8 waves on 128 channels for the 16-wide frames whose 64-channel tiles
   // would take two rounds of the 256 CUs (DV_FRAME_W8=0: off)
   static const bool w8_ok = !(getenv("DV_FRAME_W8") && atoi(getenv("DV_FRAME_W8")) == 0);
@@ -2574,7 +2578,10 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
 
 // tile choice for the glds path (mirrored by ops.conv_tile for kernel naming)
 inline void glds_tile(long long M, int cout, int K, int& bm, int& bn) {
-  bn = cout <= 64 ? 64 : 128;
+  // DV_GLDS_BN64R=1: 64-channel tiles where 128-channel ones leave a half-empty
+  // column (cout = 192: the 32x32 up-path concat dgrad computed 256 channels)
+  static const bool bn64r = getenv("DV_GLDS_BN64R") && atoi(getenv("DV_GLDS_BN64R")) != 0;
+  bn = cout <= 64 || (bn64r && cout % 128 == 64) ? 64 : 128;
   bm = bn == 64 ? 256 : 128;
   if (((M + bm - 1) / bm) * ((cout + bn - 1) / bn) < 512) bm = 128;
   // fewer 128-pixel tiles than CUs (8x8 stage, mid block): halve the pixel tile
