@@ -2546,8 +2546,11 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   // 8 waves on 128 channels for the 16-wide frames whose 64-channel tiles
   // would take two rounds of the 256 CUs (DV_FRAME_W8=0: off)
   static const bool w8_ok = !(getenv("DV_FRAME_W8") && atoi(getenv("DV_FRAME_W8")) == 0);
+  // (with DV_FRAME_CO32R: not where the 128-channel grid is ragged but the
+  // 64-channel one is whole rounds: 384 vs 768 workgroups at 16x16 x 384)
+  const bool w8_ragged = co32r && tiles64 % 256 == 0 && (tiles64 / 2) % 256 != 0;
   const bool w8 = w8_ok && a.W == 16 && co == 64 && !a.gn_sums && a.cout % 128 == 0 &&
-                  (a.M / 128) * (a.cout / 64) > 256;
+                  (a.M / 128) * (a.cout / 64) > 256 && !w8_ragged;
   a.xcd_c = frame_xcd_split(a, w8 ? 128 : co);
   const int nblk = (int)(a.M / 128) * (a.cout / (w8 ? 128 : co));
   if (w8) {
