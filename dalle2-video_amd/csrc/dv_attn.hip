@@ -785,16 +785,31 @@ __device__ __forceinline__ void soft_range2(Soft& st, bool first, const char* sK
 // f32's range, so the softmax needs no running max at all: m = 0, no max
 // chain, no rescale, one exp2 per score -- the same softmax, exactly.
 constexpr float FIX_BOUND = 64.f;
-__device__ __forceinline__ void soft_step2_fixed(Soft& st, f32x16& s0, f32x16& s1, const char* tV0, const char* tV1,
-                                                 const char* tKn0, const char* tKn1, const FragOff& fo, bf16x8 q0,
-                                                 bf16x8 q1) {
+// Row sums on the MFMA pipe (-DDV_MQA_MSUM=1, off): l^T += 1 . P^T with an
+// all-ones A operand -- every row of the 32 x 32 result is the query's sum of
+// the bf16 P that PV multiplies; 4 MFMAs per key pair instead of ~30 VALU
+// adds.  Measured slower (8,192 tokens 391 -> 402-418 us, Cfg2 20.6 -> 21.2-
+// 23.9 us, profiles/r04l_mqa_msum_ab.txt): the 16 more accumulator VGPRs put
+// the kernels at the 128-VGPR cap.
+#ifndef DV_MQA_MSUM
+#define DV_MQA_MSUM 0
+#endif
+__device__ __forceinline__ bf16x8 ones8() {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (__bf16)1.f;
+  return o;
+}
+__device__ __forceinline__ void soft_step2_fixed(Soft& st, f32x16& lacc, f32x16& s0, f32x16& s1, const char* tV0,
+                                                 const char* tV1, const char* tKn0, const char* tKn1,
+                                                 const FragOff& fo, bf16x8 q0, bf16x8 q1) {
   TrFrag vt0 = tr_issue(tV0, fo), vt1 = tr_issue(tV1, fo);
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     s0[e] = ex2(s0[e]);
     s1[e] = ex2(s1[e]);
   }
-  st.l += sum16(s0) + sum16(s1);
+  if (!DV_MQA_MSUM) st.l += sum16(s0) + sum16(s1);
   const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
   s0 = score(tKn0, fo, q0, q1, zero16());
   s1 = score(tKn1, fo, q0, q1, zero16());
@@ -805,10 +820,19 @@ __device__ __forceinline__ void soft_step2_fixed(Soft& st, f32x16& s0, f32x16& s
   st.acc = mma(a1, p01, st.acc);
   st.acc = mma(b0, p10, st.acc);
   st.acc = mma(b1, p11, st.acc);
+  if (DV_MQA_MSUM) {
+    const bf16x8 one = ones8();
+    lacc = mma(one, p00, lacc);
+    lacc = mma(one, p01, lacc);
+    lacc = mma(one, p10, lacc);
+    lacc = mma(one, p11, lacc);
+  }
 }
-// soft_range2 for a bounded wave (st.m stays 0)
-__device__ __forceinline__ void soft_range2_fixed(Soft& st, const char* sK, const char* sV, int kbeg, int kend, int kg0,
-                                                  int nkeys, const FragOff& fo, bf16x8 q0, bf16x8 q1, int h) {
+// soft_range2 for a bounded wave (st.m stays 0); lacc: the MFMA row sums
+// (DV_MQA_MSUM), carried across calls -- soft_msum_done moves them into st.l
+__device__ __forceinline__ void soft_range2_fixed(Soft& st, f32x16& lacc, const char* sK, const char* sV, int kbeg,
+                                                  int kend, int kg0, int nkeys, const FragOff& fo, bf16x8 q0,
+                                                  bf16x8 q1, int h) {
   st.m = 0.f;
   if (kbeg >= kend) return;
   int kt = kbeg;
@@ -818,11 +842,16 @@ __device__ __forceinline__ void soft_range2_fixed(Soft& st, const char* sK, cons
     TrFrag vt = tr_issue(sV + kt * 32 * ROW, fo);
 #pragma unroll
     for (int e = 0; e < 16; ++e) s[e] = ex2(s[e]);
-    st.l += sum16(s);
+    if (!DV_MQA_MSUM) st.l += sum16(s);
     bf16x8 a0, a1;
     tr_wait(vt, a0, a1);
-    st.acc = mma(a0, pack8(s, 0), st.acc);
-    st.acc = mma(a1, pack8(s, 1), st.acc);
+    const bf16x8 ps0 = pack8(s, 0), ps1 = pack8(s, 1);
+    st.acc = mma(a0, ps0, st.acc);
+    st.acc = mma(a1, ps1, st.acc);
+    if (DV_MQA_MSUM) {
+      lacc = mma(ones8(), ps0, lacc);
+      lacc = mma(ones8(), ps1, lacc);
+    }
     ++kt;
   }
   if (kt >= kend) return;
@@ -832,11 +861,16 @@ __device__ __forceinline__ void soft_range2_fixed(Soft& st, const char* sK, cons
   mask_keys(s1, kg0 + (kt + 1) * 32, nkeys, h);
   for (; kt < kend; kt += 2) {
     const int kn0 = kt + 2 < kend ? kt + 2 : kt, kn1 = kn0 + 1;
-    soft_step2_fixed(st, s0, s1, sV + kt * 32 * ROW, sV + (kt + 1) * 32 * ROW, sK + kn0 * 32 * ROW,
+    soft_step2_fixed(st, lacc, s0, s1, sV + kt * 32 * ROW, sV + (kt + 1) * 32 * ROW, sK + kn0 * 32 * ROW,
                      sK + kn1 * 32 * ROW, fo, q0, q1);
     mask_keys(s0, kg0 + kn0 * 32, nkeys, h);
     mask_keys(s1, kg0 + kn1 * 32, nkeys, h);
   }
+}
+// the MFMA row sums hold the whole 32-key sum in every element on both lane
+// halves; soft_finish adds the halves, so half 1 contributes zero
+__device__ __forceinline__ void soft_msum_done(Soft& st, const f32x16& lacc, int h) {
+  if (DV_MQA_MSUM) st.l = h == 0 ? lacc[0] : 0.f;
 }
 template <bool PAIR>
 __device__ __forceinline__ void soft_range_t(Soft& st, bool first, const char* sK, const char* sV, int kbeg, int kend,
@@ -921,9 +955,11 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
   Soft st{zero16(), zero16(), -INFINITY, 0.f};
   const bool fixed = PAIR && scores_bounded(kmax, nkb, b, lane, qf0, qf1);
-  if (fixed)
-    soft_range2_fixed(st, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
-  else
+  if (fixed) {
+    f32x16 lacc = zero16();
+    soft_range2_fixed(st, lacc, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
+    soft_msum_done(st, lacc, h);
+  } else
     soft_range_t<PAIR>(st, true, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
   soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
               lse + (long long)b * R + row);
@@ -990,12 +1026,14 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
   // two chunk loops (bounded / online): one loop holding both range bodies
   // spilled at the 128-VGPR cap
   if (fixed) {
+    f32x16 lacc = zero16();
     for (int ch = 0; ch < nch; ++ch) {
       next_chunk(ch);
       const int row0 = ch * SCK, nkt = min(SCK, NKP - row0) / 32, kmid = (nkt + 1) / 2;
-      soft_range2_fixed(st, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo, qf0,
-                        qf1, h);
+      soft_range2_fixed(st, lacc, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo,
+                        qf0, qf1, h);
     }
+    soft_msum_done(st, lacc, h);
   } else {
     for (int ch = 0; ch < nch; ++ch) {
       next_chunk(ch);
