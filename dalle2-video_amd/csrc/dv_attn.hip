@@ -509,6 +509,28 @@ __device__ __forceinline__ void tr_wait(const TrFrag& t, bf16x8& a0, bf16x8& a1)
   a0 = cat8(t.x[0], t.x[1]);
   a1 = cat8(t.x[2], t.x[3]);
 }
+// the V^T fragments of two adjacent 32-key tiles (tile1 = tile0 + 32 rows):
+// the eight reads differ from two lane bases by immediates (tr[1][t] =
+// tr[0][t] + 16 rows, tile1 = +32 rows), so two address adds instead of eight
+__device__ __forceinline__ void tr_issue_pair(const char* tile0, const FragOff& f, TrFrag& t0, TrFrag& t1) {
+  const unsigned b = lds_off(tile0);
+  const unsigned a0 = b + f.tr[0][0], a1 = b + f.tr[0][1];
+  static_assert(16 * ROW == 1024 && 32 * ROW == 2048, "immediates below");
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8\n\t"
+      "ds_read_b64_tr_b16 %1, %9\n\t"
+      "ds_read_b64_tr_b16 %2, %8 offset:1024\n\t"
+      "ds_read_b64_tr_b16 %3, %9 offset:1024\n\t"
+      "ds_read_b64_tr_b16 %4, %8 offset:2048\n\t"
+      "ds_read_b64_tr_b16 %5, %9 offset:2048\n\t"
+      "ds_read_b64_tr_b16 %6, %8 offset:3072\n\t"
+      "ds_read_b64_tr_b16 %7, %9 offset:3072\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(t0.x[0]), "=&v"(t0.x[1]), "=&v"(t0.x[2]), "=&v"(t0.x[3]), "=&v"(t1.x[0]), "=&v"(t1.x[1]),
+        "=&v"(t1.x[2]), "=&v"(t1.x[3])
+      : "v"(a0), "v"(a1)
+      : "memory");
+}
 
 // f32 pair -> packed bf16 (hipcc emits v_cvt_pk_bf16_f32).  Compiler-visible on
 // purpose: an inline-asm VALU op that reads a v_exp result or an MFMA result
@@ -707,7 +729,8 @@ __device__ __forceinline__ float sum16(const f32x16& s) {
 __device__ __forceinline__ void soft_step2(Soft& st, f32x16& s0, f32x16& s1, const char* tV0, const char* tV1,
                                            const char* tKn0, const char* tKn1, const FragOff& fo, bf16x8 q0,
                                            bf16x8 q1) {
-  TrFrag vt0 = tr_issue(tV0, fo), vt1 = tr_issue(tV1, fo);
+  TrFrag vt0, vt1;  // tV1 == tV0 + 32 rows
+  tr_issue_pair(tV0, fo, vt0, vt1);
   const float mx = col_max2(s0, s1);
   const bool upd = mx > st.m + 8.f;
   if (__builtin_amdgcn_ballot_w64(upd)) {
@@ -803,7 +826,8 @@ __device__ __forceinline__ bf16x8 ones8() {
 __device__ __forceinline__ void soft_step2_fixed(Soft& st, f32x16& lacc, f32x16& s0, f32x16& s1, const char* tV0,
                                                  const char* tV1, const char* tKn0, const char* tKn1,
                                                  const FragOff& fo, bf16x8 q0, bf16x8 q1) {
-  TrFrag vt0 = tr_issue(tV0, fo), vt1 = tr_issue(tV1, fo);
+  TrFrag vt0, vt1;  // tV1 == tV0 + 32 rows
+  tr_issue_pair(tV0, fo, vt0, vt1);
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     s0[e] = ex2(s0[e]);
