@@ -2129,14 +2129,21 @@ __device__ __forceinline__ int fw_pix(int r) {
 // NB > 0: a shallower ring (NB chunk buffers) so that two workgroups share a
 // CU (the K-split 256-tile grids: two waves per SIMD from two workgroups, one
 // hiding the other's LDS-DMA issue)
+// RS: register staging instead of LDS-DMA.  A DMA piece issued among the
+// MFMAs costs the issuing wave 100-185 cycles (MI355X_MICROARCH.md), eight of
+// them per chunk per wave; here each piece is a buffer_load_dwordx4 into
+// VGPRs, written to LDS by a ds_write_b128 two chunks later (two register
+// sets alternate by chunk parity; a 2-deep LDS ring: chunk c read, chunk c+1
+// written).  The compiler's vmcnt tracking orders each store after its load.
 template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4,
-          int KSPL = 1, int NB = 0>
+          int KSPL = 1, int NB = 0, bool RS = false>
 __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
-  using G = FwGeom<W, CO, NWV, NB>;
+  using G = FwGeom<W, CO, NWV, RS ? 2 : NB>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
   constexpr int WPC = G::WPC, NJ = CO / 32, CG = G::CG;
   static_assert(NWV == 4 || (NWV == 8 && !STATS), "the 8-wave tile has no statistics epilogue");
   static_assert(NPW <= 9, "one DMA piece per tap");
+  static_assert(!RS || NBUF == 2, "register staging runs a 2-deep ring");
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
   DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2214,16 +2221,46 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     for (int i = 0; i < NPW; ++i) issue1(c, i);
   };
   constexpr int AHEAD = NBUF - 1;  // chunks in flight beyond the one being read
+  // RS: piece i of chunk c into / out of registers (chunk c's LDS buffer:
+  // relative chunk index parity)
+  u32x4 stA[RS ? NPW : 1], stB[RS ? NPW : 1];
+  auto ld1 = [&](u32x4& dst, int c, int i) {
+    const int ci0 = c * 16;
+    const int k = min(wave + NWV * i, PIECES - 1);
+    if (k < WPC) dst = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)voff0[i], ci0 * 18, 0);
+    else if (!SPLIT || ci0 < p.c0) dst = __builtin_amdgcn_raw_buffer_load_b128(xr0, (int)voff0[i], ci0 * 2, 0);
+    else dst = __builtin_amdgcn_raw_buffer_load_b128(xr1, (int)voff1[i], (ci0 - p.c0) * 2, 0);
+  };
+  auto st1 = [&](const u32x4& v, int c, int i) {
+    const int k = min(wave + NWV * i, PIECES - 1);
+    *(u32x4*)(smem + ((c - cbeg) & 1) * BUF + k * 1024 + lane * 16) = v;
+  };
 
-  // prologue: chunks cbeg .. cbeg+AHEAD-1 in flight, wait for chunk cbeg
+  if constexpr (RS) {
+    // prologue: chunk 0 in LDS, chunk 1 in set B, chunk 2 loading into set A
 #pragma unroll
-  for (int c = 0; c < AHEAD; ++c)
-    if (c < nch) issue(cbeg + c);
-  const int pro = min(AHEAD, nch) - 1;  // younger chunks than chunk 0
-  if (pro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
-  else if (pro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
-  else if (pro == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = 0; i < NPW; ++i)
+      if (nch > 0) ld1(stA[i], cbeg, i);
+#pragma unroll
+    for (int i = 0; i < NPW; ++i)
+      if (nch > 1) ld1(stB[i], cbeg + 1, i);
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      if (nch > 0) st1(stA[i], cbeg, i);
+      if (nch > 2) ld1(stA[i], cbeg + 2, i);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  } else {
+    // prologue: chunks cbeg .. cbeg+AHEAD-1 in flight, wait for chunk cbeg
+#pragma unroll
+    for (int c = 0; c < AHEAD; ++c)
+      if (c < nch) issue(cbeg + c);
+    const int pro = min(AHEAD, nch) - 1;  // younger chunks than chunk 0
+    if (pro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
+    else if (pro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
+    else if (pro == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   DV_STAMP_AT(1);
 
@@ -2246,8 +2283,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   // one chunk; PRE (compile-time): chunk c + AHEAD exists and is issued here.
   // The loop is split into the chunks that issue and the AHEAD tail, so the
   // main loop carries no per-piece branch and a constant vmcnt
-  auto chunk = [&](int c, auto PRE) {
-    const char* b = smem + (c % NBUF) * BUF;
+  auto chunk = [&](int c, auto PRE, auto PAR) {
+    const char* b = smem + (RS ? ((c - cbeg) & 1) : (c % NBUF)) * BUF;
     // fragments of tap d + PF are read while tap d multiplies (one wave per
     // SIMD: the LDS latency is hidden by this wave's own MFMAs only)
     constexpr int NS = PF + 1;
@@ -2280,10 +2317,27 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
         acc0 = Mma<bf16>::run(aq0[d % NS], bq[d % NS], acc0);
         if (CO == 64) acc1 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc1);
       }
-      if constexpr (decltype(PRE)::value) {
+      if constexpr (RS) {
+        // chunk c+1 (loaded two chunks ago) into the LDS buffer read in
+        // chunk c-1, then chunk c+3 into the freed registers.  PAR: chunk
+        // parity (relative to cbeg); chunk j sits in set A if j is even
+        if (d < NPW) {
+          u32x4* S = decltype(PAR)::value ? stA : stB;
+          if (decltype(PRE)::value || c + 1 < cend) st1(S[d], c + 1, d);
+          if (decltype(PRE)::value || c + 3 < cend) ld1(S[d], c + 3, d);
+        }
+      } else if constexpr (decltype(PRE)::value) {
         if (d < NPW) issue1(c + AHEAD, d);
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (RS) {
+      // this wave's stores of chunk c+1 done before the barrier
+      if (DEFER && CO == 64) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0), "+v"(la1)::"memory");
+      else if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0)::"memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      return;
     }
     // chunk c+1 landed: younger are the pieces of chunks c+2 .. c+AHEAD
     if constexpr (decltype(PRE)::value) {
@@ -2299,9 +2353,22 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     else if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0)::"memory");
     __builtin_amdgcn_s_barrier();
   };
+  using P0 = std::false_type;
+  using P1 = std::true_type;
   int c = cbeg;
-  for (; c + AHEAD < cend; ++c) chunk(c, std::true_type{});
-  for (; c < cend; ++c) chunk(c, std::false_type{});
+  if constexpr (RS) {
+    for (; c + 4 < cend; c += 2) {
+      chunk(c, std::true_type{}, P0{});
+      chunk(c + 1, std::true_type{}, P1{});
+    }
+    for (; c < cend; c += 2) {
+      chunk(c, std::false_type{}, P0{});
+      if (c + 1 < cend) chunk(c + 1, std::false_type{}, P1{});
+    }
+  } else {
+    for (; c + AHEAD < cend; ++c) chunk(c, std::true_type{}, P0{});
+    for (; c < cend; ++c) chunk(c, std::false_type{}, P0{});
+  }
   if (DEFER && nch > 0) {
     acc0 = Mma<bf16>::run(la0, lb, acc0);
     if (CO == 64) acc1 = Mma<bf16>::run(la1, lb, acc1);
@@ -2553,9 +2620,32 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
                   (a.M / 128) * (a.cout / 64) > 256 && !w8_ragged;
   a.xcd_c = frame_xcd_split(a, w8 ? 128 : co);
   const int nblk = (int)(a.M / 128) * (a.cout / (w8 ? 128 : co));
+  // DV_FRAME_RS=1: register staging instead of LDS-DMA (A/B)
+  static const bool rs = getenv("DV_FRAME_RS") && atoi(getenv("DV_FRAME_RS")) != 0;
   if (w8) {
-    if (a.c0 < a.cin) conv_fwd_frame_kernel<16, false, 3, 1, 64, true, 8><<<nblk, 512, 0, st>>>(a);
-    else conv_fwd_frame_kernel<16, false, 3, 1, 64, false, 8><<<nblk, 512, 0, st>>>(a);
+    if (rs) {
+      if (a.c0 < a.cin) conv_fwd_frame_kernel<16, false, 3, 1, 64, true, 8, 1, 0, true><<<nblk, 512, 0, st>>>(a);
+      else conv_fwd_frame_kernel<16, false, 3, 1, 64, false, 8, 1, 0, true><<<nblk, 512, 0, st>>>(a);
+    } else {
+      if (a.c0 < a.cin) conv_fwd_frame_kernel<16, false, 3, 1, 64, true, 8><<<nblk, 512, 0, st>>>(a);
+      else conv_fwd_frame_kernel<16, false, 3, 1, 64, false, 8><<<nblk, 512, 0, st>>>(a);
+    }
+    return check_launch("conv_fwd_frame");
+  }
+  if (rs) {
+    switch (a.W) {
+#define DV_FR5(WW, C, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, C, SP, 4, 1, 0, true><<<nblk, 256, 0, st>>>(a) \
+                                 : conv_fwd_frame_kernel<WW, false, 3, 1, C, SP, 4, 1, 0, true><<<nblk, 256, 0, st>>>(a))
+#define DV_FR4(WW, C) (a.c0 < a.cin ? DV_FR5(WW, C, true) : DV_FR5(WW, C, false))
+#define DV_FR(WW) (co == 32 ? DV_FR4(WW, 32) : DV_FR4(WW, 64))
+      case 8: DV_FR(8); break;
+      case 16: DV_FR(16); break;
+      case 32: DV_FR(32); break;
+      default: DV_FR(64); break;
+#undef DV_FR
+#undef DV_FR4
+#undef DV_FR5
+    }
     return check_launch("conv_fwd_frame");
   }
   // fragment prefetch distance PF = 3 taps and DEFER (the last tap's MFMAs
