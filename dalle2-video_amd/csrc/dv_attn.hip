@@ -602,6 +602,30 @@ __device__ __forceinline__ void dma_kv(const bf16* kb, const bf16* vb, char* sK,
   }
 }
 
+// as dma_kv for the key tiles [a0, a1) and [b0, b1) only (two 16-row pieces
+// per 32-key tile): the phased prologue (kv_phase) stages the first tiles of
+// both key halves, starts on them, and stages the rest behind that compute
+__device__ __forceinline__ void dma_kv_tiles(const bf16* kb, const bf16* vb, char* sK, char* sV, int NKP,
+                                             int wave, int lane, int a0, int a1, int b0, int b1) {
+  const __amdgpu_buffer_rsrc_t rk = dma_rsrc(kb, (unsigned)NKP * ROW);
+  const __amdgpu_buffer_rsrc_t rv = dma_rsrc(vb, (unsigned)NKP * ROW);
+  const int na = 2 * (a1 - a0), n = na + 2 * (b1 - b0);  // pieces of K (and of V)
+  const int rr = lane >> 2, slot = lane & 3;
+  for (int i = wave; i < 2 * n; i += NW) {
+    const bool isv = i >= n;
+    const int j = isv ? i - n : i;
+    const int pc = j < na ? 2 * a0 + j : 2 * b0 + (j - na);
+    const int row = pc * 16 + rr;
+    const unsigned voff = row * ROW + 16 * (slot ^ ((row >> 2) & 3));
+    if (isv)
+      dma16(rv, sV + pc * 1024, voff);
+    else
+      dma16(rk, sK + pc * 1024, voff);
+  }
+}
+// first-phase tiles of a key half [k0, k1): a quarter, rounded up
+__device__ __forceinline__ int kv_phase(int k0, int k1) { return min(k1, k0 + (k1 - k0 + 3) / 4); }
+
 __device__ __forceinline__ bf16x8 load_row8(const bf16* p, bool ok) {
   if (!ok) return bf16x8{};
   return *(const bf16x8*)p;
@@ -954,7 +978,10 @@ __device__ __forceinline__ void soft_finish(Soft& st, float* red, int kh, int la
 // grid (ceil(R / 256), B), 1024 threads, dynamic LDS 2 * NKP * 64 B.
 // Wave w: 32 query rows (group w & 7) against key half w >> 3 of the whole
 // clip's K / V, staged once by LDS-DMA; the halves merge through LDS.
-template <bool PAIR>
+// PH: phased prologue -- the first quarter of each key half is staged and
+// multiplied while the rest lands (every workgroup bursts its whole clip's
+// K / V at once: ≈ 12.5 B/cycle/CU, MI355X_MICROARCH.md, ≈ 4.5 us at 1,056 keys)
+template <bool PAIR, bool PH = false>
 __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restrict__ q,
                                                              const bf16* __restrict__ kp,
                                                              const bf16* __restrict__ vp,
@@ -968,23 +995,44 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int rg = wave & (RG - 1), kh = wave / RG;
   const int b = blockIdx.y;
-  dma_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, wave, lane);
+  const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
+  const int qa0 = kv_phase(0, kmid), qa1 = kv_phase(kmid, nkt);
+  const bf16* kb = kp + (long long)b * NKP * 32;
+  const bf16* vb = vp + (long long)b * NKP * 32;
+  if (PH) dma_kv_tiles(kb, vb, sK, sV, NKP, wave, lane, 0, qa0, kmid, qa1);
+  else dma_kv(kb, vb, sK, sV, NKP, wave, lane);
   const int row = blockIdx.x * RG * 32 + rg * 32 + r;
   const bool rok = row < R;
   const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
   const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (PH) dma_kv_tiles(kb, vb, sK, sV, NKP, wave, lane, qa0, kmid, qa1, nkt);
   const FragOff fo = frag_off(lane);
-  const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
+  const int k0 = kh ? kmid : 0, k1 = kh ? nkt : kmid, kq = PH ? (kh ? qa1 : qa0) : k1;
+  auto rest = [&]() {  // the second phase's tiles landed (every wave's pieces)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
   Soft st{zero16(), zero16(), -INFINITY, 0.f};
   const bool fixed = PAIR && scores_bounded(kmax, nkb, b, lane, qf0, qf1);
+  // the phases as a rolled loop: one copy of each range body (two inlined
+  // copies spilled at the 128-VGPR cap)
   if (fixed) {
     f32x16 lacc = zero16();
-    soft_range2_fixed(st, lacc, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
+#pragma unroll 1
+    for (int ph = 0; ph < (PH ? 2 : 1); ++ph) {
+      if (ph) rest();
+      soft_range2_fixed(st, lacc, sK, sV, ph ? kq : k0, ph ? k1 : kq, 0, nkeys, fo, qf0, qf1, h);
+    }
     soft_msum_done(st, lacc, h);
-  } else
-    soft_range_t<PAIR>(st, true, sK, sV, kh ? kmid : 0, kh ? nkt : kmid, 0, nkeys, fo, qf0, qf1, h);
+  } else {
+#pragma unroll 1
+    for (int ph = 0; ph < (PH ? 2 : 1); ++ph) {
+      if (ph) rest();
+      soft_range_t<PAIR>(st, ph == 0, sK, sV, ph ? kq : k0, ph ? k1 : kq, 0, nkeys, fo, qf0, qf1, h);
+    }
+  }
   soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
               lse + (long long)b * R + row);
 }
@@ -1241,6 +1289,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_pp_kernel(const bf16* __restr
 // operands: S^T arrives as c s - L (keys pre-scaled by c), dP^T as dP - D, so
 // dS = exp2(.) * (.) is two VALU ops per score.  dq = (K^T dS^T) / log2 e
 // (the keys carry c = scale * log2 e; dq needs scale).
+template <bool PH = false>
 __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
@@ -1252,7 +1301,12 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int rg = wave & (RG - 1), kh = wave / RG;
   const int b = blockIdx.y;
-  dma_kv(kp + (long long)b * NKP * 32, vp + (long long)b * NKP * 32, sK, sV, NKP, wave, lane);
+  const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
+  const int qa0 = kv_phase(0, kmid), qa1 = kv_phase(kmid, nkt);  // PH: as the forward
+  const bf16* kb = kp + (long long)b * NKP * 32;
+  const bf16* vb = vp + (long long)b * NKP * 32;
+  if (PH) dma_kv_tiles(kb, vb, sK, sV, NKP, wave, lane, 0, qa0, kmid, qa1);
+  else dma_kv(kb, vb, sK, sV, NKP, wave, lane);
   const int row = blockIdx.x * RG * 32 + rg * 32 + r;
   const bool rok = row < R;
   const long long ro = ((long long)b * R + (rok ? row : 0)) * 32;
@@ -1264,12 +1318,12 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   if (rok && h == 0 && kh == 0) D[(long long)b * R + row] = dd;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (PH) dma_kv_tiles(kb, vb, sK, sV, NKP, wave, lane, qa0, kmid, qa1, nkt);
   const FragOff fo = frag_off(lane);
   const f32x16 negL = bcast16(-L2), negD = bcast16(-dd);
   f32x16 acc = zero16();
-  const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
-  const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid;
-  for (int kt = kbeg; kt < kend; ++kt) {
+  const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid, kq = PH ? (kh ? qa1 : qa0) : kend;
+  auto tile = [&](int kt) {
     const int k0 = kt * 32;
     const char* tK = sK + k0 * ROW;
     const char* tV = sV + k0 * ROW;
@@ -1287,6 +1341,12 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
     }
     acc = mma(tr_at(tK, fo, 0), pack8(s, 0), acc);
     acc = mma(tr_at(tK, fo, 1), pack8(s, 1), acc);
+  };
+  for (int kt = kbeg; kt < kq; ++kt) tile(kt);
+  if (PH) {  // the second phase's tiles landed (every wave's pieces)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = kq; kt < kend; ++kt) tile(kt);
   }
   __syncthreads();
   float* red = (float*)smem + rg * 16 * 64;
@@ -1318,11 +1378,13 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
 constexpr int TB = 2 * 32 * ROW + 2 * 32 * 4;  // one tile: Q, dO images, L, -D
 constexpr int QP = NW / 4;                      // query-tile parities
 constexpr int RED = 2 * 4 * 2 * 16 * 64 * 4;    // parity combine (two parities at a time)
+// TPS: query tiles per wave per step (one barrier per TPS tiles)
+template <bool EARLY, int TPS = 1>
 __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ D, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
     float* __restrict__ ws, int R, int NKP, int nkeys, int rows_per_split, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * QP * TB > RED ? 2 * QP * TB : RED];
+  __shared__ __attribute__((aligned(16))) char smem[2 * QP * TPS * TB > RED ? 2 * QP * TPS * TB : RED];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int b = blockIdx.z, split = blockIdx.y;
@@ -1333,28 +1395,35 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
   bf16x8 vf0 = *(const bf16x8*)(vp + krow * 32 + 8 * h), vf1 = *(const bf16x8*)(vp + krow * 32 + 16 + 8 * h);
   const int r0 = split * rows_per_split;
   const int r1 = min(R, r0 + rows_per_split);
-  const int nsteps = r1 > r0 ? (r1 - r0 + 32 * QP - 1) / (32 * QP) : 0;
+  const int nsteps = r1 > r0 ? (r1 - r0 + 32 * QP * TPS - 1) / (32 * QP * TPS) : 0;
   // staging role: thread t -> tile parity t >> 8; u < 128 Q chunk, else dO chunk; u < 32 also L, -D
   const int sp = tid >> 8, u = tid & 255, cu = u & 127, crow = cu >> 2, cch = cu & 3;
   const bf16* src = (u < 128 ? q : dout) + (long long)b * R * 32;
   const float* lsrc = lse + (long long)b * R;
   const float* dsrc = D + (long long)b * R;
-  u32x4 cv;
-  float lv, dv;
-  int lrow;
+  u32x4 cv[TPS];
+  float lv[TPS], dv[TPS];
+  int lrow[TPS];
   auto load = [&](int st) {
-    const int rr = r0 + (QP * st + sp) * 32 + crow;
-    cv = *(const u32x4*)(src + (long long)min(rr, r1 - 1) * 32 + cch * 8);
-    lrow = r0 + (QP * st + sp) * 32 + (u & 31);
-    lv = lsrc[min(lrow, r1 - 1)];
-    dv = dsrc[min(lrow, r1 - 1)];
+#pragma unroll
+    for (int j = 0; j < TPS; ++j) {
+      const int tq = QP * (TPS * st + j) + sp;  // query tile of the split
+      const int rr = r0 + tq * 32 + crow;
+      cv[j] = *(const u32x4*)(src + (long long)min(rr, r1 - 1) * 32 + cch * 8);
+      lrow[j] = r0 + tq * 32 + (u & 31);
+      lv[j] = lsrc[min(lrow[j], r1 - 1)];
+      dv[j] = dsrc[min(lrow[j], r1 - 1)];
+    }
   };
   auto store = [&](int buf) {
-    char* t = smem + (QP * buf + sp) * TB;
-    *(u32x4*)(t + (u < 128 ? 0 : 32 * ROW) + img(crow, cch)) = cv;
-    if (u < 32) {
-      ((float*)(t + 2 * 32 * ROW))[u] = lrow < r1 ? -lv : -INFINITY;
-      ((float*)(t + 2 * 32 * ROW))[32 + u] = -dv;
+#pragma unroll
+    for (int j = 0; j < TPS; ++j) {
+      char* t = smem + (QP * (TPS * buf + j) + sp) * TB;
+      *(u32x4*)(t + (u < 128 ? 0 : 32 * ROW) + img(crow, cch)) = cv[j];
+      if (u < 32) {
+        ((float*)(t + 2 * 32 * ROW))[u] = lrow[j] < r1 ? -lv[j] : -INFINITY;
+        ((float*)(t + 2 * 32 * ROW))[32 + u] = -dv[j];
+      }
     }
   };
   // retire the K/V fragment loads here so the loop carries no vmcnt for them
@@ -1365,11 +1434,23 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     store(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // EARLY: step st+1's tile was loaded during step st-1 and is stored at the
+  // top of step st (its buffer was read in step st-1, before the last
+  // barrier), then step st+2's loads go out: a whole step of latency cover
+  // instead of one step's compute (the loop waited on each tile's load)
+  if (EARLY && nsteps > 1) load(1);
   __syncthreads();
   for (int st = 0; st < nsteps; ++st) {
     const bool more = st + 1 < nsteps;
-    if (more) load(st + 1);
-    const char* t = smem + (QP * (st & 1) + qp) * TB;
+    if (EARLY) {
+      if (more) store((st + 1) & 1);
+      if (st + 2 < nsteps) load(st + 2);
+    } else if (more) {
+      load(st + 1);
+    }
+#pragma unroll
+    for (int j = 0; j < TPS; ++j) {
+    const char* t = smem + (QP * (TPS * (st & 1) + j) + qp) * TB;
     if (kvalid) {
       const char* sQ = t;
       const char* sdO = t + 32 * ROW;
@@ -1402,7 +1483,8 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
       dvv = mma(tr_frag(sdO, 1, lane), pack8a(s, 1), dvv);
       dk = mma(tr_frag(sQ, 1, lane), pack8a(dp, 1), dk);
     }
-    if (more) {
+    }
+    if (!EARLY && more) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       store((st + 1) & 1);
     }
@@ -1505,6 +1587,14 @@ void launch_finish(int s, int grid, hipStream_t st, const float* ws, int B, int 
   }
 }
 
+// DV_MQA_PH=1: the phased prologue of the forward and dq (a quarter of each
+// key half first).  Measured no faster at Cfg2 (fwd 20.4-20.9 vs 20.9-21.1 us,
+// profiles/r04o_mqa_ph_tps_ab.txt): off
+bool phased() {
+  static const bool on = getenv("DV_MQA_PH") && atoi(getenv("DV_MQA_PH")) != 0;
+  return on;
+}
+
 void set_lds(const void* fn, int bytes) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
@@ -1572,14 +1662,18 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
     }
     if (fa::eligible(dtype, ldq, ldo, H, NKP) && !force_stream) {
       const int lds = max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4);
-      const void* fn = pair ? (const void*)fa::mqa_fwd_fa_kernel<true> : (const void*)fa::mqa_fwd_fa_kernel<false>;
-      fa::set_lds(fn, lds);
-      if (pair)
-        fa::mqa_fwd_fa_kernel<true><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
-                                                                   (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
-      else
-        fa::mqa_fwd_fa_kernel<false><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
-                                                                    (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
+      const bool ph = fa::phased();
+#define DV_FWD_FA(P, PH)                                                                                       \
+  do {                                                                                                         \
+    fa::set_lds((const void*)fa::mqa_fwd_fa_kernel<P, PH>, lds);                                              \
+    fa::mqa_fwd_fa_kernel<P, PH><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp, \
+                                                                 (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);     \
+  } while (0)
+      if (pair && ph) DV_FWD_FA(true, true);
+      else if (pair) DV_FWD_FA(true, false);
+      else if (ph) DV_FWD_FA(false, true);
+      else DV_FWD_FA(false, false);
+#undef DV_FWD_FA
     } else {
       DV_REQUIRE((long long)NKP * fa::ROW < (1ll << 31), "sequence too long");
       const int lds = 4 * fa::SCK * fa::ROW;
@@ -1626,13 +1720,33 @@ extern "C" int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int 
     DV_REQUIRE(lddo == H * DH && lddq == H * DH, "bf16 path needs dense dout/dq rows");
     const int R = N * H, lds = max(NKP * 2 * fa::ROW, fa::RG * 16 * 64 * 4), S = fa::splits(NKP, B);
     const int rps = ((R + S - 1) / S + 63) / 64 * 64;
-    fa::set_lds((const void*)fa::mqa_dq_fa_kernel, lds);
-    fa::mqa_dq_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
-        (const bf16*)q, (const bf16*)o, (const bf16*)dout, lse, (const bf16*)kp, (const bf16*)vp,
-        (bf16*)dq, D, R, NKP, N + 1);
-    fa::mqa_dkdv_fa_kernel<<<dim3((NKP / 32 + 3) / 4, S, B), fa::NW * 64, 0, st>>>(
-        (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP,
-        N + 1, rps, scale);
+    if (fa::phased()) {
+      fa::set_lds((const void*)fa::mqa_dq_fa_kernel<true>, lds);
+      fa::mqa_dq_fa_kernel<true><<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
+          (const bf16*)q, (const bf16*)o, (const bf16*)dout, lse, (const bf16*)kp, (const bf16*)vp,
+          (bf16*)dq, D, R, NKP, N + 1);
+    } else {
+      fa::set_lds((const void*)fa::mqa_dq_fa_kernel<false>, lds);
+      fa::mqa_dq_fa_kernel<false><<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
+          (const bf16*)q, (const bf16*)o, (const bf16*)dout, lse, (const bf16*)kp, (const bf16*)vp,
+          (bf16*)dq, D, R, NKP, N + 1);
+    }
+    // DV_MQA_EARLY=0: the dk/dv tile loads one step ahead of their store (A/B:
+    // 33.0-33.6 -> 31.6-31.7 us with EARLY, profiles/r04o_mqa_early_ab.txt)
+    static const bool early = !(getenv("DV_MQA_EARLY") && atoi(getenv("DV_MQA_EARLY")) == 0);
+    const dim3 gkv((NKP / 32 + 3) / 4, S, B);
+    // DV_MQA_TPS=2: two query tiles per wave between barriers (measured slower:
+    // 33.1-33.8 vs 31.3-31.5 us, profiles/r04o_mqa_ph_tps_ab.txt)
+    static const bool tps2 = getenv("DV_MQA_TPS") && atoi(getenv("DV_MQA_TPS")) == 2;
+    if (early && tps2)
+      fa::mqa_dkdv_fa_kernel<true, 2><<<gkv, fa::NW * 64, 0, st>>>(
+          (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP, N + 1, rps, scale);
+    else if (early)
+      fa::mqa_dkdv_fa_kernel<true><<<gkv, fa::NW * 64, 0, st>>>(
+          (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP, N + 1, rps, scale);
+    else
+      fa::mqa_dkdv_fa_kernel<false><<<gkv, fa::NW * 64, 0, st>>>(
+          (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP, N + 1, rps, scale);
     DV_REQUIRE(S >= 1 && S <= 16, "split count out of range");
     fa::launch_finish<16>(S, grid_for((long long)B * N * 16), st, ws, B, N, NKP, (bf16*)dkv, lddkv,
                           dnull, accumulate);
