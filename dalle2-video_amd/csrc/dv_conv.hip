@@ -2847,12 +2847,15 @@ template <int W, int KS> struct StripeGeom {
 // rows then start 16 banks apart, so the transposed operand reads are
 // conflict-free WITHOUT a swizzle, and an operand address is linear in the
 // row — every tap's window offset folds into the ds_read immediate.
-template <int W, int KS>
+// STAG: only the second pixel half's waves (4-7) issue the stage DMAs, twice
+// as many each, so on every SIMD one wave (0-3) starts its MFMAs while its
+// partner pays the LDS-DMA issue (each SIMD holds one wave of each half)
+template <int W, int KS, bool STAG = false>
 __global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv_wgrad_stripe_kernel(WgradSArgs a) {
   using G = StripeGeom<W, KS>;
   constexpr int WP = G::WP, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF, NT = G::NT;
   constexpr int AIMG = G::AIMG, BHALF = G::BHALF;
-  constexpr int DPS = 2 + 2 * NRH;  // DMAs per thread per stage
+  constexpr int DPS = (STAG ? 2 : 1) * (2 + 2 * NRH);  // DMAs per issuing thread per stage
   // the bf16-partial epilogue sums the pixel halves in one pass (4 waves x
   // (NT x 16 + 1) x 64 floats), which can exceed the stage ring
   constexpr int RED1 = 4 * (NT * 16 + 1) * 64 * 4;
@@ -2877,43 +2880,60 @@ __global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv
   const int b_c = (first ? ci0 : ci0 - a.c0) + 8 * c4;  // this lane's channel in its source
   const __amdgpu_buffer_rsrc_t xrs =
       dma_rsrc(first ? a.x0 : a.x1, (unsigned)((long long)a.nstages * 128 * xld * 2));
-  int b_off[NRH], b_ry[NRH];  // b_ry: image-row offset, or a large negative for halo / junk rows
+  // DMA rows of the (virtual) waves this thread issues for: its own, or under
+  // STAG waves (w & 3) and (w | 4) from the second half's threads
+  constexpr int NV = STAG ? 2 : 1;
+  int b_off[NV][NRH], b_ry[NV][NRH];  // b_ry: image-row offset, or a large negative for halo / junk rows
 #pragma unroll
-  for (int i = 0; i < NRH; ++i) {
-    const int wr = 128 * i + 16 * wave + l4;
-    if (KS == 1) {  // the stage's own pixels
-      b_ry[i] = 0;
-      b_off[i] = wr;
-      continue;
+  for (int k = 0; k < NV; ++k) {
+    const int vw = STAG ? ((wave & 3) | (4 * k)) : wave;
+#pragma unroll
+    for (int i = 0; i < NRH; ++i) {
+      const int wr = 128 * i + 16 * vw + l4;
+      if (KS == 1) {  // the stage's own pixels
+        b_ry[k][i] = 0;
+        b_off[k][i] = wr;
+        continue;
+      }
+      const int sg = wr / segrows, rem = wr - sg * segrows;
+      const int ry = rem / WP, rx = rem - ry * WP;
+      const bool ok = sg < a.nseg && rx >= 1 && rx <= W;
+      b_ry[k][i] = ok ? ry - 1 : -(1 << 20);
+      b_off[k][i] = sg * seg * W + (ry - 1) * W + (rx - 1);
     }
-    const int sg = wr / segrows, rem = wr - sg * segrows;
-    const int ry = rem / WP, rx = rem - ry * WP;
-    const bool ok = sg < a.nseg && rx >= 1 && rx <= W;
-    b_ry[i] = ok ? ry - 1 : -(1 << 20);
-    b_off[i] = sg * seg * W + (ry - 1) * W + (rx - 1);
   }
 
-  auto issue = [&](int st, int buf) {
+  auto issue_vw = [&](int st, int buf, int vw, int k) {
     const int m0 = (sbeg + st) * 128;
     char* sA = smem + buf * STG;
     char* sB = sA + AIMG;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const bf16* src = a_src + 32 * hh + (long long)(m0 + 16 * wave + l4) * a.lddy;
+      const bf16* src = a_src + 32 * hh + (long long)(m0 + 16 * vw + l4) * a.lddy;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(sA + hh * (AIMG / 2) + 16 * wave * 64),
+                                       (__attribute__((address_space(3))) void*)(sA + hh * (AIMG / 2) + 16 * vw * 64),
                                        16, 0, 0);
     }
     const int y0 = (KS == 1 || a.nseg > 1) ? 0 : (m0 % HW) / W;
 #pragma unroll
     for (int i = 0; i < NRH; ++i) {
-      const bool in = KS == 1 || (unsigned)(y0 + b_ry[i]) < (unsigned)a.H;
+      const bool in = KS == 1 || (unsigned)(y0 + b_ry[k][i]) < (unsigned)a.H;
       // halo / pad rows load out of the raw buffer's range: 16 zero bytes
       // without a memory access (a shared zero line is one hot L2 channel)
-      const unsigned voff = in ? (unsigned)(((m0 + b_off[i]) * xld + b_c) * 2) : DMA_OOB;
+      const unsigned voff = in ? (unsigned)(((m0 + b_off[k][i]) * xld + b_c) * 2) : DMA_OOB;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
-        dma16(xrs, sB + hh * BHALF + (128 * i + 16 * wave) * 64, in ? voff + 64 * hh : DMA_OOB);
+        dma16(xrs, sB + hh * BHALF + (128 * i + 16 * vw) * 64, in ? voff + 64 * hh : DMA_OOB);
+    }
+  };
+  auto issue = [&](int st, int buf) {
+    if constexpr (STAG) {
+      if (half) {  // wave-uniform
+        issue_vw(st, buf, wave & 3, 0);
+        issue_vw(st, buf, wave, 1);
+      }
+    } else {
+      issue_vw(st, buf, wave, 0);
     }
   };
 
@@ -3374,8 +3394,18 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   a.dbpart = db ? ws + (long long)S * cout * a.K / (a.part_bf16 ? 2 : 1) : nullptr;
   a.dw = dw; a.db = db; a.acc_w = acc_w; a.acc_b = acc_b;
   dim3 grid(cout / 64, cin / 64, S);
+  // the 3x3 stage DMAs issued by waves 4-7 only: family 1,897 -> 1,874 us per
+  // step, step equal (profiles/r04p_wgrad_stag_ab.txt); DV_WG_STAG=0: every wave
+  static const bool stag = !(getenv("DV_WG_STAG") && atoi(getenv("DV_WG_STAG")) == 0);
   if (ks == 1) {
     conv_wgrad_stripe_kernel<64, 1><<<grid, 512, 0, st>>>(a);
+  } else if (stag) {
+    switch (w) {
+      case 64: conv_wgrad_stripe_kernel<64, 3, true><<<grid, 512, 0, st>>>(a); break;
+      case 32: conv_wgrad_stripe_kernel<32, 3, true><<<grid, 512, 0, st>>>(a); break;
+      case 16: conv_wgrad_stripe_kernel<16, 3, true><<<grid, 512, 0, st>>>(a); break;
+      default: conv_wgrad_stripe_kernel<8, 3, true><<<grid, 512, 0, st>>>(a); break;
+    }
   } else {
     switch (w) {
       case 64: conv_wgrad_stripe_kernel<64, 3><<<grid, 512, 0, st>>>(a); break;
