@@ -2135,8 +2135,11 @@ __device__ __forceinline__ int fw_pix(int r) {
 // VGPRs, written to LDS by a ds_write_b128 two chunks later (two register
 // sets alternate by chunk parity; a 2-deep LDS ring: chunk c read, chunk c+1
 // written).  The compiler's vmcnt tracking orders each store after its load.
+// BAR2: one barrier per two chunks.  Chunk c then refills the buffer of chunk
+// c - 2 (AHEAD = NBUF - 2), which every wave left before the last barrier,
+// and the barrier after an odd chunk waits for the next two chunks
 template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4,
-          int KSPL = 1, int NB = 0, bool RS = false>
+          int KSPL = 1, int NB = 0, bool RS = false, bool BAR2 = false>
 __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
   using G = FwGeom<W, CO, NWV, RS ? 2 : NB>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
@@ -2144,6 +2147,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   static_assert(NWV == 4 || (NWV == 8 && !STATS), "the 8-wave tile has no statistics epilogue");
   static_assert(NPW <= 9, "one DMA piece per tap");
   static_assert(!RS || NBUF == 2, "register staging runs a 2-deep ring");
+  static_assert(!BAR2 || (!RS && NBUF >= 4), "two chunks per barrier need a 4-deep ring");
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
   DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2220,7 +2224,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
 #pragma unroll
     for (int i = 0; i < NPW; ++i) issue1(c, i);
   };
-  constexpr int AHEAD = NBUF - 1;  // chunks in flight beyond the one being read
+  constexpr int AHEAD = NBUF - 1 - (BAR2 ? 1 : 0);  // chunks in flight beyond the one being read
   // RS: piece i of chunk c into / out of registers (chunk c's LDS buffer:
   // relative chunk index parity)
   u32x4 stA[RS ? NPW : 1], stB[RS ? NPW : 1];
@@ -2255,7 +2259,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
 #pragma unroll
     for (int c = 0; c < AHEAD; ++c)
       if (c < nch) issue(cbeg + c);
-    const int pro = min(AHEAD, nch) - 1;  // younger chunks than chunk 0
+    const int pro = min(AHEAD, nch) - (BAR2 ? 2 : 1);  // younger chunks than chunk 0 (BAR2: and 1)
     if (pro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
     else if (pro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
     else if (pro == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
@@ -2326,10 +2330,29 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
           if (decltype(PRE)::value || c + 1 < cend) st1(S[d], c + 1, d);
           if (decltype(PRE)::value || c + 3 < cend) ld1(S[d], c + 3, d);
         }
-      } else if constexpr (decltype(PRE)::value) {
+      } else if (decltype(PRE)::value || (BAR2 && c + AHEAD < cend)) {
+        // (BAR2: the pair loop's tail may still hold the chunk issuing the last)
         if (d < NPW) issue1(c + AHEAD, d);
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (BAR2) {
+      // even chunk (relative to cbeg) that is not the last: no barrier; the
+      // last barrier already waited for this chunk's successor
+      if (!decltype(PAR)::value && c + 1 < cend) return;
+      // chunks c+1 and c+2 landed: younger are chunks c+3 .. c+AHEAD
+      if constexpr (decltype(PRE)::value) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((AHEAD - 2) * NPW) : "memory");
+      } else {
+        const int young = min(c + AHEAD, cend - 1) - (c + 2);
+        if (young >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
+        else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (DEFER && CO == 64) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0), "+v"(la1)::"memory");
+      else if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0)::"memory");
+      __builtin_amdgcn_s_barrier();
+      return;
     }
     if constexpr (RS) {
       // this wave's stores of chunk c+1 done before the barrier
@@ -2356,7 +2379,16 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   using P0 = std::false_type;
   using P1 = std::true_type;
   int c = cbeg;
-  if constexpr (RS) {
+  if constexpr (BAR2) {
+    for (; c + 1 + AHEAD < cend; c += 2) {
+      chunk(c, std::true_type{}, P0{});
+      chunk(c + 1, std::true_type{}, P1{});
+    }
+    for (; c < cend; c += 2) {
+      chunk(c, std::false_type{}, P0{});
+      if (c + 1 < cend) chunk(c + 1, std::false_type{}, P1{});
+    }
+  } else if constexpr (RS) {
     for (; c + 4 < cend; c += 2) {
       chunk(c, std::true_type{}, P0{});
       chunk(c + 1, std::true_type{}, P1{});
@@ -2630,6 +2662,18 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
       if (a.c0 < a.cin) conv_fwd_frame_kernel<16, false, 3, 1, 64, true, 8><<<nblk, 512, 0, st>>>(a);
       else conv_fwd_frame_kernel<16, false, 3, 1, 64, false, 8><<<nblk, 512, 0, st>>>(a);
     }
+    return check_launch("conv_fwd_frame");
+  }
+  // DV_FRAME_BAR2=1: one barrier per two chunks (A/B; rings of >= 4 buffers)
+  static const bool bar2 = getenv("DV_FRAME_BAR2") && atoi(getenv("DV_FRAME_BAR2")) != 0;
+  if (bar2 && a.W == 8) {
+#define DV_FB5(C, SP) (a.gn_sums ? conv_fwd_frame_kernel<8, true, 3, 1, C, SP, 4, 1, 0, false, true><<<nblk, 256, 0, st>>>(a) \
+                             : conv_fwd_frame_kernel<8, false, 3, 1, C, SP, 4, 1, 0, false, true><<<nblk, 256, 0, st>>>(a))
+#define DV_FB4(C) (a.c0 < a.cin ? DV_FB5(C, true) : DV_FB5(C, false))
+    if (co == 32) DV_FB4(32);
+    else DV_FB4(64);
+#undef DV_FB4
+#undef DV_FB5
     return check_launch("conv_fwd_frame");
   }
   if (rs) {
