@@ -372,7 +372,10 @@ def main():
     backend = os.environ.get("DV_DIST_BACKEND", "nccl")
     if os.environ.get("DV_SHARE_GPU") == "1":
         local = local % torch.cuda.device_count()
-    if world > 1:
+    # DV_BENCH_PG=1 (+ DV_FORCE_ALLREDUCE=1): a one-rank process group, so the
+    # N > 1 step (bucketed RCCL all-reduce captured with the backward) runs on
+    # a one-GPU box
+    if world > 1 or os.environ.get("DV_BENCH_PG") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -507,7 +510,7 @@ def main():
             "fp32": fp32, "sampling": sampling, "attention": attention,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

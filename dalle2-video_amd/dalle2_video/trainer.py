@@ -923,7 +923,8 @@ class VideoDecoderTrainer(nn.Module):
             # a previous call's buckets may still be in flight on the comm
             # stream: this call's backward accumulates into the same buffer
             ov.wait()
-        if self._graphable(unet_number, max_batch_size, return_lowres_cond_video):
+        graphable = self._graphable(unet_number, max_batch_size, return_lowres_cond_video)
+        if graphable:
             out = self._graphed_call(unet_number, args, kwargs)
             if out is not None:
                 return out
@@ -932,6 +933,13 @@ class VideoDecoderTrainer(nn.Module):
         chunks = list(split_args_and_kwargs(*args, split_size=max_batch_size, **kwargs))
         # overlap only a single-chunk call (chunks accumulate into the same buffer)
         ov = self._overlap_for(unet_number) if (self.training and len(chunks) == 1) else None
+        if ov is not None and graphable and dist.get_backend() != "nccl":
+            # the eager calls that warm a capture run the pass the graph will
+            # hold: without a capturable collective (gloo) the graph has no
+            # bucket hooks, so the deferred split-K sums it replays are ONE
+            # batch; bucket flushes here would leave the captured pass a
+            # deferred-sum table no eager call built (ops._WgradDefer.flush)
+            ov = None
         self._reduced[unet_number - 1] = False
         for frac, (cargs, ckw) in chunks:
             ctx = torch.autocast("cuda", dtype=torch.bfloat16) if self.amp else nullcontext()
