@@ -2872,18 +2872,26 @@ struct WgradSArgs {
 #ifndef DV_WG1_NBUF
 #define DV_WG1_NBUF 2
 #endif
-template <int W, int KS> struct StripeGeom {
+// TRIM: where the window image rounded up to whole 128-row DMA rounds leaves
+// room for only two stages (W = 64: 264 rows in 384), allocate the rows a
+// wave's 16-row piece can reach (272) and send the pieces past them to a 1 KB
+// junk line (zeros, no memory access): three stages fit, two in flight
+template <int W, int KS, bool TRIMOK = false> struct StripeGeom {
   static constexpr int WP = W + 2;
   // window rows (max over H): KS == 1 stages the 128 pixels themselves
   static constexpr int WR = KS == 1 ? 128 : (W == 8 ? 200 : (128 / W + 2) * WP);
   static constexpr int NRH = (WR + 127) / 128;                  // 128-row DMA rounds per half
   static constexpr int AIMG = 2 * 128 * 64;                     // dY image: 2 co halves x 128 rows x 64 B
-  static constexpr int BHALF = NRH * 128 * 64;                  // window image of one ci half
+  static constexpr int WRA = (WR + 15) / 16 * 16;               // rows a 16-row piece reaches
+  static constexpr bool TRIM = TRIMOK && KS == 3 && (AIMG + 2 * NRH * 128 * 64) * 3 > 160 * 1024 &&
+                               (AIMG + 2 * WRA * 64) * 3 + 1024 <= 160 * 1024;
+  static constexpr int BHALF = (TRIM ? WRA : NRH * 128) * 64;   // window image of one ci half
   static constexpr int STG = AIMG + 2 * BHALF;
+  static constexpr int JUNK = TRIM ? 1024 : 0;                  // after the ring
   // 1x1: a 2-deep ring (64 KB) so that two workgroups share a CU -- a stage
   // holds one tap's MFMAs only, too little to cover the next stage's DMA
   // latency inside one workgroup
-  static constexpr int NBUF = KS == 1 ? DV_WG1_NBUF : (STG * 3 <= 160 * 1024 ? 3 : 2);
+  static constexpr int NBUF = KS == 1 ? DV_WG1_NBUF : (STG * 3 + JUNK <= 160 * 1024 ? 3 : 2);
   static constexpr int NT = KS * KS;                            // taps
 };
 
@@ -2894,16 +2902,17 @@ template <int W, int KS> struct StripeGeom {
 // STAG: only the second pixel half's waves (4-7) issue the stage DMAs, twice
 // as many each, so on every SIMD one wave (0-3) starts its MFMAs while its
 // partner pays the LDS-DMA issue (each SIMD holds one wave of each half)
-template <int W, int KS, bool STAG = false>
+template <int W, int KS, bool STAG = false, bool TRIMOK = false>
 __global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv_wgrad_stripe_kernel(WgradSArgs a) {
-  using G = StripeGeom<W, KS>;
+  using G = StripeGeom<W, KS, TRIMOK>;
   constexpr int WP = G::WP, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF, NT = G::NT;
   constexpr int AIMG = G::AIMG, BHALF = G::BHALF;
   constexpr int DPS = (STAG ? 2 : 1) * (2 + 2 * NRH);  // DMAs per issuing thread per stage
   // the bf16-partial epilogue sums the pixel halves in one pass (4 waves x
   // (NT x 16 + 1) x 64 floats), which can exceed the stage ring
   constexpr int RED1 = 4 * (NT * 16 + 1) * 64 * 4;
-  __shared__ __attribute__((aligned(1024))) char smem[NBUF * STG > RED1 ? NBUF * STG : RED1];
+  constexpr int RING = NBUF * STG + G::JUNK;
+  __shared__ __attribute__((aligned(1024))) char smem[RING > RED1 ? RING : RED1];
 
   DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2965,9 +2974,11 @@ __global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv
       // halo / pad rows load out of the raw buffer's range: 16 zero bytes
       // without a memory access (a shared zero line is one hot L2 channel)
       const unsigned voff = in ? (unsigned)(((m0 + b_off[k][i]) * xld + b_c) * 2) : DMA_OOB;
+      const int drow = 128 * i + 16 * vw;  // wave-uniform
+      const bool live = !G::TRIM || drow < G::WRA;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
-        dma16(xrs, sB + hh * BHALF + (128 * i + 16 * vw) * 64, in ? voff + 64 * hh : DMA_OOB);
+        dma16(xrs, live ? sB + hh * BHALF + drow * 64 : smem + NBUF * STG, live && in ? voff + 64 * hh : DMA_OOB);
     }
   };
   auto issue = [&](int st, int buf) {
@@ -3444,8 +3455,15 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   if (ks == 1) {
     conv_wgrad_stripe_kernel<64, 1><<<grid, 512, 0, st>>>(a);
   } else if (stag) {
+    // DV_WG_TRIM=1: the W = 64 window image trimmed to a 3-deep ring.  Measured
+    // no faster (36.3-36.5 -> 36.9-37.0 us per launch, profiles/r04t_wgrad_trim_ab.txt):
+    // one stage in flight already covers the load latency here
+    static const bool trim = getenv("DV_WG_TRIM") && atoi(getenv("DV_WG_TRIM")) != 0;
     switch (w) {
-      case 64: conv_wgrad_stripe_kernel<64, 3, true><<<grid, 512, 0, st>>>(a); break;
+      case 64:
+        if (trim) conv_wgrad_stripe_kernel<64, 3, true, true><<<grid, 512, 0, st>>>(a);
+        else conv_wgrad_stripe_kernel<64, 3, true><<<grid, 512, 0, st>>>(a);
+        break;
       case 32: conv_wgrad_stripe_kernel<32, 3, true><<<grid, 512, 0, st>>>(a); break;
       case 16: conv_wgrad_stripe_kernel<16, 3, true><<<grid, 512, 0, st>>>(a); break;
       default: conv_wgrad_stripe_kernel<8, 3, true><<<grid, 512, 0, st>>>(a); break;
