@@ -2283,7 +2283,37 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   // DEFER: the last tap's MFMAs of chunk c run after the chunk's barrier, while
   // chunk c+1's first fragment reads are in flight (its operands are in
   // registers before the barrier, so the buffer may be refilled under them)
-  u32x4 lb, la0, la1;
+  // DEFER = 2: taps 7 and 8 (slot 0: tap 7, odd -> chains 2 / 3; slot 1: tap 8)
+  static_assert(DEFER <= 2, "at most the last two taps are deferred");
+  u32x4 lb[2], la0[2], la1[2];
+  auto run_deferred = [&]() {
+#pragma unroll
+    for (int t = 0; t < DEFER; ++t) {
+      const int tap = 9 - DEFER + t;
+      if (tap & 1) {
+        acc2 = Mma<bf16>::run(la0[t], lb[t], acc2);
+        if (CO == 64) acc3 = Mma<bf16>::run(la1[t], lb[t], acc3);
+      } else {
+        acc0 = Mma<bf16>::run(la0[t], lb[t], acc0);
+        if (CO == 64) acc1 = Mma<bf16>::run(la1[t], lb[t], acc1);
+      }
+    }
+  };
+  // the deferred fragments are in registers before the barrier (their
+  // buffer may be refilled behind it)
+  auto defer_wait = [&]() {
+    if (DEFER == 2 && CO == 64)
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb[0]), "+v"(la0[0]), "+v"(la1[0]), "+v"(lb[1]), "+v"(la0[1]),
+                   "+v"(la1[1])::"memory");
+    else if (DEFER == 2)
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb[0]), "+v"(la0[0]), "+v"(lb[1]), "+v"(la0[1])::"memory");
+    else if (DEFER && CO == 64)
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb[0]), "+v"(la0[0]), "+v"(la1[0])::"memory");
+    else if (DEFER)
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb[0]), "+v"(la0[0])::"memory");
+    else
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
   // one chunk; PRE (compile-time): chunk c + AHEAD exists and is issued here.
   // The loop is split into the chunks that issue and the AHEAD tail, so the
   // main loop carries no per-piece branch and a constant vmcnt
@@ -2301,19 +2331,17 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     };
 #pragma unroll
     for (int d = 0; d < PF; ++d) rd(d, d);
-    if (DEFER && c > cbeg) {  // tap 8 of chunk c-1 (even tap: chains 0 / 1)
-      acc0 = Mma<bf16>::run(la0, lb, acc0);
-      if (CO == 64) acc1 = Mma<bf16>::run(la1, lb, acc1);
-    }
+    if (DEFER && c > cbeg) run_deferred();  // the last taps of chunk c-1
     // chunk c+AHEAD's pieces go out one per tap, in the MFMA shadow: its
     // buffer was last read in chunk c-1, before the last barrier
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
       if (d + PF < 9) rd(d + PF, (d + PF) % NS);
-      if (DEFER && d == 8) {
-        lb = bq[d % NS];
-        la0 = aq0[d % NS];
-        if (CO == 64) la1 = aq1[d % NS];
+      if (DEFER && d >= 9 - DEFER) {
+        const int t = d - (9 - DEFER);
+        lb[t] = bq[d % NS];
+        la0[t] = aq0[d % NS];
+        if (CO == 64) la1[t] = aq1[d % NS];
       } else if (d & 1) {
         acc2 = Mma<bf16>::run(aq0[d % NS], bq[d % NS], acc2);
         if (CO == 64) acc3 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc3);
@@ -2349,16 +2377,13 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
         else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      if (DEFER && CO == 64) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0), "+v"(la1)::"memory");
-      else if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0)::"memory");
+      if (DEFER) defer_wait();
       __builtin_amdgcn_s_barrier();
       return;
     }
     if constexpr (RS) {
       // this wave's stores of chunk c+1 done before the barrier
-      if (DEFER && CO == 64) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0), "+v"(la1)::"memory");
-      else if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0)::"memory");
-      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      defer_wait();
       __builtin_amdgcn_s_barrier();
       return;
     }
@@ -2372,8 +2397,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
       else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (DEFER && CO == 64) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0), "+v"(la1)::"memory");
-    else if (DEFER) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lb), "+v"(la0)::"memory");
+    if (DEFER) defer_wait();
     __builtin_amdgcn_s_barrier();
   };
   using P0 = std::false_type;
@@ -2401,10 +2425,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     for (; c + AHEAD < cend; ++c) chunk(c, std::true_type{}, P0{});
     for (; c < cend; ++c) chunk(c, std::false_type{}, P0{});
   }
-  if (DEFER && nch > 0) {
-    acc0 = Mma<bf16>::run(la0, lb, acc0);
-    if (CO == 64) acc1 = Mma<bf16>::run(la1, lb, acc1);
-  }
+  if (DEFER && nch > 0) run_deferred();
   DV_STAMP_AT(2);
   if constexpr (KSPL == 2) {
     // hand-off: both halves write their partial (lane-linear, 1 KB per wave
@@ -2595,6 +2616,27 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   // DV_FRAME_KS256=1: also split the 256-tile grids, two workgroups per CU on
   // a 2-deep ring (A/B)
   static const bool ks256 = getenv("DV_FRAME_KS256") && atoi(getenv("DV_FRAME_KS256")) != 0;
+  // DV_FRAME_W8KS=1 (with DV_FRAME_KSPLIT=1 / 2): the 8x8 grids of 256 64-channel
+  // tiles as 128 tiles of 128 channels (8 waves, the window staged once for both
+  // channel halves: 0.35 instead of 0.43 KB of LDS-DMA per MFMA) with the chunk
+  // loop split over two workgroups (256 workgroups); no statistics epilogue
+  static const bool w8ks = getenv("DV_FRAME_W8KS") && atoi(getenv("DV_FRAME_W8KS")) != 0;
+  if (ks_ok && w8ks && a.W == 8 && !a.gn_sums && a.cout % 128 == 0 && tiles64 == 256 &&
+      (a.cin / 16) % 2 == 0) {
+    KsScratch* ks = ks_scratch();
+    const int tiles128 = tiles64 / 2;
+    if (ks && ks->nflags > tiles128 && ks->bytes >= (long long)tiles128 * 2 * 8 * 2 * 16 * 64 * 4) {
+      a.ks_part = ks->part;
+      a.ks_flag = ks->flags;
+      a.ks_err = ks->flags + ks->nflags - 1;
+      a.ks_local = ks_local;
+      a.xcd_c = frame_xcd_split(a, 128);
+      const int nb2 = 2 * tiles128;
+      if (a.c0 < a.cin) conv_fwd_frame_kernel<8, false, 3, 1, 64, true, 8, 2><<<nb2, 512, 0, st>>>(a);
+      else conv_fwd_frame_kernel<8, false, 3, 1, 64, false, 8, 2><<<nb2, 512, 0, st>>>(a);
+      return check_launch("conv_fwd_frame");
+    }
+  }
   if (ks_ok && ks256 && tiles64 == 256 && a.W == 8 && (a.cin / 16) % 2 == 0) {
     KsScratch* ks = ks_scratch();
     if (ks && ks->nflags > tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {
@@ -2661,6 +2703,24 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
     } else {
       if (a.c0 < a.cin) conv_fwd_frame_kernel<16, false, 3, 1, 64, true, 8><<<nblk, 512, 0, st>>>(a);
       else conv_fwd_frame_kernel<16, false, 3, 1, 64, false, 8><<<nblk, 512, 0, st>>>(a);
+    }
+    return check_launch("conv_fwd_frame");
+  }
+  // DV_FRAME_DEFER2=1: the last two taps' MFMAs of a chunk run behind its barrier (A/B)
+  static const bool defer2 = getenv("DV_FRAME_DEFER2") && atoi(getenv("DV_FRAME_DEFER2")) != 0;
+  if (defer2) {
+    switch (a.W) {
+#define DV_FD5(WW, C, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 2, C, SP><<<nblk, 256, 0, st>>>(a) \
+                                 : conv_fwd_frame_kernel<WW, false, 3, 2, C, SP><<<nblk, 256, 0, st>>>(a))
+#define DV_FD4(WW, C) (a.c0 < a.cin ? DV_FD5(WW, C, true) : DV_FD5(WW, C, false))
+#define DV_FD(WW) (co == 32 ? DV_FD4(WW, 32) : DV_FD4(WW, 64))
+      case 8: DV_FD(8); break;
+      case 16: DV_FD(16); break;
+      case 32: DV_FD(32); break;
+      default: DV_FD(64); break;
+#undef DV_FD
+#undef DV_FD4
+#undef DV_FD5
     }
     return check_launch("conv_fwd_frame");
   }
