@@ -141,8 +141,10 @@ def _bench(nproc, env_extra, tmp_path):
     out = p.stdout.decode(errors="replace")
     assert p.returncode == 0, out[-4000:]
     import json
-    line = [ln for ln in out.splitlines() if ln.startswith("{")][-1]
-    return json.loads(line)
+    # rank 0's one JSON line; another rank's log output may share the line
+    # (two processes write to one pipe), so decode from the object's start
+    line = [ln for ln in out.splitlines() if '{"metric"' in ln][-1]
+    return json.JSONDecoder().raw_decode(line[line.index('{"metric"'):])[0]
 
 
 def test_bench_two_ranks_gloo_shared_gpu(tmp_path):
