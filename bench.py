@@ -509,7 +509,10 @@ def main():
             "kernels": kernels, "conv_shapes": conv_shapes[:24] if conv_shapes else None,
             "fp32": fp32, "sampling": sampling, "attention": attention,
         }
-        print(json.dumps(out), flush=True)
+        # one write (line and newline together): another rank's stderr merged
+        # into the same pipe cannot land inside the line
+        sys.stdout.write(json.dumps(out) + "\n")
+        sys.stdout.flush()
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
