@@ -21,7 +21,9 @@ for path in sys.argv[1:]:
         name = r["Kernel_Name"]
         if "frame" not in name and "stripe" not in name:
             continue
-        short = name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[-60:]
+        # mangled: keep the kernel name and its template arguments
+        short = (name.split("N_1")[-1].split("EvNS_")[0] if "_ZN" in name
+                 else name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0])[-60:]
         grid = r.get("Grid_Size", r.get("Grid_Size_X", "?"))
         acc[(short, grid)][r["Counter_Name"]].append(float(r["Counter_Value"]))
 
