@@ -15,6 +15,7 @@
 // host without RCCL; only these entry points then fail.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types and enums only: nothing is linked, RCCL is dlopen'ed
 
 #include <cstring>
 #include <mutex>
@@ -28,22 +29,22 @@ void set_error(const std::string& msg);
 
 namespace {
 
-// the few RCCL types the calls below need (ABI of rccl.h, NCCL 2.x)
-typedef struct ncclComm* ncclComm_t;
-typedef struct {
-  char internal[128];
-} ncclUniqueId;
-typedef int ncclResult_t;  // ncclSuccess = 0
-enum { kNcclFloat32 = 7, kNcclBfloat16 = 9, kNcclSum = 0, kNcclAvg = 4 };
+// the ABI comes from the image's rccl.h (the resolved symbols are cast to the
+// header's own prototypes); the unique id travels as 128 raw bytes through
+// the torch.distributed store and the Python binding
+static_assert(sizeof(ncclUniqueId) == 128 && NCCL_UNIQUE_ID_BYTES == 128,
+              "dv_comm_unique_id hands out 128 bytes (include/dv_hip.h, trainer.GradComm)");
+static_assert(ncclSuccess == 0, "status 0 is success");
 
 struct Rccl {
   void* handle = nullptr;
-  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
-  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
-  ncclResult_t (*all_reduce)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
-  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
-  ncclResult_t (*comm_get_async_error)(ncclComm_t, ncclResult_t*) = nullptr;
-  const char* (*get_error_string)(ncclResult_t) = nullptr;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;
+  decltype(&ncclCommGetAsyncError) comm_get_async_error = nullptr;
+  decltype(&ncclGetErrorString) get_error_string = nullptr;
   std::string why;
 };
 
@@ -66,9 +67,11 @@ Rccl& rccl() {
     r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
     r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.comm_abort = (decltype(r.comm_abort))dlsym(h, "ncclCommAbort");
     r.comm_get_async_error = (decltype(r.comm_get_async_error))dlsym(h, "ncclCommGetAsyncError");
     r.get_error_string = (decltype(r.get_error_string))dlsym(h, "ncclGetErrorString");
-    if (!r.get_unique_id || !r.comm_init_rank || !r.all_reduce || !r.comm_destroy || !r.get_error_string) {
+    if (!r.get_unique_id || !r.comm_init_rank || !r.all_reduce || !r.comm_destroy || !r.comm_abort ||
+        !r.get_error_string) {
       r.why = "librccl.so.1 lacks an expected symbol";
       r.handle = nullptr;
     }
@@ -133,8 +136,8 @@ extern "C" int dv_comm_allreduce(void* comm, void* buf, long long count, int dty
   }
   if (count == 0) return DV_OK;
   if (!ready("dv_comm_allreduce")) return DV_ERR_UNSUPPORTED;
-  ncclResult_t rc = rccl().all_reduce(buf, buf, (size_t)count, dtype == DV_F32 ? kNcclFloat32 : kNcclBfloat16,
-                                      average ? kNcclAvg : kNcclSum, (ncclComm_t)comm, (hipStream_t)stream);
+  ncclResult_t rc = rccl().all_reduce(buf, buf, (size_t)count, dtype == DV_F32 ? ncclFloat32 : ncclBfloat16,
+                                      average ? ncclAvg : ncclSum, (ncclComm_t)comm, (hipStream_t)stream);
   if (rc != 0) return fail("ncclAllReduce", rc);
   return DV_OK;
 }
@@ -146,10 +149,10 @@ extern "C" int dv_comm_async_error(void* comm) {
   }
   if (!ready("dv_comm_async_error")) return DV_ERR_UNSUPPORTED;
   if (!rccl().comm_get_async_error) return DV_OK;
-  ncclResult_t st = 0;
+  ncclResult_t st = ncclSuccess;
   ncclResult_t rc = rccl().comm_get_async_error((ncclComm_t)comm, &st);
-  if (rc != 0) return fail("ncclCommGetAsyncError", rc);
-  if (st != 0) return fail("communicator async error", st);
+  if (rc != ncclSuccess) return fail("ncclCommGetAsyncError", rc);
+  if (st != ncclSuccess && st != ncclInProgress) return fail("communicator async error", st);
   return DV_OK;
 }
 
@@ -161,5 +164,16 @@ extern "C" int dv_comm_destroy(void* comm) {
   if (!ready("dv_comm_destroy")) return DV_ERR_UNSUPPORTED;
   ncclResult_t rc = rccl().comm_destroy((ncclComm_t)comm);
   if (rc != 0) return fail("ncclCommDestroy", rc);
+  return DV_OK;
+}
+
+extern "C" int dv_comm_abort(void* comm) {
+  if (!comm) {
+    dv::set_error("dv_comm_abort: null communicator");
+    return DV_ERR_INVALID;
+  }
+  if (!ready("dv_comm_abort")) return DV_ERR_UNSUPPORTED;
+  ncclResult_t rc = rccl().comm_abort((ncclComm_t)comm);
+  if (rc != 0) return fail("ncclCommAbort", rc);
   return DV_OK;
 }

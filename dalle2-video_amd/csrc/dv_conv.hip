@@ -837,6 +837,19 @@ __device__ __forceinline__ s16x4 tr_read_at(unsigned base, int off) {
       (__attribute__((address_space(3))) s16x4*)((lds_char*)(size_t)base + off));
 }
 
+// ds_read_b64_tr_b16 at base + OFF outside hipcc's waitcnt tracking; the
+// caller waits with a counted lgkmcnt tied to the result.  Why: hipcc drains
+// vmcnt(0) before every ds_read_b64_tr_b16 it can see while an LDS-DMA is in
+// flight (it cannot tell ring buffers apart; a plain ds_read_b128 does not get
+// the drain), which serialises a DMA ring with the MFMAs that read it.
+template <int OFF>
+__device__ __forceinline__ u32x2 tr_read_asm(unsigned base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
+  u32x2 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
+  return r;
+}
+
 template <typename T, int BMC, int BNK>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs<T> p) {
   constexpr int VEC = 16 / sizeof(T);
@@ -1202,28 +1215,48 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
     __builtin_amdgcn_s_barrier();
     const char* sA = smem + buf * BUF;
     const char* sB = sA + BP * RA;
+    // operand bases of k-step 0 (row R0 = 8 (g >> 1) + q; the swizzle of rows
+    // R0 + 16 s and + 4 equals row R0's, so k-step s and the high half are
+    // immediate offsets 16 s RA (RB) and 4 RA (RB)); asm reads, counted waits
+    unsigned abase[TJ], bbase[TI];
 #pragma unroll
-    for (int s = 0; s < BP / 16; ++s) {
-      const int R0 = 16 * s + 8 * (g >> 1);
+    for (int j = 0; j < TJ; ++j) {
+      const int C0 = wm * 64 + 32 * j + 16 * (g & 1) + 4 * pp;  // element column
+      abase[j] = lds_u32(sA) + img_off<RA>(8 * (g >> 1) + q, C0 >> 3) + (C0 & 7) * 2;
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int C0 = wn * 32 * TI + 32 * i + 16 * (g & 1) + 4 * pp;
+      bbase[i] = lds_u32(sB) + img_off<RB>(8 * (g >> 1) + q, C0 >> 3) + (C0 & 7) * 2;
+    }
+    constexpr int NS = BP / 16, NRD = 2 * (TJ + TI);  // k-steps, reads per k-step
+    u32x2 ra[2][TJ][2], rb[2][TI][2];
+    auto rd = [&](auto S) {
+      constexpr int s = decltype(S)::value;
+      static_for<0, TJ>([&](auto J) {
+        ra[s & 1][J][0] = tr_read_asm<16 * s * RA>(abase[J]);
+        ra[s & 1][J][1] = tr_read_asm<16 * s * RA + 4 * RA>(abase[J]);
+      });
+      static_for<0, TI>([&](auto I) {
+        rb[s & 1][I][0] = tr_read_asm<16 * s * RB>(bbase[I]);
+        rb[s & 1][I][1] = tr_read_asm<16 * s * RB + 4 * RB>(bbase[I]);
+      });
+    };
+    rd(std::integral_constant<int, 0>{});
+    static_for<0, NS>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      if constexpr (s + 1 < NS) rd(std::integral_constant<int, s + 1>{});
       u32x4 fa[TJ], fb[TI];
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int C0 = wm * 64 + 32 * j + 16 * (g & 1) + 4 * pp;  // element column
-        const int ch = C0 >> 3, o8 = (C0 & 7) * 2;
-        const s16x4 lo = tr_read(sA + img_off<RA>(R0 + q, ch) + o8);
-        const s16x4 hi = tr_read(sA + img_off<RA>(R0 + 4 + q, ch) + o8);
-        const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
-        fa[j] = u32x4{l2[0], l2[1], h2[0], h2[1]};
-      }
-#pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int C0 = wn * 32 * TI + 32 * i + 16 * (g & 1) + 4 * pp;
-        const int ch = C0 >> 3, o8 = (C0 & 7) * 2;
-        const s16x4 lo = tr_read(sB + img_off<RB>(R0 + q, ch) + o8);
-        const s16x4 hi = tr_read(sB + img_off<RB>(R0 + 4 + q, ch) + o8);
-        const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
-        fb[i] = u32x4{l2[0], l2[1], h2[0], h2[1]};
-      }
+      static_for<0, TJ>([&](auto J) {
+        asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(ra[s & 1][J][0]), "+v"(ra[s & 1][J][1])
+                     : "n"(s + 1 < NS ? NRD : 0));
+        fa[J] = u32x4{ra[s & 1][J][0][0], ra[s & 1][J][0][1], ra[s & 1][J][1][0], ra[s & 1][J][1][1]};
+      });
+      static_for<0, TI>([&](auto I) {
+        asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(rb[s & 1][I][0]), "+v"(rb[s & 1][I][1])
+                     : "n"(s + 1 < NS ? NRD : 0));
+        fb[I] = u32x4{rb[s & 1][I][0][0], rb[s & 1][I][0][1], rb[s & 1][I][1][0], rb[s & 1][I][1][1]};
+      });
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
@@ -1232,7 +1265,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
 #pragma unroll
         for (int j = 0; j < TJ; ++j) accb[j] = Mma<bf16>::run(fa[j], ones, accb[j]);
       }
-    }
+    });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
@@ -2927,6 +2960,7 @@ struct WgradSArgs {
   int H, cin, cout, K;
   int nstages, stages_per_split;
   int seg, nseg;  // image rows per window segment, segments per stage
+  int xcd;        // window kernel: deal (split, co, ci) tiles to XCDs in contiguous chunks
 };
 
 #ifndef DV_WG1_NBUF
@@ -2954,6 +2988,129 @@ template <int W, int KS, bool TRIMOK = false> struct StripeGeom {
   static constexpr int NBUF = KS == 1 ? DV_WG1_NBUF : (STG * 3 + JUNK <= 160 * 1024 ? 3 : 2);
   static constexpr int NT = KS * KS;                            // taps
 };
+
+// the row-window wgrad tile epilogue (both wgrad kernels): the two pixel
+// halves summed through LDS, then the 64 x 64 x NT tile written in the torch
+// layout -- bf16 split partials, f32 split partials or the gradient itself
+template <int NT>
+__device__ __forceinline__ void wgrad_tile_store(const WgradSArgs& a, f32x16 (&acc)[NT], float accb, char* smem,
+                                                 int half, int wq, int wm, int wn, int lane, int co0, int ci0,
+                                                 bool do_bias, int bz) {
+
+  // ---- sum the two pixel halves through LDS in one pass (16-B rows per lane) ----
+  float* red = (float*)smem;
+  constexpr int PERW = (NT * 16 + 1) * 64;  // floats per wave
+  if (half == 1) {
+#pragma unroll
+    for (int d = 0; d < NT; ++d)
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4)
+        *(f32x4*)(red + wq * PERW + (d * 4 + e4) * 256 + lane * 4) =
+            f32x4{acc[d][4 * e4], acc[d][4 * e4 + 1], acc[d][4 * e4 + 2], acc[d][4 * e4 + 3]};
+    red[wq * PERW + NT * 16 * 64 + lane] = accb;
+  }
+  __syncthreads();
+  if (half == 0) {
+#pragma unroll
+    for (int d = 0; d < NT; ++d)
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const f32x4 v = *(const f32x4*)(red + wq * PERW + (d * 4 + e4) * 256 + lane * 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[d][4 * e4 + k] += v[k];
+        __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight (else they all hoist: spills)
+      }
+    accb += red[wq * PERW + NT * 16 * 64 + lane];
+  }
+  __syncthreads();
+  DV_STAMP_AT(3);
+  if (gridDim.z > 1 && a.part_bf16) {
+    // ---- bf16 split partials: the four half-0 waves round their 32 x 32 x 9
+    // tiles to bf16 and transpose them into the torch layout in LDS together
+    // (one round), and all 8 waves write the block's 64 x 576 partial as 16-B
+    // stores ----
+    constexpr int TP = 32 * NT;  // bf16 per output channel of a wave tile
+    bf16* tiles = (bf16*)smem;
+    const int r = lane & 31, h = lane >> 5;
+    if (half == 0) {
+      bf16* tb = tiles + wq * 32 * TP;
+#pragma unroll
+      for (int d = 0; d < NT; ++d)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) tb[((e & 3) + 8 * (e >> 2) + 4 * h) * TP + r * NT + d] = (bf16)acc[d][e];
+    }
+    __syncthreads();
+    bf16* dstb = (bf16*)a.part + (long long)bz * a.cout * a.K;
+    constexpr int CPR = TP / 8;  // 16-B chunks per output-channel row of a tile
+    for (int idx = threadIdx.x; idx < 4 * 32 * CPR; idx += 512) {
+      const int t4 = idx / (32 * CPR), rem = idx - t4 * (32 * CPR);
+      const int col = rem / CPR, j = rem - col * CPR;
+      const u32x4 v = *(const u32x4*)(tiles + (t4 * 32 + col) * TP + 8 * j);
+      const long long oi = (long long)(co0 + (t4 >> 1) * 32 + col) * a.K + (ci0 + (t4 & 1) * 32) * NT + 8 * j;
+      *(u32x4*)(dstb + oi) = v;
+    }
+#ifdef DV_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    DV_STAMP_AT(4);
+    if (do_bias && half == 0 && lane < 32) a.dbpart[(long long)bz * a.cout + co0 + wm * 32 + lane] = accb;
+    return;
+  }
+
+  // ---- torch-layout output [co][ci][tap]: each wave's 32 x 32 x 9 tile is
+  // transposed through LDS (two tiles per round, 36 KB each) so every output
+  // channel's 32 ci x 9 taps go out as 1152 contiguous bytes (float4 stores).
+  // One split writes the gradient itself (accumulate honoured); several
+  // splits write partials that wgrad_reduce4_kernel sums. ----
+  const bool direct = gridDim.z == 1;
+  const bool pbf = !direct && a.part_bf16;  // bf16 partials: half the split-K bytes
+  float* dst = direct ? a.dw : a.part + (pbf ? 0 : (long long)bz * a.cout * a.K);
+  bf16* dstb = (bf16*)a.part + (long long)bz * a.cout * a.K;
+  const int acc_o = direct && a.acc_w;
+  const int r = lane & 31, h = lane >> 5;
+  constexpr int TP = 32 * NT;  // floats per output channel in a tile
+#pragma unroll
+  for (int rnd = 0; rnd < 2; ++rnd) {
+    float* tile = red + wn * (32 * TP);
+    if (half == 0 && wm == rnd) {
+#pragma unroll
+      for (int d = 0; d < NT; ++d)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int col = (e & 3) + 8 * (e >> 2) + 4 * h;  // local co
+          tile[col * TP + r * NT + d] = acc[d][e];
+        }
+    }
+    __syncthreads();
+    // all 8 waves store the round's two tiles (the store phase is
+    // issue-bound: two storing waves left it at ~40 % of a small wgrad's time)
+    for (int idx = threadIdx.x; idx < 2 * 32 * (TP / 4); idx += 512) {
+      const int t2 = idx / (32 * (TP / 4)), rem = idx - t2 * (32 * (TP / 4));
+      const int col = rem / (TP / 4), j = rem - col * (TP / 4);
+      f32x4 v = *(const f32x4*)(red + t2 * (32 * TP) + col * TP + 4 * j);
+      const long long rowbase = (long long)(co0 + rnd * 32) * a.K + (ci0 + t2 * 32) * NT;
+      const long long oi = rowbase + (long long)col * a.K + 4 * j;
+      if (pbf) {
+        const float t4[4] = {v[0], v[1], v[2], v[3]};
+        store4<bf16>(dstb + oi, t4);
+        continue;
+      }
+      f32x4* o = (f32x4*)(dst + oi);
+      if (acc_o) v += *o;
+      *o = v;
+    }
+    __syncthreads();
+  }
+#ifdef DV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial stores written
+#endif
+  DV_STAMP_AT(4);
+  if (do_bias && half == 0 && lane < 32) {
+    const int co = co0 + wm * 32 + lane;
+    if (direct) a.db[co] = a.acc_b ? a.db[co] + accb : accb;
+    else a.dbpart[(long long)bz * a.cout + co] = accb;
+  }
+}
 
 // LDS images are split by 32-channel half into 64-B rows: four consecutive
 // rows then start 16 banks apart, so the transposed operand reads are
@@ -3113,6 +3270,37 @@ __global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv
       asm volatile("" : "+v"(wl[s]), "+v"(wh[s]));
     }
     const int a0 = ((half * 64 + 8 * (g >> 1) + q) * 64 + colb);
+    if constexpr (KS == 1) {
+      // 1x1: a stage is 4 k-steps of one tap; A and B of k-step s sit at
+      // + 1024 s (+ 256 for the high half) from k-step 0's: asm reads in the
+      // order (A0, B0, A1, B1, ...) with counted waits (hipcc would drain the
+      // in-flight stage DMAs before a visible tr read)
+      const unsigned ab = lds_u32(sA) + a0, bb = sBu + wlo[0];
+      u32x2 r[4][4];
+      static_for<0, 4>([&](auto S) {
+        constexpr int st4 = decltype(S)::value;
+        r[st4][0] = tr_read_asm<1024 * st4>(ab);
+        r[st4][1] = tr_read_asm<1024 * st4 + 256>(ab);
+        r[st4][2] = tr_read_asm<1024 * st4>(bb);
+        r[st4][3] = tr_read_asm<1024 * st4 + 256>(bb);
+      });
+      static_for<0, 4>([&](auto S) {
+        constexpr int st4 = decltype(S)::value;
+        asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(r[st4][0]), "+v"(r[st4][1]), "+v"(r[st4][2]), "+v"(r[st4][3])
+                     : "n"(4 * (3 - st4)));
+        const u32x4 fa1 = u32x4{r[st4][0][0], r[st4][0][1], r[st4][1][0], r[st4][1][1]};
+        const u32x4 fb1 = u32x4{r[st4][2][0], r[st4][2][1], r[st4][3][0], r[st4][3][1]};
+        acc[0] = Mma<bf16>::run(fa1, fb1, acc[0]);
+        if (do_bias) {
+          float t[8];
+          Vec<bf16>::to_f(fa1, t);
+          accb += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+        }
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      continue;
+    }
     // the 4 A fragments (dY) of the stage up front; B (window) fragments of
     // tap j + WPF are read while tap j multiplies (flattened k-step x tap)
     u32x4 fa[4];
@@ -3152,120 +3340,298 @@ __global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv
   }
   DV_STAMP_AT(2);
   accb += __shfl_xor(accb, 32, 64);  // both k-halves of the channel
+  wgrad_tile_store<NT>(a, acc, accb, smem, half, wq, wm, wn, lane, co0, ci0, do_bias, (int)blockIdx.z);
+}
 
-  // ---- sum the two pixel halves through LDS in one pass (16-B rows per lane) ----
-  float* red = (float*)smem;
-  constexpr int PERW = (NT * 16 + 1) * 64;  // floats per wave
-  if (half == 1) {
-#pragma unroll
-    for (int d = 0; d < NT; ++d)
-#pragma unroll
-      for (int e4 = 0; e4 < 4; ++e4)
-        *(f32x4*)(red + wq * PERW + (d * 4 + e4) * 256 + lane * 4) =
-            f32x4{acc[d][4 * e4], acc[d][4 * e4 + 1], acc[d][4 * e4 + 2], acc[d][4 * e4 + 3]};
-    red[wq * PERW + NT * 16 * 64 + lane] = accb;
+// ---------------------------------------------------------------------------
+// bf16 3x3 wgrad, window form (round 5; cin, cout % 64 == 0):
+//   dW[co][dy][dx][ci] = sum_p dY[p][co] X[p + (dy - 1, dx - 1)][ci]
+// Same workgroup shape as the stripe kernel (a 64 co x 64 ci x 9 tap tile over
+// a contiguous range of 128-pixel stages, 8 waves, waves 4-7 on the second
+// 64-pixel half, the halves summed through LDS by wgrad_tile_store), but the
+// four 16-pixel k-steps of a half are VERTICAL TRANSLATES of one another:
+// k-step s covers image row r0 + s (W >= 16: 16 columns; W = 8: rows s and
+// s + 4 of one 8 x 8 frame).  The window fragment of tap (dy, dx) at k-step s
+// is then the fragment of row shift t = s + dy, so each wave reads only
+// (4 + 2) x 3 = 18 window fragments per stage for its 36 MFMAs (the stripe
+// kernel read 36): half the ds_read_b64_tr_b16 traffic, which had the LDS
+// return FIFO full (profiles/r04w_conv_families_pmc.txt).  A stage is a
+// 4-row x 32-column block (W >= 32), an 8 x 16 block (W = 16) or two 8 x 8
+// frames (W = 8); its window is (rows + 2) x (columns + 2) pixels: 204 / 180
+// / 200 (the W = 64 stripe window was 264), so every width runs a 3-deep
+// ring.  Operand addresses: one VGPR per wave, every (t, dx) an immediate.
+// ---------------------------------------------------------------------------
+template <int W> struct WinGeom {
+  static constexpr int NFR = W == 8 ? 2 : 1;                      // frames per stage
+  static constexpr int SC = W >= 32 ? 32 : W;                     // stage columns
+  static constexpr int SR = W == 8 ? 8 : 128 / SC;                // stage rows (per frame)
+  static constexpr int WQ = SC + 2;                               // window pixels per row
+  static constexpr int FPIX = (SR + 2) * WQ;                      // window pixels per frame
+  static constexpr int WR = NFR * FPIX;                           // 200 / 180 / 204
+  static constexpr int NRH = (WR + 127) / 128;                    // 128-row DMA rounds per ci half
+  static constexpr int AIMG = 2 * 128 * 64;                       // dY image: 2 co halves x 128 rows x 64 B
+  static constexpr int BHALF = NRH * 128 * 64;                    // window image of one ci half
+  static constexpr int STG = AIMG + 2 * BHALF;
+  static constexpr int NBUF = 3;
+  static_assert(NBUF * STG <= 160 * 1024, "ring exceeds LDS");
+};
+
+bool wgrad_win_geom_ok(int h, int w) {
+  if (w == 8) return h == 8;
+  if (w == 16) return h % 8 == 0;
+  return (w == 32 || w == 64) && h % 4 == 0;
+}
+
+// ISS: where the stage DMAs are issued (A/B, round 5).  0: waves 4-7 issue
+// stage st + 2 before the stage's barrier (two barriers per stage); 1: one
+// barrier per stage, waves 4-7 issue two pieces per row shift among the
+// MFMAs; 2: one barrier, every wave issues its own six pieces among the
+// MFMAs; 3: one barrier, every wave issues its six right after it
+template <int W, int ISS = 0>
+__global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
+  using G = WinGeom<W>;
+  constexpr int WQ = G::WQ, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF, AIMG = G::AIMG, BHALF = G::BHALF;
+  constexpr int NT = 9;
+  constexpr bool OWN = ISS >= 2;          // every wave issues its own pieces
+  constexpr int NV = OWN ? 1 : 2;         // virtual waves an issuing wave serves
+  constexpr int DPS = NV * (2 + 2 * NRH);  // DMAs per issuing thread per stage
+  constexpr int RED1 = 4 * (NT * 16 + 1) * 64 * 4;
+  constexpr int RING = NBUF * STG;
+  __shared__ __attribute__((aligned(1024))) char smem[RING > RED1 ? RING : RED1];
+
+  DV_STAMP_AT(0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wave >> 2, wq = wave & 3, wm = wq >> 1, wn = wq & 1;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (a.xcd) {
+    // round-robin dispatch puts blocks L and L + 8 on one XCD: give XCD
+    // (L % 8) the contiguous chunk of tiles in (split, co, ci) order, so its
+    // L2 holds few dY / X tiles (host-checked: block count % 8 == 0)
+    const int nxy = gridDim.x * gridDim.y;
+    const int L = bx + gridDim.x * (by + gridDim.y * bz);
+    const int T = (L & 7) * ((nxy * gridDim.z) >> 3) + (L >> 3);
+    bz = T / nxy;
+    const int r = T - bz * nxy;
+    bx = r / gridDim.y;
+    by = r - bx * gridDim.y;
   }
-  __syncthreads();
-  if (half == 0) {
+  const int co0 = bx * 64, ci0 = by * 64;
+  const int sbeg = bz * a.stages_per_split;
+  const int send = min(sbeg + a.stages_per_split, a.nstages);
+  const int nst = send - sbeg;
+  const int H = a.H, HW = H * W;
+  constexpr int CB = W >= 32 ? W / 32 : 1;  // column blocks per row block
+  const int spf = W == 8 ? 1 : (H / G::SR) * CB;  // stages per frame
+  // first pixel (frame-linear) and image row / column of stage st
+  auto stage_base = [&](int st, int& y0, int& x0) -> int {
+    if constexpr (W == 8) {
+      y0 = 0;
+      x0 = 0;
+      return st * 128;
+    } else {
+      const int f = st / spf, r = st - f * spf;
+      const int rb = r / CB, cb = r - rb * CB;
+      y0 = rb * G::SR;
+      x0 = cb * G::SC;
+      return f * HW + y0 * W + x0;
+    }
+  };
+  // stage-local pixel j = 64 half + 16 s + k -> offset from the stage's first pixel
+  auto rel = [&](int j) -> int {
+    const int h = j >> 6, s = (j >> 4) & 3, k = j & 15;
+    if constexpr (W >= 32) return s * W + 16 * h + k;
+    else if constexpr (W == 16) return j;
+    else return h * 64 + (s + 4 * (k >> 3)) * 8 + (k & 7);
+  };
+
+  // ---- static per-lane DMA slots: row 16 * vw + (lane >> 2) of each 128-row
+  // round, 16-B chunk (lane & 3) of a 64-B half row; waves 4-7 issue for the
+  // virtual waves (w & 3) and w ----
+  const int l4 = lane >> 2, c4 = lane & 3;
+  // dY through a raw buffer resource as well (a global_load_lds DMA made hipcc
+  // drain vmcnt before every LDS read: the ring then ran one stage deep)
+  const __amdgpu_buffer_rsrc_t yrs = dma_rsrc(a.dy, (unsigned)((long long)a.nstages * 128 * a.lddy * 2));
+  const int a_c = co0 + 8 * c4;
+  const bool first = ci0 < a.c0;
+  const int xld = first ? a.ld0 : a.ld1;
+  const int b_c = (first ? ci0 : ci0 - a.c0) + 8 * c4;
+  const __amdgpu_buffer_rsrc_t xrs =
+      dma_rsrc(first ? a.x0 : a.x1, (unsigned)((long long)a.nstages * 128 * xld * 2));
+  int a_rel[NV], b_off[NV][NRH], b_ry[NV][NRH], b_rx[NV][NRH];
 #pragma unroll
-    for (int d = 0; d < NT; ++d)
+  for (int k = 0; k < NV; ++k) {
+    const int vw = OWN ? wave : (wave & 3) | (4 * k);
+    a_rel[k] = rel(16 * vw + l4);
 #pragma unroll
-      for (int e4 = 0; e4 < 4; ++e4) {
-        const f32x4 v = *(const f32x4*)(red + wq * PERW + (d * 4 + e4) * 256 + lane * 4);
+    for (int i = 0; i < NRH; ++i) {
+      const int wpx = 128 * i + 16 * vw + l4;
+      const int fr = wpx / G::FPIX, rem = wpx - fr * G::FPIX;
+      const int wy = rem / WQ, wx = rem - wy * WQ;
+      const bool ok = wpx < G::WR;
+      b_ry[k][i] = ok ? wy - 1 : -(1 << 20);
+      b_rx[k][i] = wx - 1;
+      b_off[k][i] = fr * HW + (wy - 1) * W + (wx - 1);
+    }
+  }
+  // piece p of virtual wave slot k: p = 0 the dY rows (2 DMAs), p = 1 + i
+  // window round i (2 DMAs)
+  auto issue_piece = [&](int base, int y0, int x0, int buf, int k, int p) {
+    const int vw = OWN ? wave : (wave & 3) | (4 * k);
+    char* sA = smem + buf * STG;
+    char* sB = sA + AIMG;
+    if (p == 0) {
+      const unsigned yoff = (unsigned)(((base + a_rel[k]) * a.lddy + a_c) * 2);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc[d][4 * e4 + k] += v[k];
-        __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight (else they all hoist: spills)
+      for (int hh = 0; hh < 2; ++hh) dma16(yrs, sA + hh * (AIMG / 2) + 16 * vw * 64, yoff + 64 * hh);
+    } else {
+      const int i = p - 1;
+      // halo / pad rows load out of the raw buffer's range: zeros, no access
+      const bool in = (unsigned)(y0 + b_ry[k][i]) < (unsigned)H && (unsigned)(x0 + b_rx[k][i]) < (unsigned)W;
+      const unsigned voff = in ? (unsigned)(((base + b_off[k][i]) * xld + b_c) * 2) : DMA_OOB;
+      const int drow = 128 * i + 16 * vw;  // wave-uniform
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) dma16(xrs, sB + hh * BHALF + drow * 64, in ? voff + 64 * hh : DMA_OOB);
+    }
+  };
+  constexpr int NP = 1 + NRH;  // pieces per virtual wave
+  auto issue = [&](int st, int buf) {
+    if (OWN || half) {  // wave-uniform
+      int y0, x0;
+      const int base = stage_base(sbeg + st, y0, x0);
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) issue_piece(base, y0, x0, buf, k, p);
+    }
+  };
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int d = 0; d < NT; ++d)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[d][e] = 0.f;
+  float accb = 0.f;
+  const bool do_bias = a.db != nullptr && by == 0 && wn == 0;  // wave-uniform
+
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int colb = 32 * (g & 1) + 8 * pp;  // byte column of this lane in a 64-B half row
+  const int k0 = 8 * (g >> 1) + q;         // this lane's first k (pixel) of a k-step
+  // window pixel of (t, dx) = (0, 0) for this lane's k-step-0 pixel
+  const int bpix = W >= 32 ? 16 * half + k0
+                 : W == 16 ? 4 * half * WQ + k0
+                           : half * G::FPIX + 4 * (g >> 1) * WQ + q;
+  const int blane = bpix * 64 + colb;
+  const int a0 = (half * 64 + 8 * (g >> 1) + q) * 64 + colb;
+
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < nst) issue(i, i);
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st % NBUF;
+    // ISS > 0: stage st + 2 goes into the buffer of stage st - 1, which every
+    // wave finished reading before this barrier
+    const bool pre = ISS > 0 && st + NBUF - 1 < nst;
+    int nbase = 0, ny0 = 0, nx0 = 0;
+    if constexpr (ISS == 0) {
+      if (st + NBUF - 1 < nst) {
+        issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS * (NBUF - 1)) : "memory");
+      } else if (st + 1 < nst) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-    accb += red[wq * PERW + NT * 16 * 64 + lane];
-  }
-  __syncthreads();
-  DV_STAMP_AT(3);
-  if (gridDim.z > 1 && a.part_bf16) {
-    // ---- bf16 split partials: the four half-0 waves round their 32 x 32 x 9
-    // tiles to bf16 and transpose them into the torch layout in LDS together
-    // (one round), and all 8 waves write the block's 64 x 576 partial as 16-B
-    // stores ----
-    constexpr int TP = 32 * NT;  // bf16 per output channel of a wave tile
-    bf16* tiles = (bf16*)smem;
-    const int r = lane & 31, h = lane >> 5;
-    if (half == 0) {
-      bf16* tb = tiles + wq * 32 * TP;
-#pragma unroll
-      for (int d = 0; d < NT; ++d)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) tb[((e & 3) + 8 * (e >> 2) + 4 * h) * TP + r * NT + d] = (bf16)acc[d][e];
+    } else {
+      if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (pre) nbase = stage_base(sbeg + st + NBUF - 1, ny0, nx0);
     }
-    __syncthreads();
-    bf16* dstb = (bf16*)a.part + (long long)blockIdx.z * a.cout * a.K;
-    constexpr int CPR = TP / 8;  // 16-B chunks per output-channel row of a tile
-    for (int idx = threadIdx.x; idx < 4 * 32 * CPR; idx += 512) {
-      const int t4 = idx / (32 * CPR), rem = idx - t4 * (32 * CPR);
-      const int col = rem / CPR, j = rem - col * CPR;
-      const u32x4 v = *(const u32x4*)(tiles + (t4 * 32 + col) * TP + 8 * j);
-      const long long oi = (long long)(co0 + (t4 >> 1) * 32 + col) * a.K + (ci0 + (t4 & 1) * 32) * NT + 8 * j;
-      *(u32x4*)(dstb + oi) = v;
+    __builtin_amdgcn_s_barrier();
+    const int nbuf = (st + NBUF - 1) % NBUF;
+    if constexpr (ISS == 3) {
+      if (pre) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) issue_piece(nbase, ny0, nx0, nbuf, 0, p);
+      }
     }
-#ifdef DV_STAMP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    DV_STAMP_AT(4);
-    if (do_bias && half == 0 && lane < 32) a.dbpart[(long long)blockIdx.z * a.cout + co0 + wm * 32 + lane] = accb;
-    return;
-  }
-
-  // ---- torch-layout output [co][ci][tap]: each wave's 32 x 32 x 9 tile is
-  // transposed through LDS (two tiles per round, 36 KB each) so every output
-  // channel's 32 ci x 9 taps go out as 1152 contiguous bytes (float4 stores).
-  // One split writes the gradient itself (accumulate honoured); several
-  // splits write partials that wgrad_reduce4_kernel sums. ----
-  const bool direct = gridDim.z == 1;
-  const bool pbf = !direct && a.part_bf16;  // bf16 partials: half the split-K bytes
-  float* dst = direct ? a.dw : a.part + (pbf ? 0 : (long long)blockIdx.z * a.cout * a.K);
-  bf16* dstb = (bf16*)a.part + (long long)blockIdx.z * a.cout * a.K;
-  const int acc_o = direct && a.acc_w;
-  const int r = lane & 31, h = lane >> 5;
-  constexpr int TP = 32 * NT;  // floats per output channel in a tile
+    if (st == 0) DV_STAMP_AT(1);
+    const char* sA = smem + buf * STG + wm * (AIMG / 2);
+    // one operand base per stage, made opaque so that each (t, dx) offset
+    // stays the ds_read immediate (otherwise hoisted as loop invariants)
+    unsigned bb = lds_u32(smem + buf * STG + AIMG + wn * BHALF) + blane;
+    asm volatile("" : "+v"(bb));
+    // The operand reads are inline asm with hand-counted lgkmcnt waits: hipcc
+    // drains vmcnt(0) before a ds_read_b64_tr_b16 it can see while any LDS-DMA
+    // is in flight (it cannot tell the ring buffers apart), which collapsed
+    // the three-stage ring to one stage and parked the waves ~half of the time
+    // (SQ_WAIT_ANY 0.46-0.50, r05b).  Nothing else in the stage loop touches
+    // LDS or the scalar cache, so the counts below are exact: fa (8 reads),
+    // then 6 per row shift.
+    const unsigned ab = lds_u32(sA) + a0;
+    u32x2 fa2[4][2], fb2[3][3][2];
 #pragma unroll
-  for (int rnd = 0; rnd < 2; ++rnd) {
-    float* tile = red + wn * (32 * TP);
-    if (half == 0 && wm == rnd) {
+    for (int s = 0; s < 4; ++s) {
+      fa2[s][0] = tr_read_asm<0>(ab + s * 1024);
+      fa2[s][1] = tr_read_asm<256>(ab + s * 1024);
+    }
+    auto rdT = [&](auto T) {
+      constexpr int t = decltype(T)::value;
+      static_for<0, 3>([&](auto DX) {
+        constexpr int dx = decltype(DX)::value, off = (t * WQ + dx) * 64;
+        fb2[t % 3][dx][0] = tr_read_asm<off>(bb);
+        fb2[t % 3][dx][1] = tr_read_asm<off + 256>(bb);
+      });
+    };
+    rdT(std::integral_constant<int, 0>{});
+    rdT(std::integral_constant<int, 1>{});
+    u32x4 fa[4];
+    static_for<0, 6>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      if constexpr (t + 2 < 6) rdT(std::integral_constant<int, t + 2>{});
+      // reads issued after row shift t's: those of t + 1 and t + 2
+      constexpr int younger = 6 * ((t + 2 < 6 ? 2 : (t + 1 < 6 ? 1 : 0)));
+      u32x2(&f)[3][2] = fb2[t % 3];
+      asm volatile("s_waitcnt lgkmcnt(%6)"
+                   : "+v"(f[0][0]), "+v"(f[0][1]), "+v"(f[1][0]), "+v"(f[1][1]), "+v"(f[2][0]), "+v"(f[2][1])
+                   : "n"(younger));
+      if constexpr (t == 0) {
+        asm volatile("" : "+v"(fa2[0][0]), "+v"(fa2[0][1]), "+v"(fa2[1][0]), "+v"(fa2[1][1]));
+        asm volatile("" : "+v"(fa2[2][0]), "+v"(fa2[2][1]), "+v"(fa2[3][0]), "+v"(fa2[3][1]));
 #pragma unroll
-      for (int d = 0; d < NT; ++d)
+        for (int s = 0; s < 4; ++s) fa[s] = u32x4{fa2[s][0][0], fa2[s][0][1], fa2[s][1][0], fa2[s][1][1]};
+      }
+      u32x4 fb[3];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int col = (e & 3) + 8 * (e >> 2) + 4 * h;  // local co
-          tile[col * TP + r * NT + d] = acc[d][e];
+      for (int dx = 0; dx < 3; ++dx) fb[dx] = u32x4{f[dx][0][0], f[dx][0][1], f[dx][1][0], f[dx][1][1]};
+      constexpr int slo = t > 2 ? t - 2 : 0, shi = t < 3 ? t : 3;
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int s = slo; s <= shi; ++s) acc[(t - s) * 3 + dx] = Mma<bf16>::run(fa[s], fb[dx], acc[(t - s) * 3 + dx]);
+      // the next stage's pieces among the MFMAs (ISS 1: waves 4-7, six per
+      // virtual wave over t = 0..5; ISS 2: every wave, its own over t = 0..NP-1)
+      if constexpr (ISS == 1) {
+        constexpr int k = t / 3, p = t % 3;
+        if (pre && half && p < NP) issue_piece(nbase, ny0, nx0, nbuf, k, p);
+      } else if constexpr (ISS == 2) {
+        if (pre && t < NP) issue_piece(nbase, ny0, nx0, nbuf, 0, t);
+      }
+      if constexpr (t < 4) {
+        if (do_bias) {
+          float f8[8];
+          Vec<bf16>::to_f(fa[t], f8);
+          accb += ((f8[0] + f8[1]) + (f8[2] + f8[3])) + ((f8[4] + f8[5]) + (f8[6] + f8[7]));
         }
-    }
-    __syncthreads();
-    // all 8 waves store the round's two tiles (the store phase is
-    // issue-bound: two storing waves left it at ~40 % of a small wgrad's time)
-    for (int idx = threadIdx.x; idx < 2 * 32 * (TP / 4); idx += 512) {
-      const int t2 = idx / (32 * (TP / 4)), rem = idx - t2 * (32 * (TP / 4));
-      const int col = rem / (TP / 4), j = rem - col * (TP / 4);
-      f32x4 v = *(const f32x4*)(red + t2 * (32 * TP) + col * TP + 4 * j);
-      const long long rowbase = (long long)(co0 + rnd * 32) * a.K + (ci0 + t2 * 32) * NT;
-      const long long oi = rowbase + (long long)col * a.K + 4 * j;
-      if (pbf) {
-        const float t4[4] = {v[0], v[1], v[2], v[3]};
-        store4<bf16>(dstb + oi, t4);
-        continue;
       }
-      f32x4* o = (f32x4*)(dst + oi);
-      if (acc_o) v += *o;
-      *o = v;
-    }
-    __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (ISS == 0) __builtin_amdgcn_s_barrier();
   }
-#ifdef DV_STAMP
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial stores written
-#endif
-  DV_STAMP_AT(4);
-  if (do_bias && half == 0 && lane < 32) {
-    const int co = co0 + wm * 32 + lane;
-    if (direct) a.db[co] = a.acc_b ? a.db[co] + accb : accb;
-    else a.dbpart[(long long)blockIdx.z * a.cout + co] = accb;
-  }
+  DV_STAMP_AT(2);
+  accb += __shfl_xor(accb, 32, 64);  // both k-halves of the channel
+  wgrad_tile_store<NT>(a, acc, accb, smem, half, wq, wm, wn, lane, co0, ci0, do_bias, bz);
 }
 
 // dw (+)= sum_s part[s] over float4s (partials already in torch layout).
@@ -3456,8 +3822,8 @@ bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout
   if ((ks != 3 && ks != 1) || cin % 64 || cout % 64 || (split && c0 % 64)) return false;
   const long long M = (long long)nf * h * w;
   if (M % 128 || M >= (1ll << 31)) return false;
-  if (M * maxld * 2 >= (long long)DMA_OOB) return false;  // the window's raw-buffer resource
-  return ks == 1 || stripe_geom(h, w, seg, nseg);
+  if (M * std::max<long long>(maxld, cout) * 2 >= (long long)DMA_OOB) return false;  // raw-buffer resources
+  return ks == 1 || wgrad_win_geom_ok(h, w) || stripe_geom(h, w, seg, nseg);
 }
 
 // split count: ~256 workgroups (one per CU: the stage ring takes up to 112 KB of LDS)
@@ -3509,11 +3875,25 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   a.dbpart = db ? ws + (long long)S * cout * a.K / (a.part_bf16 ? 2 : 1) : nullptr;
   a.dw = dw; a.db = db; a.acc_w = acc_w; a.acc_b = acc_b;
   dim3 grid(cout / 64, cin / 64, S);
+  static const int xcdk = getenv("DV_WG_XCD") ? atoi(getenv("DV_WG_XCD")) : 0;  // temporary A/B
+  a.xcd = xcdk && ((long long)grid.x * grid.y * grid.z) % 8 == 0;
   // the 3x3 stage DMAs issued by waves 4-7 only: family 1,897 -> 1,874 us per
   // step, step equal (profiles/r04p_wgrad_stag_ab.txt); DV_WG_STAG=0: every wave
   static const bool stag = !(getenv("DV_WG_STAG") && atoi(getenv("DV_WG_STAG")) == 0);
+  static const bool old3 = getenv("DV_WG_OLD") && atoi(getenv("DV_WG_OLD")) != 0;  // temporary A/B
   if (ks == 1) {
     conv_wgrad_stripe_kernel<64, 1><<<grid, 512, 0, st>>>(a);
+  } else if (!old3 && wgrad_win_geom_ok(h, w)) {
+    static const int iss = getenv("DV_WG_ISS") ? atoi(getenv("DV_WG_ISS")) : 0;  // temporary A/B
+#define DV_WW(I)                                                          \
+  switch (w) {                                                            \
+    case 64: conv_wgrad_win_kernel<64, I><<<grid, 512, 0, st>>>(a); break; \
+    case 32: conv_wgrad_win_kernel<32, I><<<grid, 512, 0, st>>>(a); break; \
+    case 16: conv_wgrad_win_kernel<16, I><<<grid, 512, 0, st>>>(a); break; \
+    default: conv_wgrad_win_kernel<8, I><<<grid, 512, 0, st>>>(a); break;  \
+  }
+    if (iss == 1) DV_WW(1) else if (iss == 2) DV_WW(2) else if (iss == 3) DV_WW(3) else DV_WW(0)
+#undef DV_WW
   } else if (stag) {
     // DV_WG_TRIM=1: the W = 64 window image trimmed to a 3-deep ring.  Measured
     // no faster (36.3-36.5 -> 36.9-37.0 us per launch, profiles/r04t_wgrad_trim_ab.txt):

@@ -94,6 +94,7 @@ _SIGS = {
     "dv_comm_allreduce": [_P, _P, _L, _I, _I, _P],
     "dv_comm_async_error": [_P],
     "dv_comm_destroy": [_P],
+    "dv_comm_abort": [_P],
 }
 
 

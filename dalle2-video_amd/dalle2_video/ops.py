@@ -1784,13 +1784,24 @@ def cross_attention(x, context, g1, null_kv, wq, wkv, wo, g2, nb, eps, kv=None, 
 MQA_DH = 32
 
 
+# the bf16 backward kernels hold a whole clip's K / V in LDS (dv_mqa_bwd)
+MQA_BF16_BWD_MAX_NKP = 1280
+
+
 class MQAFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, kv, null_kv, B, N, H, scale):
         require_gpu(q, kv, null_kv)
         dev = q.device
-        qc, kvc = q.contiguous(), kv.contiguous()
         NKP = (N + 1 + 31) // 32 * 32
+        # a bf16 sequence too long for the bf16 backward (config 5: 8,193 keys)
+        # that needs gradients runs forward AND backward on the f32 kernels (one
+        # lse layout for both); outputs and input gradients stay bf16
+        ctx.cast = (q.dtype == torch.bfloat16 and NKP > MQA_BF16_BWD_MAX_NKP
+                    and any(ctx.needs_input_grad[:3]))
+        if ctx.cast:
+            q, kv = q.float(), kv.float()
+        qc, kvc = q.contiguous(), kv.contiguous()
         kp = torch.empty(B, NKP, MQA_DH, dtype=q.dtype, device=dev)
         vp = torch.empty_like(kp)
         nkv = null_kv.detach().float().contiguous()
@@ -1807,14 +1818,14 @@ class MQAFn(torch.autograd.Function):
         ctx.save_for_backward(qc, kp, vp, o, lse)
         ctx.params = (null_kv,)
         ctx.meta = (B, N, H, NKP, scale, kvc.shape[-1])
-        return o
+        return o.to(torch.bfloat16) if ctx.cast else o
 
     @staticmethod
     def backward(ctx, do):
         qc, kp, vp, o, lse = ctx.saved_tensors
         B, N, H, NKP, scale, ldkv = ctx.meta
         dev = qc.device
-        do = do.contiguous()
+        do = do.to(qc.dtype).contiguous()
         dq = torch.empty_like(qc)
         D = torch.empty(B, H, N, dtype=torch.float32, device=dev)
         need = ctypes.c_longlong(0)
@@ -1829,6 +1840,8 @@ class MQAFn(torch.autograd.Function):
                              do.shape[-1], ptr(lse), ptr(kp), ptr(vp), ptr(dq), dq.shape[-1], ptr(D),
                              ptr(ws), need.value, ptr(dkv), dkv.shape[-1], ptr(dnull), B, N, NKP, H,
                              ctypes_float(scale), int(sn[1]) if sn else 0, stream()))
+        if ctx.cast:
+            dq, dkv = dq.to(torch.bfloat16), dkv.to(torch.bfloat16)
         return dq, dkv, (None if sn else dnull), None, None, None, None
 
 

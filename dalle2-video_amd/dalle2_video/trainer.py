@@ -18,8 +18,12 @@ on the MI355X path.
 """
 from __future__ import annotations
 
+import atexit
 import math
 import os
+import sys
+import threading
+import time
 from contextlib import contextmanager, nullcontext
 from pathlib import Path
 
@@ -28,7 +32,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import _lib, ops
-from ._lib import call, ptr, stream
+from ._lib import DVError, call, ptr, stream
 from .dalle2_video import VideoDecoder, cast_tuple, default, exists
 from .ops import ctypes_float
 
@@ -401,9 +405,17 @@ class _BatchStridedLoader:
     def __init__(self, loader, world, rank, seed=0):
         from torch.utils.data import DataLoader, RandomSampler
 
-        inner = getattr(loader.batch_sampler, "sampler", None)
+        import copy
+
+        # seed COPIES of the batch sampler and its RandomSampler: the caller's
+        # DataLoader keeps drawing from the global RNG as before
+        bs = loader.batch_sampler
+        inner = getattr(bs, "sampler", None)
         if isinstance(inner, RandomSampler) and inner.generator is None:
+            inner = copy.copy(inner)
             inner.generator = torch.Generator().manual_seed(seed)
+            bs = copy.copy(bs)
+            bs.sampler = inner
 
         class _Strided:
             def __init__(self, bs):
@@ -419,7 +431,7 @@ class _BatchStridedLoader:
                 return n // world + (1 if rank < n % world else 0)
 
         self.original = loader
-        kw = dict(batch_sampler=_Strided(loader.batch_sampler), num_workers=loader.num_workers,
+        kw = dict(batch_sampler=_Strided(bs), num_workers=loader.num_workers,
                   collate_fn=loader.collate_fn, pin_memory=loader.pin_memory, timeout=loader.timeout,
                   worker_init_fn=loader.worker_init_fn, generator=loader.generator)
         if loader.num_workers > 0:
@@ -450,8 +462,108 @@ def broadcast_parameters(module, src=0):
 
 BUCKET_BYTES = int(os.environ.get("DV_BUCKET_MB", "25")) * (1 << 20)
 
-_NATIVE_COMMS = {}  # process group -> RCCL communicator of libdv_hip (one per process)
-_COMM_SERIAL = [0]
+class _NativeComms:
+    """libdv_hip's RCCL communicators of this process, one per (process group,
+    rank, world), with what ProcessGroupNCCL's watchdog gave the reference's
+    DDP: a daemon thread polls dv_comm_async_error every second and, while a
+    training call or update is in flight, enforces a deadline
+    (DV_COMM_TIMEOUT seconds, default 1800 like the c10d timeout); on an
+    error or a missed deadline it aborts the communicators and ends the
+    process with exit code 70, so a dead peer does not leave the other ranks
+    blocked in a stream wait forever.  Communicators are destroyed at exit
+    (or when their process group is no longer the default one)."""
+
+    def __init__(self):
+        self.comms = {}     # (id(group), rank, world) -> (group, handle)
+        self.serial = 0     # every rank makes its communicators in the same order
+        self.lock = threading.Lock()
+        self.busy_since = None
+        self.failed = False
+        self.thread = None
+        self.timeout = float(os.environ.get("DV_COMM_TIMEOUT", "1800"))
+        atexit.register(self.close)
+
+    def get(self, device):
+        import ctypes
+
+        group = dist.distributed_c10d._get_default_group()
+        rank, world = dist.get_rank(), dist.get_world_size()
+        key = (id(group), rank, world)
+        with self.lock:
+            ent = self.comms.get(key)
+            if ent is not None and ent[0] is group:
+                return ent[1]
+            # communicators of groups that are no longer the default one
+            stale = [k for k, (g, _) in self.comms.items() if g is not group]
+        for k in stale:
+            self._drop(k, destroy=True)
+        self.serial += 1
+        name = f"dv_comm/{self.serial}"
+        store = dist.distributed_c10d._get_default_store()
+        buf = ctypes.create_string_buffer(128)
+        if rank == 0:
+            call("dv_comm_unique_id", buf)
+            store.set(name, buf.raw)
+        else:
+            ctypes.memmove(buf, store.get(name), 128)
+        handle = ctypes.c_void_p()
+        call("dv_comm_init", buf, world, rank, device.index if device.index is not None
+             else torch.cuda.current_device(), ctypes.byref(handle))
+        with self.lock:
+            self.comms[key] = (group, handle)
+        if self.thread is None and os.environ.get("DV_COMM_WATCHDOG", "1") != "0":
+            self.thread = threading.Thread(target=self._watch, name="dv_comm_watchdog", daemon=True)
+            self.thread.start()
+        return handle
+
+    def _drop(self, key, destroy):
+        with self.lock:
+            ent = self.comms.pop(key, None)
+        if ent is not None:
+            getattr(_lib.lib(), "dv_comm_destroy" if destroy else "dv_comm_abort")(ent[1])
+
+    def check(self):
+        """Raise DVError if a communicator reports an asynchronous error
+        (update() calls this outside any capture)."""
+        with self.lock:
+            handles = [h for _, h in self.comms.values()]
+        for h in handles:
+            call("dv_comm_async_error", h)
+
+    def mark(self, busy):
+        self.busy_since = time.monotonic() if busy else None
+
+    def _watch(self):
+        L = _lib.lib()
+        while True:
+            time.sleep(1.0)
+            with self.lock:
+                handles = [h for _, h in self.comms.values()]
+            bad = next((h for h in handles if L.dv_comm_async_error(h) != 0), None)
+            since = self.busy_since
+            late = since is not None and time.monotonic() - since > self.timeout
+            if bad is None and not late:
+                continue
+            why = ("RCCL communicator error: " + L.dv_last_error().decode(errors="replace")) if bad is not None else \
+                f"no progress for {self.timeout:.0f} s in a training call with collectives (DV_COMM_TIMEOUT)"
+            sys.stderr.write(f"[dv_comm watchdog] {why}; aborting the communicators and exiting\n")
+            sys.stderr.flush()
+            self.failed = True
+            for h in handles:
+                L.dv_comm_abort(h)
+            os._exit(70)
+
+    def close(self):
+        with self.lock:
+            keys = list(self.comms)
+        for k in keys:
+            try:
+                self._drop(k, destroy=not self.failed)
+            except Exception:  # interpreter teardown: best effort
+                pass
+
+
+_NATIVE = _NativeComms()
 
 
 class GradComm:
@@ -461,52 +573,53 @@ class GradComm:
     calls before update() stay correct however often a part is reduced).
 
     * RCCL (`nccl` process group, CUDA tensors): a communicator owned by
-      libdv_hip (dv_comm_*), made once per process; the id travels through
-      the torch.distributed store.  The all-reduce is enqueued on the CURRENT
-      stream — eagerly, or inside a HIP-graph capture of the backward — with
-      no c10d work object: ProcessGroupNCCL's watchdog polls the events of
-      its works from another thread, and one recorded in a capturing stream
-      aborts the process (hipErrorCapturedEvent), so captured collectives
-      never go through it.
+      libdv_hip (dv_comm_*, _NativeComms), made once per process group; the
+      id travels through the torch.distributed store.  The all-reduce is
+      enqueued on the CURRENT stream — eagerly, or inside a HIP-graph capture
+      of the backward — with no c10d work object: ProcessGroupNCCL's watchdog
+      polls the events of its works from another thread, and one recorded in a
+      capturing stream aborts the process (hipErrorCapturedEvent), so captured
+      collectives never go through it.
     * anything else (gloo: the CPU tests, the shared-GPU rehearsals): c10d
-      SUM then a 1/world scale."""
+      SUM then a 1/world scale.
+    Which of the two is resolved from the first tensor reduced (parameters
+    may still be on the host when the trainer is built); an `nccl` group with
+    host tensors is an error, never a silent c10d fallback."""
 
     def __init__(self, world, device=None):
         self.world = world
-        self.native = None
-        if (device is not None and device.type == "cuda" and dist.is_initialized()
-                and dist.get_backend() == "nccl"):
-            self.native = self._native(device)
+        self._native = None
+        self._resolved = False
+        if device is not None and device.type == "cuda":
+            self.resolve(device)
 
-    @staticmethod
-    def _native(device):
-        import ctypes
+    def resolve(self, device):
+        if not self._resolved:
+            nccl = dist.is_initialized() and dist.get_backend() == "nccl"
+            if nccl and device.type != "cuda":
+                raise DVError("the nccl (RCCL) gradient all-reduce needs CUDA tensors; "
+                              "move the decoder to the GPU before training")
+            self._native = _NATIVE.get(device) if nccl else None
+            self._resolved = True
+        return self._native
 
-        key = id(dist.distributed_c10d._get_default_group())
-        if key in _NATIVE_COMMS:
-            return _NATIVE_COMMS[key]
-        rank, world = dist.get_rank(), dist.get_world_size()
-        _COMM_SERIAL[0] += 1  # every rank makes its communicators in the same order
-        name = f"dv_comm/{_COMM_SERIAL[0]}"
-        store = dist.distributed_c10d._get_default_store()
-        buf = ctypes.create_string_buffer(128)
-        if rank == 0:
-            call("dv_comm_unique_id", buf)
-            store.set(name, buf.raw)
-        else:
-            raw = store.get(name)
-            ctypes.memmove(buf, raw, 128)
-        handle = ctypes.c_void_p()
-        call("dv_comm_init", buf, world, rank, device.index if device.index is not None
-             else torch.cuda.current_device(), ctypes.byref(handle))
-        _NATIVE_COMMS[key] = handle
-        return handle
+    @property
+    def native(self):
+        return self._native
+
+    def capturable(self, device):
+        """True when the collective can go into a HIP-graph capture (RCCL)."""
+        return self.resolve(device) is not None
+
+    def check(self):
+        if self._native is not None:
+            _NATIVE.check()
 
     def allreduce_mean_(self, t):
         """Mean over ranks, in place, on the current stream.  Returns None
         (stream-ordered: RCCL) or a pending c10d work for finish()."""
-        if self.native is not None:
-            call("dv_comm_allreduce", self.native, ptr(t), t.numel(), _lib.dt(t), 1, stream())
+        if self.resolve(t.device) is not None:
+            call("dv_comm_allreduce", self._native, ptr(t), t.numel(), _lib.dt(t), 1, stream())
             return None
         return (dist.all_reduce(t, async_op=True), t)
 
@@ -525,7 +638,7 @@ def allreduce_flat_grad(flat_grad, world, bucket_bytes=None, force=False, comm=N
     if (world <= 1 and not force) or flat_grad is None:
         return flat_grad
     comm = comm or GradComm(world, flat_grad.device)
-    if comm.native is not None:
+    if comm.resolve(flat_grad.device) is not None:
         comm.allreduce_mean_(flat_grad)
         return flat_grad
     n = flat_grad.numel()
@@ -740,7 +853,8 @@ class VideoDecoderTrainer(nn.Module):
         self.overlap = None
         self.gcomm = None
         if self.world > 1 or self.force_allreduce:
-            self.gcomm = GradComm(self.world, next(decoder.parameters()).device)
+            # resolved from the first gradient reduced (the decoder may move later)
+            self.gcomm = GradComm(self.world)
         if (self.world > 1 or self.force_allreduce) and os.environ.get("DV_OVERLAP", "1") != "0":
             self.overlap = []
             for i, unet in enumerate(decoder.unets):
@@ -807,6 +921,8 @@ class VideoDecoderTrainer(nn.Module):
         return True
 
     def update(self, unet_number=None):
+        if self.gcomm is not None:
+            self.gcomm.check()  # an asynchronous RCCL error surfaces here, outside any capture
         unet_number = self.validate_and_return_unet_number(unet_number)
         index = unet_number - 1
         opt = getattr(self, f"optim{index}")
@@ -870,7 +986,7 @@ class VideoDecoderTrainer(nn.Module):
             # the overlapped all-reduce goes into the graph only where the
             # collective can be captured (RCCL); with gloo the update reduces
             ov = self._overlap_for(unet_number)
-            if ov is not None and not (dist.get_backend() == "nccl"):
+            if ov is not None and not self.gcomm.capturable(self.device):
                 ov = None
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
@@ -910,6 +1026,18 @@ class VideoDecoderTrainer(nn.Module):
 
     def forward(self, *args, unet_number=None, max_batch_size=None, return_lowres_cond_video=False,
                 **kwargs):
+        watched = self.gcomm is not None and self.gcomm.native is not None
+        if watched:
+            _NATIVE.mark(True)  # the watchdog's deadline covers the blocking loss.item()
+        try:
+            return self._forward(*args, unet_number=unet_number, max_batch_size=max_batch_size,
+                                 return_lowres_cond_video=return_lowres_cond_video, **kwargs)
+        finally:
+            if watched:
+                _NATIVE.mark(False)
+
+    def _forward(self, *args, unet_number=None, max_batch_size=None, return_lowres_cond_video=False,
+                 **kwargs):
         unet_number = self.validate_and_return_unet_number(unet_number)
         args = tuple(self._to_device(a) for a in args)
         kwargs = {k: self._to_device(v) for k, v in kwargs.items()}
@@ -933,7 +1061,7 @@ class VideoDecoderTrainer(nn.Module):
         chunks = list(split_args_and_kwargs(*args, split_size=max_batch_size, **kwargs))
         # overlap only a single-chunk call (chunks accumulate into the same buffer)
         ov = self._overlap_for(unet_number) if (self.training and len(chunks) == 1) else None
-        if ov is not None and graphable and dist.get_backend() != "nccl":
+        if ov is not None and graphable and not self.gcomm.capturable(self.device):
             # the eager calls that warm a capture run the pass the graph will
             # hold: without a capturable collective (gloo) the graph has no
             # bucket hooks, so the deferred split-K sums it replays are ONE

@@ -537,12 +537,16 @@ int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int ldo, const 
  * (the trainer uses the torch.distributed store).  init: blocking, every rank
  * at once, on `device`.  allreduce: in place on `stream`, `average` != 0 ->
  * mean over ranks (idempotent on data every rank already holds, as DDP's
- * averaged buckets are), else sum.                                          */
+ * averaged buckets are), else sum.  async_error: DV_OK while the
+ * communicator is healthy (pollable from any thread: the trainer's
+ * watchdog).  destroy: after the last collective completed; abort: frees it
+ * without waiting for outstanding work (a dead peer).                        */
 int dv_comm_unique_id(void* id_out);
 int dv_comm_init(const void* id, int nranks, int rank, int device, void** comm_out);
 int dv_comm_allreduce(void* comm, void* buf, long long count, int dtype, int average, void* stream);
 int dv_comm_async_error(void* comm);
 int dv_comm_destroy(void* comm);
+int dv_comm_abort(void* comm);
 
 #ifdef __cplusplus
 }

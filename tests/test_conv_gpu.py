@@ -24,6 +24,9 @@ CASES = [
     (2, 8, 8, 512, 256, 512, 3),    # W=8, 12 channel chunks x 3 tap rows, one split
     (8, 16, 16, 256, 0, 64, 1),     # 1x1 (Downsample3D-like), many splits
     (16, 8, 8, 64, 0, 128, 3),      # W=8, 2 cout tiles
+    (2, 64, 64, 64, 64, 64, 3),     # window wgrad W=64: two 32-column blocks, dual source
+    (2, 32, 64, 64, 0, 128, 3),     # window wgrad W=64, H=32 (non-square: 8 row blocks x 2 column blocks)
+    (3, 32, 16, 64, 0, 64, 3),      # window wgrad W=16, H=32 (four 8-row stages per frame)
     (16, 32, 32, 128, 0, 64, 1),    # 1x1 stripe wgrad (res_conv-like), 2 channel chunks
     (8, 16, 16, 64, 64, 128, 1),    # 1x1 stripe wgrad, dual source
     # stripe forward / dgrad (64 input channels, W in {32, 64})

@@ -216,6 +216,26 @@ def test_shard_loader_keeps_custom_batch_sampler_batches():
     assert got[1] == [batches[1], batches[3]]
 
 
+def test_shard_loader_leaves_the_callers_sampler_unseeded():
+    """sharding a loader whose batch sampler draws from an
+    unseeded RandomSampler seeds a COPY (every rank draws the broadcast-seeded
+    order); the caller's DataLoader keeps its own sampler, unseeded."""
+    from torch.utils.data import BatchSampler, DataLoader, RandomSampler, TensorDataset
+
+    from dalle2_video.trainer import shard_loader
+
+    ds = TensorDataset(torch.arange(32))
+    rs = RandomSampler(ds)
+    loader = DataLoader(ds, batch_sampler=BatchSampler(rs, 4, drop_last=False))
+    orders = []
+    for r in range(2):
+        sh = shard_loader(loader, 2, r)
+        orders.append([b[0].tolist() for b in sh])
+    assert rs.generator is None and loader.batch_sampler.sampler is rs
+    flat = sorted(v for o in orders for b in o for v in b)
+    assert flat == list(range(32))  # the two ranks' batches partition one seeded order
+
+
 def test_decoder_state_dict_keys_match_the_reference_layout():
     """VideoDecoder's checkpoint keys (what train_decoder.py:177-184 saves):
     the reference module tree (dalle2_video.py:1169-1506) registers, per unet

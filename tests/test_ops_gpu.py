@@ -330,6 +330,36 @@ def test_mqa_forward_streamed_long_sequence(parity_log, N, B, qmag):
     assert e < 2.5e-2
 
 
+def test_mqa_bf16_backward_long_sequence():
+    """A bf16 mid attention longer than the bf16 backward's LDS limit (NKP >
+    1280; config 5 trains at 8,193 keys) runs forward and backward on the f32
+    kernels when gradients are needed: same values as the f32 path on the
+    same (bf16-rounded) inputs, bf16 outputs and input gradients."""
+    from dalle2_video import ops
+
+    g = torch.Generator().manual_seed(21)
+    B, N, H, D = 1, 2048, 16, 32
+    q = torch.randn(B * N, H * D, generator=g).to(torch.bfloat16)
+    kv = (torch.randn(B * N, 2 * D, generator=g) * 2).to(torch.bfloat16)
+    null_kv = torch.randn(2, D, generator=g)
+    gy = torch.randn(B * N, H * D, generator=g).cuda()
+    outs = []
+    for dtype in (torch.bfloat16, torch.float32):
+        qd = _leaf(q.float(), "cuda", dtype)
+        kvd = _leaf(kv.float(), "cuda", dtype)
+        nd = _leaf(null_kv, "cuda")
+        y = ops.mqa(qd, kvd, nd, B, N, H, 1.0 / D)
+        assert y.dtype == dtype
+        (y.float() * gy).sum().backward()
+        assert qd.grad.dtype == dtype and kvd.grad.dtype == dtype
+        outs.append([y.float(), qd.grad.float(), kvd.grad.float(), nd.grad])
+    for a, b in zip(*outs):
+        assert rel(a, b) < 1e-2  # one bf16 rounding of each output / gradient
+    with torch.no_grad():  # no gradients: the bf16 streamed forward itself
+        y = ops.mqa(q.cuda(), kv.cuda(), null_kv.cuda(), B, N, H, 1.0 / D)
+    assert y.dtype == torch.bfloat16 and rel(y.float(), outs[1][0]) < 2.5e-2
+
+
 @pytest.mark.parametrize("ngemm,nb,P,n", [(3, 4, 1000, 64), (3, 2, 4096, 128), (2, 1, 77, 256), (1, 3, 300, 64)])
 def test_gemm_tn_batched_multi(ngemm, nb, P, n):
     """The one-launch form of the cross-attention token reductions: problem g,

@@ -1,0 +1,16 @@
+#!/bin/bash
+export TMPDIR=/tmp
+tag=r05e
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py tests/test_ops_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_tests.log; exit 1; }
+tail -1 gpurun_out/${tag}_tests.log
+DV_WG_ISS=2 timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests2.log 2>&1 || { tail -30 gpurun_out/${tag}_tests2.log; exit 1; }
+tail -1 gpurun_out/${tag}_tests2.log
+for rep in 1 2; do
+  for v in 0 2; do
+    DV_WG_ISS=$v timeout -k 10 120 python tools/wgrad_ab.py 2>/dev/null | sed "s/^/ISS=$v /" >> gpurun_out/${tag}_wg.log || exit 1
+  done
+done
+DV_WG_OLD=1 timeout -k 10 120 python tools/wgrad_ab.py 2>/dev/null | sed "s/^/OLD /" >> gpurun_out/${tag}_wg.log || exit 1
+grep total gpurun_out/${tag}_wg.log
+bash tools/ab_env.sh DV_WG_ISS "0 2" ${tag}_step
