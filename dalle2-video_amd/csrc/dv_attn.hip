@@ -602,30 +602,6 @@ __device__ __forceinline__ void dma_kv(const bf16* kb, const bf16* vb, char* sK,
   }
 }
 
-// as dma_kv for the key tiles [a0, a1) and [b0, b1) only (two 16-row pieces
-// per 32-key tile): the phased prologue (kv_phase) stages the first tiles of
-// both key halves, starts on them, and stages the rest behind that compute
-__device__ __forceinline__ void dma_kv_tiles(const bf16* kb, const bf16* vb, char* sK, char* sV, int NKP,
-                                             int wave, int lane, int a0, int a1, int b0, int b1) {
-  const __amdgpu_buffer_rsrc_t rk = dma_rsrc(kb, (unsigned)NKP * ROW);
-  const __amdgpu_buffer_rsrc_t rv = dma_rsrc(vb, (unsigned)NKP * ROW);
-  const int na = 2 * (a1 - a0), n = na + 2 * (b1 - b0);  // pieces of K (and of V)
-  const int rr = lane >> 2, slot = lane & 3;
-  for (int i = wave; i < 2 * n; i += NW) {
-    const bool isv = i >= n;
-    const int j = isv ? i - n : i;
-    const int pc = j < na ? 2 * a0 + j : 2 * b0 + (j - na);
-    const int row = pc * 16 + rr;
-    const unsigned voff = row * ROW + 16 * (slot ^ ((row >> 2) & 3));
-    if (isv)
-      dma16(rv, sV + pc * 1024, voff);
-    else
-      dma16(rk, sK + pc * 1024, voff);
-  }
-}
-// first-phase tiles of a key half [k0, k1): a quarter, rounded up
-__device__ __forceinline__ int kv_phase(int k0, int k1) { return min(k1, k0 + (k1 - k0 + 3) / 4); }
-
 __device__ __forceinline__ bf16x8 load_row8(const bf16* p, bool ok) {
   if (!ok) return bf16x8{};
   return *(const bf16x8*)p;
@@ -716,22 +692,6 @@ __device__ __forceinline__ void soft_tile(Soft& st, f32x16& s, f32x16& sn, const
   tr_wait(vt, v0, v1);
   st.acc = mma(v0, pack8(s, 0), st.acc);
   st.acc = mma(v1, pack8(s, 1), st.acc);
-}
-// key tiles [kbeg, kend) of LDS images sK / sV (tile t at t * 32 rows; global
-// key of tile t = kg0 + 32 t), pipelined one tile ahead; `first` starts the state
-__device__ __forceinline__ void soft_range(Soft& st, bool first, const char* sK, const char* sV, int kbeg, int kend,
-                                           int kg0, int nkeys, const FragOff& fo, bf16x8 q0, bf16x8 q1, int h) {
-  if (kbeg >= kend) return;
-  f32x16 s = score(sK + kbeg * 32 * ROW, fo, q0, q1, first ? zero16() : st.negm);
-  mask_keys(s, kg0 + kbeg * 32, nkeys, h);
-  if (first) soft_init(st, s);
-  for (int kt = kbeg; kt < kend; ++kt) {
-    const int kn = kt + 1 < kend ? kt + 1 : kt;  // the last trip re-scores its own tile (discarded)
-    f32x16 sn = score(sK + kn * 32 * ROW, fo, q0, q1, st.negm);
-    soft_tile(st, s, sn, sV + kt * 32 * ROW, fo);
-    mask_keys(sn, kg0 + kn * 32, nkeys, h);
-    s = sn;
-  }
 }
 // Two key tiles per step (64 keys): one max chain, 32 independent exps and
 // 4 PV MFMAs per dependency round — the per-wave chain max -> exp -> PV is
@@ -832,22 +792,9 @@ __device__ __forceinline__ void soft_range2(Soft& st, bool first, const char* sK
 // f32's range, so the softmax needs no running max at all: m = 0, no max
 // chain, no rescale, one exp2 per score -- the same softmax, exactly.
 constexpr float FIX_BOUND = 64.f;
-// Row sums on the MFMA pipe (-DDV_MQA_MSUM=1, off): l^T += 1 . P^T with an
-// all-ones A operand -- every row of the 32 x 32 result is the query's sum of
-// the bf16 P that PV multiplies; 4 MFMAs per key pair instead of ~30 VALU
-// adds.  Measured slower (8,192 tokens 391 -> 402-418 us, Cfg2 20.6 -> 21.2-
-// 23.9 us, profiles/r04l_mqa_msum_ab.txt): the 16 more accumulator VGPRs put
-// the kernels at the 128-VGPR cap.
-#ifndef DV_MQA_MSUM
-#define DV_MQA_MSUM 0
-#endif
-__device__ __forceinline__ bf16x8 ones8() {
-  bf16x8 o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (__bf16)1.f;
-  return o;
-}
-__device__ __forceinline__ void soft_step2_fixed(Soft& st, f32x16& lacc, f32x16& s0, f32x16& s1, const char* tV0,
+// (Row sums on the MFMA pipe, an all-ones A operand, measured slower in
+// round 4 -- profiles/r04l_mqa_msum_ab.txt -- and were removed in round 5.)
+__device__ __forceinline__ void soft_step2_fixed(Soft& st, f32x16& s0, f32x16& s1, const char* tV0,
                                                  const char* tV1, const char* tKn0, const char* tKn1,
                                                  const FragOff& fo, bf16x8 q0, bf16x8 q1) {
   TrFrag vt0, vt1;  // tV1 == tV0 + 32 rows
@@ -857,7 +804,7 @@ __device__ __forceinline__ void soft_step2_fixed(Soft& st, f32x16& lacc, f32x16&
     s0[e] = ex2(s0[e]);
     s1[e] = ex2(s1[e]);
   }
-  if (!DV_MQA_MSUM) st.l += sum16(s0) + sum16(s1);
+  st.l += sum16(s0) + sum16(s1);
   const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
   s0 = score(tKn0, fo, q0, q1, zero16());
   s1 = score(tKn1, fo, q0, q1, zero16());
@@ -868,17 +815,9 @@ __device__ __forceinline__ void soft_step2_fixed(Soft& st, f32x16& lacc, f32x16&
   st.acc = mma(a1, p01, st.acc);
   st.acc = mma(b0, p10, st.acc);
   st.acc = mma(b1, p11, st.acc);
-  if (DV_MQA_MSUM) {
-    const bf16x8 one = ones8();
-    lacc = mma(one, p00, lacc);
-    lacc = mma(one, p01, lacc);
-    lacc = mma(one, p10, lacc);
-    lacc = mma(one, p11, lacc);
-  }
 }
-// soft_range2 for a bounded wave (st.m stays 0); lacc: the MFMA row sums
-// (DV_MQA_MSUM), carried across calls -- soft_msum_done moves them into st.l
-__device__ __forceinline__ void soft_range2_fixed(Soft& st, f32x16& lacc, const char* sK, const char* sV, int kbeg,
+// soft_range2 for a bounded wave (st.m stays 0)
+__device__ __forceinline__ void soft_range2_fixed(Soft& st, const char* sK, const char* sV, int kbeg,
                                                   int kend, int kg0, int nkeys, const FragOff& fo, bf16x8 q0,
                                                   bf16x8 q1, int h) {
   st.m = 0.f;
@@ -890,16 +829,12 @@ __device__ __forceinline__ void soft_range2_fixed(Soft& st, f32x16& lacc, const 
     TrFrag vt = tr_issue(sV + kt * 32 * ROW, fo);
 #pragma unroll
     for (int e = 0; e < 16; ++e) s[e] = ex2(s[e]);
-    if (!DV_MQA_MSUM) st.l += sum16(s);
+    st.l += sum16(s);
     bf16x8 a0, a1;
     tr_wait(vt, a0, a1);
     const bf16x8 ps0 = pack8(s, 0), ps1 = pack8(s, 1);
     st.acc = mma(a0, ps0, st.acc);
     st.acc = mma(a1, ps1, st.acc);
-    if (DV_MQA_MSUM) {
-      lacc = mma(ones8(), ps0, lacc);
-      lacc = mma(ones8(), ps1, lacc);
-    }
     ++kt;
   }
   if (kt >= kend) return;
@@ -909,24 +844,11 @@ __device__ __forceinline__ void soft_range2_fixed(Soft& st, f32x16& lacc, const 
   mask_keys(s1, kg0 + (kt + 1) * 32, nkeys, h);
   for (; kt < kend; kt += 2) {
     const int kn0 = kt + 2 < kend ? kt + 2 : kt, kn1 = kn0 + 1;
-    soft_step2_fixed(st, lacc, s0, s1, sV + kt * 32 * ROW, sV + (kt + 1) * 32 * ROW, sK + kn0 * 32 * ROW,
+    soft_step2_fixed(st, s0, s1, sV + kt * 32 * ROW, sV + (kt + 1) * 32 * ROW, sK + kn0 * 32 * ROW,
                      sK + kn1 * 32 * ROW, fo, q0, q1);
     mask_keys(s0, kg0 + kn0 * 32, nkeys, h);
     mask_keys(s1, kg0 + kn1 * 32, nkeys, h);
   }
-}
-// the MFMA row sums hold the whole 32-key sum in every element on both lane
-// halves; soft_finish adds the halves, so half 1 contributes zero
-__device__ __forceinline__ void soft_msum_done(Soft& st, const f32x16& lacc, int h) {
-  if (DV_MQA_MSUM) st.l = h == 0 ? lacc[0] : 0.f;
-}
-template <bool PAIR>
-__device__ __forceinline__ void soft_range_t(Soft& st, bool first, const char* sK, const char* sV, int kbeg, int kend,
-                                             int kg0, int nkeys, const FragOff& fo, bf16x8 q0, bf16x8 q1, int h) {
-  if constexpr (PAIR)
-    soft_range2(st, first, sK, sV, kbeg, kend, kg0, nkeys, fo, q0, q1, h);
-  else
-    soft_range(st, first, sK, sV, kbeg, kend, kg0, nkeys, fo, q0, q1, h);
 }
 // wave-uniform: every score of this wave's rows within FIX_BOUND?  (kmax:
 // the prep's per-block key norms of clip b; NULL = unknown -> online max)
@@ -978,10 +900,6 @@ __device__ __forceinline__ void soft_finish(Soft& st, float* red, int kh, int la
 // grid (ceil(R / 256), B), 1024 threads, dynamic LDS 2 * NKP * 64 B.
 // Wave w: 32 query rows (group w & 7) against key half w >> 3 of the whole
 // clip's K / V, staged once by LDS-DMA; the halves merge through LDS.
-// PH: phased prologue -- the first quarter of each key half is staged and
-// multiplied while the rest lands (every workgroup bursts its whole clip's
-// K / V at once: ≈ 12.5 B/cycle/CU, MI355X_MICROARCH.md, ≈ 4.5 us at 1,056 keys)
-template <bool PAIR, bool PH = false>
 __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restrict__ q,
                                                              const bf16* __restrict__ kp,
                                                              const bf16* __restrict__ vp,
@@ -996,43 +914,22 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   const int rg = wave & (RG - 1), kh = wave / RG;
   const int b = blockIdx.y;
   const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
-  const int qa0 = kv_phase(0, kmid), qa1 = kv_phase(kmid, nkt);
   const bf16* kb = kp + (long long)b * NKP * 32;
   const bf16* vb = vp + (long long)b * NKP * 32;
-  if (PH) dma_kv_tiles(kb, vb, sK, sV, NKP, wave, lane, 0, qa0, kmid, qa1);
-  else dma_kv(kb, vb, sK, sV, NKP, wave, lane);
+  dma_kv(kb, vb, sK, sV, NKP, wave, lane);
   const int row = blockIdx.x * RG * 32 + rg * 32 + r;
   const bool rok = row < R;
   const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
   const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (PH) dma_kv_tiles(kb, vb, sK, sV, NKP, wave, lane, qa0, kmid, qa1, nkt);
   const FragOff fo = frag_off(lane);
-  const int k0 = kh ? kmid : 0, k1 = kh ? nkt : kmid, kq = PH ? (kh ? qa1 : qa0) : k1;
-  auto rest = [&]() {  // the second phase's tiles landed (every wave's pieces)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
+  const int k0 = kh ? kmid : 0, k1 = kh ? nkt : kmid;
   Soft st{zero16(), zero16(), -INFINITY, 0.f};
-  const bool fixed = PAIR && scores_bounded(kmax, nkb, b, lane, qf0, qf1);
-  // the phases as a rolled loop: one copy of each range body (two inlined
-  // copies spilled at the 128-VGPR cap)
-  if (fixed) {
-    f32x16 lacc = zero16();
-#pragma unroll 1
-    for (int ph = 0; ph < (PH ? 2 : 1); ++ph) {
-      if (ph) rest();
-      soft_range2_fixed(st, lacc, sK, sV, ph ? kq : k0, ph ? k1 : kq, 0, nkeys, fo, qf0, qf1, h);
-    }
-    soft_msum_done(st, lacc, h);
-  } else {
-#pragma unroll 1
-    for (int ph = 0; ph < (PH ? 2 : 1); ++ph) {
-      if (ph) rest();
-      soft_range_t<PAIR>(st, ph == 0, sK, sV, ph ? kq : k0, ph ? k1 : kq, 0, nkeys, fo, qf0, qf1, h);
-    }
-  }
+  if (scores_bounded(kmax, nkb, b, lane, qf0, qf1))
+    soft_range2_fixed(st, sK, sV, k0, k1, 0, nkeys, fo, qf0, qf1, h);
+  else
+    soft_range2(st, true, sK, sV, k0, k1, 0, nkeys, fo, qf0, qf1, h);
   soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
               lse + (long long)b * R + row);
 }
@@ -1060,7 +957,6 @@ __device__ __forceinline__ void dma_kv_chunk(const __amdgpu_buffer_rsrc_t& rk,
   }
 }
 
-template <bool PAIR>
 __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* __restrict__ q,
                                                                     const bf16* __restrict__ kp,
                                                                     const bf16* __restrict__ vp,
@@ -1084,7 +980,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
   const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
   const FragOff fo = frag_off(lane);
   Soft st{zero16(), zero16(), -INFINITY, 0.f};
-  const bool fixed = PAIR && scores_bounded(kmax, nkb, b, lane, qf0, qf1);
+  const bool fixed = scores_bounded(kmax, nkb, b, lane, qf0, qf1);
   // chunk ch landed (the only DMA in flight); every wave is done with the
   // buffer chunk ch + 1 goes to (it held chunk ch - 1)
   auto next_chunk = [&](int ch) {
@@ -1098,198 +994,32 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
   // two chunk loops (bounded / online): one loop holding both range bodies
   // spilled at the 128-VGPR cap
   if (fixed) {
-    f32x16 lacc = zero16();
     for (int ch = 0; ch < nch; ++ch) {
       next_chunk(ch);
       const int row0 = ch * SCK, nkt = min(SCK, NKP - row0) / 32, kmid = (nkt + 1) / 2;
-      soft_range2_fixed(st, lacc, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo,
-                        qf0, qf1, h);
+      soft_range2_fixed(st, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo, qf0,
+                        qf1, h);
     }
-    soft_msum_done(st, lacc, h);
   } else {
     for (int ch = 0; ch < nch; ++ch) {
       next_chunk(ch);
       const int row0 = ch * SCK, nkt = min(SCK, NKP - row0) / 32, kmid = (nkt + 1) / 2;
-      soft_range_t<PAIR>(st, ch == 0, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys,
-                         fo, qf0, qf1, h);
+      soft_range2(st, ch == 0, buf_k(ch & 1), buf_v(ch & 1), kh ? kmid : 0, kh ? nkt : kmid, row0, nkeys, fo, qf0,
+                  qf1, h);
     }
   }
   soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
               lse + (long long)b * R + row);
 }
 
-// ---- forward, ping-pong (round 4) ------------------------------------------
-// At d = 32 a key tile costs a wave as much VALU (16 v_exp at 8 issue cycles
-// each + the max / sum / pack) as MFMA (4 x 32 cycles), and the two do not
-// overlap inside one wave.  Here the two key halves of a workgroup are two
-// wave GROUPS that sit on every SIMD (waves w and w + 8 share one) and run
-// half an iteration apart, separated by workgroup barriers: while group 0 is
-// in its MFMA phase (score the next tile, PV of the current one), group 1 is
-// in its softmax phase (max, exp2, row sums, bf16 pack), then they swap.
-//   M(x): S_{x+1} = K_{x+1} Q^T (C operand -m: log2 units minus the max),
-//         O^T += V_x^T P_x^T
-//   V(x+1): mask, max, lazy rescale, P = exp2(S), l += sum, pack
-// Group 1 enters one barrier late; both run the same number of iterations
-// (the half with fewer tiles runs fully masked dummies).  STREAM: K / V
-// arrive in 512-key chunks by LDS-DMA into a double buffer (each wave issues
-// its pieces of chunk c + 1 at its first M phase of chunk c, when both groups
-// are past chunk c - 1, and drains them in the last two iterations of chunk
-// c); otherwise the whole clip's K / V are staged once.
-struct PPState {
-  f32x16 acc, negm, s;
-  bf16x8 p0, p1;
-  float m, l;
-};
-// kg: the tile's first key (a dummy passes kg = nkeys: every key masked)
-__device__ __forceinline__ void pp_softmax(PPState& st, int kg, int nkeys, int h) {
-  mask_keys(st.s, kg, nkeys, h);
-  const float mx = col_max(st.s);
-  const bool upd = mx > 8.f;
-  if (__builtin_amdgcn_ballot_w64(upd)) {
-    const float d = upd ? mx : 0.f;
-    const float a = ex2(-d);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      st.s[e] -= d;
-      st.acc[e] *= a;
-    }
-    st.l *= a;
-    st.m += d;
-    st.negm = bcast16(-st.m);
-  }
-#pragma unroll
-  for (int e = 0; e < 16; ++e) st.s[e] = ex2(st.s[e]);
-  st.l += sum16(st.s);
-  st.p0 = pack8(st.s, 0);
-  st.p1 = pack8(st.s, 1);
-}
-__device__ __forceinline__ void pp_mfma(PPState& st, const char* tKn, const char* tV, const FragOff& fo, bf16x8 q0,
-                                        bf16x8 q1) {
-  const bf16x8 k0 = row_at(tKn, fo, 0), k1 = row_at(tKn, fo, 1);
-  TrFrag vt = tr_issue(tV, fo);
-  bf16x8 v0, v1;
-  tr_wait(vt, v0, v1);
-  st.s = mma(k0, q0, st.negm);
-  st.acc = mma(v0, st.p0, st.acc);
-  st.s = mma(k1, q1, st.s);
-  st.acc = mma(v1, st.p1, st.acc);
-}
-
-template <bool STREAM>
-__global__ __launch_bounds__(NW * 64) void mqa_fwd_pp_kernel(const bf16* __restrict__ q,
-                                                             const bf16* __restrict__ kp,
-                                                             const bf16* __restrict__ vp,
-                                                             bf16* __restrict__ o, float* lse,
-                                                             int R, int NKP, int nkeys) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int rg = wave & (RG - 1), g = wave / RG;  // g: key half = ping-pong group
-  const int b = blockIdx.y;
-  const int CK = STREAM ? SCK : NKP;  // keys per chunk
-  const int nch = (NKP + CK - 1) / CK;
-  const __amdgpu_buffer_rsrc_t rk = dma_rsrc(kp + (long long)b * NKP * 32, (unsigned)NKP * ROW);
-  const __amdgpu_buffer_rsrc_t rv = dma_rsrc(vp + (long long)b * NKP * 32, (unsigned)NKP * ROW);
-  auto buf_k = [&](int c) { return smem + (STREAM ? (c & 1) * 2 * SCK * ROW : 0); };
-  auto buf_v = [&](int c) { return smem + (STREAM ? (c & 1) * 2 * SCK * ROW : 0) + CK * ROW; };
-  dma_kv_chunk(rk, rv, buf_k(0), buf_v(0), 0, min(CK, NKP), wave, lane);
-  const int row = blockIdx.x * RG * 32 + rg * 32 + r;
-  const bool rok = row < R;
-  const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
-  const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const FragOff fo = frag_off(lane);
-  // this group's tiles of chunk c: [tb(c), tb(c) + it(c)), valid below te(c)
-  auto nkt_of = [&](int c) { return min(CK, NKP - c * CK) / 32; };
-  auto it_of = [&](int c) { return (nkt_of(c) + 1) / 2; };
-  auto tb_of = [&](int c) { return g ? it_of(c) : 0; };
-  auto te_of = [&](int c) { return g ? nkt_of(c) : it_of(c); };
-  // prologue: score + softmax of the group's first tile (chunk 0)
-  PPState st;
-  st.acc = zero16();
-  st.l = 0.f;
-  {
-    const int t0 = tb_of(0);
-    const bool dummy = t0 >= te_of(0);
-    const int tt = dummy ? te_of(0) - 1 : t0;
-    st.s = score(buf_k(0) + tt * 32 * ROW, fo, qf0, qf1, zero16());
-    mask_keys(st.s, dummy ? nkeys : tt * 32, nkeys, h);
-    st.m = col_max(st.s);  // the first tile is never a dummy for NKP >= 64
-#pragma unroll
-    for (int e = 0; e < 16; ++e) st.s[e] = ex2(st.s[e] - st.m);
-    st.l = sum16(st.s);
-    st.p0 = pack8(st.s, 0);
-    st.p1 = pack8(st.s, 1);
-    st.negm = bcast16(-st.m);
-  }
-  static_assert(NW == 16, "two groups of 8 waves");
-  if (g) {
-    __builtin_amdgcn_s_setprio(1);  // the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD" 4)
-    __builtin_amdgcn_s_barrier();   // half a step behind group 0
-  }
-  for (int c = 0; c < nch; ++c) {
-    const int its = it_of(c), tb = tb_of(c), te = te_of(c);
-    const char* sK = buf_k(c);
-    const char* sV = buf_v(c);
-    for (int i = 0; i < its; ++i) {
-      const int tcur = min(tb + i, te - 1);  // a dummy re-reads a valid tile (its P is zero)
-      // the next tile: this chunk's next, or the next chunk's first
-      const bool last_in_chunk = i + 1 == its;
-      const bool has_next_chunk = c + 1 < nch;
-      int tn;
-      const char* sKn;
-      bool ndummy;
-      int kgn;
-      if (!last_in_chunk) {
-        tn = tb + i + 1;
-        ndummy = tn >= te;
-        tn = ndummy ? te - 1 : tn;
-        sKn = sK;
-        kgn = c * CK + tn * 32;
-      } else if (has_next_chunk) {
-        const int tb2 = tb_of(c + 1), te2 = te_of(c + 1);
-        ndummy = tb2 >= te2;
-        tn = ndummy ? te2 - 1 : tb2;
-        sKn = buf_k(c + 1);
-        kgn = (c + 1) * CK + tn * 32;
-      } else {
-        tn = tcur;  // past the end: scored and discarded
-        ndummy = true;
-        sKn = sK;
-        kgn = 0;
-      }
-      if (STREAM && i == 0 && has_next_chunk)  // chunk c - 1 is read by nobody now
-        dma_kv_chunk(rk, rv, buf_k(c + 1), buf_v(c + 1), (c + 1) * CK, min(CK, NKP - (c + 1) * CK), wave, lane);
-      const bool drain = STREAM && has_next_chunk && i + 2 >= its;
-      // ---- M phase ----  (sched_barrier: hipcc would move MFMAs / VALU across s_barrier)
-      pp_mfma(st, sKn + tn * 32 * ROW, sV + tcur * 32 * ROW, fo, qf0, qf1);
-      if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- V phase (the next tile's softmax) ----
-      pp_softmax(st, ndummy ? nkeys : kgn, nkeys, h);
-      if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if (!g) __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_s_setprio(0);
-  // the last V phase scored a tile past the end: its P was never used
-  Soft fin{st.acc, st.negm, st.m, st.l};
-  soft_finish(fin, (float*)smem + rg * 18 * 64, g, lane, h, rok, o + ((long long)b * R + row) * 32,
-              lse + (long long)b * R + row);
-}
+// (A ping-pong forward -- two 8-wave groups per SIMD a half iteration apart
+// -- measured slower in round 4, profiles/r04b_pp_ab.txt; removed in round 5.)
 
 // dq (query-major, as the forward: key halves summed through LDS) and
 // D = rowsum(dO * O) for the dk/dv pass.  Both per-row constants enter as C
 // operands: S^T arrives as c s - L (keys pre-scaled by c), dP^T as dP - D, so
 // dS = exp2(.) * (.) is two VALU ops per score.  dq = (K^T dS^T) / log2 e
 // (the keys carry c = scale * log2 e; dq needs scale).
-template <bool PH = false>
 __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
@@ -1302,11 +1032,9 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   const int rg = wave & (RG - 1), kh = wave / RG;
   const int b = blockIdx.y;
   const int nkt = NKP / 32, kmid = (nkt + 1) / 2;
-  const int qa0 = kv_phase(0, kmid), qa1 = kv_phase(kmid, nkt);  // PH: as the forward
   const bf16* kb = kp + (long long)b * NKP * 32;
   const bf16* vb = vp + (long long)b * NKP * 32;
-  if (PH) dma_kv_tiles(kb, vb, sK, sV, NKP, wave, lane, 0, qa0, kmid, qa1);
-  else dma_kv(kb, vb, sK, sV, NKP, wave, lane);
+  dma_kv(kb, vb, sK, sV, NKP, wave, lane);
   const int row = blockIdx.x * RG * 32 + rg * 32 + r;
   const bool rok = row < R;
   const long long ro = ((long long)b * R + (rok ? row : 0)) * 32;
@@ -1318,11 +1046,10 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   if (rok && h == 0 && kh == 0) D[(long long)b * R + row] = dd;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (PH) dma_kv_tiles(kb, vb, sK, sV, NKP, wave, lane, qa0, kmid, qa1, nkt);
   const FragOff fo = frag_off(lane);
   const f32x16 negL = bcast16(-L2), negD = bcast16(-dd);
   f32x16 acc = zero16();
-  const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid, kq = PH ? (kh ? qa1 : qa0) : kend;
+  const int kbeg = kh ? kmid : 0, kend = kh ? nkt : kmid;
   auto tile = [&](int kt) {
     const int k0 = kt * 32;
     const char* tK = sK + k0 * ROW;
@@ -1342,12 +1069,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
     acc = mma(tr_at(tK, fo, 0), pack8(s, 0), acc);
     acc = mma(tr_at(tK, fo, 1), pack8(s, 1), acc);
   };
-  for (int kt = kbeg; kt < kq; ++kt) tile(kt);
-  if (PH) {  // the second phase's tiles landed (every wave's pieces)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = kq; kt < kend; ++kt) tile(kt);
-  }
+  for (int kt = kbeg; kt < kend; ++kt) tile(kt);
   __syncthreads();
   float* red = (float*)smem + rg * 16 * 64;
   if (kh) {
@@ -1378,12 +1100,13 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
 constexpr int TB = 2 * 32 * ROW + 2 * 32 * 4;  // one tile: Q, dO images, L, -D
 constexpr int QP = NW / 4;                      // query-tile parities
 constexpr int RED = 2 * 4 * 2 * 16 * 64 * 4;    // parity combine (two parities at a time)
-// TPS: query tiles per wave per step (one barrier per TPS tiles)
-template <bool EARLY, int TPS = 1>
+// (Two query tiles per wave between barriers measured slower in round 4,
+// profiles/r04o_mqa_ph_tps_ab.txt: one tile per step.)
 __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ D, const bf16* __restrict__ kp, const bf16* __restrict__ vp,
     float* __restrict__ ws, int R, int NKP, int nkeys, int rows_per_split, float scale) {
+  constexpr int TPS = 1;
   __shared__ __attribute__((aligned(16))) char smem[2 * QP * TPS * TB > RED ? 2 * QP * TPS * TB : RED];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
@@ -1434,20 +1157,16 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     store(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // EARLY: step st+1's tile was loaded during step st-1 and is stored at the
-  // top of step st (its buffer was read in step st-1, before the last
-  // barrier), then step st+2's loads go out: a whole step of latency cover
-  // instead of one step's compute (the loop waited on each tile's load)
-  if (EARLY && nsteps > 1) load(1);
+  // step st+1's tile was loaded during step st-1 and is stored at the top of
+  // step st (its buffer was read in step st-1, before the last barrier), then
+  // step st+2's loads go out: a whole step of latency cover instead of one
+  // step's compute (33.0-33.6 -> 31.6-31.7 us, profiles/r04o_mqa_early_ab.txt)
+  if (nsteps > 1) load(1);
   __syncthreads();
   for (int st = 0; st < nsteps; ++st) {
     const bool more = st + 1 < nsteps;
-    if (EARLY) {
-      if (more) store((st + 1) & 1);
-      if (st + 2 < nsteps) load(st + 2);
-    } else if (more) {
-      load(st + 1);
-    }
+    if (more) store((st + 1) & 1);
+    if (st + 2 < nsteps) load(st + 2);
 #pragma unroll
     for (int j = 0; j < TPS; ++j) {
     const char* t = smem + (QP * (TPS * (st & 1) + j) + qp) * TB;
@@ -1483,10 +1202,6 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
       dvv = mma(tr_frag(sdO, 1, lane), pack8a(s, 1), dvv);
       dk = mma(tr_frag(sQ, 1, lane), pack8a(dp, 1), dk);
     }
-    }
-    if (!EARLY && more) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      store((st + 1) & 1);
     }
     __syncthreads();
   }
@@ -1587,14 +1302,6 @@ void launch_finish(int s, int grid, hipStream_t st, const float* ws, int B, int 
   }
 }
 
-// DV_MQA_PH=1: the phased prologue of the forward and dq (a quarter of each
-// key half first).  Measured no faster at Cfg2 (fwd 20.4-20.9 vs 20.9-21.1 us,
-// profiles/r04o_mqa_ph_tps_ab.txt): off
-bool phased() {
-  static const bool on = getenv("DV_MQA_PH") && atoi(getenv("DV_MQA_PH")) != 0;
-  return on;
-}
-
 void set_lds(const void* fn, int bytes) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
@@ -1629,8 +1336,6 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
                           void* o, int ldo, float* lse, int B, int N, int NKP, int H, float scale,
                           const float* kmax, void* stream) {
   // kmax: dv_mqa_prep's key-norm bound (NULL: online max everywhere)
-  static const bool no_fixed = getenv("DV_MQA_FIXED") && atoi(getenv("DV_MQA_FIXED")) == 0;  // A/B
-  if (no_fixed) kmax = nullptr;
   const int nkb = (NKP + PREP_KEYS - 1) / PREP_KEYS;
   DV_REQUIRE(q && kp && vp && o && lse && H % 4 == 0 && NKP % 32 == 0, "bad arguments");
   DV_REQUIRE(ldq % 8 == 0 && ldo >= H * DH, "bad strides");
@@ -1639,53 +1344,19 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
     // bf16 keys come from dv_mqa_prep pre-scaled: only the fa kernels read them
     DV_REQUIRE(ldq == H * DH && ldo == H * DH, "bf16 path needs dense q / o rows");
     const int R = N * H;
-    // DV_MQA_STREAM=1: the K/V-streamed kernel at every length; DV_MQA_PAIR=0:
-    // one key tile per softmax step (A/B)
-    static const bool force_stream = getenv("DV_MQA_STREAM") && atoi(getenv("DV_MQA_STREAM")) != 0;
-    static const bool pair = !getenv("DV_MQA_PAIR") || atoi(getenv("DV_MQA_PAIR")) != 0;
     const dim3 grid((R + 255) / 256, B);
-    // DV_MQA_PP=1: the ping-pong kernel (two wave groups per SIMD) instead of the single-group ones
-    static const bool pp = getenv("DV_MQA_PP") && atoi(getenv("DV_MQA_PP")) != 0;
-    if (pp && NKP >= 64) {
-      const bool whole = fa::eligible(dtype, ldq, ldo, H, NKP) && !force_stream;
-      DV_REQUIRE((long long)NKP * fa::ROW < (1ll << 31), "sequence too long");
-      const int lds = whole ? max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4) : 4 * fa::SCK * fa::ROW;
-      const void* fn = whole ? (const void*)fa::mqa_fwd_pp_kernel<false> : (const void*)fa::mqa_fwd_pp_kernel<true>;
-      fa::set_lds(fn, lds);
-      if (whole)
-        fa::mqa_fwd_pp_kernel<false><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
-                                                                    (bf16*)o, lse, R, NKP, N + 1);
-      else
-        fa::mqa_fwd_pp_kernel<true><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
-                                                                   (bf16*)o, lse, R, NKP, N + 1);
-      return check_launch("mqa_fwd");
-    }
-    if (fa::eligible(dtype, ldq, ldo, H, NKP) && !force_stream) {
+    if (fa::eligible(dtype, ldq, ldo, H, NKP)) {
       const int lds = max(NKP * 2 * fa::ROW, fa::RG * 18 * 64 * 4);
-      const bool ph = fa::phased();
-#define DV_FWD_FA(P, PH)                                                                                       \
-  do {                                                                                                         \
-    fa::set_lds((const void*)fa::mqa_fwd_fa_kernel<P, PH>, lds);                                              \
-    fa::mqa_fwd_fa_kernel<P, PH><<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp, \
-                                                                 (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);     \
-  } while (0)
-      if (pair && ph) DV_FWD_FA(true, true);
-      else if (pair) DV_FWD_FA(true, false);
-      else if (ph) DV_FWD_FA(false, true);
-      else DV_FWD_FA(false, false);
-#undef DV_FWD_FA
+      fa::set_lds((const void*)fa::mqa_fwd_fa_kernel, lds);
+      fa::mqa_fwd_fa_kernel<<<grid, fa::NW * 64, lds, st>>>((const bf16*)q, (const bf16*)kp, (const bf16*)vp,
+                                                            (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
     } else {
+      // the whole clip's K / V do not fit LDS: stream them in 512-key chunks
       DV_REQUIRE((long long)NKP * fa::ROW < (1ll << 31), "sequence too long");
       const int lds = 4 * fa::SCK * fa::ROW;
-      const void* fn = pair ? (const void*)fa::mqa_fwd_fa_stream_kernel<true>
-                            : (const void*)fa::mqa_fwd_fa_stream_kernel<false>;
-      fa::set_lds(fn, lds);
-      if (pair)
-        fa::mqa_fwd_fa_stream_kernel<true><<<grid, fa::NW * 64, lds, st>>>(
-            (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
-      else
-        fa::mqa_fwd_fa_stream_kernel<false><<<grid, fa::NW * 64, lds, st>>>(
-            (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
+      fa::set_lds((const void*)fa::mqa_fwd_fa_stream_kernel, lds);
+      fa::mqa_fwd_fa_stream_kernel<<<grid, fa::NW * 64, lds, st>>>(
+          (const bf16*)q, (const bf16*)kp, (const bf16*)vp, (bf16*)o, lse, R, NKP, N + 1, kmax, nkb);
     }
   } else {
     dim3 grid((N + 31) / 32, H / 4, B);
@@ -1720,33 +1391,13 @@ extern "C" int dv_mqa_bwd(int dtype, const void* q, int ldq, const void* o, int 
     DV_REQUIRE(lddo == H * DH && lddq == H * DH, "bf16 path needs dense dout/dq rows");
     const int R = N * H, lds = max(NKP * 2 * fa::ROW, fa::RG * 16 * 64 * 4), S = fa::splits(NKP, B);
     const int rps = ((R + S - 1) / S + 63) / 64 * 64;
-    if (fa::phased()) {
-      fa::set_lds((const void*)fa::mqa_dq_fa_kernel<true>, lds);
-      fa::mqa_dq_fa_kernel<true><<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
-          (const bf16*)q, (const bf16*)o, (const bf16*)dout, lse, (const bf16*)kp, (const bf16*)vp,
-          (bf16*)dq, D, R, NKP, N + 1);
-    } else {
-      fa::set_lds((const void*)fa::mqa_dq_fa_kernel<false>, lds);
-      fa::mqa_dq_fa_kernel<false><<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
-          (const bf16*)q, (const bf16*)o, (const bf16*)dout, lse, (const bf16*)kp, (const bf16*)vp,
-          (bf16*)dq, D, R, NKP, N + 1);
-    }
-    // DV_MQA_EARLY=0: the dk/dv tile loads one step ahead of their store (A/B:
-    // 33.0-33.6 -> 31.6-31.7 us with EARLY, profiles/r04o_mqa_early_ab.txt)
-    static const bool early = !(getenv("DV_MQA_EARLY") && atoi(getenv("DV_MQA_EARLY")) == 0);
+    fa::set_lds((const void*)fa::mqa_dq_fa_kernel, lds);
+    fa::mqa_dq_fa_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
+        (const bf16*)q, (const bf16*)o, (const bf16*)dout, lse, (const bf16*)kp, (const bf16*)vp, (bf16*)dq, D, R,
+        NKP, N + 1);
     const dim3 gkv((NKP / 32 + 3) / 4, S, B);
-    // DV_MQA_TPS=2: two query tiles per wave between barriers (measured slower:
-    // 33.1-33.8 vs 31.3-31.5 us, profiles/r04o_mqa_ph_tps_ab.txt)
-    static const bool tps2 = getenv("DV_MQA_TPS") && atoi(getenv("DV_MQA_TPS")) == 2;
-    if (early && tps2)
-      fa::mqa_dkdv_fa_kernel<true, 2><<<gkv, fa::NW * 64, 0, st>>>(
-          (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP, N + 1, rps, scale);
-    else if (early)
-      fa::mqa_dkdv_fa_kernel<true><<<gkv, fa::NW * 64, 0, st>>>(
-          (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP, N + 1, rps, scale);
-    else
-      fa::mqa_dkdv_fa_kernel<false><<<gkv, fa::NW * 64, 0, st>>>(
-          (const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp, (const bf16*)vp, ws, R, NKP, N + 1, rps, scale);
+    fa::mqa_dkdv_fa_kernel<<<gkv, fa::NW * 64, 0, st>>>((const bf16*)q, (const bf16*)dout, lse, D, (const bf16*)kp,
+                                                        (const bf16*)vp, ws, R, NKP, N + 1, rps, scale);
     DV_REQUIRE(S >= 1 && S <= 16, "split count out of range");
     fa::launch_finish<16>(S, grid_for((long long)B * N * 16), st, ws, B, N, NKP, (bf16*)dkv, lddkv,
                           dnull, accumulate);

@@ -96,13 +96,6 @@ struct ConvFwdArgs {
   // window kernel: output-channel groups the 8 XCDs split into (the other
   // factor of 8 splits the pixel tiles); 0: one channel block per XCD
   int xcd_c;
-  // window kernel, K split in two (KSPL = 2): each tile's two halves hand
-  // their f32 partial sums through ks_part (32 KB per half) and a per-tile
-  // ticket in ks_flag (zero between launches)
-  float* ks_part;
-  int* ks_flag;
-  int* ks_err;   // count of hand-offs whose halves sat on different XCDs (must stay 0)
-  int ks_local;  // 1: XCD-local hand-off (no L2 write-back; blocks b, b + 8 share an L2)
 };
 
 // GroupNorm statistics of a wave's tile, register-light: every lane holds
@@ -1297,7 +1290,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(WgradGArgs p) {
 template <int BMC, int BNK>
 int launch_wgrad_glds(WgradGArgs a, hipStream_t st) {
   const int mt = (a.cout + BMC - 1) / BMC, nt = (a.K + BNK - 1) / BNK;
-  static const long long target = getenv("DV_WGRAD_TARGET") ? atoll(getenv("DV_WGRAD_TARGET")) : 512;
+  constexpr long long target = 512;
   // many K tiles (the 15x15 init conv: K = 1800) make the im2col gather the
   // cost: 4x the workgroups there (measured 244 -> 179 us); a one- or two-tile
   // output keeps 512 (more splits only add same-address atomics: 43 -> 65 us)
@@ -1311,7 +1304,7 @@ int launch_wgrad_glds(WgradGArgs a, hipStream_t st) {
   // (same-address atomic contention); measured at 16 / 32 / 64 / 128 for the
   // cross-attention token reductions (4 x 16384 rows, 32 x 64): 19.9 / 11.6 /
   // 8.5 / 8.7 us -- below 64 the per-block row loop dominates
-  static const int cap = getenv("DV_GEMM_SPLITCAP") ? atoi(getenv("DV_GEMM_SPLITCAP")) : 64;
+  constexpr int cap = 64;
   if (a.batch_pix > 0 && (a.batch_pix + per - 1) / per > cap)
     per = ((a.batch_pix + cap - 1) / cap + 63) / 64 * 64;
   unsigned splits;
@@ -1648,8 +1641,7 @@ int launch_fwd(const ConvFwdArgs<T>& a, hipStream_t st) {
 
 // the 1x1 streaming kernel's shapes (see conv1x1_stream_kernel)
 bool conv1x1_ok(const ConvFwdArgs<bf16>& a, bool split) {
-  static const bool off = getenv("DV_NO_1X1") != nullptr;  // A/B switch
-  return !off && a.ks == 1 && (a.cin == 64 || a.cin == 128) && (!split || a.c0 == 64) &&
+  return a.ks == 1 && (a.cin == 64 || a.cin == 128) && (!split || a.c0 == 64) &&
          (a.cout == 64 || a.cout == 128) && a.gn_sums == nullptr && (a.ldy & 3) == 0 &&
          (a.res == nullptr || (a.ldres & 3) == 0) && (a.ld0 & 7) == 0 && (!split || (a.ld1 & 7) == 0) &&
          a.M * std::max(a.ld0, split ? a.ld1 : 0) < (1ll << 31) &&
@@ -1679,10 +1671,8 @@ int launch_fwd_glds(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   const bool stats = a.gn_sums != nullptr;
 #define DV_GL(NB) (stats ? conv_fwd_glds_kernel<BM, BN, NB, true><<<(unsigned)nb, 256, 0, st>>>(a, tn) \
                          : conv_fwd_glds_kernel<BM, BN, NB, false><<<(unsigned)nb, 256, 0, st>>>(a, tn))
-  // DV_GLDS_RING=deep|mid|2 forces one ring depth (A/B)
-  static const int force = getenv("DV_GLDS_RING") ? (getenv("DV_GLDS_RING")[0] == 'd' ? 3 : getenv("DV_GLDS_RING")[0] == 'm' ? 2 : 1) : 0;
-  if (force == 3 || (!force && nb <= 256)) DV_GL(DEEP);
-  else if (force == 2 || (!force && nb <= 512 && MID >= 3)) DV_GL(MID);
+  if (nb <= 256) DV_GL(DEEP);
+  else if (nb <= 512 && MID >= 3) DV_GL(MID);
   else DV_GL(2);
 #undef DV_GL
   return check_launch("conv_fwd_glds");
@@ -2153,34 +2143,15 @@ __device__ __forceinline__ int fw_pix(int r) {
 // NWV = 8: a 128-pixel x 2*CO-channel tile per workgroup, waves 4-7 on the
 // second channel half (the pixel window is staged once for both halves): for
 // the grids whose CO-channel tiles would run in two rounds on the 256 CUs.
-// KSPL = 2: the 16-channel chunks are split in two halves over two
-// workgroups per tile (grid doubled) for grids whose tiles leave half the
-// CUs idle; the last of the two to finish adds the other's partial sums
-// (written to p.ks_part, agent-scope release / acquire around a per-tile
-// ticket: no spin, the halves may sit on different XCDs) and runs the
-// epilogue.
-// NB > 0: a shallower ring (NB chunk buffers) so that two workgroups share a
-// CU (the K-split 256-tile grids: two waves per SIMD from two workgroups, one
-// hiding the other's LDS-DMA issue)
-// RS: register staging instead of LDS-DMA.  A DMA piece issued among the
-// MFMAs costs the issuing wave 100-185 cycles (MI355X_MICROARCH.md), eight of
-// them per chunk per wave; here each piece is a buffer_load_dwordx4 into
-// VGPRs, written to LDS by a ds_write_b128 two chunks later (two register
-// sets alternate by chunk parity; a 2-deep LDS ring: chunk c read, chunk c+1
-// written).  The compiler's vmcnt tracking orders each store after its load.
-// BAR2: one barrier per two chunks.  Chunk c then refills the buffer of chunk
-// c - 2 (AHEAD = NBUF - 2), which every wave left before the last barrier,
-// and the barrier after an odd chunk waits for the next two chunks
-template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4,
-          int KSPL = 1, int NB = 0, bool RS = false, bool BAR2 = false>
+// (Measured and removed in round 5, see DESIGN.md: a K split over two
+// workgroups per tile, register staging, one barrier per two chunks.)
+template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4>
 __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
-  using G = FwGeom<W, CO, NWV, RS ? 2 : NB>;
+  using G = FwGeom<W, CO, NWV>;
   constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
   constexpr int WPC = G::WPC, NJ = CO / 32, CG = G::CG;
   static_assert(NWV == 4 || (NWV == 8 && !STATS), "the 8-wave tile has no statistics epilogue");
   static_assert(NPW <= 9, "one DMA piece per tap");
-  static_assert(!RS || NBUF == 2, "register staging runs a 2-deep ring");
-  static_assert(!BAR2 || (!RS && NBUF >= 4), "two chunks per barrier need a 4-deep ring");
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
   DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2189,12 +2160,6 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   const int wq = wave & 3, chh = wave >> 2;  // pixel sub-tile, channel half
   const int npx = (int)(p.M / 128), nblk = npx * (p.cout / CG);
   int L = blockIdx.x;
-  int kh = 0;  // K half (KSPL = 2): blocks b and b + 8 (one XCD) take the two halves of tile L
-  if constexpr (KSPL == 2) {
-    kh = (L >> 3) & 1;
-    L = ((L >> 4) << 3) | (L & 7);
-  }
-  const int tile = L;
   int co0;
   long long m0;
   if (p.xcd_c > 0) {
@@ -2209,10 +2174,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     co0 = (L / npx) * CG;
     m0 = (long long)(L % npx) * 128;
   }
-  const int nch_all = p.cin / 16;
-  const int cbeg = KSPL == 2 ? kh * (nch_all / 2) : 0;
-  const int cend = KSPL == 2 ? cbeg + nch_all / 2 : nch_all;
-  const int nch = cend - cbeg;  // chunks of this workgroup
+  const int cbeg = 0, cend = p.cin / 16;
+  const int nch = cend - cbeg;  // 16-channel chunks
   const int HW = p.H * W;
   const int y0 = W == 8 ? 0 : (int)((m0 % HW) / W);        // tile's first image row
   const long long fb = W == 8 ? m0 : m0 - (m0 % HW) + (long long)y0 * W;  // pixel of (y0, 0)
@@ -2257,42 +2220,13 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
 #pragma unroll
     for (int i = 0; i < NPW; ++i) issue1(c, i);
   };
-  constexpr int AHEAD = NBUF - 1 - (BAR2 ? 1 : 0);  // chunks in flight beyond the one being read
-  // RS: piece i of chunk c into / out of registers (chunk c's LDS buffer:
-  // relative chunk index parity)
-  u32x4 stA[RS ? NPW : 1], stB[RS ? NPW : 1];
-  auto ld1 = [&](u32x4& dst, int c, int i) {
-    const int ci0 = c * 16;
-    const int k = min(wave + NWV * i, PIECES - 1);
-    if (k < WPC) dst = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)voff0[i], ci0 * 18, 0);
-    else if (!SPLIT || ci0 < p.c0) dst = __builtin_amdgcn_raw_buffer_load_b128(xr0, (int)voff0[i], ci0 * 2, 0);
-    else dst = __builtin_amdgcn_raw_buffer_load_b128(xr1, (int)voff1[i], (ci0 - p.c0) * 2, 0);
-  };
-  auto st1 = [&](const u32x4& v, int c, int i) {
-    const int k = min(wave + NWV * i, PIECES - 1);
-    *(u32x4*)(smem + ((c - cbeg) & 1) * BUF + k * 1024 + lane * 16) = v;
-  };
-
-  if constexpr (RS) {
-    // prologue: chunk 0 in LDS, chunk 1 in set B, chunk 2 loading into set A
+  constexpr int AHEAD = NBUF - 1;  // chunks in flight beyond the one being read
+  // prologue: chunks cbeg .. cbeg+AHEAD-1 in flight, wait for chunk cbeg
 #pragma unroll
-    for (int i = 0; i < NPW; ++i)
-      if (nch > 0) ld1(stA[i], cbeg, i);
-#pragma unroll
-    for (int i = 0; i < NPW; ++i)
-      if (nch > 1) ld1(stB[i], cbeg + 1, i);
-#pragma unroll
-    for (int i = 0; i < NPW; ++i) {
-      if (nch > 0) st1(stA[i], cbeg, i);
-      if (nch > 2) ld1(stA[i], cbeg + 2, i);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  } else {
-    // prologue: chunks cbeg .. cbeg+AHEAD-1 in flight, wait for chunk cbeg
-#pragma unroll
-    for (int c = 0; c < AHEAD; ++c)
-      if (c < nch) issue(cbeg + c);
-    const int pro = min(AHEAD, nch) - (BAR2 ? 2 : 1);  // younger chunks than chunk 0 (BAR2: and 1)
+  for (int c = 0; c < AHEAD; ++c)
+    if (c < nch) issue(cbeg + c);
+  {
+    const int pro = min(AHEAD, nch) - 1;  // younger chunks than chunk 0
     if (pro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPW) : "memory");
     else if (pro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
     else if (pro == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
@@ -2350,8 +2284,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   // one chunk; PRE (compile-time): chunk c + AHEAD exists and is issued here.
   // The loop is split into the chunks that issue and the AHEAD tail, so the
   // main loop carries no per-piece branch and a constant vmcnt
-  auto chunk = [&](int c, auto PRE, auto PAR) {
-    const char* b = smem + (RS ? ((c - cbeg) & 1) : (c % NBUF)) * BUF;
+  auto chunk = [&](int c, auto PRE) {
+    const char* b = smem + (c % NBUF) * BUF;
     // fragments of tap d + PF are read while tap d multiplies (one wave per
     // SIMD: the LDS latency is hidden by this wave's own MFMAs only)
     constexpr int NS = PF + 1;
@@ -2382,43 +2316,10 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
         acc0 = Mma<bf16>::run(aq0[d % NS], bq[d % NS], acc0);
         if (CO == 64) acc1 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc1);
       }
-      if constexpr (RS) {
-        // chunk c+1 (loaded two chunks ago) into the LDS buffer read in
-        // chunk c-1, then chunk c+3 into the freed registers.  PAR: chunk
-        // parity (relative to cbeg); chunk j sits in set A if j is even
-        if (d < NPW) {
-          u32x4* S = decltype(PAR)::value ? stA : stB;
-          if (decltype(PRE)::value || c + 1 < cend) st1(S[d], c + 1, d);
-          if (decltype(PRE)::value || c + 3 < cend) ld1(S[d], c + 3, d);
-        }
-      } else if (decltype(PRE)::value || (BAR2 && c + AHEAD < cend)) {
-        // (BAR2: the pair loop's tail may still hold the chunk issuing the last)
+      if constexpr (decltype(PRE)::value) {
         if (d < NPW) issue1(c + AHEAD, d);
       }
       __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (BAR2) {
-      // even chunk (relative to cbeg) that is not the last: no barrier; the
-      // last barrier already waited for this chunk's successor
-      if (!decltype(PAR)::value && c + 1 < cend) return;
-      // chunks c+1 and c+2 landed: younger are chunks c+3 .. c+AHEAD
-      if constexpr (decltype(PRE)::value) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((AHEAD - 2) * NPW) : "memory");
-      } else {
-        const int young = min(c + AHEAD, cend - 1) - (c + 2);
-        if (young >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
-        else if (young == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      if (DEFER) defer_wait();
-      __builtin_amdgcn_s_barrier();
-      return;
-    }
-    if constexpr (RS) {
-      // this wave's stores of chunk c+1 done before the barrier
-      defer_wait();
-      __builtin_amdgcn_s_barrier();
-      return;
     }
     // chunk c+1 landed: younger are the pieces of chunks c+2 .. c+AHEAD
     if constexpr (decltype(PRE)::value) {
@@ -2433,95 +2334,11 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     if (DEFER) defer_wait();
     __builtin_amdgcn_s_barrier();
   };
-  using P0 = std::false_type;
-  using P1 = std::true_type;
   int c = cbeg;
-  if constexpr (BAR2) {
-    for (; c + 1 + AHEAD < cend; c += 2) {
-      chunk(c, std::true_type{}, P0{});
-      chunk(c + 1, std::true_type{}, P1{});
-    }
-    for (; c < cend; c += 2) {
-      chunk(c, std::false_type{}, P0{});
-      if (c + 1 < cend) chunk(c + 1, std::false_type{}, P1{});
-    }
-  } else if constexpr (RS) {
-    for (; c + 4 < cend; c += 2) {
-      chunk(c, std::true_type{}, P0{});
-      chunk(c + 1, std::true_type{}, P1{});
-    }
-    for (; c < cend; c += 2) {
-      chunk(c, std::false_type{}, P0{});
-      if (c + 1 < cend) chunk(c + 1, std::false_type{}, P1{});
-    }
-  } else {
-    for (; c + AHEAD < cend; ++c) chunk(c, std::true_type{}, P0{});
-    for (; c < cend; ++c) chunk(c, std::false_type{}, P0{});
-  }
+  for (; c + AHEAD < cend; ++c) chunk(c, std::true_type{});
+  for (; c < cend; ++c) chunk(c, std::false_type{});
   if (DEFER && nch > 0) run_deferred();
   DV_STAMP_AT(2);
-  if constexpr (KSPL == 2) {
-    // hand-off: both halves write their partial (lane-linear, 1 KB per wave
-    // store), release, take a ticket; the second adds the first's partial
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      acc0[e] += acc2[e];
-      if (CO == 64) acc1[e] += acc3[e];
-      acc2[e] = acc3[e] = 0.f;
-    }
-    constexpr int PART = NWV * 2 * 16 * 64;  // floats per half
-    float* mine = p.ks_part + ((long long)tile * 2 + kh) * PART + wave * (2 * 16 * 64);
-#pragma unroll
-    for (int e4 = 0; e4 < 4; ++e4) {
-      *(f32x4*)(mine + e4 * 256 + lane * 4) = f32x4{acc0[4 * e4], acc0[4 * e4 + 1], acc0[4 * e4 + 2], acc0[4 * e4 + 3]};
-      if (CO == 64)
-        *(f32x4*)(mine + 1024 + e4 * 256 + lane * 4) =
-            f32x4{acc1[4 * e4], acc1[4 * e4 + 1], acc1[4 * e4 + 2], acc1[4 * e4 + 3]};
-    }
-    int* tk = (int*)smem;
-    if (p.ks_local) {
-      // XCD-local: round-robin dispatch puts blocks b and b + 8 on one XCD, so
-      // the partner reads this partial from the L2 both share; waiting for the
-      // stores' acknowledgement replaces the agent-scope release (a write-back
-      // of the whole L2, which cost more than the split gained).  The ticket
-      // carries the XCD id: a partner elsewhere is counted in ks_err.
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        int x;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-        x &= 15;
-        const int t = __hip_atomic_fetch_add(p.ks_flag + tile, 1 + (x << 4), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        if (t != 0 && (t >> 4) != x) __hip_atomic_fetch_add(p.ks_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *tk = t;
-      }
-      __syncthreads();
-      if (*tk == 0) return;  // the other half finishes the tile
-      asm volatile("buffer_inv sc0" ::: "memory");  // no stale L1 line of the partner's partial
-    } else {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's stores out of its L2
-      __syncthreads();
-      if (threadIdx.x == 0) *tk = __hip_atomic_fetch_add(p.ks_flag + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      if (*tk == 0) return;  // the other half finishes the tile
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    const float* other = p.ks_part + ((long long)tile * 2 + (kh ^ 1)) * PART + wave * (2 * 16 * 64);
-#pragma unroll
-    for (int e4 = 0; e4 < 4; ++e4) {
-      const f32x4 o0 = *(const f32x4*)(other + e4 * 256 + lane * 4);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) acc0[4 * e4 + k] += o0[k];
-      if (CO == 64) {
-        const f32x4 o1 = *(const f32x4*)(other + 1024 + e4 * 256 + lane * 4);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc1[4 * e4 + k] += o1[k];
-      }
-    }
-    if (threadIdx.x == 0) __hip_atomic_store(p.ks_flag + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();  // the ticket word is LDS the statistics epilogue reuses
-  }
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e.  Bias and
   // residual are loaded for all 8 channel groups BEFORE the first store (vmcnt
   // retires loads and stores in order: a load behind a store waits for the
@@ -2599,13 +2416,10 @@ bool fwd_frame_ok(const ConvFwdArgs<bf16>& a, int h, int w) {
 
 // channel x pixel split of the window conv's tiles over the 8 XCDs that
 // minimises the L2 fill traffic xp * |w| + xc * |x| (each XCD's L2 reads its
-// 1/xc of the weights and 1/xp of the input once); DV_FRAME_XC forces xc
+// 1/xc of the weights and 1/xp of the input once)
 int frame_xcd_split(const ConvFwdArgs<bf16>& a, int co) {
-  static const int forced = getenv("DV_FRAME_XC") ? atoi(getenv("DV_FRAME_XC")) : -1;
   const int ntco = a.cout / co, npx = (int)(a.M / 128);
   auto ok = [&](int xc) { return ntco % xc == 0 && npx % (8 / xc) == 0; };
-  if (forced == 0) return 0;
-  if (forced > 0) return (forced <= 8 && 8 % forced == 0 && ok(forced)) ? forced : 0;
   const double wb = (double)a.cout * a.K, xb = (double)a.M * a.cin;
   int best = 0;
   double bc = 0;
@@ -2617,178 +2431,25 @@ int frame_xcd_split(const ConvFwdArgs<bf16>& a, int co) {
   return best;
 }
 
-// caller-owned scratch of the window conv's K split (dv_conv_scratch), per device
-struct KsScratch {
-  float* part = nullptr;
-  long long bytes = 0;
-  int* flags = nullptr;
-  int nflags = 0;
-};
-KsScratch g_ks[64];
-
-KsScratch* ks_scratch() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  return g_ks[dev].part ? &g_ks[dev] : nullptr;
-}
-
 int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   ConvFwdArgs<bf16> a = a0;
   const int tiles64 = (int)(a.M / 128) * (a.cout / 64);
-  // grids of <= 128 64-channel tiles (half the CUs): the chunk loop split in
-  // two workgroups per tile (KSPL = 2) when the caller registered scratch
-  // (DV_FRAME_KSPLIT=0: off); otherwise 32-channel tiles (DV_FRAME_CO32=0: off)
-  // opt-in: measured 104.0 -> 100.6 steps/s (gpurun_out/ks_r04a): the agent-scope release of
-  // the partial (an L2 write-back) costs more than the idle CUs it fills; the XCD-local
-  // hand-off (=2) removes that cost and still loses per launch to the 32-channel tiles
-  // (13.7 vs 11.1 us, 16.3 vs 13.2 us with statistics; step 102.8 vs 102.9,
-  // profiles/r04f_ksplit_xcd_local_ab.txt)
-  static const bool ks_ok = getenv("DV_FRAME_KSPLIT") && atoi(getenv("DV_FRAME_KSPLIT")) != 0;
-  // DV_FRAME_KSPLIT=2: the XCD-local hand-off (no agent-scope release)
-  static const int ks_local = ks_ok && atoi(getenv("DV_FRAME_KSPLIT")) == 2 ? 1 : 0;
-  // DV_FRAME_KS256=1: also split the 256-tile grids, two workgroups per CU on
-  // a 2-deep ring (A/B)
-  static const bool ks256 = getenv("DV_FRAME_KS256") && atoi(getenv("DV_FRAME_KS256")) != 0;
-  // DV_FRAME_W8KS=1 (with DV_FRAME_KSPLIT=1 / 2): the 8x8 grids of 256 64-channel
-  // tiles as 128 tiles of 128 channels (8 waves, the window staged once for both
-  // channel halves: 0.35 instead of 0.43 KB of LDS-DMA per MFMA) with the chunk
-  // loop split over two workgroups (256 workgroups); no statistics epilogue
-  static const bool w8ks = getenv("DV_FRAME_W8KS") && atoi(getenv("DV_FRAME_W8KS")) != 0;
-  if (ks_ok && w8ks && a.W == 8 && !a.gn_sums && a.cout % 128 == 0 && tiles64 == 256 &&
-      (a.cin / 16) % 2 == 0) {
-    KsScratch* ks = ks_scratch();
-    const int tiles128 = tiles64 / 2;
-    if (ks && ks->nflags > tiles128 && ks->bytes >= (long long)tiles128 * 2 * 8 * 2 * 16 * 64 * 4) {
-      a.ks_part = ks->part;
-      a.ks_flag = ks->flags;
-      a.ks_err = ks->flags + ks->nflags - 1;
-      a.ks_local = ks_local;
-      a.xcd_c = frame_xcd_split(a, 128);
-      const int nb2 = 2 * tiles128;
-      if (a.c0 < a.cin) conv_fwd_frame_kernel<8, false, 3, 1, 64, true, 8, 2><<<nb2, 512, 0, st>>>(a);
-      else conv_fwd_frame_kernel<8, false, 3, 1, 64, false, 8, 2><<<nb2, 512, 0, st>>>(a);
-      return check_launch("conv_fwd_frame");
-    }
-  }
-  if (ks_ok && ks256 && tiles64 == 256 && a.W == 8 && (a.cin / 16) % 2 == 0) {
-    KsScratch* ks = ks_scratch();
-    if (ks && ks->nflags > tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {
-      a.ks_part = ks->part;
-      a.ks_flag = ks->flags;
-      a.ks_err = ks->flags + ks->nflags - 1;
-      a.ks_local = ks_local;
-      a.xcd_c = frame_xcd_split(a, 64);
-      const int nb2 = 2 * tiles64;
-      if (a.c0 < a.cin)
-        a.gn_sums ? conv_fwd_frame_kernel<8, true, 3, 1, 64, true, 4, 2, 2><<<nb2, 256, 0, st>>>(a)
-                  : conv_fwd_frame_kernel<8, false, 3, 1, 64, true, 4, 2, 2><<<nb2, 256, 0, st>>>(a);
-      else
-        a.gn_sums ? conv_fwd_frame_kernel<8, true, 3, 1, 64, false, 4, 2, 2><<<nb2, 256, 0, st>>>(a)
-                  : conv_fwd_frame_kernel<8, false, 3, 1, 64, false, 4, 2, 2><<<nb2, 256, 0, st>>>(a);
-      return check_launch("conv_fwd_frame");
-    }
-  }
-  if (ks_ok && tiles64 <= 128 && tiles64 % 8 == 0 && (a.cin / 16) % 2 == 0) {
-    KsScratch* ks = ks_scratch();
-    if (ks && ks->nflags > tiles64 && ks->bytes >= (long long)tiles64 * 2 * 4 * 2 * 16 * 64 * 4) {
-      a.ks_part = ks->part;
-      a.ks_flag = ks->flags;
-      a.ks_err = ks->flags + ks->nflags - 1;
-      a.ks_local = ks_local;
-      a.xcd_c = frame_xcd_split(a, 64);
-      const int nb2 = 2 * tiles64;
-#define DV_FK(WW, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, 64, SP, 4, 2><<<nb2, 256, 0, st>>>(a) \
-                              : conv_fwd_frame_kernel<WW, false, 3, 1, 64, SP, 4, 2><<<nb2, 256, 0, st>>>(a))
-#define DV_FK2(WW) (a.c0 < a.cin ? DV_FK(WW, true) : DV_FK(WW, false))
-      switch (a.W) {
-        case 8: DV_FK2(8); break;
-        case 16: DV_FK2(16); break;
-        case 32: DV_FK2(32); break;
-        default: DV_FK2(64); break;
-      }
-#undef DV_FK2
-#undef DV_FK
-      return check_launch("conv_fwd_frame");
-    }
-  }
-  static const bool co32_ok = !(getenv("DV_FRAME_CO32") && atoi(getenv("DV_FRAME_CO32")) == 0);
-  // DV_FRAME_CO32R=1: 32-channel tiles also where the 64-channel grid ends in a
-  // half-empty round (384 tiles = 1.5 rounds: the 8x8 dgrad 768 -> 512)
-  static const bool co32r = getenv("DV_FRAME_CO32R") && atoi(getenv("DV_FRAME_CO32R")) != 0;
-  const bool ragged = co32r && tiles64 > 256 && tiles64 % 256 != 0 && tiles64 % 256 <= 128;
-  const int co = co32_ok && (tiles64 <= 128 || ragged) ? 32 : 64;
+  // grids of <= 128 64-channel tiles (half the CUs): 32-channel tiles
+  const int co = tiles64 <= 128 ? 32 : 64;
   // 8 waves on 128 channels for the 16-wide frames whose 64-channel tiles
-  // would take two rounds of the 256 CUs (DV_FRAME_W8=0: off)
-  static const bool w8_ok = !(getenv("DV_FRAME_W8") && atoi(getenv("DV_FRAME_W8")) == 0);
-  // (with DV_FRAME_CO32R: not where the 128-channel grid is ragged but the
-  // 64-channel one is whole rounds: 384 vs 768 workgroups at 16x16 x 384)
-  const bool w8_ragged = co32r && tiles64 % 256 == 0 && (tiles64 / 2) % 256 != 0;
-  const bool w8 = w8_ok && a.W == 16 && co == 64 && !a.gn_sums && a.cout % 128 == 0 &&
-                  (a.M / 128) * (a.cout / 64) > 256 && !w8_ragged;
+  // would take two rounds of the 256 CUs
+  const bool w8 = a.W == 16 && co == 64 && !a.gn_sums && a.cout % 128 == 0 && (a.M / 128) * (a.cout / 64) > 256;
   a.xcd_c = frame_xcd_split(a, w8 ? 128 : co);
   const int nblk = (int)(a.M / 128) * (a.cout / (w8 ? 128 : co));
-  // DV_FRAME_RS=1: register staging instead of LDS-DMA (A/B)
-  static const bool rs = getenv("DV_FRAME_RS") && atoi(getenv("DV_FRAME_RS")) != 0;
   if (w8) {
-    if (rs) {
-      if (a.c0 < a.cin) conv_fwd_frame_kernel<16, false, 3, 1, 64, true, 8, 1, 0, true><<<nblk, 512, 0, st>>>(a);
-      else conv_fwd_frame_kernel<16, false, 3, 1, 64, false, 8, 1, 0, true><<<nblk, 512, 0, st>>>(a);
-    } else {
-      if (a.c0 < a.cin) conv_fwd_frame_kernel<16, false, 3, 1, 64, true, 8><<<nblk, 512, 0, st>>>(a);
-      else conv_fwd_frame_kernel<16, false, 3, 1, 64, false, 8><<<nblk, 512, 0, st>>>(a);
-    }
-    return check_launch("conv_fwd_frame");
-  }
-  // DV_FRAME_DEFER2=1: the last two taps' MFMAs of a chunk run behind its barrier (A/B)
-  static const bool defer2 = getenv("DV_FRAME_DEFER2") && atoi(getenv("DV_FRAME_DEFER2")) != 0;
-  if (defer2) {
-    switch (a.W) {
-#define DV_FD5(WW, C, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 2, C, SP><<<nblk, 256, 0, st>>>(a) \
-                                 : conv_fwd_frame_kernel<WW, false, 3, 2, C, SP><<<nblk, 256, 0, st>>>(a))
-#define DV_FD4(WW, C) (a.c0 < a.cin ? DV_FD5(WW, C, true) : DV_FD5(WW, C, false))
-#define DV_FD(WW) (co == 32 ? DV_FD4(WW, 32) : DV_FD4(WW, 64))
-      case 8: DV_FD(8); break;
-      case 16: DV_FD(16); break;
-      case 32: DV_FD(32); break;
-      default: DV_FD(64); break;
-#undef DV_FD
-#undef DV_FD4
-#undef DV_FD5
-    }
-    return check_launch("conv_fwd_frame");
-  }
-  // DV_FRAME_BAR2=1: one barrier per two chunks (A/B; rings of >= 4 buffers)
-  static const bool bar2 = getenv("DV_FRAME_BAR2") && atoi(getenv("DV_FRAME_BAR2")) != 0;
-  if (bar2 && a.W == 8) {
-#define DV_FB5(C, SP) (a.gn_sums ? conv_fwd_frame_kernel<8, true, 3, 1, C, SP, 4, 1, 0, false, true><<<nblk, 256, 0, st>>>(a) \
-                             : conv_fwd_frame_kernel<8, false, 3, 1, C, SP, 4, 1, 0, false, true><<<nblk, 256, 0, st>>>(a))
-#define DV_FB4(C) (a.c0 < a.cin ? DV_FB5(C, true) : DV_FB5(C, false))
-    if (co == 32) DV_FB4(32);
-    else DV_FB4(64);
-#undef DV_FB4
-#undef DV_FB5
-    return check_launch("conv_fwd_frame");
-  }
-  if (rs) {
-    switch (a.W) {
-#define DV_FR5(WW, C, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, C, SP, 4, 1, 0, true><<<nblk, 256, 0, st>>>(a) \
-                                 : conv_fwd_frame_kernel<WW, false, 3, 1, C, SP, 4, 1, 0, true><<<nblk, 256, 0, st>>>(a))
-#define DV_FR4(WW, C) (a.c0 < a.cin ? DV_FR5(WW, C, true) : DV_FR5(WW, C, false))
-#define DV_FR(WW) (co == 32 ? DV_FR4(WW, 32) : DV_FR4(WW, 64))
-      case 8: DV_FR(8); break;
-      case 16: DV_FR(16); break;
-      case 32: DV_FR(32); break;
-      default: DV_FR(64); break;
-#undef DV_FR
-#undef DV_FR4
-#undef DV_FR5
-    }
+    if (a.c0 < a.cin) conv_fwd_frame_kernel<16, false, 3, 1, 64, true, 8><<<nblk, 512, 0, st>>>(a);
+    else conv_fwd_frame_kernel<16, false, 3, 1, 64, false, 8><<<nblk, 512, 0, st>>>(a);
     return check_launch("conv_fwd_frame");
   }
   // fragment prefetch distance PF = 3 taps and DEFER (the last tap's MFMAs
   // after the chunk barrier): same-box per-launch A/B (tools/frame_ab.py,
   // profiles/r03_frame_ab.txt) put PF 3 + DEFER 1 1-3 % ahead of PF 2 without
-  // the deferral; the template keeps both knobs
+  // the deferral
   switch (a.W) {
 #define DV_FW5(WW, C, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, C, SP><<<nblk, 256, 0, st>>>(a) \
                                  : conv_fwd_frame_kernel<WW, false, 3, 1, C, SP><<<nblk, 256, 0, st>>>(a))
@@ -2808,10 +2469,9 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
 
 // tile choice for the glds path (mirrored by ops.conv_tile for kernel naming)
 inline void glds_tile(long long M, int cout, int K, int& bm, int& bn) {
-  // DV_GLDS_BN64R=1: 64-channel tiles where 128-channel ones leave a half-empty
-  // column (cout = 192: the 32x32 up-path concat dgrad computed 256 channels)
-  static const bool bn64r = getenv("DV_GLDS_BN64R") && atoi(getenv("DV_GLDS_BN64R")) != 0;
-  bn = cout <= 64 || (bn64r && cout % 128 == 64) ? 64 : 128;
+  // (64-channel tiles where 128-channel ones leave a half-empty column, cout =
+  // 192, measured slower: profiles/r04k_ragged_tiles_ab.txt)
+  bn = cout <= 64 ? 64 : 128;
   bm = bn == 64 ? 256 : 128;
   if (((M + bm - 1) / bm) * ((cout + bn - 1) / bn) < 512) bm = 128;
   // fewer 128-pixel tiles than CUs (8x8 stage, mid block): halve the pixel tile
@@ -2849,9 +2509,7 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
         (res == nullptr || (ldres & 3) == 0) && (!gn_sums || gn_P % 128 == 0))
       return launch_fwd_stripe(a, st);
     int seg, nseg;
-    static const bool no_s2 = getenv("DV_NO_STRIPE2") != nullptr;  // A/B switch for profiling
-    if (!no_s2 &&
-        fwd_stripe2_ok(a.M, h, wd, cin, a.c0, x1 != nullptr, cout, ks, seg, nseg) &&
+    if (fwd_stripe2_ok(a.M, h, wd, cin, a.c0, x1 != nullptr, cout, ks, seg, nseg) &&
         a.M * std::max(ld0, x1 ? ld1 : 0) < (1ll << 31))
       return launch_fwd_stripe2(a, seg, nseg, st);
     if (conv1x1_ok(a, x1 != nullptr)) {
@@ -3742,7 +3400,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_batched_kernel(const DvWgrad
 
 // split groups per workgroup: each lane keeps >= 4 splits (4 loads in flight)
 inline int reduce4_groups(int S) {
-  static const int gmax = getenv("DV_RED_G") ? atoi(getenv("DV_RED_G")) : 8;
+  constexpr int gmax = 8;
   int G = 1;
   while (G * 2 <= gmax && G * 8 <= S) G *= 2;
   return G;
@@ -3832,10 +3490,8 @@ bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout
 // slower on every Cfg2 shape (tools/ab_fwd.sh): occupancy wins.
 inline void stripe_split(int nstages, int grid_xy, long long grad_floats, int ks, int& sps, int& S) {
   (void)grad_floats;
-  static const int minst = getenv("DV_WG_MINST") ? atoi(getenv("DV_WG_MINST")) : 1;  // A/B knob
   // 1x1 with the 2-deep ring: two workgroups per CU
   long long want = (ks == 1 && DV_WG1_NBUF == 2 ? 512 : 256) / grid_xy;
-  if (minst > 1 && want > nstages / minst) want = nstages / minst;
   if (want > nstages) want = nstages;
   if (want < 1) want = 1;
   sps = (int)((nstages + want - 1) / want);
@@ -3843,11 +3499,8 @@ inline void stripe_split(int nstages, int grid_xy, long long grad_floats, int ks
 }
 
 // split-K partials in bf16 (halves their write and the sum's read; the sum
-// and the gradient stay f32).  DV_WG_F32PART=1 keeps f32 partials (A/B).
-inline bool stripe_part_bf16() {
-  static const bool f32 = getenv("DV_WG_F32PART") && atoi(getenv("DV_WG_F32PART"));
-  return !f32;
-}
+// and the gradient stay f32)
+inline bool stripe_part_bf16() { return true; }
 
 long long wgrad_stripe_ws(int nf, int h, int w, int cin, int cout, int ks) {
   const int nstages = (int)((long long)nf * h * w / 128);
@@ -3951,17 +3604,6 @@ extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const voi
     return conv_fwd_t<bf16>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, y, ldy, nf, h, w,
                             cin, cout, ksize, act, gn_sums, gn_P, gn_R, st);
   DV_REQUIRE(false, "unknown dtype");
-}
-
-extern "C" int dv_conv_scratch(void* part, long long bytes, int* flags, int nflags) {
-  DV_REQUIRE((part && flags && bytes > 0 && nflags > 0) || (!part && !flags), "bad scratch");
-  int dev = 0;
-  DV_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "no current device");
-  g_ks[dev].part = (float*)part;
-  g_ks[dev].bytes = part ? bytes : 0;
-  g_ks[dev].flags = flags;
-  g_ks[dev].nflags = flags ? nflags : 0;
-  return DV_OK;
 }
 
 extern "C" int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,

@@ -676,8 +676,7 @@ extern "C" int dv_conv_fwd_mx8(const void* q0, const void* s0, int c0, const voi
   a.y = (bf16*)y; a.ldy = ldy; a.H = h; a.cin = cin; a.cout = cout; a.M = M;
   hipStream_t st = (hipStream_t)stream;
   // the persistent resident-weight form for the wide frames with <= 2 chunks
-  static const bool no_p = getenv("DV_MX8_NO_PERSIST") != nullptr;  // A/B switch
-  if (!no_p && !res && (w == 64 || w == 128) && cin <= 128) {
+  if (!res && (w == 64 || w == 128) && cin <= 128) {
     if (w == 128) return cin == 64 ? launch_mx8p<128, 1>(a, st) : launch_mx8p<128, 2>(a, st);
     return cin == 64 ? launch_mx8p<64, 1>(a, st) : launch_mx8p<64, 2>(a, st);
   }

@@ -842,17 +842,12 @@ int grid_for(long long work, int per_block = 256) {
 
 // rows per workgroup: a multiple of one unrolled pass (rpp * U), sized for
 // about `target` workgroups over the whole call
-// DV_GN_MINB (A/B knob, default off): a floor on the bytes of z each
-// workgroup streams.  Measured on the whole step (tools/gn_ab.sh): 32 KiB
-// 78.9, 64 KiB 76.7-78.2, 128 KiB 74.3 vs 79.2 steps/s without — the small
-// 8x8 / 16x16 calls want the parallelism more than fewer prologues.
+// (A floor on the bytes each workgroup streams measured slower on the whole
+// step, 74.3-78.9 vs 79.2 steps/s: the small 8x8 / 16x16 calls want the
+// parallelism more than fewer prologues.)
 long long gn_rows(const GnArgs& a, int vec, int u, long long target) {
-  static const long long min_bytes = getenv("DV_GN_MINB") ? atoll(getenv("DV_GN_MINB")) : 0;
   const long long pass = (long long)(256 / (a.C / vec)) * u;
   long long r = (a.P * a.nb + target - 1) / target;
-  const long long row_bytes = (long long)a.C * (16 / vec);
-  const long long rmin = min_bytes > 0 ? (min_bytes + row_bytes - 1) / row_bytes : 0;
-  if (r < rmin) r = rmin;
   r = (r + pass - 1) / pass * pass;
   return r < pass ? pass : r;
 }
@@ -861,32 +856,21 @@ long long gn_rows(const GnArgs& a, int vec, int u, long long target) {
 // (a clip's reduce blocks all add into its C sums), no more -- every apply
 // workgroup reads all R replicas in its prologue
 int gn_replicas(const GnArgs& a, int blocks_per_clip) {
-  static const int fixed = getenv("DV_GN_R") ? atoi(getenv("DV_GN_R")) : 0;  // A/B switch
-  int r = fixed > 0 ? fixed : (blocks_per_clip + 15) / 16;
+  int r = (blocks_per_clip + 15) / 16;
   r = std::min(r, 8);
   if (a.R < r) r = a.R;  // the caller's buffer holds a.R replicas
   return std::max(r, 1);
 }
 
-// Launch shape knobs (A/B switches, read once): unroll depth U (pixel rows
+// Launch shape (measured, tools/gn_*_sweep.sh): unroll depth U (pixel rows
 // in flight per lane) and the workgroup-count target of each pass.
 struct GnTune {
   int ur0, ua0, ur1, ua1;   // U: fwd reduce / fwd apply / bwd reduce / bwd apply
   long long tr0, ta0, tr1, ta1;
 };
 const GnTune& gn_tune() {
-  static const GnTune t = [] {
-    auto env = [](const char* n, long long d) {
-      const char* v = getenv(n);
-      return v && atoll(v) > 0 ? atoll(v) : d;
-    };
-    GnTune g;
-    g.ur0 = (int)env("DV_GN_UR0", 2 * GN_U); g.ua0 = (int)env("DV_GN_UA0", GN_U);
-    g.ur1 = (int)env("DV_GN_UR1", GN_U);     g.ua1 = (int)env("DV_GN_UA1", 2);
-    g.tr0 = env("DV_GN_TR0", 768);  g.ta0 = env("DV_GN_TA0", 512);  // ta0: 1024 before the register prologue
-    g.tr1 = env("DV_GN_TR1", 768);  g.ta1 = env("DV_GN_TA1", 768);
-    return g;
-  }();
+  // ta0: 1024 before the register prologue
+  static const GnTune t{2 * GN_U, GN_U, GN_U, 2, 768, 512, 768, 768};
   return t;
 }
 
@@ -897,9 +881,8 @@ void gn_reduce_launch(GnArgs& a, int u, long long target, hipStream_t st) {
   dim3 g((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   a.R = gn_replicas(a, (int)g.x);
   const bool silu = a.act == DV_ACT_SILU;
-  // A/B: DV_GN_DIRECT bit 2 (default on): the backward reduce's register prologue
-  static const int dflag = getenv("DV_GN_DIRECT") ? atoi(getenv("DV_GN_DIRECT")) : 5;
-  const bool dir = MODE == 1 && (dflag & 4) && (a.C / a.G) % VEC == 0;
+  // the backward reduce's register prologue
+  const bool dir = MODE == 1 && (a.C / a.G) % VEC == 0;
 #define DV_GN_RED2(UU, D) (silu ? gn_reduce_kernel<T, MODE, UU, true, D><<<g, 256, 0, st>>>(a) \
                                 : gn_reduce_kernel<T, MODE, UU, false, D><<<g, 256, 0, st>>>(a))
 #define DV_GN_RED(UU) (dir ? DV_GN_RED2(UU, true) : DV_GN_RED2(UU, false))
@@ -926,15 +909,13 @@ void gn_apply_go(const GnArgs& a, dim3 g, hipStream_t st) {
 template <typename T, int MODE>
 void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
   const int VEC = 16 / sizeof(T);
-  static const int exp = getenv("DV_GN_EXP") ? atoi(getenv("DV_GN_EXP")) : 0;
-  a.exp = exp;
+  a.exp = 0;
   a.rows_per_block = gn_rows(a, VEC, u, target);
   dim3 g((unsigned)((a.P + a.rows_per_block - 1) / a.rows_per_block), a.nb);
   const bool silu = a.act == DV_ACT_SILU;
   const bool res = MODE == 0 && a.res != nullptr;
-  // A/B: DV_GN_DIRECT bit 0 forward, bit 1 backward apply (register prologue; else LDS)
-  static const int dflag = getenv("DV_GN_DIRECT") ? atoi(getenv("DV_GN_DIRECT")) : 5;
-  const int dq = sizeof(T) == 2 && (dflag >> MODE & 1) && gn_direct_ok(a, VEC) ? gn_direct_dq(a, VEC) : 0;
+  // the forward apply's register prologue (the backward apply's measured equal: LDS)
+  const int dq = sizeof(T) == 2 && MODE == 0 && gn_direct_ok(a, VEC) ? gn_direct_dq(a, VEC) : 0;
 #define DV_GN_APP2(UU, D)                                                 \
   (silu ? (res ? gn_apply_go<T, MODE, UU, true, true, D>(a, g, st)         \
                : gn_apply_go<T, MODE, UU, true, false, D>(a, g, st))       \

@@ -1043,19 +1043,14 @@ extern "C" int dv_xattn_fold(int dtype, const float* wq, const float* wo, const 
   return fold_t<float>(wq, wo, kv, null_kv, g1, at, vt, Kt, KtT, Vt, VtT, colsum, nb, C, scale, st);
 }
 
-// channel-split threshold (A/B knob DV_XA_SPLIT_TILES): token tiles below it
-// run 4 waves per tile
-static long long xa_split_tiles() {
-  static const long long v = getenv("DV_XA_SPLIT_TILES") ? atoll(getenv("DV_XA_SPLIT_TILES")) : 1024;
-  return v;
-}
+// channel-split threshold: token tiles below it run 4 waves per tile
+static long long xa_split_tiles() { return 1024; }
 // 8 waves per tile (512-thread workgroups) for the grids of <= 256 tiles whose
 // channels split 8 ways (the 8x8 stage at 256 / 512 channels: each wave's serial
-// channel chain halves; DV_XA_CS8=0: 4 waves)
+// channel chain halves)
 static int xa_cs(long long tiles, int C, bool split) {
-  static const bool cs8 = !(getenv("DV_XA_CS8") && atoi(getenv("DV_XA_CS8")) == 0);
   if (!split) return 1;
-  return cs8 && tiles <= 256 && C % 256 == 0 ? 8 : 4;
+  return tiles <= 256 && C % 256 == 0 ? 8 : 4;
 }
 
 // unrolled channel-loop trips: 32-channel tiles per wave (0 if above 8)

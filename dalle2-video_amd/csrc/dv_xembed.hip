@@ -155,11 +155,9 @@ __global__ __launch_bounds__(256) void xe_pack_kernel(DvCrossEmbed ce, XeGeom g,
 // D[co][px]: lane holds pixel (l & 15), channels 4 (l >> 4) .. +3 -> one
 // 8-byte store per lane per tile and pixel block.
 // ---------------------------------------------------------------------------
-// rows per forward workgroup; DV_XE_R / DV_XE_WB: A/B knobs (rows, columns)
-int xe_r() {
-  static const int r = getenv("DV_XE_R") ? std::max(1, atoi(getenv("DV_XE_R"))) : 8;
-  return r;
-}
+// rows per forward workgroup (the tile knobs measured flat within +-5 %,
+// profiles/r02_u_unet2_knob_sweep.txt)
+int xe_r() { return 8; }
 
 template <int CP>
 __global__ __launch_bounds__(512) void xe_fwd_kernel(XeGeom g, const bf16* img, const bf16* x,
@@ -548,8 +546,6 @@ long long xe_total_grads(const XeGeom& g) {
 }
 
 int xe_fwd_wb(int w) {
-  static const int forced = getenv("DV_XE_WB") ? atoi(getenv("DV_XE_WB")) : 0;
-  if (forced >= 32 && forced % 32 == 0 && w % forced == 0) return forced;
   return w % 64 == 0 ? 64 : 32;
 }
 

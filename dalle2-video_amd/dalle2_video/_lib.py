@@ -28,7 +28,6 @@ _SIGS = {
     "dv_zero_f32": [_P, _L, _P],
     "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I,
                     _P, _L, _I, _P],
-    "dv_conv_scratch": [_P, _L, _P, _I],
     "dv_conv_fwd8": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
                      _P, _L, _I, _P],
     "dv_mx8_quant": [_P, _I, _I, _L, _P, _P, _P],

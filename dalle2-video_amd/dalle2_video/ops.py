@@ -94,7 +94,7 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0):
             and (w == 8 or (w == 16 and cin * cout <= 256 * 256))):
         return f"conv_fwd_stripe2_kernel<{w}>"
     if (dtype_name == "bf16" and ks == 1 and cin in (64, 128) and c0 in (cin, 64) and cout in (64, 128)
-            and gn_P == 0 and m * maxld < (1 << 31) and not _NO_1X1):
+            and gn_P == 0 and m * maxld < (1 << 31)):
         return f"conv1x1_stream_kernel<{cout},{cin // 64}>"
     if dtype_name == "bf16" and cin % 64 == 0 and c0 % 64 == 0 and m * maxld < (1 << 31):
         bn = 64 if cout <= 64 else 128
@@ -112,7 +112,6 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0):
     return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"
 
 
-_NO_1X1 = bool(os.environ.get("DV_NO_1X1"))  # A/B switch: 1x1 convs on the glds kernel
 # A/B switch: the cross-attention token reductions as three launches, not one
 _NO_GEMM_MULTI = os.environ.get("DV_NO_GEMM_MULTI", "0") not in ("", "0")
 _NO_WINDOW = bool(os.environ.get("DV_NO_WINDOW"))  # A/B switch: 3x3 convs on dv_conv_fwd only
@@ -209,20 +208,6 @@ def _grad_out(p, zero=False):
 
 
 _WS = {}
-_KS_SCRATCH = {}
-
-
-def _conv_scratch(device):
-    """The window conv's K-split hand-off scratch (dv_conv_scratch), registered
-    once per device before its first launch (so a captured graph replays on
-    the same addresses): 16 MB of f32 partials, 1,024 zeroed tile tickets."""
-    key = str(device)
-    if key not in _KS_SCRATCH:
-        part = torch.empty(4 << 20, dtype=torch.float32, device=device)
-        flags = torch.zeros(1024, dtype=torch.int32, device=device)
-        call("dv_conv_scratch", ptr(part), part.numel() * 4, ptr(flags), flags.numel())
-        _KS_SCRATCH[key] = (part, flags)
-    return _KS_SCRATCH[key]
 
 
 def _wgrad_workspace(dname, nf, h, w, cin, c0, split, cout, ks, device):
@@ -913,7 +898,6 @@ class ConvFn(torch.autograd.Function):
                                  ldr, ptr(y), cout, nf, h, w, cin_real, cout, ksize, stream()), shape)
         elif use_win:
             wp = pack_conv_weight(weight, x0.dtype, cin, 2, cache)
-            _conv_scratch(x0.device)
             _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                     lambda: call("dv_conv_fwd8", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp),
                                  ptr(b), ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ACT_NONE,
@@ -967,7 +951,6 @@ class ConvFn(torch.autograd.Function):
             shape = ("dgrad", m, cin_real, cout8 * ksize * ksize)
             if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, ldx, rld, ksize, h, w, nf):
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 3, ctx.cache)
-                _conv_scratch(dy8.device)
                 _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                         lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd),
                                      None, rp, rld, ptr(dx), ldx, nf, h, w, cout8, cin_real, ACT_NONE,

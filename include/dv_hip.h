@@ -156,16 +156,6 @@ int dv_conv_small_fwd(const void* x0, int ld0, int c0, const void* x1, int ld1, 
                       const void* res, int ldres, void* y, int ldy, int nf, int h, int w, int cin,
                       int cout, int ksize, void* stream);
 
-/* Caller-owned scratch of the window conv (dv_conv_fwd8) for the CURRENT
- * device, registered once before its first launch: grids of <= 128 64-channel
- * tiles split the chunk loop over two workgroups per tile, which hand their
- * f32 partial sums through `part` (64 KB per tile) and a per-tile ticket in
- * `flags` (zeroed by the caller at registration; the kernel leaves them zero;
- * the LAST flag counts XCD-local hand-offs whose halves ran on different XCDs,
- * DV_FRAME_KSPLIT=2, and must stay 0).  The split is opt-in (DV_FRAME_KSPLIT).
- * Launches using it must be ordered (one stream).  part = flags = NULL
- * unregisters (no K split).                                                */
-int dv_conv_scratch(void* part, long long bytes, int* flags, int nflags);
 /* 3x3 forward / dgrad, window form (dalle2_video.py:107 Block3D.project at
  * the 8x8 .. 64x64 stages, and the dgrads of those convs): same contract as
  * dv_conv_fwd with ksize = 3, but `wpack` is the 16-channel-chunk-major

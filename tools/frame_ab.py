@@ -41,7 +41,6 @@ def bench(nf, h, w, cin, cout, iters=50):
 
 
 tag = sys.argv[1] if len(sys.argv) > 1 else ""
-ops._conv_scratch(torch.device("cuda", torch.cuda.current_device()))  # the K-split hand-off scratch, as ops.conv registers it
 for shp in SHAPES:
     t, tf, err = bench(*shp)
     print(f"{tag:10s} {str(shp):26s} {t:7.2f} us  {tf:6.1f} TF/s  {tf / 2516.6:.3f}  err {err:.1e}", flush=True)

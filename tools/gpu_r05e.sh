@@ -1,11 +1,11 @@
 #!/bin/bash
+# round-5 check: full GPU suite on the cleaned library, the window wgrad A/B
+# (DV_WG_ISS 0 / 2, the stripe kernel DV_WG_OLD=1), and the step A/B
 export TMPDIR=/tmp
-tag=r05e
+tag=${1:-r05e}
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py tests/test_ops_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_tests.log; exit 1; }
-tail -1 gpurun_out/${tag}_tests.log
-DV_WG_ISS=2 timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests2.log 2>&1 || { tail -30 gpurun_out/${tag}_tests2.log; exit 1; }
-tail -1 gpurun_out/${tag}_tests2.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_tests.log; exit 1; }
+tail -2 gpurun_out/${tag}_tests.log
 for rep in 1 2; do
   for v in 0 2; do
     DV_WG_ISS=$v timeout -k 10 120 python tools/wgrad_ab.py 2>/dev/null | sed "s/^/ISS=$v /" >> gpurun_out/${tag}_wg.log || exit 1
