@@ -2617,34 +2617,6 @@ struct WgradSArgs {
   int acc_w, acc_b, part_bf16;
   int H, cin, cout, K;
   int nstages, stages_per_split;
-  int seg, nseg;  // image rows per window segment, segments per stage
-  int xcd;        // window kernel: deal (split, co, ci) tiles to XCDs in contiguous chunks
-};
-
-#ifndef DV_WG1_NBUF
-#define DV_WG1_NBUF 2
-#endif
-// TRIM: where the window image rounded up to whole 128-row DMA rounds leaves
-// room for only two stages (W = 64: 264 rows in 384), allocate the rows a
-// wave's 16-row piece can reach (272) and send the pieces past them to a 1 KB
-// junk line (zeros, no memory access): three stages fit, two in flight
-template <int W, int KS, bool TRIMOK = false> struct StripeGeom {
-  static constexpr int WP = W + 2;
-  // window rows (max over H): KS == 1 stages the 128 pixels themselves
-  static constexpr int WR = KS == 1 ? 128 : (W == 8 ? 200 : (128 / W + 2) * WP);
-  static constexpr int NRH = (WR + 127) / 128;                  // 128-row DMA rounds per half
-  static constexpr int AIMG = 2 * 128 * 64;                     // dY image: 2 co halves x 128 rows x 64 B
-  static constexpr int WRA = (WR + 15) / 16 * 16;               // rows a 16-row piece reaches
-  static constexpr bool TRIM = TRIMOK && KS == 3 && (AIMG + 2 * NRH * 128 * 64) * 3 > 160 * 1024 &&
-                               (AIMG + 2 * WRA * 64) * 3 + 1024 <= 160 * 1024;
-  static constexpr int BHALF = (TRIM ? WRA : NRH * 128) * 64;   // window image of one ci half
-  static constexpr int STG = AIMG + 2 * BHALF;
-  static constexpr int JUNK = TRIM ? 1024 : 0;                  // after the ring
-  // 1x1: a 2-deep ring (64 KB) so that two workgroups share a CU -- a stage
-  // holds one tap's MFMAs only, too little to cover the next stage's DMA
-  // latency inside one workgroup
-  static constexpr int NBUF = KS == 1 ? DV_WG1_NBUF : (STG * 3 + JUNK <= 160 * 1024 ? 3 : 2);
-  static constexpr int NT = KS * KS;                            // taps
 };
 
 // the row-window wgrad tile epilogue (both wgrad kernels): the two pixel
@@ -2770,23 +2742,23 @@ __device__ __forceinline__ void wgrad_tile_store(const WgradSArgs& a, f32x16 (&a
   }
 }
 
-// LDS images are split by 32-channel half into 64-B rows: four consecutive
-// rows then start 16 banks apart, so the transposed operand reads are
-// conflict-free WITHOUT a swizzle, and an operand address is linear in the
-// row — every tap's window offset folds into the ds_read immediate.
-// STAG: only the second pixel half's waves (4-7) issue the stage DMAs, twice
-// as many each, so on every SIMD one wave (0-3) starts its MFMAs while its
-// partner pays the LDS-DMA issue (each SIMD holds one wave of each half)
-template <int W, int KS, bool STAG = false, bool TRIMOK = false>
-__global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv_wgrad_stripe_kernel(WgradSArgs a) {
-  using G = StripeGeom<W, KS, TRIMOK>;
-  constexpr int WP = G::WP, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF, NT = G::NT;
-  constexpr int AIMG = G::AIMG, BHALF = G::BHALF;
-  constexpr int DPS = (STAG ? 2 : 1) * (2 + 2 * NRH);  // DMAs per issuing thread per stage
-  // the bf16-partial epilogue sums the pixel halves in one pass (4 waves x
-  // (NT x 16 + 1) x 64 floats), which can exceed the stage ring
-  constexpr int RED1 = 4 * (NT * 16 + 1) * 64 * 4;
-  constexpr int RING = NBUF * STG + G::JUNK;
+// ---------------------------------------------------------------------------
+// bf16 1x1 wgrad (res_conv / Downsample3D / PixelShuffle / stage-3 1x1 convs,
+// cin, cout % 64 == 0): dW[co][ci] = sum_p dY[p][co] X[p][ci].  A workgroup
+// owns a 64 co x 64 ci tile over a contiguous range of 128-pixel stages, 8
+// waves (waves 4-7 on the second 64-pixel half, one 32 x 32 quadrant per
+// wave), the halves summed by wgrad_tile_store.  A stage is 128 dY rows and
+// 128 X rows by LDS-DMA into a 2-deep ring of 64-B half-row images (conflict-
+// free transposed reads, every k-step an immediate offset); 64 KB of LDS and
+// 4 waves per SIMD: two workgroups share a CU (a stage holds 4 MFMAs per wave,
+// too little to cover the next stage's DMA inside one workgroup).
+// ---------------------------------------------------------------------------
+template <int NBUF = 2>
+__global__ __launch_bounds__(512, 4) void conv_wgrad_1x1_kernel(WgradSArgs a) {
+  constexpr int AIMG = 2 * 128 * 64, BHALF = 128 * 64, STG = AIMG + 2 * BHALF;
+  constexpr int DPS = 4;                      // DMAs per thread per stage
+  constexpr int RED1 = 4 * (16 + 1) * 64 * 4;  // wgrad_tile_store's halves sum
+  constexpr int RING = NBUF * STG;
   __shared__ __attribute__((aligned(1024))) char smem[RING > RED1 ? RING : RED1];
 
   DV_STAMP_AT(0);
@@ -2797,103 +2769,36 @@ __global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv
   const int sbeg = blockIdx.z * a.stages_per_split;
   const int send = min(sbeg + a.stages_per_split, a.nstages);
   const int nst = send - sbeg;
-  const int HW = a.H * W, seg = a.seg, segrows = (seg + 2) * WP;
 
-  // ---- static per-lane DMA slots: row 16*wave + (lane >> 2) of each 128-row
-  // round, 16-B chunk (lane & 3) of a 64-B half row ----
-  const int l4 = lane >> 2, c4 = lane & 3;
-  const bf16* a_src = a.dy + co0 + 8 * c4;
+  // this lane's DMA slot: row 16 * wave + (lane >> 2), 16-B chunk (lane & 3)
+  // of a 64-B half row
+  const int l4 = lane >> 2, c4 = lane & 3, drow = 16 * wave;
   const bool first = ci0 < a.c0;
   const int xld = first ? a.ld0 : a.ld1;
-  const int b_c = (first ? ci0 : ci0 - a.c0) + 8 * c4;  // this lane's channel in its source
+  const __amdgpu_buffer_rsrc_t yrs = dma_rsrc(a.dy, (unsigned)((long long)a.nstages * 128 * a.lddy * 2));
   const __amdgpu_buffer_rsrc_t xrs =
       dma_rsrc(first ? a.x0 : a.x1, (unsigned)((long long)a.nstages * 128 * xld * 2));
-  // DMA rows of the (virtual) waves this thread issues for: its own, or under
-  // STAG waves (w & 3) and (w | 4) from the second half's threads
-  constexpr int NV = STAG ? 2 : 1;
-  int b_off[NV][NRH], b_ry[NV][NRH];  // b_ry: image-row offset, or a large negative for halo / junk rows
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int vw = STAG ? ((wave & 3) | (4 * k)) : wave;
-#pragma unroll
-    for (int i = 0; i < NRH; ++i) {
-      const int wr = 128 * i + 16 * vw + l4;
-      if (KS == 1) {  // the stage's own pixels
-        b_ry[k][i] = 0;
-        b_off[k][i] = wr;
-        continue;
-      }
-      const int sg = wr / segrows, rem = wr - sg * segrows;
-      const int ry = rem / WP, rx = rem - ry * WP;
-      const bool ok = sg < a.nseg && rx >= 1 && rx <= W;
-      b_ry[k][i] = ok ? ry - 1 : -(1 << 20);
-      b_off[k][i] = sg * seg * W + (ry - 1) * W + (rx - 1);
-    }
-  }
-
-  auto issue_vw = [&](int st, int buf, int vw, int k) {
-    const int m0 = (sbeg + st) * 128;
+  const unsigned yoff = (unsigned)(((drow + l4) * a.lddy + co0 + 8 * c4) * 2);
+  const unsigned xoff = (unsigned)(((drow + l4) * xld + (first ? ci0 : ci0 - a.c0) + 8 * c4) * 2);
+  auto issue = [&](int st, int buf) {
+    const unsigned m0 = (unsigned)(sbeg + st) * 128;
     char* sA = smem + buf * STG;
     char* sB = sA + AIMG;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const bf16* src = a_src + 32 * hh + (long long)(m0 + 16 * vw + l4) * a.lddy;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(sA + hh * (AIMG / 2) + 16 * vw * 64),
-                                       16, 0, 0);
-    }
-    const int y0 = (KS == 1 || a.nseg > 1) ? 0 : (m0 % HW) / W;
-#pragma unroll
-    for (int i = 0; i < NRH; ++i) {
-      const bool in = KS == 1 || (unsigned)(y0 + b_ry[k][i]) < (unsigned)a.H;
-      // halo / pad rows load out of the raw buffer's range: 16 zero bytes
-      // without a memory access (a shared zero line is one hot L2 channel)
-      const unsigned voff = in ? (unsigned)(((m0 + b_off[k][i]) * xld + b_c) * 2) : DMA_OOB;
-      const int drow = 128 * i + 16 * vw;  // wave-uniform
-      const bool live = !G::TRIM || drow < G::WRA;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-        dma16(xrs, live ? sB + hh * BHALF + drow * 64 : smem + NBUF * STG, live && in ? voff + 64 * hh : DMA_OOB);
-    }
-  };
-  auto issue = [&](int st, int buf) {
-    if constexpr (STAG) {
-      if (half) {  // wave-uniform
-        issue_vw(st, buf, wave & 3, 0);
-        issue_vw(st, buf, wave, 1);
-      }
-    } else {
-      issue_vw(st, buf, wave, 0);
+      dma16s(yrs, sA + hh * (AIMG / 2) + drow * 64, yoff + 64 * hh, m0 * a.lddy * 2);
+      dma16s(xrs, sB + hh * BHALF + drow * 64, xoff + 64 * hh, m0 * xld * 2);
     }
   };
 
-  f32x16 acc[NT];
+  f32x16 acc[1];
 #pragma unroll
-  for (int d = 0; d < NT; ++d)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[d][e] = 0.f;
-  // bias gradient on the VALU: a lane's A fragment holds 8 pixels of ONE
-  // output channel (row lane % 32 of the 32x32x16 A operand)
+  for (int e = 0; e < 16; ++e) acc[0][e] = 0.f;
   float accb = 0.f;
   const bool do_bias = a.db != nullptr && blockIdx.y == 0 && wn == 0;  // wave-uniform
-
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const int colb = 32 * (g & 1) + 8 * pp;  // byte column of this lane in a 64-B half row
-  // window rows (tap (0,0)) of this lane's two pixels in each of the 4 k-steps
-  int wlo[4], whi[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int plo = half * 64 + 16 * s + 8 * (g >> 1) + q, phi = plo + 4;
-    if (KS == 1) {
-      wlo[s] = plo * 64 + colb;
-      whi[s] = phi * 64 + colb;
-      continue;
-    }
-    const int sl = plo / (seg * W), sh = phi / (seg * W);
-    const int rl = plo - sl * seg * W, rh = phi - sh * seg * W;
-    wlo[s] = (sl * segrows + (rl / W) * WP + rl % W) * 64 + colb;
-    whi[s] = (sh * segrows + (rh / W) * WP + rh % W) * 64 + colb;
-  }
+  const int colb = 32 * (g & 1) + 8 * pp;
+  const int r0 = (half * 64 + 8 * (g >> 1) + q) * 64 + colb;  // k-step 0's row of this lane
 
 #pragma unroll
   for (int i = 0; i < NBUF - 1; ++i)
@@ -2903,102 +2808,42 @@ __global__ __launch_bounds__(512, KS == 1 && DV_WG1_NBUF == 2 ? 4 : 1) void conv
     if (st + NBUF - 1 < nst) {
       issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS * (NBUF - 1)) : "memory");
-    } else if (NBUF >= 3 && st + 2 < nst) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS * 2) : "memory");
-    } else if (st + 1 < nst) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     if (st == 0) DV_STAMP_AT(1);
-    const char* sA = smem + buf * STG + wm * (AIMG / 2);
-    const char* sB = smem + buf * STG + AIMG + wn * BHALF;
-    // This stage's operand addresses: one VGPR per (k-step, pixel half), the
-    // tap offset an immediate of the ds_read.  The empty asm makes the lane
-    // offsets opaque per stage: otherwise the (offset + tap) sums are hoisted
-    // out of the stage loop as 36 loop-invariant registers, each read then
-    // costs two VALU, and the registers left no room for a prefetch.
-    unsigned wl[4], wh[4];
-    const unsigned sBu = lds_u32(sB);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      wl[s] = sBu + wlo[s];
-      wh[s] = sBu + whi[s];
-      asm volatile("" : "+v"(wl[s]), "+v"(wh[s]));
-    }
-    const int a0 = ((half * 64 + 8 * (g >> 1) + q) * 64 + colb);
-    if constexpr (KS == 1) {
-      // 1x1: a stage is 4 k-steps of one tap; A and B of k-step s sit at
-      // + 1024 s (+ 256 for the high half) from k-step 0's: asm reads in the
-      // order (A0, B0, A1, B1, ...) with counted waits (hipcc would drain the
-      // in-flight stage DMAs before a visible tr read)
-      const unsigned ab = lds_u32(sA) + a0, bb = sBu + wlo[0];
-      u32x2 r[4][4];
-      static_for<0, 4>([&](auto S) {
-        constexpr int st4 = decltype(S)::value;
-        r[st4][0] = tr_read_asm<1024 * st4>(ab);
-        r[st4][1] = tr_read_asm<1024 * st4 + 256>(ab);
-        r[st4][2] = tr_read_asm<1024 * st4>(bb);
-        r[st4][3] = tr_read_asm<1024 * st4 + 256>(bb);
-      });
-      static_for<0, 4>([&](auto S) {
-        constexpr int st4 = decltype(S)::value;
-        asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(r[st4][0]), "+v"(r[st4][1]), "+v"(r[st4][2]), "+v"(r[st4][3])
-                     : "n"(4 * (3 - st4)));
-        const u32x4 fa1 = u32x4{r[st4][0][0], r[st4][0][1], r[st4][1][0], r[st4][1][1]};
-        const u32x4 fb1 = u32x4{r[st4][2][0], r[st4][2][1], r[st4][3][0], r[st4][3][1]};
-        acc[0] = Mma<bf16>::run(fa1, fb1, acc[0]);
-        if (do_bias) {
-          float t[8];
-          Vec<bf16>::to_f(fa1, t);
-          accb += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
-        }
-      });
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      continue;
-    }
-    // the 4 A fragments (dY) of the stage up front; B (window) fragments of
-    // tap j + WPF are read while tap j multiplies (flattened k-step x tap)
-    u32x4 fa[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const s16x4 lo = tr_read(sA + a0 + s * 1024);
-      const s16x4 hi = tr_read(sA + a0 + s * 1024 + 256);
-      const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
-      fa[s] = u32x4{l2[0], l2[1], h2[0], h2[1]};
-    }
-    constexpr int NJ = 4 * NT, WPF = NT >= 3 ? 3 : NT, NR = WPF + 1;
-    u32x4 fb[NR];
-    auto rdB = [&](int j) {
-      const int s = j / NT, d = j % NT;
-      const int toff = KS == 1 ? 0 : ((d / 3) * WP + (d % 3)) * 64;
-      const s16x4 lo = tr_read_at(wl[s], toff);
-      const s16x4 hi = tr_read_at(wh[s], toff);
-      const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
-      fb[j % NR] = u32x4{l2[0], l2[1], h2[0], h2[1]};
-    };
-#pragma unroll
-    for (int j = 0; j < WPF; ++j) rdB(j);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      if (j + WPF < NJ) rdB(j + WPF);
-      const int s = j / NT, d = j % NT;
-      acc[d] = Mma<bf16>::run(fa[s], fb[j % NR], acc[d]);
-      if (d == NT - 1 && do_bias) {
+    // A and B of k-step s at + 1024 s (+ 256 for the high half): asm reads in
+    // the order (A0, B0, A1, B1, ...), counted waits (tr_read_asm)
+    const unsigned ab = lds_u32(smem + buf * STG + wm * (AIMG / 2)) + r0;
+    const unsigned bb = lds_u32(smem + buf * STG + AIMG + wn * BHALF) + r0;
+    u32x2 r[4][4];
+    static_for<0, 4>([&](auto S) {
+      constexpr int k = decltype(S)::value;
+      r[k][0] = tr_read_asm<1024 * k>(ab);
+      r[k][1] = tr_read_asm<1024 * k + 256>(ab);
+      r[k][2] = tr_read_asm<1024 * k>(bb);
+      r[k][3] = tr_read_asm<1024 * k + 256>(bb);
+    });
+    static_for<0, 4>([&](auto S) {
+      constexpr int k = decltype(S)::value;
+      asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(r[k][0]), "+v"(r[k][1]), "+v"(r[k][2]), "+v"(r[k][3])
+                   : "n"(4 * (3 - k)));
+      const u32x4 fa = u32x4{r[k][0][0], r[k][0][1], r[k][1][0], r[k][1][1]};
+      const u32x4 fb = u32x4{r[k][2][0], r[k][2][1], r[k][3][0], r[k][3][1]};
+      acc[0] = Mma<bf16>::run(fa, fb, acc[0]);
+      if (do_bias) {  // a lane's A fragment holds 8 pixels of ONE output channel
         float t[8];
-        Vec<bf16>::to_f(fa[s], t);
+        Vec<bf16>::to_f(fa, t);
         accb += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
       }
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
   DV_STAMP_AT(2);
   accb += __shfl_xor(accb, 32, 64);  // both k-halves of the channel
-  wgrad_tile_store<NT>(a, acc, accb, smem, half, wq, wm, wn, lane, co0, ci0, do_bias, (int)blockIdx.z);
+  wgrad_tile_store<1>(a, acc, accb, smem, half, wq, wm, wn, lane, co0, ci0, do_bias, (int)blockIdx.z);
 }
 
 // ---------------------------------------------------------------------------
@@ -3040,19 +2885,15 @@ bool wgrad_win_geom_ok(int h, int w) {
   return (w == 32 || w == 64) && h % 4 == 0;
 }
 
-// ISS: where the stage DMAs are issued (A/B, round 5).  0: waves 4-7 issue
-// stage st + 2 before the stage's barrier (two barriers per stage); 1: one
-// barrier per stage, waves 4-7 issue two pieces per row shift among the
-// MFMAs; 2: one barrier, every wave issues its own six pieces among the
-// MFMAs; 3: one barrier, every wave issues its six right after it
-template <int W, int ISS = 0>
+// One barrier per stage; every wave issues its own six DMA pieces of stage
+// st + 2 among the MFMAs of row shifts 0-2 (same box, r05e: 387 vs 407 us
+// over the Cfg2 shapes for waves 4-7 issuing all of them before the barrier).
+template <int W>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
   using G = WinGeom<W>;
   constexpr int WQ = G::WQ, NRH = G::NRH, STG = G::STG, NBUF = G::NBUF, AIMG = G::AIMG, BHALF = G::BHALF;
   constexpr int NT = 9;
-  constexpr bool OWN = ISS >= 2;          // every wave issues its own pieces
-  constexpr int NV = OWN ? 1 : 2;         // virtual waves an issuing wave serves
-  constexpr int DPS = NV * (2 + 2 * NRH);  // DMAs per issuing thread per stage
+  constexpr int DPS = 2 + 2 * NRH;  // DMAs per thread per stage
   constexpr int RED1 = 4 * (NT * 16 + 1) * 64 * 4;
   constexpr int RING = NBUF * STG;
   __shared__ __attribute__((aligned(1024))) char smem[RING > RED1 ? RING : RED1];
@@ -3061,19 +2902,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int half = wave >> 2, wq = wave & 3, wm = wq >> 1, wn = wq & 1;
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (a.xcd) {
-    // round-robin dispatch puts blocks L and L + 8 on one XCD: give XCD
-    // (L % 8) the contiguous chunk of tiles in (split, co, ci) order, so its
-    // L2 holds few dY / X tiles (host-checked: block count % 8 == 0)
-    const int nxy = gridDim.x * gridDim.y;
-    const int L = bx + gridDim.x * (by + gridDim.y * bz);
-    const int T = (L & 7) * ((nxy * gridDim.z) >> 3) + (L >> 3);
-    bz = T / nxy;
-    const int r = T - bz * nxy;
-    bx = r / gridDim.y;
-    by = r - bx * gridDim.y;
-  }
+  // (dealing the tiles to XCDs in contiguous chunks cut the L2 fill traffic
+  // 1.2-3x and measured slower: 424-430 vs 409-411 us over the Cfg2 shapes, r05b)
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   const int co0 = bx * 64, ci0 = by * 64;
   const int sbeg = bz * a.stages_per_split;
   const int send = min(sbeg + a.stages_per_split, a.nstages);
@@ -3116,10 +2947,10 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
   const int b_c = (first ? ci0 : ci0 - a.c0) + 8 * c4;
   const __amdgpu_buffer_rsrc_t xrs =
       dma_rsrc(first ? a.x0 : a.x1, (unsigned)((long long)a.nstages * 128 * xld * 2));
-  int a_rel[NV], b_off[NV][NRH], b_ry[NV][NRH], b_rx[NV][NRH];
+  int a_rel[1], b_off[1][NRH], b_ry[1][NRH], b_rx[1][NRH];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int vw = OWN ? wave : (wave & 3) | (4 * k);
+  for (int k = 0; k < 1; ++k) {
+    const int vw = wave;
     a_rel[k] = rel(16 * vw + l4);
 #pragma unroll
     for (int i = 0; i < NRH; ++i) {
@@ -3135,7 +2966,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
   // piece p of virtual wave slot k: p = 0 the dY rows (2 DMAs), p = 1 + i
   // window round i (2 DMAs)
   auto issue_piece = [&](int base, int y0, int x0, int buf, int k, int p) {
-    const int vw = OWN ? wave : (wave & 3) | (4 * k);
+    const int vw = wave;
     char* sA = smem + buf * STG;
     char* sB = sA + AIMG;
     if (p == 0) {
@@ -3154,14 +2985,10 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
   };
   constexpr int NP = 1 + NRH;  // pieces per virtual wave
   auto issue = [&](int st, int buf) {
-    if (OWN || half) {  // wave-uniform
-      int y0, x0;
-      const int base = stage_base(sbeg + st, y0, x0);
+    int y0, x0;
+    const int base = stage_base(sbeg + st, y0, x0);
 #pragma unroll
-      for (int k = 0; k < NV; ++k)
-#pragma unroll
-        for (int p = 0; p < NP; ++p) issue_piece(base, y0, x0, buf, k, p);
-    }
+    for (int p = 0; p < NP; ++p) issue_piece(base, y0, x0, buf, 0, p);
   };
 
   f32x16 acc[NT];
@@ -3187,32 +3014,15 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
     if (i < nst) issue(i, i);
   for (int st = 0; st < nst; ++st) {
     const int buf = st % NBUF;
-    // ISS > 0: stage st + 2 goes into the buffer of stage st - 1, which every
-    // wave finished reading before this barrier
-    const bool pre = ISS > 0 && st + NBUF - 1 < nst;
+    // stage st + 2 goes into the buffer of stage st - 1, which every wave
+    // finished reading before this barrier; stage st + 1 may still land
+    const bool pre = st + NBUF - 1 < nst;
     int nbase = 0, ny0 = 0, nx0 = 0;
-    if constexpr (ISS == 0) {
-      if (st + NBUF - 1 < nst) {
-        issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS * (NBUF - 1)) : "memory");
-      } else if (st + 1 < nst) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    } else {
-      if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (pre) nbase = stage_base(sbeg + st + NBUF - 1, ny0, nx0);
-    }
+    if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pre) nbase = stage_base(sbeg + st + NBUF - 1, ny0, nx0);
     __builtin_amdgcn_s_barrier();
     const int nbuf = (st + NBUF - 1) % NBUF;
-    if constexpr (ISS == 3) {
-      if (pre) {
-#pragma unroll
-        for (int p = 0; p < NP; ++p) issue_piece(nbase, ny0, nx0, nbuf, 0, p);
-      }
-    }
     if (st == 0) DV_STAMP_AT(1);
     const char* sA = smem + buf * STG + wm * (AIMG / 2);
     // one operand base per stage, made opaque so that each (t, dx) offset
@@ -3267,13 +3077,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
       for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
         for (int s = slo; s <= shi; ++s) acc[(t - s) * 3 + dx] = Mma<bf16>::run(fa[s], fb[dx], acc[(t - s) * 3 + dx]);
-      // the next stage's pieces among the MFMAs (ISS 1: waves 4-7, six per
-      // virtual wave over t = 0..5; ISS 2: every wave, its own over t = 0..NP-1)
-      if constexpr (ISS == 1) {
-        constexpr int k = t / 3, p = t % 3;
-        if (pre && half && p < NP) issue_piece(nbase, ny0, nx0, nbuf, k, p);
-      } else if constexpr (ISS == 2) {
-        if (pre && t < NP) issue_piece(nbase, ny0, nx0, nbuf, 0, t);
+      // the next stage's pieces among the MFMAs: piece t after row shift t
+      if constexpr (t < NP) {
+        if (pre) issue_piece(nbase, ny0, nx0, nbuf, 0, t);
       }
       if constexpr (t < 4) {
         if (do_bias) {
@@ -3285,7 +3091,6 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (ISS == 0) __builtin_amdgcn_s_barrier();
   }
   DV_STAMP_AT(2);
   accb += __shfl_xor(accb, 32, 64);  // both k-halves of the channel
@@ -3476,22 +3281,20 @@ bool stripe_geom(int h, int w, int& seg, int& nseg) {
 
 bool wgrad_stripe_ok(int nf, int h, int w, int cin, int c0, bool split, int cout, int ks,
                      long long maxld = 0) {
-  int seg, nseg;
   if ((ks != 3 && ks != 1) || cin % 64 || cout % 64 || (split && c0 % 64)) return false;
   const long long M = (long long)nf * h * w;
   if (M % 128 || M >= (1ll << 31)) return false;
   if (M * std::max<long long>(maxld, cout) * 2 >= (long long)DMA_OOB) return false;  // raw-buffer resources
-  return ks == 1 || wgrad_win_geom_ok(h, w) || stripe_geom(h, w, seg, nseg);
+  return ks == 1 || wgrad_win_geom_ok(h, w);
 }
 
-// split count: ~256 workgroups (one per CU: the stage ring takes up to 112 KB of LDS)
-// split count: ~256 workgroups (one per CU: the stage ring takes up to 147 KB
-// of LDS).  Capping the splits by stages or by partial bytes was measured
+// split count: ~256 workgroups (one per CU: the 3x3 stage ring takes 144 KB
+// of LDS; the 1x1 kernel's 64 KB ring runs two per CU: ~512).  Capping the splits by stages or by partial bytes was measured
 // slower on every Cfg2 shape (tools/ab_fwd.sh): occupancy wins.
 inline void stripe_split(int nstages, int grid_xy, long long grad_floats, int ks, int& sps, int& S) {
   (void)grad_floats;
   // 1x1 with the 2-deep ring: two workgroups per CU
-  long long want = (ks == 1 && DV_WG1_NBUF == 2 ? 512 : 256) / grid_xy;
+  long long want = (ks == 1 ? 512 : 256) / grid_xy;
   if (want > nstages) want = nstages;
   if (want < 1) want = 1;
   sps = (int)((nstages + want - 1) / want);
@@ -3518,8 +3321,6 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   a.dy = (const bf16*)dy; a.lddy = lddy; a.x0 = (const bf16*)x0;
   a.x1 = (const bf16*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0; a.c0 = x1 ? c0 : cin;
   a.H = h; a.cin = cin; a.cout = cout; a.K = ks * ks * cin;
-  a.seg = 1; a.nseg = 1;
-  if (ks == 3) stripe_geom(h, w, a.seg, a.nseg);
   a.nstages = (int)((long long)nf * h * w / 128);
   int S;
   stripe_split(a.nstages, (cout / 64) * (cin / 64), (long long)cout * a.K, ks, a.stages_per_split, S);
@@ -3528,45 +3329,14 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
   a.dbpart = db ? ws + (long long)S * cout * a.K / (a.part_bf16 ? 2 : 1) : nullptr;
   a.dw = dw; a.db = db; a.acc_w = acc_w; a.acc_b = acc_b;
   dim3 grid(cout / 64, cin / 64, S);
-  static const int xcdk = getenv("DV_WG_XCD") ? atoi(getenv("DV_WG_XCD")) : 0;  // temporary A/B
-  a.xcd = xcdk && ((long long)grid.x * grid.y * grid.z) % 8 == 0;
-  // the 3x3 stage DMAs issued by waves 4-7 only: family 1,897 -> 1,874 us per
-  // step, step equal (profiles/r04p_wgrad_stag_ab.txt); DV_WG_STAG=0: every wave
-  static const bool stag = !(getenv("DV_WG_STAG") && atoi(getenv("DV_WG_STAG")) == 0);
-  static const bool old3 = getenv("DV_WG_OLD") && atoi(getenv("DV_WG_OLD")) != 0;  // temporary A/B
   if (ks == 1) {
-    conv_wgrad_stripe_kernel<64, 1><<<grid, 512, 0, st>>>(a);
-  } else if (!old3 && wgrad_win_geom_ok(h, w)) {
-    static const int iss = getenv("DV_WG_ISS") ? atoi(getenv("DV_WG_ISS")) : 0;  // temporary A/B
-#define DV_WW(I)                                                          \
-  switch (w) {                                                            \
-    case 64: conv_wgrad_win_kernel<64, I><<<grid, 512, 0, st>>>(a); break; \
-    case 32: conv_wgrad_win_kernel<32, I><<<grid, 512, 0, st>>>(a); break; \
-    case 16: conv_wgrad_win_kernel<16, I><<<grid, 512, 0, st>>>(a); break; \
-    default: conv_wgrad_win_kernel<8, I><<<grid, 512, 0, st>>>(a); break;  \
-  }
-    if (iss == 1) DV_WW(1) else if (iss == 2) DV_WW(2) else if (iss == 3) DV_WW(3) else DV_WW(0)
-#undef DV_WW
-  } else if (stag) {
-    // DV_WG_TRIM=1: the W = 64 window image trimmed to a 3-deep ring.  Measured
-    // no faster (36.3-36.5 -> 36.9-37.0 us per launch, profiles/r04t_wgrad_trim_ab.txt):
-    // one stage in flight already covers the load latency here
-    static const bool trim = getenv("DV_WG_TRIM") && atoi(getenv("DV_WG_TRIM")) != 0;
-    switch (w) {
-      case 64:
-        if (trim) conv_wgrad_stripe_kernel<64, 3, true, true><<<grid, 512, 0, st>>>(a);
-        else conv_wgrad_stripe_kernel<64, 3, true><<<grid, 512, 0, st>>>(a);
-        break;
-      case 32: conv_wgrad_stripe_kernel<32, 3, true><<<grid, 512, 0, st>>>(a); break;
-      case 16: conv_wgrad_stripe_kernel<16, 3, true><<<grid, 512, 0, st>>>(a); break;
-      default: conv_wgrad_stripe_kernel<8, 3, true><<<grid, 512, 0, st>>>(a); break;
-    }
+    conv_wgrad_1x1_kernel<><<<grid, 512, 0, st>>>(a);
   } else {
     switch (w) {
-      case 64: conv_wgrad_stripe_kernel<64, 3><<<grid, 512, 0, st>>>(a); break;
-      case 32: conv_wgrad_stripe_kernel<32, 3><<<grid, 512, 0, st>>>(a); break;
-      case 16: conv_wgrad_stripe_kernel<16, 3><<<grid, 512, 0, st>>>(a); break;
-      default: conv_wgrad_stripe_kernel<8, 3><<<grid, 512, 0, st>>>(a); break;
+      case 64: conv_wgrad_win_kernel<64><<<grid, 512, 0, st>>>(a); break;
+      case 32: conv_wgrad_win_kernel<32><<<grid, 512, 0, st>>>(a); break;
+      case 16: conv_wgrad_win_kernel<16><<<grid, 512, 0, st>>>(a); break;
+      default: conv_wgrad_win_kernel<8><<<grid, 512, 0, st>>>(a); break;
     }
   }
   if (S > 1) {
@@ -3659,7 +3429,7 @@ static int conv_wgrad_impl(int dtype, const void* dy, int lddy, const void* x0, 
   hipStream_t st = (hipStream_t)stream;
   if ((long long)nf * h * w == 0) return DV_OK;
   if (dtype == DV_BF16 && cout_real == cout && cin_real == cin &&
-      wgrad_stripe_ok(nf, h, w, cin, c0, x1 != nullptr, cout, ksize, std::max(ld0, x1 ? ld1 : 0)))
+      wgrad_stripe_ok(nf, h, w, cin, c0, x1 != nullptr, cout, ksize, std::max(std::max(ld0, x1 ? ld1 : 0), lddy)))
     return conv_wgrad_stripe(dy, lddy, x0, ld0, c0, x1, ld1, ws, dw, accumulate_w, db, accumulate_b,
                              nf, h, w, cin, cout, ksize, st, defer);
   // general path: f32 atomics into the zeroed packed workspace, then one reduce

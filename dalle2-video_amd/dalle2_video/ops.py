@@ -22,6 +22,7 @@ class KernelTimer:
 
     def __init__(self):
         self.records = []  # (name, shape, flops, bytes, start_event, end_event)
+        self.fns = {}      # name -> the launch closures, in order (replay_ms)
 
     # a short device-side spin before each timed launch keeps the GPU behind the
     # host, so the start event, the kernel and the end event run back to back and
@@ -36,6 +37,31 @@ class KernelTimer:
         fn()
         e.record()
         self.records.append((name, shape, flops, nbytes, s, e))
+        self.fns.setdefault(name, []).append(fn)
+
+    def replay_ms(self, name, n_launch, reps=10):
+        """Per-launch device time of kernel `name` the way a kernel trace sees
+        it: its last `n_launch` launches (one step's) captured back to back in
+        a HIP graph with no event brackets between them, replayed `reps`
+        times; elapsed / (reps * n_launch).  Includes the ~1.5 us kernel
+        boundaries (MI355X_MICROARCH.md, boundary row): a slight upper bound."""
+        fns = self.fns[name][-n_launch:]
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for f in fns:
+                f()
+        g.replay()
+        torch.cuda.synchronize()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            g.replay()
+        e.record()
+        torch.cuda.synchronize()
+        del g
+        return s.elapsed_time(e) / (reps * len(fns))
 
     def overhead_ms(self, n=32):
         """Median elapsed time of an EMPTY start/end event pair recorded the
@@ -148,13 +174,11 @@ def conv_wgrad_name(dtype_name, m, cout, cin, c0, split, ks, h, w, maxld):
     """Mirror of dv_conv_wgrad's kernel choice (wgrad_stripe_ok / conv_wgrad_glds)."""
     if (dtype_name == "bf16" and ks == 1 and cin % 64 == 0 and cout % 64 == 0
             and (not split or c0 % 64 == 0) and m % 128 == 0):
-        return "conv_wgrad_stripe_kernel<64,1>"
+        return "conv_wgrad_1x1_kernel"
     if (dtype_name == "bf16" and ks == 3 and cin % 64 == 0 and cout % 64 == 0
-            and (not split or c0 % 64 == 0) and m % 128 == 0 and w in (8, 16, 32, 64)
-            and ((h * w >= 128 and h % (128 // w) == 0)
-                 or (h * w < 128 and 128 % (h * w) == 0
-                     and (128 // (h * w)) * (h + 2) * (w + 2) <= (200 if w == 8 else (128 // w + 2) * (w + 2))))):
-        return f"conv_wgrad_stripe_kernel<{w},3>"
+            and (not split or c0 % 64 == 0) and m % 128 == 0
+            and ((w == 8 and h == 8) or (w == 16 and h % 8 == 0) or (w in (32, 64) and h % 4 == 0))):
+        return f"conv_wgrad_win_kernel<{w}>"
     K = ks * ks * cin
     return gemm_wgrad_name(dtype_name, m, cout, K, maxld)
 
@@ -996,7 +1020,7 @@ class ConvFn(torch.autograd.Function):
                                      max(lddy, ld0, ld1)) if (cout8 == cout and cin_real == cin)
                      else gemm_wgrad_name(dname, m, cout8, cin * ksize * ksize, max(lddy, ld0, ld1)))
             if (WGRAD_DEFER.active and dw is None and db is None and not _WgradStream.enabled
-                    and kname.startswith("conv_wgrad_stripe")):
+                    and kname.startswith(("conv_wgrad_win", "conv_wgrad_1x1"))):
                 # leaf .grad targets: leave the split partials for the pass-end sum
                 if (not WGRAD_DEFER.STREAM
                         and WGRAD_DEFER.conflicts(dw_t.data_ptr(), db_t.data_ptr() if db_t is not None else None)):

@@ -862,6 +862,9 @@ class VideoDecoderTrainer(nn.Module):
                 ov.attach(unet.parameters())
                 self.overlap.append(ov)
         self._reduced = [False] * self.num_unets  # the last call's gradient is already all-reduced
+        # bench.py at N > 1: a list -> eager calls record ["exposed", end of the
+        # backward's compute, every bucket joined] event pairs
+        self.comm_probe = None
         self._gen_seen = [getattr(self, f"optim{i}").generation for i in range(self.num_unets)]
         # accelerator.prepare(..., train, val) (trainer.py:117-124) shards the
         # loaders per process: each rank iterates a disjoint rank-strided part
@@ -931,6 +934,10 @@ class VideoDecoderTrainer(nn.Module):
             self._reduced[index] = False  # re-pointed buffers: reduce the copied gradient again
         if self._reduced[index]:
             self.overlap[index].wait()  # the overlapped buckets (a captured call joined them already)
+            if self.comm_probe is not None and self.comm_probe and self.comm_probe[-1][0] == "bwd":
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()  # every bucket joined: the all-reduce time left after the backward
+                self.comm_probe[-1] = ["exposed", self.comm_probe[-1][1], ev]
         else:
             allreduce_flat_grad(opt.flat_grad, self.world, force=self.force_allreduce, comm=self.gcomm)
         self._reduced[index] = False
@@ -1090,6 +1097,10 @@ class VideoDecoderTrainer(nn.Module):
                     ov.abort()
                 raise
             if ov is not None:
+                if self.comm_probe is not None:  # the backward's compute is queued
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record()
+                    self.comm_probe.append(["bwd", ev])
                 self._reduced[unet_number - 1] = ov.end(join=False)
         if return_lowres_cond_video:
             return total_loss, torch.stack(cond_videos)

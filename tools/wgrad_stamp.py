@@ -1,4 +1,4 @@
-"""Phase timeline of the row-window wgrad (conv_wgrad_stripe_kernel) and the
+"""Phase timeline of the window wgrad (conv_wgrad_win_kernel) and the
 window conv (conv_fwd_frame_kernel) at the Cfg2 shapes, from the diagnostic
 build's per-workgroup s_memrealtime stamps (make -C dalle2-video_amd/csrc
 stamp; DV_STAMP in dv_conv.hip):
@@ -65,7 +65,7 @@ def wgrad_case(nf, h, w, cin, cout):
     want = max(1, min(256 // tiles, nst))
     sps = (nst + want - 1) // want
     S = (nst + sps - 1) // sps
-    report(f"wgrad stripe ({nf},{h},{w}) {cin}->{cout} S={S}", stamps(tiles * S), [0, 1, 2, 3, 4])
+    report(f"wgrad ({nf},{h},{w}) {cin}->{cout} S={S}", stamps(tiles * S), [0, 1, 2, 3, 4])
 
 
 def frame_case(nf, h, w, cin, cout):
@@ -91,7 +91,8 @@ def frame_case(nf, h, w, cin, cout):
            stamps((m // 128) * (cout // cw)), [0, 1, 2, 4])
 
 
-for shp in [(64, 64, 64, 64, 64), (64, 32, 32, 128, 128), (64, 16, 16, 256, 256), (64, 8, 8, 512, 512)]:
+for shp in [(64, 64, 64, 64, 64), (64, 32, 32, 64, 64), (64, 32, 32, 128, 128), (64, 16, 16, 256, 256),
+            (64, 8, 8, 512, 512)]:
     wgrad_case(*shp)
 for shp in [(64, 8, 8, 512, 512), (64, 8, 8, 256, 256), (64, 16, 16, 256, 256)]:
     frame_case(*shp)
