@@ -497,10 +497,17 @@ def main():
                          "achieved": round(fl / (ms * 1e-3) / 1e12, 1), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4)}
         ops.TIMER = None
+        del summ
 
     log(f"train: {args.steps / elapsed:.2f} steps/s per GPU")
     fp32 = None
     if not args.no_fp32 and args.dtype == "bf16" and world == 1:
+        # hand the cached blocks of the bf16 legs back first: on a cache the
+        # bf16 step and the timer's closures have carved up, the f32 step ran
+        # at 12.7-13.1 steps/s instead of 17.7-18.1 (r05, same box, same tree)
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
         fp32 = fp32_leg(args, device)
         log("fp32:", fp32["value"], "steps/s")
     sampling = None

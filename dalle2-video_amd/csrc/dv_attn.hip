@@ -17,6 +17,30 @@
 
 using namespace dv;
 
+// Diagnostic build only (make stamp): per-workgroup s_memrealtime stamps of
+// the mid-attention kernels' phases (tools/mqa_stamp.py): kernel k (0 fwd,
+// 1 dq, 2 dk/dv), stamps 0 entry, 1 operands staged (loop start), 2 loop
+// done, 3 results stored.  The product build compiles none of it.
+#ifdef DV_STAMP
+constexpr int MQ_NBLK = 4096, MQ_NSTAMP = 4;
+__device__ unsigned long long g_mq_stamp[3 * MQ_NBLK * MQ_NSTAMP];
+#define MQ_STAMP_AT(k, i)                                                                                  \
+  do {                                                                                                     \
+    if (threadIdx.x == 0) {                                                                                \
+      const long long blin = blockIdx.x + (long long)gridDim.x * (blockIdx.y + (long long)gridDim.y * blockIdx.z); \
+      if (blin < MQ_NBLK) g_mq_stamp[((k) * MQ_NBLK + blin) * MQ_NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                                      \
+  } while (0)
+extern "C" int dv_debug_stamps_mqa(unsigned long long* host, long long n) {
+  if (n > 3 * MQ_NBLK * MQ_NSTAMP) n = 3 * MQ_NBLK * MQ_NSTAMP;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mq_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#else
+#define MQ_STAMP_AT(k, i) \
+  do {                    \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr int DH = 32;  // head dim
@@ -909,6 +933,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sK = smem;
   char* sV = smem + NKP * ROW;
+  MQ_STAMP_AT(0, 0);
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int rg = wave & (RG - 1), kh = wave / RG;
@@ -923,6 +948,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
   const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  MQ_STAMP_AT(0, 1);
   const FragOff fo = frag_off(lane);
   const int k0 = kh ? kmid : 0, k1 = kh ? nkt : kmid;
   Soft st{zero16(), zero16(), -INFINITY, 0.f};
@@ -930,8 +956,13 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_kernel(const bf16* __restr
     soft_range2_fixed(st, sK, sV, k0, k1, 0, nkeys, fo, qf0, qf1, h);
   else
     soft_range2(st, true, sK, sV, k0, k1, 0, nkeys, fo, qf0, qf1, h);
+  MQ_STAMP_AT(0, 2);
   soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
               lse + (long long)b * R + row);
+#ifdef DV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  MQ_STAMP_AT(0, 3);
 }
 
 // Long sequences (config 5: 32 x 16 x 16 = 8,192 tokens, K / V = 1 MiB per
@@ -1027,6 +1058,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sK = smem;
   char* sV = smem + NKP * ROW;
+  MQ_STAMP_AT(1, 0);
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int rg = wave & (RG - 1), kh = wave / RG;
@@ -1046,6 +1078,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
   if (rok && h == 0 && kh == 0) D[(long long)b * R + row] = dd;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  MQ_STAMP_AT(1, 1);
   const FragOff fo = frag_off(lane);
   const f32x16 negL = bcast16(-L2), negD = bcast16(-dd);
   f32x16 acc = zero16();
@@ -1070,6 +1103,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
     acc = mma(tr_at(tK, fo, 1), pack8(s, 1), acc);
   };
   for (int kt = kbeg; kt < kend; ++kt) tile(kt);
+  MQ_STAMP_AT(1, 2);
   __syncthreads();
   float* red = (float*)smem + rg * 16 * 64;
   if (kh) {
@@ -1090,6 +1124,10 @@ __global__ __launch_bounds__(NW * 64) void mqa_dq_fa_kernel(
       *(u32x2*)(qrow + 8 * g + 4 * h) = v;
     }
   }
+#ifdef DV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  MQ_STAMP_AT(1, 3);
 }
 
 // dk/dv, key-major.  grid (ceil(nkt / 4), S, B); wave w: key tile
@@ -1108,6 +1146,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     float* __restrict__ ws, int R, int NKP, int nkeys, int rows_per_split, float scale) {
   constexpr int TPS = 1;
   __shared__ __attribute__((aligned(16))) char smem[2 * QP * TPS * TB > RED ? 2 * QP * TPS * TB : RED];
+  MQ_STAMP_AT(2, 0);
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int b = blockIdx.z, split = blockIdx.y;
@@ -1163,6 +1202,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
   // step's compute (33.0-33.6 -> 31.6-31.7 us, profiles/r04o_mqa_early_ab.txt)
   if (nsteps > 1) load(1);
   __syncthreads();
+  MQ_STAMP_AT(2, 1);
   for (int st = 0; st < nsteps; ++st) {
     const bool more = st + 1 < nsteps;
     if (more) store((st + 1) & 1);
@@ -1205,6 +1245,7 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
     }
     __syncthreads();
   }
+  MQ_STAMP_AT(2, 2);
   // combine the parities through LDS (3,2 -> 1,0, then 1 -> 0), one partial per split
   float* red = (float*)smem;
   auto park = [&](int slot) {
@@ -1242,6 +1283,10 @@ __global__ __launch_bounds__(NW * 64) void mqa_dkdv_fa_kernel(
       *(f32x4*)(w + 32 + 8 * g + 4 * h) = v;
     }
   }
+#ifdef DV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  MQ_STAMP_AT(2, 3);
 }
 
 // dkv[b*N + n] = sum over splits of ws[.][b][n + 1]; dnull (+)= sum over b, splits of key 0
