@@ -80,6 +80,11 @@ struct ConvFwdArgs {
   const float* bias;
   const T* res;
   int ldres;
+  // a second residual (the unet skip gradient a dgrad adds besides the shared
+  // input-gradient buffer, ops.SkipGrad); null: none.  Launchers move a lone
+  // res2 into res, so res2 != null implies res != null.
+  const T* res2 = nullptr;
+  int ldres2 = 0;
   T* y;
   int ldy;
   int H, W, cin, cout, ks, act;
@@ -203,7 +208,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32
                                               long long mb, int nb, int r, int h,
                                               long long blk_m0 = 0, int blk_bm = 0, int blk_n0 = 0,
                                               int blk_bn = 0, float* red = nullptr) {
-  const bool vec_ok = ((p.ldy & 3) == 0) && (p.res == nullptr || (p.ldres & 3) == 0);
+  const bool vec_ok = ((p.ldy & 3) == 0) && (p.res == nullptr || (p.ldres & 3) == 0) &&
+                      (p.res2 == nullptr || (p.ldres2 & 3) == 0);
   constexpr int NC = 16 * TJ, NV = STATS ? 2 * NC : 1;
   float sv[NV];
   long long clip = 0;
@@ -225,7 +231,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32
   // clamped (unconditional loads); lanes past M / cout skip the store.
   f32x4 bv[TJ][4];
   using RV = typename std::conditional<sizeof(T) == 2, u32x2, f32x4>::type;
-  RV rv[TI][TJ][4];
+  RV rv[TI][TJ][4], rv2[TI][TJ][4];
   if (vec_ok && p.cout >= 4) {
     if (p.bias) {
 #pragma unroll
@@ -246,6 +252,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32
           for (int g = 0; g < 4; ++g) {
             const int n = min(nb + 32 * j + 8 * g + 4 * h, p.cout - 4);
             rv[i][j][g] = *(const RV*)(p.res + m * p.ldres + n);
+            if (p.res2) rv2[i][j][g] = *(const RV*)(p.res2 + m * p.ldres2 + n);
           }
       }
     }
@@ -284,6 +291,18 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32
             }
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += rr[e];
+            if (p.res2) {
+              if constexpr (sizeof(T) == 2) {
+                const bf16x4 t4 = __builtin_bit_cast(bf16x4, rv2[i][j][g]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) rr[e] = (float)t4[e];
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) rr[e] = rv2[i][j][g][e];
+              }
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += rr[e];
+            }
           }
           store4<T>(p.y + m * p.ldy + n, v);
           if constexpr (STATS) {
@@ -305,6 +324,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs<T>& p, const f32
             float t = v[e] + (p.bias ? p.bias[n + e] : 0.f);
             if (p.act == DV_ACT_SILU) t = silu_f(t);
             if (p.res) t += (float)p.res[m * p.ldres + n + e];
+            if (p.res2) t += (float)p.res2[m * p.ldres2 + n + e];
             p.y[m * p.ldy + n + e] = (T)t;
             if constexpr (STATS) {
               const float q = stored<T>(t);
@@ -1722,7 +1742,7 @@ struct FsGeom {
   static constexpr int LDS = RING;
 };
 
-template <int W, bool RES, bool STATS>
+template <int W, int NRES, bool STATS>
 __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> p, int nstages,
                                                               int stages_per_block) {
   using G = FsGeom<W>;
@@ -1803,7 +1823,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   const int r = lane & 31, h = lane >> 5;
   const int px = pt * 32 + r;  // lane's pixel in the stage; window row of tap (0,0)
   const int bofs = ((px / W) * WP + (px % W)) * FS_XP + h * 16;
-  // GroupNorm statistics (STATS, compile-time like RES): each stage's 32 x 16
+  // GroupNorm statistics (STATS, compile-time like NRES): each stage's 32 x 16
   // sums / squares are reduce-scattered over the half-wave (gn_rs_reduce), so
   // a lane carries ONE running total across stages; it is added when the
   // stage range crosses into the next clip (128-pixel stages never straddle
@@ -1833,12 +1853,17 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
       constexpr int k = decltype(kk)::value;
       bq[k] = ds_read_b128_off<fs_koff<W>(k)>(xa);
     });
-    bf16x4 rv[4];
+    bf16x4 rv[4], rv2[4];
     const long long m = (long long)(sbeg + st) * 128 + px;
-    if (RES) {  // (a compile-time branch: a runtime one becomes a per-stage vmcnt(0))
+    if (NRES > 0) {  // (a compile-time branch: a runtime one becomes a per-stage vmcnt(0))
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         rv[g] = *(const bf16x4*)(p.res + m * p.ldres + co0 + ch * 32 + 8 * g + 4 * h);
+    }
+    if (NRES > 1) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        rv2[g] = *(const bf16x4*)(p.res2 + m * p.ldres2 + co0 + ch * 32 + 8 * g + 4 * h);
     }
     f32x16 acc = bias_acc;  // the accumulator starts at the bias
     static_for<0, 36>([&](auto kk) {
@@ -1862,9 +1887,13 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
       }
-      if (RES) {
+      if (NRES > 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += (float)rv[g][e];
+      }
+      if (NRES > 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (float)rv2[g][e];
       }
       store4<bf16>(p.y + m * p.ldy + co0 + n, v);
       if constexpr (stats) {
@@ -1918,15 +1947,17 @@ int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   const int sps = (nstages + bx - 1) / bx;
   bx = (nstages + sps - 1) / sps;
   dim3 grid(bx, ct);
-  const bool res = a.res != nullptr;
+  const int nres = a.res2 ? 2 : a.res ? 1 : 0;
   const bool stats = a.gn_sums != nullptr;
 #define DV_FS(WW, RR) (stats ? conv_fwd_stripe_kernel<WW, RR, true><<<grid, 512, 0, st>>>(a, nstages, sps) \
                              : conv_fwd_stripe_kernel<WW, RR, false><<<grid, 512, 0, st>>>(a, nstages, sps))
-  if (a.W == 64) {
-    if (res) DV_FS(64, true); else DV_FS(64, false);
-  } else {
-    if (res) DV_FS(32, true); else DV_FS(32, false);
-  }
+  // (two residuals come from dgrads only: no statistics epilogue beside them,
+  // whose registers would spill)
+#define DV_FSR(WW) (nres == 2 ? (void)conv_fwd_stripe_kernel<WW, 2, false><<<grid, 512, 0, st>>>(a, nstages, sps) \
+                              : nres == 1 ? DV_FS(WW, 1) : DV_FS(WW, 0))
+  if (a.W == 64) DV_FSR(64);
+  else DV_FSR(32);
+#undef DV_FSR
 #undef DV_FS
   return check_launch("conv_fwd_stripe");
 }
@@ -2347,7 +2378,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   const int cw = co0 + chh * CO;  // this wave's first output channel
   float sv[STATS ? CO : 1];  // STATS: [0,CO/2) sums, [CO/2,CO) squares of the lane's CO/2 channels
   f32x4 bb[NJ][4];
-  u32x2 rq[NJ][4];
+  u32x2 rq[NJ][4], rq2[NJ][4];
   if (p.bias) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -2359,6 +2390,12 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) rq[j][g] = *(const u32x2*)(p.res + m * p.ldres + cw + 32 * j + 8 * g + 4 * h);
+  }
+  if (p.res2) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) rq2[j][g] = *(const u32x2*)(p.res2 + m * p.ldres2 + cw + 32 * j + 8 * g + 4 * h);
   }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -2378,6 +2415,11 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
       }
       if (p.res) {
         const bf16x4 t4 = __builtin_bit_cast(bf16x4, rq[j][g]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (float)t4[e];
+      }
+      if (p.res2) {
+        const bf16x4 t4 = __builtin_bit_cast(bf16x4, rq2[j][g]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += (float)t4[e];
       }
@@ -2409,7 +2451,8 @@ bool fwd_frame_ok(const ConvFwdArgs<bf16>& a, int h, int w) {
   const bool geom = (h == 8 && w == 8) || ((w == 16 || w == 32 || w == 64) && (h * w) % 128 == 0);
   return a.ks == 3 && geom && a.cin % 16 == 0 && a.c0 % 16 == 0 && a.cout % 64 == 0 &&
          a.M % 128 == 0 && a.ld0 % 8 == 0 && a.ld1 % 8 == 0 && (a.ldy & 3) == 0 &&
-         (a.res == nullptr || (a.ldres & 3) == 0) && a.M * a.ld0 * 2 < maxb &&
+         (a.res == nullptr || (a.ldres & 3) == 0) && (a.res2 == nullptr || (a.ldres2 & 3) == 0) &&
+         a.M * a.ld0 * 2 < maxb &&
          a.M * a.ld1 * 2 < maxb && (long long)a.cout * a.K * 2 < maxb &&
          ((uintptr_t)a.x0 & 15) == 0 && ((uintptr_t)a.x1 & 15) == 0 && ((uintptr_t)a.w & 15) == 0;
 }
@@ -2492,13 +2535,17 @@ void set_gn(ConvFwdArgs<T>& a, float* gn_sums, long long gn_P, int gn_R) {
 
 template <typename T>
 int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const void* w,
-               const float* bias, const void* res, int ldres, void* y, int ldy, int nf, int h,
-               int wd, int cin, int cout, int ks, int act, float* gn_sums, long long gn_P,
-               int gn_R, hipStream_t st) {
+               const float* bias, const void* res, int ldres, const void* res2, int ldres2, void* y,
+               int ldy, int nf, int h, int wd, int cin, int cout, int ks, int act, float* gn_sums,
+               long long gn_P, int gn_R, hipStream_t st) {
+  if (!res && res2) {  // a lone second residual is the first
+    res = res2; ldres = ldres2; res2 = nullptr; ldres2 = 0;
+  }
   ConvFwdArgs<T> a;
   a.x0 = (const T*)x0; a.x1 = (const T*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0;
   a.c0 = x1 ? c0 : cin; a.w = (const T*)w; a.bias = bias; a.res = (const T*)res;
-  a.ldres = ldres; a.y = (T*)y; a.ldy = ldy; a.H = h; a.W = wd; a.cin = cin; a.cout = cout;
+  a.ldres = ldres; a.res2 = (const T*)res2; a.ldres2 = ldres2;
+  a.y = (T*)y; a.ldy = ldy; a.H = h; a.W = wd; a.cin = cin; a.cout = cout;
   a.ks = ks; a.act = act; a.M = (long long)nf * h * wd; a.K = ks * ks * cin;
   set_gn(a, gn_sums, gn_P, gn_R);
   if (a.M == 0 || cout == 0) return DV_OK;
@@ -2506,13 +2553,14 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
     // the stripe kernel flushes statistics per 128-pixel stage: clips must
     // be whole stages
     if (fwd_stripe_ok(a.M, h, wd, cin, x1 != nullptr, cout, ks, ld0) && (ldy & 3) == 0 &&
-        (res == nullptr || (ldres & 3) == 0) && (!gn_sums || gn_P % 128 == 0))
+        (res == nullptr || (ldres & 3) == 0) && (res2 == nullptr || ((ldres2 & 3) == 0 && !gn_sums)) &&
+        (!gn_sums || gn_P % 128 == 0))
       return launch_fwd_stripe(a, st);
     int seg, nseg;
     if (fwd_stripe2_ok(a.M, h, wd, cin, a.c0, x1 != nullptr, cout, ks, seg, nseg) &&
         a.M * std::max(ld0, x1 ? ld1 : 0) < (1ll << 31))
       return launch_fwd_stripe2(a, seg, nseg, st);
-    if (conv1x1_ok(a, x1 != nullptr)) {
+    if (conv1x1_ok(a, x1 != nullptr) && !res2) {  // (the streamed 1x1 takes one residual)
       if (cout == 64) return cin == 64 ? launch_conv1x1<64, 1>(a, st) : launch_conv1x1<64, 2>(a, st);
       return cin == 64 ? launch_conv1x1<128, 1>(a, st) : launch_conv1x1<128, 2>(a, st);
     }
@@ -3356,8 +3404,9 @@ int conv_wgrad_stripe(const void* dy, int lddy, const void* x0, int ld0, int c0,
 
 extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
                            const void* wpack, const float* bias, const void* res, int ldres,
-                           void* y, int ldy, int nf, int h, int w, int cin, int cout, int ksize,
-                           int act, float* gn_sums, long long gn_P, int gn_R, void* stream) {
+                           const void* res2, int ldres2, void* y, int ldy, int nf, int h, int w,
+                           int cin, int cout, int ksize, int act, float* gn_sums, long long gn_P,
+                           int gn_R, void* stream) {
   DV_REQUIRE(x0 && wpack && y, "null pointer");
   DV_REQUIRE(cin > 0 && cin % 8 == 0, "cin must be a positive multiple of 8");
   DV_REQUIRE(!gn_sums || (gn_P > 0 && ((long long)nf * h * w) % gn_P == 0 && gn_R >= 1),
@@ -3365,32 +3414,36 @@ extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const voi
   DV_REQUIRE(ld0 % 8 == 0 && (!x1 || (ld1 % 8 == 0 && c0 % 8 == 0 && c0 > 0 && c0 < cin)),
              "input strides / split must be multiples of 8");
   DV_REQUIRE(ksize >= 1 && (ksize & 1), "ksize must be odd");
-  DV_REQUIRE(ldy >= cout && (!res || ldres >= cout), "bad output stride");
+  DV_REQUIRE(ldy >= cout && (!res || ldres >= cout) && (!res2 || ldres2 >= cout), "bad output stride");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DV_F32)
-    return conv_fwd_t<float>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, y, ldy, nf, h, w,
-                             cin, cout, ksize, act, gn_sums, gn_P, gn_R, st);
+    return conv_fwd_t<float>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, res2, ldres2, y, ldy, nf,
+                             h, w, cin, cout, ksize, act, gn_sums, gn_P, gn_R, st);
   if (dtype == DV_BF16)
-    return conv_fwd_t<bf16>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, y, ldy, nf, h, w,
-                            cin, cout, ksize, act, gn_sums, gn_P, gn_R, st);
+    return conv_fwd_t<bf16>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, res2, ldres2, y, ldy, nf,
+                            h, w, cin, cout, ksize, act, gn_sums, gn_P, gn_R, st);
   DV_REQUIRE(false, "unknown dtype");
 }
 
 extern "C" int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
                             const void* wpack, const float* bias, const void* res, int ldres,
-                            void* y, int ldy, int nf, int h, int w, int cin, int cout, int act,
-                            float* gn_sums, long long gn_P, int gn_R, void* stream) {
+                            const void* res2, int ldres2, void* y, int ldy, int nf, int h, int w,
+                            int cin, int cout, int act, float* gn_sums, long long gn_P, int gn_R,
+                            void* stream) {
   DV_REQUIRE(dtype == DV_BF16, "the window conv is bf16 only");
   DV_REQUIRE(!gn_sums || (gn_P > 0 && gn_P % 128 == 0 && ((long long)nf * h * w) % gn_P == 0 &&
                           gn_R >= 1),
              "GroupNorm statistics in the window conv: clips of gn_P % 128 == 0 pixels");
   DV_REQUIRE(x0 && wpack && y, "null pointer");
   DV_REQUIRE(cin > 0 && (!x1 || (c0 > 0 && c0 < cin)), "bad channel split");
-  DV_REQUIRE(ldy >= cout && (!res || ldres >= cout), "bad output stride");
+  DV_REQUIRE(ldy >= cout && (!res || ldres >= cout) && (!res2 || ldres2 >= cout), "bad output stride");
+  if (!res && res2) {  // a lone second residual is the first
+    res = res2; ldres = ldres2; res2 = nullptr; ldres2 = 0;
+  }
   ConvFwdArgs<bf16> a;
   a.x0 = (const bf16*)x0; a.x1 = (const bf16*)(x1 ? x1 : x0); a.ld0 = ld0; a.ld1 = x1 ? ld1 : ld0;
   a.c0 = x1 ? c0 : cin; a.w = (const bf16*)wpack; a.bias = bias; a.res = (const bf16*)res;
-  a.ldres = ldres; a.y = (bf16*)y; a.ldy = ldy; a.H = h; a.W = w; a.cin = cin; a.cout = cout;
+  a.ldres = ldres; a.res2 = (const bf16*)res2; a.ldres2 = ldres2; a.y = (bf16*)y; a.ldy = ldy; a.H = h; a.W = w; a.cin = cin; a.cout = cout;
   a.ks = 3; a.act = act; a.M = (long long)nf * h * w; a.K = 9 * cin;
   set_gn(a, gn_sums, gn_P, gn_R);
   DV_REQUIRE(fwd_frame_ok(a, h, w), "shape/stride outside the window conv (see dv_hip.h)");

@@ -50,9 +50,11 @@ __global__ void cl_to_ncthw_kernel(const T* y, int ld, float* x, int B, int C, i
 // low-res rows (f, y), grid x a row's (x, channel group) units: one 32-bit
 // division per unit (a flat 64-bit index took four 64-bit divisions, each a
 // ~150-instruction sequence, and left the pass VALU-bound)
+// MODE 1 adds r0 / r1 (high-res, strides ldr0 / ldr1; null: none) to the output
 template <typename T, int MODE>
-__global__ void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* z, int ldz, int nf,
-                               int H, int W, int C, int act) {
+__global__ void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* z, int ldz,
+                               const T* r0, int ldr0, const T* r1, int ldr1, int nf, int H, int W,
+                               int C, int act) {
   constexpr int VEC = 16 / sizeof(T);
   const int cg = C / VEC;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -74,9 +76,24 @@ __global__ void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* 
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const long long hp = (f * 2 * H + 2 * y + i) * 2 * W + 2 * x + j;
+          float hv[VEC];
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) hv[e] = lo[e * 4 + i * 2 + j];
+          if (r0) {
+            float rv[VEC];
+            Vec<T>::to_f(*(const u32x4*)(r0 + hp * ldr0 + c0), rv);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) hv[e] += rv[e];
+          }
+          if (r1) {
+            float rv[VEC];
+            Vec<T>::to_f(*(const u32x4*)(r1 + hp * ldr1 + c0), rv);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) hv[e] += rv[e];
+          }
           T o[VEC];
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) o[e] = (T)lo[e * 4 + i * 2 + j];
+          for (int e = 0; e < VEC; ++e) o[e] = (T)hv[e];
           *(u32x4*)(dst + hp * ldd + c0) = *(const u32x4*)o;
         }
     } else {
@@ -663,22 +680,27 @@ extern "C" int dv_cl_to_ncthw(int dtype, const void* y, int ld, float* x, int B,
 }
 
 extern "C" int dv_shuffle(int dtype, int mode, const void* src, int lds, void* dst, int ldd,
-                          const void* z, int ldz, int nf, int H, int W, int C, int act,
-                          void* stream) {
+                          const void* z, int ldz, const void* r0, int ldr0, const void* r1,
+                          int ldr1, int nf, int H, int W, int C, int act, void* stream) {
   DV_REQUIRE(src && dst && (mode == 0 || mode == 1), "bad arguments");
+  DV_REQUIRE(mode == 1 || (!r0 && !r1), "residuals are added by mode 1 only");
+  if (!r0 && r1) {
+    r0 = r1; ldr0 = ldr1; r1 = nullptr;
+  }
   const int VEC = dtype == DV_BF16 ? 8 : 4;
-  DV_REQUIRE(C % VEC == 0 && lds % VEC == 0 && ldd % VEC == 0 && (!z || ldz % VEC == 0),
+  DV_REQUIRE(C % VEC == 0 && lds % VEC == 0 && ldd % VEC == 0 && (!z || ldz % VEC == 0) &&
+                 (!r0 || (ldr0 % VEC == 0 && ldr0 >= C)) && (!r1 || (ldr1 % VEC == 0 && ldr1 >= C)),
              "channels / strides must be multiples of 16 bytes");
   if ((long long)nf * H * W * C == 0) return DV_OK;
   DV_REQUIRE((long long)W * (C / VEC) < (1ll << 31) && (long long)nf * H < (1ll << 31), "shape too large");
   const dim3 grid((unsigned)((W * (C / VEC) + 255) / 256), (unsigned)std::min(nf * H, 65535));
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DV_F32) {
-    if (mode == 0) shuffle_kernel<float, 0><<<grid, 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, nf, H, W, C, act);
-    else shuffle_kernel<float, 1><<<grid, 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, nf, H, W, C, act);
+    if (mode == 0) shuffle_kernel<float, 0><<<grid, 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, (const float*)r0, ldr0, (const float*)r1, ldr1, nf, H, W, C, act);
+    else shuffle_kernel<float, 1><<<grid, 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, (const float*)r0, ldr0, (const float*)r1, ldr1, nf, H, W, C, act);
   } else {
-    if (mode == 0) shuffle_kernel<bf16, 0><<<grid, 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, nf, H, W, C, act);
-    else shuffle_kernel<bf16, 1><<<grid, 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, nf, H, W, C, act);
+    if (mode == 0) shuffle_kernel<bf16, 0><<<grid, 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, (const bf16*)r0, ldr0, (const bf16*)r1, ldr1, nf, H, W, C, act);
+    else shuffle_kernel<bf16, 1><<<grid, 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, (const bf16*)r0, ldr0, (const bf16*)r1, ldr1, nf, H, W, C, act);
   }
   return check_launch("shuffle");
 }

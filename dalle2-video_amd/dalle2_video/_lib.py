@@ -26,10 +26,10 @@ _F = ctypes.c_float
 _SIGS = {
     "dv_abi_version": [],
     "dv_zero_f32": [_P, _L, _P],
-    "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I,
-                    _P, _L, _I, _P],
-    "dv_conv_fwd8": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
-                     _P, _L, _I, _P],
+    "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
+                    _I, _P, _L, _I, _P],
+    "dv_conv_fwd8": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I,
+                     _I, _P, _L, _I, _P],
     "dv_mx8_quant": [_P, _I, _I, _L, _P, _P, _P],
     "dv_mx8_image_bytes": [_I, _I, _P],
     "dv_mx8_pack_conv_weight": [_P, _I, _I, _P, _P],
@@ -64,7 +64,7 @@ _SIGS = {
     "dv_ln_bwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _F, _P, _P, _P, _L, _P],
     "dv_ncthw_to_cl": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_cl_to_ncthw": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P],
-    "dv_shuffle": [_I, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dv_shuffle": [_I, _I, _P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P],
     "dv_q_sample": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_mse_loss": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P],
     "dv_mse_loss_bwd": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],

@@ -351,8 +351,8 @@ class NullVQGanVAE(nn.Module):
 
 
 class _Downsample3D(nn.Sequential):
-    def forward_cl(self, x):
-        return ops.conv(ops.space_to_depth(x), self[1].weight, self[1].bias)
+    def forward_cl(self, x, skip_in=None):
+        return ops.conv(ops.space_to_depth(x, skip_in=skip_in), self[1].weight, self[1].bias)
 
     def forward(self, x):
         b, c, t = x.shape[:3]
@@ -367,8 +367,8 @@ def Downsample3D(dim, dim_out=None):
 
 
 class _Conv1x1(nn.Conv3d):
-    def forward_cl(self, x):
-        return ops.conv(x, self.weight, self.bias)
+    def forward_cl(self, x, skip_in=None):
+        return ops.conv(x, self.weight, self.bias, skip_in=skip_in)
 
 
 class PixelShuffleUpsample3D(nn.Module):
@@ -405,12 +405,14 @@ class Block3D(nn.Module):
         self.norm = nn.GroupNorm(groups, dim_out)
         self.act = nn.SiLU()
 
-    def forward_cl(self, x0, nb, x1=None, scale_shift=None, res=None, sink=None, res_sink=None):
+    def forward_cl(self, x0, nb, x1=None, scale_shift=None, res=None, sink=None, res_sink=None,
+                   skip_in=None, skip_out=None):
         # the conv's epilogue accumulates the GroupNorm statistics of z, so the
         # norm is a single apply pass over z
         nf, h, w = x0.shape[:3]
         st = ops.gn_stats(nb, self.project.out_channels, (nf // nb) * h * w, x0.device)
-        z = ops.conv(x0, self.project.weight, self.project.bias, x1=x1, sink=sink, gn=st)
+        z = ops.conv(x0, self.project.weight, self.project.bias, x1=x1, sink=sink, gn=st,
+                     skip_in=skip_in, skip_out=skip_out)
         return ops.group_norm_act(z, self.norm.weight, self.norm.bias, nb, self.norm.num_groups,
                                   self.norm.eps, scale_shift=scale_shift, res=res, act=ACT_SILU,
                                   stats=st, res_sink=res_sink)
@@ -439,9 +441,13 @@ class ResnetBlock3D(nn.Module):
         self.block2 = Block3D(dim_out, dim_out, groups=groups, weight_standardization=weight_standardization)
         self.res_conv = nn.Conv3d(dim, dim_out, 1) if dim != dim_out else nn.Identity()
 
-    def forward_cl(self, x0, time_emb, cond, nb, x1=None, ss=None, kv=None, fold=None):
+    def forward_cl(self, x0, time_emb, cond, nb, x1=None, ss=None, kv=None, fold=None,
+                   skip_in=None, skip_out=None):
         """ss / kv: this block's time_mlp(time_emb) / to_kv(cond) when the Unet
-        computed them for all blocks in one grouped launch (ops.linear_group)."""
+        computed them for all blocks in one grouped launch (ops.linear_group).
+        skip_in: the ops.SkipGrad of x0 when x0 is a unet skip (block1's conv
+        adds its parked up-path gradients); skip_out: that of x1 when x1 is one
+        (the up-path dgrad parks dX1 there)."""
         if ss is None and exists(self.time_mlp) and exists(time_emb):
             ss = ops.linear_group(time_emb, [self.time_mlp[1].weight], [self.time_mlp[1].bias],
                                   act_in=ACT_SILU)[0]
@@ -460,8 +466,12 @@ class ResnetBlock3D(nn.Module):
             sink, res = ops.GradSink(), x0
         else:
             sink = ops.GradSink()
-            res = ops.conv(x0, self.res_conv.weight, self.res_conv.bias, x1=x1, sink=sink)
-        h = self.block1.forward_cl(x0, nb, x1=x1, scale_shift=ss, sink=sink)
+            res = ops.conv(x0, self.res_conv.weight, self.res_conv.bias, x1=x1, sink=sink,
+                           skip_out=skip_out)
+        # block1's conv is x0's gradient owner either way: the second reader of
+        # the shared buffer (identity) or the first (res_conv), so it takes skip_in
+        h = self.block1.forward_cl(x0, nb, x1=x1, scale_shift=ss, sink=sink, skip_in=skip_in,
+                                   skip_out=skip_out)
         if exists(self.cross_attn):
             assert exists(cond)
             h = self.cross_attn.forward_cl(h, cond, nb, kv=kv, fold=fold)
@@ -752,33 +762,44 @@ class Unet3D(nn.Module):
 
         mark = ops.backward_mark  # backward progress marks (trainer's overlapped all-reduce)
 
-        def run(blk, x, cond, x1=None):
+        def run(blk, x, cond, x1=None, skip_in=None, skip_out=None):
             ss, kv, fold = pre.get(id(blk), (None, None, None))
             mark(x)
-            return blk.forward_cl(x, t, cond, batch, x1=x1, ss=ss, kv=kv, fold=fold)
+            return blk.forward_cl(x, t, cond, batch, x1=x1, ss=ss, kv=kv, fold=fold,
+                                  skip_in=skip_in, skip_out=skip_out)
 
+        # every skip (r and the hiddens) carries an ops.SkipGrad: its up-path
+        # readers park their input gradient there and its down-path reader adds
+        # them in its own kernel -- no autograd sum of strided gradient views
+        skip_r = ops.SkipGrad()
+        pending = skip_r  # the SkipGrad of the next down-path block's input
         hiddens = []
         for _, init_block, blocks, attn, post in self.downs:
-            x = run(init_block, x, c)
+            x = run(init_block, x, c, skip_in=pending)
+            pending = None
             for blk in blocks:
-                x = run(blk, x, c)
-                hiddens.append(x)
-            hiddens.append(x)  # after the Identity attention
+                x = run(blk, x, c, skip_in=pending)
+                pending = ops.SkipGrad()
+                hiddens.append((x, pending))
+            hiddens.append((x, pending))  # after the Identity attention
             mark(x)
-            x = post.forward_cl(x)
+            x = post.forward_cl(x, skip_in=pending)
+            pending = None
         x = run(self.mid_block1, x, mid_c)
         if exists(self.mid_attn):
             mark(x)
             x = self.mid_attn.forward_cl(x, batch)
         x = run(self.mid_block2, x, mid_c)
         for init_block, blocks, attn, up in self.ups:
-            x = run(init_block, x, c, x1=hiddens.pop())
+            hx, hs = hiddens.pop()
+            x = run(init_block, x, c, x1=hx, skip_out=hs)
             for blk in blocks:
-                x = run(blk, x, c, x1=hiddens.pop())
+                hx, hs = hiddens.pop()
+                x = run(blk, x, c, x1=hx, skip_out=hs)
             if not isinstance(up, nn.Identity):
                 mark(x)
                 x = up.forward_cl(x)
-        x = run(self.final_resnet_block, x, None, x1=r)
+        x = run(self.final_resnet_block, x, None, x1=r, skip_out=skip_r)
         mark(x)
         return ops.conv(x, self.to_out.weight, self.to_out.bias, x1=lowres_cl)
 

@@ -108,7 +108,7 @@ def _launch(name, flops, nbytes, fn, shape=None):
         TIMER.run(name, flops, nbytes, fn, shape)
 
 
-def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0):
+def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0, nres2=False):
     """Kernel instantiation dv_conv_fwd dispatches to (mirror of conv_fwd_t /
     glds_tile in dv_conv.hip) — names the launch for the live roofline."""
     if (dtype_name == "bf16" and ks == 3 and cin == 64 and c0 == cin and cout % 64 == 0
@@ -120,7 +120,7 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0):
             and (w == 8 or (w == 16 and cin * cout <= 256 * 256))):
         return f"conv_fwd_stripe2_kernel<{w}>"
     if (dtype_name == "bf16" and ks == 1 and cin in (64, 128) and c0 in (cin, 64) and cout in (64, 128)
-            and gn_P == 0 and m * maxld < (1 << 31)):
+            and gn_P == 0 and not nres2 and m * maxld < (1 << 31)):
         return f"conv1x1_stream_kernel<{cout},{cin // 64}>"
     if dtype_name == "bf16" and cin % 64 == 0 and c0 % 64 == 0 and m * maxld < (1 << 31):
         bn = 64 if cout <= 64 else 128
@@ -146,7 +146,7 @@ _NO_WINDOW = bool(os.environ.get("DV_NO_WINDOW"))  # A/B switch: 3x3 convs on dv
 _WINDOW_W = tuple(int(v) for v in os.environ.get("DV_WINDOW_W", "8,16").split(",") if v)
 
 
-def window_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf, gn_P=0):
+def window_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf, gn_P=0, ldres2=0):
     """Mirror of fwd_frame_ok (dv_conv.hip): the window-form 3x3 conv (dv_conv_fwd8);
     with the GroupNorm statistics epilogue its clips must be whole 128-pixel tiles."""
     geom = (h == 8 and w == 8 and nf % 2 == 0) or (w in (16, 32, 64) and (h * w) % 128 == 0)
@@ -154,7 +154,7 @@ def window_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf, gn_P
             and gn_P % 128 == 0
             and geom and cin % 16 == 0 and c0 % 16 == 0 and cout % 64 == 0
             and not (cin == 64 and c0 == cin and w in (32, 64))  # the resident-weight stripe kernel
-            and ld0 % 8 == 0 and ld1 % 8 == 0 and ldy % 4 == 0 and ldres % 4 == 0
+            and ld0 % 8 == 0 and ld1 % 8 == 0 and ldy % 4 == 0 and ldres % 4 == 0 and ldres2 % 4 == 0
             and nf * h * w * max(ld0, ld1) * 2 < (1 << 31)
             and x0.data_ptr() % 16 == 0 and (x1 is None or x1.data_ptr() % 16 == 0))
 
@@ -752,6 +752,56 @@ class GradSink:
         self.dx = None
 
 
+class SkipGrad:
+    """Gradient hand-off of a unet skip tensor: the hiddens the down path
+    pushes and the up path pops as the second input of its channel concats
+    (dalle2_video.py:926-936).  A hidden has one down-path reader (the
+    consumer: the next block's conv, or the downsample) and one or two
+    up-path readers.  The up-path convs run first in the backward (the
+    consumer's output feeds them), so instead of returning their dX1 -- a
+    strided channel slice of their [dX0 | dX1] buffer -- for autograd to add
+    to the consumer's gradient, they park it here; the consumer adds what is
+    parked in its own kernel (a dgrad epilogue residual, or the space-to-depth
+    backward's residual inputs) and closes the hand-off.  A reader that comes
+    after the close, or a hand-off whose consumer takes no input gradient (not
+    armed), returns its gradient to autograd as usual: no order loses one."""
+
+    def __init__(self):
+        self.armed = False
+        self.closed = False
+        self.parked = []
+        self.n_parked = 0  # gradients handed over (diagnostics / tests)
+
+    def arm(self, needs_grad):
+        """Consumer's forward (ctx.needs_input_grad of its input: grad mode is
+        off inside a Function's forward): only a consumer computing dX takes."""
+        if needs_grad:
+            self.armed = True
+
+    def park(self, g):
+        if not self.armed or self.closed:
+            return False
+        self.parked.append(g)
+        self.n_parked += 1
+        return True
+
+    def take(self):
+        self.closed = True
+        out, self.parked = self.parked, []
+        return out
+
+
+def _take_skips(skip, like):
+    """The parked skip gradients a consumer adds (shape-checked)."""
+    if skip is None:
+        return []
+    out = skip.take()
+    for g in out:
+        if tuple(g.shape) != tuple(like.shape):
+            raise _lib.DVError(f"skip gradient {tuple(g.shape)} does not match {tuple(like.shape)}")
+    return out
+
+
 # ---------------------------------------------------------------------------
 # MX-fp8 3x3 convs for sampling (BASELINE config 5; dv_mx8.hip)
 # ---------------------------------------------------------------------------
@@ -874,7 +924,7 @@ class ConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x0, x1, weight, bias, res, ksize, sink=None, cache=True, algo_scale=1.0,
-                gn=None):
+                gn=None, skip_in=None, skip_out=None):
         require_gpu(x0, x1, weight, bias, res)
         nf, h, w, c0 = x0.shape
         c1 = 0 if x1 is None else x1.shape[3]
@@ -924,21 +974,24 @@ class ConvFn(torch.autograd.Function):
             wp = pack_conv_weight(weight, x0.dtype, cin, 2, cache)
             _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                     lambda: call("dv_conv_fwd8", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp),
-                                 ptr(b), ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ACT_NONE,
-                                 gs, gP, gR, stream()), shape)
+                                 ptr(b), ptr(res), ldr, None, 0, ptr(y), cout, nf, h, w, cin, cout,
+                                 ACT_NONE, gs, gP, gR, stream()), shape)
         else:
             wp = pack_conv_weight(weight, x0.dtype, cin, 0, cache)
             _launch(conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
                                   max(ld0, ld1), ksize, h, w, gP), flops, nbytes,
                     lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b),
-                                 ptr(res), ldr, ptr(y), cout, nf, h, w, cin, cout, ksize, ACT_NONE,
-                                 gs, gP, gR, stream()), shape)
+                                 ptr(res), ldr, None, 0, ptr(y), cout, nf, h, w, cin, cout, ksize,
+                                 ACT_NONE, gs, gP, gR, stream()), shape)
         ctx.save_for_backward(x0, x1, weight)
         ctx.params = (weight, bias)
         ctx.meta = (ksize, c0, c1, bias is not None, res is not None)
         ctx.sink = sink
         ctx.cache = cache
         ctx.algo_scale = algo_scale
+        if skip_in is not None and x1 is None:
+            skip_in.arm(ctx.needs_input_grad[0])
+        ctx.skip_in, ctx.skip_out = skip_in, skip_out
         return y
 
     @staticmethod
@@ -968,29 +1021,41 @@ class ConvFn(torch.autograd.Function):
             # the accumulated buffer may be a strided channel view (the dy a
             # GroupNorm handed over): read and write it through its pixel stride
             ldx = cl_ld(dx) if acc is not None else cin
-            rp, rld = (ptr(dx), ldx) if acc is not None else (None, 0)
+            # epilogue residuals: the shared buffer (in place), then the unet
+            # skip gradients parked for this input (SkipGrad); more than two
+            # (none in Unet3D) are added after the launch
+            resid = ([dx] if acc is not None else []) + (
+                _take_skips(ctx.skip_in, dx) if ctx.needs_input_grad[0] and x1 is None else [])
+            rp, rld = (ptr(resid[0]), cl_ld(resid[0])) if resid else (None, 0)
+            rp2, rld2 = (ptr(resid[1]), cl_ld(resid[1])) if len(resid) > 1 else (None, 0)
             m = nf * h * w
             flops = 2.0 * m * cin_real * cout8 * ksize * ksize * ctx.algo_scale
             nbytes = dy8.element_size() * m * (cin + cout8)
             shape = ("dgrad", m, cin_real, cout8 * ksize * ksize)
-            if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, ldx, rld, ksize, h, w, nf):
+            if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, ldx, rld, ksize, h, w, nf,
+                         ldres2=rld2):
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 3, ctx.cache)
                 _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                         lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd),
-                                     None, rp, rld, ptr(dx), ldx, nf, h, w, cout8, cin_real, ACT_NONE,
-                                     None, 0, 0, stream()), shape)
+                                     None, rp, rld, rp2, rld2, ptr(dx), ldx, nf, h, w, cout8, cin_real,
+                                     ACT_NONE, None, 0, 0, stream()), shape)
             else:
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 1, ctx.cache)
-                _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, lddy, ksize, h, w),
+                _launch(conv_fwd_name(_lib.dtype_name(dy8), m, cout8, cout8, cin_real, lddy, ksize, h, w,
+                                      nres2=rp2 is not None),
                         flops, nbytes,
                         lambda: call("dv_conv_fwd", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd), None,
-                                     rp, rld, ptr(dx), ldx, nf, h, w, cout8, cin_real, ksize, ACT_NONE,
-                                     None, 0, 0, stream()), shape)
+                                     rp, rld, rp2, rld2, ptr(dx), ldx, nf, h, w, cout8, cin_real, ksize,
+                                     ACT_NONE, None, 0, 0, stream()), shape)
+            for g in resid[2:]:
+                dx.add_(g)
             if sink is not None and acc is None:
                 sink.dx = dx  # first reader: the other conv's backward adds into it
             else:
                 dx0 = dx[..., :c0]
                 dx1 = dx[..., c0:] if x1 is not None else None
+                if dx1 is not None and ctx.skip_out is not None and ctx.skip_out.park(dx1):
+                    dx1 = None  # the skip's down-path reader adds it in its kernel
         wparam, bparam = ctx.params
         want_w = ctx.needs_input_grad[2]
         want_b = has_bias and ctx.needs_input_grad[3]
@@ -1040,7 +1105,7 @@ class ConvFn(torch.autograd.Function):
                 if ent.S > 0:
                     WGRAD_DEFER.add(ent, dy.device)
                 dres = dy if has_res else None
-                return dx0, dx1, dw, db, dres, None, None, None, None, None
+                return dx0, dx1, dw, db, dres, None, None, None, None, None, None, None
             WGRAD_DEFER.before_write(dw_t.data_ptr(), db_t.data_ptr() if db_t is not None else None)
             ws = _wgrad_workspace(_lib.dtype_name(dy8), nf, h, w, cin, c0, x1 is not None, cout8,
                                   ksize, dy.device)
@@ -1072,7 +1137,7 @@ class ConvFn(torch.autograd.Function):
             elif db_buf is not bslot[0]:
                 bslot[0].add_(db_buf[:cout])
         dres = dy if has_res else None
-        return dx0, dx1, dw, db, dres, None, None, None, None, None
+        return dx0, dx1, dw, db, dres, None, None, None, None, None, None, None
 
 
 # small-channel forward (cin <= 16, cout <= 32: the cascade's 256x256 unet at
@@ -1120,7 +1185,8 @@ def _small_image(weight, bias, cin, cout, k, cache):
     return img
 
 
-def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_scale=1.0, gn=None):
+def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_scale=1.0, gn=None,
+         skip_in=None, skip_out=None):
     """(1,k,k) 'same' convolution over channels-last frames (weight in torch
     Conv3d layout (cout, cin, 1, k, k) or Linear layout (cout, cin)).
     sink: a GradSink shared with the other conv reading (x0, x1).
@@ -1128,9 +1194,12 @@ def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_s
     packed image is made on every call instead of kept in the PackCache.
     algo_scale: algorithmic / executed FLOPs (timing labels only).
     gn: a GnStats (gn_stats()) — the kernel's epilogue accumulates the
-    GroupNorm statistics of y for the group_norm_act(stats=gn) that follows."""
+    GroupNorm statistics of y for the group_norm_act(stats=gn) that follows.
+    skip_in: the SkipGrad of x0 when this conv is its down-path reader (the
+    dgrad adds the parked skip gradients); skip_out: the SkipGrad of x1 when
+    x1 is a unet skip (the dgrad parks dX1 there)."""
     k = weight.shape[-1] if weight.dim() == 5 else 1
-    return ConvFn.apply(x0, x1, weight, bias, res, k, sink, cache, algo_scale, gn)
+    return ConvFn.apply(x0, x1, weight, bias, res, k, sink, cache, algo_scale, gn, skip_in, skip_out)
 
 
 # ---------------------------------------------------------------------------
@@ -1861,12 +1930,16 @@ def mqa(q, kv, null_kv, B, N, H, scale):
 # ---------------------------------------------------------------------------
 class SpaceToDepthFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, skip_in=None):
         require_gpu(x)
         nf, H2, W2, C = x.shape
         H, W = H2 // 2, W2 // 2
         y = torch.empty(nf, H, W, 4 * C, dtype=x.dtype, device=x.device)
-        call("dv_shuffle", dt(x), 0, ptr(x), cl_ld(x), ptr(y), 4 * C, None, 0, nf, H, W, C, 0, stream())
+        call("dv_shuffle", dt(x), 0, ptr(x), cl_ld(x), ptr(y), 4 * C, None, 0, None, 0, None, 0,
+             nf, H, W, C, 0, stream())
+        if skip_in is not None:
+            skip_in.arm(ctx.needs_input_grad[0])
+        ctx.skip_in = skip_in
         return y
 
     @staticmethod
@@ -1875,8 +1948,16 @@ class SpaceToDepthFn(torch.autograd.Function):
         nf, H, W, C4 = dy.shape
         C = C4 // 4
         dx = torch.empty(nf, 2 * H, 2 * W, C, dtype=dy.dtype, device=dy.device)
-        call("dv_shuffle", dt(dy), 1, ptr(dy), ldd, ptr(dx), C, None, 0, nf, H, W, C, 0, stream())
-        return dx
+        # the skip gradients of x (the level's last hidden, read twice by the
+        # up path) are added by the depth-to-space pass itself
+        sk = _take_skips(ctx.skip_in, dx)
+        r0, l0 = (ptr(sk[0]), cl_ld(sk[0])) if sk else (None, 0)
+        r1, l1 = (ptr(sk[1]), cl_ld(sk[1])) if len(sk) > 1 else (None, 0)
+        call("dv_shuffle", dt(dy), 1, ptr(dy), ldd, ptr(dx), C, None, 0, r0, l0, r1, l1, nf, H, W, C, 0,
+             stream())
+        for g in sk[2:]:
+            dx.add_(g)
+        return dx, None
 
 
 class SiLUPixelShuffleFn(torch.autograd.Function):
@@ -1886,7 +1967,8 @@ class SiLUPixelShuffleFn(torch.autograd.Function):
         nf, H, W, C4 = z.shape
         C = C4 // 4
         y = torch.empty(nf, 2 * H, 2 * W, C, dtype=z.dtype, device=z.device)
-        call("dv_shuffle", dt(z), 1, ptr(z), cl_ld(z), ptr(y), C, None, 0, nf, H, W, C, _lib.ACT_SILU, stream())
+        call("dv_shuffle", dt(z), 1, ptr(z), cl_ld(z), ptr(y), C, None, 0, None, 0, None, 0, nf, H, W, C,
+             _lib.ACT_SILU, stream())
         ctx.save_for_backward(z)
         return y
 
@@ -1897,12 +1979,13 @@ class SiLUPixelShuffleFn(torch.autograd.Function):
         nf, H, W, C4 = z.shape
         C = C4 // 4
         dz = torch.empty(nf, H, W, C4, dtype=z.dtype, device=z.device)
-        call("dv_shuffle", dt(z), 0, ptr(dy), ldd, ptr(dz), C4, ptr(z), cl_ld(z), nf, H, W, C, 0, stream())
+        call("dv_shuffle", dt(z), 0, ptr(dy), ldd, ptr(dz), C4, ptr(z), cl_ld(z), None, 0, None, 0,
+             nf, H, W, C, 0, stream())
         return dz
 
 
-def space_to_depth(x):
-    return SpaceToDepthFn.apply(x)
+def space_to_depth(x, skip_in=None):
+    return SpaceToDepthFn.apply(x, skip_in)
 
 
 def silu_pixel_shuffle(z):

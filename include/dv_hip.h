@@ -47,7 +47,10 @@ int dv_zero_f32(float* p, long long n, void* stream);
  * Input channels [0,c0) come from x0 (stride ld0), [c0,cin) from x1 (ld1);
  * c0 must be a multiple of 8 (pass c0=cin, x1=NULL for one source).
  * wpack: packed weight [cout][k*k][cin] of `dtype` (dv_pack_conv_weight).
- * Epilogue: y = act(acc + bias) + res.  cin % 8 == 0 required.
+ * Epilogue: y = act(acc + bias) + res + res2 (res / res2 may be NULL; each
+ * with its own pixel stride; res2 carries the unet skip gradient a dgrad
+ * adds besides the shared input-gradient buffer, ops.SkipGrad, the hiddens
+ * of dalle2_video.py:926-936).  cin % 8 == 0 required.
  * GroupNorm statistics epilogue (Block3D conv -> GroupNorm, :107-109): when
  * gn_sums != NULL the stored y's per-(clip, channel) sum and sum of squares
  * are added into gn_sums[replica][nf*h*w / gn_P][cout][2] (zero on entry;
@@ -56,8 +59,9 @@ int dv_zero_f32(float* p, long long n, void* stream);
  * reduce pass.  NULL: no statistics (gn_P / gn_R ignored).                */
 int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
                 const void* wpack, const float* bias, const void* res, int ldres,
-                void* y, int ldy, int nf, int h, int w, int cin, int cout, int ksize,
-                int act, float* gn_sums, long long gn_P, int gn_R, void* stream);
+                const void* res2, int ldres2, void* y, int ldy, int nf, int h, int w, int cin,
+                int cout, int ksize, int act, float* gn_sums, long long gn_P, int gn_R,
+                void* stream);
 
 /* Weight (and fused bias) gradient of dv_conv_fwd, written in torch layout:
  * dw (cout_real, cin_real, 1, k, k) (+)= sum_p dY[p][co] X[p + tap][ci]
@@ -162,13 +166,13 @@ int dv_conv_small_fwd(const void* x0, int ld0, int c0, const void* x1, int ld1, 
  * image of dv_pack_conv_weight mode 2 (forward) or 3 (dgrad).  bf16 only;
  * needs (h, w) = (8, 8) with nf even, or w in {16, 32, 64} with
  * h * w % 128 == 0; cin % 16 == 0, c0 % 16 == 0 (split), cout % 64 == 0,
- * ld0 / ld1 % 8 == 0, ldy / ldres % 4 == 0, 16-B aligned x0 / x1 / wpack,
+ * ld0 / ld1 % 8 == 0, ldy / ldres / ldres2 % 4 == 0, 16-B aligned x0 / x1 / wpack,
  * nf * h * w * ld * 2 < 2^31; returns DV_ERR_INVALID otherwise.
  * gn_sums / gn_P / gn_R as dv_conv_fwd, with gn_P % 128 == 0.             */
 int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,
-                 const void* wpack, const float* bias, const void* res, int ldres, void* y,
-                 int ldy, int nf, int h, int w, int cin, int cout, int act, float* gn_sums,
-                 long long gn_P, int gn_R, void* stream);
+                 const void* wpack, const float* bias, const void* res, int ldres,
+                 const void* res2, int ldres2, void* y, int ldy, int nf, int h, int w, int cin,
+                 int cout, int act, float* gn_sums, long long gn_P, int gn_R, void* stream);
 
 /* ---- MX-fp8 3x3 forward (sampling; BASELINE config 5 — Block3D.project,
  * dalle2_video.py:107, no autograd).  OCP MX-fp8: e4m3 elements, one e8m0
@@ -331,9 +335,12 @@ int dv_cl_to_ncthw(int dtype, const void* y, int ld, float* x, int B, int C, int
  * mode 1: PixelShuffle(2) after SiLU (PixelShuffleUpsample3D,
  * dalle2_video.py:64-79), src [nf][H][W][4C] -> dst [nf][2H][2W][C];
  * backward passes use the inverse mode, with z (the pre-SiLU conv output)
- * for SiLU' when act = DV_ACT_SILU.                                         */
+ * for SiLU' when act = DV_ACT_SILU.  Mode 1 adds r0 / r1 ([nf][2H][2W][C],
+ * strides ldr0 / ldr1; NULL: none) to its output: the space-to-depth
+ * backward sums the unet skip gradients of its input there (ops.SkipGrad). */
 int dv_shuffle(int dtype, int mode, const void* src, int lds, void* dst, int ldd, const void* z,
-               int ldz, int nf, int H, int W, int C, int act, void* stream);
+               int ldz, const void* r0, int ldr0, const void* r1, int ldr1, int nf, int H, int W,
+               int C, int act, void* stream);
 
 /* ---- diffusion step pieces (VideoDecoder.p_losses, dalle2_video.py:1908-2010)
  * x_noisy = sqrt_ac[t]*x0 + sqrt_1m_ac[t]*noise, written channels-last into

@@ -22,7 +22,7 @@ def bench(nf, h, w, cin, cout, iters=50):
     b = torch.randn(cout, device="cuda", generator=g)
     y = torch.empty(nf, h, w, cout, device="cuda", dtype=torch.bfloat16)
     wp = ops.pack_conv_weight(wt, torch.bfloat16, cin, 2, cache=False)
-    f = lambda: call("dv_conv_fwd8", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y), cout,
+    f = lambda: call("dv_conv_fwd8", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, None, 0, ptr(y), cout,
                      nf, h, w, cin, cout, 0, None, 0, 0, stream())
     for _ in range(5):
         f()

@@ -30,10 +30,10 @@ def case(nb, T, h, w, cin, cout, R_list=(0, 8, 64), x1c=0):
     for R in R_list:
         gs = ptr(sums) if R else None
         if win:
-            fn = lambda: call("dv_conv_fwd8", dt(x), ptr(x), c0, c0, ptr(x1), x1c, ptr(wp), ptr(b), None, 0,
+            fn = lambda: call("dv_conv_fwd8", dt(x), ptr(x), c0, c0, ptr(x1), x1c, ptr(wp), ptr(b), None, 0, None, 0,
                               ptr(y), cout, nf, h, w, cin, cout, 0, gs, P, R, stream())
         else:
-            fn = lambda: call("dv_conv_fwd", dt(x), ptr(x), c0, c0, ptr(x1), x1c, ptr(wp), ptr(b), None, 0,
+            fn = lambda: call("dv_conv_fwd", dt(x), ptr(x), c0, c0, ptr(x1), x1c, ptr(wp), ptr(b), None, 0, None, 0,
                               ptr(y), cout, nf, h, w, cin, cout, 3, 0, gs, P, R, stream())
         out.append(timeit(fn) * 1e3)
     # the separate GroupNorm reduce + apply vs apply only

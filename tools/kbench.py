@@ -33,12 +33,12 @@ def conv_case(nf, h, w, cin, cout, k, dtype=torch.bfloat16):
     if ops.window_ok(x, None, cin, cin, cout, cin, cin, cout, 0, k, h, w, nf):
         wp = ops.pack_conv_weight(wt, dtype, cin, 2)
         def fwd():
-            call("dv_conv_fwd8", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
+            call("dv_conv_fwd8", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, None, 0, ptr(y),
                  cout, nf, h, w, cin, cout, 0, None, 0, 0, stream())
     else:
         wp = ops.pack_conv_weight(wt, dtype, cin, 0)
         def fwd():
-            call("dv_conv_fwd", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
+            call("dv_conv_fwd", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), None, 0, None, 0, ptr(y),
                  cout, nf, h, w, cin, cout, k, 0, None, 0, 0, stream())
     ms = timeit(fwd)
     dy = torch.randn_like(y)
@@ -74,7 +74,7 @@ if __name__ == "__main__":
         y = torch.empty_like(x)
         from dalle2_video._lib import call, ptr, stream, dt
         for _ in range(20):
-            call("dv_conv_fwd", dt(x), ptr(x), 64, 64, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
+            call("dv_conv_fwd", dt(x), ptr(x), 64, 64, None, 0, ptr(wp), ptr(b), None, 0, None, 0, ptr(y),
                  64, 64, 64, 64, 64, 64, 3, 0, None, 0, 0, stream())
         torch.cuda.synchronize()
         sys.exit(0)
@@ -86,7 +86,7 @@ if __name__ == "__main__":
         y = torch.empty_like(x)
         from dalle2_video._lib import call, ptr, stream, dt
         for _ in range(20):
-            call("dv_conv_fwd8", dt(x), ptr(x), 512, 512, None, 0, ptr(wp), ptr(b), None, 0, ptr(y),
+            call("dv_conv_fwd8", dt(x), ptr(x), 512, 512, None, 0, ptr(wp), ptr(b), None, 0, None, 0, ptr(y),
                  512, 64, 8, 8, 512, 512, 0, None, 0, 0, stream())
         torch.cuda.synchronize()
         sys.exit(0)
