@@ -669,7 +669,29 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(ConvFwdArgs<bf16> p,
 // vmcnt per tile, every DMA issued unconditionally (tiles past the end read
 // the zero line) so the count is a constant.
 // 8 waves = 4 pixel groups of 32 x 2 channel halves of BN / 2.
+// The residual loads are inline asm: hipcc cannot count them against the
+// LDS-DMA queue and drained it (vmcnt(0)) at every tile, twice, when they were
+// compiler-visible.  Two register sets alternate (the loop is unrolled by two)
+// so a prefetched residual is never copied before it lands, and the
+// top-of-tile wait is tied to the set it releases.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ u32x2 gload_b64_asm(const void* ptr) {
+  u32x2 v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
+  return v;
+}
+template <int N, int R>
+__device__ __forceinline__ void vm_wait_tied(u32x2 (&v)[R]) {
+  static_assert(R == 1 || R == 4 || R == 8, "residual sets of 1 / 4 / 8");
+  if constexpr (R == 8)
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                 : "n"(N) : "memory");
+  else if constexpr (R == 4)
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : "n"(N) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v[0]) : "n"(N) : "memory");
+}
 template <int BN, int KT, int NB, bool RES>
 __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p, int ntiles) {
   constexpr int BM = 128;
@@ -706,8 +728,9 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
     }
   };
   // residual of this lane's outputs (pixel row r of group wm, channels n0 + 8g + 4h .. +3)
-  u32x2 rcur[RES ? 4 * TJ : 1], rnxt[RES ? 4 * TJ : 1];
-  auto load_res = [&](int t, u32x2 (&dst)[RES ? 4 * TJ : 1]) {
+  constexpr int NR = RES ? 4 * TJ : 1;
+  u32x2 resA[NR], resB[NR];
+  auto load_res = [&](int t, u32x2 (&dst)[NR]) {
     if constexpr (RES) {
       long long m = (long long)t * BM + wm * 32 + r;
       if (t >= ntiles || m >= p.M) m = 0;  // a valid address; the value is not stored
@@ -716,7 +739,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int n = wn * (BN / 2) + 32 * j + 8 * g + 4 * h;
-          dst[4 * j + g] = *(const u32x2*)(p.res + m * p.ldres + n);
+          dst[4 * j + g] = gload_b64_asm(p.res + m * p.ldres + n);
         }
     }
   };
@@ -740,7 +763,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
   int t = blockIdx.x;
 #pragma unroll
   for (int i = 0; i < NB - 2; ++i) issue_x(t + i * (int)gridDim.x, i);
-  load_res(t, rcur);
+  load_res(t, resA);
   issue_x(t + (NB - 2) * (int)gridDim.x, NB - 2);
 
   float bias[TJ][4][4];
@@ -754,11 +777,13 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
         bias[j][g][e] = p.bias ? p.bias[n] : 0.f;
       }
 
-  for (int it = 0; t < ntiles; ++it, t += gridDim.x) {
+  // one tile: its residual in `rcur` (prefetched a tile ago), the next tile's into `rnxt`
+  auto tile = [&](int it, u32x2 (&rcur)[NR], u32x2 (&rnxt)[NR]) {
     const int buf = it % NB;
     load_res(t + (int)gridDim.x, rnxt);
     issue_x(t + (NB - 1) * (int)gridDim.x, (it + NB - 1) % NB);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * XD + RL) : "memory");
+    if constexpr (RES) vm_wait_tied<2 * XD + RL>(rcur);
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * XD + RL) : "memory");
     __builtin_amdgcn_s_barrier();
     f32x16 acc[TJ];
 #pragma unroll
@@ -802,15 +827,20 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
           store4<bf16>(p.y + m * p.ldy + n, v);
         }
     }
-    if constexpr (RES) {
-#pragma unroll
-      for (int q = 0; q < 4 * TJ; ++q) rcur[q] = rnxt[q];
-    }
     // every wave's reads of `buf` are done before the next iteration re-fills it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+  };
+  for (int it = 0; t < ntiles;) {
+    tile(it, resA, resB);
+    ++it;
+    t += gridDim.x;
+    if (t >= ntiles) break;
+    tile(it, resB, resA);
+    ++it;
+    t += gridDim.x;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing DMAs (zero line) drain
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing DMAs and residual loads drain
 }
 
 // ---------------------------------------------------------------------------
@@ -2174,21 +2204,33 @@ __device__ __forceinline__ int fw_pix(int r) {
 // NWV = 8: a 128-pixel x 2*CO-channel tile per workgroup, waves 4-7 on the
 // second channel half (the pixel window is staged once for both halves): for
 // the grids whose CO-channel tiles would run in two rounds on the 256 CUs.
+// TS (tap split, round 5; NWV = 8): the same 128 x CO tile as 4 waves, but 8
+// waves, waves 4-7 taking taps 5-8 of every chunk and waves 0-3 taps 0-4:
+// two waves per SIMD on the M = 4,096 grids whose tile count already equals
+// the CU count (one tile per CU leaves one wave per SIMD to hide every LDS /
+// DMA latency with its own MFMAs).  Same ring, same LDS reads and DMA pieces
+// per MFMA; the halves' partial sums meet in LDS and each half stores 32 of
+// the CO channels.
 // (Measured and removed in round 5, see DESIGN.md: a K split over two
 // workgroups per tile, register staging, one barrier per two chunks.)
-template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4>
+template <int W, bool STATS = false, int PF = 2, int DEFER = 0, int CO = 64, bool SPLIT = true, int NWV = 4,
+          bool TS = false>
 __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf16> p) {
-  using G = FwGeom<W, CO, NWV>;
-  constexpr int NPW = G::NPW, PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
-  constexpr int WPC = G::WPC, NJ = CO / 32, CG = G::CG;
-  static_assert(NWV == 4 || (NWV == 8 && !STATS), "the 8-wave tile has no statistics epilogue");
+  using G = FwGeom<W, CO, TS ? 4 : NWV>;
+  constexpr int PIECES = G::PIECES, BUF = G::BUF, NBUF = G::NBUF, WQ = G::WQ;
+  constexpr int NPW = (PIECES + NWV - 1) / NWV;  // DMA pieces per wave per chunk
+  constexpr int WPC = G::WPC, NJ = TS ? 1 : CO / 32, CG = G::CG;
+  static_assert(NWV == 4 || (NWV == 8 && (TS || !STATS)), "the 8-wave 2*CO tile has no statistics epilogue");
+  static_assert(!TS || (NWV == 8 && CO == 64), "the tap split runs 8 waves on a 64-channel tile");
   static_assert(NPW <= 9, "one DMA piece per tap");
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF];
   DV_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
   // masked: the DMA piece type folds per (wave, i) at compile time
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6) & (NWV - 1);
-  const int wq = wave & 3, chh = wave >> 2;  // pixel sub-tile, channel half
+  const int wq = wave & 3;                    // pixel sub-tile
+  const int chh = TS ? 0 : wave >> 2;         // channel half (NWV = 8 without TS)
+  const int half = TS ? wave >> 2 : 0;        // tap half (TS)
   const int npx = (int)(p.M / 128), nblk = npx * (p.cout / CG);
   int L = blockIdx.x;
   int co0;
@@ -2284,10 +2326,11 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   // DEFER = 2: taps 7 and 8 (slot 0: tap 7, odd -> chains 2 / 3; slot 1: tap 8)
   static_assert(DEFER <= 2, "at most the last two taps are deferred");
   u32x4 lb[2], la0[2], la1[2];
-  auto run_deferred = [&]() {
+  auto run_deferred = [&](auto HALF) {
+    constexpr int D1 = TS && decltype(HALF)::value == 0 ? 5 : 9;  // the half's last tap + 1
 #pragma unroll
     for (int t = 0; t < DEFER; ++t) {
-      const int tap = 9 - DEFER + t;
+      const int tap = D1 - DEFER + t;
       if (tap & 1) {
         acc2 = Mma<bf16>::run(la0[t], lb[t], acc2);
         if (CO == 64) acc3 = Mma<bf16>::run(la1[t], lb[t], acc3);
@@ -2315,8 +2358,11 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   // one chunk; PRE (compile-time): chunk c + AHEAD exists and is issued here.
   // The loop is split into the chunks that issue and the AHEAD tail, so the
   // main loop carries no per-piece branch and a constant vmcnt
-  auto chunk = [&](int c, auto PRE) {
+  auto chunk = [&](int c, auto PRE, auto HALF) {
     const char* b = smem + (c % NBUF) * BUF;
+    // this wave's taps [D0, D1): all nine, or one half of them (TS)
+    constexpr int D0 = TS && decltype(HALF)::value == 1 ? 5 : 0;
+    constexpr int D1 = TS && decltype(HALF)::value == 0 ? 5 : 9;
     // fragments of tap d + PF are read while tap d multiplies (one wave per
     // SIMD: the LDS latency is hidden by this wave's own MFMAs only)
     constexpr int NS = PF + 1;
@@ -2328,15 +2374,15 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
       if (CO == 64) aq1[s] = *(const u32x4*)(b + aofs + 32 * F8_WROW * 16 + d * 32);
     };
 #pragma unroll
-    for (int d = 0; d < PF; ++d) rd(d, d);
-    if (DEFER && c > cbeg) run_deferred();  // the last taps of chunk c-1
+    for (int d = D0; d < D0 + PF; ++d) rd(d, d % NS);
+    if (DEFER && c > cbeg) run_deferred(HALF);  // the last taps of chunk c-1
     // chunk c+AHEAD's pieces go out one per tap, in the MFMA shadow: its
     // buffer was last read in chunk c-1, before the last barrier
 #pragma unroll
-    for (int d = 0; d < 9; ++d) {
-      if (d + PF < 9) rd(d + PF, (d + PF) % NS);
-      if (DEFER && d >= 9 - DEFER) {
-        const int t = d - (9 - DEFER);
+    for (int d = D0; d < D1; ++d) {
+      if (d + PF < D1) rd(d + PF, (d + PF) % NS);
+      if (DEFER && d >= D1 - DEFER) {
+        const int t = d - (D1 - DEFER);
         lb[t] = bq[d % NS];
         la0[t] = aq0[d % NS];
         if (CO == 64) la1[t] = aq1[d % NS];
@@ -2348,7 +2394,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
         if (CO == 64) acc1 = Mma<bf16>::run(aq1[d % NS], bq[d % NS], acc1);
       }
       if constexpr (decltype(PRE)::value) {
-        if (d < NPW) issue1(c + AHEAD, d);
+        if (d - D0 < NPW) issue1(c + AHEAD, d - D0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -2365,18 +2411,59 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     if (DEFER) defer_wait();
     __builtin_amdgcn_s_barrier();
   };
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
   int c = cbeg;
-  for (; c + AHEAD < cend; ++c) chunk(c, std::true_type{});
-  for (; c < cend; ++c) chunk(c, std::false_type{});
-  if (DEFER && nch > 0) run_deferred();
+  if (half == 0) {  // wave-uniform
+    for (; c + AHEAD < cend; ++c) chunk(c, std::true_type{}, H0{});
+    for (; c < cend; ++c) chunk(c, std::false_type{}, H0{});
+    if (DEFER && nch > 0) run_deferred(H0{});
+  } else {
+    for (; c + AHEAD < cend; ++c) chunk(c, std::true_type{}, H1{});
+    for (; c < cend; ++c) chunk(c, std::false_type{}, H1{});
+    if (DEFER && nch > 0) run_deferred(H1{});
+  }
   DV_STAMP_AT(2);
+  // per output-channel group j of this wave: the accumulated sum (two tap
+  // chains).  TS: each half holds partial sums of all CO channels; half 0
+  // keeps channels [0, 32) and half 1 [32, 64), the other half's part of
+  // them arriving through LDS (the ring is dead: every wave passed the last
+  // chunk's barrier)
+  f32x16 fin[NJ];
+  if constexpr (TS) {
+    f32x16 keep, give;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float s0 = acc0[e] + acc2[e], s1 = acc1[e] + acc3[e];
+      keep[e] = half ? s1 : s0;
+      give[e] = half ? s0 : s1;
+    }
+    f32x4* xb = (f32x4*)smem;  // [2 halves][4 pixel groups][4][64 lanes]
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      xb[((half * 4 + wq) * 4 + g) * 64 + lane] = f32x4{give[4 * g], give[4 * g + 1], give[4 * g + 2], give[4 * g + 3]};
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 o = xb[(((1 - half) * 4 + wq) * 4 + g) * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) keep[4 * g + e] += o[e];
+    }
+    fin[0] = keep;
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) fin[j][e] = j ? acc1[e] + acc3[e] : acc0[e] + acc2[e];
+  }
   // epilogue: lane owns pixel m, channels co0 + 32j + 8g + 4h + e.  Bias and
   // residual are loaded for all 8 channel groups BEFORE the first store (vmcnt
   // retires loads and stores in order: a load behind a store waits for the
   // write, one round trip per group when they interleaved)
   const long long m = m0 + tpx;
-  const int cw = co0 + chh * CO;  // this wave's first output channel
-  float sv[STATS ? CO : 1];  // STATS: [0,CO/2) sums, [CO/2,CO) squares of the lane's CO/2 channels
+  const int cw = co0 + chh * CO + half * 32;  // this wave's first output channel
+  constexpr int NSV = 32 * NJ;                // STATS: [0, 16 NJ) sums, then squares, of the lane's channels
+  float sv[STATS ? NSV : 1];
   f32x4 bb[NJ][4];
   u32x2 rq[NJ][4], rq2[NJ][4];
   if (p.bias) {
@@ -2404,7 +2491,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
       const int n = cw + 32 * j + 8 * g + 4 * h;
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = j ? acc1[4 * g + e] + acc3[4 * g + e] : acc0[4 * g + e] + acc2[4 * g + e];
+      for (int e = 0; e < 4; ++e) v[e] = fin[j][4 * g + e];
       if (p.bias) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += bb[j][g][e];
@@ -2429,16 +2516,16 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
         for (int e = 0; e < 4; ++e) {
           const float q = stored<bf16>(v[e]);
           sv[16 * j + 4 * g + e] = q;
-          sv[CO / 2 + 16 * j + 4 * g + e] = q * q;
+          sv[NSV / 2 + 16 * j + 4 * g + e] = q * q;
         }
       }
     }
   }
   if constexpr (STATS) {  // the host requires gn_P % 128 == 0: the tile is in one clip
-    gn_rs_reduce<CO>(sv, r);
-    gn_block_add<bf16, CO>(p, sv, m0 / p.gn_P, [&](int k) {
-      return co0 + 32 * (k / 16) + 8 * ((k % 16) / 4) + 4 * h + (k % 4);
-    }, (float*)smem, co0, CO);
+    gn_rs_reduce<NSV>(sv, r);
+    gn_block_add<bf16, NSV>(p, sv, m0 / p.gn_P, [&](int k) {
+      return cw + 32 * (k / 16) + 8 * ((k % 16) / 4) + 4 * h + (k % 4);
+    }, (float*)smem, co0, CG);
   }
 #ifdef DV_STAMP
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2493,6 +2580,15 @@ int launch_fwd_frame(const ConvFwdArgs<bf16>& a0, hipStream_t st) {
   // after the chunk barrier): same-box per-launch A/B (tools/frame_ab.py,
   // profiles/r03_frame_ab.txt) put PF 3 + DEFER 1 1-3 % ahead of PF 2 without
   // the deferral
+  // 8x8 frames with 64-channel tiles: the tap split (two waves per SIMD)
+  if (a.W == 8 && co == 64) {
+#define DV_FTS(SP) (a.gn_sums ? conv_fwd_frame_kernel<8, true, 3, 1, 64, SP, 8, true><<<nblk, 512, 0, st>>>(a) \
+                              : conv_fwd_frame_kernel<8, false, 3, 1, 64, SP, 8, true><<<nblk, 512, 0, st>>>(a))
+    if (a.c0 < a.cin) DV_FTS(true);
+    else DV_FTS(false);
+#undef DV_FTS
+    return check_launch("conv_fwd_frame");
+  }
   switch (a.W) {
 #define DV_FW5(WW, C, SP) (a.gn_sums ? conv_fwd_frame_kernel<WW, true, 3, 1, C, SP><<<nblk, 256, 0, st>>>(a) \
                                  : conv_fwd_frame_kernel<WW, false, 3, 1, C, SP><<<nblk, 256, 0, st>>>(a))
