@@ -1778,6 +1778,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   using G = FsGeom<W>;
   constexpr int WP = G::WP, NSLOT = G::NSLOT, NP = G::NP, NPW = G::NPW, WBUF = G::WBUF;
   __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
+  DV_STAMP_AT(0);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1800,16 +1801,17 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   }
   // x0 as a raw buffer: halo and pad slots load out of range (zeros, no traffic)
   const __amdgpu_buffer_rsrc_t xr = dma_rsrc(p.x0, (unsigned)(p.M * p.ld0 * 2));
-  auto issue = [&](int st, int buf) {
+  auto issue1 = [&](int st, int buf, int i) {
     const int m0 = (sbeg + st) * 128;
     const int y0 = (m0 % HW) / W;
     const int base = m0 * p.ld0 * 2;
+    const int piece = min(wave + 8 * i, NP - 1);
+    const bool in = (unsigned)(y0 + s_ry[i]) < (unsigned)p.H;
+    dma16(xr, smem + buf * WBUF + piece * 1024, in ? (unsigned)(base + s_off[i]) : DMA_OOB);
+  };
+  auto issue = [&](int st, int buf) {
 #pragma unroll
-    for (int i = 0; i < NPW; ++i) {
-      const int piece = min(wave + 8 * i, NP - 1);
-      const bool in = (unsigned)(y0 + s_ry[i]) < (unsigned)p.H;
-      dma16(xr, smem + buf * WBUF + piece * 1024, in ? (unsigned)(base + s_off[i]) : DMA_OOB);
-    }
+    for (int i = 0; i < NPW; ++i) issue1(st, buf, i);
   };
 
   // weights: the block's 64 contiguous packed rows are DMA'd once into a
@@ -1849,6 +1851,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   __syncthreads();  // the weight image is dead: ring buffer 1 may be refilled
   if (nst > 1) issue(1, 1);
   if (nst > 2) issue(2, 2);
+  DV_STAMP_AT(1);
 
   const int r = lane & 31, h = lane >> 5;
   const int px = pt * 32 + r;  // lane's pixel in the stage; window row of tap (0,0)
@@ -1876,7 +1879,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     // k / 4, 16 channels at (k % 4) * 16).  The reads are inline asm with
     // hand-counted lgkmcnt: beside the LDS-DMA hipcc's waitcnt pass treats
     // the LGKM queue as out of order and drains it to 0 every few reads.
-    constexpr int FSD = 8;
+    constexpr int FSD = NRES > 1 ? 6 : 8;  // (two residuals: 8 VGPRs of read-ahead fewer, no spill)
     const unsigned xa = lds_addr(smem + buf * WBUF + bofs);
     u32x4 bq[FSD];
     static_for<0, FSD>([&](auto kk) {
@@ -1896,14 +1899,28 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
         rv2[g] = *(const bf16x4*)(p.res2 + m * p.ldres2 + co0 + ch * 32 + 8 * g + 4 * h);
     }
     f32x16 acc = bias_acc;  // the accumulator starts at the bias
+    // stage st+3's window pieces go out among this stage's MFMAs (one per 7):
+    // their buffer, (st+3) % 4 = (st-1) % 4, was last read in stage st-1,
+    // before the barrier that ended it.  (Issued at the end of the stage they
+    // cost ≈0.8 us per stage with the barrier: phase stamps, r05m.)
+    const bool pre = st + 3 < nst;  // wave-uniform
     static_for<0, 36>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       constexpr int younger = (FSD - 1 < 35 - k) ? FSD - 1 : 35 - k;
       lgkm_wait_tied<younger>(bq[k % FSD]);
       acc = Mma<bf16>::run(wA[k], bq[k % FSD], acc);
       if constexpr (k + FSD < 36) bq[k % FSD] = ds_read_b128_off<fs_koff<W>(k + FSD)>(xa);
+      if constexpr (k % 7 == 3 && k / 7 < NPW) {
+        if (pre) issue1(st + 3, (st + 3) & 3, k / 7);
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
+#ifdef DV_STAMP
+    if (st == 1) {
+      asm volatile("s_nop 0" : "+v"(acc));
+      DV_STAMP_AT(4);
+    }
+#endif
     // epilogue: lane owns pixel m, channels 8g + 4h + e of the wave's 32
     const bool silu = p.act == DV_ACT_SILU;
     float sv[stats ? 32 : 1];
@@ -1939,22 +1956,40 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
       gn_rs_reduce<32>(sv, r);
       sacc[0] += sv[0];
     }
-    // stage st+1's window landed.  vmcnt retires in order over loads AND
-    // stores; younger than DMA(st+1) are the previous stage's 4 stores, the
-    // NPW DMAs of st+2 (when issued) and this stage's 4 stores.  Every window
-    // read of this stage was waited for by the last MFMA: no lgkmcnt drain.
-    if (st + 2 < nst) {
-      if (st > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW + 8) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW + 4) : "memory");
-    } else {
-      if (st > 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (st == 1) DV_STAMP_AT(5);
+    // stage st+1's window landed.  vmcnt(N) = all but the wave's N youngest
+    // vector-memory ops done (loads, stores, DMA in issue order).  Per stage s
+    // a wave issues: its residual loads R (NR), the NPW pieces of D(s+3) (if
+    // s+3 < nst) among the MFMAs, its 4 stores.  D(1), D(2) come from the
+    // prologue; D(s+1), s >= 2, from stage s-2.  Younger than D(st+1):
+    //   st = 0: D2, R0, D3, S0;   st = 1: R0, D3, S0, R1, D4, S1;
+    //   st >= 2: S(st-2), R(st-1), D(st+2), S(st-1), R(st), D(st+3), S(st).
+    // (A statistics epilogue's clip-boundary atomics only add younger ops:
+    // the wait then covers more, never less.)  Every window read of this
+    // stage was waited for by the last MFMA: no lgkmcnt drain.
+    if (st + 1 < nst) {
+      constexpr int NR = 4 * NRES;
+      const int nd = (st + 2 < nst) + (st + 3 < nst);  // DMA stages issued after D(st+1)
+      if (st == 0) {
+        if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NR + 4 + 2 * NPW) : "memory");
+        else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NR + 4 + NPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NR + 4) : "memory");
+      } else if (st == 1) {
+        if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 8 + 2 * NPW) : "memory");
+        else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 8 + NPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 8) : "memory");
+      } else {
+        if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 12 + 2 * NPW) : "memory");
+        else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 12 + NPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 12) : "memory");
+      }
     }
-    // buffer (st+3)%4 was last read in stage st-1: every wave passed that
-    // barrier.  Issued here, where a wave would otherwise wait at the barrier.
-    if (st + 3 < nst) issue(st + 3, (st + 3) & 3);
+    if (st == 1) DV_STAMP_AT(6);
     __builtin_amdgcn_s_barrier();
+    if (st == 0) DV_STAMP_AT(2);
+    if (st == 1) DV_STAMP_AT(7);
   }
+  DV_STAMP_AT(3);
   if constexpr (stats) {
     // the clip of the block's last stage (block-uniform); earlier clips were
     // added per wave at the crossing (rare: stage ranges align with clips)
@@ -1981,10 +2016,11 @@ int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   const bool stats = a.gn_sums != nullptr;
 #define DV_FS(WW, RR) (stats ? conv_fwd_stripe_kernel<WW, RR, true><<<grid, 512, 0, st>>>(a, nstages, sps) \
                              : conv_fwd_stripe_kernel<WW, RR, false><<<grid, 512, 0, st>>>(a, nstages, sps))
-  // (two residuals come from dgrads only: no statistics epilogue beside them,
-  // whose registers would spill)
+  // (residuals come from dgrads only: no statistics epilogue beside them,
+  // whose registers would spill; conv_fwd_t routes that pair elsewhere)
 #define DV_FSR(WW) (nres == 2 ? (void)conv_fwd_stripe_kernel<WW, 2, false><<<grid, 512, 0, st>>>(a, nstages, sps) \
-                              : nres == 1 ? DV_FS(WW, 1) : DV_FS(WW, 0))
+                    : nres == 1 ? (void)conv_fwd_stripe_kernel<WW, 1, false><<<grid, 512, 0, st>>>(a, nstages, sps) \
+                                : DV_FS(WW, 0))
   if (a.W == 64) DV_FSR(64);
   else DV_FSR(32);
 #undef DV_FSR
@@ -2649,7 +2685,7 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
     // the stripe kernel flushes statistics per 128-pixel stage: clips must
     // be whole stages
     if (fwd_stripe_ok(a.M, h, wd, cin, x1 != nullptr, cout, ks, ld0) && (ldy & 3) == 0 &&
-        (res == nullptr || (ldres & 3) == 0) && (res2 == nullptr || ((ldres2 & 3) == 0 && !gn_sums)) &&
+        (res == nullptr || ((ldres & 3) == 0 && !gn_sums)) && (res2 == nullptr || (ldres2 & 3) == 0) &&
         (!gn_sums || gn_P % 128 == 0))
       return launch_fwd_stripe(a, st);
     int seg, nseg;

@@ -91,8 +91,36 @@ def frame_case(nf, h, w, cin, cout):
            stamps((m // 128) * (cout // cw)), [0, 1, 2, 4])
 
 
+def stripe_case(nf, h, w, cin, cout, res=False):
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = torch.randn(nf, h, w, cin, device="cuda", generator=g).bfloat16()
+    wt = torch.randn(cout, cin, 1, 3, 3, device="cuda", generator=g) / (9 * cin) ** 0.5
+    b = torch.randn(cout, device="cuda", generator=g)
+    rr = torch.randn(nf, h, w, cout, device="cuda", generator=g).bfloat16() if res else None
+    y = torch.empty(nf, h, w, cout, device="cuda", dtype=torch.bfloat16)
+    wp = ops.pack_conv_weight(wt, torch.bfloat16, cin, 0, cache=False)
+    f = lambda: call("dv_conv_fwd", dt(x), ptr(x), cin, cin, None, 0, ptr(wp), ptr(b), ptr(rr), cout if res else 0,
+                     None, 0, ptr(y), cout, nf, h, w, cin, cout, 3, 0, None, 0, 0, stream())
+    for _ in range(3):
+        f()
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000)
+    f()
+    ct = cout // 64
+    nst = nf * h * w // 128
+    bx = max(1, min(256 // ct, nst))
+    sps = (nst + bx - 1) // bx
+    bx = (nst + sps - 1) // sps
+    st = stamps(bx * ct)
+    report(f"stripe fwd ({nf},{h},{w}) {cin}->{cout}{' +res' if res else ''} {sps} stages", st, [0, 1, 2, 3])
+    report("  stage 1: mfma / epilogue / wait / issue+barrier", st, [2, 4, 5, 6, 7])
+
+
 for shp in [(64, 64, 64, 64, 64), (64, 32, 32, 64, 64), (64, 32, 32, 128, 128), (64, 16, 16, 256, 256),
             (64, 8, 8, 512, 512)]:
     wgrad_case(*shp)
+stripe_case(64, 64, 64, 64, 64)
+stripe_case(64, 64, 64, 64, 64, res=True)
+stripe_case(64, 64, 64, 64, 128, res=True)
 for shp in [(64, 8, 8, 512, 512), (64, 8, 8, 256, 256), (64, 16, 16, 256, 256)]:
     frame_case(*shp)
