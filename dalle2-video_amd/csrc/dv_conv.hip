@@ -1750,33 +1750,43 @@ int launch_fwd_glds(const ConvFwdArgs<bf16>& a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 constexpr int FS_XP = 144;   // window pixel pitch (64 bf16 + 16 B)
 
-// byte offset of k-step k (tap k / 4, 16 channels at (k % 4) * 16) from a
-// lane's tap-(0,0) window row
-template <int W>
-constexpr int fs_koff(int k) {
-  return (((k >> 2) / 3) * (W + 2) + ((k >> 2) % 3)) * FS_XP + (k & 3) * 32;
-}
-
 constexpr int FS_WROW = 1168;    // LDS weight row pitch: 576 bf16 + 16 B
 constexpr int FS_WPIECES = 73;   // 64 rows x 73 16-B slots = 73 DMA pieces of 1 KB
 
+// Row ring (round 5).  A stage's window is SEG + 2 image rows, of which the
+// first two are the previous stage's last two: only SEG new rows are staged
+// per stage (half the LDS-DMA bytes at W = 64, where the per-CU DMA intake
+// bound the loop: phase stamps, profiles/r05n_conv_stamps.txt).  Rows live in
+// a ring of R = 4 SEG + 2 row slots (three stages ahead + the stage being
+// read); a row slot is PPR whole 1-KB DMA pieces (WP pixels x 9 16-B slots,
+// padded), so no piece straddles two rows and rows need not be adjacent: each
+// tap row dy has its own base address.  A workgroup's stages lie in one frame
+// (the launcher picks stages_per_block | stages per frame), so the reused rows
+// are always the right ones.
 template <int W>
 struct FsGeom {
-  static constexpr int WP = W + 2, SEG = 128 / W, NWIN = (SEG + 2) * WP;
-  static constexpr int NSLOT = NWIN * 9;      // 16-B slots: 8 data + 1 pad per pixel
-  static constexpr int NP = (NSLOT + 63) / 64;  // 1-KB DMA pieces per stage
-  static constexpr int NPW = (NP + 7) / 8;      // pieces per wave (uniform: spare ones repeat the last)
-  static constexpr int WBUF = NP * 1024;
-  static constexpr int NBUF = 4;
-  static constexpr int RING = NBUF * WBUF > WBUF + 64 * FS_WROW ? NBUF * WBUF : WBUF + 64 * FS_WROW;
-  static constexpr int LDS = RING;
+  static constexpr int WP = W + 2, SEG = 128 / W;
+  static constexpr int PPR = (WP * 9 + 63) / 64;     // 1-KB pieces per row slot
+  static constexpr int ROWB = PPR * 1024;            // row slot bytes
+  static constexpr int R = 4 * SEG + 2;              // row slots in the ring
+  static constexpr int NP = SEG * PPR;               // pieces of a stage's new rows
+  static constexpr int NPW = (NP + 7) / 8;           // per wave (spare ones repeat the last)
+  static constexpr int NP0 = (SEG + 2) * PPR;        // stage 0 stages its whole window
+  static constexpr int NPW0 = (NP0 + 7) / 8;
+  static constexpr int WOFF = (3 * SEG + 2) * ROWB;  // weight image: beyond the rows of stages 0..2
+  static constexpr int LDS = R * ROWB > WOFF + 64 * FS_WROW ? R * ROWB : WOFF + 64 * FS_WROW;
+  static_assert(LDS <= 160 * 1024, "stripe ring exceeds the LDS");
 };
+// immediate offset of k-step k (tap k / 4 = 3 dy + dx, 16 channels at
+// (k % 4) * 16) from the lane's tap row dy base
+constexpr int fs_koff(int k) { return ((k >> 2) % 3) * FS_XP + (k & 3) * 32; }
 
 template <int W, int NRES, bool STATS>
 __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> p, int nstages,
                                                               int stages_per_block) {
   using G = FsGeom<W>;
-  constexpr int WP = G::WP, NSLOT = G::NSLOT, NP = G::NP, NPW = G::NPW, WBUF = G::WBUF;
+  constexpr int WP = G::WP, SEG = G::SEG, PPR = G::PPR, ROWB = G::ROWB, R = G::R;
+  constexpr int NP = G::NP, NPW = G::NPW, NP0 = G::NP0, NPW0 = G::NPW0;
   __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
   DV_STAMP_AT(0);
 
@@ -1787,41 +1797,57 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   const int sbeg = blockIdx.x * stages_per_block;
   const int nst = min(sbeg + stages_per_block, nstages) - sbeg;
   const int HW = p.H * W;
+  // the workgroup's frame and first output row; window row q is image row yq0 + q
+  const int m00 = sbeg * 128;
+  const int fbase = (m00 / HW) * HW;                 // first pixel of the frame
+  const int yq0 = (m00 - fbase) / W - 1;
 
-  // this lane's slot of each of the wave's pieces: window pixel, 16-B chunk
-  int s_off[NPW], s_ry[NPW];  // byte offset from the stage base; image-row offset (or invalid)
+  // this lane's 16-B slot of each of the wave's pieces: a column byte offset
+  // within an image row (or -1: halo / pad slot) and the row within the
+  // pieces' rows (stage 0: the window's SEG + 2 rows; later: the SEG new ones)
+  auto slot_of = [&](int piece, int& rr, int& coff) {
+    rr = piece / PPR;
+    const int slot = (piece - rr * PPR) * 64 + lane, px = slot / 9, c = slot - px * 9;
+    const bool ok = slot < WP * 9 && c < 8 && px >= 1 && px <= W;
+    coff = ok ? ((px - 1) * p.ld0 + c * 8) * 2 : -1;
+  };
+  int s_rr[NPW], s_co[NPW];
 #pragma unroll
-  for (int i = 0; i < NPW; ++i) {
-    const int piece = min(wave + 8 * i, NP - 1);
-    const int slot = piece * 64 + lane, px = slot / 9, c = slot - px * 9;
-    const int wy = px / WP, wx = px - wy * WP;
-    const bool ok = slot < NSLOT && c < 8 && wx >= 1 && wx <= W;
-    s_ry[i] = ok ? wy - 1 : -(1 << 20);
-    s_off[i] = (((wy - 1) * W + (wx - 1)) * p.ld0 + c * 8) * 2;
-  }
+  for (int i = 0; i < NPW; ++i) slot_of(min(wave + 8 * i, NP - 1), s_rr[i], s_co[i]);
   // x0 as a raw buffer: halo and pad slots load out of range (zeros, no traffic)
   const __amdgpu_buffer_rsrc_t xr = dma_rsrc(p.x0, (unsigned)(p.M * p.ld0 * 2));
-  auto issue1 = [&](int st, int buf, int i) {
-    const int m0 = (sbeg + st) * 128;
-    const int y0 = (m0 % HW) / W;
-    const int base = m0 * p.ld0 * 2;
-    const int piece = min(wave + 8 * i, NP - 1);
-    const bool in = (unsigned)(y0 + s_ry[i]) < (unsigned)p.H;
-    dma16(xr, smem + buf * WBUF + piece * 1024, in ? (unsigned)(base + s_off[i]) : DMA_OOB);
+  // one piece of window row q (its ring slot q % R, piece part of the row)
+  auto dma_row = [&](int q, int piece, int coff) {
+    const int y = yq0 + q;
+    const bool in = coff >= 0 && (unsigned)y < (unsigned)p.H;
+    dma16(xr, smem + (q % R) * ROWB + (piece % PPR) * 1024,
+          in ? (unsigned)((fbase + y * W) * p.ld0 * 2 + coff) : DMA_OOB);
   };
-  auto issue = [&](int st, int buf) {
+  // piece i of stage st >= 1: its new rows q = st SEG + 2 .. st SEG + SEG + 1
+  auto issue1 = [&](int st, int i) {
+    dma_row(st * SEG + 2 + s_rr[i], min(wave + 8 * i, NP - 1), s_co[i]);
+  };
+  auto issue = [&](int st) {
 #pragma unroll
-    for (int i = 0; i < NPW; ++i) issue1(st, buf, i);
+    for (int i = 0; i < NPW; ++i) issue1(st, i);
   };
 
-  // weights: the block's 64 contiguous packed rows are DMA'd once into a
-  // padded LDS image (1168-B rows: conflict-free fragment reads) laid over
-  // ring buffers 1..2, then each wave reads its A fragments into registers.
-  // (Direct per-wave global loads of the fragments touch 32 lines per
+  // prologue: stage 0's whole window, the weight image (beyond the rows of
+  // stages 0..2), the bias, then stages 1 and 2: only the weights and stage 0
+  // are waited for before the fragments are read into registers.
+  // (Direct per-wave global loads of the weight fragments touch 32 lines per
   // instruction for 8 KB of use: ~20k cycles of prologue.)
-  if (nst > 0) issue(0, 0);
+  if (nst > 0) {
+#pragma unroll
+    for (int i = 0; i < NPW0; ++i) {
+      const int piece = min(wave + 8 * i, NP0 - 1);
+      int rr, coff;
+      slot_of(piece, rr, coff);
+      dma_row(rr, piece, coff);
+    }
+  }
   {
-    char* sW = smem + WBUF;
+    char* sW = smem + G::WOFF;
     const __amdgpu_buffer_rsrc_t wr = dma_rsrc(p.w + (long long)co0 * 576, 64 * 576 * 2);
 #pragma unroll
     for (int i = 0; i < FS_WPIECES / 8 + 1; ++i) {
@@ -1839,23 +1865,27 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias_acc[4 * g + e] = b[e];
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weights, bias, stage 0
+  if (nst > 1) issue(1);
+  if (nst > 2) issue(2);
+  // stage 0, weights and bias landed; stages 1 and 2 (when issued) younger
+  if (nst > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
+  else if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   u32x4 wA[36];
   {
-    const char* aw = smem + WBUF + (ch * 32 + (lane & 31)) * FS_WROW + (lane >> 5) * 16;
+    const char* aw = smem + G::WOFF + (ch * 32 + (lane & 31)) * FS_WROW + (lane >> 5) * 16;
 #pragma unroll
     for (int k = 0; k < 36; ++k) wA[k] = *(const u32x4*)(aw + 32 * k);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();  // the weight image is dead: ring buffer 1 may be refilled
-  if (nst > 1) issue(1, 1);
-  if (nst > 2) issue(2, 2);
+  __syncthreads();  // the weight image is dead: stage 3's rows may land over it
   DV_STAMP_AT(1);
 
   const int r = lane & 31, h = lane >> 5;
-  const int px = pt * 32 + r;  // lane's pixel in the stage; window row of tap (0,0)
-  const int bofs = ((px / W) * WP + (px % W)) * FS_XP + h * 16;
+  const int px = pt * 32 + r;           // lane's pixel in the stage
+  const int orow = px / W;              // its output row in the stage (wave-uniform)
+  const int loff = (px % W) * FS_XP + h * 16;
   // GroupNorm statistics (STATS, compile-time like NRES): each stage's 32 x 16
   // sums / squares are reduce-scattered over the half-wave (gn_rs_reduce), so
   // a lane carries ONE running total across stages; it is added when the
@@ -1874,17 +1904,21 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
         sacc[0] = 0.f;
       }
     }
-    const int buf = st & 3;
+    // the lane's three tap rows dy = 0..2: window rows st SEG + orow + dy
+    const int q0 = st * SEG + orow;
+    const unsigned xa0 = lds_addr(smem + (q0 % R) * ROWB + loff);
+    const unsigned xa1 = lds_addr(smem + ((q0 + 1) % R) * ROWB + loff);
+    const unsigned xa2 = lds_addr(smem + ((q0 + 2) % R) * ROWB + loff);
+    auto xrow = [&](int k) { return (k >> 2) / 3 == 0 ? xa0 : ((k >> 2) / 3 == 1 ? xa1 : xa2); };
     // window fragments read FSD k-steps ahead of their MFMA (k-step k = tap
     // k / 4, 16 channels at (k % 4) * 16).  The reads are inline asm with
     // hand-counted lgkmcnt: beside the LDS-DMA hipcc's waitcnt pass treats
     // the LGKM queue as out of order and drains it to 0 every few reads.
     constexpr int FSD = NRES > 1 ? 6 : 8;  // (two residuals: 8 VGPRs of read-ahead fewer, no spill)
-    const unsigned xa = lds_addr(smem + buf * WBUF + bofs);
     u32x4 bq[FSD];
     static_for<0, FSD>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
-      bq[k] = ds_read_b128_off<fs_koff<W>(k)>(xa);
+      bq[k] = ds_read_b128_off<fs_koff(k)>(xrow(k));
     });
     bf16x4 rv[4], rv2[4];
     const long long m = (long long)(sbeg + st) * 128 + px;
@@ -1899,19 +1933,18 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
         rv2[g] = *(const bf16x4*)(p.res2 + m * p.ldres2 + co0 + ch * 32 + 8 * g + 4 * h);
     }
     f32x16 acc = bias_acc;  // the accumulator starts at the bias
-    // stage st+3's window pieces go out among this stage's MFMAs (one per 7):
-    // their buffer, (st+3) % 4 = (st-1) % 4, was last read in stage st-1,
-    // before the barrier that ended it.  (Issued at the end of the stage they
-    // cost ≈0.8 us per stage with the barrier: phase stamps, r05m.)
+    // stage st+3's new rows go out among this stage's MFMAs (one piece per 7):
+    // their ring slots were last read in stage st-1, before the barrier that
+    // ended it
     const bool pre = st + 3 < nst;  // wave-uniform
     static_for<0, 36>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       constexpr int younger = (FSD - 1 < 35 - k) ? FSD - 1 : 35 - k;
       lgkm_wait_tied<younger>(bq[k % FSD]);
       acc = Mma<bf16>::run(wA[k], bq[k % FSD], acc);
-      if constexpr (k + FSD < 36) bq[k % FSD] = ds_read_b128_off<fs_koff<W>(k + FSD)>(xa);
+      if constexpr (k + FSD < 36) bq[k % FSD] = ds_read_b128_off<fs_koff(k + FSD)>(xrow(k + FSD));
       if constexpr (k % 7 == 3 && k / 7 < NPW) {
-        if (pre) issue1(st + 3, (st + 3) & 3, k / 7);
+        if (pre) issue1(st + 3, k / 7);
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -1957,7 +1990,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
       sacc[0] += sv[0];
     }
     if (st == 1) DV_STAMP_AT(5);
-    // stage st+1's window landed.  vmcnt(N) = all but the wave's N youngest
+    // stage st+1's rows landed.  vmcnt(N) = all but the wave's N youngest
     // vector-memory ops done (loads, stores, DMA in issue order).  Per stage s
     // a wave issues: its residual loads R (NR), the NPW pieces of D(s+3) (if
     // s+3 < nst) among the MFMAs, its 4 stores.  D(1), D(2) come from the
@@ -2009,7 +2042,12 @@ int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   int bx = 256 / ct;
   if (bx < 1) bx = 1;
   if (bx > nstages) bx = nstages;
-  const int sps = (nstages + bx - 1) / bx;
+  // the row ring reuses rows across a workgroup's stages: its stage range
+  // must lie in one frame, so stages_per_block divides the stages per frame
+  const int spf = a.H / (128 / a.W);
+  int sps = (nstages + bx - 1) / bx;
+  if (sps >= spf) sps = spf;
+  else while (spf % sps) ++sps;
   bx = (nstages + sps - 1) / sps;
   dim3 grid(bx, ct);
   const int nres = a.res2 ? 2 : a.res ? 1 : 0;
