@@ -692,16 +692,25 @@ __device__ __forceinline__ void vm_wait_tied(u32x2 (&v)[R]) {
   else
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v[0]) : "n"(N) : "memory");
 }
+// RLDS (where the ring still fits the LDS): the residual tile rides in the
+// ring beside the X tile, by the same LDS-DMA (1-KB coalesced pieces, 16-B
+// chunks swizzled by row), and the epilogue reads it from LDS -- instead of
+// per-lane 8-B register loads (32 rows x 16 B per instruction).
 template <int BN, int KT, int NB, bool RES>
 __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p, int ntiles) {
   constexpr int BM = 128;
   constexpr int XT = BM * 128 * KT;  // one pixel tile: KT 64-channel blocks of 128-B rows
   constexpr int WBYTES = BN * 128 * KT;
+  constexpr int RT = BM * BN * 2;    // one residual tile: 128 rows of BN bf16
+  constexpr bool RLDS = RES && WBYTES + NB * (XT + RT) <= 160 * 1024;
   constexpr int TJ = BN / 64;        // 32-channel MFMA tiles per wave
   constexpr int XD = 2 * KT;         // X-tile DMA instructions per thread (64 rows per round)
   constexpr int WD = BN * KT / 64;   // weight DMA instructions per thread
-  constexpr int RL = RES ? 4 * TJ : 0;  // residual loads per thread per tile
-  __shared__ __attribute__((aligned(1024))) char smem[WBYTES + NB * XT];
+  constexpr int RD = RLDS ? RT / (512 * 16) : 0;        // residual DMA instructions per thread
+  constexpr int RL = RES && !RLDS ? 4 * TJ : 0;         // residual register loads per thread per tile
+  constexpr int SLOT = XT + (RLDS ? RT : 0);            // one ring slot: X tile (+ residual tile)
+  constexpr int CPR = BN / 8;                           // 16-B chunks per residual row
+  __shared__ __attribute__((aligned(1024))) char smem[WBYTES + NB * SLOT];
   char* sW = smem;
   char* sX = smem + WBYTES;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -722,16 +731,29 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
                             ? (first ? p.x0 + m * p.ld0 + kb * 64 : p.x1 + m * p.ld1 + (kb * 64 - p.c0)) + cs * 8
                             : zero_src(tid + 97u * blockIdx.x + 31u * i);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(sX + buf * XT + kb * (BM * 128) +
+                                       (__attribute__((address_space(3))) void*)(sX + buf * SLOT + kb * (BM * 128) +
                                                                                (64 * (i % 2) + 8 * wave) * 128),
                                        16, 0, 0);
     }
+    if constexpr (RLDS) {  // the residual tile: slot q = i * 512 + tid -> row q / CPR, chunk q % CPR
+#pragma unroll
+      for (int i = 0; i < RD; ++i) {
+        const int q = i * 512 + tid, row = q / CPR, cs = (q % CPR) ^ (row % CPR);
+        const long long m = m0 + row;
+        const bf16* src = (t < ntiles && m < p.M) ? p.res + m * p.ldres + cs * 8
+                                                  : zero_src(tid + 89u * blockIdx.x + 37u * i);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(sX + buf * SLOT + XT +
+                                                                                 (i * 512 + 64 * wave) * 16),
+                                         16, 0, 0);
+      }
+    }
   };
   // residual of this lane's outputs (pixel row r of group wm, channels n0 + 8g + 4h .. +3)
-  constexpr int NR = RES ? 4 * TJ : 1;
+  constexpr int NR = RES && !RLDS ? 4 * TJ : 1;
   u32x2 resA[NR], resB[NR];
   auto load_res = [&](int t, u32x2 (&dst)[NR]) {
-    if constexpr (RES) {
+    if constexpr (RES && !RLDS) {
       long long m = (long long)t * BM + wm * 32 + r;
       if (t >= ntiles || m >= p.M) m = 0;  // a valid address; the value is not stored
 #pragma unroll
@@ -758,7 +780,8 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
   // issue order (vmcnt is in order): prologue W, X(0 .. NB-3), res(0), X(NB-2);
   // iteration k: res(k+1), X(k+NB-1).  After res(k) come exactly X(k+NB-2),
   // res(k+1), X(k+NB-1), so vmcnt(2 XD + RL) means res(k) — and X(k), issued
-  // before it (NB >= 3) — landed, with two X tiles still in flight.
+  // before it (NB >= 3) — landed, with two X tiles still in flight.  (RLDS:
+  // X(k) carries its residual tile, RD more pieces per tile: 2 (XD + RD).)
   static_assert(NB >= 3, "the ring needs two tiles in flight");
   int t = blockIdx.x;
 #pragma unroll
@@ -782,15 +805,15 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
     const int buf = it % NB;
     load_res(t + (int)gridDim.x, rnxt);
     issue_x(t + (NB - 1) * (int)gridDim.x, (it + NB - 1) % NB);
-    if constexpr (RES) vm_wait_tied<2 * XD + RL>(rcur);
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * XD + RL) : "memory");
+    if constexpr (RES && !RLDS) vm_wait_tied<2 * XD + RL>(rcur);
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (XD + RD) + RL) : "memory");
     __builtin_amdgcn_s_barrier();
     f32x16 acc[TJ];
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    const char* xs = sX + buf * XT;
+    const char* xs = sX + buf * SLOT;
 #pragma unroll
     for (int kb = 0; kb < KT; ++kb)
 #pragma unroll
@@ -819,7 +842,12 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvFwdArgs<bf16> p
             v[e] = acc[j][4 * g + e] + bias[j][g][e];
             if (p.act == DV_ACT_SILU) v[e] = silu_f(v[e]);
           }
-          if constexpr (RES) {
+          if constexpr (RLDS) {
+            const int row = wm * 32 + r, c16 = n >> 3;
+            const bf16x4 rv = *(const bf16x4*)(xs + XT + row * (BN * 2) + ((c16 ^ (row % CPR)) << 4) + (n & 7) * 2);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+          } else if constexpr (RES) {
             const bf16x4 rv = __builtin_bit_cast(bf16x4, rcur[4 * j + g]);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
@@ -1702,9 +1730,11 @@ template <int BN, int KT>
 int launch_conv1x1(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   constexpr int NB = 3;
   constexpr int LDS = BN * 128 * KT + NB * 128 * 128 * KT;
-  constexpr int PER_CU = (160 * 1024) / LDS;
+  // (the residual variant keeps its residual tiles in the ring when they fit:
+  // mirror of conv1x1_stream_kernel's RLDS)
+  constexpr int LDS_RES = LDS + NB * 128 * BN * 2 <= 160 * 1024 ? LDS + NB * 128 * BN * 2 : LDS;
   const int ntiles = (int)((a.M + 127) / 128);
-  const int grid = std::min(ntiles, 256 * PER_CU);
+  const int grid = std::min(ntiles, 256 * ((160 * 1024) / (a.res ? LDS_RES : LDS)));
   if (a.res) conv1x1_stream_kernel<BN, KT, NB, true><<<grid, 512, 0, st>>>(a, ntiles);
   else conv1x1_stream_kernel<BN, KT, NB, false><<<grid, 512, 0, st>>>(a, ntiles);
   return check_launch("conv1x1_stream");
