@@ -694,53 +694,6 @@ def pack_conv_weight(weight: torch.Tensor, dtype, pad_to: int, mode: int, cache:
     return out
 
 
-class _WgradStream:
-    """Weight gradients run on a second HIP stream of the device, concurrent
-    with the critical path of the backward (dgrad -> GroupNorm -> dgrad ...):
-    the two kernel chains fill each other's tails and low-occupancy phases.
-    Each launch forks from the current stream (it needs dY and X); the side
-    stream is joined back once, at the end of the backward pass (autograd
-    engine callback), before anything reads the gradients (clip / AdamW) —
-    also inside a captured HIP graph, where fork / join become graph edges.
-    Tensors the side stream reads are record_stream'ed so the caching
-    allocator cannot hand their memory out before the side work is done.
-    DV_WGRAD_STREAM=1 turns it on (off by default, see `enabled`)."""
-
-    # measured slower on the full step (77 vs 80-82 steps/s, same box): the
-    # concurrent kernels contend for LDS / L2 more than they fill tails — opt-in
-    enabled = os.environ.get("DV_WGRAD_STREAM", "0") == "1"
-    _streams = {}
-    _join_queued = False
-
-    @classmethod
-    def side(cls, device):
-        key = str(device)
-        if key not in cls._streams:
-            cls._streams[key] = torch.cuda.Stream(device=device)
-        return cls._streams[key]
-
-    @classmethod
-    def run(cls, device, fn, tensors):
-        if not cls.enabled or TIMER is not None:
-            fn()
-            return
-        main = torch.cuda.current_stream(device)
-        side = cls.side(device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            fn()
-        for t in tensors:
-            if t is not None:
-                t.record_stream(side)
-        if not cls._join_queued:
-            cls._join_queued = True
-
-            def join():
-                cls._join_queued = False
-                torch.cuda.current_stream(device).wait_stream(side)
-            torch.autograd.Variable._execution_engine.queue_callback(join)
-
-
 class GradSink:
     """Shared input-gradient buffer of two convolutions reading the same input
     (ResnetBlock3D's block1 conv and res_conv, dalle2_video.py:170, 188-205):
@@ -1084,7 +1037,7 @@ class ConvFn(torch.autograd.Function):
             kname = (conv_wgrad_name(dname, m, cout8, cin, c0, x1 is not None, ksize, h, w,
                                      max(lddy, ld0, ld1)) if (cout8 == cout and cin_real == cin)
                      else gemm_wgrad_name(dname, m, cout8, cin * ksize * ksize, max(lddy, ld0, ld1)))
-            if (WGRAD_DEFER.active and dw is None and db is None and not _WgradStream.enabled
+            if (WGRAD_DEFER.active and dw is None and db is None
                     and kname.startswith(("conv_wgrad_win", "conv_wgrad_1x1"))):
                 # leaf .grad targets: leave the split partials for the pass-end sum
                 if (not WGRAD_DEFER.STREAM
@@ -1109,18 +1062,16 @@ class ConvFn(torch.autograd.Function):
             WGRAD_DEFER.before_write(dw_t.data_ptr(), db_t.data_ptr() if db_t is not None else None)
             ws = _wgrad_workspace(_lib.dtype_name(dy8), nf, h, w, cin, c0, x1 is not None, cout8,
                                   ksize, dy.device)
-            # on the side stream only when the results go straight into leaf
-            # .grad buffers (a returned gradient is consumed by autograd on
-            # this stream at once)
-            run = _WgradStream.run if (dw is None and db is None) else (lambda dev, f, ts: f())
-            run(dy.device, lambda: _launch(
-                kname,
-                2.0 * m * cout8 * cin * ksize * ksize * ctx.algo_scale,
-                dy8.element_size() * m * (cin + cout8),
-                lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), lddy, ptr(x0), ld0, c0, ptr(x1), ld1,
-                             ptr(dw_t), int(acc_w), ptr(db_t), int(acc_b), ptr(ws), ws.numel(),
-                             nf, h, w, cin, cout8, cout, cin_real, ksize, stream()),
-                ("wgrad", cout8, cin * ksize * ksize, m)), (dy8, x0, x1, dw_t, db_t))
+            # (on a side stream, concurrent with the dgrad -> GroupNorm chain,
+            # the wgrads measured slower: 77 vs 80-82 steps/s in round 1, 96.5
+            # vs 104.7 in round 5 with the deferred sums kept -- removed)
+            _launch(kname,
+                    2.0 * m * cout8 * cin * ksize * ksize * ctx.algo_scale,
+                    dy8.element_size() * m * (cin + cout8),
+                    lambda: call("dv_conv_wgrad", dt(dy8), ptr(dy8), lddy, ptr(x0), ld0, c0, ptr(x1), ld1,
+                                 ptr(dw_t), int(acc_w), ptr(db_t), int(acc_b), ptr(ws), ws.numel(),
+                                 nf, h, w, cin, cout8, cout, cin_real, ksize, stream()),
+                    ("wgrad", cout8, cin * ksize * ksize, m))
         elif want_b:
             bslot = _grad_out(bparam, zero=True)
             if bslot is None or cout8 != cout:
@@ -1128,10 +1079,7 @@ class ConvFn(torch.autograd.Function):
             else:
                 db_buf = bslot[0]
             WGRAD_DEFER.before_write(bslot[0].data_ptr() if bslot is not None else None)
-            run = (_WgradStream.run if bslot is not None and db_buf is bslot[0]
-                   else (lambda dev, f, ts: f()))
-            run(dy.device, lambda: call("dv_bias_grad", dt(dy8), ptr(dy8), lddy, ptr(db_buf),
-                                        nf * h * w, cout, stream()), (dy8, db_buf))
+            call("dv_bias_grad", dt(dy8), ptr(dy8), lddy, ptr(db_buf), nf * h * w, cout, stream())
             if bslot is None:
                 db = db_buf[:cout]
             elif db_buf is not bslot[0]:

@@ -767,8 +767,6 @@ class OverlappedAllReduce:
             side = ops.WGRAD_DEFER.streamed
             if side is not None:
                 self.comm.wait_stream(ops.WGRAD_DEFER._side(side))
-            if ops._WgradStream.enabled and str(dev) in ops._WgradStream._streams:
-                self.comm.wait_stream(ops._WgradStream._streams[str(dev)])
             with torch.cuda.stream(self.comm):
                 pend = self.gcomm.allreduce_mean_(G[start:end])
             if pend is not None:
