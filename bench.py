@@ -321,9 +321,27 @@ def sampling_leg(args, device):
     mx = {k: v for k, v in summ8.items() if k.startswith("conv_fwd_mx8")}
     kname, kd = max(mx.items(), key=lambda kv: kv[1]["ms"])
     k_tf = kd["flops"] / (kd["ms"] * 1e-3) / 1e12
+    # the mid attention with PV in MX-fp8 (dv_mqa_fwd_fp8) against the bf16
+    # streamed kernel of the bf16 leg, same process / box; half its FLOPs (QK^T)
+    # stay bf16, so the peak is the harmonic blend of the two MFMA peaks
+    att8 = summ8.get("attn:mqa_fwd8")
+    mid8 = None
+    if att8 is not None:
+        a8_us = att8["ms"] / att8["count"] * 1e3
+        a8_tf = att8["flops"] / (att8["ms"] * 1e-3) / 1e12
+        blend = 2.0 / (1.0 / PEAK_BF16_TFLOPS + 1.0 / PEAK_FP8_TFLOPS)
+        mid8 = {"tokens": 8192, "us": round(a8_us, 1), "tflops": round(a8_tf, 1),
+                "bf16_us": None if att is None else round(att["ms"] / att["count"] * 1e3, 1),
+                "speedup_vs_bf16": None if att is None else round(att["ms"] / att["count"] * 1e3 / a8_us, 3),
+                "roofline": {"bound": "mfma", "achieved": round(a8_tf, 1), "peak": round(blend, 1),
+                             "unit": "TFLOP/s", "frac": round(a8_tf / blend, 4),
+                             "frac_of_fp8_peak": round(a8_tf / PEAK_FP8_TFLOPS, 4),
+                             "note": "QK^T bf16 + PV MX-fp8 (v_mfma_scale_f32_32x32x64_f8f6f4); peak = harmonic "
+                                     "blend of the dense bf16 and fp8 peaks (half the FLOPs each)"}}
     out["config5_fp8"] = {
         "config": "BASELINE config 5: unet1 sampling, 32x128x128 clip, bs=2, every 3x3 conv with cin, cout % 64 == 0 "
-                  f"in MX-fp8 (e4m3 + e8m0 per 32 channels); per-step rate from {T5A}- and {T5B}-step DDPM loops",
+                  "in MX-fp8 (e4m3 + e8m0 per 32 channels) and the mid attention's PV in MX-fp8; "
+                  f"per-step rate from {T5A}- and {T5B}-step DDPM loops",
         "value": round(1 / step8, 2), "unit": "denoise-steps/s", "speedup_vs_bf16": round(step16 / step8, 3),
         "est_1000_step_s": round(est8, 1), "loops_s": [round(t, 3) for t in ts8],
         "fp8_convs_per_step": sum(v["count"] for v in mx.values()),
@@ -332,6 +350,7 @@ def sampling_leg(args, device):
                      "avg_launch_us": round(kd["ms"] / kd["count"] * 1e3, 2),
                      "note": "dominant MX-fp8 conv kernel, HIP events per launch; peak = dense MX-fp8 MFMA"},
         "kernels_ms_per_step": {k: round(v["ms"], 3) for k, v in sorted(mx.items(), key=lambda kv: -kv[1]["ms"])},
+        "mid_attention_fp8": mid8,
     }
     log(f"config5 fp8: {1 / step8:.2f} steps/s")
     del decs, u

@@ -1043,6 +1043,229 @@ __global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream_kernel(const bf16* 
               lse + (long long)b * R + row);
 }
 
+// ---- MX-fp8 PV (BASELINE config 5 sampling) --------------------------------
+// The streamed forward with O^T += V^T P^T on the block-scaled
+// v_mfma_scale_f32_32x32x64_f8f6f4: one MFMA per two 32-key tiles instead of
+// four bf16 32x32x16.  The K index k of a 32-key K-block is key
+// sigma(k) = 4 (k >> 4) + 8 ((k >> 2) & 3) + (k & 3) of its tile -- the order
+// in which lane (q, h) already holds the tile's probabilities in the S^T
+// accumulator (element 4g + e = key 4h + 8g + e) -- so P^T is the B operand
+// straight from registers (tile t -> bytes 0-15, tile t + 1 -> 16-31; the
+// instruction's lane layout, dv_mx8.hip).  V^T comes from an fp8 image
+// (mqa_v8_kernel): per 32-key tile 32 rows d of 32 e4m3 bytes in that K order
+// (the two 16-B halves swapped on rows with d & 8: conflict-free ds_read_b128)
+// and one e8m0 scale per (tile, d), the image of a chunk staged by LDS-DMA
+// beside its bf16 K.  P's scale is per key pair and query:
+// 2^(floor(max s - m) - 7) puts the pair's largest probability in [128, 256)
+// (e4m3 max 448; v_cvt_pk_fp8_f32 does not saturate); the row sums l stay f32
+// over the unquantised probabilities.  Online max only (the bounded-score path
+// computes no per-tile max to scale by).  QK^T stays bf16: at d = 32 the
+// 64-deep fp8 MFMA would be half zeros.
+constexpr int V8_TILE = 32 * 32;  // one tile's image: 32 rows d x 32 B
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int v8_key(int k) { return 4 * (k >> 4) + 8 * ((k >> 2) & 3) + (k & 3); }
+// lane (d, h)'s 16-B half h of row d in a tile image
+__device__ __forceinline__ int v8_off(int d, int h) { return d * 32 + 16 * (h ^ ((d >> 3) & 1)); }
+__device__ __forceinline__ v8i cat_v8(u32x4 a, u32x4 b) {
+  typedef __attribute__((ext_vector_type(8))) unsigned u32x8;
+  return __builtin_bit_cast(v8i, (u32x8)__builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// 16 floats (already scaled, |v| < 448) -> 16 e4m3 bytes, element i at byte i
+__device__ __forceinline__ u32x4 f8pack16(const float* v) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    // high half first over an unspecified word (no zeroing / copy move), then the low half
+    const unsigned w =
+        __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i + 2], v[4 * i + 3], __builtin_nondeterministic_value(0u), true);
+    r[i] = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i], v[4 * i + 1], w, false);
+  }
+  return r;
+}
+__device__ __forceinline__ u32x4 f8pack16(const f32x16& s) {
+  float v[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) v[e] = s[e];
+  return f8pack16(v);
+}
+__device__ __forceinline__ f32x16 mma8(v8i a, v8i b, f32x16 c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+}
+// scale exponent of a probability block whose largest log2-unit score is mx
+// (running max m): p / 2^e then peaks in [128, 256)
+__device__ __forceinline__ int p8_exp(float mx, float m) { return (int)floorf(fmaxf(mx - m, -120.f)) - 7; }
+
+// one step over the tiles in s0 / s1 (raw scores, masked), as soft_step2
+__device__ __forceinline__ void soft_step2_f8(Soft& st, f32x16& s0, f32x16& s1, const char* tV, const uint8_t* tS,
+                                              const char* tKn0, const char* tKn1, const FragOff& fo, int aoff,
+                                              int d, int h, bf16x8 q0, bf16x8 q1) {
+  const u32x4 va0 = *(const u32x4*)(tV + aoff), va1 = *(const u32x4*)(tV + V8_TILE + aoff);
+  const int sa = tS[32 * h + d];  // lane half h: the scale of tile t + h, row d
+  const float mx = col_max2(s0, s1);
+  const bool upd = mx > st.m + 8.f;
+  if (__builtin_amdgcn_ballot_w64(upd)) {
+    const float mn = upd ? mx : st.m;
+    const float a = ex2(st.m - mn);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) st.acc[e] *= a;
+    st.l *= a;
+    st.m = mn;
+  }
+  const int ex = p8_exp(mx, st.m);
+  const float mo = st.m + (float)ex;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    s0[e] = ex2(s0[e] - mo);
+    s1[e] = ex2(s1[e] - mo);
+  }
+  st.l += ldexpf(sum16(s0) + sum16(s1), ex);
+  v8i pb = cat_v8(f8pack16(s0), f8pack16(s1));
+  // the next pair's scores go into s0 / s1 only after P is packed: the K
+  // fragment offsets pass through one asm statement with P, so the loads (and
+  // MFMAs) cannot move above the exps.  Unordered, hipcc sank the exps below
+  // the next scores: 32 more live VGPRs, spills and 16 copies per step.
+  FragOff fk = fo;
+  asm volatile("" : "+v"(pb), "+v"(fk.row[0]), "+v"(fk.row[1]));
+  s0 = score(tKn0, fk, q0, q1, zero16());
+  s1 = score(tKn1, fk, q0, q1, zero16());
+  st.acc = mma8(cat_v8(va0, va1), pb, st.acc, sa, ex + 127);
+}
+__device__ __forceinline__ void soft_range2_f8(Soft& st, const char* sK, const char* sV, const uint8_t* sS, int kbeg,
+                                               int kend, int kg0, int nkeys, const FragOff& fo, int aoff, int d,
+                                               int h, bf16x8 q0, bf16x8 q1) {
+  if (kbeg >= kend) return;
+  int kt = kbeg;
+  if ((kend - kbeg) & 1) {  // one tile: K-block 1 of both operands is zero
+    f32x16 s = score(sK + kt * 32 * ROW, fo, q0, q1, zero16());
+    mask_keys(s, kg0 + kt * 32, nkeys, h);
+    const u32x4 va = *(const u32x4*)(sV + kt * V8_TILE + aoff), z = {0u, 0u, 0u, 0u};
+    const int sa = h ? 127 : sS[kt * 32 + d];  // (tile kt + 1 may lie past the chunk)
+    const float mx = col_max(s);
+    const bool upd = mx > st.m + 8.f;
+    if (__builtin_amdgcn_ballot_w64(upd)) {
+      const float mn = upd ? mx : st.m;
+      const float a = st.m == -INFINITY ? 0.f : ex2(st.m - mn);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) st.acc[e] *= a;
+      st.l *= a;
+      st.m = mn;
+    }
+    const int ex = p8_exp(mx, st.m);
+    const float mo = st.m + (float)ex;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s[e] = ex2(s[e] - mo);
+    st.l += ldexpf(sum16(s), ex);
+    st.acc = mma8(cat_v8(va, z), cat_v8(f8pack16(s), z), st.acc, sa, ex + 127);
+    ++kt;
+  }
+  if (kt >= kend) return;
+  f32x16 s0 = score(sK + kt * 32 * ROW, fo, q0, q1, zero16());
+  f32x16 s1 = score(sK + (kt + 1) * 32 * ROW, fo, q0, q1, zero16());
+  mask_keys(s0, kg0 + kt * 32, nkeys, h);
+  mask_keys(s1, kg0 + (kt + 1) * 32, nkeys, h);
+  if (st.m == -INFINITY) st.m = col_max2(s0, s1);
+  for (; kt < kend; kt += 2) {
+    const int kn0 = kt + 2 < kend ? kt + 2 : kt, kn1 = kn0 + 1;
+    soft_step2_f8(st, s0, s1, sV + kt * V8_TILE, sS + kt * 32, sK + kn0 * 32 * ROW, sK + kn1 * 32 * ROW, fo, aoff,
+                  d, h, q0, q1);
+    mask_keys(s0, kg0 + kn0 * 32, nkeys, h);
+    mask_keys(s1, kg0 + kn1 * 32, nkeys, h);
+  }
+}
+
+// the fp8 V^T image of clip b: [NKP / 32 tiles][32 d][32 B] then the scales
+// [NKP / 32][32 d] (NKP * 33 bytes per clip).  grid (ceil(NKP / 256), B),
+// thread (tile blockIdx.x * 8 + tid / 32, d = tid % 32); vp: dv_mqa_prep's
+// bf16 image (null value at key 0, zero padding)
+__global__ __launch_bounds__(256) void mqa_v8_kernel(const bf16* __restrict__ vp, uint8_t* __restrict__ v8,
+                                                     int NKP) {
+  const int b = blockIdx.y, t = blockIdx.x * 8 + (threadIdx.x >> 5), d = threadIdx.x & 31;
+  if (t * 32 >= NKP) return;
+  const bf16* src = vp + ((long long)b * NKP + t * 32) * DH + d;
+  float v[32], amax = 0.f;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    v[k] = (float)src[v8_key(k) * DH];
+    amax = fmaxf(amax, fabsf(v[k]));
+  }
+  // e8m0 scale 2^(sb - 127) with amax / scale in [128, 256)
+  const int eb = (int)((__float_as_uint(amax) >> 23) & 255u);
+  const int sb = amax > 0.f ? max(eb - 7, 0) : 127;
+  const float inv = __uint_as_float((unsigned)(254 - sb) << 23);
+#pragma unroll
+  for (int k = 0; k < 32; ++k) v[k] *= inv;
+  uint8_t* img = v8 + (long long)b * NKP * 33;
+  char* row = (char*)img + (long long)t * V8_TILE + d * 32;
+  const int sw = (d >> 3) & 1;
+  *(u32x4*)(row + 16 * sw) = f8pack16(v);
+  *(u32x4*)(row + 16 * (1 - sw)) = f8pack16(v + 16);
+  img[(long long)NKP * 32 + t * 32 + d] = (uint8_t)sb;
+}
+
+// chunk pieces: bf16 K rows (16 per piece, swizzled as dma_kv), the chunk's
+// fp8 V^T tiles (one per piece) and one piece of scales (32 tiles' worth)
+__device__ __forceinline__ void dma_kv8_chunk(const __amdgpu_buffer_rsrc_t& rk, const __amdgpu_buffer_rsrc_t& rv,
+                                              char* sK, char* sV, char* sS, int row0, int nrows, int NKP, int wave,
+                                              int lane) {
+  const int np = nrows / 16, nv = nrows / 32;
+  const int rr = lane >> 2, slot = lane & 3;
+  for (int i = wave; i < np + nv + 1; i += NW) {
+    if (i < np) {
+      const int row = row0 + i * 16 + rr;
+      dma16(rk, sK + i * 1024, row * ROW + 16 * (slot ^ ((row >> 2) & 3)));
+    } else if (i < np + nv) {
+      const int t = i - np;
+      dma16(rv, sV + t * V8_TILE, (unsigned)((row0 / 32 + t) * V8_TILE + lane * 16));
+    } else {
+      dma16(rv, sS, (unsigned)(NKP * 32 + row0 + lane * 16));  // scales of tiles row0 / 32 ..
+    }
+  }
+}
+
+// grid (ceil(R / 256), B), 1024 threads, dynamic LDS 2 * (SCK * (64 + 32) + 1024) B
+constexpr int S8_BUF = SCK * ROW + SCK * 32 + 1024;
+__global__ __launch_bounds__(NW * 64) void mqa_fwd_fa_stream8_kernel(const bf16* __restrict__ q,
+                                                                     const bf16* __restrict__ kp,
+                                                                     const uint8_t* __restrict__ v8,
+                                                                     bf16* __restrict__ o, float* lse, int R,
+                                                                     int NKP, int nkeys) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rg = wave & (RG - 1), kh = wave / RG;
+  const int b = blockIdx.y;
+  const __amdgpu_buffer_rsrc_t rk = dma_rsrc(kp + (long long)b * NKP * 32, (unsigned)NKP * ROW);
+  const __amdgpu_buffer_rsrc_t rv = dma_rsrc(v8 + (long long)b * NKP * 33, (unsigned)NKP * 33);
+  auto buf_k = [&](int i) { return smem + i * S8_BUF; };
+  auto buf_v = [&](int i) { return smem + i * S8_BUF + SCK * ROW; };
+  auto buf_s = [&](int i) { return smem + i * S8_BUF + SCK * ROW + SCK * 32; };
+  const int nch = (NKP + SCK - 1) / SCK;
+  dma_kv8_chunk(rk, rv, buf_k(0), buf_v(0), buf_s(0), 0, min(SCK, NKP), NKP, wave, lane);
+  const int row = blockIdx.x * RG * 32 + rg * 32 + r;
+  const bool rok = row < R;
+  const bf16* qrow = q + ((long long)b * R + (rok ? row : 0)) * 32;
+  const bf16x8 qf0 = load_row8(qrow + 8 * h, rok), qf1 = load_row8(qrow + 16 + 8 * h, rok);
+  const FragOff fo = frag_off(lane);
+  const int aoff = v8_off(r, h);
+  Soft st{zero16(), zero16(), -INFINITY, 0.f};
+  for (int ch = 0; ch < nch; ++ch) {
+    // chunk ch landed (the only DMA in flight); every wave is done with the
+    // buffer chunk ch + 1 goes to (it held chunk ch - 1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int row0 = ch * SCK;
+    if (ch + 1 < nch)
+      dma_kv8_chunk(rk, rv, buf_k((ch + 1) & 1), buf_v((ch + 1) & 1), buf_s((ch + 1) & 1), row0 + SCK,
+                    min(SCK, NKP - row0 - SCK), NKP, wave, lane);
+    const int nkt = min(SCK, NKP - row0) / 32, kmid = (nkt + 1) / 2;
+    soft_range2_f8(st, buf_k(ch & 1), buf_v(ch & 1), (const uint8_t*)buf_s(ch & 1), kh ? kmid : 0,
+                   kh ? nkt : kmid, row0, nkeys, fo, aoff, r, h, qf0, qf1);
+  }
+  soft_finish(st, (float*)smem + rg * 18 * 64, kh, lane, h, rok, o + ((long long)b * R + row) * 32,
+              lse + (long long)b * R + row);
+}
+
 // (A ping-pong forward -- two 8-wave groups per SIMD a half iteration apart
 // -- measured slower in round 4, profiles/r04b_pp_ab.txt; removed in round 5.)
 
@@ -1409,6 +1632,28 @@ extern "C" int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, con
                                                 ldo, lse, N, NKP, N + 1, H, scale);
   }
   return check_launch("mqa_fwd");
+}
+
+extern "C" int dv_mqa_fwd_fp8_ws(int B, int NKP, long long* bytes) {
+  DV_REQUIRE(bytes && B > 0 && NKP > 0 && NKP % 32 == 0, "bad arguments");
+  *bytes = (long long)B * NKP * 33;
+  return DV_OK;
+}
+
+extern "C" int dv_mqa_fwd_fp8(const void* q, int ldq, const void* kp, const void* vp, void* v8, long long v8_bytes,
+                              void* o, int ldo, float* lse, int B, int N, int NKP, int H, void* stream) {
+  DV_REQUIRE(q && kp && vp && v8 && o && lse && B > 0 && N > 0, "bad arguments");
+  DV_REQUIRE(NKP % 32 == 0 && NKP >= N + 1 && ldq == H * DH && ldo == H * DH && H > 0, "bad shape / strides");
+  DV_REQUIRE(v8_bytes >= (long long)B * NKP * 33 && (long long)NKP * fa::ROW < (1ll << 31),
+             "workspace too small (see dv_mqa_fwd_fp8_ws) or sequence too long");
+  hipStream_t st = (hipStream_t)stream;
+  fa::mqa_v8_kernel<<<dim3((NKP / 32 + 7) / 8, B), 256, 0, st>>>((const bf16*)vp, (uint8_t*)v8, NKP);
+  const int R = N * H;
+  const int lds = 2 * fa::S8_BUF;
+  fa::set_lds((const void*)fa::mqa_fwd_fa_stream8_kernel, lds);
+  fa::mqa_fwd_fa_stream8_kernel<<<dim3((R + 255) / 256, B), fa::NW * 64, lds, st>>>(
+      (const bf16*)q, (const bf16*)kp, (const uint8_t*)v8, (bf16*)o, lse, R, NKP, N + 1);
+  return check_launch("mqa_fwd_fp8");
 }
 
 extern "C" int dv_mqa_bwd_ws(int dtype, int ldq, int ldo, int B, int N, int NKP, int H,

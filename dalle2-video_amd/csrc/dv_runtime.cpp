@@ -34,7 +34,7 @@ int check_launch(const char* what) {
 }  // namespace dv
 
 extern "C" const char* dv_last_error(void) { return dv::g_last_error.c_str(); }
-extern "C" int dv_abi_version(void) { return 3; }
+extern "C" int dv_abi_version(void) { return 4; }
 
 extern "C" int dv_zero_f32(float* p, long long n, void* stream) {
   if (!p) {

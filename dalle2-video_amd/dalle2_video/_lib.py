@@ -86,6 +86,8 @@ _SIGS = {
     "dv_gaussian_blur": [_P, _P, _L, _I, _I, _I, _P, _P],
     "dv_mqa_prep": [_I, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P, _P],
     "dv_mqa_fwd": [_I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _F, _P, _P],
+    "dv_mqa_fwd_fp8_ws": [_I, _I, _P],
+    "dv_mqa_fwd_fp8": [_P, _I, _P, _P, _P, _L, _P, _I, _P, _I, _I, _I, _I, _P],
     "dv_mqa_bwd_ws": [_I, _I, _I, _I, _I, _I, _I, _P],
     "dv_mqa_bwd": [_I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _L, _P, _I, _P, _I, _I, _I, _I, _F, _I, _P],
     "dv_comm_unique_id": [_P],

@@ -1812,6 +1812,14 @@ MQA_DH = 32
 MQA_BF16_BWD_MAX_NKP = 1280
 
 
+def mqa_fp8_ok(q, NKP, H, ldq, needs_grad):
+    """MX-fp8 PV (dv_mqa_fwd_fp8): inside mx8_convs() (the unet's fp8 flag,
+    BASELINE config 5), forward only, bf16 dense rows, and a clip whose K / V
+    stream through LDS (NKP > 1280: the config-5 8,193 keys)."""
+    return (_Mx8State.active > 0 and not needs_grad and q.dtype == torch.bfloat16 and ldq == H * MQA_DH
+            and NKP > MQA_BF16_BWD_MAX_NKP)
+
+
 class MQAFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, kv, null_kv, B, N, H, scale):
@@ -1836,6 +1844,17 @@ class MQAFn(torch.autograd.Function):
              ctypes_float(scale), ptr(kmax), stream())
         o = torch.empty(B * N, H * MQA_DH, dtype=q.dtype, device=dev)
         lse = torch.empty(B, H, N, dtype=torch.float32, device=dev)
+        if mqa_fp8_ok(q, NKP, H, qc.shape[-1], any(ctx.needs_input_grad[:3])):
+            # sampling inside mx8_convs() on a K/V-streamed clip: PV in MX-fp8
+            # (dv_mqa_fwd_fp8; forward only -- no autograd records this call)
+            need = ctypes.c_longlong(0)
+            call("dv_mqa_fwd_fp8_ws", B, NKP, ctypes.byref(need))
+            v8 = torch.empty(need.value, dtype=torch.uint8, device=dev)
+            _launch("attn:mqa_fwd8", 4.0 * B * H * N * (N + 1) * MQA_DH, 0,
+                    lambda: call("dv_mqa_fwd_fp8", ptr(qc), qc.shape[-1], ptr(kp), ptr(vp), ptr(v8), need.value,
+                                 ptr(o), o.shape[-1], ptr(lse), B, N, NKP, H, stream()))
+            ctx.meta = None
+            return o
         _launch("attn:mqa_fwd", 4.0 * B * H * N * (N + 1) * MQA_DH, 0,
                 lambda: call("dv_mqa_fwd", dt(q), ptr(qc), qc.shape[-1], ptr(kp), ptr(vp), ptr(o),
                              o.shape[-1], ptr(lse), B, N, NKP, H, ctypes_float(scale), ptr(kmax), stream()))

@@ -511,6 +511,15 @@ int dv_mqa_prep(int dtype, const void* kv, int ldkv, const float* null_kv, void*
  * keeps the online running max).                                           */
 int dv_mqa_fwd(int dtype, const void* q, int ldq, const void* kp, const void* vp, void* o, int ldo,
                float* lse, int B, int N, int NKP, int H, float scale, const float* kmax, void* stream);
+/* MX-fp8 PV forward (BASELINE config 5 sampling; forward only): the
+ * K/V-streamed forward with O^T += V^T P^T on the block-scaled
+ * v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 P and V, an e8m0 scale per 32 keys;
+ * QK^T stays bf16).  kp / vp: dv_mqa_prep's bf16 images; v8 (>=
+ * dv_mqa_fwd_fp8_ws bytes) receives V's fp8 image; o / lse as dv_mqa_fwd's
+ * streamed bf16 path (dense rows, lse [B][N*H] log2 units).                 */
+int dv_mqa_fwd_fp8_ws(int B, int NKP, long long* bytes);
+int dv_mqa_fwd_fp8(const void* q, int ldq, const void* kp, const void* vp, void* v8, long long v8_bytes,
+                   void* o, int ldo, float* lse, int B, int N, int NKP, int H, void* stream);
 /* f32 scratch dv_mqa_bwd needs (floats); same path choice as dv_mqa_fwd.     */
 int dv_mqa_bwd_ws(int dtype, int ldq, int ldo, int B, int N, int NKP, int H, long long* floats);
 /* dq, dkv (k at 0, v at 32, stride lddkv) and dnull (+)= (accumulate);
