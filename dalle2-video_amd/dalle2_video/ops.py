@@ -1822,15 +1822,18 @@ def mqa_fp8_ok(q, NKP, H, ldq, needs_grad):
 
 class MQAFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, kv, null_kv, B, N, H, scale):
+    def forward(ctx, q, kv, null_kv, B, N, H, scale, grad_mode=True):
         require_gpu(q, kv, null_kv)
         dev = q.device
         NKP = (N + 1 + 31) // 32 * 32
+        # needs_input_grad follows requires_grad even under no_grad (null_kv is
+        # a Parameter): `grad_mode` is the caller's torch.is_grad_enabled(), so
+        # sampling never takes the training-only paths below
+        needs_grad = grad_mode and any(ctx.needs_input_grad[:3])
         # a bf16 sequence too long for the bf16 backward (config 5: 8,193 keys)
         # that needs gradients runs forward AND backward on the f32 kernels (one
         # lse layout for both); outputs and input gradients stay bf16
-        ctx.cast = (q.dtype == torch.bfloat16 and NKP > MQA_BF16_BWD_MAX_NKP
-                    and any(ctx.needs_input_grad[:3]))
+        ctx.cast = q.dtype == torch.bfloat16 and NKP > MQA_BF16_BWD_MAX_NKP and needs_grad
         if ctx.cast:
             q, kv = q.float(), kv.float()
         qc, kvc = q.contiguous(), kv.contiguous()
@@ -1844,7 +1847,7 @@ class MQAFn(torch.autograd.Function):
              ctypes_float(scale), ptr(kmax), stream())
         o = torch.empty(B * N, H * MQA_DH, dtype=q.dtype, device=dev)
         lse = torch.empty(B, H, N, dtype=torch.float32, device=dev)
-        if mqa_fp8_ok(q, NKP, H, qc.shape[-1], any(ctx.needs_input_grad[:3])):
+        if mqa_fp8_ok(q, NKP, H, qc.shape[-1], needs_grad):
             # sampling inside mx8_convs() on a K/V-streamed clip: PV in MX-fp8
             # (dv_mqa_fwd_fp8; forward only -- no autograd records this call)
             need = ctypes.c_longlong(0)
@@ -1885,11 +1888,11 @@ class MQAFn(torch.autograd.Function):
                              ctypes_float(scale), int(sn[1]) if sn else 0, stream()))
         if ctx.cast:
             dq, dkv = dq.to(torch.bfloat16), dkv.to(torch.bfloat16)
-        return dq, dkv, (None if sn else dnull), None, None, None, None
+        return dq, dkv, (None if sn else dnull), None, None, None, None, None
 
 
 def mqa(q, kv, null_kv, B, N, H, scale):
-    return MQAFn.apply(q, kv, null_kv, B, N, H, scale)
+    return MQAFn.apply(q, kv, null_kv, B, N, H, scale, torch.is_grad_enabled())
 
 
 # ---------------------------------------------------------------------------
