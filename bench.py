@@ -413,6 +413,11 @@ def main():
         trainer(video_embed=embed, video=video, unet_number=1)
         trainer.update(1)
 
+    # the trainer captures its HIP graph on the 4th call (the first update()
+    # builds the flat gradient buffers, then two eager calls warm the pass):
+    # with fewer warm-up steps the capture lands in the timed region
+    if args.warmup < 4 and not args.no_graphs:
+        log(f"warning: --warmup {args.warmup} < 4 times the graph capture (the 4th call) as a step")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
