@@ -1761,7 +1761,7 @@ int launch_fwd_glds(const ConvFwdArgs<bf16>& a, hipStream_t st) {
 
 // ---------------------------------------------------------------------------
 // bf16 3x3 forward / dgrad, stripe form (cin == 64 single source, cout % 64
-// == 0, W in {32, 64}): one workgroup = 64 output channels over a contiguous
+// == 0, W in {32, 64, 128}): one workgroup = 64 output channels over a contiguous
 // range of 128-pixel stages.  8 waves: 4 pixel tiles x 2 channel halves, one
 // 32 x 32 accumulator each (initialised to the bias).  Each wave keeps the A
 // fragments of its 32 output channels for all 36 k-steps in REGISTERS (144
@@ -1803,7 +1803,11 @@ struct FsGeom {
   static constexpr int NPW = (NP + 7) / 8;           // per wave (spare ones repeat the last)
   static constexpr int NP0 = (SEG + 2) * PPR;        // stage 0 stages its whole window
   static constexpr int NPW0 = (NP0 + 7) / 8;
-  static constexpr int WOFF = (3 * SEG + 2) * ROWB;  // weight image: beyond the rows of stages 0..2
+  // weight image: beyond the rows of stages 0..2; where that does not fit
+  // (W = 128: 19-KB rows) beyond stages 0..1, and stage 2's rows go out only
+  // after the weights are in registers (LATE)
+  static constexpr bool LATE = (3 * SEG + 2) * ROWB + 64 * FS_WROW > 160 * 1024;
+  static constexpr int WOFF = (LATE ? 2 * SEG + 2 : 3 * SEG + 2) * ROWB;
   static constexpr int LDS = R * ROWB > WOFF + 64 * FS_WROW ? R * ROWB : WOFF + 64 * FS_WROW;
   static_assert(LDS <= 160 * 1024, "stripe ring exceeds the LDS");
 };
@@ -1896,9 +1900,9 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     for (int e = 0; e < 4; ++e) bias_acc[4 * g + e] = b[e];
   }
   if (nst > 1) issue(1);
-  if (nst > 2) issue(2);
+  if (!G::LATE && nst > 2) issue(2);
   // stage 0, weights and bias landed; stages 1 and 2 (when issued) younger
-  if (nst > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
+  if (!G::LATE && nst > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
   else if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1910,6 +1914,10 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();  // the weight image is dead: stage 3's rows may land over it
+  // LATE: stage 2's rows now (over the dead weight image).  They are still
+  // issued after D1 and before stage 0's residual loads: the per-stage vmcnt
+  // counts below hold unchanged.
+  if (G::LATE && nst > 2) issue(2);
   DV_STAMP_AT(1);
 
   const int r = lane & 31, h = lane >> 5;
@@ -2062,7 +2070,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
 }
 
 bool fwd_stripe_ok(long long M, int h, int w, int cin, bool split, int cout, int ks, int ld0) {
-  return ks == 3 && cin == 64 && !split && cout % 64 == 0 && (w == 32 || w == 64) &&
+  return ks == 3 && cin == 64 && !split && cout % 64 == 0 && (w == 32 || w == 64 || w == 128) &&
          h % (128 / w) == 0 && M % 128 == 0 && ld0 % 8 == 0 && M * ld0 * 2 < (long long)DMA_OOB;
 }
 
@@ -2090,6 +2098,7 @@ int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
                     : nres == 1 ? (void)conv_fwd_stripe_kernel<WW, 1, false><<<grid, 512, 0, st>>>(a, nstages, sps) \
                                 : DV_FS(WW, 0))
   if (a.W == 64) DV_FSR(64);
+  else if (a.W == 128) DV_FSR(128);
   else DV_FSR(32);
 #undef DV_FSR
 #undef DV_FS

@@ -112,7 +112,7 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0, n
     """Kernel instantiation dv_conv_fwd dispatches to (mirror of conv_fwd_t /
     glds_tile in dv_conv.hip) — names the launch for the live roofline."""
     if (dtype_name == "bf16" and ks == 3 and cin == 64 and c0 == cin and cout % 64 == 0
-            and w in (32, 64) and h % (128 // w) == 0 and m % 128 == 0 and m * maxld < (1 << 31)
+            and w in (32, 64, 128) and h % (128 // w) == 0 and m % 128 == 0 and m * maxld < (1 << 31)
             and gn_P % 128 == 0):
         return f"conv_fwd_stripe_kernel<{w}>"
     if (dtype_name == "bf16" and ks == 3 and cin % 32 == 0 and c0 % 32 == 0 and cout % 64 == 0
@@ -153,7 +153,7 @@ def window_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf, gn_P
     return (not _NO_WINDOW and w in _WINDOW_W and x0.dtype == torch.bfloat16 and ksize == 3
             and gn_P % 128 == 0
             and geom and cin % 16 == 0 and c0 % 16 == 0 and cout % 64 == 0
-            and not (cin == 64 and c0 == cin and w in (32, 64))  # the resident-weight stripe kernel
+            and not (cin == 64 and c0 == cin and w in (32, 64, 128))  # the resident-weight stripe kernel
             and ld0 % 8 == 0 and ld1 % 8 == 0 and ldy % 4 == 0 and ldres % 4 == 0 and ldres2 % 4 == 0
             and nf * h * w * max(ld0, ld1) * 2 < (1 << 31)
             and x0.data_ptr() % 16 == 0 and (x1 is None or x1.data_ptr() % 16 == 0))

@@ -29,9 +29,11 @@ CASES = [
     (3, 32, 16, 64, 0, 64, 3),      # window wgrad W=16, H=32 (four 8-row stages per frame)
     (16, 32, 32, 128, 0, 64, 1),    # 1x1 stripe wgrad (res_conv-like), 2 channel chunks
     (8, 16, 16, 64, 64, 128, 1),    # 1x1 stripe wgrad, dual source
-    # stripe forward / dgrad (64 input channels, W in {32, 64})
+    # stripe forward / dgrad (64 input channels, W in {32, 64, 128})
     (8, 32, 32, 64, 0, 128, 3),     # W=32, 2 cout tiles (dgrad: 128 -> 64 implicit GEMM)
     (4, 64, 64, 64, 0, 64, 3),      # W=64, forward and dgrad both stripe
+    (2, 128, 128, 64, 0, 64, 3),    # W=128 (config 5's 128x128 stage): one-row stages, late stage-2 rows
+    (1, 128, 128, 64, 0, 128, 3),   # W=128, 2 cout tiles
     # 8x8-frame forward / dgrad (H = W = 8, 16-channel chunks, two frames per block)
     (4, 8, 8, 48, 16, 64, 3),       # dual source at a 16-channel boundary, dgrad 64 -> 48 + 16
     (6, 8, 8, 128, 0, 192, 3),      # three channel blocks (no XCD regrouping), 8 chunks
