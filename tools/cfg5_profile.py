@@ -1,6 +1,7 @@
 """Unet1 forward at a sampling shape -- default the BASELINE config-5 shape (32 frames
-x 128 x 128, bs 2, bf16; argv: bs frames size) -- per-shape conv times
-(KernelTimer) and the whole forward by HIP-graph replay."""
+x 128 x 128, bs 2, bf16; argv: bs frames size [fp8]) -- per-shape conv times
+(KernelTimer) and the whole forward by HIP-graph replay; a 4th argument `fp8`
+runs the MX-fp8 sampling mode (Unet3D.fp8)."""
 import os
 import sys
 
@@ -14,6 +15,7 @@ from dalle2_video.utils import deterministic_fill_  # noqa: E402
 un = D.Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
 deterministic_fill_(un)
 un = un.cuda()
+un.fp8 = len(sys.argv) > 4 and sys.argv[4] == "fp8"
 bs, fr, sz = (int(v) for v in (sys.argv[1:4] if len(sys.argv) > 3 else (2, 32, 128)))
 x = torch.randn(bs, 3, fr, sz, sz, device="cuda")
 emb = torch.randn(bs, 512, device="cuda")
