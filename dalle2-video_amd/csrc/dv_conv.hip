@@ -1381,8 +1381,10 @@ int launch_wgrad_glds(WgradGArgs a, hipStream_t st) {
   // batched GEMMs have tiny outputs: cap the blocks adding into one element
   // (same-address atomic contention); measured at 16 / 32 / 64 / 128 for the
   // cross-attention token reductions (4 x 16384 rows, 32 x 64): 19.9 / 11.6 /
-  // 8.5 / 8.7 us -- below 64 the per-block row loop dominates
-  constexpr int cap = 64;
+  // 8.5 / 8.7 us -- below 64 the per-block row loop dominates.  Wider outputs
+  // (32 x K) add K / 64 times the atomics per block: the cap falls with K
+  // (the chip's L2 atomics run ~270 G adds/s, profiles/r04d_l2_atomic_probe.txt)
+  const int cap = a.K <= 64 ? 64 : std::max(16, 64 * 64 / a.K);
   if (a.batch_pix > 0 && (a.batch_pix + per - 1) / per > cap)
     per = ((a.batch_pix + cap - 1) / cap + 63) / 64 * 64;
   unsigned splits;
