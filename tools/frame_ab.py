@@ -1,6 +1,6 @@
 """Per-launch time of the window-form 3x3 conv (conv_fwd_frame_kernel) at the
-Cfg2 8x8 / 16x16 shapes — run once per kernel variant (env knobs such as
-DV_FRAME_PF are read once per process):  python tools/frame_ab.py [tag]"""
+Cfg2 8x8 / 16x16 shapes — run once per library build (DV_HIP_LIB selects one;
+tools/frame_pmc.sh runs it under the PMC passes):  python tools/frame_ab.py [tag]"""
 import os
 import sys
 

@@ -84,7 +84,7 @@ def frame_case(nf, h, w, cin, cout):
     f()
     m = nf * h * w
     co = 32 if (m // 128) * (cout // 64) <= 128 else 64
-    # 8 waves on 128 channels where 64-channel tiles would take two rounds (dv_conv.hip, DV_FRAME_W8)
+    # 8 waves on 128 channels where 64-channel tiles would take two rounds (dv_conv.hip, launch_fwd_frame)
     w8 = w == 16 and co == 64 and cout % 128 == 0 and (m // 128) * (cout // 64) > 256
     cw = 128 if w8 else co
     report(f"frame fwd ({nf},{h},{w}) {cin}->{cout} {'8 waves x ' if w8 else ''}co{cw}",
