@@ -1892,14 +1892,20 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
       dma16(wr, sW + piece * 1024, c < 72 ? (unsigned)((row * 576 + c * 8) * 2) : DMA_OOB);
     }
   }
-  // bias of the lane's 16 accumulator channels (8g + 4h + e of the wave's 32)
+  // bias of the lane's 16 accumulator channels (8g + 4h + e of the wave's 32),
+  // by SCALAR loads of the wave's 32 (lgkmcnt): a vector load here was the
+  // last vmcnt op hipcc knew of before the stage loop, so it put a vmcnt(0)
+  // at the loop entry -- which also drained the DMA of stages 1 and 2
   f32x16 bias_acc;
+  {
+    float bw[32];
+    const float* bp = p.bias ? p.bias + co0 + ch * 32 : nullptr;
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 b = p.bias ? *(const f32x4*)(p.bias + co0 + ch * 32 + 8 * g + 4 * (lane >> 5))
-                           : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 32; ++j) bw[j] = bp ? __builtin_nontemporal_load(bp + j) : 0.f;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bias_acc[4 * g + e] = b[e];
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bias_acc[4 * g + e] = (lane >> 5) ? bw[8 * g + 4 + e] : bw[8 * g + e];
   }
   if (nst > 1) issue(1);
   if (!G::LATE && nst > 2) issue(2);
@@ -1907,19 +1913,28 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   if (!G::LATE && nst > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
   else if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // raw barriers (asm, memory-clobbering): __syncthreads()'s fence made hipcc
+  // wait for EVERY outstanding vector-memory op (vmcnt(0)) -- the DMA of
+  // stages 1 and 2 as well -- before the weights could be read
+  asm volatile("s_barrier" ::: "memory");
   u32x4 wA[36];
   {
-    const char* aw = smem + G::WOFF + (ch * 32 + (lane & 31)) * FS_WROW + (lane >> 5) * 16;
-#pragma unroll
-    for (int k = 0; k < 36; ++k) wA[k] = *(const u32x4*)(aw + 32 * k);
+    // inline-asm reads (a compiler-visible LDS read beside the pending DMA
+    // got a vmcnt(0) in front in some instantiations: stages 1 and 2 drained)
+    const unsigned aw = lds_addr(smem + G::WOFF + (ch * 32 + (lane & 31)) * FS_WROW + (lane >> 5) * 16);
+    static_for<0, 36>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      wA[k] = ds_read_b128_off<32 * k>(aw);
+    });
+    static_for<0, 36>([&](auto kk) { lgkm_wait_tied<0>(wA[decltype(kk)::value]); });
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();  // the weight image is dead: stage 3's rows may land over it
+  asm volatile("s_barrier" ::: "memory");  // the weight image is dead: stage 3's rows may land over it
   // LATE: stage 2's rows now (over the dead weight image).  They are still
   // issued after D1 and before stage 0's residual loads: the per-stage vmcnt
   // counts below hold unchanged.
   if (G::LATE && nst > 2) issue(2);
+  asm volatile("" ::: "memory");  // (stage 0's residual loads stay younger than D2)
   DV_STAMP_AT(1);
 
   const int r = lane & 31, h = lane >> 5;
