@@ -51,8 +51,18 @@ __global__ void cl_to_ncthw_kernel(const T* y, int ld, float* x, int B, int C, i
 // division per unit (a flat 64-bit index took four 64-bit divisions, each a
 // ~150-instruction sequence, and left the pass VALU-bound)
 // MODE 1 adds r0 / r1 (high-res, strides ldr0 / ldr1; null: none) to the output
-template <typename T, int MODE>
-__global__ void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* z, int ldz,
+// Rows past the grid's 65,535 go two per trip, both rows' loads ahead of
+// either row's stores.
+template <typename T>
+struct ShufIn {
+  u32x4 a[4];  // MODE 1: the low-res span; MODE 0: the four high-res pixels
+  u32x4 b[4];  // MODE 1: r0 at the four high-res pixels; MODE 0: z (the low-res span)
+  u32x4 c[4];  // MODE 1: r1 at the four high-res pixels
+};
+// NX: the extra sources (MODE 1: r0, r1; MODE 0: z), a template count so no
+// load sits under a run-time branch (hipcc drained vmcnt at each such join)
+template <typename T, int MODE, int NX>
+__global__ __launch_bounds__(256, 2) void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* z, int ldz,
                                const T* r0, int ldr0, const T* r1, int ldr1, int nf, int H, int W,
                                int C, int act) {
   constexpr int VEC = 16 / sizeof(T);
@@ -60,57 +70,77 @@ __global__ void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* 
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= W * cg) return;
   const int x = t / cg, g = t - x * cg;
-  for (int row = blockIdx.y; row < nf * H; row += gridDim.y) {
+  const int c0 = g * VEC;
+  const int rows = nf * H;
+  auto hp_of = [&](int row, int i, int j) {
     const long long f = row / H;
     const int y = row - (int)f * H;
+    return (f * 2 * H + 2 * y + i) * 2 * W + 2 * x + j;
+  };
+  auto load = [&](int row, ShufIn<T>& in) {
     const long long lp = (long long)row * W + x;  // low-res pixel
-    const int c0 = g * VEC;
+    if (MODE == 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) in.a[q] = *(const u32x4*)(src + lp * lds + c0 * 4 + q * VEC);
+      if constexpr (NX >= 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) in.b[q] = *(const u32x4*)(r0 + hp_of(row, q >> 1, q & 1) * ldr0 + c0);
+      }
+      if constexpr (NX >= 2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) in.c[q] = *(const u32x4*)(r1 + hp_of(row, q >> 1, q & 1) * ldr1 + c0);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) in.a[q] = *(const u32x4*)(src + hp_of(row, q >> 1, q & 1) * lds + c0);
+      if constexpr (NX >= 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) in.b[q] = *(const u32x4*)(z + lp * ldz + c0 * 4 + q * VEC);
+      }
+    }
+  };
+  auto finish = [&](int row, const ShufIn<T>& in) {
+    const long long lp = (long long)row * W + x;
     float lo[4 * VEC];  // low-res span, element (c - c0)*4 + i*2 + j
     if (MODE == 1) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Vec<T>::to_f(*(const u32x4*)(src + lp * lds + c0 * 4 + q * VEC), lo + q * VEC);
+      for (int q = 0; q < 4; ++q) Vec<T>::to_f(in.a[q], lo + q * VEC);
 #pragma unroll
       for (int e = 0; e < 4 * VEC; ++e) lo[e] = act == DV_ACT_SILU ? silu_f(lo[e]) : lo[e];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int q = 0; q < 4; ++q) {
+        float hv[VEC];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const long long hp = (f * 2 * H + 2 * y + i) * 2 * W + 2 * x + j;
-          float hv[VEC];
+        for (int e = 0; e < VEC; ++e) hv[e] = lo[e * 4 + q];
+        if constexpr (NX >= 1) {
+          float rv[VEC];
+          Vec<T>::to_f(in.b[q], rv);
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) hv[e] = lo[e * 4 + i * 2 + j];
-          if (r0) {
-            float rv[VEC];
-            Vec<T>::to_f(*(const u32x4*)(r0 + hp * ldr0 + c0), rv);
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) hv[e] += rv[e];
-          }
-          if (r1) {
-            float rv[VEC];
-            Vec<T>::to_f(*(const u32x4*)(r1 + hp * ldr1 + c0), rv);
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) hv[e] += rv[e];
-          }
-          T o[VEC];
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) o[e] = (T)hv[e];
-          *(u32x4*)(dst + hp * ldd + c0) = *(const u32x4*)o;
+          for (int e = 0; e < VEC; ++e) hv[e] += rv[e];
         }
+        if constexpr (NX >= 2) {
+          float rv[VEC];
+          Vec<T>::to_f(in.c[q], rv);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) hv[e] += rv[e];
+        }
+        T o[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) o[e] = (T)hv[e];
+        *(u32x4*)(dst + hp_of(row, q >> 1, q & 1) * ldd + c0) = *(const u32x4*)o;
+      }
     } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int q = 0; q < 4; ++q) {
+        float hv[VEC];
+        Vec<T>::to_f(in.a[q], hv);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const long long hp = (f * 2 * H + 2 * y + i) * 2 * W + 2 * x + j;
-          float hv[VEC];
-          Vec<T>::to_f(*(const u32x4*)(src + hp * lds + c0), hv);
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) lo[e * 4 + i * 2 + j] = hv[e];
-        }
-      if (z) {  // backward of SiLU+shuffle: multiply by silu'(z)
+        for (int e = 0; e < VEC; ++e) lo[e * 4 + q] = hv[e];
+      }
+      if constexpr (NX >= 1) {  // backward of SiLU+shuffle: multiply by silu'(z)
         float zz[4 * VEC];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) Vec<T>::to_f(*(const u32x4*)(z + lp * ldz + c0 * 4 + q * VEC), zz + q * VEC);
+        for (int q = 0; q < 4; ++q) Vec<T>::to_f(in.b[q], zz + q * VEC);
 #pragma unroll
         for (int e = 0; e < 4 * VEC; ++e) {
           const float sg = sigmoid_f(zz[e]);
@@ -125,6 +155,21 @@ __global__ void shuffle_kernel(const T* src, int lds, T* dst, int ldd, const T* 
         *(u32x4*)(dst + lp * ldd + c0 * 4 + q * VEC) = *(const u32x4*)o;
       }
     }
+  };
+  const int gy = gridDim.y;
+  int row = blockIdx.y;
+  for (; row + gy < rows; row += 2 * gy) {
+    ShufIn<T> in0, in1;
+    load(row, in0);
+    load(row + gy, in1);
+    __builtin_amdgcn_sched_barrier(0);  // every load of both rows ahead of the math
+    finish(row, in0);
+    finish(row + gy, in1);
+  }
+  if (row < rows) {
+    ShufIn<T> in0;
+    load(row, in0);
+    finish(row, in0);
   }
 }
 
@@ -693,15 +738,29 @@ extern "C" int dv_shuffle(int dtype, int mode, const void* src, int lds, void* d
              "channels / strides must be multiples of 16 bytes");
   if ((long long)nf * H * W * C == 0) return DV_OK;
   DV_REQUIRE((long long)W * (C / VEC) < (1ll << 31) && (long long)nf * H < (1ll << 31), "shape too large");
+  // (a grid of fewer rows -- several row pairs per workgroup -- measured equal:
+  // profiles/r05ag_shuffle_ab.txt)
   const dim3 grid((unsigned)((W * (C / VEC) + 255) / 256), (unsigned)std::min(nf * H, 65535));
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == DV_F32) {
-    if (mode == 0) shuffle_kernel<float, 0><<<grid, 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, (const float*)r0, ldr0, (const float*)r1, ldr1, nf, H, W, C, act);
-    else shuffle_kernel<float, 1><<<grid, 256, 0, st>>>((const float*)src, lds, (float*)dst, ldd, (const float*)z, ldz, (const float*)r0, ldr0, (const float*)r1, ldr1, nf, H, W, C, act);
-  } else {
-    if (mode == 0) shuffle_kernel<bf16, 0><<<grid, 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, (const bf16*)r0, ldr0, (const bf16*)r1, ldr1, nf, H, W, C, act);
-    else shuffle_kernel<bf16, 1><<<grid, 256, 0, st>>>((const bf16*)src, lds, (bf16*)dst, ldd, (const bf16*)z, ldz, (const bf16*)r0, ldr0, (const bf16*)r1, ldr1, nf, H, W, C, act);
+  const int nx = mode == 0 ? (z ? 1 : 0) : (r1 ? 2 : r0 ? 1 : 0);
+#define DV_SH(TT, M, NX) shuffle_kernel<TT, M, NX><<<grid, 256, 0, st>>>((const TT*)src, lds, (TT*)dst, ldd, \
+    (const TT*)z, ldz, (const TT*)r0, ldr0, (const TT*)r1, ldr1, nf, H, W, C, act)
+#define DV_SH_T(TT)                          \
+  if (mode == 0) {                           \
+    if (nx) DV_SH(TT, 0, 1);                 \
+    else DV_SH(TT, 0, 0);                    \
+  } else {                                   \
+    if (nx == 2) DV_SH(TT, 1, 2);            \
+    else if (nx == 1) DV_SH(TT, 1, 1);       \
+    else DV_SH(TT, 1, 0);                    \
   }
+  if (dtype == DV_F32) {
+    DV_SH_T(float)
+  } else {
+    DV_SH_T(bf16)
+  }
+#undef DV_SH_T
+#undef DV_SH
   return check_launch("shuffle");
 }
 

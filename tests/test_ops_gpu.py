@@ -182,11 +182,14 @@ def test_mqa(dtype, tol, N, qmag):
 
 
 @pytest.mark.parametrize("dtype,tol", DTYPES)
-def test_shuffles(dtype, tol):
+@pytest.mark.parametrize("nf,H,W,C", [(3, 4, 6, 16), (64, 32, 32, 64), (31, 5, 48, 40), (1, 70001, 1, 8)])
+def test_shuffles(dtype, tol, nf, H, W, C):
+    """Space-to-depth and SiLU + pixel shuffle (forward and backward): Cfg2's 64x64 -> 32x32
+    level, a ragged one, and more low-res rows than the grid's 65,535 (row pairs per trip
+    plus lone rows)."""
     from dalle2_video import ops
 
     g = torch.Generator().manual_seed(13)
-    nf, H, W, C = 3, 4, 6, 16
     x = torch.randn(nf, 2 * H, 2 * W, C, generator=g)
     xr = _leaf(x.to(dtype).float())
     # reference: Downsample3D's rearrange 'b c t (h s1) (w s2) -> b (c s1 s2) t h w' per frame
