@@ -380,29 +380,60 @@ __device__ __forceinline__ int lg_entry(const LinGroupArgs& a, int blk) {
   return e;
 }
 
+// act_in(x) into LDS: every thread's (at most 16) loads issued together from
+// clamped indices (a run-time trip count left one load in flight per thread)
+__device__ __forceinline__ void lg_stage_x(const LinGroupArgs& a, float* xs) {
+  const int nx = a.B * a.K, tid = threadIdx.x;
+  float v[LG_MAXB * LG_MAXK / 256];
+#pragma unroll
+  for (int u = 0; u < LG_MAXB * LG_MAXK / 256; ++u) v[u] = a.x[min(tid + 256 * u, nx - 1)];
+#pragma unroll
+  for (int u = 0; u < LG_MAXB * LG_MAXK / 256; ++u)
+    if (tid + 256 * u < nx) xs[tid + 256 * u] = act_in_f(v[u], a.act_in);
+}
+
 __global__ __launch_bounds__(256) void linear_group_fwd_kernel(LinGroupArgs a) {
   __shared__ __attribute__((aligned(16))) float xs[LG_MAXB * LG_MAXK];
   const int tid = threadIdx.x;
-  for (int i = tid; i < a.B * a.K; i += 256) xs[i] = act_in_f(a.x[i], a.act_in);
-  __syncthreads();
   const int e = lg_entry(a, blockIdx.x);
   const DvLinEntry E = a.e[e];
   const int lane = tid & 63, q = lane & 3;
   const int n = (blockIdx.x - a.blk0[e]) * LG_ROWS + (tid >> 6) * 16 + (lane >> 2);
+  // the lane's W pieces (k = 4q + 16u), 8 at a time in flight; rows past the
+  // entry and k past K read clamped addresses and are masked (the loop waited
+  // for each load before the next with one load per trip under a branch)
+  const float* wr = E.w + (long long)min(n, E.n - 1) * a.K;
+  constexpr int U = 8;
+  f32x4 w[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) w[u] = *(const f32x4*)(wr + min(q * 4 + 16 * u, a.K - 4));
+  lg_stage_x(a, xs);
+  __syncthreads();
   float acc[LG_MAXB];
 #pragma unroll
   for (int b = 0; b < LG_MAXB; ++b) acc[b] = 0.f;
-  if (n < E.n) {
-    const float* wr = E.w + (long long)n * a.K;
-    for (int k = q * 4; k < a.K; k += 16) {
-      const f32x4 w = *(const f32x4*)(wr + k);
+  for (int k0 = 0; k0 < a.K; k0 += 16 * U) {
+    f32x4 wn[U];
+    if (k0 + 16 * U < a.K) {
 #pragma unroll
-      for (int b = 0; b < LG_MAXB; ++b) {
-        if (b < a.B) {
-          const f32x4 xv = *(const f32x4*)(xs + b * a.K + k);
-          acc[b] += w[0] * xv[0] + w[1] * xv[1] + w[2] * xv[2] + w[3] * xv[3];
+      for (int u = 0; u < U; ++u) wn[u] = *(const f32x4*)(wr + min(k0 + 16 * U + q * 4 + 16 * u, a.K - 4));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + q * 4 + 16 * u;
+      if (k < a.K) {
+#pragma unroll
+        for (int b = 0; b < LG_MAXB; ++b) {
+          if (b < a.B) {
+            const f32x4 xv = *(const f32x4*)(xs + b * a.K + k);
+            acc[b] += w[u][0] * xv[0] + w[u][1] * xv[1] + w[u][2] * xv[2] + w[u][3] * xv[3];
+          }
         }
       }
+    }
+    if (k0 + 16 * U < a.K) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) w[u] = wn[u];
     }
   }
 #pragma unroll
@@ -423,14 +454,23 @@ __global__ __launch_bounds__(256) void linear_group_bwd_kernel(LinGroupArgs a) {
   __shared__ float gs[LG_MAXB][LG_ROWS];
   __shared__ int last;
   const int tid = threadIdx.x;
-  for (int i = tid; i < a.B * a.K; i += 256) xs[i] = act_in_f(a.x[i], a.act_in);
+  lg_stage_x(a, xs);
   const int e = lg_entry(a, blockIdx.x);
   const DvLinEntry E = a.e[e];
   const int row0 = (blockIdx.x - a.blk0[e]) * LG_ROWS;
   const int rows = min(LG_ROWS, E.n - row0);
-  for (int i = tid; i < LG_MAXB * LG_ROWS; i += 256) {
-    const int b = i / LG_ROWS, r = i % LG_ROWS;
-    gs[b][r] = (b < a.B && r < rows) ? E.y[(long long)b * E.n + row0 + r] : 0.f;
+  {
+    float g[LG_MAXB * LG_ROWS / 256];
+#pragma unroll
+    for (int u = 0; u < LG_MAXB * LG_ROWS / 256; ++u) {
+      const int i = tid + 256 * u, b = i / LG_ROWS, r = i % LG_ROWS;
+      g[u] = E.y[(long long)min(b, a.B - 1) * E.n + row0 + min(r, rows - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < LG_MAXB * LG_ROWS / 256; ++u) {
+      const int i = tid + 256 * u, b = i / LG_ROWS, r = i % LG_ROWS;
+      gs[b][r] = (b < a.B && r < rows) ? g[u] : 0.f;
+    }
   }
   __syncthreads();
   // dW / db rows: 4 lanes per row
@@ -439,17 +479,29 @@ __global__ __launch_bounds__(256) void linear_group_bwd_kernel(LinGroupArgs a) {
     if (r < rows) {
       const int n = row0 + r;
       float* dwr = E.dw + (long long)n * a.K;
-      for (int k = q * 4; k < a.K; k += 16) {
-        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+      constexpr int U = 8;  // pieces k = k0 + 4q + 16u; the accumulated dW read U at a time
+      for (int k0 = 0; k0 < a.K; k0 += 16 * U) {
+        f32x4 prev[U];
+        if (E.accumulate_w) {
 #pragma unroll
-        for (int b = 0; b < LG_MAXB; ++b) {
-          if (b < a.B) {
-            const f32x4 xv = *(const f32x4*)(xs + b * a.K + k);
-            s += gs[b][r] * xv;
+          for (int u = 0; u < U; ++u) prev[u] = *(const f32x4*)(dwr + min(k0 + q * 4 + 16 * u, a.K - 4));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int k = k0 + q * 4 + 16 * u;
+          if (k < a.K) {
+            f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int b = 0; b < LG_MAXB; ++b) {
+              if (b < a.B) {
+                const f32x4 xv = *(const f32x4*)(xs + b * a.K + k);
+                s += gs[b][r] * xv;
+              }
+            }
+            if (E.accumulate_w) s += prev[u];
+            *(f32x4*)(dwr + k) = s;
           }
         }
-        if (E.accumulate_w) s += *(const f32x4*)(dwr + k);
-        *(f32x4*)(dwr + k) = s;
       }
       if (E.db && q == 0) {
         float sb = 0.f;
@@ -465,11 +517,15 @@ __global__ __launch_bounds__(256) void linear_group_bwd_kernel(LinGroupArgs a) {
 #pragma unroll
       for (int b = 0; b < LG_MAXB; ++b) acc[b] = 0.f;
       const float* wp = E.w + (long long)row0 * a.K + k;
-#pragma unroll 8
-      for (int r = 0; r < rows; ++r) {
-        const float w = wp[(long long)r * a.K];
+      // 8 rows per trip, their loads together (clamped rows: gs is zero past `rows`)
+      for (int r0 = 0; r0 < rows; r0 += 8) {
+        float w[8];
 #pragma unroll
-        for (int b = 0; b < LG_MAXB; ++b) acc[b] += gs[b][r] * w;  // rows b >= B are zero
+        for (int j = 0; j < 8; ++j) w[j] = wp[(long long)min(r0 + j, rows - 1) * a.K];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int b = 0; b < LG_MAXB; ++b) acc[b] += gs[b][r0 + j] * w[j];  // rows b >= B are zero
       }
       for (int b = 0; b < a.B; ++b) atomicAdd(a.ws + b * a.K + k, acc[b]);
     }
@@ -479,11 +535,24 @@ __global__ __launch_bounds__(256) void linear_group_bwd_kernel(LinGroupArgs a) {
     if (tid == 0) last = atomicAdd((unsigned*)(a.ws + a.B * a.K), 1u) == gridDim.x - 1;
     __syncthreads();
     if (!last) return;
-    for (int i = tid; i < a.B * a.K; i += 256) {
-      const float v = __hip_atomic_load(a.ws + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      a.ws[i] = 0.f;
-      const float d = v * act_in_d(a.x[i], a.act_in);
-      a.dx[i] = a.acc_dx ? a.dx[i] + d : d;
+    // the last workgroup's pass is the launch's tail: every load of it in one batch
+    constexpr int UF = LG_MAXB * LG_MAXK / 256;
+    const int nx = a.B * a.K;
+    float v[UF], xv[UF], dv[UF];
+#pragma unroll
+    for (int u = 0; u < UF; ++u) {
+      const int i = min(tid + 256 * u, nx - 1);
+      v[u] = __hip_atomic_load(a.ws + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      xv[u] = a.x[i];
+      dv[u] = a.acc_dx ? a.dx[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UF; ++u) {
+      const int i = tid + 256 * u;
+      if (i < nx) {
+        a.ws[i] = 0.f;
+        a.dx[i] = dv[u] + v[u] * act_in_d(xv[u], a.act_in);
+      }
     }
     if (tid == 0) *(unsigned*)(a.ws + a.B * a.K) = 0u;
   }

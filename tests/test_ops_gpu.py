@@ -276,7 +276,8 @@ def test_linear_small():
 
 
 @pytest.mark.parametrize("act_in,ns,K", [(1, (128, 1024, 70, 512), 256), (0, (1024,) * 3, 64),
-                                         (1, tuple(64 + 8 * i for i in range(50)), 32)])
+                                         (1, tuple(64 + 8 * i for i in range(50)), 32),
+                                         (0, (100, 33), 512), (1, (40, 130), 36), (0, (65,), 4)])
 def test_linear_group(act_in, ns, K):
     """Grouped small linears (time MLPs / to_kv): every entry's output and the
     dx / dW / db gradients vs per-layer fp32 torch; 50 entries span 2 launches."""
