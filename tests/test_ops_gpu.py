@@ -120,16 +120,17 @@ def _ref_cross_attention(x_tok, ctx, g1, null_kv, wq, wkv, wo, g2, eps):
 
 
 @pytest.mark.parametrize("dtype,tol", DTYPES)
-@pytest.mark.parametrize("C,T,H", [(64, 2, 8), (256, 2, 8), (16, 2, 4), (8, 2, 2), (48, 3, 3),
-                                   (512, 2, 8), (192, 2, 8), (128, 4, 16), (32, 2, 8),
-                                   (128, 16, 32)])  # C >= 128: channel-split waves below 1024 token tiles
-def test_cross_attention(dtype, tol, C, T, H):
+@pytest.mark.parametrize("C,T,H,nb", [(64, 2, 8, 2), (256, 2, 8, 2), (16, 2, 4, 2), (8, 2, 2, 2), (48, 3, 3, 2),
+                                      (512, 2, 8, 2), (192, 2, 8, 2), (128, 4, 16, 2), (32, 2, 8, 2),
+                                      (128, 16, 32, 2),  # C >= 128: channel-split waves below 1024 token tiles
+                                      (64, 2, 8, 3), (48, 3, 3, 4)])  # clips (<= 4: to_kv's 8 rows)
+def test_cross_attention(dtype, tol, C, T, H, nb):
     # (16,2,4), (8,2,2), (48,3,3): channel counts below / not a multiple of one
     # 32-channel MFMA tile and tokens per clip (T*H*W) not a multiple of 32
     from dalle2_video import ops
 
     g = torch.Generator().manual_seed(7)
-    nb, W = 2, H
+    W = H
     x = torch.randn(nb * T, H, W, C, generator=g)
     ctx = torch.randn(nb, 2, 64, generator=g)
     g1 = 1 + 0.1 * torch.randn(C, generator=g)
