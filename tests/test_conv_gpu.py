@@ -189,21 +189,24 @@ def test_paired_repack_matches_single_packs():
     both images); every (forward, dgrad) mode combination, beside a weight the
     pairing rejects (cout % 64 != 0), writes the same bytes as single packs."""
     from dalle2_video import ops
-    cases = [((64, 64, 3), 2, 3), ((512, 768, 3), 2, 3), ((128, 48, 3), 0, 1), ((64, 16, 3), 0, 3),
-             ((192, 64, 3), 2, 1), ((40, 24, 3), 0, 1)]
+    # (the last pair: a weight 4 B past a 16-B boundary, a view into a flat buffer --
+    # the tile loads fall back from 16-B to dword pieces)
+    cases = [((64, 64, 3), 2, 3, 0), ((512, 768, 3), 2, 3, 0), ((128, 48, 3), 0, 1, 0), ((64, 16, 3), 0, 3, 0),
+             ((192, 64, 3), 2, 1, 0), ((40, 24, 3), 0, 1, 0), ((128, 32, 3), 2, 3, 1)]
     cache = ops.PackCache()
     cache.enabled = True
     g = torch.Generator(device="cuda").manual_seed(5)
     imgs = []
-    for (co, ci, k), mf, md in cases:
-        w = torch.randn(co, ci, 1, k, k, device="cuda", generator=g)
+    for (co, ci, k), mf, md, off in cases:
+        flat = torch.randn(off + co * ci * k * k, device="cuda", generator=g)
+        w = flat[off:].view(co, ci, 1, k, k)
         for mode in (mf, md):
             pad = ci if mode % 2 == 0 else co
             out, stale = cache.lookup(w, w, torch.bfloat16, co, ci, k, pad, mode)
             assert stale
             imgs.append((w, pad, mode, out))
     pairs, rest = cache._pair(list(cache.entries.values()))
-    assert len(pairs) == 5 and len(rest) == 2
+    assert len(pairs) == 6 and len(rest) == 2
     for w, _, _, _ in imgs:
         w.copy_(torch.randn(w.shape, device="cuda", generator=g))
     cache.refresh()
