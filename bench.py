@@ -282,7 +282,8 @@ def sampling_leg(args, device):
         step = (ts[1] - ts[0]) / (T5B - T5A)
         return step, ts[0] + (1000 - T5A) * step, ts
 
-    def timed_forward():
+    def timed_forward(fp8_attention=False):
+        u.fp8_attention = fp8_attention
         ops.TIMER = ops.KernelTimer()
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16), ops.private_pack_cache():
             xin = torch.randn(2, 3, 32, 128, 128, device=device)
@@ -292,6 +293,7 @@ def sampling_leg(args, device):
             u(xin, tin)
         summ = ops.TIMER.summary()
         ops.TIMER = None
+        u.fp8_attention = False
         return summ
 
     step16, est16, ts16 = loop_rate()
@@ -313,10 +315,13 @@ def sampling_leg(args, device):
     }
     log(f"config5 bf16: {1 / step16:.2f} steps/s")
     # the same loops with the MX-fp8 convs (Unet3D.fp8: e4m3 operands with a
-    # power-of-two scale per 32 channels on v_mfma_scale_f32_32x32x64_f8f6f4)
+    # power-of-two scale per 32 channels on v_mfma_scale_f32_32x32x64_f8f6f4);
+    # the mid attention stays on the bf16 bounded-score kernel (the fp8-PV
+    # kernel measured slower: its opt-in A/B is `mid_attention_fp8` below)
     u.fp8 = True
     step8, est8, ts8 = loop_rate()
     summ8 = timed_forward()
+    summ8a = timed_forward(fp8_attention=True)
     u.fp8 = False
     mx = {k: v for k, v in summ8.items() if k.startswith("conv_fwd_mx8")}
     kname, kd = max(mx.items(), key=lambda kv: kv[1]["ms"])
@@ -324,7 +329,7 @@ def sampling_leg(args, device):
     # the mid attention with PV in MX-fp8 (dv_mqa_fwd_fp8) against the bf16
     # streamed kernel of the bf16 leg, same process / box; half its FLOPs (QK^T)
     # stay bf16, so the peak is the harmonic blend of the two MFMA peaks
-    att8 = summ8.get("attn:mqa_fwd8")
+    att8 = summ8a.get("attn:mqa_fwd8")
     mid8 = None
     if att8 is not None:
         a8_us = att8["ms"] / att8["count"] * 1e3
@@ -340,7 +345,8 @@ def sampling_leg(args, device):
                                      "blend of the dense bf16 and fp8 peaks (half the FLOPs each)"}}
     out["config5_fp8"] = {
         "config": "BASELINE config 5: unet1 sampling, 32x128x128 clip, bs=2, every 3x3 conv with cin, cout % 64 == 0 "
-                  "in MX-fp8 (e4m3 + e8m0 per 32 channels) and the mid attention's PV in MX-fp8; "
+                  "in MX-fp8 (e4m3 + e8m0 per 32 channels), the mid attention bf16 (its fp8-PV form is "
+                  "an opt-in A/B: mid_attention_fp8); "
                   f"per-step rate from {T5A}- and {T5B}-step DDPM loops",
         "value": round(1 / step8, 2), "unit": "denoise-steps/s", "speedup_vs_bf16": round(step16 / step8, 3),
         "est_1000_step_s": round(est8, 1), "loops_s": [round(t, 3) for t in ts8],
@@ -350,7 +356,7 @@ def sampling_leg(args, device):
                      "avg_launch_us": round(kd["ms"] / kd["count"] * 1e3, 2),
                      "note": "dominant MX-fp8 conv kernel, HIP events per launch; peak = dense MX-fp8 MFMA"},
         "kernels_ms_per_step": {k: round(v["ms"], 3) for k, v in sorted(mx.items(), key=lambda kv: -kv[1]["ms"])},
-        "mid_attention_fp8": mid8,
+        "mid_attention_fp8": mid8,  # Unet3D.fp8_attention (opt-in, not in `value`)
     }
     log(f"config5 fp8: {1 / step8:.2f} steps/s")
     del decs, u

@@ -1812,6 +1812,12 @@ struct FsGeom {
   static constexpr int WOFF = (LATE ? 2 * SEG + 2 : 3 * SEG + 2) * ROWB;
   static constexpr int LDS = R * ROWB > WOFF + 64 * FS_WROW ? R * ROWB : WOFF + 64 * FS_WROW;
   static_assert(LDS <= 160 * 1024, "stripe ring exceeds the LDS");
+  // the stage loop issues a wave's pieces of stage st+3 at k-steps k % 7 == 3
+  // (k < 36: at most 5 of them), and the hand-counted waits assume exactly NPW
+  // pieces per stage; the largest vmcnt immediate (two residuals: 2*8 + 12 +
+  // 2*NPW) must fit the 6-bit field
+  static_assert(NPW <= 5, "stripe stage pieces exceed the k-step issue slots");
+  static_assert(2 * 8 + 12 + 2 * NPW <= 63, "stripe vmcnt immediate out of range");
 };
 // immediate offset of k-step k (tap k / 4 = 3 dy + dx, 16 channels at
 // (k % 4) * 16) from the lane's tap row dy base

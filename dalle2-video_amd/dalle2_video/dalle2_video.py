@@ -657,6 +657,9 @@ class Unet3D(nn.Module):
         # ops.mx8_convs); training always stays bf16 / f32.  DV_FP8=1 sets it.
         import os
         self.fp8 = os.environ.get("DV_FP8", "0") == "1"
+        # also the mid attention's PV in MX-fp8 (ops.mx8_convs(attention=True));
+        # off: measured slower than the bf16 kernel on MI355X
+        self.fp8_attention = False
 
     # dalle2_video.py:652-681 — `cond_on_image_embeds` is swallowed by **kwargs
     # so the rebuilt unet keeps cond_on_video_embeds=False.
@@ -744,7 +747,7 @@ class Unet3D(nn.Module):
         """Core denoiser on channels-last frames x (batch*T, H, W, C8); returns
         channels-last (batch*T, H, W, channels_out)."""
         if getattr(self, "fp8", False) and not torch.is_grad_enabled():
-            with ops.mx8_convs():
+            with ops.mx8_convs(attention=getattr(self, "fp8_attention", False)):
                 return self._forward_cl(x, time, batch=batch, lowres_cl=lowres_cl,
                                         video_cond_drop_prob=video_cond_drop_prob,
                                         text_cond_drop_prob=text_cond_drop_prob)

@@ -8,7 +8,6 @@ is no torch-compute fallback.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -22,12 +21,15 @@ class KernelTimer:
 
     def __init__(self):
         self.records = []  # (name, shape, flops, bytes, start_event, end_event)
-        self.fns = {}      # name -> the launch closures, in order (replay_ms)
+        # name -> the most recent launch closures (replay_ms needs one step's):
+        # bounded, since each closure keeps its tensors alive
+        self.fns = {}
 
     # a short device-side spin before each timed launch keeps the GPU behind the
     # host, so the start event, the kernel and the end event run back to back and
     # the elapsed time is the kernel's own (not host launch gaps)
     SPIN_CYCLES = 400_000
+    KEEP_FNS = 128  # launch closures kept per kernel name (>= one step's launches)
 
     def run(self, name, flops, nbytes, fn, shape=None):
         s = torch.cuda.Event(enable_timing=True)
@@ -37,15 +39,24 @@ class KernelTimer:
         fn()
         e.record()
         self.records.append((name, shape, flops, nbytes, s, e))
-        self.fns.setdefault(name, []).append(fn)
+        q = self.fns.get(name)
+        if q is None:
+            import collections
+            q = self.fns[name] = collections.deque(maxlen=self.KEEP_FNS)
+        q.append(fn)
 
     def replay_ms(self, name, n_launch, reps=10):
         """Per-launch device time of kernel `name` the way a kernel trace sees
         it: its last `n_launch` launches (one step's) captured back to back in
         a HIP graph with no event brackets between them, replayed `reps`
         times; elapsed / (reps * n_launch).  Includes the ~1.5 us kernel
-        boundaries (MI355X_MICROARCH.md, boundary row): a slight upper bound."""
-        fns = self.fns[name][-n_launch:]
+        boundaries (MI355X_MICROARCH.md, boundary row): a slight upper bound.
+
+        The replayed launches write their real outputs again (a dgrad whose
+        residual is its own output, a wgrad accumulating into a leaf's .grad):
+        the caller's training state is not valid after this call (bench.py
+        uses the trainer for nothing afterwards)."""
+        fns = list(self.fns[name])[-n_launch:]
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -138,19 +149,16 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0, n
     return f"conv_fwd_kernel<{dtype_name},{bm},{bn}>"
 
 
-# A/B switch: the cross-attention token reductions as three launches, not one
-_NO_GEMM_MULTI = os.environ.get("DV_NO_GEMM_MULTI", "0") not in ("", "0")
-_NO_WINDOW = bool(os.environ.get("DV_NO_WINDOW"))  # A/B switch: 3x3 convs on dv_conv_fwd only
-# measured (tools/kbench.py fwd): the window form wins at 8x8 and 16x16, the glds /
-# stripe kernels at 32x32 and 64x64
-_WINDOW_W = tuple(int(v) for v in os.environ.get("DV_WINDOW_W", "8,16").split(",") if v)
+# measured (round 2, per-shape kernel bench): the window form wins at 8x8 and
+# 16x16, the glds / stripe kernels at 32x32 and 64x64
+_WINDOW_W = (8, 16)
 
 
 def window_ok(x0, x1, cin, c0, cout, ld0, ld1, ldy, ldres, ksize, h, w, nf, gn_P=0, ldres2=0):
     """Mirror of fwd_frame_ok (dv_conv.hip): the window-form 3x3 conv (dv_conv_fwd8);
     with the GroupNorm statistics epilogue its clips must be whole 128-pixel tiles."""
     geom = (h == 8 and w == 8 and nf % 2 == 0) or (w in (16, 32, 64) and (h * w) % 128 == 0)
-    return (not _NO_WINDOW and w in _WINDOW_W and x0.dtype == torch.bfloat16 and ksize == 3
+    return (w in _WINDOW_W and x0.dtype == torch.bfloat16 and ksize == 3
             and gn_P % 128 == 0
             and geom and cin % 16 == 0 and c0 % 16 == 0 and cout % 64 == 0
             and not (cin == 64 and c0 == cin and w in (32, 64, 128))  # the resident-weight stripe kernel
@@ -263,8 +271,8 @@ class _WgradDefer:
     CHUNK_FLOATS = 1 << 27  # 512 MB arena chunks (kept for the process: graphs hold their addresses)
     # flush once this many partial bytes are pending (0 = only at the end of
     # the pass): a smaller batch is read back while still in the 256 MB MALL
-    FLUSH_BYTES = int(os.environ.get("DV_DEFER_MB", "0")) << 20
-    # streamed sums (DV_DEFER_STREAM=1): each conv's split-K sum is launched
+    FLUSH_BYTES = 0
+    # streamed sums (STREAM = True; tests/test_trainer_gpu.py): each conv's split-K sum is launched
     # on a side stream right after its wgrad, to overlap the memory-bound sum
     # with the MFMA / LDS-bound convs of the rest of the backward; the side
     # stream is joined when the pass ends (and before any other kernel writes
@@ -272,7 +280,7 @@ class _WgradDefer:
     # (same box, tools/gpu_r03e.sh: 84.7 vs 95.3 steps/s — the side-stream
     # sums take CU slots and HBM from the 1-workgroup-per-CU convs), so the
     # default is one batched sum at the end of the pass.
-    STREAM = os.environ.get("DV_DEFER_STREAM", "0") == "1"
+    STREAM = False
     _sides = {}
 
     def __init__(self):
@@ -479,8 +487,8 @@ class GnStats:
     # replicas: the conv's device-scope atomics serialise per address (they
     # resolve past the XCD L2s), so the statistics spread over as many
     # replicas as the buffer holds (<= 64); the apply sums them from L2
-    MAX_R = int(os.environ.get("DV_GN_STATS_R", "8"))
-    ALL = os.environ.get("DV_GN_STATS_ALL") == "1"  # A/B switch: every conv kernel accumulates
+    MAX_R = 8
+    ALL = False  # every conv kernel accumulates (tests/test_cfg2_gpu.py sets it)
 
     def __init__(self, nb, C, P, device):
         self.cur, self.nxt = _gn_sums(device).take(nb * C * 2)
@@ -624,9 +632,7 @@ class PackCache:
         """(forward, dgrad) entry pairs of the bf16 3x3 weights that
         dv_pack_conv_weight_pairs packs from one read of the weight
         (cout % 64 == 0, cin % 16 == 0, unpadded rows, exactly one image of
-        each kind), and the rest.  DV_PACK_PAIRS=0: no pairs (A/B)."""
-        if os.environ.get("DV_PACK_PAIRS", "1") == "0":
-            return [], ents
+        each kind), and the rest."""
         by_w = {}
         for e in ents:
             by_w.setdefault(e["w"].data_ptr(), []).append(e)
@@ -759,21 +765,34 @@ def _take_skips(skip, like):
 # MX-fp8 3x3 convs for sampling (BASELINE config 5; dv_mx8.hip)
 # ---------------------------------------------------------------------------
 class _Mx8State:
-    active = 0  # > 0 inside mx8_convs()
+    active = 0     # > 0 inside mx8_convs()
+    attention = 0  # > 0 inside mx8_convs(attention=True): the mid attention's PV too
 
 
 class mx8_convs:
     """Context: eligible 3x3 convs run in MX-fp8 (e4m3 operands with a power-
     of-two scale per 32 channels, f32 accumulation, bf16 output) — forward
     only: ignored while autograd records (training stays bf16 / f32).
-    Unet3D.forward_cl enters it when the unet's `fp8` flag is set."""
+    Unet3D.forward_cl enters it when the unet's `fp8` flag is set.
+
+    attention=True also runs the long-sequence mid attention's PV in MX-fp8
+    (dv_mqa_fwd_fp8; the unet's `fp8_attention` flag).  Off by default: on
+    MI355X it measured SLOWER than the bf16 bounded-score kernel at the
+    config-5 shape (499 vs 353 us per call, bench `config5_fp8.mid_attention_fp8`)
+    and its rounding error is ~4e-2 relative vs f32 against <1e-2 for bf16
+    (tests/test_mqa_fp8_gpu.py); inside mx8_convs() the attention stays bf16."""
+
+    def __init__(self, attention=False):
+        self.attention = bool(attention)
 
     def __enter__(self):
         _Mx8State.active += 1
+        _Mx8State.attention += int(self.attention)
         return self
 
     def __exit__(self, *exc):
         _Mx8State.active -= 1
+        _Mx8State.attention -= int(self.attention)
         return False
 
 
@@ -782,11 +801,10 @@ class mx8_convs:
 # at W <= 32 only 9.57 ms, at every width 9.00 ms with the GroupNorm-fused
 # quantisation (9.56 without it: the separate quantisation pass of the wide
 # 64² / 128² activations ate the conv gain), bf16 9.74-9.99 ms.
-# DV_FP8_MAX_W=32 restricts it to the 8² .. 32² stages.
-_MX8_MAX_W = int(os.environ.get("DV_FP8_MAX_W", "128"))
+_MX8_MAX_W = 128
 # the GroupNorm apply writes the fp8 copy of its output (dv_gn_fwd_mx8) so the
-# consuming conv skips its quantisation pass; DV_FP8_FUSE=0 turns it off (A/B)
-_MX8_FUSE = os.environ.get("DV_FP8_FUSE", "1") != "0"
+# consuming conv skips its quantisation pass (tests/test_mx8_gpu.py turns it off)
+_MX8_FUSE = True
 
 
 def _mx8_geom(nf, h, w):
@@ -1089,13 +1107,11 @@ class ConvFn(torch.autograd.Function):
 
 
 # small-channel forward (cin <= 16, cout <= 32: the cascade's 256x256 unet at
-# dim 8) on the direct kernel of dv_xembed.hip; DV_NO_SMALL=1 keeps the
-# implicit GEMM (A/B switch)
-_NO_SMALL = os.environ.get("DV_NO_SMALL", "0") not in ("", "0")
+# dim 8) on the direct kernel of dv_xembed.hip
 
 
 def small_conv_ok(x0, x1, cin, cin_real, cout, ld0, ld1, ldr, ksize, w):
-    if _NO_SMALL or x0.dtype != torch.bfloat16 or not x0.is_cuda:
+    if x0.dtype != torch.bfloat16 or not x0.is_cuda:
         return False
     if not (cin_real <= 16 and cout <= 32 and cout % 8 == 0 and ksize % 2 == 1 and ksize <= 15
             and w % 32 == 0 and ldr % 4 == 0):
@@ -1739,23 +1755,15 @@ class CrossAttnFn(torch.autograd.Function):
         # per-batch token reductions: R = dS'^T X, V' = P^T dO, Q = P'^T dY (three batched
         # GEMMs of one shape, one launch)
         probs = ((dsbuf, x, ldx, wsR), (pbuf, dobuf, C, wsV), (p2buf, dy, lddy, wsQ))
-        if _NO_GEMM_MULTI:
-            for a_, b_, ldb, o_ in probs:
-                _launch(gemm_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldb)),
-                        2.0 * ntok * 32 * C, 0,
-                        lambda a_=a_, b_=b_, ldb=ldb, o_=o_: call(
-                            "dv_gemm_tn_batched", dt(x), ptr(a_), 32, ptr(b_), ldb, ptr(o_), P, nb, 32,
-                            C, stream()))
-        else:
-            pa = (ctypes.c_void_p * 3)(*(a_.data_ptr() for a_, _, _, _ in probs))
-            la = (ctypes.c_int * 3)(32, 32, 32)
-            pb = (ctypes.c_void_p * 3)(*(b_.data_ptr() for _, b_, _, _ in probs))
-            lb = (ctypes.c_int * 3)(*(ldb for _, _, ldb, _ in probs))
-            po = (ctypes.c_void_p * 3)(*(o_.data_ptr() for _, _, _, o_ in probs))
-            _launch(gemm_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldx, C, lddy)),
-                    3 * 2.0 * ntok * 32 * C, 0,
-                    lambda: call("dv_gemm_tn_batched_multi", dt(x), 3, pa, la, pb, lb, po, P, nb, 32, C,
-                                 stream()))
+        pa = (ctypes.c_void_p * 3)(*(a_.data_ptr() for a_, _, _, _ in probs))
+        la = (ctypes.c_int * 3)(32, 32, 32)
+        pb = (ctypes.c_void_p * 3)(*(b_.data_ptr() for _, b_, _, _ in probs))
+        lb = (ctypes.c_int * 3)(*(ldb for _, _, ldb, _ in probs))
+        po = (ctypes.c_void_p * 3)(*(o_.data_ptr() for _, _, _, o_ in probs))
+        _launch(gemm_wgrad_name(_lib.dtype_name(x), ntok, 32, C, max(32, ldx, C, lddy)),
+                3 * 2.0 * ntok * 32 * C, 0,
+                lambda: call("dv_gemm_tn_batched_multi", dt(x), 3, pa, la, pb, lb, po, P, nb, 32, C,
+                             stream()))
         dat = torch.empty(nb, C, 24, dtype=torch.float32, device=dev)
         dvt = torch.empty_like(dat)
         s1, s2 = _grad_out(g1p), _grad_out(g2p)
@@ -1813,10 +1821,10 @@ MQA_BF16_BWD_MAX_NKP = 1280
 
 
 def mqa_fp8_ok(q, NKP, H, ldq, needs_grad):
-    """MX-fp8 PV (dv_mqa_fwd_fp8): inside mx8_convs() (the unet's fp8 flag,
-    BASELINE config 5), forward only, bf16 dense rows, and a clip whose K / V
+    """MX-fp8 PV (dv_mqa_fwd_fp8): inside mx8_convs(attention=True) (the unet's
+    fp8_attention flag, BASELINE config 5), forward only, bf16 dense rows, and a clip whose K / V
     stream through LDS (NKP > 1280: the config-5 8,193 keys)."""
-    return (_Mx8State.active > 0 and not needs_grad and q.dtype == torch.bfloat16 and ldq == H * MQA_DH
+    return (_Mx8State.attention > 0 and not needs_grad and q.dtype == torch.bfloat16 and ldq == H * MQA_DH
             and NKP > MQA_BF16_BWD_MAX_NKP)
 
 

@@ -471,23 +471,45 @@ class _NativeComms:
     error or a missed deadline it aborts the communicators and ends the
     process with exit code 70, so a dead peer does not leave the other ranks
     blocked in a stream wait forever.  Communicators are destroyed at exit
-    (or when their process group is no longer the default one)."""
+    (or when their process group is no longer the default one).
 
-    def __init__(self):
+    Handle lifetime: every use of a handle -- the watchdog's poll and abort,
+    check(), destroy -- happens while holding `lock`, and a destroyed handle
+    leaves `comms` in the same critical section, so the watchdog can never
+    poll a freed communicator.  close() also stops and joins the watchdog
+    before it destroys anything.  `lib` / `exit_fn` are injectable (tests run
+    the supervision logic on the CPU with a stub library)."""
+
+    def __init__(self, lib=None, exit_fn=None, poll_s=1.0, timeout=None):
         self.comms = {}     # (id(group), rank, world) -> (group, handle)
         self.serial = 0     # every rank makes its communicators in the same order
         self.lock = threading.Lock()
         self.busy_since = None
         self.failed = False
         self.thread = None
-        self.timeout = float(os.environ.get("DV_COMM_TIMEOUT", "1800"))
-        atexit.register(self.close)
+        self.stop = threading.Event()
+        self.poll_s = poll_s
+        self._lib = lib
+        self._exit = exit_fn if exit_fn is not None else os._exit
+        self.timeout = float(os.environ.get("DV_COMM_TIMEOUT", "1800")) if timeout is None else timeout
+        if lib is None:
+            atexit.register(self.close)
 
-    def get(self, device):
+    def L(self):
+        return self._lib if self._lib is not None else _lib.lib()
+
+    def _call(self, name, *args):
+        L = self.L()
+        rc = getattr(L, name)(*args)
+        if rc != 0:
+            raise DVError(f"{name} failed ({rc}): {L.dv_last_error().decode(errors='replace')}")
+
+    def get(self, device, group=None, rank=None, world=None, store=None):
         import ctypes
 
-        group = dist.distributed_c10d._get_default_group()
-        rank, world = dist.get_rank(), dist.get_world_size()
+        group = dist.distributed_c10d._get_default_group() if group is None else group
+        rank = dist.get_rank() if rank is None else rank
+        world = dist.get_world_size() if world is None else world
         key = (id(group), rank, world)
         with self.lock:
             ent = self.comms.get(key)
@@ -499,61 +521,73 @@ class _NativeComms:
             self._drop(k, destroy=True)
         self.serial += 1
         name = f"dv_comm/{self.serial}"
-        store = dist.distributed_c10d._get_default_store()
+        store = dist.distributed_c10d._get_default_store() if store is None else store
         buf = ctypes.create_string_buffer(128)
         if rank == 0:
-            call("dv_comm_unique_id", buf)
+            self._call("dv_comm_unique_id", buf)
             store.set(name, buf.raw)
         else:
             ctypes.memmove(buf, store.get(name), 128)
         handle = ctypes.c_void_p()
-        call("dv_comm_init", buf, world, rank, device.index if device.index is not None
-             else torch.cuda.current_device(), ctypes.byref(handle))
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+        self._call("dv_comm_init", buf, world, rank, dev, ctypes.byref(handle))
         with self.lock:
             self.comms[key] = (group, handle)
         if self.thread is None and os.environ.get("DV_COMM_WATCHDOG", "1") != "0":
+            self.stop.clear()
             self.thread = threading.Thread(target=self._watch, name="dv_comm_watchdog", daemon=True)
             self.thread.start()
         return handle
 
     def _drop(self, key, destroy):
+        # destroy under the lock: the watchdog polls only while holding it
         with self.lock:
             ent = self.comms.pop(key, None)
-        if ent is not None:
-            getattr(_lib.lib(), "dv_comm_destroy" if destroy else "dv_comm_abort")(ent[1])
+            if ent is not None:
+                getattr(self.L(), "dv_comm_destroy" if destroy else "dv_comm_abort")(ent[1])
 
     def check(self):
         """Raise DVError if a communicator reports an asynchronous error
         (update() calls this outside any capture)."""
         with self.lock:
-            handles = [h for _, h in self.comms.values()]
-        for h in handles:
-            call("dv_comm_async_error", h)
+            for _, h in self.comms.values():
+                self._call("dv_comm_async_error", h)
 
     def mark(self, busy):
         self.busy_since = time.monotonic() if busy else None
 
     def _watch(self):
-        L = _lib.lib()
-        while True:
-            time.sleep(1.0)
+        L = self.L()
+        while not self.stop.wait(self.poll_s):
             with self.lock:
+                if self.stop.is_set():
+                    return
                 handles = [h for _, h in self.comms.values()]
-            bad = next((h for h in handles if L.dv_comm_async_error(h) != 0), None)
-            since = self.busy_since
-            late = since is not None and time.monotonic() - since > self.timeout
-            if bad is None and not late:
-                continue
-            why = ("RCCL communicator error: " + L.dv_last_error().decode(errors="replace")) if bad is not None else \
-                f"no progress for {self.timeout:.0f} s in a training call with collectives (DV_COMM_TIMEOUT)"
-            sys.stderr.write(f"[dv_comm watchdog] {why}; aborting the communicators and exiting\n")
-            sys.stderr.flush()
-            self.failed = True
-            for h in handles:
-                L.dv_comm_abort(h)
-            os._exit(70)
+                bad = next((h for h in handles if L.dv_comm_async_error(h) != 0), None)
+                since = self.busy_since
+                late = since is not None and time.monotonic() - since > self.timeout
+                if bad is None and not late:
+                    continue
+                why = ("RCCL communicator error: " + L.dv_last_error().decode(errors="replace")) \
+                    if bad is not None else \
+                    f"no progress for {self.timeout:.0f} s in a training call with collectives (DV_COMM_TIMEOUT)"
+                sys.stderr.write(f"[dv_comm watchdog] {why}; aborting the communicators and exiting\n")
+                sys.stderr.flush()
+                self.failed = True
+                for h in handles:
+                    L.dv_comm_abort(h)
+                self.comms.clear()
+            self._exit(70)
+            return
 
     def close(self):
+        """Stop and join the watchdog, then destroy (or, after a failure,
+        abort) every communicator."""
+        self.stop.set()
+        t = self.thread
+        if t is not None and t is not threading.current_thread():
+            t.join(timeout=10 * self.poll_s + 1)
+        self.thread = None
         with self.lock:
             keys = list(self.comms)
         for k in keys:

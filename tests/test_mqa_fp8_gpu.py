@@ -43,7 +43,7 @@ def test_mqa_fp8_pv_matches_reference(N, qmag):
         o16 = ops.mqa(q, kv, null_kv, B, N, H, scale)
         ops.TIMER = ops.KernelTimer()
         try:
-            with ops.mx8_convs():
+            with ops.mx8_convs(attention=True):
                 o8 = ops.mqa(q, kv, null_kv, B, N, H, scale)
             names = set(ops.TIMER.summary())
         finally:
@@ -62,17 +62,18 @@ def test_mqa_fp8_pv_matches_reference(N, qmag):
 
 def test_mqa_fp8_not_taken_with_grad_or_short_clips():
     """Training (autograd) and the whole-clip-in-LDS kernel (NKP <= 1280) stay
-    on the bf16 path inside mx8_convs()."""
+    on the bf16 path inside mx8_convs(attention=True); without attention=True
+    (the default fp8 sampling mode) every clip length stays bf16."""
     from dalle2_video import ops
 
     B, H = 1, 16
-    for N, grad in ((1024, False), (4096, True)):
+    for N, grad, att in ((1024, False, True), (4096, True, True), (4096, False, False)):
         q = torch.randn(B * N, H * 32, device="cuda").bfloat16().requires_grad_(grad)
         kv = torch.randn(B * N, 64, device="cuda").bfloat16()
         null_kv = torch.randn(2, 32, device="cuda")
         ops.TIMER = ops.KernelTimer()
         try:
-            with ops.mx8_convs(), torch.set_grad_enabled(grad):
+            with ops.mx8_convs(attention=att), torch.set_grad_enabled(grad):
                 ops.mqa(q, kv, null_kv, B, N, H, 1.0 / 32)
             names = set(ops.TIMER.summary())
         finally:
