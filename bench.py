@@ -15,6 +15,7 @@ Rank 0 prints ONE JSON line.  Extra objects:
   conv_shapes   the same per (kernel, GEMM shape) — the actionable rows
   attention     mid MQA QK^T/PV fwd+bwd vs the bf16 MFMA peak (north-star target)
   fp32          the same training step in the reference's f32 arithmetic
+  config3       BASELINE config 3's alternating unet1 + unet2 training step (1 GPU)
   sampling      DDPM denoise steps (one Unet3D forward + posterior update,
                 HIP-graph replay) at 16x64x64 bs=4 and bs=1, and the config-4
                 cascade (base 16x64x64 + SR unet2 to 256x256, 250 steps each)
@@ -66,6 +67,7 @@ def parse():
                     help="launch every kernel eagerly instead of replaying the captured HIP graph")
     ap.add_argument("--no-sampling", action="store_true")
     ap.add_argument("--no-fp32", action="store_true")
+    ap.add_argument("--no-config3", action="store_true")
     ap.add_argument("--sample-steps", type=int, default=250,
                     help="DDPM steps of the sampling legs (config 4: 250)")
     return ap.parse_args()
@@ -207,6 +209,96 @@ def fp32_leg(args, device):
             "mfma_frac": round(STEP_TFLOP * sps / PEAK_F32_TFLOPS, 4),
             "peak": PEAK_F32_TFLOPS, "note": "f32 activations and f32 MFMA (v_mfma_f32_32x32x2f32); "
                                              "frac against the dense f32 MFMA peak"}
+
+
+def forward_flops(unet, shape, device, lowres=None, batch=None):
+    """Algorithmic contraction FLOPs of one no-grad Unet3D forward: the sum of
+    the conv / attention FLOPs the ops report to the kernel timer (2*M*N*K per
+    conv at its unpadded shape; QK^T + PV for the mid attention).  The folded
+    cross-attention projections are not counted, so fractions built on it
+    are lower bounds."""
+    from dalle2_video import ops
+    b, c, t, h, w = shape
+    x = torch.randn(*shape, device=device)
+    tt = torch.full((b,), 500, device=device, dtype=torch.long)
+    ops.TIMER = ops.KernelTimer()
+    try:
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16), ops.private_pack_cache():
+            kw = {} if lowres is None else {"lowres_cond_video": torch.rand(b, c, t, h, w, device=device)}
+            unet(x, tt, **kw)
+        torch.cuda.synchronize()
+        return sum(r[2] for r in ops.TIMER.records)
+    finally:
+        ops.TIMER = None
+
+
+def config3_leg(args, device):
+    """BASELINE config 3 on one GPU: the reference's alternating training step
+    (train_decoder.py:127-138): trainer(unet 1) + update(1), then trainer(unet 2)
+    + update(2), on synthetic 224x224 CelebV-Text-shape clips (bs 4 x 16
+    frames) that VideoDecoder.forward resizes to 64^2 / 128^2; unet2 (dim 8,
+    mults 1..16) is low-res conditioned (64^2 -> 128^2, kornia blur with
+    p = 0.5 drawn per call).  Both unets' calls replay captured HIP graphs (one
+    per blur decision for unet2).  N>1 of this config is the driver's scaling
+    run of the same trainer (bench main leg)."""
+    import random
+    from dalle2_video.dalle2_video import Unet3D, VideoDecoder
+    from dalle2_video.trainer import VideoDecoderTrainer
+    from dalle2_video.utils import deterministic_fill_
+
+    random.seed(1234)
+    u1 = Unet3D(64, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8), cond_on_text_encodings=False)
+    u2 = Unet3D(8, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8, 16), cond_on_text_encodings=False)
+    dec = VideoDecoder(unet=(u1, u2), frame_sizes=(64, 128), frame_numbers=(args.frames, args.frames),
+                       timesteps=1000, learned_variance=False)
+    for un in dec.unets:
+        deterministic_fill_(un)
+    dec = dec.to(device)
+    tr = VideoDecoderTrainer(dec, lr=3e-4, wd=1e-2, use_ema=False, amp=True, use_graphs=True)
+    g = torch.Generator(device=device).manual_seed(99)
+    video = torch.rand(args.batch, 3, args.frames, 224, 224, device=device, generator=g)
+    emb = torch.randn(args.batch, 512, device=device, generator=g)
+    t_unet = [0.0, 0.0]
+
+    def pair(timed=False):
+        for un in (1, 2):
+            if timed:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            tr(video_embed=emb, video=video, unet_number=un)
+            tr.update(un)
+            if timed:
+                torch.cuda.synchronize()
+                t_unet[un - 1] += time.perf_counter() - t0
+
+    for _ in range(12):  # every graph (unet1, unet2 x 2 blur decisions) captured
+        pair()
+    torch.cuda.synchronize()
+    n = 20
+    t0 = time.perf_counter()
+    for _ in range(n):
+        pair()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    for _ in range(5):  # per-unet split (synchronised calls)
+        pair(timed=True)
+    n_graphs = len(tr._graphs)
+    fl1 = STEP_TFLOP * 1e12
+    fl2 = 3.0 * forward_flops(dec.unets[1], (args.batch, 3, args.frames, 128, 128), device, lowres=True)
+    rate = n / dt
+    achieved = (fl1 + fl2) * rate / 1e12
+    out = {"config": "BASELINE config 3 (1 GPU): alternating unet1 (64^2) + update(1), unet2 (128^2, low-res "
+                     f"conditioned, blur p=0.5) + update(2); {args.batch}x3x{args.frames}x224x224 synthetic clips, "
+                     "bf16, HIP-graph replay",
+           "value": round(rate, 3), "unit": "alternating steps/s (one unet1 + one unet2 training step each)",
+           "ms_per_pair": round(1e3 / rate, 3), "pairs": n, "graphs_captured": n_graphs,
+           "unet1_ms": round(t_unet[0] / 5 * 1e3, 3), "unet2_ms": round(t_unet[1] / 5 * 1e3, 3),
+           "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                        "flop_per_pair": f"{(fl1 + fl2) / 1e12:.4f}e12 (unet1 {STEP_TFLOP} + unet2 3 x timed "
+                                         f"forward contractions {fl2 / 3e12:.4f})"}}
+    del tr, dec
+    return out
 
 
 def sampling_leg(args, device):
@@ -377,11 +469,22 @@ def sampling_leg(args, device):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     assert vid.shape == (1, 3, args.frames, 256, 256) and torch.isfinite(vid).all()
+    # per-step contraction FLOPs of each stage's forward (bs 1), both stages' loops
+    dec.to(device)
+    fc1 = forward_flops(dec.unets[0], (1, 3, args.frames, args.size, args.size), device)
+    fc2 = forward_flops(dec.unets[1], (1, 3, args.frames, 256, 256), device, lowres=True)
+    casc_tf = T * (fc1 + fc2) / dt / 1e12
     out["cascade"] = {"config": f"BASELINE config 4: base {args.frames}x{args.size}x{args.size} + SR to "
                                 f"{args.frames}x256x256, bs=1, {T}-step DDPM per stage, one unet on the GPU "
                                 "at a time (the reference's sample() default)",
                       "seconds": round(dt, 3), "value": round(2 * T / dt, 2),
-                      "unit": "denoise-steps/s (both stages)"}
+                      "unit": "denoise-steps/s (both stages)",
+                      "roofline": {"bound": "mfma", "achieved": round(casc_tf, 1), "peak": PEAK_BF16_TFLOPS,
+                                   "unit": "TFLOP/s", "frac": round(casc_tf / PEAK_BF16_TFLOPS, 4),
+                                   "flop_per_step": f"base {fc1 / 1e12:.4f}e12, SR {fc2 / 1e12:.4f}e12 (timed "
+                                                    "forward contractions, bs 1)",
+                                   "note": "whole sample() call incl. one-unet-at-a-time host moves and the "
+                                           "per-stage graph captures"}}
     del dec
     return out
 
@@ -543,6 +646,13 @@ def main():
     sampling = None
     if not args.no_sampling and world == 1:
         sampling = sampling_leg(args, device)
+    config3 = None
+    if not args.no_config3 and world == 1:
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        config3 = config3_leg(args, device)
+        log(f"config3: {config3['value']} alternating steps/s")
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -571,7 +681,7 @@ def main():
             # the bulky per-kernel tables first, the headline sub-results LAST:
             # the driver keeps the tail of stdout
             "kernels": kernels, "conv_shapes": conv_shapes[:24] if conv_shapes else None,
-            "fp32": fp32, "sampling": sampling, "attention": attention,
+            "fp32": fp32, "sampling": sampling, "config3": config3, "attention": attention,
         }
         # one write (line and newline together): another rank's stderr merged
         # into the same pipe cannot land inside the line

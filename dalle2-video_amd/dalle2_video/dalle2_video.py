@@ -865,6 +865,9 @@ class LowresVideoConditioner(nn.Module):
         self.normalize_video = normalize_video_fn
         self.unnormalize_video = unnormalize_video_fn
         self.noise_scheduler = None
+        # the trainer's graphed calls draw the blur decision themselves (the
+        # same one random.random() per call) and pin it here for the call
+        self.forced_blur = None
 
     def forward(self, cond_fmap, *, target_frame_size, downsample_frame_size=None,
                 target_frame_number=None, downsample_frame_number=None, should_blur=True,
@@ -872,7 +875,8 @@ class LowresVideoConditioner(nn.Module):
         if self.downsample_first and exists(downsample_frame_size):
             cond_fmap = resize_video_to(cond_fmap, downsample_frame_size,
                                         clamp_range=self.input_video_range)
-        if self.use_blur and should_blur and random.random() < self.blur_prob:
+        if self.use_blur and should_blur and (
+                self.forced_blur if self.forced_blur is not None else random.random() < self.blur_prob):
             sigma = default(blur_sigma, self.blur_sigma)
             ks = default(blur_kernel_size, self.blur_kernel_size)
             if isinstance(sigma, tuple):

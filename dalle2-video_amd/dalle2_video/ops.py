@@ -2125,12 +2125,22 @@ def gaussian_kernel1d(ks, sigma):
     return g / g.sum()
 
 
+_BLUR_TAPS = {}
+
+
 def gaussian_blur(video, ks, sigma):
     """kornia gaussian_blur2d((ks,ks), (sigma,sigma)) per frame, reflect border."""
     require_gpu(video)
     v = video.float().contiguous()
     B, C, T, H, W = v.shape
-    w1 = gaussian_kernel1d(ks, sigma).to(v.device)
+    # device taps cached per (ks, sigma, device): no host-to-device copy once
+    # warm, so a captured training call (the trainer's unet2 graphs) holds none
+    key = (int(ks), float(sigma), str(v.device))
+    w1 = _BLUR_TAPS.get(key)
+    if w1 is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise _lib.DVError("gaussian_blur taps first built inside a captured region")
+        w1 = _BLUR_TAPS[key] = gaussian_kernel1d(ks, sigma).to(v.device)
     y = torch.empty_like(v)
     call("dv_gaussian_blur", ptr(v), ptr(y), B * C * T, H, W, ks, ptr(w1), stream())
     return y

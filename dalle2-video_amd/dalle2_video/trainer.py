@@ -21,6 +21,7 @@ from __future__ import annotations
 import atexit
 import math
 import os
+import random
 import sys
 import threading
 import time
@@ -1001,15 +1002,20 @@ class VideoDecoderTrainer(nn.Module):
 
     def _graphable(self, unet_number, max_batch_size, return_lowres_cond_video):
         from . import ops
-        # host-side randomness (lowres blur choice) or per-launch timing cannot be replayed
+        # per-launch timing cannot be replayed; a low-res conditioner's blur
+        # decision is host-side randomness: it is drawn per call and selects
+        # one of two captured graphs (_forward), which needs a fixed sigma and
+        # kernel size (a tuple range would draw more per call)
+        lc = self.decoder.lowres_conds[unet_number - 1]
+        fixed = lc is None or not (isinstance(lc.blur_sigma, tuple) or isinstance(lc.blur_kernel_size, tuple))
         return (self.use_graphs and self.training and max_batch_size is None
-                and not return_lowres_cond_video and ops.TIMER is None
-                and self.decoder.lowres_conds[unet_number - 1] is None
+                and not return_lowres_cond_video and ops.TIMER is None and fixed
                 and getattr(self, f"optim{unet_number - 1}").flat_grad is not None)
 
-    def _graphed_call(self, unet_number, args, kwargs):
-        """Replay (capturing on first use) forward + backward of one training call."""
-        sig = (unet_number, self.amp,
+    def _graphed_call(self, unet_number, args, kwargs, variant=None):
+        """Replay (capturing on first use) forward + backward of one training
+        call; `variant` (the pinned blur decision) selects the graph."""
+        sig = (unet_number, self.amp, variant,
                tuple((tuple(a.shape), a.dtype) if torch.is_tensor(a) else repr(a) for a in args),
                tuple((k, (tuple(v.shape), v.dtype) if torch.is_tensor(v) else repr(v))
                      for k, v in sorted(kwargs.items())))
@@ -1091,8 +1097,23 @@ class VideoDecoderTrainer(nn.Module):
             # stream: this call's backward accumulates into the same buffer
             ov.wait()
         graphable = self._graphable(unet_number, max_batch_size, return_lowres_cond_video)
+        lc = self.decoder.lowres_conds[unet_number - 1]
+        if graphable and lc is not None:
+            # the conditioner's one host draw per call (LowresVideoConditioner.forward),
+            # made here and pinned for this call: the graph of that decision replays,
+            # and the eager warm-up calls below see the same decision
+            lc.forced_blur = bool(lc.use_blur and random.random() < lc.blur_prob)
+        try:
+            return self._forward_calls(args, kwargs, unet_number, max_batch_size, return_lowres_cond_video,
+                                       graphable, None if lc is None else lc.forced_blur)
+        finally:
+            if lc is not None:
+                lc.forced_blur = None
+
+    def _forward_calls(self, args, kwargs, unet_number, max_batch_size, return_lowres_cond_video,
+                       graphable, variant):
         if graphable:
-            out = self._graphed_call(unet_number, args, kwargs)
+            out = self._graphed_call(unet_number, args, kwargs, variant)
             if out is not None:
                 return out
         total_loss = 0.0
