@@ -932,9 +932,412 @@ void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
 #undef DV_GN_APP2
 }
 
+// --------------------------------------------------------------------------
+// Single-launch GroupNorm (bf16, round 6): reduce and apply in ONE kernel with
+// the workgroup's rows held in registers between the two phases.
+//   grid = nb * k workgroups of GN_CT threads, nb * k <= 256 (one per CU: every
+//   workgroup of the grid is resident at once); workgroup (b, j) owns rows
+//   [j * rpw, (j + 1) * rpw) of clip b, all C channels.
+//   phase 1  load the rows (z; and dy in the backward) into registers, sum the
+//            per-channel statistics (MODE 0: z, z^2; MODE 1: dv, dv * zhat),
+//            add them into replica j % R of `sums` (agent-scope atomics), then
+//            count the workgroup in its clip's arrival counter (release).
+//   wait     one lane polls the counter (acquire) until the clip's k workgroups
+//            have arrived.  Bounded: after GN_SPIN polls the workgroup sums the
+//            whole clip from memory itself (correct, only slower), so a
+//            workgroup that is not resident can never hang the grid.
+//   phase 2  group terms from the clip totals, applied to the rows still in
+//            registers.  Workgroup j == 0 also writes the clip's mean / rstd
+//            (fwd) or FiLM gradients and its dgamma / dbeta share (bwd).
+// HBM traffic per element: fwd read z (+ res) and write y, bwd read z, dy and
+// write dz -- each once (the two-launch form re-reads z, and dy, in its apply),
+// and one launch instead of two.
+// --------------------------------------------------------------------------
+constexpr int GN_CT = 512;      // threads per workgroup
+constexpr int GN_SPIN = 20000;  // counter polls (s_sleep 2 each, ~1 ms) before the fallback
+
+struct GnCoop {
+  GnArgs a;
+  int k;               // workgroups per clip
+  long long rpw;       // rows per workgroup (NV passes of rpp rows)
+  int* cnt;            // [nb] arrival counters, zero on entry (the tail of `sums`)
+  int force_fallback;  // test hook: skip the wait and recompute the clip's sums
+};
+
+template <int MODE, bool SILU>
+__device__ __forceinline__ void coop_accum(const float* z, const float* dy, const Coef2<8>& k2, f2* s1, f2* s2) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f2 zz{z[2 * j], z[2 * j + 1]};
+    if (MODE == 0) {
+      s1[j] += zz;
+      s2[j] += zz * zz;
+    } else {
+      f2 dv = f2{dy[2 * j], dy[2 * j + 1]};
+      if (SILU) dv *= silu_grad2(zz * k2.A[j] + k2.B[j]);
+      s1[j] += dv;
+      s2[j] += dv * (zz * k2.rs[j] + k2.zb[j]);
+    }
+  }
+}
+
+// per-channel totals of this workgroup's threads: fold the lanes holding the
+// same channel vector, then the waves' partials in LDS; thread c < C gets
+// channel c's (sum1, sum2)
+__device__ __forceinline__ void coop_block_sum(f2* s1, f2* s2, int C, int tpr, float* red, float& t1, float& t2) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, cv = (tid % tpr) * 8;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    for (int o = tpr; o < 64; o <<= 1) {
+      s1[j].x += __shfl_xor(s1[j].x, o, 64);
+      s1[j].y += __shfl_xor(s1[j].y, o, 64);
+      s2[j].x += __shfl_xor(s2[j].x, o, 64);
+      s2[j].y += __shfl_xor(s2[j].y, o, 64);
+    }
+  }
+  __syncthreads();  // red may still be read by a previous use
+  if (lane < tpr) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(wv * C + cv + e) * 2] = s1[e / 2][e % 2];
+      red[(wv * C + cv + e) * 2 + 1] = s2[e / 2][e % 2];
+    }
+  }
+  __syncthreads();
+  t1 = t2 = 0.f;
+  if (tid < C) {
+#pragma unroll
+    for (int w = 0; w < GN_CT / 64; ++w) {  // every wave wrote a partial of every channel
+      t1 += red[(w * C + tid) * 2];
+      t2 += red[(w * C + tid) * 2 + 1];
+    }
+  }
+}
+
+// KEEPX: the second stream (dy, or res) stays in registers too; otherwise
+// phase 2 reads it again (an L2 / MALL hit: the largest slabs, whose two
+// streams do not fit the register budget at 16 passes)
+template <int MODE, int NV, bool SILU, bool RES, bool KEEPX>
+__global__ __launch_bounds__(GN_CT) void gn_coop_kernel(GnCoop q) {
+  const GnArgs& a = q.a;
+  __shared__ float red[(GN_CT / 64) * 512 * 2];  // wave partials [wave][C][2]
+  __shared__ float cs[2 * 512];                   // the clip's per-channel totals
+  __shared__ float gt1[64], gt2[64];              // group terms
+  __shared__ int ok_sh;
+  const int tid = threadIdx.x;
+  const int C = a.C, tpr = C / 8, rpp = GN_CT / tpr;
+  const int r0 = tid / tpr, cv = (tid % tpr) * 8;
+  const int b = blockIdx.x % a.nb, j = blockIdx.x / a.nb;
+  const long long beg = (long long)j * q.rpw;
+  const long long end = beg + q.rpw < a.P ? beg + q.rpw : a.P;
+  constexpr bool has_x = MODE == 1 || RES;
+  const int ldx = MODE == 1 ? a.lddy : a.ldres;
+  // rows through raw buffer resources: one 32-bit lane offset per tensor, the
+  // pass stride in the instruction's scalar offset, rows past the workgroup's
+  // end out of range (loads return zeros, stores are dropped)
+  const long long row0 = (long long)b * a.P + beg + r0;
+  const unsigned nvalid = beg + r0 < end ? (unsigned)((end - beg - r0 + rpp - 1) / rpp) : 0u;
+  const __amdgpu_buffer_rsrc_t zrs = dma_rsrc(a.z, (unsigned)((long long)a.nb * a.P * a.ldz * 2));
+  const __amdgpu_buffer_rsrc_t xrs = dma_rsrc(MODE == 1 ? a.dy : (RES ? a.res : a.z),
+                                              (unsigned)((long long)a.nb * a.P * (has_x ? ldx : a.ldz) * 2));
+  const __amdgpu_buffer_rsrc_t ors = dma_rsrc(a.out, (unsigned)((long long)a.nb * a.P * a.ldo * 2));
+  const unsigned zoff = (unsigned)((row0 * a.ldz + cv) * 2), zstr = (unsigned)(rpp * a.ldz * 2);
+  const unsigned xoff = has_x ? (unsigned)((row0 * ldx + cv) * 2) : 0u, xstr = has_x ? (unsigned)(rpp * ldx * 2) : 0u;
+  const unsigned ooff = (unsigned)((row0 * a.ldo + cv) * 2), ostr = (unsigned)(rpp * a.ldo * 2);
+  auto vo = [&](unsigned off, int i) { return (unsigned)i < nvalid ? off : DMA_OOB; };
+
+  // parameters of the thread's 8 channels (and, bwd, its group's forward
+  // statistics): issued before the data rows (loads return in order)
+  const bool has_ss = a.ss != nullptr;
+  const float* scp = has_ss ? a.ss + (long long)b * 2 * C + cv : a.gamma + cv;
+  const float* shp = has_ss ? scp + C : a.gamma + cv;
+  const int grp = cv / (C / a.G);
+  Coef2<8> k2;
+  auto coef = [&](float mu, float rs) {
+    f32x4 gm[2], bt[2], sc[2], sh[2];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      gm[v] = *(const f32x4*)(a.gamma + cv + 4 * v);
+      bt[v] = *(const f32x4*)(a.beta + cv + 4 * v);
+      sc[v] = *(const f32x4*)(scp + 4 * v);
+      sh[v] = *(const f32x4*)(shp + 4 * v);
+    }
+    ChanCoef k[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float g = gm[e / 4][e % 4], bb = bt[e / 4][e % 4];
+      const float c = has_ss ? 1.f + sc[e / 4][e % 4] : 1.f, h = has_ss ? sh[e / 4][e % 4] : 0.f;
+      k[e].A = rs * g * c;
+      k[e].B = (bb - mu * rs * g) * c + h;
+      k[e].rs = rs;
+      k[e].zb = -mu * rs;
+      k[e].K1 = rs * c * g;
+    }
+    k2.set(k);
+  };
+  float mu_f = 0.f, rs_f = 0.f;
+  if (MODE == 1) {
+    mu_f = a.mean[b * a.G + grp];
+    rs_f = a.rstd[b * a.G + grp];
+    coef(mu_f, rs_f);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  u32x4 zr[NV], xr[KEEPX ? NV : 1];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    zr[i] = __builtin_amdgcn_raw_buffer_load_b128(zrs, vo(zoff, i), i * zstr, 0);
+    if (MODE == 1 && KEEPX) xr[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo(xoff, i), i * xstr, 0);
+  }
+  // the next GroupNorm call's sums and counters start at zero
+  if (a.next) gn_zero_next(a);
+
+  // ---- phase 1: this workgroup's statistics (rows out of range read zeros:
+  // they add nothing in the forward; the backward masks them)
+  f2 s1[4], s2[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) s1[jj] = s2[jj] = f2{0.f, 0.f};
+  // without KEEPX the second stream is read in groups of XG rows, each group
+  // fenced off so the scheduler cannot hoist every load (and its registers)
+  constexpr int XG = 4;
+  u32x4 xt[XG];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float z[8], dy[8];
+    Vec<bf16>::to_f(zr[i], z);
+    if (MODE == 1) {
+      if constexpr (!KEEPX) {
+        if (i % XG == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int u = 0; u < XG; ++u)
+            xt[u] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo(xoff, i + u), (i + u) * xstr, 0);
+        }
+      }
+      Vec<bf16>::to_f(KEEPX ? xr[KEEPX ? i : 0] : xt[i % XG], dy);  // zero past the end: dv = 0
+    }
+    coop_accum<MODE, SILU>(z, dy, k2, s1, s2);
+  }
+  float t1, t2;
+  coop_block_sum(s1, s2, C, tpr, red, t1, t2);
+  if (tid < C) {
+    float* rp = a.sums + (long long)(j % a.R) * a.rstride + ((long long)b * C + tid) * 2;
+    atomicAdd(rp, t1);
+    atomicAdd(rp + 1, t2);
+  }
+  // every wave's atomics performed, then the workgroup counts itself in
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_fetch_add(q.cnt + b, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = !q.force_fallback;
+    for (int n = 0; ok && __hip_atomic_load(q.cnt + b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < q.k; ++n) {
+      if (n >= GN_SPIN) ok = 0;
+      else __builtin_amdgcn_s_sleep(2);
+    }
+    ok_sh = ok;
+  }
+  __syncthreads();
+  if (ok_sh) {
+    if (tid < C) {
+      float v1 = 0.f, v2 = 0.f;
+      for (int r = 0; r < a.R; ++r) {
+        float* rp = a.sums + (long long)r * a.rstride + ((long long)b * C + tid) * 2;
+        v1 += __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v2 += __hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      cs[tid] = v1;
+      cs[C + tid] = v2;
+    }
+  } else {
+    // fallback: the whole clip from memory, by this workgroup alone
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) s1[jj] = s2[jj] = f2{0.f, 0.f};
+    const unsigned zc0 = (unsigned)((((long long)b * a.P + r0) * a.ldz + cv) * 2);
+    const unsigned xc0 = has_x ? (unsigned)((((long long)b * a.P + r0) * ldx + cv) * 2) : 0u;
+    for (long long p = r0, i = 0; p < a.P; p += rpp, ++i) {
+      float z[8], dy[8];
+      Vec<bf16>::to_f(__builtin_amdgcn_raw_buffer_load_b128(zrs, zc0, (unsigned)(i * zstr), 0), z);
+      if (MODE == 1) Vec<bf16>::to_f(__builtin_amdgcn_raw_buffer_load_b128(xrs, xc0, (unsigned)(i * xstr), 0), dy);
+      coop_accum<MODE, SILU>(z, dy, k2, s1, s2);
+    }
+    float u1, u2;
+    coop_block_sum(s1, s2, C, tpr, red, u1, u2);
+    if (tid < C) {
+      cs[tid] = u1;
+      cs[C + tid] = u2;
+    }
+  }
+  __syncthreads();
+
+  // ---- group terms (MODE 0: mean, rstd; MODE 1: m1, m2)
+  {
+    const int lane = tid & 63, wave = tid >> 6, cg = C / a.G;
+    for (int g = wave; g < a.G; g += GN_CT / 64) {
+      if (MODE == 0) {
+        double d1 = 0.0, d2 = 0.0;
+        for (int c = g * cg + lane; c < (g + 1) * cg; c += 64) { d1 += cs[c]; d2 += cs[C + c]; }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { d1 += __shfl_xor(d1, o, 64); d2 += __shfl_xor(d2, o, 64); }
+        if (lane == 0) {
+          const double n = (double)a.P * cg;
+          const double m = d1 / n;
+          double var = d2 / n - m * m;
+          if (var < 0) var = 0;
+          gt1[g] = (float)m;
+          gt2[g] = (float)(1.0 / sqrt(var + (double)a.eps));
+        }
+      } else {
+        const float* ssb = has_ss ? a.ss + (long long)b * 2 * C : nullptr;
+        float m1 = 0.f, m2 = 0.f;
+        for (int c = g * cg + lane; c < (g + 1) * cg; c += 64) {
+          const float kk = a.gamma[c] * (ssb ? 1.f + ssb[c] : 1.f);
+          m1 += kk * cs[c];
+          m2 += kk * cs[C + c];
+        }
+        m1 = wave_sum(m1);
+        m2 = wave_sum(m2);
+        if (lane == 0) {
+          const float n = (float)((double)a.P * cg);
+          gt1[g] = m1 / n;
+          gt2[g] = m2 / n;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (j == 0) {
+    if (MODE == 0) {
+      if (tid < a.G) { a.mean[b * a.G + tid] = gt1[tid]; a.rstd[b * a.G + tid] = gt2[tid]; }
+    } else if (tid < C) {
+      const float r1 = cs[tid], r2 = cs[C + tid];
+      const float scc = has_ss ? 1.f + a.ss[(long long)b * 2 * C + tid] : 1.f;
+      const float gmc = a.gamma[tid], btc = a.beta[tid];
+      if (a.dss) {
+        a.dss[(long long)b * 2 * C + tid] = gmc * r2 + btc * r1;  // d scale
+        a.dss[(long long)b * 2 * C + C + tid] = r1;               // d shift
+      }
+      if (a.dgamma) atomicAdd(a.dgamma + tid, scc * r2);  // fresh buffers were zeroed by the host
+      if (a.dbeta) atomicAdd(a.dbeta + tid, scc * r1);
+    }
+  }
+
+  // ---- phase 2: apply to the rows held in registers
+  f2 m1v = f2{0.f, 0.f}, m2v = f2{0.f, 0.f};
+  if (MODE == 0) {
+    coef(gt1[grp], gt2[grp]);
+  } else {
+    m1v = f2{-rs_f * gt1[grp], -rs_f * gt1[grp]};
+    m2v = f2{-rs_f * gt2[grp], -rs_f * gt2[grp]};
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float z[8], o[8];
+    // opaque: hipcc would otherwise keep phase 1's unpacked floats of every
+    // row alive across the wait (8 VGPRs per row instead of 4)
+    asm volatile("" : "+v"(zr[i]));
+    if constexpr (KEEPX && MODE == 1) asm volatile("" : "+v"(xr[KEEPX ? i : 0]));
+    Vec<bf16>::to_f(zr[i], z);
+    if constexpr (has_x && !(KEEPX && MODE == 1)) {
+      if (i % XG == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < XG && u < NV; ++u)
+          xt[u] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo(xoff, i + u), (i + u) * xstr, 0);
+      }
+    }
+    float x[8];
+    Vec<bf16>::to_f(KEEPX && MODE == 1 ? xr[KEEPX ? i : 0] : xt[i % XG], x);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const f2 zz{z[2 * jj], z[2 * jj + 1]};
+      if (MODE == 0) {
+        f2 v = zz * k2.A[jj] + k2.B[jj];
+        if (SILU) v *= sigmoid2(v);
+        if (RES) v += f2{x[2 * jj], x[2 * jj + 1]};
+        o[2 * jj] = v.x;
+        o[2 * jj + 1] = v.y;
+      } else {
+        f2 dv = f2{x[2 * jj], x[2 * jj + 1]};
+        if (SILU) dv *= silu_grad2(zz * k2.A[jj] + k2.B[jj]);
+        const f2 zhat = zz * k2.rs[jj] + k2.zb[jj];
+        const f2 v = dv * k2.K1[jj] + m1v + zhat * m2v;
+        o[2 * jj] = v.x;
+        o[2 * jj + 1] = v.y;
+      }
+    }
+    const bf16x8 ob = bf16x8{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3],
+                             (bf16)o[4], (bf16)o[5], (bf16)o[6], (bf16)o[7]};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ob), ors, vo(ooff, i), i * ostr, 0);
+  }
+}
+
+// 0: automatic, 1: always the two-launch form, 2: single launch with the
+// wait skipped (every workgroup recomputes its clip's sums: the fallback's test)
+int g_gn_path = 0;
+
+// The single-launch plan: bf16, C a power of two in [8, 512], nb <= 256, the
+// rows of a workgroup in NV <= 16 register passes, and a `next` buffer large
+// enough for R replicas of the sums plus nb counters.
+bool gn_coop_plan(const GnArgs& a, GnCoop& q, int& nv) {
+  if (g_gn_path == 1) return false;
+  const int C = a.C;
+  // a thread's 8 channels lie in one group (cg % 8 == 0)
+  if (C < 8 || C > 512 || (C & (C - 1)) || a.G > 64 || (C / a.G) % 8 || a.nb < 1 || a.nb > 256 || !a.next)
+    return false;
+  if (a.ldz % 8 || a.ldo % 8 || (a.dy && a.lddy % 8) || (a.res && a.ldres % 8)) return false;
+  const long long rows = (long long)a.nb * a.P;  // raw-buffer ranges stay below DMA_OOB
+  const int ldmax = std::max({a.ldz, a.ldo, a.dy ? a.lddy : 0, a.res ? a.ldres : 0});
+  if (rows * ldmax * 2 >= (long long)DMA_OOB) return false;
+  const int tpr = C / 8, rpp = GN_CT / tpr;
+  const long long kmax = 256 / a.nb;
+  const long long nvmin = (a.P + kmax * rpp - 1) / (kmax * rpp);
+  if (nvmin > 16) return false;
+  nv = nvmin <= 1 ? 1 : nvmin <= 2 ? 2 : nvmin <= 4 ? 4 : nvmin <= 8 ? 8 : 16;
+  q.rpw = (long long)nv * rpp;
+  q.k = (int)((a.P + q.rpw - 1) / q.rpw);
+  const long long rs = (long long)a.nb * C * 2;
+  long long R = (a.next_n - a.nb) / rs;
+  if (R < 1) return false;
+  q.a = a;
+  q.a.R = (int)(R < 4 ? R : 4);  // 64 workgroups per clip: 16 adds per address
+  q.a.rstride = rs;
+  q.cnt = (int*)(a.sums + a.next_n - a.nb);
+  q.force_fallback = g_gn_path == 2;
+  return true;
+}
+
+// backward: dy stays in registers up to this many passes (both streams fit)
+constexpr int GN_KEEPX_NV = 8;
+
+template <int MODE>
+void gn_coop_launch(const GnCoop& q, int nv, hipStream_t st) {
+  const bool silu = q.a.act == DV_ACT_SILU, res = MODE == 0 && q.a.res != nullptr;
+  dim3 g((unsigned)(q.a.nb * q.k));
+#define DV_GNC3(NVV, S, R) gn_coop_kernel<MODE, NVV, S, R, (MODE == 1 && NVV <= GN_KEEPX_NV)><<<g, GN_CT, 0, st>>>(q)
+#define DV_GNC2(NVV) (silu ? (res ? DV_GNC3(NVV, true, true) : DV_GNC3(NVV, true, false)) \
+                           : (res ? DV_GNC3(NVV, false, true) : DV_GNC3(NVV, false, false)))
+  switch (nv) {
+    case 1: DV_GNC2(1); break;
+    case 2: DV_GNC2(2); break;
+    case 4: DV_GNC2(4); break;
+    case 8: DV_GNC2(8); break;
+    default: DV_GNC2(16); break;
+  }
+#undef DV_GNC2
+#undef DV_GNC3
+}
+
 template <typename T>
 int gn_fwd_t(GnArgs a, int sums_replicas, hipStream_t st) {
   const GnTune& t = gn_tune();
+  if constexpr (sizeof(T) == 2) {
+    GnCoop q{};
+    int nv = 0;
+    if (sums_replicas == 0 && !a.q && gn_coop_plan(a, q, nv)) {  // one launch: reduce + apply
+      gn_coop_launch<0>(q, nv, st);
+      return check_launch("gn_fwd");
+    }
+  }
   if (sums_replicas > 0) a.R = sums_replicas;  // statistics from the conv epilogue
   else gn_reduce_launch<T, 0>(a, t.ur0, t.tr0, st);
   gn_apply_launch<T, 0>(a, t.ua0, t.ta0, st);
@@ -944,6 +1347,18 @@ int gn_fwd_t(GnArgs a, int sums_replicas, hipStream_t st) {
 template <typename T>
 int gn_bwd_t(GnArgs a, hipStream_t st) {
   const GnTune& t = gn_tune();
+  if constexpr (sizeof(T) == 2) {
+    GnCoop q{};
+    int nv = 0;
+    if (gn_coop_plan(a, q, nv)) {  // one launch: reduce + apply, data in registers
+      if (!a.accumulate) {  // the kernel adds every clip's share
+        if (a.dgamma) zero_f32(a.dgamma, a.C, st);
+        if (a.dbeta) zero_f32(a.dbeta, a.C, st);
+      }
+      gn_coop_launch<1>(q, nv, st);
+      return check_launch("gn_bwd");
+    }
+  }
   gn_reduce_launch<T, 1>(a, t.ur1, t.tr1, st);
   gn_apply_launch<T, 1>(a, t.ua1, t.ta1, st);  // U=2 (123 VGPRs, 4 waves/SIMD) measured ahead of U=4
   return check_launch("gn_bwd");
@@ -1202,6 +1617,12 @@ extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int
   if (nb == 0 || P == 0) return DV_OK;
   hipStream_t st = (hipStream_t)stream;
   return dtype == DV_BF16 ? gn_bwd_t<bf16>(a, st) : gn_bwd_t<float>(a, st);
+}
+
+extern "C" int dv_gn_path(int mode) {
+  DV_REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (auto), 1 (two launches) or 2 (single launch, fallback)");
+  g_gn_path = mode;
+  return DV_OK;
 }
 
 // 16-byte vectors per lane of one row (1, 2 or 4)

@@ -59,6 +59,7 @@ _SIGS = {
                   _I, _P],
     "dv_gn_fwd_mx8": [_P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _F, _P, _P, _P, _I, _P, _P, _P, _P, _L, _I, _P, _P, _P],
     "dv_gn_bwd": [_I, _P, _I, _P, _I, _P, _I, _I, _L, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
+    "dv_gn_path": [_I],
     "dv_ln_fwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _P, _F, _P, _P, _P],
     "dv_ln_bwd_ws": [_L, _I, _P],
     "dv_ln_bwd": [_I, _P, _I, _P, _I, _P, _I, _L, _I, _P, _F, _P, _P, _P, _L, _P],

@@ -450,14 +450,16 @@ class _GnSums:
     dv_gn_bwd contract): call i accumulates into buffer i % 2, which is zero on
     entry, and zeroes buffer (i + 1) % 2 for call i + 1."""
 
-    CAP = 1 << 15  # floats per buffer (nb * C * 2 <= 32768)
+    # floats per buffer: up to 8 replicas of nb * C * 2 sums (<= 32768 floats
+    # each) and, for the single-launch GroupNorm, nb arrival counters at the end
+    CAP = 1 << 16
 
     def __init__(self, device):
         self.bufs = torch.zeros(2, self.CAP, dtype=torch.float32, device=device)
         self.i = 0
 
     def take(self, n):
-        if n > self.CAP:
+        if n > self.CAP // 2:
             raise _lib.DVError(f"GroupNorm: nb*C*2 = {n} exceeds the sums buffer ({self.CAP})")
         cur, nxt = self.bufs[self.i % 2], self.bufs[(self.i + 1) % 2]
         self.i += 1

@@ -310,6 +310,16 @@ int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void*
               float* dbeta, float* dss, float* sums, float* next, long long next_n,
               int accumulate, void* stream);
 
+/* GroupNorm path selection (A/B and test hook; process-wide).  0: automatic --
+ * bf16 calls whose clip fits the single-launch form (C a power of two in
+ * [8, 512], nb <= 256, a workgroup's rows in 16 register passes) run reduce
+ * and apply as ONE kernel (per-clip arrival counters in the last nb words of
+ * `sums`, which must then hold next_n floats as `next` does); others the two
+ * launches.  1: always two launches.  2: single launch with the cross-
+ * workgroup wait skipped (each workgroup recomputes its clip's sums: the
+ * bounded-wait fallback, for tests).                                        */
+int dv_gn_path(int mode);
+
 /* ---- row LayerNorm over channels (dalle2-pytorch LayerNorm, gain only, eps
  * 1e-5 fp32; the mid-attention pre/post norms, dalle2_video.py:431, 551,
  * 921-922).  y = (x-mu)*rstd*g (+b) (+res).  One wave per row; C a

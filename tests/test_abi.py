@@ -84,7 +84,11 @@ def test_abi_version_and_error_channel():
             continue
         vals = [None if a is ctypes.c_void_p else a(0) for a in args]
         rc = getattr(L, name)(*vals)
-        assert rc == -1, (name, rc)  # DV_ERR_INVALID, detected on the host
+        if name == "dv_gn_path":  # a process-wide mode switch: 0 (automatic) is valid
+            assert rc == 0 and L.dv_gn_path(7) == -1
+            name = "dv_gn_path"
+        else:
+            assert rc == -1, (name, rc)  # DV_ERR_INVALID, detected on the host
         msg = L.dv_last_error().decode()
         assert msg.startswith(name + ":"), (name, msg)
 

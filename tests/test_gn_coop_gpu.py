@@ -1,0 +1,129 @@
+"""Single-launch GroupNorm (dv_norm.hip gn_coop_kernel, round 6): reduce and
+apply of Block3D's GroupNorm + FiLM + SiLU (+ residual) (reference
+dalle2_video.py:99-133, 183-205) in ONE kernel whose workgroups meet at a
+per-clip arrival counter, the rows held in registers across the wait.
+
+At every Cfg2 GroupNorm shape (bf16, nb 4 x 16 frames), forward and backward:
+  * single launch vs the two-launch path (dv_gn_path(1)) on the same inputs:
+    the same arithmetic in another summation order, so the outputs agree to a
+    bf16 rounding flip: y, dz <= 4e-3 relative; the f32 sums-derived outputs
+    (dgamma, dbeta, d scale/shift, mean, rstd) <= 1e-4
+  * single launch vs torch f32 (F.group_norm on the same bf16 values) within the
+    bf16 tolerance of tests/test_cfg2_gpu.py (2.5e-2)
+  * the bounded wait's fallback (dv_gn_path(2): every workgroup sums its whole
+    clip itself) gives the same results
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+SHAPES = [  # (H, C): every Cfg2 GroupNorm shape
+    (64, 64), (32, 64), (32, 128), (16, 128), (16, 256), (8, 256), (8, 512)]
+
+
+def _inputs(H, C, with_ss, with_res, seed):
+    g = torch.Generator().manual_seed(seed)
+    nb, T = 4, 16
+    z = (torch.randn(nb * T, H, H, C, generator=g) * 2 + 0.5).bfloat16()
+    gamma = 1 + 0.1 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    ss = 0.3 * torch.randn(nb, 2 * C, generator=g) if with_ss else None
+    res = torch.randn(nb * T, H, H, C, generator=g).bfloat16() if with_res else None
+    gy = torch.randn(nb * T, H, H, C, generator=g)
+    return nb, z, gamma, beta, ss, res, gy
+
+
+def _run(path, nb, z, gamma, beta, ss, res, gy):
+    from dalle2_video import _lib, ops
+    _lib.call("dv_gn_path", path)
+    try:
+        zd = z.cuda().requires_grad_()
+        gd, bd = gamma.cuda().requires_grad_(), beta.cuda().requires_grad_()
+        ssd = ss.cuda().requires_grad_() if ss is not None else None
+        y = ops.group_norm_act(zd, gd, bd, nb, 8, 1e-5, scale_shift=ssd,
+                               res=None if res is None else res.cuda())
+        (y.float() * gy.cuda()).sum().backward()
+        torch.cuda.synchronize()
+        out = {"y": y.detach().float(), "dz": zd.grad.float(), "dgamma": gd.grad, "dbeta": bd.grad}
+        if ssd is not None:
+            out["dss"] = ssd.grad
+        return out
+    finally:
+        _lib.call("dv_gn_path", 0)
+
+
+def _reference(nb, z, gamma, beta, ss, res, gy):
+    import torch.nn.functional as F
+    T, H, W, C = z.shape[0] // nb, z.shape[1], z.shape[2], z.shape[3]
+    leaf = lambda t: t.detach().float().clone().requires_grad_()
+    zr, gr, br = leaf(z), leaf(gamma), leaf(beta)
+    ssr = leaf(ss) if ss is not None else None
+    x5 = zr.reshape(nb, T, H, W, C).permute(0, 4, 1, 2, 3)
+    y5 = F.group_norm(x5, 8, gr, br, eps=1e-5)
+    if ssr is not None:
+        y5 = y5 * (ssr[:, :C, None, None, None] + 1) + ssr[:, C:, None, None, None]
+    y = F.silu(y5).permute(0, 2, 3, 4, 1).reshape(nb * T, H, W, C)
+    if res is not None:
+        y = y + res.float()
+    (y * gy).sum().backward()
+    out = {"y": y.detach(), "dz": zr.grad, "dgamma": gr.grad, "dbeta": br.grad}
+    if ssr is not None:
+        out["dss"] = ssr.grad
+    return out
+
+
+@pytest.mark.parametrize("H,C", SHAPES)
+@pytest.mark.parametrize("with_ss,with_res", [(True, False), (False, True)])
+def test_single_launch_groupnorm_matches_two_launch_and_f32(parity_log, H, C, with_ss, with_res):
+    args = _inputs(H, C, with_ss, with_res, seed=H * 1000 + C)
+    one = _run(0, *args)
+    two = _run(1, *args)
+    ref = _reference(*args)
+    errs = {}
+    for k in one:
+        errs[f"{k}_vs_two"] = rel(one[k], two[k])
+        errs[f"{k}_vs_f32"] = rel(one[k], ref[k])
+    parity_log(config=f"gn single launch 4x16x{H}x{H}x{C} ss={with_ss} res={with_res}", **errs)
+    for k in one:
+        tight = 4e-3 if k in ("y", "dz") else 1e-4
+        assert errs[f"{k}_vs_two"] <= tight, (k, errs)
+        assert errs[f"{k}_vs_f32"] <= 2.5e-2, (k, errs)
+
+
+@pytest.mark.parametrize("H,C", [(64, 64), (8, 512)])
+def test_single_launch_fallback_matches(H, C):
+    args = _inputs(H, C, True, False, seed=7)
+    one = _run(0, *args)
+    fb = _run(2, *args)
+    for k in one:
+        tight = 4e-3 if k in ("y", "dz") else 1e-4
+        assert rel(fb[k], one[k]) <= tight, (k, rel(fb[k], one[k]))
+
+
+def test_single_launch_replays_in_a_graph():
+    """Captured and replayed (the trainer's graphs): the arrival counters and
+    sums are re-zeroed call to call through the alternating buffers."""
+    from dalle2_video import ops
+    nb, z, gamma, beta, ss, res, gy = _inputs(16, 256, True, False, seed=3)
+    zd, gd, bd, ssd = z.cuda(), gamma.cuda(), beta.cuda(), ss.cuda()
+    ref = ops.group_norm_act(zd, gd, bd, nb, 8, 1e-5, scale_shift=ssd).float()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            outs = [ops.group_norm_act(zd, gd, bd, nb, 8, 1e-5, scale_shift=ssd) for _ in range(3)]
+            ops.gn_graph_boundary(zd.device)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    for o in outs:
+        assert rel(o.float(), ref) <= 4e-3
