@@ -1124,13 +1124,18 @@ __global__ __launch_bounds__(GN_CT) void gn_coop_kernel(GnCoop q) {
     atomicAdd(rp, t1);
     atomicAdd(rp + 1, t2);
   }
-  // every wave's atomics performed, then the workgroup counts itself in
+  // every wave's atomics performed (acknowledged by the coherent point), then
+  // the workgroup counts itself in.  Deliberately no release / acquire fences:
+  // on gfx950 those write back / invalidate the whole XCD L2 (measured: ~15 us
+  // per launch).  Nothing but atomics crosses workgroups here -- the sums and
+  // the counter are agent-scope atomic RMWs and are read back with agent-scope
+  // atomic loads (sc1), issued only after the counter load returned k.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __hip_atomic_fetch_add(q.cnt + b, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(q.cnt + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = !q.force_fallback;
-    for (int n = 0; ok && __hip_atomic_load(q.cnt + b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < q.k; ++n) {
+    for (int n = 0; ok && __hip_atomic_load(q.cnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < q.k; ++n) {
       if (n >= GN_SPIN) ok = 0;
       else __builtin_amdgcn_s_sleep(2);
     }
@@ -1307,7 +1312,7 @@ bool gn_coop_plan(const GnArgs& a, GnCoop& q, int& nv) {
 }
 
 // backward: dy stays in registers up to this many passes (both streams fit)
-constexpr int GN_KEEPX_NV = 8;
+constexpr int GN_KEEPX_NV = 16;
 
 template <int MODE>
 void gn_coop_launch(const GnCoop& q, int nv, hipStream_t st) {
