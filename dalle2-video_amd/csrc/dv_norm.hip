@@ -9,6 +9,27 @@
 
 using namespace dv;
 
+// Diagnostic build only (make stamp): per-workgroup s_memrealtime stamps of the
+// single-launch GroupNorm's phases (tools/gn_coop_probe.py reads them with
+// dv_debug_stamps_gn).  The product build compiles none of it.
+#ifdef DV_STAMP
+constexpr int GN_NSTAMP = 8;
+__device__ unsigned long long g_gn_stamp[4096 * GN_NSTAMP];
+#define GN_STAMP_AT(i)                                                                   \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                                           \
+      g_gn_stamp[blockIdx.x * GN_NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime();       \
+  } while (0)
+extern "C" int dv_debug_stamps_gn(unsigned long long* host, long long n) {
+  if (n > 4096 * GN_NSTAMP) n = 4096 * GN_NSTAMP;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gn_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#else
+#define GN_STAMP_AT(i) \
+  do {                 \
+  } while (0)
+#endif
+
 namespace {
 
 template <typename T>
@@ -1020,6 +1041,7 @@ __device__ __forceinline__ void coop_block_sum(f2* s1, f2* s2, int C, int tpr, f
 template <int MODE, int NV, bool SILU, bool RES, bool KEEPX>
 __global__ __launch_bounds__(GN_CT) void gn_coop_kernel(GnCoop q) {
   const GnArgs& a = q.a;
+  GN_STAMP_AT(0);
   __shared__ float red[(GN_CT / 64) * 512 * 2];  // wave partials [wave][C][2]
   __shared__ float cs[2 * 512];                   // the clip's per-channel totals
   __shared__ float gt1[64], gt2[64];              // group terms
@@ -1118,6 +1140,7 @@ __global__ __launch_bounds__(GN_CT) void gn_coop_kernel(GnCoop q) {
     coop_accum<MODE, SILU>(z, dy, k2, s1, s2);
   }
   float t1, t2;
+  GN_STAMP_AT(1);
   coop_block_sum(s1, s2, C, tpr, red, t1, t2);
   if (tid < C) {
     float* rp = a.sums + (long long)(j % a.R) * a.rstride + ((long long)b * C + tid) * 2;
@@ -1132,6 +1155,7 @@ __global__ __launch_bounds__(GN_CT) void gn_coop_kernel(GnCoop q) {
   // atomic loads (sc1), issued only after the counter load returned k.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  GN_STAMP_AT(2);
   if (tid == 0) {
     __hip_atomic_fetch_add(q.cnt + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = !q.force_fallback;
@@ -1142,6 +1166,7 @@ __global__ __launch_bounds__(GN_CT) void gn_coop_kernel(GnCoop q) {
     ok_sh = ok;
   }
   __syncthreads();
+  GN_STAMP_AT(3);
   if (ok_sh) {
     if (tid < C) {
       float v1 = 0.f, v2 = 0.f;
@@ -1227,6 +1252,7 @@ __global__ __launch_bounds__(GN_CT) void gn_coop_kernel(GnCoop q) {
   }
 
   // ---- phase 2: apply to the rows held in registers
+  GN_STAMP_AT(4);
   f2 m1v = f2{0.f, 0.f}, m2v = f2{0.f, 0.f};
   if (MODE == 0) {
     coef(gt1[grp], gt2[grp]);
@@ -1274,16 +1300,28 @@ __global__ __launch_bounds__(GN_CT) void gn_coop_kernel(GnCoop q) {
                              (bf16)o[4], (bf16)o[5], (bf16)o[6], (bf16)o[7]};
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ob), ors, vo(ooff, i), i * ostr, 0);
   }
+#ifdef DV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  GN_STAMP_AT(5);
+#endif
 }
 
-// 0: automatic, 1: always the two-launch form, 2: single launch with the
-// wait skipped (every workgroup recomputes its clip's sums: the fallback's test)
+// 0: automatic, 1: always the two-launch form, 2: single launch wherever it
+// applies, with the wait skipped (every workgroup recomputes its clip's sums:
+// the fallback's test), 3: single launch wherever it applies.
+// Automatic = single launch only for the backward at 16 register passes (the
+// 64^2 Cfg2 slabs): there it saves the second read of z and dy (33.0 vs 34.3
+// us); everywhere else the two launches are faster.  The cross-workgroup sum
+// costs ~8-10 us on MI355X -- agent-scope atomics and sc1 loads each take
+// ~2 us to the coherent point and back (phase stamps, tools/gn_coop_probe.py,
+// profiles/r06d_gn_single_launch_ab.txt) -- more than the kernel boundary it
+// removes.
 int g_gn_path = 0;
 
 // The single-launch plan: bf16, C a power of two in [8, 512], nb <= 256, the
 // rows of a workgroup in NV <= 16 register passes, and a `next` buffer large
 // enough for R replicas of the sums plus nb counters.
-bool gn_coop_plan(const GnArgs& a, GnCoop& q, int& nv) {
+bool gn_coop_plan(const GnArgs& a, GnCoop& q, int& nv, bool bwd) {
   if (g_gn_path == 1) return false;
   const int C = a.C;
   // a thread's 8 channels lie in one group (cg % 8 == 0)
@@ -1298,6 +1336,7 @@ bool gn_coop_plan(const GnArgs& a, GnCoop& q, int& nv) {
   const long long nvmin = (a.P + kmax * rpp - 1) / (kmax * rpp);
   if (nvmin > 16) return false;
   nv = nvmin <= 1 ? 1 : nvmin <= 2 ? 2 : nvmin <= 4 ? 4 : nvmin <= 8 ? 8 : 16;
+  if (g_gn_path == 0 && !(bwd && nv == 16)) return false;  // measured: two launches win
   q.rpw = (long long)nv * rpp;
   q.k = (int)((a.P + q.rpw - 1) / q.rpw);
   const long long rs = (long long)a.nb * C * 2;
@@ -1338,7 +1377,7 @@ int gn_fwd_t(GnArgs a, int sums_replicas, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
     GnCoop q{};
     int nv = 0;
-    if (sums_replicas == 0 && !a.q && gn_coop_plan(a, q, nv)) {  // one launch: reduce + apply
+    if (sums_replicas == 0 && !a.q && gn_coop_plan(a, q, nv, false)) {  // one launch: reduce + apply
       gn_coop_launch<0>(q, nv, st);
       return check_launch("gn_fwd");
     }
@@ -1355,7 +1394,7 @@ int gn_bwd_t(GnArgs a, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
     GnCoop q{};
     int nv = 0;
-    if (gn_coop_plan(a, q, nv)) {  // one launch: reduce + apply, data in registers
+    if (gn_coop_plan(a, q, nv, true)) {  // one launch: reduce + apply, data in registers
       if (!a.accumulate) {  // the kernel adds every clip's share
         if (a.dgamma) zero_f32(a.dgamma, a.C, st);
         if (a.dbeta) zero_f32(a.dbeta, a.C, st);
@@ -1625,7 +1664,8 @@ extern "C" int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int
 }
 
 extern "C" int dv_gn_path(int mode) {
-  DV_REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (auto), 1 (two launches) or 2 (single launch, fallback)");
+  DV_REQUIRE(mode >= 0 && mode <= 3,
+             "mode must be 0 (auto), 1 (two launches), 2 (single launch, fallback) or 3 (single launch)");
   g_gn_path = mode;
   return DV_OK;
 }

@@ -310,14 +310,16 @@ int dv_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, void*
               float* dbeta, float* dss, float* sums, float* next, long long next_n,
               int accumulate, void* stream);
 
-/* GroupNorm path selection (A/B and test hook; process-wide).  0: automatic --
- * bf16 calls whose clip fits the single-launch form (C a power of two in
- * [8, 512], nb <= 256, a workgroup's rows in 16 register passes) run reduce
- * and apply as ONE kernel (per-clip arrival counters in the last nb words of
- * `sums`, which must then hold next_n floats as `next` does); others the two
- * launches.  1: always two launches.  2: single launch with the cross-
- * workgroup wait skipped (each workgroup recomputes its clip's sums: the
- * bounded-wait fallback, for tests).                                        */
+/* GroupNorm path selection (A/B and test hook; process-wide).  The single-
+ * launch form runs reduce and apply as ONE kernel (bf16, C a power of two in
+ * [8, 512] with C/G % 8 == 0, nb <= 256, a workgroup's rows in <= 16 register
+ * passes; per-clip arrival counters in the last nb words of `sums`, which
+ * must then hold next_n floats as `next` does).  0: automatic -- the single
+ * launch only for backward calls at 16 passes (measured faster there only),
+ * two launches otherwise.  1: always two launches.  2: single launch wherever
+ * it applies, with the cross-workgroup wait skipped (each workgroup
+ * recomputes its clip's sums: the bounded-wait fallback, for tests).
+ * 3: single launch wherever it applies.                                     */
 int dv_gn_path(int mode);
 
 /* ---- row LayerNorm over channels (dalle2-pytorch LayerNorm, gain only, eps
