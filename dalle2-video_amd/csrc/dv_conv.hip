@@ -101,6 +101,10 @@ struct ConvFwdArgs {
   // window kernel: output-channel groups the 8 XCDs split into (the other
   // factor of 8 splits the pixel tiles); 0: one channel block per XCD
   int xcd_c;
+  // stripe kernel: the weight image holds wcin channels per tap (0: 64) and
+  // this pass reads channels [wc0, wc0 + 64) of each tap -- one source of a
+  // dual-source conv run as two passes (conv_fwd_t)
+  int wcin = 0, wc0 = 0;
 };
 
 // GroupNorm statistics of a wave's tile, register-light: every lane holds
@@ -1890,12 +1894,15 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   }
   {
     char* sW = smem + G::WOFF;
-    const __amdgpu_buffer_rsrc_t wr = dma_rsrc(p.w + (long long)co0 * 576, 64 * 576 * 2);
+    const int wci = p.wcin ? p.wcin : 64;  // image channels per tap (row pitch 9 wci)
+    const __amdgpu_buffer_rsrc_t wr = dma_rsrc(p.w + (long long)co0 * 9 * wci, 64 * 9 * wci * 2);
 #pragma unroll
     for (int i = 0; i < FS_WPIECES / 8 + 1; ++i) {
       const int piece = min(wave + 8 * i, FS_WPIECES - 1);
       const int slot = piece * 64 + lane, row = slot / 73, c = slot - row * 73;
-      dma16(wr, sW + piece * 1024, c < 72 ? (unsigned)((row * 576 + c * 8) * 2) : DMA_OOB);
+      // 16-B slot c of the row's 9 x 64 channels: tap c / 8, channels wc0 + 8 (c % 8)
+      dma16(wr, sW + piece * 1024,
+            c < 72 ? (unsigned)((row * 9 * wci + (c >> 3) * wci + p.wc0 + (c & 7) * 8) * 2) : DMA_OOB);
     }
   }
   // bias of the lane's 16 accumulator channels (8g + 4h + e of the wave's 32),
@@ -1947,13 +1954,22 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   const int px = pt * 32 + r;           // lane's pixel in the stage
   const int orow = px / W;              // its output row in the stage (wave-uniform)
   const int loff = (px % W) * FS_XP + h * 16;
-  // GroupNorm statistics (STATS, compile-time like NRES): each stage's 32 x 16
-  // sums / squares are reduce-scattered over the half-wave (gn_rs_reduce), so
-  // a lane carries ONE running total across stages; it is added when the
-  // stage range crosses into the next clip (128-pixel stages never straddle
-  // one: the host requires gn_P % 128 == 0) and at the end
-  float sacc[32];  // only sacc[0] is live between stages
-  sacc[0] = 0.f;
+  // GroupNorm statistics (STATS, compile-time like NRES): per stage only the
+  // first step of the half-wave reduce-scatter (lanes r, r ^ 16: 16 shuffles
+  // instead of the 31 of gn_rs_reduce) and a lane accumulates the 16 values
+  // it keeps over the stages (16 VGPRs); the remaining four steps run once,
+  // when the stage range crosses into the next clip (128-pixel stages never
+  // straddle one: the host requires gn_P % 128 == 0) and at the end.  (Round 5
+  // reduced every stage fully: ~6 us per 64^2 launch over the plain kernel.)
+  float sacc[32];  // [0, 16) live across stages
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
+  auto rs_tail = [&]() {  // gn_rs_reduce's steps after the first
+    rs_step<32, 8>(sacc, r);
+    rs_step<32, 4>(sacc, r);
+    rs_step<32, 2>(sacc, r);
+    rs_step<32, 1>(sacc, r);
+  };
   constexpr bool stats = STATS;
   auto chan = [&](int k) { return co0 + ch * 32 + 8 * (k / 4) + 4 * h + (k % 4); };
 
@@ -1961,8 +1977,10 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     if constexpr (stats) if (st > 0) {
       const long long c_prev = (long long)(sbeg + st - 1) * 128 / p.gn_P;
       if ((long long)(sbeg + st) * 128 / p.gn_P != c_prev) {
+        rs_tail();
         gn_rs_add<bf16, 32>(p, sacc, c_prev, chan);
-        sacc[0] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
       }
     }
     // the lane's three tap rows dy = 0..2: window rows st SEG + orow + dy
@@ -2047,8 +2065,9 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
       }
     }
     if constexpr (stats) {
-      gn_rs_reduce<32>(sv, r);
-      sacc[0] += sv[0];
+      rs_step<32, 16>(sv, r);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[i] += sv[i];
     }
     if (st == 1) DV_STAMP_AT(5);
     // stage st+1's rows landed.  vmcnt(N) = all but the wave's N youngest
@@ -2088,6 +2107,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     // the clip of the block's last stage (block-uniform); earlier clips were
     // added per wave at the crossing (rare: stage ranges align with clips)
     __shared__ float red[2 * 64];
+    rs_tail();
     if (nst > 0) gn_block_add<bf16, 32>(p, sacc, (long long)(sbeg + nst - 1) * 128 / p.gn_P, chan, red, co0, 64);
   }
 }
@@ -2782,6 +2802,24 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
   set_gn(a, gn_sums, gn_P, gn_R);
   if (a.M == 0 || cout == 0) return DV_OK;
   if constexpr (sizeof(T) == 2) {
+    // a 3x3 conv over a 64 + 64 channel concat (the 64^2 up-path block1 convs,
+    // dalle2_video.py:926-945): two resident-weight stripe passes, one per
+    // source -- pass 2 adds onto pass 1's output in its residual epilogue
+    // (in place: each lane reads its pixel's y before it stores it).  Measured
+    // against the glds implicit GEMM it replaces: DESIGN.md §3.
+    if (x1 && c0 == 64 && cin == 128 && act == DV_ACT_NONE && !gn_sums && !res2 && ld1 % 8 == 0 &&
+        fwd_stripe_ok(a.M, h, wd, 64, false, cout, ks, ld0) && a.M * ld1 * 2 < (long long)DMA_OOB &&
+        (ldy & 3) == 0 && (res == nullptr || (ldres & 3) == 0)) {
+      ConvFwdArgs<T> p1 = a;
+      p1.cin = 64; p1.c0 = 64; p1.x1 = p1.x0; p1.ld1 = p1.ld0; p1.K = ks * ks * 64;
+      p1.wcin = 128; p1.wc0 = 0;
+      const int rc = launch_fwd_stripe(p1, st);
+      if (rc != DV_OK) return rc;
+      ConvFwdArgs<T> p2 = p1;
+      p2.x0 = a.x1; p2.ld0 = a.ld1; p2.x1 = a.x1; p2.ld1 = a.ld1; p2.wc0 = 64;
+      p2.bias = nullptr; p2.res = a.y; p2.ldres = ldy;
+      return launch_fwd_stripe(p2, st);
+    }
     // the stripe kernel flushes statistics per 128-pixel stage: clips must
     // be whole stages
     if (fwd_stripe_ok(a.M, h, wd, cin, x1 != nullptr, cout, ks, ld0) && (ldy & 3) == 0 &&

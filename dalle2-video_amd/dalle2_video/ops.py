@@ -126,6 +126,10 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0, n
             and w in (32, 64, 128) and h % (128 // w) == 0 and m % 128 == 0 and m * maxld < (1 << 31)
             and gn_P % 128 == 0):
         return f"conv_fwd_stripe_kernel<{w}>"
+    if (dtype_name == "bf16" and ks == 3 and cin == 128 and c0 == 64 and cout % 64 == 0 and gn_P == 0
+            and not nres2 and w in (32, 64, 128) and h % (128 // w) == 0 and m % 128 == 0
+            and m * maxld < (1 << 31)):
+        return f"conv_fwd_stripe_kernel<{w}>"  # dual source: two stripe passes (conv_fwd_t)
     if (dtype_name == "bf16" and ks == 3 and cin % 32 == 0 and c0 % 32 == 0 and cout % 64 == 0
             and m % 128 == 0 and m * maxld < (1 << 31) and _stripe_geom_ok(h, w)
             and (w == 8 or (w == 16 and cin * cout <= 256 * 256))):

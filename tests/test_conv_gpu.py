@@ -34,6 +34,9 @@ CASES = [
     (4, 64, 64, 64, 0, 64, 3),      # W=64, forward and dgrad both stripe
     (2, 128, 128, 64, 0, 64, 3),    # W=128 (config 5's 128x128 stage): one-row stages, late stage-2 rows
     (1, 128, 128, 64, 0, 128, 3),   # W=128, 2 cout tiles
+    # dual-source 64 + 64 -> cout 3x3 forward as two stripe passes (64^2 up-path block1 convs)
+    (1, 128, 128, 64, 64, 64, 3),   # W=128
+    (2, 64, 64, 64, 64, 128, 3),    # W=64, 2 cout tiles
     # 8x8-frame forward / dgrad (H = W = 8, 16-channel chunks, two frames per block)
     (4, 8, 8, 48, 16, 64, 3),       # dual source at a 16-channel boundary, dgrad 64 -> 48 + 16
     (6, 8, 8, 128, 0, 192, 3),      # three channel blocks (no XCD regrouping), 8 chunks
