@@ -300,13 +300,18 @@ __global__ __launch_bounds__(512) void xe_fwd_kernel(XeGeom g, const bf16* img, 
 }
 
 // ---------------------------------------------------------------------------
-// weight gradient.  Workgroup = a band of `rows` image rows of one frame;
-// per row: LDS dY row [W][cout + 8] and the kmax input rows around it
-// [kmax][W + kmax + 7][CP] (double-buffered: the next row's global loads are
-// in registers while this row's MFMAs run).  Wave w owns accumulator items
-// [w * per, w * per + per) of the flat (tile, dy, 16-column block) list.
+// weight gradient.  Workgroup = a band of `rows` image rows of one frame,
+// walked RB rows per step: LDS dY rows [RB][W][cout + 8] and the kmax + RB - 1
+// input rows around them [kmax + RB - 1][W + kmax + 7][CP] (double-buffered:
+// the next step's global loads are in registers while this step's MFMAs run).
+// Wave w owns accumulator items [w * per, w * per + per) of the flat (tile,
+// dy, 16-column block) list.  (Round 6: one row per step left each step's
+// global loads exposed -- ~640 MFMA cycles per SIMD against a load round trip
+// -- and re-read the kmax window rows for every output row: 65 us for the
+// Cfg2 cross-embed, 0.06 of HBM.  RB = 4 rows per step amortises the latency
+// and reads (kmax + 3) / 4 window rows per output row instead of kmax.)
 // ---------------------------------------------------------------------------
-template <int CP, int MAXI>
+template <int CP, int MAXI, int RB>
 __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy, int lddy,
                                                        const bf16* x, int ldx, float* part, int H,
                                                        int W, int rows, int per) {
@@ -316,11 +321,11 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
   const int bands = (H + rows - 1) / rows;
   const int f = blockIdx.x / bands, yb = (blockIdx.x % bands) * rows;
   const int yend = min(yb + rows, H);
-  const int half = g.kmax / 2, XC = W + g.kmax + 7;
-  const int DS = g.cpad + 8;                 // dY row pitch (elements)
-  const int DYB = W * DS, XB = g.kmax * XC * CP;  // buffer sizes (elements)
-  bf16* sD = (bf16*)smem;                    // [2][W][DS]
-  bf16* sX = sD + 2 * DYB;                   // [2][kmax][XC][CP]
+  const int half = g.kmax / 2, XC = W + g.kmax + 7, XR = g.kmax + RB - 1;
+  const int DS = g.cpad + 8;                      // dY row pitch (elements)
+  const int DYB = RB * W * DS, XB = XR * XC * CP;  // buffer sizes (elements)
+  bf16* sD = (bf16*)smem;                         // [2][RB][W][DS]
+  bf16* sX = sD + 2 * DYB;                        // [2][XR][XC][CP]
 
   // ---- this wave's items: tile, LDS offsets ----
   int it_t[MAXI], it_boff[MAXI];
@@ -338,7 +343,7 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
     const int d = idx / g.nb16[t], nb = idx - d * g.nb16[t];
     const int cofs = half - g.k[t] / 2;
     it_t[i] = t;
-    it_boff[i] = ((d + cofs) * XC + cofs) * CP + 16 * nb;  // element offset (pixel 0)
+    it_boff[i] = ((d + cofs) * XC + cofs) * CP + 16 * nb;  // element offset (pixel 0, step row 0)
   }
 
   int t_lo = XE_MAXT, t_hi = -1;
@@ -354,19 +359,22 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
   for (int i = 0; i < MAXI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float accb = 0.f;  // bias: waves < ntiles own tile `wave`
 
-  // ---- staging: global -> registers (next row) -> LDS ----
-  const int dchunks = W * (g.cout / 8);       // 16-B dY chunks per row
-  const int xelems = g.kmax * XC;             // window pixels per row
-  constexpr int DPT = 4, XPT = 9;             // per-thread register slots (w = 256, k = 15: 4170 pixels)
+  // ---- staging: global -> registers (next step) -> LDS ----
+  const int cch = g.cout / 8;                 // 16-B dY chunks per pixel
+  const int dchunks = RB * W * cch;           // per step
+  const int xelems = XR * XC;                 // window pixels per step
+  constexpr int DPT = 4, XPT = 9;             // per-thread register slots (checked by the host)
   u32x4 dreg[DPT];
   bf16 xreg[XPT][CP];
-  auto load_row = [&](int yy) {
+  auto load_step = [&](int y0) {
 #pragma unroll
     for (int s = 0; s < DPT; ++s) {
       const int i = tid + 512 * s;
+      dreg[s] = u32x4{0u, 0u, 0u, 0u};
       if (i < dchunks) {
-        const int p = i / (g.cout / 8), c8 = i - p * (g.cout / 8);
-        dreg[s] = *(const u32x4*)(dy + ((long long)(f * H + yy) * W + p) * lddy + 8 * c8);
+        const int rp = i / cch, c8 = i - rp * cch, r = rp / W, p = rp - r * W;
+        if (y0 + r < yend)  // rows of the next band stay zero: they add nothing
+          dreg[s] = *(const u32x4*)(dy + ((long long)(f * H + y0 + r) * W + p) * lddy + 8 * c8);
       }
     }
 #pragma unroll
@@ -376,7 +384,7 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
       for (int c = 0; c < CP; ++c) xreg[s][c] = (bf16)0.f;
       if (i < xelems) {
         const int rr = i / XC, cc = i - rr * XC;
-        const int sy = yy + rr - half, sx = cc - half;
+        const int sy = y0 + rr - half, sx = cc - half;
         if ((unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W) {
           const bf16* src = x + ((long long)(f * H + sy) * W + sx) * ldx;
           if (CP == 4) {
@@ -392,14 +400,14 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
       }
     }
   };
-  auto store_row = [&](int buf) {
+  auto store_step = [&](int buf) {
     bf16* d = sD + buf * DYB;
 #pragma unroll
     for (int s = 0; s < DPT; ++s) {
       const int i = tid + 512 * s;
       if (i < dchunks) {
-        const int p = i / (g.cout / 8), c8 = i - p * (g.cout / 8);
-        *(u32x4*)(d + p * DS + 8 * c8) = dreg[s];
+        const int rp = i / cch, c8 = i - rp * cch;
+        *(u32x4*)(d + rp * DS + 8 * c8) = dreg[s];
       }
     }
     bf16* xs = sX + buf * XB;
@@ -419,44 +427,47 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
   const int plo = 8 * kg + q;
 
   if (g.cpad != g.cout) {  // channels [cout, cpad) of both dY buffers stay zero
-    for (int i = tid; i < 2 * W; i += 512)
+    for (int i = tid; i < 2 * RB * W; i += 512)
       for (int c = g.cout; c < g.cpad; c += 8) *(u32x4*)(sD + i * DS + c) = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
   }
   if (yb < yend) {
-    load_row(yb);
-    store_row(0);
+    load_step(yb);
+    store_step(0);
   }
   __syncthreads();
-  for (int yy = yb; yy < yend; ++yy) {
-    const int buf = (yy - yb) & 1;
-    const bool more = yy + 1 < yend;
-    if (more) load_row(yy + 1);
-    const char* d = (const char*)(sD + buf * DYB);
-    const char* xs = (const char*)(sX + buf * XB);
-    for (int p0 = 0; p0 < W; p0 += 32) {
-      const char* arow = d + ((p0 + plo) * DS + 4 * pp) * 2;
-      if (wave < g.ntiles) {  // bias: the dY^T fragment of tile `wave` summed on the VALU
-        const char* a = arow + 32 * wave;
-        const bf16x8 e = __builtin_bit_cast(bf16x8, tr_pair(a, a + 4 * DS * 2));
+  for (int y0 = yb; y0 < yend; y0 += RB) {
+    const int buf = ((y0 - yb) / RB) & 1;
+    const bool more = y0 + RB < yend;
+    if (more) load_step(y0 + RB);
+    const int nr = min(RB, yend - y0);
+    for (int r = 0; r < nr; ++r) {
+      const char* d = (const char*)(sD + buf * DYB + r * W * DS);
+      const char* xs = (const char*)(sX + buf * XB + r * XC * CP);
+      for (int p0 = 0; p0 < W; p0 += 32) {
+        const char* arow = d + ((p0 + plo) * DS + 4 * pp) * 2;
+        if (wave < g.ntiles) {  // bias: the dY^T fragment of tile `wave` summed on the VALU
+          const char* a = arow + 32 * wave;
+          const bf16x8 e = __builtin_bit_cast(bf16x8, tr_pair(a, a + 4 * DS * 2));
 #pragma unroll
-        for (int j = 0; j < 8; ++j) accb += (float)e[j];
-      }
-      const int lanex = ((p0 + plo) * CP + 4 * pp) * 2;
-      // items are ordered by tile: one dY^T fragment per tile this wave touches
-      for (int t = t_lo; t <= t_hi; ++t) {
-        const char* a = arow + 32 * t;
-        const u32x4 fa = tr_pair(a, a + 4 * DS * 2);
+          for (int j = 0; j < 8; ++j) accb += (float)e[j];
+        }
+        const int lanex = ((p0 + plo) * CP + 4 * pp) * 2;
+        // items are ordered by tile: one dY^T fragment per tile this wave touches
+        for (int t = t_lo; t <= t_hi; ++t) {
+          const char* a = arow + 32 * t;
+          const u32x4 fa = tr_pair(a, a + 4 * DS * 2);
 #pragma unroll
-        for (int i = 0; i < MAXI; ++i) {
-          if (it_t[i] != t) continue;
-          const char* b = xs + it_boff[i] * 2 + lanex;
-          acc[i] = mma16(fa, tr_pair(b, b + 4 * CP * 2), acc[i]);
+          for (int i = 0; i < MAXI; ++i) {
+            if (it_t[i] != t) continue;
+            const char* b = xs + it_boff[i] * 2 + lanex;
+            acc[i] = mma16(fa, tr_pair(b, b + 4 * CP * 2), acc[i]);
+          }
         }
       }
     }
     if (more) {
-      store_row(buf ^ 1);
+      store_step(buf ^ 1);
     }
     __syncthreads();
   }
@@ -554,8 +565,17 @@ size_t xe_fwd_lds(const XeGeom& g, int w) {
   return (size_t)g.image_elems * 2 + (size_t)(xe_r() + g.kmax - 1) * (WB + g.kmax + 7) * g.cp * 2;
 }
 
-size_t xe_wgrad_lds(const XeGeom& g, int w) {
-  return (size_t)2 * w * (g.cpad + 8) * 2 + (size_t)2 * g.kmax * (w + g.kmax + 7) * g.cp * 2;
+constexpr int XE_RB = 4;  // wgrad: image rows per staging step (1 where 4 do not fit)
+
+size_t xe_wgrad_lds(const XeGeom& g, int w, int rb) {
+  return (size_t)2 * rb * w * (g.cpad + 8) * 2 + (size_t)2 * (g.kmax + rb - 1) * (w + g.kmax + 7) * g.cp * 2;
+}
+
+// the register staging slots (DPT = 4 dY chunks, XPT = 9 window pixels per
+// thread) and the LDS hold rb rows per step
+bool xe_wgrad_fits(const XeGeom& g, int w, int rb) {
+  return (long long)rb * w * (g.cout / 8) <= 4 * 512 && (long long)(g.kmax + rb - 1) * (w + g.kmax + 7) <= 9 * 512 &&
+         xe_wgrad_lds(g, w, rb) <= 160 * 1024;
 }
 
 int xe_rows(int nf, int h) {
@@ -711,23 +731,24 @@ extern "C" int dv_cross_embed_wgrad(const DvCrossEmbed* ce, const void* dy, int 
   long long need = 0;
   dv_cross_embed_wgrad_ws(ce, nf, h, w, &need);
   DV_REQUIRE(ws_floats >= need, "workspace too small (see dv_cross_embed_wgrad_ws)");
-  const size_t lds = xe_wgrad_lds(g, w);
-  DV_REQUIRE(lds <= 160 * 1024, "LDS footprint too large");
-  // register staging slots: DPT = 4 dY chunks, XPT = 9 window pixels per thread
-  DV_REQUIRE((long long)w * (g.cout / 8) <= 4 * 512 && (long long)g.kmax * (w + g.kmax + 7) <= 9 * 512,
-             "image row too wide for the staging slots");
+  const int rb = xe_wgrad_fits(g, w, XE_RB) ? XE_RB : 1;
+  DV_REQUIRE(xe_wgrad_fits(g, w, rb), "image row too wide for the staging slots / LDS");
+  const size_t lds = xe_wgrad_lds(g, w, rb);
   const int per = (g.items + 7) / 8;
   DV_REQUIRE(per <= 24, "too many accumulator tiles");
   const int rows = xe_rows(nf, h);
   const int S = nf * ((h + rows - 1) / rows);
   hipStream_t st = (hipStream_t)stream;
-  static bool once = (xe_allow_lds(xe_wgrad_kernel<4, 12>), xe_allow_lds(xe_wgrad_kernel<4, 24>),
-                      xe_allow_lds(xe_wgrad_kernel<8, 12>), xe_allow_lds(xe_wgrad_kernel<8, 24>), true);
+  static bool once = (xe_allow_lds(xe_wgrad_kernel<4, 12, XE_RB>), xe_allow_lds(xe_wgrad_kernel<4, 24, XE_RB>),
+                      xe_allow_lds(xe_wgrad_kernel<8, 12, XE_RB>), xe_allow_lds(xe_wgrad_kernel<8, 24, XE_RB>),
+                      xe_allow_lds(xe_wgrad_kernel<4, 12, 1>), xe_allow_lds(xe_wgrad_kernel<4, 24, 1>),
+                      xe_allow_lds(xe_wgrad_kernel<8, 12, 1>), xe_allow_lds(xe_wgrad_kernel<8, 24, 1>), true);
   (void)once;
   const bf16* d = (const bf16*)dy;
   const bf16* xx = (const bf16*)x;
-#define XE_WG(CP, MI) \
-  xe_wgrad_kernel<CP, MI><<<(unsigned)S, 512, lds, st>>>(g, d, lddy, xx, ldx, ws, h, w, rows, per)
+#define XE_WG2(CP, MI, RB) \
+  xe_wgrad_kernel<CP, MI, RB><<<(unsigned)S, 512, lds, st>>>(g, d, lddy, xx, ldx, ws, h, w, rows, per)
+#define XE_WG(CP, MI) (rb == XE_RB ? XE_WG2(CP, MI, XE_RB) : XE_WG2(CP, MI, 1))
   if (g.cp == 4) {
     if (per <= 12) XE_WG(4, 12);
     else XE_WG(4, 24);
@@ -736,6 +757,7 @@ extern "C" int dv_cross_embed_wgrad(const DvCrossEmbed* ce, const void* dy, int 
     else XE_WG(8, 24);
   }
 #undef XE_WG
+#undef XE_WG2
   const long long total = xe_total_grads(g);
   xe_wgrad_finish_kernel<<<(unsigned)((total + 31) / 32), 256, 0, st>>>(*ce, g, ws, S, total);
   return check_launch("cross_embed_wgrad");
