@@ -565,7 +565,7 @@ size_t xe_fwd_lds(const XeGeom& g, int w) {
   return (size_t)g.image_elems * 2 + (size_t)(xe_r() + g.kmax - 1) * (WB + g.kmax + 7) * g.cp * 2;
 }
 
-constexpr int XE_RB = 4;  // wgrad: image rows per staging step (1 where 4 do not fit)
+constexpr int XE_RB = 4;  // wgrad: image rows per staging step (8 where they fit, 1 where 4 do not)
 
 size_t xe_wgrad_lds(const XeGeom& g, int w, int rb) {
   return (size_t)2 * rb * w * (g.cpad + 8) * 2 + (size_t)2 * (g.kmax + rb - 1) * (w + g.kmax + 7) * g.cp * 2;
@@ -686,6 +686,68 @@ extern "C" int dv_conv_small_pack(const float* wt, const float* bias, int cin, i
   return check_launch("conv_small_pack");
 }
 
+namespace {
+struct XeSmallPack {
+  DvCrossEmbed ce;
+  XeGeom g;
+  bf16* img;
+};
+// entry blockIdx.y: the xe_pack_kernel loop over that entry's image
+__global__ __launch_bounds__(256) void xe_pack_batched_kernel(const XeSmallPack* t) {
+  const XeSmallPack& e = t[blockIdx.y];
+  const DvCrossEmbed& ce = e.ce;
+  const XeGeom& g = e.g;
+  bf16* img = e.img;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < g.boff + g.cpad; i += gridDim.x * 256) {
+    if (i >= g.boff) {
+      const int co = i - g.boff;
+      ((float*)(img + g.boff))[co] = co < g.cout && ce.b[0] ? ce.b[0][co] : 0.f;
+      continue;
+    }
+    int tt = 0;
+    while (tt + 1 < g.ntiles && i >= g.woff[tt + 1]) ++tt;
+    const int k = g.k[tt], jwp = g.jwp[tt];
+    const int local = i - g.woff[tt];
+    float v = 0.f;
+    if (local < 16 * k * jwp) {
+      const int col = local / (k * jwp), rem = local - col * k * jwp;
+      const int dy = rem / jwp, j = rem - dy * jwp;
+      const int co = 16 * tt + col;
+      const int dx = j / g.cp, c = j - dx * g.cp;
+      if (co < g.cout && j < k * g.cp && c < g.cin && dx < k)
+        v = ce.w[0][(((long long)co * g.cin + c) * k + dy) * k + dx];
+    }
+    img[i] = (bf16)v;
+  }
+}
+}  // namespace
+
+extern "C" int dv_conv_small_pack_plan(const DvSmallPackEntry* entries, int n, void* table, long long* bytes,
+                                       long long* max_elems) {
+  DV_REQUIRE(entries && bytes && max_elems && n > 0, "null pointer / empty");
+  *bytes = (long long)n * sizeof(XeSmallPack);
+  long long mx = 0;
+  for (int i = 0; i < n; ++i) {
+    const DvSmallPackEntry& e = entries[i];
+    DV_REQUIRE(e.w && e.image, "null weight / image");
+    XeSmallPack t{};
+    t.ce = small_desc(e.w, e.bias, e.cin, e.cout, e.ksize);
+    DV_REQUIRE(xe_geom(t.ce, t.g, true), "unsupported shape");
+    t.img = (bf16*)e.image;
+    mx = std::max(mx, (long long)(t.g.boff + t.g.cpad));
+    if (table) ((XeSmallPack*)table)[i] = t;
+  }
+  *max_elems = mx;
+  return DV_OK;
+}
+
+extern "C" int dv_conv_small_pack_batched(const void* table, int n, long long max_elems, void* stream) {
+  DV_REQUIRE(table && n > 0 && n <= 65535 && max_elems > 0, "bad table");
+  const int blocks = (int)std::min<long long>(64, (max_elems + 255) / 256);
+  xe_pack_batched_kernel<<<dim3(blocks, n), 256, 0, (hipStream_t)stream>>>((const XeSmallPack*)table);
+  return check_launch("conv_small_pack_batched");
+}
+
 extern "C" int dv_conv_small_fwd(const void* x0, int ld0, int c0, const void* x1, int ld1,
                                  const void* image, const void* res, int ldres, void* y, int ldy,
                                  int nf, int h, int w, int cin, int cout, int ksize, void* stream) {
@@ -731,7 +793,7 @@ extern "C" int dv_cross_embed_wgrad(const DvCrossEmbed* ce, const void* dy, int 
   long long need = 0;
   dv_cross_embed_wgrad_ws(ce, nf, h, w, &need);
   DV_REQUIRE(ws_floats >= need, "workspace too small (see dv_cross_embed_wgrad_ws)");
-  const int rb = xe_wgrad_fits(g, w, XE_RB) ? XE_RB : 1;
+  const int rb = xe_wgrad_fits(g, w, 2 * XE_RB) ? 2 * XE_RB : xe_wgrad_fits(g, w, XE_RB) ? XE_RB : 1;
   DV_REQUIRE(xe_wgrad_fits(g, w, rb), "image row too wide for the staging slots / LDS");
   const size_t lds = xe_wgrad_lds(g, w, rb);
   const int per = (g.items + 7) / 8;
@@ -742,13 +804,17 @@ extern "C" int dv_cross_embed_wgrad(const DvCrossEmbed* ce, const void* dy, int 
   static bool once = (xe_allow_lds(xe_wgrad_kernel<4, 12, XE_RB>), xe_allow_lds(xe_wgrad_kernel<4, 24, XE_RB>),
                       xe_allow_lds(xe_wgrad_kernel<8, 12, XE_RB>), xe_allow_lds(xe_wgrad_kernel<8, 24, XE_RB>),
                       xe_allow_lds(xe_wgrad_kernel<4, 12, 1>), xe_allow_lds(xe_wgrad_kernel<4, 24, 1>),
-                      xe_allow_lds(xe_wgrad_kernel<8, 12, 1>), xe_allow_lds(xe_wgrad_kernel<8, 24, 1>), true);
+                      xe_allow_lds(xe_wgrad_kernel<8, 12, 1>), xe_allow_lds(xe_wgrad_kernel<8, 24, 1>),
+                      xe_allow_lds(xe_wgrad_kernel<4, 12, 2 * XE_RB>), xe_allow_lds(xe_wgrad_kernel<4, 24, 2 * XE_RB>),
+                      xe_allow_lds(xe_wgrad_kernel<8, 12, 2 * XE_RB>), xe_allow_lds(xe_wgrad_kernel<8, 24, 2 * XE_RB>),
+                      true);
   (void)once;
   const bf16* d = (const bf16*)dy;
   const bf16* xx = (const bf16*)x;
 #define XE_WG2(CP, MI, RB) \
   xe_wgrad_kernel<CP, MI, RB><<<(unsigned)S, 512, lds, st>>>(g, d, lddy, xx, ldx, ws, h, w, rows, per)
-#define XE_WG(CP, MI) (rb == XE_RB ? XE_WG2(CP, MI, XE_RB) : XE_WG2(CP, MI, 1))
+#define XE_WG(CP, MI) \
+  (rb == 2 * XE_RB ? XE_WG2(CP, MI, 2 * XE_RB) : rb == XE_RB ? XE_WG2(CP, MI, XE_RB) : XE_WG2(CP, MI, 1))
   if (g.cp == 4) {
     if (per <= 12) XE_WG(4, 12);
     else XE_WG(4, 24);

@@ -50,6 +50,8 @@ _SIGS = {
     "dv_cross_embed_wgrad": [_P, _P, _I, _P, _I, _P, _L, _I, _I, _I, _P],
     "dv_conv_small_image_elems": [_I, _I, _I, _P],
     "dv_conv_small_pack": [_P, _P, _I, _I, _I, _P, _P],
+    "dv_conv_small_pack_plan": [_P, _I, _P, _P, _P],
+    "dv_conv_small_pack_batched": [_P, _I, _L, _P],
     "dv_conv_small_fwd": [_P, _I, _I, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "dv_bias_grad": [_I, _P, _I, _P, _L, _I, _P],
     "dv_pack_conv_weight": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
@@ -104,6 +106,11 @@ class DvWgradReduceEntry(ctypes.Structure):
     """Mirror of DvWgradReduceEntry (include/dv_hip.h)."""
     _fields_ = [("part", _P), ("dbpart", _P), ("dw", _P), ("db", _P), ("n4", _L), ("blk0", _L),
                 ("S", _I), ("G", _I), ("cout", _I), ("acc_w", _I), ("acc_b", _I), ("part_bf16", _I)]
+
+
+class DvSmallPackEntry(ctypes.Structure):
+    """Mirror of DvSmallPackEntry (include/dv_hip.h)."""
+    _fields_ = [("w", _P), ("bias", _P), ("image", _P), ("cin", _I), ("cout", _I), ("ksize", _I)]
 
 
 class DVError(RuntimeError):

@@ -554,7 +554,9 @@ class PackCache:
         self.static = False  # weights do not change while this cache is current (sampling)
         self.epoch = 0
         self.entries = {}  # key -> dict(out, w, meta, epoch, version)
-        self.small = {}  # small-channel conv images (_small_image)
+        self.small = {}  # small-channel conv images (_small_image, no trainer / sampling)
+        self.small_tr = {}  # small-channel conv images under a trainer: refreshed per update
+        self._small_table = None
         self.mx8 = {}  # MX-fp8 conv weight images (mx8_weight_image)
         self._table = None
         self._table_key = None
@@ -576,6 +578,43 @@ class PackCache:
         e["epoch"], e["version"] = self.epoch, weight._version
         return e["out"], True
 
+    def small_entry(self, weight, w, bias, cin, cout, k):
+        """The trainer-cache image of a small-channel conv: packed now when
+        new (an eager call: the trainer's warm-up precedes every capture), then
+        only by refresh()."""
+        import weakref
+        key = (w.data_ptr(), tuple(w.shape), None if bias is None else bias.data_ptr(), cin, cout, k)
+        e = self.small_tr.get(key)
+        if e is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise _lib.DVError("small-conv image first built inside a captured region")
+            n = ctypes.c_longlong(0)
+            call("dv_conv_small_image_elems", cin, cout, k, ctypes.byref(n))
+            img = torch.empty(n.value, dtype=torch.bfloat16, device=w.device)
+            call("dv_conv_small_pack", ptr(w), ptr(bias), cin, cout, k, ptr(img), stream())
+            e = self.small_tr[key] = dict(img=img, w=w, bias=bias, meta=(cin, cout, k), param=weakref.ref(weight))
+            self._small_table = None
+        return e["img"]
+
+    def _refresh_small(self):
+        if not self.small_tr:
+            return
+        if self._small_table is None:
+            ents = list(self.small_tr.values())
+            host = (_lib.DvSmallPackEntry * len(ents))(*[
+                _lib.DvSmallPackEntry(e["w"].data_ptr(), None if e["bias"] is None else e["bias"].data_ptr(),
+                                      e["img"].data_ptr(), *e["meta"]) for e in ents])
+            nbytes, mx = ctypes.c_longlong(0), ctypes.c_longlong(0)
+            call("dv_conv_small_pack_plan", ctypes.byref(host), len(ents), None, ctypes.byref(nbytes),
+                 ctypes.byref(mx))
+            buf = ctypes.create_string_buffer(nbytes.value)
+            call("dv_conv_small_pack_plan", ctypes.byref(host), len(ents), buf, ctypes.byref(nbytes),
+                 ctypes.byref(mx))
+            raw = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8)
+            self._small_table = (raw.to(ents[0]["img"].device), len(ents), mx.value)
+        tab, n, mx = self._small_table
+        call("dv_conv_small_pack_batched", ptr(tab), n, mx, stream())
+
     def prune(self):
         """Drop the entries whose parameter is gone or now lives elsewhere
         (re-pointed into a new flat buffer, moved by `.to()`); the others —
@@ -591,11 +630,17 @@ class PackCache:
         gone = [k for k, e in self.mx8.items() if e[2]() is None or e[2]().data_ptr() != k[0]]
         for k in gone:
             del self.mx8[k]
+        stale = [k for k, e in self.small_tr.items() if e["param"]() is None or e["param"]().data_ptr() != k[0]]
+        for k in stale:
+            del self.small_tr[k]
+        if stale:
+            self._small_table = None
 
     def refresh(self):
         """New epoch (weights were updated): repack all entries in one launch."""
         import ctypes
         self.epoch += 1
+        self._refresh_small()
         if not self.entries:
             return
         ents = list(self.entries.values())
@@ -661,6 +706,8 @@ class PackCache:
     def clear(self):
         self.entries.clear()
         self.mx8.clear()
+        self.small_tr.clear()
+        self._small_table = None
         self._table = self._table_key = None
 
 
@@ -1057,6 +1104,30 @@ class ConvFn(torch.autograd.Function):
             ld0 = cl_ld(x0)
             ld1 = cl_ld(x1) if x1 is not None else 0
             m = nf * h * w
+            if (x1 is None and weight.dim() == 5 and cin_real <= 8 and lddy % 8 == 0
+                    and cross_embed_ok(x0, [weight])):
+                # a small-input-channel conv (the cascade SR unet's dim-8 convs at
+                # 128^2 / 64^2): its weight gradient is the single-branch case of
+                # the cross-embed kernel (row-band MFMA partials + one finishing
+                # sum), not an implicit GEMM with 8 of 64 output rows live
+                desc = _cross_embed_desc(cin_real, [weight.detach()], [None])
+                desc.dw[0], desc.accumulate_w = dw_t.data_ptr(), int(acc_w)
+                if want_b:
+                    desc.db[0], desc.accumulate_b = db_t.data_ptr(), int(acc_b)
+                WGRAD_DEFER.before_write(dw_t.data_ptr(), db_t.data_ptr() if db_t is not None else None)
+                need = ctypes.c_longlong(0)
+                call("dv_cross_embed_wgrad_ws", ctypes.byref(desc), nf, h, w, ctypes.byref(need))
+                key = str(dy.device)
+                xws = _XE_WS.get(key)
+                if xws is None or xws.numel() < need.value:
+                    xws = _XE_WS[key] = torch.empty(need.value, dtype=torch.float32, device=dy.device)
+                _launch("cross_embed_wgrad_kernel", 2.0 * m * cout * cin_real * ksize * ksize,
+                        dy8.element_size() * m * (cin + cout8),
+                        lambda: call("dv_cross_embed_wgrad", ctypes.byref(desc), ptr(dy8), lddy, ptr(x0), ld0,
+                                     ptr(xws), xws.numel(), nf, h, w, stream()),
+                        ("wgrad", cout, cin_real * ksize * ksize, m))
+                dres = dy if has_res else None
+                return dx0, dx1, dw, db, dres, None, None, None, None, None, None, None
             dname = _lib.dtype_name(dy8)
             kname = (conv_wgrad_name(dname, m, cout8, cin, c0, x1 is not None, ksize, h, w,
                                      max(lddy, ld0, ld1)) if (cout8 == cout and cin_real == cin)
@@ -1133,11 +1204,14 @@ def _small_image(weight, bias, cin, cout, k, cache):
     current PackCache (torch version counters checked) while its weights
     cannot change behind torch's back: a sampling region's private cache, or
     no trainer at all.  Under a trainer's cache (AdamW writes the weights in
-    place) it is rebuilt by every call, so a captured graph repacks on
-    replay."""
+    place) the image is a PackCache entry too, repacked -- all of them in ONE
+    launch -- by the cache's per-update refresh(): the forward (and a captured
+    graph of it) then launches no pack kernel."""
     w = weight.detach()
     if w.dtype != torch.float32 or not w.is_contiguous():
         w = w.float().contiguous()
+    if cache and PACK.enabled and not PACK.static and w.data_ptr() == weight.data_ptr():
+        return PACK.small_entry(weight, w, bias, cin, cout, k)
     keep = cache and (PACK.static or not PACK.enabled) and w.data_ptr() == weight.data_ptr()
     key = (weight.data_ptr(), tuple(weight.shape), None if bias is None else bias.data_ptr())
     ver = (weight._version, None if bias is None else bias._version)

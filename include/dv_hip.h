@@ -159,6 +159,21 @@ int dv_conv_small_pack(const float* w, const float* bias, int cin, int cout, int
 int dv_conv_small_fwd(const void* x0, int ld0, int c0, const void* x1, int ld1, const void* image,
                       const void* res, int ldres, void* y, int ldy, int nf, int h, int w, int cin,
                       int cout, int ksize, void* stream);
+/* Many dv_conv_small_pack calls in ONE launch (the trainer repacks every
+ * small-channel conv image once per optimizer step).  dv_conv_small_pack_plan
+ * expands n host entries into the launch table: with `table` NULL it only
+ * reports its size in *bytes; the caller copies the table to the device and
+ * passes it to dv_conv_small_pack_batched (tables depend on the entries'
+ * pointers and shapes only, so one upload serves every step).              */
+typedef struct {
+  const float* w;     /* f32 torch weight (cout, cin, 1, k, k) */
+  const float* bias;  /* f32 [cout] or NULL */
+  void* image;        /* dv_conv_small_image_elems bf16 elements */
+  int cin, cout, ksize;
+} DvSmallPackEntry;
+int dv_conv_small_pack_plan(const DvSmallPackEntry* entries, int n, void* table, long long* bytes,
+                            long long* max_elems);
+int dv_conv_small_pack_batched(const void* table, int n, long long max_elems, void* stream);
 
 /* 3x3 forward / dgrad, window form (dalle2_video.py:107 Block3D.project at
  * the 8x8 .. 64x64 stages, and the dgrads of those convs): same contract as

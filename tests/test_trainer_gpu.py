@@ -227,6 +227,43 @@ def test_graph_replay_matches_eager():
             raise AssertionError(f"{e} vs {gph}: rel {err:.3e}; worst params {worst}")
 
 
+def test_graph_replay_sees_inputs_modified_in_place():
+    """The replay skips copying an input that is the previous call's very
+    tensor, unmodified (its version counter): an in-place change of that
+    tensor, or another tensor, must be copied in.  Replays with modified /
+    new inputs equal the eager calls on the same data."""
+    from dalle2_video import dalle2_video as D
+    from dalle2_video.trainer import VideoDecoderTrainer
+    from dalle2_video.utils import deterministic_fill_
+
+    u = D.Unet3D(16, video_embed_dim=512, channels=3, dim_mults=(1, 2, 4, 8))
+    dec = D.VideoDecoder(u, frame_sizes=(32,), frame_numbers=(4,), timesteps=1000, learned_variance=False)
+    deterministic_fill_(dec.unets[0])
+    dec = dec.cuda()
+
+    def run(graphs):
+        tr = VideoDecoderTrainer(dec, lr=0.0, use_ema=False, use_graphs=graphs)
+        g = torch.Generator(device="cuda").manual_seed(3)
+        video = torch.rand(2, 3, 4, 32, 32, device="cuda", generator=g)
+        other = torch.rand(2, 3, 4, 32, 32, device="cuda", generator=g)
+        torch.cuda.manual_seed(1)
+        tr(video=video, unet_number=1)
+        tr.update(1)
+        out = []
+        for step in range(7):  # calls 3.. replay when graphs=True
+            if step == 4:
+                video.mul_(0.5)  # in place: same object, new version
+            x = other if step == 6 else video
+            torch.cuda.manual_seed(11)
+            out.append(tr(video=x, unet_number=1))
+        return out
+
+    eager, graph = run(False), run(True)
+    for a, b in zip(eager, graph):
+        assert abs(a - b) <= 1e-5 * abs(a), (eager, graph)
+    assert abs(eager[3] - eager[4]) > 1e-4 * abs(eager[3])  # the in-place change mattered
+
+
 def test_graph_replay_after_checkpoint_load(tmp_path):
     """A captured graph keeps writing the live gradient buffer after
     trainer.save/load (the flat buffers are kept): replayed calls
