@@ -364,8 +364,17 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
   const int dchunks = RB * W * cch;           // per step
   const int xelems = XR * XC;                 // window pixels per step
   constexpr int DPT = 4, XPT = 9;             // per-thread register slots (checked by the host)
+  // a window pixel is CP bf16 = one 8- or 16-B vector: loaded, channel-masked
+  // (c >= cin zero) and written to LDS whole (round 5 moved it element by
+  // element: 8 ds_write_b16 per pixel)
+  typedef typename std::conditional<CP == 8, u32x4, u32x2>::type XV;
+  constexpr int XW = CP / 2;  // dwords per pixel
   u32x4 dreg[DPT];
-  bf16 xreg[XPT][CP];
+  XV xreg[XPT];
+  XV cmask;
+#pragma unroll
+  for (int j = 0; j < XW; ++j)
+    cmask[j] = (2 * j < g.cin ? 0x0000ffffu : 0u) | (2 * j + 1 < g.cin ? 0xffff0000u : 0u);
   auto load_step = [&](int y0) {
 #pragma unroll
     for (int s = 0; s < DPT; ++s) {
@@ -381,22 +390,12 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
     for (int s = 0; s < XPT; ++s) {
       const int i = tid + 512 * s;
 #pragma unroll
-      for (int c = 0; c < CP; ++c) xreg[s][c] = (bf16)0.f;
+      for (int j = 0; j < XW; ++j) xreg[s][j] = 0u;
       if (i < xelems) {
         const int rr = i / XC, cc = i - rr * XC;
         const int sy = y0 + rr - half, sx = cc - half;
-        if ((unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W) {
-          const bf16* src = x + ((long long)(f * H + sy) * W + sx) * ldx;
-          if (CP == 4) {
-            const bf16x4 e = __builtin_bit_cast(bf16x4, *(const u32x2*)src);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) xreg[s][c] = c < g.cin ? e[c] : (bf16)0.f;
-          } else {
-            const bf16x8 e = __builtin_bit_cast(bf16x8, *(const u32x4*)src);
-#pragma unroll
-            for (int c = 0; c < CP; ++c) xreg[s][c] = c < g.cin ? e[c % 8] : (bf16)0.f;
-          }
-        }
+        if ((unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W)
+          xreg[s] = *(const XV*)(x + ((long long)(f * H + sy) * W + sx) * ldx) & cmask;
       }
     }
   };
@@ -414,10 +413,7 @@ __global__ __launch_bounds__(512) void xe_wgrad_kernel(XeGeom g, const bf16* dy,
 #pragma unroll
     for (int s = 0; s < XPT; ++s) {
       const int i = tid + 512 * s;
-      if (i < xelems) {
-#pragma unroll
-        for (int c = 0; c < CP; ++c) xs[i * CP + c] = xreg[s][c];
-      }
+      if (i < xelems) *(XV*)(xs + i * CP) = xreg[s];
     }
   };
 
@@ -691,6 +687,7 @@ struct XeSmallPack {
   DvCrossEmbed ce;
   XeGeom g;
   bf16* img;
+  int mode, wcin;  // DvSmallPackEntry
 };
 // entry blockIdx.y: the xe_pack_kernel loop over that entry's image
 __global__ __launch_bounds__(256) void xe_pack_batched_kernel(const XeSmallPack* t) {
@@ -714,8 +711,11 @@ __global__ __launch_bounds__(256) void xe_pack_batched_kernel(const XeSmallPack*
       const int dy = rem / jwp, j = rem - dy * jwp;
       const int co = 16 * tt + col;
       const int dx = j / g.cp, c = j - dx * g.cp;
-      if (co < g.cout && j < k * g.cp && c < g.cin && dx < k)
-        v = ce.w[0][(((long long)co * g.cin + c) * k + dy) * k + dx];
+      if (co < g.cout && j < k * g.cp && c < g.cin && dx < k) {
+        if (e.mode == 0) v = ce.w[0][(((long long)co * g.cin + c) * k + dy) * k + dx];
+        else if (co < e.wcin)  // dgrad image: w[c][co][k-1-dy][k-1-dx] of the (cin_img, wcin) weight
+          v = ce.w[0][(((long long)c * e.wcin + co) * k + (k - 1 - dy)) * k + (k - 1 - dx)];
+      }
     }
     img[i] = (bf16)v;
   }
@@ -734,6 +734,10 @@ extern "C" int dv_conv_small_pack_plan(const DvSmallPackEntry* entries, int n, v
     t.ce = small_desc(e.w, e.bias, e.cin, e.cout, e.ksize);
     DV_REQUIRE(xe_geom(t.ce, t.g, true), "unsupported shape");
     t.img = (bf16*)e.image;
+    DV_REQUIRE(e.mode == 0 || (e.mode == 1 && e.wcin > 0 && e.wcin <= e.cout && !e.bias),
+               "mode 1 (dgrad image) needs 0 < wcin <= cout and no bias");
+    t.mode = e.mode;
+    t.wcin = e.wcin;
     mx = std::max(mx, (long long)(t.g.boff + t.g.cpad));
     if (table) ((XeSmallPack*)table)[i] = t;
   }

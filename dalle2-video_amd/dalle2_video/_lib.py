@@ -110,7 +110,8 @@ class DvWgradReduceEntry(ctypes.Structure):
 
 class DvSmallPackEntry(ctypes.Structure):
     """Mirror of DvSmallPackEntry (include/dv_hip.h)."""
-    _fields_ = [("w", _P), ("bias", _P), ("image", _P), ("cin", _I), ("cout", _I), ("ksize", _I)]
+    _fields_ = [("w", _P), ("bias", _P), ("image", _P), ("cin", _I), ("cout", _I), ("ksize", _I),
+                ("mode", _I), ("wcin", _I)]
 
 
 class DVError(RuntimeError):

@@ -578,12 +578,13 @@ class PackCache:
         e["epoch"], e["version"] = self.epoch, weight._version
         return e["out"], True
 
-    def small_entry(self, weight, w, bias, cin, cout, k):
-        """The trainer-cache image of a small-channel conv: packed now when
-        new (an eager call: the trainer's warm-up precedes every capture), then
-        only by refresh()."""
+    def small_entry(self, weight, w, bias, cin, cout, k, mode=0, wcin=0):
+        """The trainer-cache image of a small-channel conv (mode 0) or of its
+        input gradient (mode 1, DvSmallPackEntry): packed now when new (an
+        eager call: the trainer's warm-up precedes every capture), then only by
+        refresh()."""
         import weakref
-        key = (w.data_ptr(), tuple(w.shape), None if bias is None else bias.data_ptr(), cin, cout, k)
+        key = (w.data_ptr(), tuple(w.shape), None if bias is None else bias.data_ptr(), cin, cout, k, mode)
         e = self.small_tr.get(key)
         if e is None:
             if torch.cuda.is_current_stream_capturing():
@@ -591,8 +592,10 @@ class PackCache:
             n = ctypes.c_longlong(0)
             call("dv_conv_small_image_elems", cin, cout, k, ctypes.byref(n))
             img = torch.empty(n.value, dtype=torch.bfloat16, device=w.device)
-            call("dv_conv_small_pack", ptr(w), ptr(bias), cin, cout, k, ptr(img), stream())
-            e = self.small_tr[key] = dict(img=img, w=w, bias=bias, meta=(cin, cout, k), param=weakref.ref(weight))
+            e = dict(img=img, w=w, bias=bias, meta=(cin, cout, k, mode, wcin), param=weakref.ref(weight))
+            tab = _small_pack_table([e])
+            call("dv_conv_small_pack_batched", ptr(tab[0]), tab[1], tab[2], stream())
+            self.small_tr[key] = e
             self._small_table = None
         return e["img"]
 
@@ -600,18 +603,7 @@ class PackCache:
         if not self.small_tr:
             return
         if self._small_table is None:
-            ents = list(self.small_tr.values())
-            host = (_lib.DvSmallPackEntry * len(ents))(*[
-                _lib.DvSmallPackEntry(e["w"].data_ptr(), None if e["bias"] is None else e["bias"].data_ptr(),
-                                      e["img"].data_ptr(), *e["meta"]) for e in ents])
-            nbytes, mx = ctypes.c_longlong(0), ctypes.c_longlong(0)
-            call("dv_conv_small_pack_plan", ctypes.byref(host), len(ents), None, ctypes.byref(nbytes),
-                 ctypes.byref(mx))
-            buf = ctypes.create_string_buffer(nbytes.value)
-            call("dv_conv_small_pack_plan", ctypes.byref(host), len(ents), buf, ctypes.byref(nbytes),
-                 ctypes.byref(mx))
-            raw = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8)
-            self._small_table = (raw.to(ents[0]["img"].device), len(ents), mx.value)
+            self._small_table = _small_pack_table(list(self.small_tr.values()))
         tab, n, mx = self._small_table
         call("dv_conv_small_pack_batched", ptr(tab), n, mx, stream())
 
@@ -712,6 +704,19 @@ class PackCache:
 
 
 PACK = PackCache()
+
+
+def _small_pack_table(ents):
+    """(device launch table, n, max elements) of dv_conv_small_pack_batched."""
+    host = (_lib.DvSmallPackEntry * len(ents))(*[
+        _lib.DvSmallPackEntry(e["w"].data_ptr(), None if e["bias"] is None else e["bias"].data_ptr(),
+                              e["img"].data_ptr(), *e["meta"]) for e in ents])
+    nbytes, mx = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    call("dv_conv_small_pack_plan", ctypes.byref(host), len(ents), None, ctypes.byref(nbytes), ctypes.byref(mx))
+    buf = ctypes.create_string_buffer(nbytes.value)
+    call("dv_conv_small_pack_plan", ctypes.byref(host), len(ents), buf, ctypes.byref(nbytes), ctypes.byref(mx))
+    raw = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8)
+    return raw.to(ents[0]["img"].device), len(ents), mx.value
 
 
 class private_pack_cache:
@@ -1056,8 +1061,18 @@ class ConvFn(torch.autograd.Function):
             flops = 2.0 * m * cin_real * cout8 * ksize * ksize * ctx.algo_scale
             nbytes = dy8.element_size() * m * (cin + cout8)
             shape = ("dgrad", m, cin_real, cout8 * ksize * ksize)
-            if window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, ldx, rld, ksize, h, w, nf,
-                         ldres2=rld2):
+            if (dy8.dtype == torch.bfloat16 and cout <= 16 and cin <= 32 and ksize % 2 == 1 and ksize <= 15
+                    and w % 32 == 0 and rp2 is None and lddy % 8 == 0 and ldx % 4 == 0 and rld % 4 == 0
+                    and weight.dim() == 5 and dy8.data_ptr() % 16 == 0):
+                # small-channel dgrad (the cascade SR unet's dim-8 / 16 convs): a
+                # conv of dY with the transposed, flipped weight on the direct
+                # small-channel kernel (an implicit GEMM ran it 8 of 64 rows live)
+                img = _small_dgrad_image(weight, cout, cin, cin_real, ksize, ctx.cache)
+                _launch("xe_fwd_kernel", flops, nbytes,
+                        lambda: call("dv_conv_small_fwd", ptr(dy8), lddy, cout, None, 0, ptr(img), rp, rld,
+                                     ptr(dx), ldx, nf, h, w, cout, cin, ksize, stream()), shape)
+            elif window_ok(dy8, None, cout8, cout8, cin_real, lddy, lddy, ldx, rld, ksize, h, w, nf,
+                           ldres2=rld2):
                 wpd = pack_conv_weight(weight, dy.dtype, cout8, 3, ctx.cache)
                 _launch(f"conv_fwd_frame_kernel<{w}>", flops, nbytes,
                         lambda: call("dv_conv_fwd8", dt(dy8), ptr(dy8), lddy, cout8, None, 0, ptr(wpd),
@@ -1227,6 +1242,21 @@ def _small_image(weight, bias, cin, cout, k, cache):
     if keep:
         cache_d[key] = (ver, img, weight)
     return img
+
+
+def _small_dgrad_image(weight, cout, cin_pad, cin_real, k, cache):
+    """Image of the input-gradient conv of a small-channel conv: input channels
+    = its cout, outputs = its (padded) cin, taps flipped.  Under a trainer's
+    cache a PackCache entry (DvSmallPackEntry mode 1, repacked per update);
+    else built here from the transposed weight."""
+    w = weight.detach()
+    if w.dtype != torch.float32 or not w.is_contiguous():
+        w = w.float().contiguous()
+    if cache and PACK.enabled and not PACK.static and w.data_ptr() == weight.data_ptr():
+        return PACK.small_entry(weight, w, None, cout, cin_pad, k, mode=1, wcin=cin_real)
+    wt = torch.zeros(cin_pad, cout, 1, k, k, dtype=torch.float32, device=w.device)
+    wt[:cin_real] = w.flip(-1, -2).transpose(0, 1)
+    return _small_image(wt, None, cout, cin_pad, k, False)
 
 
 def conv(x0, weight, bias=None, x1=None, res=None, sink=None, cache=True, algo_scale=1.0, gn=None,

@@ -166,10 +166,15 @@ int dv_conv_small_fwd(const void* x0, int ld0, int c0, const void* x1, int ld1, 
  * passes it to dv_conv_small_pack_batched (tables depend on the entries'
  * pointers and shapes only, so one upload serves every step).              */
 typedef struct {
-  const float* w;     /* f32 torch weight (cout, cin, 1, k, k) */
-  const float* bias;  /* f32 [cout] or NULL */
-  void* image;        /* dv_conv_small_image_elems bf16 elements */
+  const float* w;     /* f32 torch weight (cout_w, cin_w, 1, k, k) */
+  const float* bias;  /* f32 [cout] or NULL (mode 0 only) */
+  void* image;        /* dv_conv_small_image_elems(cin, cout, ksize) bf16 elements */
   int cin, cout, ksize;
+  /* 0: the conv's own image (cin = cin_w, cout = cout_w).  1: the image of its
+   * input gradient (dgrad as a conv of dY): input channels cin = cout_w, output
+   * channels cout >= wcin (rows >= wcin zero), taps flipped,
+   * image[ci][co][dy][dx] = w[co][ci][k-1-dy][k-1-dx]                        */
+  int mode, wcin;
 } DvSmallPackEntry;
 int dv_conv_small_pack_plan(const DvSmallPackEntry* entries, int n, void* table, long long* bytes,
                             long long* max_elems);
