@@ -105,6 +105,21 @@ struct ConvFwdArgs {
   // this pass reads channels [wc0, wc0 + 64) of each tap -- one source of a
   // dual-source conv run as two passes (conv_fwd_t)
   int wcin = 0, wc0 = 0;
+  // stripe kernel, W = 64: a GroupNorm (+ FiLM) + SiLU folded into the input
+  // (dv_conv_fwd_gn_in).  x0 holds the GroupNorm's input z; each staged window
+  // row becomes silu(A z + B) in LDS before the MFMAs read it, A / B per
+  // (clip, channel) from z's statistics (gi_sums: gi_R replicas, stride
+  // gi_rstride, [clip][64][2]) and gamma / beta / FiLM.  Null gi_sums: off.
+  const float* gi_sums = nullptr;
+  long long gi_rstride = 0, gi_P = 1;
+  int gi_R = 1;
+  float gi_eps = 0.f;
+  const float *gi_gamma = nullptr, *gi_beta = nullptr, *gi_ss = nullptr;
+  float *gi_mean = nullptr, *gi_rstd = nullptr;  // the GroupNorm's saved statistics
+  T* gi_y = nullptr;                              // silu(A z + B), stored for the wgrad
+  int gi_ldy = 0;
+  float* gi_zero = nullptr;                       // zeroed (the next GroupNorm's sums)
+  long long gi_zero_n = 0;
 };
 
 // GroupNorm statistics of a wave's tile, register-light: every lane holds
@@ -1827,13 +1842,17 @@ struct FsGeom {
 // (k % 4) * 16) from the lane's tap row dy base
 constexpr int fs_koff(int k) { return ((k >> 2) % 3) * FS_XP + (k & 3) * 32; }
 
-template <int W, int NRES, bool STATS>
+typedef float __attribute__((ext_vector_type(2))) gf2;
+
+template <int W, int NRES, bool STATS, bool GNIN = false>
 __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> p, int nstages,
                                                               int stages_per_block) {
   using G = FsGeom<W>;
   constexpr int WP = G::WP, SEG = G::SEG, PPR = G::PPR, ROWB = G::ROWB, R = G::R;
   constexpr int NP = G::NP, NPW = G::NPW, NP0 = G::NP0, NPW0 = G::NPW0;
-  __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
+  static_assert(!GNIN || (W == 64 && NRES == 0), "the folded GroupNorm input is built for W = 64, no residual");
+  // GNIN: the coefficient scratch (128 sums, 4 x 64 parameters, the A / B table) past the ring
+  __shared__ __attribute__((aligned(1024))) char smem[G::LDS + (GNIN ? 2048 : 0)];
   DV_STAMP_AT(0);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1847,6 +1866,125 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   const int m00 = sbeg * 128;
   const int fbase = (m00 / HW) * HW;                 // first pixel of the frame
   const int yq0 = (m00 - fbase) / W - 1;
+
+  // GNIN: this thread's window slot of every staged row (W = 64: a row's 64
+  // pixels x 8 16-B channel slots are the 512 threads): pixel gx, channels
+  // 8 gc .. 8 gc + 7 = GroupNorm group gc (64 channels, 8 groups).  The
+  // per-channel A / B are computed here, before any DMA is issued (plain loads
+  // + two barriers, ~1 round trip: no compiler-counted vector load among the
+  // hand-counted DMA waits below), into an LDS table [group][A 0..7, B 0..7]
+  // that fold_rows reads (registers would spill beside the statistics epilogue).
+  const int gx = tid >> 3, gc = tid & 7;
+  float* gi_tab = (float*)(smem + G::LDS) + 384;
+  if constexpr (GNIN) {
+    // the next GroupNorm's sums buffer, zeroed across the grid (stores older
+    // than every DMA: the prologue's waits cover them)
+    if (p.gi_zero) {
+      const long long nblk = (long long)gridDim.x * gridDim.y;
+      const long long per = ((p.gi_zero_n + nblk - 1) / nblk + 3) / 4 * 4;
+      const long long i0 = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * per;
+      for (long long i = i0 + tid * 4; i < i0 + per && i < p.gi_zero_n; i += 2048) {
+        if (i + 4 <= p.gi_zero_n) *(f32x4*)(p.gi_zero + i) = f32x4{0.f, 0.f, 0.f, 0.f};
+        else for (long long j = i; j < p.gi_zero_n; ++j) p.gi_zero[j] = 0.f;
+      }
+    }
+    float* cs = (float*)(smem + G::LDS);  // [64][2] clip totals, then gamma, beta, 1 + scale, shift
+    float* prm = cs + 128;
+    const long long b = m00 / p.gi_P;     // the workgroup's clip (stages never straddle one)
+    if (tid < 128) {
+      float s = 0.f;
+      for (int r = 0; r < p.gi_R; ++r) s += p.gi_sums[r * p.gi_rstride + b * 128 + tid];
+      cs[tid] = s;
+    } else if (tid < 192) {
+      const int c = tid - 128;
+      prm[c] = p.gi_gamma[c];
+      prm[64 + c] = p.gi_beta[c];
+      prm[128 + c] = p.gi_ss ? 1.f + p.gi_ss[b * 128 + c] : 1.f;
+      prm[192 + c] = p.gi_ss ? p.gi_ss[b * 128 + 64 + c] : 0.f;
+    }
+    __syncthreads();
+    if (tid < 64) {  // channel tid of group tid / 8
+      const int g = tid >> 3;
+      double d1 = 0.0, d2 = 0.0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        d1 += cs[2 * (8 * g + e)];
+        d2 += cs[2 * (8 * g + e) + 1];
+      }
+      const double n = (double)p.gi_P * 8;
+      const double m = d1 / n;
+      double var = d2 / n - m * m;
+      if (var < 0) var = 0;
+      const float mu = (float)m, rs = (float)(1.0 / sqrt(var + (double)p.gi_eps));
+      const float gm = prm[tid], bt = prm[64 + tid], sc = prm[128 + tid], sh = prm[192 + tid];
+      gi_tab[16 * g + (tid & 7)] = rs * gm * sc;
+      gi_tab[16 * g + 8 + (tid & 7)] = (bt - mu * rs * gm) * sc + sh;
+      // the clip's first workgroup of channel tile 0 saves the statistics
+      if (blockIdx.y == 0 && m00 % p.gi_P == 0 && (tid & 7) == 0) {
+        p.gi_mean[b * 8 + g] = mu;
+        p.gi_rstd[b * 8 + g] = rs;
+      }
+    }
+    __syncthreads();
+  }
+  const __amdgpu_buffer_rsrc_t yr =
+      dma_rsrc(GNIN ? (const void*)p.gi_y : nullptr, GNIN && p.gi_y ? (unsigned)(p.M * p.gi_ldy * 2) : 0u);
+  // GNIN: rows q0 .. q0 + NQ - 1 of the window ring -> silu(A z + B) in place
+  // (image rows outside the frame stay zero), each also stored to gi_y when
+  // the workgroup owns it (window rows 1 .. nst SEG: its output rows).  Every
+  // thread issues exactly NQ stores (a dropped one goes out of range), so the
+  // stage loop's hand-counted vmcnt waits can count them.
+  auto fold_rows = [&](auto nq, int q0) {
+    constexpr int NQ = decltype(nq)::value;
+    u32x4 v[NQ], kt[4];
+    unsigned la[NQ];
+    const unsigned ta = lds_addr(gi_tab + 16 * gc);
+    kt[0] = ds_read_b128_off<0>(ta);
+    kt[1] = ds_read_b128_off<16>(ta);
+    kt[2] = ds_read_b128_off<32>(ta);
+    kt[3] = ds_read_b128_off<48>(ta);
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      la[i] = lds_addr(smem + ((q0 + i) % R) * ROWB + (gx + 1) * FS_XP + gc * 16);
+      v[i] = ds_read_b128_off<0>(la[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lgkm_wait_tied<0>(kt[i]);
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) lgkm_wait_tied<0>(v[i]);
+    gf2 gi_A[4], gi_B[4];
+    {
+      const f32x4 a0 = __builtin_bit_cast(f32x4, kt[0]), a1 = __builtin_bit_cast(f32x4, kt[1]);
+      const f32x4 b0 = __builtin_bit_cast(f32x4, kt[2]), b1 = __builtin_bit_cast(f32x4, kt[3]);
+      gi_A[0] = gf2{a0[0], a0[1]}; gi_A[1] = gf2{a0[2], a0[3]};
+      gi_A[2] = gf2{a1[0], a1[1]}; gi_A[3] = gf2{a1[2], a1[3]};
+      gi_B[0] = gf2{b0[0], b0[1]}; gi_B[1] = gf2{b0[2], b0[3]};
+      gi_B[2] = gf2{b1[0], b1[1]}; gi_B[3] = gf2{b1[2], b1[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int q = q0 + i, y = yq0 + q;
+      const bool in = (unsigned)y < (unsigned)p.H;
+      float z[8];
+      Vec<bf16>::to_f(v[i], z);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        gf2 t = gf2{z[2 * j], z[2 * j + 1]} * gi_A[j] + gi_B[j];
+        const gf2 mm = t * -1.4426950408889634f;  // silu as the GroupNorm apply computes it
+        const gf2 d = 1.f + gf2{__builtin_amdgcn_exp2f(mm.x), __builtin_amdgcn_exp2f(mm.y)};
+        t *= gf2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+        o[2 * j] = (bf16)t.x;
+        o[2 * j + 1] = (bf16)t.y;
+      }
+      const u32x4 ov = in ? __builtin_bit_cast(u32x4, o) : u32x4{0u, 0u, 0u, 0u};
+      asm volatile("ds_write_b128 %0, %1" ::"v"(la[i]), "v"(ov) : "memory");
+      const bool own = in && q >= 1 && q <= nst * SEG;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          ov, yr, own ? (unsigned)(((fbase + y * W + gx) * p.gi_ldy + gc * 8) * 2) : DMA_OOB, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
 
   // this lane's 16-B slot of each of the wave's pieces: a column byte offset
   // within an image row (or -1: halo / pad slot) and the row within the
@@ -1948,6 +2086,15 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   // counts below hold unchanged.
   if (G::LATE && nst > 2) issue(2);
   asm volatile("" ::: "memory");  // (stage 0's residual loads stay younger than D2)
+  // GNIN: stage 0's whole window (SEG + 2 rows, landed) transformed (Y0)
+  constexpr int Y0 = GNIN ? SEG + 2 : 0, YS = GNIN ? SEG : 0;  // stores per thread: prologue / stage
+  if constexpr (GNIN) {
+    if (nst > 0) {  // (two rows at a time: four spill beside the statistics accumulators)
+      fold_rows(std::integral_constant<int, 2>{}, 0);
+      fold_rows(std::integral_constant<int, SEG>{}, 2);
+    }
+    asm volatile("s_barrier" ::: "memory");
+  }
   DV_STAMP_AT(1);
 
   const int r = lane & 31, h = lane >> 5;
@@ -1983,6 +2130,12 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
         for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
       }
     }
+    // GNIN: this stage's SEG new rows (landed at the last barrier) transformed
+    // before any wave reads them (Y(st))
+    if constexpr (GNIN) if (st > 0) {
+      fold_rows(std::integral_constant<int, SEG>{}, st * SEG + 2);
+      asm volatile("s_barrier" ::: "memory");
+    }
     // the lane's three tap rows dy = 0..2: window rows st SEG + orow + dy
     const int q0 = st * SEG + orow;
     const unsigned xa0 = lds_addr(smem + (q0 % R) * ROWB + loff);
@@ -1993,7 +2146,9 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     // k / 4, 16 channels at (k % 4) * 16).  The reads are inline asm with
     // hand-counted lgkmcnt: beside the LDS-DMA hipcc's waitcnt pass treats
     // the LGKM queue as out of order and drains it to 0 every few reads.
-    constexpr int FSD = NRES > 1 ? 6 : 8;  // (two residuals: 8 VGPRs of read-ahead fewer, no spill)
+    // (fewer VGPRs of read-ahead beside two residuals, a folded input, a
+    // residual with the statistics epilogue: no spill)
+    constexpr int FSD = (GNIN || NRES > 0) && STATS ? 4 : (NRES > 1 || GNIN) ? 6 : 8;
     u32x4 bq[FSD];
     static_for<0, FSD>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
@@ -2080,21 +2235,26 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     // (A statistics epilogue's clip-boundary atomics only add younger ops:
     // the wait then covers more, never less.)  Every window read of this
     // stage was waited for by the last MFMA: no lgkmcnt drain.
+    // GNIN adds the transformed rows' stores: Y0 after D2 (prologue), Y(s)
+    // at the start of stage s >= 1, so younger than D(st+1) are also
+    //   st = 0: Y0;   st = 1: Y0, Y1;   st >= 2: Y(st-1), Y(st).
     if (st + 1 < nst) {
       constexpr int NR = 4 * NRES;
+      constexpr int A0 = NR + 4 + Y0, A1 = 2 * NR + 8 + Y0 + YS, A2 = 2 * NR + 12 + 2 * YS;
+      static_assert(A1 + 2 * NPW <= 63 && A2 + 2 * NPW <= 63, "stripe vmcnt immediate out of range");
       const int nd = (st + 2 < nst) + (st + 3 < nst);  // DMA stages issued after D(st+1)
       if (st == 0) {
-        if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NR + 4 + 2 * NPW) : "memory");
-        else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NR + 4 + NPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NR + 4) : "memory");
+        if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A0 + 2 * NPW) : "memory");
+        else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A0 + NPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A0) : "memory");
       } else if (st == 1) {
-        if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 8 + 2 * NPW) : "memory");
-        else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 8 + NPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 8) : "memory");
+        if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A1 + 2 * NPW) : "memory");
+        else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A1 + NPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A1) : "memory");
       } else {
-        if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 12 + 2 * NPW) : "memory");
-        else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 12 + NPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NR + 12) : "memory");
+        if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A2 + 2 * NPW) : "memory");
+        else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A2 + NPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A2) : "memory");
       }
     }
     if (st == 1) DV_STAMP_AT(6);
@@ -2133,6 +2293,11 @@ int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
   dim3 grid(bx, ct);
   const int nres = a.res2 ? 2 : a.res ? 1 : 0;
   const bool stats = a.gn_sums != nullptr;
+  if (a.gi_sums) {  // (conv_fwd_gn_in checked W = 64, no residual)
+    if (stats) conv_fwd_stripe_kernel<64, 0, true, true><<<grid, 512, 0, st>>>(a, nstages, sps);
+    else conv_fwd_stripe_kernel<64, 0, false, true><<<grid, 512, 0, st>>>(a, nstages, sps);
+    return check_launch("conv_fwd_stripe_gn_in");
+  }
 #define DV_FS(WW, RR) (stats ? conv_fwd_stripe_kernel<WW, RR, true><<<grid, 512, 0, st>>>(a, nstages, sps) \
                              : conv_fwd_stripe_kernel<WW, RR, false><<<grid, 512, 0, st>>>(a, nstages, sps))
   // (residuals come from dgrads only: no statistics epilogue beside them,
@@ -2140,7 +2305,10 @@ int launch_fwd_stripe(const ConvFwdArgs<bf16>& a, hipStream_t st) {
 #define DV_FSR(WW) (nres == 2 ? (void)conv_fwd_stripe_kernel<WW, 2, false><<<grid, 512, 0, st>>>(a, nstages, sps) \
                     : nres == 1 ? (void)conv_fwd_stripe_kernel<WW, 1, false><<<grid, 512, 0, st>>>(a, nstages, sps) \
                                 : DV_FS(WW, 0))
-  if (a.W == 64) DV_FSR(64);
+  // W = 64 also has the residual + statistics pairing: the second pass of a
+  // dual-source conv whose GroupNorm reads its output (conv_fwd_t)
+  if (a.W == 64 && nres == 1 && stats) conv_fwd_stripe_kernel<64, 1, true><<<grid, 512, 0, st>>>(a, nstages, sps);
+  else if (a.W == 64) DV_FSR(64);
   else if (a.W == 128) DV_FSR(128);
   else DV_FSR(32);
 #undef DV_FSR
@@ -2807,17 +2975,20 @@ int conv_fwd_t(const void* x0, int ld0, int c0, const void* x1, int ld1, const v
     // source -- pass 2 adds onto pass 1's output in its residual epilogue
     // (in place: each lane reads its pixel's y before it stores it).  Measured
     // against the glds implicit GEMM it replaces: DESIGN.md §3.
-    if (x1 && c0 == 64 && cin == 128 && act == DV_ACT_NONE && !gn_sums && !res2 && ld1 % 8 == 0 &&
+    if (x1 && c0 == 64 && cin == 128 && act == DV_ACT_NONE && (!gn_sums || (wd == 64 && gn_P % 128 == 0)) &&
+        !res2 && ld1 % 8 == 0 &&
         fwd_stripe_ok(a.M, h, wd, 64, false, cout, ks, ld0) && a.M * ld1 * 2 < (long long)DMA_OOB &&
         (ldy & 3) == 0 && (res == nullptr || (ldres & 3) == 0)) {
       ConvFwdArgs<T> p1 = a;
       p1.cin = 64; p1.c0 = 64; p1.x1 = p1.x0; p1.ld1 = p1.ld0; p1.K = ks * ks * 64;
       p1.wcin = 128; p1.wc0 = 0;
+      set_gn(p1, nullptr, 0, 0);  // statistics of the final sum: pass 2's epilogue
       const int rc = launch_fwd_stripe(p1, st);
       if (rc != DV_OK) return rc;
       ConvFwdArgs<T> p2 = p1;
       p2.x0 = a.x1; p2.ld0 = a.ld1; p2.x1 = a.x1; p2.ld1 = a.ld1; p2.wc0 = 64;
       p2.bias = nullptr; p2.res = a.y; p2.ldres = ldy;
+      set_gn(p2, gn_sums, gn_P, gn_R);
       return launch_fwd_stripe(p2, st);
     }
     // the stripe kernel flushes statistics per 128-pixel stage: clips must
@@ -3693,6 +3864,32 @@ extern "C" int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const voi
     return conv_fwd_t<bf16>(x0, ld0, c0, x1, ld1, wpack, bias, res, ldres, res2, ldres2, y, ldy, nf,
                             h, w, cin, cout, ksize, act, gn_sums, gn_P, gn_R, st);
   DV_REQUIRE(false, "unknown dtype");
+}
+
+extern "C" int dv_conv_fwd_gn_in(const DvGnIn* g, const void* z, int ldz, const void* wpack,
+                                 const float* bias, void* y, int ldy, int nf, int h, int w, int cin,
+                                 int cout, float* gn_sums, long long gn_P, int gn_R, void* stream) {
+  DV_REQUIRE(g && z && wpack && y && g->sums && g->gamma && g->beta && g->mean && g->rstd, "null pointer");
+  DV_REQUIRE(g->R >= 1 && g->P > 0 && ((long long)nf * h * w) % g->P == 0, "GroupNorm: whole clips of P pixels");
+  DV_REQUIRE(!gn_sums || (gn_P > 0 && ((long long)nf * h * w) % gn_P == 0 && gn_R >= 1),
+             "GroupNorm statistics: the pixels must be whole clips of gn_P");
+  DV_REQUIRE(ldy >= cout && ldz >= cin && (!g->y || g->ldy >= cin) && g->zero_n >= 0, "bad stride");
+  const long long M = (long long)nf * h * w;
+  // the one shape the folded stripe kernel is built for: 64 -> 64k channels at
+  // W = 64, 8 groups of 8 channels, clips of whole 128-pixel stages
+  if (!(cin == 64 && g->groups == 8 && w == 64 && fwd_stripe_ok(M, h, w, 64, false, cout, 3, ldz) &&
+        (ldy & 3) == 0 && g->P % 128 == 0 && (!gn_sums || gn_P % 128 == 0) &&
+        (!g->y || (g->ldy % 8 == 0 && M * g->ldy * 2 < (long long)DMA_OOB))))
+    return DV_ERR_UNSUPPORTED;
+  ConvFwdArgs<bf16> a;
+  a.x0 = a.x1 = (const bf16*)z; a.ld0 = a.ld1 = ldz; a.c0 = cin; a.w = (const bf16*)wpack; a.bias = bias;
+  a.res = nullptr; a.ldres = 0; a.y = (bf16*)y; a.ldy = ldy; a.H = h; a.W = w; a.cin = cin; a.cout = cout;
+  a.ks = 3; a.act = DV_ACT_NONE; a.M = M; a.K = 9 * cin;
+  set_gn(a, gn_sums, gn_P, gn_R);
+  a.gi_sums = g->sums; a.gi_rstride = g->rstride; a.gi_P = g->P; a.gi_R = g->R; a.gi_eps = g->eps;
+  a.gi_gamma = g->gamma; a.gi_beta = g->beta; a.gi_ss = g->ss; a.gi_mean = g->mean; a.gi_rstd = g->rstd;
+  a.gi_y = (bf16*)g->y; a.gi_ldy = g->y ? g->ldy : 0; a.gi_zero = g->zero; a.gi_zero_n = g->zero ? g->zero_n : 0;
+  return launch_fwd_stripe(a, (hipStream_t)stream);
 }
 
 extern "C" int dv_conv_fwd8(int dtype, const void* x0, int ld0, int c0, const void* x1, int ld1,

@@ -26,6 +26,7 @@ _F = ctypes.c_float
 _SIGS = {
     "dv_abi_version": [],
     "dv_zero_f32": [_P, _L, _P],
+    "dv_conv_fwd_gn_in": [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _L, _I, _P],
     "dv_conv_fwd": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
                     _I, _P, _L, _I, _P],
     "dv_conv_fwd8": [_I, _P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I,

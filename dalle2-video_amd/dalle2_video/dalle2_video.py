@@ -406,16 +406,18 @@ class Block3D(nn.Module):
         self.act = nn.SiLU()
 
     def forward_cl(self, x0, nb, x1=None, scale_shift=None, res=None, sink=None, res_sink=None,
-                   skip_in=None, skip_out=None):
+                   skip_in=None, skip_out=None, defer_norm=False):
         # the conv's epilogue accumulates the GroupNorm statistics of z, so the
-        # norm is a single apply pass over z
+        # norm is a single apply pass over z -- or none (defer_norm: the output
+        # feeds only the next Block3D's conv, which applies the norm while it
+        # stages z, ops.group_norm_act(defer=True))
         nf, h, w = x0.shape[:3]
         st = ops.gn_stats(nb, self.project.out_channels, (nf // nb) * h * w, x0.device)
         z = ops.conv(x0, self.project.weight, self.project.bias, x1=x1, sink=sink, gn=st,
                      skip_in=skip_in, skip_out=skip_out)
         return ops.group_norm_act(z, self.norm.weight, self.norm.bias, nb, self.norm.num_groups,
                                   self.norm.eps, scale_shift=scale_shift, res=res, act=ACT_SILU,
-                                  stats=st, res_sink=res_sink)
+                                  stats=st, res_sink=res_sink, defer=defer_norm)
 
     def forward(self, x, scale_shift=None):
         b, c, t = x.shape[:3]
@@ -470,8 +472,9 @@ class ResnetBlock3D(nn.Module):
                            skip_out=skip_out)
         # block1's conv is x0's gradient owner either way: the second reader of
         # the shared buffer (identity) or the first (res_conv), so it takes skip_in
+        # block1's output feeds block2's conv alone when there is no cross-attention
         h = self.block1.forward_cl(x0, nb, x1=x1, scale_shift=ss, sink=sink, skip_in=skip_in,
-                                   skip_out=skip_out)
+                                   skip_out=skip_out, defer_norm=self.cross_attn is None and ops.GN_FOLD)
         if exists(self.cross_attn):
             assert exists(cond)
             h = self.cross_attn.forward_cl(h, cond, nb, kv=kv, fold=fold)

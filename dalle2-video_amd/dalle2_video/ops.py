@@ -126,8 +126,8 @@ def conv_fwd_name(dtype_name, m, cin, c0, cout, maxld, ks=1, h=0, w=0, gn_P=0, n
             and w in (32, 64, 128) and h % (128 // w) == 0 and m % 128 == 0 and m * maxld < (1 << 31)
             and gn_P % 128 == 0):
         return f"conv_fwd_stripe_kernel<{w}>"
-    if (dtype_name == "bf16" and ks == 3 and cin == 128 and c0 == 64 and cout % 64 == 0 and gn_P == 0
-            and not nres2 and w in (32, 64, 128) and h % (128 // w) == 0 and m % 128 == 0
+    if (dtype_name == "bf16" and ks == 3 and cin == 128 and c0 == 64 and cout % 64 == 0
+            and (gn_P == 0 or (w == 64 and gn_P % 128 == 0)) and not nres2 and w in (32, 64, 128) and h % (128 // w) == 0 and m % 128 == 0
             and m * maxld < (1 << 31)):
         return f"conv_fwd_stripe_kernel<{w}>"  # dual source: two stripe passes (conv_fwd_t)
     if (dtype_name == "bf16" and ks == 3 and cin % 32 == 0 and c0 % 32 == 0 and cout % 64 == 0
@@ -450,22 +450,27 @@ def backward_mark(x):
 
 
 class _GnSums:
-    """The two alternating GroupNorm sums buffers of a device (dv_gn_fwd /
-    dv_gn_bwd contract): call i accumulates into buffer i % 2, which is zero on
-    entry, and zeroes buffer (i + 1) % 2 for call i + 1."""
+    """The rotating GroupNorm sums buffers of a device (dv_gn_fwd / dv_gn_bwd
+    contract: `sums` zero on entry, `next` zeroed by the call): call i
+    accumulates into buffer i % 3 and zeroes buffer (i + 2) % 3 = the previous
+    call's sums, so buffer i % 3 was zeroed by call i - 2.  Three buffers, not
+    two, so that a GroupNorm whose apply is folded into the next conv
+    (group_norm_act(defer=...)) can have that conv read its sums while the
+    next call already accumulates into its own: the folded conv takes over the
+    deferred call's zeroing (dv_conv_fwd_gn_in's `zero`)."""
 
     # floats per buffer: up to 8 replicas of nb * C * 2 sums (<= 32768 floats
     # each) and, for the single-launch GroupNorm, nb arrival counters at the end
     CAP = 1 << 16
 
     def __init__(self, device):
-        self.bufs = torch.zeros(2, self.CAP, dtype=torch.float32, device=device)
+        self.bufs = torch.zeros(3, self.CAP, dtype=torch.float32, device=device)
         self.i = 0
 
     def take(self, n):
         if n > self.CAP // 2:
             raise _lib.DVError(f"GroupNorm: nb*C*2 = {n} exceeds the sums buffer ({self.CAP})")
-        cur, nxt = self.bufs[self.i % 2], self.bufs[(self.i + 1) % 2]
+        cur, nxt = self.bufs[self.i % 3], self.bufs[(self.i + 2) % 3]
         self.i += 1
         return cur, nxt
 
@@ -961,6 +966,14 @@ class ConvFn(torch.autograd.Function):
         cout, cin_real = weight.shape[0], weight.shape[1]
         if cin_real > cin:
             raise _lib.DVError(f"conv: weight expects {cin_real} input channels, got {cin}")
+        gi = getattr(x0, "_dv_gn_in", None)
+        if gi is not None:  # x0 is a deferred GroupNorm output (group_norm_act(defer=True))
+            x0._dv_gn_in = None
+            if (x1 is None and res is None and ksize == 3 and cin_real == cin and cl_ld(x0) == c0
+                    and gn_in_ok(nf, h, w, c0, gi["groups"], x0.dtype, gi["nb"], cout)):
+                return ConvFn._forward_gn_in(ctx, gi, x0, weight, bias, sink, cache, algo_scale, gn,
+                                             skip_in, skip_out)
+            _gn_in_materialize(gi, x0)
         if mx8_ok(x0, x1, weight, res, ksize, h, w, nf):
             if gn is not None:
                 gn.used = False  # the GroupNorm reduces z itself
@@ -1012,15 +1025,51 @@ class ConvFn(torch.autograd.Function):
                     lambda: call("dv_conv_fwd", dt(x0), ptr(x0), ld0, c0, ptr(x1), ld1, ptr(wp), ptr(b),
                                  ptr(res), ldr, None, 0, ptr(y), cout, nf, h, w, cin, cout, ksize,
                                  ACT_NONE, gs, gP, gR, stream()), shape)
+        ConvFn._save(ctx, x0, x1, weight, bias, ksize, c0, c1, res is not None, sink, cache, algo_scale,
+                     skip_in, skip_out)
+        return y
+
+    @staticmethod
+    def _save(ctx, x0, x1, weight, bias, ksize, c0, c1, has_res, sink, cache, algo_scale, skip_in, skip_out):
         ctx.save_for_backward(x0, x1, weight)
         ctx.params = (weight, bias)
-        ctx.meta = (ksize, c0, c1, bias is not None, res is not None)
+        ctx.meta = (ksize, c0, c1, bias is not None, has_res)
         ctx.sink = sink
         ctx.cache = cache
         ctx.algo_scale = algo_scale
         if skip_in is not None and x1 is None:
             skip_in.arm(ctx.needs_input_grad[0])
         ctx.skip_in, ctx.skip_out = skip_in, skip_out
+
+    @staticmethod
+    def _forward_gn_in(ctx, gi, x0, weight, bias, sink, cache, algo_scale, gn, skip_in, skip_out):
+        """conv(silu(GroupNorm(z) (+FiLM))) with the GroupNorm applied while the
+        stripe kernel stages z (dv_conv_fwd_gn_in): x0 is the deferred GroupNorm
+        output, written by this launch only when the weight gradient will read it."""
+        z, st = gi["z"], gi["stats"]
+        nf, h, w, cin = x0.shape
+        cout = weight.shape[0]
+        m = nf * h * w
+        y = torch.empty(nf, h, w, cout, dtype=x0.dtype, device=x0.device)
+        b = None if bias is None else bias.detach().float().contiguous()
+        wp = pack_conv_weight(weight, x0.dtype, cin, 0, cache)
+        d = DvGnIn()
+        d.sums, d.rstride, d.R = st.cur.data_ptr(), gi["nb"] * cin * 2, st.R
+        d.P, d.groups, d.eps = gi["P"], gi["groups"], float(gi["eps"])
+        d.gamma, d.beta = gi["g"].data_ptr(), gi["b"].data_ptr()
+        d.ss = None if gi["s"] is None else gi["s"].data_ptr()
+        d.mean, d.rstd = gi["mean"].data_ptr(), gi["rstd"].data_ptr()
+        d.y = x0.data_ptr() if ctx.needs_input_grad[2] else None  # the wgrad reads it
+        d.ldy = cin
+        d.zero, d.zero_n = st.nxt.data_ptr(), st.nxt.numel()  # the deferred call's zeroing duty
+        if gn is not None:
+            gn.used = True
+        gs, gP, gR = (ptr(gn.cur), gn.P, gn.R) if gn is not None else (None, 0, 0)
+        _launch("conv_fwd_stripe_kernel<64,gn_in>", 2.0 * m * cout * cin * 9 * algo_scale,
+                x0.element_size() * m * (cin * (2 if d.y else 1) + cout),
+                lambda: call("dv_conv_fwd_gn_in", ctypes.byref(d), ptr(z), cl_ld(z), ptr(wp), ptr(b), ptr(y),
+                             cout, nf, h, w, cin, cout, gs, gP, gR, stream()), ("fwd", m, cout, cin * 9))
+        ConvFn._save(ctx, x0, None, weight, bias, 3, cin, 0, False, sink, cache, algo_scale, skip_in, skip_out)
         return y
 
     @staticmethod
@@ -1438,10 +1487,56 @@ def _gn_forward(z, gamma, beta, ss, res, nb, groups, eps, act, stats, mx8=False)
     return y, g, b, s, mean, rstd
 
 
+class DvGnIn(ctypes.Structure):
+    """Mirror of DvGnIn (include/dv_hip.h): a GroupNorm folded into the conv reading it."""
+    _fields_ = [("sums", ctypes.c_void_p), ("rstride", ctypes.c_longlong), ("R", ctypes.c_int),
+                ("P", ctypes.c_longlong), ("groups", ctypes.c_int), ("eps", ctypes.c_float),
+                ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("ss", ctypes.c_void_p),
+                ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p), ("y", ctypes.c_void_p),
+                ("ldy", ctypes.c_int), ("zero", ctypes.c_void_p), ("zero_n", ctypes.c_longlong)]
+
+
+# Block3D -> Block3D GroupNorm folded into the second conv's input staging
+# (tests switch it off to compare against the two-pass form)
+GN_FOLD = True
+
+
+def gn_in_ok(nf, h, w, c, groups, dtype, nb, cout):
+    """The GroupNorm (+FiLM) + SiLU output a 3x3 conv can fold into its input
+    staging (dv_conv_fwd_gn_in): bf16, 64 channels in 8 groups, 64-pixel rows,
+    whole 128-pixel stages per clip (mirror of the C-ABI's shape check)."""
+    m = nf * h * w
+    return (dtype == torch.bfloat16 and c == 64 and groups == 8 and w == 64 and h % 2 == 0
+            and m % 128 == 0 and ((nf // nb) * h * w) % 128 == 0 and cout % 64 == 0
+            and m * c * 2 < (1 << 31) and not _Mx8State.active)
+
+
+def _gn_in_materialize(gi, y):
+    """The deferred GroupNorm apply, run on its own (the conv reading y did not
+    take the folded form): one dv_gn_fwd apply over the producing conv's sums."""
+    z, st = gi["z"], gi["stats"]
+    nf, h, w, c = z.shape
+    call("dv_gn_fwd", dt(z), ptr(z), cl_ld(z), ptr(y), c, None, 0, gi["nb"], gi["P"], c, gi["groups"],
+         ctypes_float(gi["eps"]), ptr(gi["g"]), ptr(gi["b"]), ptr(gi["s"]), gi["act"], ptr(gi["mean"]),
+         ptr(gi["rstd"]), ptr(st.cur), ptr(st.nxt), st.nxt.numel(), st.R, stream())
+
+
 class GroupNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, z, gamma, beta, ss, res, nb, groups, eps, act, stats=None, res_sink=None):
-        y, g, b, s, mean, rstd = _gn_forward(z, gamma, beta, ss, res, nb, groups, eps, act, stats)
+    def forward(ctx, z, gamma, beta, ss, res, nb, groups, eps, act, stats=None, res_sink=None, defer=None):
+        if defer is not None:
+            # y is produced by the 3x3 conv that reads it (ConvFn, dv_conv_fwd_gn_in),
+            # which also fills mean / rstd; `defer` is attached to y by group_norm_act
+            nf, h, w, c = z.shape
+            y = torch.empty(nf, h, w, c, dtype=z.dtype, device=z.device)
+            mean = torch.empty(nb * groups, dtype=torch.float32, device=z.device)
+            rstd = torch.empty_like(mean)
+            g, b = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
+            s = None if ss is None else ss.detach().float().contiguous()
+            defer.update(z=z, stats=stats, g=g, b=b, s=s, mean=mean, rstd=rstd, nb=nb, groups=groups,
+                         eps=eps, act=act, P=(nf // nb) * h * w)
+        else:
+            y, g, b, s, mean, rstd = _gn_forward(z, gamma, beta, ss, res, nb, groups, eps, act, stats)
         ctx.save_for_backward(z, g, b, s, mean, rstd)
         ctx.params = (gamma, beta)
         ctx.meta = (nb, groups, act, ss is not None, res is not None)
@@ -1480,7 +1575,7 @@ class GroupNormActFn(torch.autograd.Function):
             # epilogue (GradSink) instead of autograd adding two tensors
             ctx.res_sink.dx = dy
             dres = None
-        return dz, dg, db, dss, dres, None, None, None, None, None, None
+        return dz, dg, db, dss, dres, None, None, None, None, None, None, None
 
 
 def ctypes_float(v):
@@ -1489,7 +1584,7 @@ def ctypes_float(v):
 
 
 def group_norm_act(z, gamma, beta, nb, groups=8, eps=1e-5, scale_shift=None, res=None,
-                   act=_lib.ACT_SILU, stats=None, res_sink=None):
+                   act=_lib.ACT_SILU, stats=None, res_sink=None, defer=False):
     """stats: the GnStats z's conv filled (one apply launch) or None (reduce + apply).
     res_sink: a GradSink shared with the conv that also reads `res` (the
     residual's gradient is handed to it instead of returned to autograd).
@@ -1500,6 +1595,14 @@ def group_norm_act(z, gamma, beta, nb, groups=8, eps=1e-5, scale_shift=None, res
         nf, h, w, c = z.shape
         if c % 64 == 0 and w <= _MX8_MAX_W and _mx8_geom(nf, h, w):
             return _gn_forward(z, gamma, beta, scale_shift, res, nb, groups, eps, act, stats, mx8=True)[0]
+    if (defer and res is None and act == _lib.ACT_SILU and stats is not None and stats.used
+            and gn_in_ok(*z.shape, groups, z.dtype, nb, 64)):
+        # the apply folds into the next 3x3 conv's input staging (Block3D ->
+        # Block3D, dalle2_video.py:107-133 then :107): y is written by that conv
+        info = {}
+        y = GroupNormActFn.apply(z, gamma, beta, scale_shift, res, nb, groups, eps, act, stats, res_sink, info)
+        y._dv_gn_in = info
+        return y
     return GroupNormActFn.apply(z, gamma, beta, scale_shift, res, nb, groups, eps, act, stats, res_sink)
 
 

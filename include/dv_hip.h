@@ -63,6 +63,40 @@ int dv_conv_fwd(int dtype, const void* x0, int ld0, int c0, const void* x1, int 
                 int cout, int ksize, int act, float* gn_sums, long long gn_P, int gn_R,
                 void* stream);
 
+/* 3x3 conv of a GroupNorm + FiLM + SiLU output that is never produced by its
+ * own pass (Block3D -> the next Block3D's project, dalle2_video.py:107-133):
+ * z is the GroupNorm's INPUT; the conv stages y = silu(A z + B) into LDS,
+ * A = rstd*gamma*(1+scale), B = (beta - mean*rstd*gamma)*(1+scale) + shift,
+ * mean / rstd per (clip, group) from z's statistics `sums` (R replicas,
+ * stride rstride, [clip][C][2], as dv_conv_fwd's statistics epilogue leaves
+ * them).  Writes mean / rstd ([clip][groups], the GroupNorm's saved
+ * statistics), y itself when y != NULL (for the conv's weight gradient), and
+ * zeroes zero[0, zero_n) (the GroupNorm call's duty towards the next call's
+ * sums, dv_gn_fwd's `next`).  Output / statistics as dv_conv_fwd (bf16, no
+ * residual, act none).  Built for cin = 64, 8 groups, w = 64, cout % 64 == 0,
+ * clips of whole 128-pixel stages; DV_ERR_UNSUPPORTED otherwise (run
+ * dv_gn_fwd + dv_conv_fwd instead).                                        */
+typedef struct {
+  const float* sums;
+  long long rstride;
+  int R;
+  long long P;        /* pixels per clip */
+  int groups;
+  float eps;
+  const float* gamma; /* [C] */
+  const float* beta;  /* [C] */
+  const float* ss;    /* [clips][2C] (scale, shift) or NULL */
+  float* mean;        /* [clips][groups], written */
+  float* rstd;
+  void* y;            /* [M][ldy] bf16, written, or NULL */
+  int ldy;
+  float* zero;        /* zeroed, or NULL */
+  long long zero_n;
+} DvGnIn;
+int dv_conv_fwd_gn_in(const DvGnIn* g, const void* z, int ldz, const void* wpack,
+                      const float* bias, void* y, int ldy, int nf, int h, int w, int cin,
+                      int cout, float* gn_sums, long long gn_P, int gn_R, void* stream);
+
 /* Weight (and fused bias) gradient of dv_conv_fwd, written in torch layout:
  * dw (cout_real, cin_real, 1, k, k) (+)= sum_p dY[p][co] X[p + tap][ci]
  * (accumulate_w), db[cout_real] (+)= sum_p dY[p][co] (accumulate_b; db may

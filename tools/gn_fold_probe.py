@@ -1,0 +1,91 @@
+"""Per-call device time at the Cfg2 64^2 shape (bf16, 4 clips x 16 frames, 64
+channels): the 3x3 stripe conv with its statistics epilogue, the GroupNorm
+apply it replaces when folded (dv_gn_fwd over the conv's sums), and the
+folded conv (dv_conv_fwd_gn_in, with and without storing y).  Each as N calls
+replayed from one HIP graph.
+
+  python tools/gn_fold_probe.py
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dalle2-video_amd"))
+import torch  # noqa: E402
+
+from dalle2_video import _lib, ops  # noqa: E402
+
+N = 8
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(N):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(5):
+        g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / (5 * N) * 1e3
+
+
+def main():
+    torch.manual_seed(0)
+    nb, T, H, C = 4, 16, 64, 64
+    nf, P = nb * T, T * H * H
+    dev = "cuda"
+    z = torch.randn(nf, H, H, C, device=dev).bfloat16()
+    y = torch.empty_like(z)
+    out = torch.empty_like(z)
+    w = torch.randn(C, C, 1, 3, 3, device=dev) * 0.05
+    wp = ops.pack_conv_weight(w, torch.bfloat16, C, 0, False)
+    bias = torch.zeros(C, device=dev)
+    R = 8
+    sums = torch.zeros(3, 1 << 16, device=dev)
+    # plausible statistics in replica 0 (sum, sum of squares per clip / channel)
+    sums[0, :nb * C * 2].view(nb, C, 2)[..., 0] = 0.0
+    sums[0, :nb * C * 2].view(nb, C, 2)[..., 1] = float(P)
+    gamma, beta = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+    ss = 0.1 * torch.randn(nb, 2 * C, device=dev)
+    mean = torch.empty(nb * 8, device=dev)
+    rstd = torch.empty_like(mean)
+    st = _lib.stream
+
+    def conv_stats():
+        _lib.call("dv_conv_fwd", _lib.dt(z), _lib.ptr(z), C, C, None, 0, _lib.ptr(wp), _lib.ptr(bias), None, 0,
+                  None, 0, _lib.ptr(out), C, nf, H, H, C, C, 3, _lib.ACT_NONE, _lib.ptr(sums[1]), P, R, st())
+
+    def apply():
+        _lib.call("dv_gn_fwd", _lib.dt(z), _lib.ptr(z), C, _lib.ptr(y), C, None, 0, nb, P, C, 8,
+                  ops.ctypes_float(1e-5), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(ss), _lib.ACT_SILU,
+                  _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(sums[0]), _lib.ptr(sums[2]), sums.shape[1], R, st())
+
+    def fold(store):
+        d = ops.DvGnIn()
+        d.sums, d.rstride, d.R, d.P, d.groups, d.eps = sums[0].data_ptr(), nb * C * 2, R, P, 8, 1e-5
+        d.gamma, d.beta, d.ss, d.mean, d.rstd = (gamma.data_ptr(), beta.data_ptr(), ss.data_ptr(),
+                                                 mean.data_ptr(), rstd.data_ptr())
+        d.y, d.ldy = (y.data_ptr() if store else None), C
+        d.zero, d.zero_n = sums[2].data_ptr(), sums.shape[1]
+        _lib.call("dv_conv_fwd_gn_in", ctypes.byref(d), _lib.ptr(z), C, _lib.ptr(wp), _lib.ptr(bias),
+                  _lib.ptr(out), C, nf, H, H, C, C, _lib.ptr(sums[1]), P, R, st())
+
+    t_conv = timed(conv_stats)
+    t_apply = timed(apply)
+    t_fold = timed(lambda: fold(True))
+    t_fold_ns = timed(lambda: fold(False))
+    print(f"64^2 x 64, 4 clips x 16 frames (us per call): conv+stats {t_conv:6.1f}  gn apply {t_apply:6.1f}  "
+          f"sum {t_conv + t_apply:6.1f}  |  folded conv (y stored) {t_fold:6.1f}  (y not stored) {t_fold_ns:6.1f}",
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
