@@ -1843,6 +1843,9 @@ struct FsGeom {
 constexpr int fs_koff(int k) { return ((k >> 2) % 3) * FS_XP + (k & 3) * 32; }
 
 typedef float __attribute__((ext_vector_type(2))) gf2;
+#ifndef FS_TSTEP
+#define FS_TSTEP 4
+#endif
 
 template <int W, int NRES, bool STATS, bool GNIN = false>
 __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> p, int nstages,
@@ -1851,8 +1854,8 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   constexpr int WP = G::WP, SEG = G::SEG, PPR = G::PPR, ROWB = G::ROWB, R = G::R;
   constexpr int NP = G::NP, NPW = G::NPW, NP0 = G::NP0, NPW0 = G::NPW0;
   static_assert(!GNIN || (W == 64 && NRES == 0), "the folded GroupNorm input is built for W = 64, no residual");
-  // GNIN: the coefficient scratch (128 sums, 4 x 64 parameters, the A / B table) past the ring
-  __shared__ __attribute__((aligned(1024))) char smem[G::LDS + (GNIN ? 2048 : 0)];
+  // GNIN: the coefficient scratch (128 sums, 4 x 64 parameters, the A / B table, 64 biases) past the ring
+  __shared__ __attribute__((aligned(1024))) char smem[G::LDS + (GNIN ? 2304 : 0)];
   DV_STAMP_AT(0);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1876,6 +1879,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   // that fold_rows reads (registers would spill beside the statistics epilogue).
   const int gx = tid >> 3, gc = tid & 7;
   float* gi_tab = (float*)(smem + G::LDS) + 384;
+  float* gi_bias = gi_tab + 128;  // the workgroup's 64 output channels' bias
   if constexpr (GNIN) {
     // the next GroupNorm's sums buffer, zeroed across the grid (stores older
     // than every DMA: the prologue's waits cover them)
@@ -1891,11 +1895,18 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     float* cs = (float*)(smem + G::LDS);  // [64][2] clip totals, then gamma, beta, 1 + scale, shift
     float* prm = cs + 128;
     const long long b = m00 / p.gi_P;     // the workgroup's clip (stages never straddle one)
-    if (tid < 128) {
+    if (tid < 128) {  // all replicas in flight at once (a runtime-bound loop waited per load)
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = p.gi_sums[min(r, p.gi_R - 1) * p.gi_rstride + b * 128 + tid];
       float s = 0.f;
-      for (int r = 0; r < p.gi_R; ++r) s += p.gi_sums[r * p.gi_rstride + b * 128 + tid];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s += r < p.gi_R ? v[r] : 0.f;
+      for (int r = 8; r < p.gi_R; ++r) s += p.gi_sums[r * p.gi_rstride + b * 128 + tid];
       cs[tid] = s;
-    } else if (tid < 192) {
+    } else if (tid >= 256 && tid < 320) {
+      gi_bias[tid - 256] = p.bias ? p.bias[co0 + tid - 256] : 0.f;
+    } else if (tid >= 128 && tid < 192) {
       const int c = tid - 128;
       prm[c] = p.gi_gamma[c];
       prm[64 + c] = p.gi_beta[c];
@@ -2009,7 +2020,17 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   };
   // piece i of stage st >= 1: its new rows q = st SEG + 2 .. st SEG + SEG + 1
   auto issue1 = [&](int st, int i) {
-    dma_row(st * SEG + 2 + s_rr[i], min(wave + 8 * i, NP - 1), s_co[i]);
+    if constexpr (GNIN) {  // recomputed from an opaque lane id: no VGPRs held across the stage loop
+      int ln = lane, rr;
+      asm volatile("" : "+v"(ln));
+      const int piece = min(wave + 8 * i, NP - 1);
+      rr = piece / PPR;
+      const int slot = (piece - rr * PPR) * 64 + ln, px = slot / 9, c = slot - px * 9;
+      const bool ok = slot < WP * 9 && c < 8 && px >= 1 && px <= W;
+      dma_row(st * SEG + 2 + rr, piece, ok ? ((px - 1) * p.ld0 + c * 8) * 2 : -1);
+    } else {
+      dma_row(st * SEG + 2 + s_rr[i], min(wave + 8 * i, NP - 1), s_co[i]);
+    }
   };
   auto issue = [&](int st) {
 #pragma unroll
@@ -2047,8 +2068,10 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   // by SCALAR loads of the wave's 32 (lgkmcnt): a vector load here was the
   // last vmcnt op hipcc knew of before the stage loop, so it put a vmcnt(0)
   // at the loop entry -- which also drained the DMA of stages 1 and 2
+  // (GNIN: the bias is added in the epilogue from LDS instead -- 16 VGPRs the
+  // in-loop transform needs beside the statistics accumulators)
   f32x16 bias_acc;
-  {
+  if constexpr (!GNIN) {
     float bw[32];
     const float* bp = p.bias ? p.bias + co0 + ch * 32 : nullptr;
 #pragma unroll
@@ -2060,10 +2083,16 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   }
   if (nst > 1) issue(1);
   if (!G::LATE && nst > 2) issue(2);
-  // stage 0, weights and bias landed; stages 1 and 2 (when issued) younger
-  if (!G::LATE && nst > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
-  else if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // stage 0, weights and bias landed; stages 1 and 2 (when issued) younger.
+  // GNIN: stage 1's rows too (stage 0 transforms them among its MFMAs)
+  if constexpr (GNIN) {
+    if (nst > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (!G::LATE && nst > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPW) : "memory");
+    else if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   // raw barriers (asm, memory-clobbering): __syncthreads()'s fence made hipcc
   // wait for EVERY outstanding vector-memory op (vmcnt(0)) -- the DMA of
   // stages 1 and 2 as well -- before the weights could be read
@@ -2086,8 +2115,9 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   // counts below hold unchanged.
   if (G::LATE && nst > 2) issue(2);
   asm volatile("" ::: "memory");  // (stage 0's residual loads stay younger than D2)
-  // GNIN: stage 0's whole window (SEG + 2 rows, landed) transformed (Y0)
-  constexpr int Y0 = GNIN ? SEG + 2 : 0, YS = GNIN ? SEG : 0;  // stores per thread: prologue / stage
+  // GNIN: stage 0's whole window (SEG + 2 rows, landed) transformed here (Y0
+  // stores per thread); stage s >= 1's SEG new rows during stage s - 1
+  constexpr int Y0 = SEG + 2;
   if constexpr (GNIN) {
     if (nst > 0) {  // (two rows at a time: four spill beside the statistics accumulators)
       fold_rows(std::integral_constant<int, 2>{}, 0);
@@ -2130,11 +2160,27 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
         for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
       }
     }
-    // GNIN: this stage's SEG new rows (landed at the last barrier) transformed
-    // before any wave reads them (Y(st))
-    if constexpr (GNIN) if (st > 0) {
-      fold_rows(std::integral_constant<int, SEG>{}, st * SEG + 2);
-      asm volatile("s_barrier" ::: "memory");
+    // GNIN: the next stage's SEG new rows (landed at the last barrier; no wave
+    // reads them in this stage) are transformed among this stage's MFMAs: the
+    // thread's slot of each row and its group's A / B read here, ahead of the
+    // window fragments (the first fragment wait covers them), one channel
+    // pair per k-step 1 .. 4 SEG, written back / stored after the loop.
+    const bool tr = GNIN && st + 1 < nst;  // wave-uniform
+    u32x4 tk[4], tv[SEG];
+    if constexpr (GNIN) if (tr) {
+      // (slot coordinates from an opaque thread id: recomputed per stage, not
+      // held in VGPRs across the loop beside the statistics accumulators)
+      int ot = tid;
+      asm volatile("" : "+v"(ot));
+      const int gx = ot >> 3, gc = ot & 7;
+      const unsigned ta = lds_addr(gi_tab + 16 * gc);
+      tk[0] = ds_read_b128_off<0>(ta);
+      tk[1] = ds_read_b128_off<16>(ta);
+      tk[2] = ds_read_b128_off<32>(ta);
+      tk[3] = ds_read_b128_off<48>(ta);
+#pragma unroll
+      for (int i = 0; i < SEG; ++i)
+        tv[i] = ds_read_b128_off<0>(lds_addr(smem + (((st + 1) * SEG + 2 + i) % R) * ROWB + (gx + 1) * FS_XP + gc * 16));
     }
     // the lane's three tap rows dy = 0..2: window rows st SEG + orow + dy
     const int q0 = st * SEG + orow;
@@ -2148,7 +2194,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     // the LGKM queue as out of order and drains it to 0 every few reads.
     // (fewer VGPRs of read-ahead beside two residuals, a folded input, a
     // residual with the statistics epilogue: no spill)
-    constexpr int FSD = (GNIN || NRES > 0) && STATS ? 4 : (NRES > 1 || GNIN) ? 6 : 8;
+    constexpr int FSD = GNIN && STATS ? 2 : NRES > 0 && STATS ? 4 : (NRES > 1 || GNIN) ? 6 : 8;
     u32x4 bq[FSD];
     static_for<0, FSD>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
@@ -2166,7 +2212,9 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
       for (int g = 0; g < 4; ++g)
         rv2[g] = *(const bf16x4*)(p.res2 + m * p.ldres2 + co0 + ch * 32 + 8 * g + 4 * h);
     }
-    f32x16 acc = bias_acc;  // the accumulator starts at the bias
+    f32x16 acc;  // the accumulator starts at the bias (GNIN: at zero)
+    if constexpr (GNIN) acc = f32x16{};
+    else acc = bias_acc;
     // stage st+3's new rows go out among this stage's MFMAs (one piece per 7):
     // their ring slots were last read in stage st-1, before the barrier that
     // ended it
@@ -2180,8 +2228,39 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
       if constexpr (k % 7 == 3 && k / 7 < NPW) {
         if (pre) issue1(st + 3, k / 7);
       }
+      // (one channel pair every FS_TSTEP k-steps: the transform's VALU spread thin between MFMAs)
+      if constexpr (GNIN && k >= 1 && (k - 1) % FS_TSTEP == 0 && (k - 1) / FS_TSTEP < 4 * SEG) {
+        if (tr) {  // channel pair j of row slot i: silu(A z + B) as the GroupNorm apply computes it
+          constexpr int i = ((k - 1) / FS_TSTEP) >> 2, j = ((k - 1) / FS_TSTEP) & 3;
+          const unsigned wd = tv[i][j];
+          const f32x4 a4 = __builtin_bit_cast(f32x4, tk[j >> 1]), b4 = __builtin_bit_cast(f32x4, tk[2 + (j >> 1)]);
+          gf2 t = gf2{__uint_as_float(wd << 16), __uint_as_float(wd & 0xffff0000u)} *
+                      gf2{a4[(2 * j) & 3], a4[(2 * j + 1) & 3]} + gf2{b4[(2 * j) & 3], b4[(2 * j + 1) & 3]};
+          const gf2 mm = t * -1.4426950408889634f;
+          const gf2 d = 1.f + gf2{__builtin_amdgcn_exp2f(mm.x), __builtin_amdgcn_exp2f(mm.y)};
+          t *= gf2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+          const bf16 lo = (bf16)t.x, hi = (bf16)t.y;
+          tv[i][j] = (unsigned)__builtin_bit_cast(unsigned short, lo) | ((unsigned)__builtin_bit_cast(unsigned short, hi) << 16);
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
+    if constexpr (GNIN) if (tr) {  // the transformed rows back into the ring (Y(st): SEG stores)
+      int ot = tid;
+      asm volatile("" : "+v"(ot));
+      const int gx = ot >> 3, gc = ot & 7;
+#pragma unroll
+      for (int i = 0; i < SEG; ++i) {
+        const int q = (st + 1) * SEG + 2 + i, y = yq0 + q;
+        const bool in = (unsigned)y < (unsigned)p.H;
+        const u32x4 ov = in ? tv[i] : u32x4{0u, 0u, 0u, 0u};
+        asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(smem + (q % R) * ROWB + (gx + 1) * FS_XP + gc * 16)),
+                     "v"(ov) : "memory");
+        const bool own = in && q <= nst * SEG;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            ov, yr, own ? (unsigned)(((fbase + y * W + gx) * p.gi_ldy + gc * 8) * 2) : DMA_OOB, 0, 0);
+      }
+    }
 #ifdef DV_STAMP
     if (st == 1) {
       asm volatile("s_nop 0" : "+v"(acc));
@@ -2191,12 +2270,20 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     // epilogue: lane owns pixel m, channels 8g + 4h + e of the wave's 32
     const bool silu = p.act == DV_ACT_SILU;
     float sv[stats ? 32 : 1];
+    const unsigned gba = lds_addr(gi_bias + ch * 32 + 4 * h);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int n = ch * 32 + 8 * g + 4 * h;
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = acc[4 * g + e];
+      if constexpr (GNIN) {
+        u32x4 gb = ds_read_b128_off<0>(gba + 32 * g);
+        lgkm_wait_tied<0>(gb);
+        const f32x4 bb = __builtin_bit_cast(f32x4, gb);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bb[e];
+      }
       if (silu) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
@@ -2235,12 +2322,27 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     // (A statistics epilogue's clip-boundary atomics only add younger ops:
     // the wait then covers more, never less.)  Every window read of this
     // stage was waited for by the last MFMA: no lgkmcnt drain.
-    // GNIN adds the transformed rows' stores: Y0 after D2 (prologue), Y(s)
-    // at the start of stage s >= 1, so younger than D(st+1) are also
-    //   st = 0: Y0;   st = 1: Y0, Y1;   st >= 2: Y(st-1), Y(st).
-    if (st + 1 < nst) {
+    // GNIN waits one stage further ahead, for D(st+2) (transformed during
+    // stage st+1), and a stage's transformed rows add SEG stores Y(s) before
+    // its output stores.  Younger than D(st+2):
+    //   st = 0: Y0, D3, Y(0), S0;   st >= 1: Y(st-1), S(st-1), D(st+3), Y(st), S(st).
+    if constexpr (GNIN) {
+      if (st + 2 < nst) {
+        constexpr int B0 = Y0 + SEG + 4, B1 = 2 * SEG + 8;
+        static_assert(B0 + NPW <= 63 && B1 + NPW <= 63, "stripe vmcnt immediate out of range");
+        const bool d3 = st + 3 < nst;
+        if (st == 0) {
+          if (d3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B0 + NPW) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B0) : "memory");
+        } else {
+          if (d3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B1 + NPW) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B1) : "memory");
+        }
+      }
+      if (tr) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring writes, before the barrier
+    } else if (st + 1 < nst) {
       constexpr int NR = 4 * NRES;
-      constexpr int A0 = NR + 4 + Y0, A1 = 2 * NR + 8 + Y0 + YS, A2 = 2 * NR + 12 + 2 * YS;
+      constexpr int A0 = NR + 4, A1 = 2 * NR + 8, A2 = 2 * NR + 12;
       static_assert(A1 + 2 * NPW <= 63 && A2 + 2 * NPW <= 63, "stripe vmcnt immediate out of range");
       const int nd = (st + 2 < nst) + (st + 3 < nst);  // DMA stages issued after D(st+1)
       if (st == 0) {

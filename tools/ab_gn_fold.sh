@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 tag=$1
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests/test_gn_fold_gpu.py tests/test_conv_gpu.py tests/test_cfg2_trainer_gpu.py tests/test_gn_coop_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_$tag.log 2>&1 || { tail -40 gpurun_out/tests_$tag.log; exit 1; }
+timeout -k 10 100 python tools/gn_fold_probe.py > gpurun_out/probe_$tag.log 2>&1 && cat gpurun_out/probe_$tag.log | tail -1 && timeout -k 10 700 python -u -m pytest tests/test_gn_fold_gpu.py tests/test_conv_gpu.py tests/test_cfg2_trainer_gpu.py tests/test_gn_coop_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_$tag.log 2>&1 || { tail -40 gpurun_out/tests_$tag.log; exit 1; }
 tail -2 gpurun_out/tests_$tag.log
 B="--no-cpu-baseline --no-sampling --no-fp32 --no-config3"
 for i in 1 2; do

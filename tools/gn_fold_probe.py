@@ -2,7 +2,11 @@
 channels): the 3x3 stripe conv with its statistics epilogue, the GroupNorm
 apply it replaces when folded (dv_gn_fwd over the conv's sums), and the
 folded conv (dv_conv_fwd_gn_in, with and without storing y).  Each as N calls
-replayed from one HIP graph.
+replayed from one HIP graph.  With the diagnostic build (make -C
+dalle2-video_amd/csrc stamp; DV_HIP_LIB=<libdv_hip_stamp.so>) also the stripe
+kernel's per-workgroup phases, plain vs folded (stamps: 0 entry, 1 prologue
+done, 2 stage 0 done, 4 stage 1's MFMA loop, 5 its epilogue, 6 its DMA wait,
+7 its barrier, 3 end; median us per workgroup).
 
   python tools/gn_fold_probe.py
 """
@@ -17,6 +21,23 @@ import torch  # noqa: E402
 from dalle2_video import _lib, ops  # noqa: E402
 
 N = 8
+L = _lib.lib()
+STAMPS = hasattr(L, "dv_debug_stamps")
+if STAMPS:
+    L.dv_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+
+
+def phases(fn, nblk=256):
+    import numpy as np
+    fn()
+    torch.cuda.synchronize()
+    buf = np.zeros(nblk * 8, dtype=np.uint64)
+    assert L.dv_debug_stamps(buf.ctypes.data, buf.size) == 0
+    t = buf.reshape(nblk, 8).astype(np.int64)
+    med = lambda a, b: np.median(t[:, b] - t[:, a]) / 100
+    return (f"span {(t[:, 3].max() - t[:, 0].min()) / 100:6.2f}  prologue {med(0, 1):5.2f}  stage0 {med(1, 2):5.2f}"
+            f"  s1 loop {med(2, 4):5.2f}  epi {med(4, 5):5.2f}  wait {med(5, 6):5.2f}  bar {med(6, 7):5.2f}"
+            f"  rest {med(7, 3):5.2f}  total {med(0, 3):5.2f}")
 
 
 def timed(fn):
@@ -63,9 +84,9 @@ def main():
         _lib.call("dv_conv_fwd", _lib.dt(z), _lib.ptr(z), C, C, None, 0, _lib.ptr(wp), _lib.ptr(bias), None, 0,
                   None, 0, _lib.ptr(out), C, nf, H, H, C, C, 3, _lib.ACT_NONE, _lib.ptr(sums[1]), P, R, st())
 
-    def apply():
+    def apply(act=_lib.ACT_SILU):
         _lib.call("dv_gn_fwd", _lib.dt(z), _lib.ptr(z), C, _lib.ptr(y), C, None, 0, nb, P, C, 8,
-                  ops.ctypes_float(1e-5), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(ss), _lib.ACT_SILU,
+                  ops.ctypes_float(1e-5), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(ss), act,
                   _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(sums[0]), _lib.ptr(sums[2]), sums.shape[1], R, st())
 
     def fold(store):
@@ -85,6 +106,10 @@ def main():
     print(f"64^2 x 64, 4 clips x 16 frames (us per call): conv+stats {t_conv:6.1f}  gn apply {t_apply:6.1f}  "
           f"sum {t_conv + t_apply:6.1f}  |  folded conv (y stored) {t_fold:6.1f}  (y not stored) {t_fold_ns:6.1f}",
           flush=True)
+    print(f"  gn apply without the SiLU {timed(lambda: apply(_lib.ACT_NONE)):6.1f} us", flush=True)
+    if STAMPS:
+        print(f"  plain : {phases(conv_stats)}", flush=True)
+        print(f"  folded: {phases(lambda: fold(True))}", flush=True)
 
 
 if __name__ == "__main__":
