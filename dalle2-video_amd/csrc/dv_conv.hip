@@ -43,6 +43,16 @@ extern "C" int dv_debug_stamps(unsigned long long* host, long long n) {
   do {                 \
   } while (0)
 #endif
+// the stripe kernel's stamps 4..7: stage 1's phases, or (DV_STAMP_PRO) the
+// prologue's (7 stage 0 DMA issued, 4 all DMA issued, 5 stage 0 + weights landed,
+// 6 weights in registers; tools/gn_fold_probe.py with DV_STAMP_PRO=1)
+#ifdef DV_STAMP_PRO
+#define DV_SP(i) DV_STAMP_AT(i)
+#define DV_S1(i) do { } while (0)
+#else
+#define DV_SP(i) do { } while (0)
+#define DV_S1(i) DV_STAMP_AT(i)
+#endif
 
 namespace {
 
@@ -2051,6 +2061,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
       dma_row(rr, piece, coff);
     }
   }
+  DV_SP(7);
   {
     char* sW = smem + G::WOFF;
     const int wci = p.wcin ? p.wcin : 64;  // image channels per tap (row pitch 9 wci)
@@ -2083,8 +2094,12 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   }
   if (nst > 1) issue(1);
   if (!G::LATE && nst > 2) issue(2);
+  DV_SP(4);
   // stage 0, weights and bias landed; stages 1 and 2 (when issued) younger.
-  // GNIN: stage 1's rows too (stage 0 transforms them among its MFMAs)
+  // GNIN: stage 1's rows too (stage 0 transforms them among its MFMAs).
+  // (The weight image loaded through VGPRs -- coalesced 16-B loads, then
+  // ds_write -- instead of LDS-DMA measured slower: 33.9 vs 30.9 us per 64^2
+  // call, profiles/r06o_stripe_prologue.txt.)
   if constexpr (GNIN) {
     if (nst > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2097,6 +2112,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   // wait for EVERY outstanding vector-memory op (vmcnt(0)) -- the DMA of
   // stages 1 and 2 as well -- before the weights could be read
   asm volatile("s_barrier" ::: "memory");
+  DV_SP(5);
   u32x4 wA[36];
   {
     // inline-asm reads (a compiler-visible LDS read beside the pending DMA
@@ -2110,6 +2126,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   asm volatile("s_barrier" ::: "memory");  // the weight image is dead: stage 3's rows may land over it
+  DV_SP(6);
   // LATE: stage 2's rows now (over the dead weight image).  They are still
   // issued after D1 and before stage 0's residual loads: the per-stage vmcnt
   // counts below hold unchanged.
@@ -2264,7 +2281,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
 #ifdef DV_STAMP
     if (st == 1) {
       asm volatile("s_nop 0" : "+v"(acc));
-      DV_STAMP_AT(4);
+      DV_S1(4);
     }
 #endif
     // epilogue: lane owns pixel m, channels 8g + 4h + e of the wave's 32
@@ -2311,7 +2328,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
 #pragma unroll
       for (int i = 0; i < 16; ++i) sacc[i] += sv[i];
     }
-    if (st == 1) DV_STAMP_AT(5);
+    if (st == 1) DV_S1(5);
     // stage st+1's rows landed.  vmcnt(N) = all but the wave's N youngest
     // vector-memory ops done (loads, stores, DMA in issue order).  Per stage s
     // a wave issues: its residual loads R (NR), the NPW pieces of D(s+3) (if
@@ -2359,10 +2376,10 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A2) : "memory");
       }
     }
-    if (st == 1) DV_STAMP_AT(6);
+    if (st == 1) DV_S1(6);
     __builtin_amdgcn_s_barrier();
     if (st == 0) DV_STAMP_AT(2);
-    if (st == 1) DV_STAMP_AT(7);
+    if (st == 1) DV_S1(7);
   }
   DV_STAMP_AT(3);
   if constexpr (stats) {

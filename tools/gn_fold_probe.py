@@ -27,6 +27,9 @@ if STAMPS:
     L.dv_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
 
 
+PRO = os.environ.get("DV_STAMP_PRO") == "1"  # the library was built with -DDV_STAMP_PRO
+
+
 def phases(fn, nblk=256):
     import numpy as np
     fn()
@@ -35,6 +38,10 @@ def phases(fn, nblk=256):
     assert L.dv_debug_stamps(buf.ctypes.data, buf.size) == 0
     t = buf.reshape(nblk, 8).astype(np.int64)
     med = lambda a, b: np.median(t[:, b] - t[:, a]) / 100
+    if PRO:  # stamps 7, 4..6 in the prologue: stage 0 DMA issued, all DMA issued, stage 0 + weights landed, weights in registers
+        return (f"span {(t[:, 3].max() - t[:, 0].min()) / 100:6.2f}  issue-D0 {med(0, 7):5.2f}  issue-W,D1,D2 {med(7, 4):5.2f}  landed {med(4, 5):5.2f}"
+                f"  wregs {med(5, 6):5.2f}  to-loop {med(6, 1):5.2f}  stage0 {med(1, 2):5.2f}  rest {med(2, 3):5.2f}"
+                f"  total {med(0, 3):5.2f}  start-skew {(t[:, 0].max() - t[:, 0].min()) / 100:5.2f}")
     return (f"span {(t[:, 3].max() - t[:, 0].min()) / 100:6.2f}  prologue {med(0, 1):5.2f}  stage0 {med(1, 2):5.2f}"
             f"  s1 loop {med(2, 4):5.2f}  epi {med(4, 5):5.2f}  wait {med(5, 6):5.2f}  bar {med(6, 7):5.2f}"
             f"  rest {med(7, 3):5.2f}  total {med(0, 3):5.2f}")
