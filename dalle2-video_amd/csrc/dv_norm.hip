@@ -975,6 +975,9 @@ void gn_apply_launch(GnArgs& a, int u, long long target, hipStream_t st) {
 // and one launch instead of two.
 // --------------------------------------------------------------------------
 constexpr int GN_CT = 512;      // threads per workgroup
+#ifndef GN_COOP_RMAX
+#define GN_COOP_RMAX 4
+#endif
 constexpr int GN_SPIN = 20000;  // counter polls (s_sleep 2 each, ~1 ms) before the fallback
 
 struct GnCoop {
@@ -1168,13 +1171,18 @@ __global__ __launch_bounds__(GN_CT) void gn_coop_kernel(GnCoop q) {
   __syncthreads();
   GN_STAMP_AT(3);
   if (ok_sh) {
-    if (tid < C) {
-      float v1 = 0.f, v2 = 0.f;
-      for (int r = 0; r < a.R; ++r) {
-        float* rp = a.sums + (long long)r * a.rstride + ((long long)b * C + tid) * 2;
-        v1 += __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v2 += __hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < C) {  // every replica's pair in flight at once (a runtime loop waited per load)
+      float v[2 * GN_COOP_RMAX];
+#pragma unroll
+      for (int r = 0; r < GN_COOP_RMAX; ++r) {
+        float* rp = a.sums + (long long)min(r, a.R - 1) * a.rstride + ((long long)b * C + tid) * 2;
+        v[2 * r] = __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[2 * r + 1] = __hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      float v1 = 0.f, v2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < GN_COOP_RMAX; ++r)
+        if (r < a.R) { v1 += v[2 * r]; v2 += v[2 * r + 1]; }
       cs[tid] = v1;
       cs[C + tid] = v2;
     }
@@ -1343,7 +1351,7 @@ bool gn_coop_plan(const GnArgs& a, GnCoop& q, int& nv, bool bwd) {
   long long R = (a.next_n - a.nb) / rs;
   if (R < 1) return false;
   q.a = a;
-  q.a.R = (int)(R < 4 ? R : 4);  // 64 workgroups per clip: 16 adds per address
+  q.a.R = (int)(R < GN_COOP_RMAX ? R : GN_COOP_RMAX);  // 64 workgroups per clip: 64 / R adds per address
   q.a.rstride = rs;
   q.cnt = (int*)(a.sums + a.next_n - a.nb);
   q.force_fallback = g_gn_path == 2;

@@ -173,3 +173,28 @@ def test_fold_dual_source_block():
     ref = ref.permute(0, 2, 3, 4, 1).reshape(8, 64, 64, 64)
     r = rel(a["y"], ref)
     assert r <= 2.5e-2, f"folded up-path block vs torch f32 rel {r:.2e}"
+
+
+def test_deferred_output_materialises_for_other_consumers():
+    """A deferred GroupNorm output read by a conv that cannot fold it (here a
+    1x1 conv) gets the plain apply first: same values as the two-pass form."""
+    from dalle2_video import ops
+    g = torch.Generator().manual_seed(13)
+    nb, C = 2, 64
+    x = torch.randn(8, 64, 64, C, generator=g).bfloat16().cuda()
+    w1 = (0.05 * torch.randn(C, C, 1, 3, 3, generator=g)).cuda()
+    gamma = (1 + 0.1 * torch.randn(C, generator=g)).cuda()
+    beta = (0.1 * torch.randn(C, generator=g)).cuda()
+    ss = (0.2 * torch.randn(nb, 2 * C, generator=g)).cuda()
+    w2 = (0.05 * torch.randn(C, C, 1, 1, 1, generator=g)).cuda()
+    outs = []
+    for defer in (True, False):
+        with torch.no_grad():
+            st = ops.gn_stats(nb, C, 4 * 64 * 64, x.device)
+            z = ops.conv(x, w1, None, gn=st)
+            y = ops.group_norm_act(z, gamma, beta, nb, 8, 1e-5, scale_shift=ss, stats=st, defer=defer)
+            assert (getattr(y, "_dv_gn_in", None) is not None) == (defer and st.used)
+            outs.append(ops.conv(y, w2).float())
+            outs.append(y.float())
+    torch.cuda.synchronize()
+    assert rel(outs[0], outs[2]) <= 5e-3 and rel(outs[1], outs[3]) <= 5e-3
