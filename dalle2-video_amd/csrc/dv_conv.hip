@@ -2750,6 +2750,13 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
   }
   __builtin_amdgcn_s_barrier();
   DV_STAMP_AT(1);
+#ifdef DV_STAMP
+  // diagnostic: one wave's (FRAME_STAMP_WAVE, default 0) shader-clock totals
+  // over the chunk loop of its time at the DMA wait and at the barrier
+  // (stamps 5, 6) and of the whole loop (7)
+  unsigned long long st_wait = 0, st_bar = 0;
+  const unsigned long long st_l0 = __builtin_amdgcn_s_memtime();
+#endif
 
   const int r = lane & 31, h = lane >> 5;
   const int pix = fw_pix<W>(r);                    // within the wave's 32 pixels
@@ -2842,6 +2849,9 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
       __builtin_amdgcn_sched_barrier(0);
     }
     // chunk c+1 landed: younger are the pieces of chunks c+2 .. c+AHEAD
+#ifdef DV_STAMP
+    const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
+#endif
     if constexpr (decltype(PRE)::value) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"((AHEAD - 1) * NPW) : "memory");
     } else {
@@ -2852,7 +2862,15 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     if (DEFER) defer_wait();
+#ifdef DV_STAMP
+    const unsigned long long tw1 = __builtin_amdgcn_s_memtime();
+#endif
     __builtin_amdgcn_s_barrier();
+#ifdef DV_STAMP
+    const unsigned long long tw2 = __builtin_amdgcn_s_memtime();
+    st_wait += tw1 - tw0;
+    st_bar += tw2 - tw1;
+#endif
   };
   using H0 = std::integral_constant<int, 0>;
   using H1 = std::integral_constant<int, 1>;
@@ -2867,6 +2885,19 @@ __global__ __launch_bounds__(NWV * 64) void conv_fwd_frame_kernel(ConvFwdArgs<bf
     if (DEFER && nch > 0) run_deferred(H1{});
   }
   DV_STAMP_AT(2);
+#ifdef DV_STAMP
+#ifndef FRAME_STAMP_WAVE
+#define FRAME_STAMP_WAVE 0
+#endif
+  if (threadIdx.x == 64 * (FRAME_STAMP_WAVE < NWV ? FRAME_STAMP_WAVE : NWV - 1)) {
+    const long long blin = blockIdx.x + (long long)gridDim.x * (blockIdx.y + (long long)gridDim.y * blockIdx.z);
+    if (blin < 16384) {
+      g_dv_stamp[blin * DV_NSTAMP + 5] = st_wait;
+      g_dv_stamp[blin * DV_NSTAMP + 6] = st_bar;
+      g_dv_stamp[blin * DV_NSTAMP + 7] = __builtin_amdgcn_s_memtime() - st_l0;
+    }
+  }
+#endif
   // per output-channel group j of this wave: the accumulated sum (two tap
   // chains).  TS: each half holds partial sums of all CO channels; half 0
   // keeps channels [0, 32) and half 1 [32, 64), the other half's part of

@@ -87,8 +87,13 @@ def frame_case(nf, h, w, cin, cout):
     # 8 waves on 128 channels where 64-channel tiles would take two rounds (dv_conv.hip, launch_fwd_frame)
     w8 = w == 16 and co == 64 and cout % 128 == 0 and (m // 128) * (cout // 64) > 256
     cw = 128 if w8 else co
-    report(f"frame fwd ({nf},{h},{w}) {cin}->{cout} {'8 waves x ' if w8 else ''}co{cw}",
-           stamps((m // 128) * (cout // cw)), [0, 1, 2, 4])
+    st = stamps((m // 128) * (cout // cw))
+    report(f"frame fwd ({nf},{h},{w}) {cin}->{cout} {'8 waves x ' if w8 else ''}co{cw}", st, [0, 1, 2, 4])
+    # wave 0's chunk loop split (shader clock): at the DMA wait, at the barrier, the rest (MFMAs + reads + issue)
+    tot = st[:, 7].astype(np.float64)
+    wt, bt = np.median(st[:, 5] / tot), np.median(st[:, 6] / tot)
+    print(f"  chunk loop (wave 0): DMA wait {100 * wt:4.1f} %  barrier {100 * bt:4.1f} %  "
+          f"MFMA + LDS reads + DMA issue {100 * (1 - wt - bt):4.1f} %", flush=True)
 
 
 def stripe_case(nf, h, w, cin, cout, res=False):
