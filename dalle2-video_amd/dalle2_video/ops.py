@@ -1590,7 +1590,11 @@ def group_norm_act(z, gamma, beta, nb, groups=8, eps=1e-5, scale_shift=None, res
     residual's gradient is handed to it instead of returned to autograd).
     Inside mx8_convs() without autograd, an output an MX-fp8 conv can read
     (bf16, C % 64 == 0, a frame width it runs at) also gets its fp8 copy from
-    the same launch: the conv then skips its quantisation pass."""
+    the same launch: the conv then skips its quantisation pass.
+    defer=True: the caller guarantees the output is read first by ops.conv (as
+    its x0); when the shape allows, no apply runs and that conv produces the
+    output while it stages z (dv_conv_fwd_gn_in), else the conv runs the apply
+    before itself.  Any other first reader would see an unwritten tensor."""
     if _MX8_FUSE and _Mx8State.active and not torch.is_grad_enabled() and z.dtype == torch.bfloat16:
         nf, h, w, c = z.shape
         if c % 64 == 0 and w <= _MX8_MAX_W and _mx8_geom(nf, h, w):
