@@ -2211,7 +2211,7 @@ __global__ __launch_bounds__(512) void conv_fwd_stripe_kernel(ConvFwdArgs<bf16> 
     // the LGKM queue as out of order and drains it to 0 every few reads.
     // (fewer VGPRs of read-ahead beside two residuals, a folded input, a
     // residual with the statistics epilogue: no spill)
-    constexpr int FSD = GNIN && STATS ? 2 : NRES > 0 && STATS ? 4 : (NRES > 1 || GNIN) ? 6 : 8;
+    constexpr int FSD = (GNIN || NRES > 0 || W == 128) && STATS ? 4 : (NRES > 1 || GNIN) ? 6 : 8;
     u32x4 bq[FSD];
     static_for<0, FSD>([&](auto kk) {
       constexpr int k = decltype(kk)::value;

@@ -1004,8 +1004,7 @@ class ConvFn(torch.autograd.Function):
             name = (f"conv_fwd_frame_kernel<{w}>" if use_win else
                     conv_fwd_name(_lib.dtype_name(x0), m, cin, c0 if x1 is not None else cin, cout,
                                   max(ld0, ld1), ksize, h, w, gn.P))
-            gn.used = GnStats.ALL or name in ("conv_fwd_stripe_kernel<64>", "conv_fwd_stripe_kernel<32>",
-                                              "conv_fwd_frame_kernel<8>")
+            gn.used = GnStats.ALL or name in GN_STATS_KERNELS
         gs, gP, gR = (ptr(gn.cur), gn.P, gn.R) if gn is not None and gn.used else (None, 0, 0)
         if use_small:
             img = _small_image(weight, b, cin_real, cout, ksize, cache)
@@ -1495,6 +1494,11 @@ class DvGnIn(ctypes.Structure):
                 ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p), ("y", ctypes.c_void_p),
                 ("ldy", ctypes.c_int), ("zero", ctypes.c_void_p), ("zero_n", ctypes.c_longlong)]
 
+
+# the conv kernels whose GroupNorm-statistics epilogue measured cheaper than
+# the GroupNorm's own reduce pass (tools/gnstats_bench.py; W = 128: config 5)
+GN_STATS_KERNELS = ("conv_fwd_stripe_kernel<64>", "conv_fwd_stripe_kernel<32>", "conv_fwd_stripe_kernel<128>",
+                    "conv_fwd_frame_kernel<8>")
 
 # Block3D -> Block3D GroupNorm folded into the second conv's input staging
 # (tests switch it off to compare against the two-pass form)
