@@ -91,7 +91,9 @@ def prob_mask_like(shape, prob, device):
         return torch.ones(shape, device=device, dtype=torch.bool)
     if prob == 0:
         return torch.zeros(shape, device=device, dtype=torch.bool)
-    return torch.zeros(shape, device=device).float().uniform_(0, 1) < prob
+    # (the reference fills zeros first; uniform_ overwrites every element, so
+    # the draw -- and the generator state after it -- is the same without the fill)
+    return torch.empty(shape, device=device).uniform_(0, 1) < prob
 
 
 def _compute_dtype(module, ref: torch.Tensor):

@@ -228,17 +228,119 @@ def cl_ld(t: torch.Tensor) -> int:
     return ld
 
 
-def _grad_out(p, zero=False):
+class _FreshGrads:
+    """Gradients the trainer's update zeroed only logically (FusedAdamW.
+    zero_grad(defer=True)): instead of a fill of the whole flat buffer before
+    the next backward, the first in-place writer of such a gradient
+    overwrites it (accumulate = False: the wgrad sums write dw instead of
+    reading it back).  Only parameters the conv backward has written before
+    (`whole(p)`: its whole dw / db in one write) are deferred; the rest are
+    zeroed for real.  Correct for every other writer too: a zero=True site or
+    an autograd AccumulateGrad (leaf pre-hook) zeroes the gradient first, and
+    whatever is still pending when the owner's backward ends is zeroed by
+    finish().  Pending sets are per owner (one optimizer per unet), so one
+    unet's backward never touches another unet's deferred zeros.  Entries
+    hold weak references (a dropped trainer keeps no buffers alive)."""
+
+    def __init__(self):
+        import weakref
+        self.pending = {}  # id(p) -> (weakref p, weakref owner)
+        self.tokens = weakref.WeakKeyDictionary()  # owner -> token of the armed set (graph signature)
+
+    @staticmethod
+    def whole(p):
+        return getattr(p, "_dv_whole_grad", False)
+
+    def _get(self, p):
+        ent = self.pending.get(id(p))
+        return ent if ent is not None and ent[0]() is p else None
+
+    def _mine(self, owner):
+        return [k for k, (pr, orf) in self.pending.items() if orf() is owner and pr() is not None]
+
+    def arm(self, owner, params):
+        import weakref
+        oref = weakref.ref(owner)
+        for p in params:
+            self.pending[id(p)] = (weakref.ref(p), oref)
+            if not getattr(p, "_dv_fresh_hook", False):
+                p._dv_fresh_hook = True
+                p.register_hook(self._pre_hook(weakref.ref(p)))
+        self.tokens[owner] = hash(tuple(sorted(id(p) for p in params)))
+
+    def _pre_hook(self, ref):
+        def pre(g):
+            q = ref()
+            if g is not None and q is not None and self._get(q) is not None:
+                del self.pending[id(q)]
+                WGRAD_DEFER.before_write(q.grad.data_ptr())
+                q.grad.zero_()  # autograd adds into it: the zero becomes real first
+        return pre
+
+    def token(self, owner):
+        """Graph-signature part: which deferred zeros a call starts from."""
+        return self.tokens.get(owner) if self._mine(owner) else None
+
+    def drop(self, params):
+        for p in params:
+            if self._get(p) is not None:
+                del self.pending[id(p)]
+
+    def take(self, p, overwrite):
+        """True: `p`'s gradient is logically zero and the caller overwrites it."""
+        if self._get(p) is None:
+            return False
+        del self.pending[id(p)]
+        if overwrite:
+            return True
+        WGRAD_DEFER.before_write(p.grad.data_ptr())
+        p.grad.zero_()
+        return False
+
+    def finish(self, owner, sync=None):
+        """Zero the owner's gradients still pending after its backward (after
+        `sync()`: e.g. the join of gradient buckets already being reduced in
+        place); True if there were any."""
+        left = self._mine(owner)
+        if not left:
+            return False
+        if sync is not None:
+            sync()
+        grads = [self.pending.pop(k)[0]().grad for k in left]
+        torch._foreach_zero_(grads)
+        return True
+
+    def consume(self, owner):
+        """A replayed graph settled the owner's pending gradients (written, or
+        zeroed by the finish() it captured)."""
+        for k in self._mine(owner):
+            del self.pending[k]
+        for k in [k for k, (pr, orf) in self.pending.items() if pr() is None or orf() is None]:
+            del self.pending[k]  # entries of dropped parameters / trainers
+
+
+FRESH = _FreshGrads()
+GRAD_OVERWRITE = True  # FusedAdamW.zero_grad(defer=True) defers the conv gradients' zeros
+
+
+def _grad_out(p, zero=False, overwrite=False):
     """In-place gradient target for a leaf parameter: (buffer, accumulate).
 
     Backward kernels write a parameter's gradient straight into `p.grad`
     (the trainer's flat-buffer view) and the autograd Function returns None
     for it, so no AccumulateGrad add runs.  Returns None when `p` is not a
-    leaf that requires grad (the Function then returns the gradient)."""
+    leaf that requires grad (the Function then returns the gradient).
+    zero: the kernel adds into a zeroed buffer; overwrite: the caller writes
+    the whole gradient in one kernel when told accumulate = False (the conv
+    backward), so a deferred zero (FRESH) needs no fill."""
     if p is None or not (p.requires_grad and p.is_leaf) or p.dtype != torch.float32:
         return None
+    if overwrite and not zero and not FRESH.whole(p):
+        p._dv_whole_grad = True
     if p.grad is None:
         p.grad = (torch.zeros_like if zero else torch.empty_like)(p)
+        return p.grad, False
+    if FRESH.pending and FRESH.take(p, overwrite and not zero):
         return p.grad, False
     return p.grad, True
 
@@ -1149,8 +1251,8 @@ class ConvFn(torch.autograd.Function):
         if want_w:
             # weight (+ fused bias) gradient straight into the parameters' .grad
             # (the trainer's flat buffer) when they are leaves; else returned
-            wslot = _grad_out(wparam)
-            bslot = _grad_out(bparam) if want_b else None
+            wslot = _grad_out(wparam, overwrite=True)
+            bslot = _grad_out(bparam, overwrite=True) if want_b else None
             if wslot is not None:
                 dw_t, acc_w = wslot
             else:

@@ -64,6 +64,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.generation = 0
         self._probe = ()  # (param, data offset, grad offset) spot checks of the aliasing
         self.order_key = None  # optional sort key of the parameters within a group
+        self._zero_plan = None  # (key, flat-gradient spans zero_grad(defer=True) fills)
 
     # -- flat storage ------------------------------------------------------
     def _build_flat(self):
@@ -179,11 +180,48 @@ class FusedAdamW(torch.optim.Optimizer):
                 self.state[p]["step"] = torch.tensor(float(self._t))
         return super().state_dict()
 
-    def zero_grad(self, set_to_none: bool = True):
+    def zero_grad(self, set_to_none: bool = True, defer: bool = False):
+        """defer=True (the trainer's update): the gradients the conv backward
+        writes whole are zeroed only logically (ops.FRESH: the next backward's
+        first write overwrites them), the rest for real -- the next backward
+        must then run through the trainer (it zeroes what stayed unwritten).
+        Reading .grad before that backward shows the old values."""
         if self._flat is not None:
-            self._flat[1].zero_()  # grads stay views of the flat buffer
+            # moved parameters (sampling through host memory) hold their .grad
+            # outside the flat buffer: re-point them first, so the zeros (real
+            # or deferred) land in the gradients the next backward sees
+            self.ensure_flat()
+            params = self._flat[5]
+            armed = [p for p in params if ops.FRESH.whole(p)] if defer and ops.GRAD_OVERWRITE else []
+            if not armed:
+                ops.FRESH.drop(params)
+                self._flat[1].zero_()  # grads stay views of the flat buffer
+                return
+            key = (self.generation, tuple(sorted(id(p) for p in armed)))
+            if self._zero_plan is None or self._zero_plan[0] != key:
+                self._zero_plan = (key, self._zero_spans(set(key[1])))
+            if self._zero_plan[1]:
+                torch._foreach_zero_(self._zero_plan[1])
+            ops.FRESH.arm(self, armed)
             return
         super().zero_grad(set_to_none=set_to_none)
+
+    def _zero_spans(self, armed_ids):
+        """Views of the flat gradient covering every parameter not in
+        `armed_ids`, runs of them merged (over the alignment gaps between
+        them, which stay zero anyway)."""
+        G = self._flat[1]
+        spans, run = [], None
+        for off, k, armed in sorted((self._offsets[id(p)], p.numel(), id(p) in armed_ids) for p in self._flat[5]):
+            if armed:
+                if run is not None:
+                    spans.append(G[run[0]:run[1]])
+                run = None
+            else:
+                run = (off, off + k) if run is None else (run[0], off + k)
+        if run is not None:
+            spans.append(G[run[0]:run[1]])
+        return spans
 
     def clip_coefficient(self, max_norm, prescale=1.0):
         """Device scalar: prescale * min(max_norm / (||prescale g|| + 1e-6), 1)."""
@@ -965,6 +1003,7 @@ class VideoDecoderTrainer(nn.Module):
         sched = getattr(self, f"sched{index}")
         if self._check_flat(unet_number):
             self._reduced[index] = False  # re-pointed buffers: reduce the copied gradient again
+        ops.FRESH.finish(opt)  # no backward since the last update: its deferred zeros become real
         if self._reduced[index]:
             self.overlap[index].wait()  # the overlapped buckets (a captured call joined them already)
             if self.comm_probe is not None and self.comm_probe and self.comm_probe[-1][0] == "bwd":
@@ -976,7 +1015,7 @@ class VideoDecoderTrainer(nn.Module):
         self._reduced[index] = False
         coef = opt.clip_coefficient(self.max_grad_norm)  # the gradient is already the mean over ranks
         opt.step(clip_coef=coef)
-        opt.zero_grad()
+        opt.zero_grad(defer=True)  # the next call's backward overwrites the conv gradients
         if ops.PACK.enabled:
             ops.PACK.refresh()  # repack every cached image in one launch
         warm = self.warmup_schedulers[index]
@@ -1015,7 +1054,11 @@ class VideoDecoderTrainer(nn.Module):
     def _graphed_call(self, unet_number, args, kwargs, variant=None):
         """Replay (capturing on first use) forward + backward of one training
         call; `variant` (the pinned blur decision) selects the graph."""
-        sig = (unet_number, self.amp, variant,
+        opt = getattr(self, f"optim{unet_number - 1}")
+        # the deferred gradient zeros the call starts from (ops.FRESH): a call
+        # right after update() overwrites the conv gradients, an accumulating
+        # call adds to them -- two different captured passes
+        sig = (unet_number, self.amp, variant, ops.FRESH.token(opt),
                tuple((tuple(a.shape), a.dtype) if torch.is_tensor(a) else repr(a) for a in args),
                tuple((k, (tuple(v.shape), v.dtype) if torch.is_tensor(v) else repr(v))
                      for k, v in sorted(kwargs.items())))
@@ -1049,12 +1092,15 @@ class VideoDecoderTrainer(nn.Module):
                         with ctx:
                             loss = self.decoder(*sargs, unet_number=unet_number, **skw)
                         loss.backward()
+                    left = ops.FRESH.finish(opt, sync=None if ov is None else ov.wait)
                 except BaseException:
                     if ov is not None:
                         ov.abort()
                     raise
                 if ov is not None:
-                    overlapped = ov.end(join=True)  # collectives captured and joined
+                    # collectives captured and joined; a gradient zeroed after
+                    # its bucket went out is reduced again by update()
+                    overlapped = ov.end(join=True) and not left
                 # replays start from zeroed GroupNorm sums whatever the parity
                 # of the GroupNorm calls inside the graph (ops._GnSums)
                 ops.gn_graph_boundary(loss.device)
@@ -1080,6 +1126,7 @@ class VideoDecoderTrainer(nn.Module):
             if torch.is_tensor(v):
                 feed(k, ent["kwargs"][k], v)
         ent["graph"].replay()
+        ops.FRESH.consume(opt)
         self._reduced[unet_number - 1] = ent["overlapped"]
         return ent["loss"].item()
 
@@ -1159,6 +1206,9 @@ class VideoDecoderTrainer(nn.Module):
                     total_loss += loss.item()
                     if self.training:
                         loss.backward()
+                # deferred gradient zeros (ops.FRESH) this backward did not overwrite
+                left = self.training and ops.FRESH.finish(getattr(self, f"optim{unet_number - 1}"),
+                                                          sync=None if ov is None else ov.wait)
             except BaseException:
                 if ov is not None:
                     ov.abort()
@@ -1168,7 +1218,8 @@ class VideoDecoderTrainer(nn.Module):
                     ev = torch.cuda.Event(enable_timing=True)
                     ev.record()
                     self.comm_probe.append(["bwd", ev])
-                self._reduced[unet_number - 1] = ov.end(join=False)
+                # a gradient zeroed after its bucket went out is reduced again by update()
+                self._reduced[unet_number - 1] = ov.end(join=False) and not left
         if return_lowres_cond_video:
             return total_loss, torch.stack(cond_videos)
         return total_loss
