@@ -3731,6 +3731,12 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_win_kernel(WgradSArgs a) {
     });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  // the halves sum below reuses the ring: no wave may write it while another
+  // still reads the last stage's operands (the loop has no end-of-stage
+  // barrier; without this one a wave ahead by part of a stage clobbered them
+  // -- an occasional wrong split partial, found as a rare non-finite
+  // gradient, tools/nan_stress.py)
+  __syncthreads();
   DV_STAMP_AT(2);
   accb += __shfl_xor(accb, 32, 64);  // both k-halves of the channel
   wgrad_tile_store<NT>(a, acc, accb, smem, half, wq, wm, wn, lane, co0, ci0, do_bias, bz);

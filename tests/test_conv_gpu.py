@@ -154,6 +154,41 @@ def test_stripe_wgrad_bf16_partials(case, parity_log):
     assert err < 2.5e-3, err
 
 
+@pytest.mark.parametrize("case", [(64, 16, 16, 64, 64), (64, 8, 8, 128, 128), (64, 64, 64, 64, 64),
+                                  (64, 32, 32, 128, 128)])
+def test_window_wgrad_repeatable(case):
+    """The row-window 3x3 wgrad (split-K partials + one ordered sum) has no
+    atomics: repeated launches on the same inputs must give the same bits.
+    Guards the race fixed in round 6 -- a wave that finished its last stage
+    early wrote the halves-sum scratch over the ring while another wave still
+    read its operands (a rare wrong split partial, seen as an occasional
+    non-finite gradient at the 16^2 / 8^2 up-path convs)."""
+    from dalle2_video import _lib, ops
+
+    nf, h, w, cin, cout = case
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(nf, h, w, cin, generator=g).bfloat16().cuda()
+    dy = torch.randn(nf, h, w, cout, generator=g).bfloat16().cuda()
+    ws = ops._wgrad_workspace("bf16", nf, h, w, cin, cin, False, cout, 3, x.device)
+    dw = torch.empty(cout, cin, 1, 3, 3, device="cuda")
+    db = torch.empty(cout, device="cuda")
+
+    def run():
+        _lib.call("dv_conv_wgrad", _lib.DV_BF16, _lib.ptr(dy), cout, _lib.ptr(x), cin, cin, None, 0,
+                  _lib.ptr(dw), 0, _lib.ptr(db), 0, _lib.ptr(ws), ws.numel(), nf, h, w, cin, cout, cout, cin, 3,
+                  _lib.stream())
+        return dw.clone(), db.clone()
+
+    w0, b0 = run()
+    assert torch.isfinite(w0).all()
+    diff = 0
+    for _ in range(300):
+        w1, b1 = run()
+        diff += int(not (torch.equal(w1, w0) and torch.equal(b1, b0)))
+    torch.cuda.synchronize()
+    assert diff == 0, f"{diff} of 300 launches differ"
+
+
 def test_batched_repack_matches_single_packs():
     """PackCache.refresh (one flat-tile launch over every cached image) writes the
     same bytes as packing each weight alone, for both layouts and both dtypes,
