@@ -244,8 +244,10 @@ class _FreshGrads:
 
     def __init__(self):
         import weakref
-        self.pending = {}  # id(p) -> (weakref p, weakref owner)
+        self.pending = {}  # id(p) -> (weakref p, owner key)
+        self.owned = {}  # owner key id(owner) -> (weakref owner, ids pending): per-owner work stays O(own)
         self.tokens = weakref.WeakKeyDictionary()  # owner -> token of the armed set (graph signature)
+        self.marks = 0  # parameters marked whole so far (a trainer's cached armed set is valid while equal)
 
     @staticmethod
     def whole(p):
@@ -255,42 +257,82 @@ class _FreshGrads:
         ent = self.pending.get(id(p))
         return ent if ent is not None and ent[0]() is p else None
 
-    def _mine(self, owner):
-        return [k for k, (pr, orf) in self.pending.items() if orf() is owner and pr() is not None]
+    def _remove(self, k):
+        ent = self.pending.pop(k)
+        o = self.owned.get(ent[1])
+        if o is not None:
+            o[1].discard(k)
 
-    def arm(self, owner, params):
+    def _own(self, owner):
+        o = self.owned.get(id(owner))
+        return o if o is not None and o[0]() is owner else None
+
+    def _mine(self, owner):
+        o = self._own(owner)
+        if o is None:
+            return []
+        oid = id(owner)
+        return [k for k in o[1] if self.pending.get(k, (None, None))[1] == oid and self.pending[k][0]() is not None]
+
+    def _forget(self, oid, ref):
+        """A dropped owner: its entries go (weakref callback)."""
+        o = self.owned.get(oid)
+        if o is None or o[0] is not ref:
+            return
+        del self.owned[oid]
+        for k in o[1]:
+            if self.pending.get(k, (None, None))[1] == oid:
+                del self.pending[k]
+
+    def plan(self, params):
+        """(entries, token) for arm(): computed once per armed set (the
+        trainer caches it), hooks registered on first use."""
         import weakref
-        oref = weakref.ref(owner)
+        entries = []
         for p in params:
-            self.pending[id(p)] = (weakref.ref(p), oref)
             if not getattr(p, "_dv_fresh_hook", False):
                 p._dv_fresh_hook = True
                 p.register_hook(self._pre_hook(weakref.ref(p)))
-        self.tokens[owner] = hash(tuple(sorted(id(p) for p in params)))
+            entries.append((id(p), weakref.ref(p)))
+        return entries, hash(tuple(sorted(k for k, _ in entries)))
+
+    def arm(self, owner, params=None, plan=None):
+        import weakref
+        entries, token = plan if plan is not None else self.plan(params)
+        oid = id(owner)
+        o = self._own(owner)
+        if o is None:
+            o = self.owned[oid] = (weakref.ref(owner, lambda r, oid=oid: self._forget(oid, r)), set())
+        # (an entry another owner still held is overwritten: that owner's
+        # lookups check the entry's owner key, so it no longer sees it)
+        self.pending.update((k, (w, oid)) for k, w in entries)
+        o[1].update(k for k, _ in entries)
+        self.tokens[owner] = token
 
     def _pre_hook(self, ref):
         def pre(g):
             q = ref()
             if g is not None and q is not None and self._get(q) is not None:
-                del self.pending[id(q)]
+                self._remove(id(q))
                 WGRAD_DEFER.before_write(q.grad.data_ptr())
                 q.grad.zero_()  # autograd adds into it: the zero becomes real first
         return pre
 
     def token(self, owner):
         """Graph-signature part: which deferred zeros a call starts from."""
-        return self.tokens.get(owner) if self._mine(owner) else None
+        o = self._own(owner)
+        return self.tokens.get(owner) if o is not None and o[1] else None
 
     def drop(self, params):
         for p in params:
             if self._get(p) is not None:
-                del self.pending[id(p)]
+                self._remove(id(p))
 
     def take(self, p, overwrite):
         """True: `p`'s gradient is logically zero and the caller overwrites it."""
         if self._get(p) is None:
             return False
-        del self.pending[id(p)]
+        self._remove(id(p))
         if overwrite:
             return True
         WGRAD_DEFER.before_write(p.grad.data_ptr())
@@ -303,20 +345,29 @@ class _FreshGrads:
         place); True if there were any."""
         left = self._mine(owner)
         if not left:
+            o = self._own(owner)
+            if o is not None:
+                o[1].clear()  # (entries of dropped parameters)
             return False
         if sync is not None:
             sync()
-        grads = [self.pending.pop(k)[0]().grad for k in left]
+        grads = [self.pending[k][0]().grad for k in left]
+        for k in left:
+            self._remove(k)
         torch._foreach_zero_(grads)
         return True
 
     def consume(self, owner):
         """A replayed graph settled the owner's pending gradients (written, or
         zeroed by the finish() it captured)."""
-        for k in self._mine(owner):
-            del self.pending[k]
-        for k in [k for k, (pr, orf) in self.pending.items() if pr() is None or orf() is None]:
-            del self.pending[k]  # entries of dropped parameters / trainers
+        o = self._own(owner)
+        if o is None:
+            return
+        oid = id(owner)
+        for k in o[1]:
+            if self.pending.get(k, (None, None))[1] == oid:
+                del self.pending[k]
+        o[1].clear()
 
 
 FRESH = _FreshGrads()
@@ -337,6 +388,7 @@ def _grad_out(p, zero=False, overwrite=False):
         return None
     if overwrite and not zero and not FRESH.whole(p):
         p._dv_whole_grad = True
+        FRESH.marks += 1
     if p.grad is None:
         p.grad = (torch.zeros_like if zero else torch.empty_like)(p)
         return p.grad, False

@@ -192,17 +192,23 @@ class FusedAdamW(torch.optim.Optimizer):
             # or deferred) land in the gradients the next backward sees
             self.ensure_flat()
             params = self._flat[5]
-            armed = [p for p in params if ops.FRESH.whole(p)] if defer and ops.GRAD_OVERWRITE else []
-            if not armed:
-                ops.FRESH.drop(params)
-                self._flat[1].zero_()  # grads stay views of the flat buffer
-                return
-            key = (self.generation, tuple(sorted(id(p) for p in armed)))
-            if self._zero_plan is None or self._zero_plan[0] != key:
-                self._zero_plan = (key, self._zero_spans(set(key[1])))
-            if self._zero_plan[1]:
-                torch._foreach_zero_(self._zero_plan[1])
-            ops.FRESH.arm(self, armed)
+            if defer and ops.GRAD_OVERWRITE:
+                # (the armed set, its zero spans and bookkeeping are cached
+                # while no parameter gets newly marked: per-update host work
+                # stays a few dict updates)
+                key = (self.generation, ops.FRESH.marks)
+                if self._zero_plan is None or self._zero_plan[0] != key:
+                    armed = [p for p in params if ops.FRESH.whole(p)]
+                    self._zero_plan = (key, self._zero_spans({id(p) for p in armed}) if armed else None,
+                                       ops.FRESH.plan(armed) if armed else None)
+                _, spans, plan = self._zero_plan
+                if plan is not None:
+                    if spans:
+                        torch._foreach_zero_(spans)
+                    ops.FRESH.arm(self, plan=plan)
+                    return
+            ops.FRESH.drop(params)
+            self._flat[1].zero_()  # grads stay views of the flat buffer
             return
         super().zero_grad(set_to_none=set_to_none)
 

@@ -106,3 +106,29 @@ def test_zero_spans_cover_exactly_the_other_parameters():
         assert bool(covered[off:off + p.numel()].all()) == want
         assert bool(covered[off:off + p.numel()].any()) == want
     assert len(spans) == 3  # {0}, {2}, {4, 5}: adjacent parameters merged
+
+
+def test_dropped_owner_leaves_no_entries():
+    """A trainer that goes away takes its deferred zeros with it (weakref
+    callback), so the per-call bookkeeping of the live ones never scans them."""
+    import gc
+
+    keep = _params(16, 16)
+    ok = FusedAdamW(keep)
+    ok.ensure_flat()
+    for p in keep:
+        ops._grad_out(p, overwrite=True)
+    ok.zero_grad(defer=True)
+    before = len(ops.FRESH.pending)
+    gone = _params(32, 32, 32)
+    og = FusedAdamW(gone)
+    og.ensure_flat()
+    for p in gone:
+        ops._grad_out(p, overwrite=True)
+    og.zero_grad(defer=True)
+    assert len(ops.FRESH.pending) == before + 3
+    del og, gone, p
+    gc.collect()
+    assert len(ops.FRESH.pending) == before
+    assert ops.FRESH.token(ok) is not None and len(ops.FRESH._mine(ok)) == 2
+    ops.FRESH.drop(keep)
